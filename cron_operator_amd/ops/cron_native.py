@@ -1,0 +1,114 @@
+"""Python-facing wrapper of the native cron engine (``csrc/cron_engine.cpp``).
+
+Zones: the extension knows nothing about the filesystem.  This module hands it
+TZif blobs from the ``tzdata`` wheel (there is no ``/usr/share/zoneinfo`` in the
+image) and maps :class:`~cron_operator_amd.utils.gotime.Location` objects to
+native zone ids.  ``Local`` is resolved the same way Go resolves ``time.Local``
+($TZ, else /etc/localtime, else UTC).
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import threading
+from typing import Dict, Optional
+
+from ..utils.gotime import LOCAL, UTC, FixedZone, Location, ZoneLocation, load_location
+from . import build as _build
+
+_lock = threading.Lock()
+_mod = None
+_zone_ids: Dict[str, int] = {}
+_load_error: Optional[BaseException] = None
+
+
+def _tzif_bytes(name: str) -> bytes:
+    if name.startswith("/"):
+        with open(name, "rb") as fh:
+            return fh.read()
+    from importlib import resources
+
+    parts = name.split("/")
+    node = resources.files("tzdata").joinpath("zoneinfo", *parts)
+    return node.read_bytes()
+
+
+def load(build_if_missing: bool = True):
+    """Import (building first if needed) the extension; raises on failure."""
+    global _mod, _load_error
+    if _mod is not None:
+        return _mod
+    with _lock:
+        if _mod is not None:
+            return _mod
+        try:
+            if build_if_missing and _build.needs_build("_cron_engine"):
+                _build.build_extension("_cron_engine")
+            mod = importlib.import_module("cron_operator_amd.ops._cron_engine")
+            mod.set_zone_resolver(_resolve_name)
+            _mod = mod
+        except BaseException as e:  # noqa: BLE001 - recorded for diagnostics
+            _load_error = e
+            raise
+    return _mod
+
+
+def available() -> bool:
+    try:
+        load()
+        return True
+    except Exception:
+        return False
+
+
+def load_error() -> Optional[BaseException]:
+    return _load_error
+
+
+def _resolve_name(name: str) -> int:
+    return zone_id(load_location(name))
+
+
+def zone_id(loc: Location) -> int:
+    """Native zone id for a Location (registering it on first use)."""
+    mod = load()
+    if loc is UTC:
+        return 0
+    if loc is LOCAL:
+        impl = LOCAL.impl()
+        key = "Local:" + (impl.key if isinstance(impl, ZoneLocation) else f"fixed{impl.fixed}")
+        zid = _zone_ids.get(key)
+        if zid is None:
+            if isinstance(impl, ZoneLocation):
+                zid = mod.register_zone("Local", _tzif_bytes(impl.key))
+            else:
+                zid = mod.register_fixed_zone("Local", int(impl.fixed or 0))
+            _zone_ids[key] = zid
+        return zid
+    if isinstance(loc, FixedZone):
+        key = f"fixed:{loc.name}:{loc.offset}"
+        zid = _zone_ids.get(key)
+        if zid is None:
+            zid = mod.register_fixed_zone(loc.name, loc.offset)
+            _zone_ids[key] = zid
+        return zid
+    if isinstance(loc, ZoneLocation):
+        key = "zone:" + loc.key
+        zid = _zone_ids.get(key)
+        if zid is None:
+            zid = mod.register_zone(loc.name, _tzif_bytes(loc.key))
+            _zone_ids[key] = zid
+        return zid
+    raise TypeError(f"unsupported location {loc!r}")
+
+
+def reset_local() -> None:
+    """Forget the cached Local zone (after $TZ changes)."""
+    LOCAL.reset()
+    for k in [k for k in _zone_ids if k.startswith("Local:")]:
+        del _zone_ids[k]
+
+
+def engine_path() -> str:
+    mod = load()
+    return os.path.abspath(mod.__file__)
