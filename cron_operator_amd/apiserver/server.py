@@ -1,0 +1,782 @@
+"""In-process fake Kubernetes API server -- the framework's envtest.
+
+The reference's integration tier runs a real kube-apiserver + etcd with no
+controllers (``internal/controller/suite_test.go:53-124``).  Neither binary
+exists here, so this module provides the same contract in-process:
+
+* CRUD on any registered resource, namespaced or cluster-scoped; LIST with label
+  and field selectors and limit/continue paging; a global etcd-like
+  ``resourceVersion`` counter;
+* WATCH with resume-from-resourceVersion out of a bounded event window (410
+  Expired beyond it), synthetic ADDED events for ``rv=""/"0"``, and filtered
+  watches that turn "stops matching" into DELETED like the watch cache;
+* ``/status`` subresource semantics (main-resource writes ignore status, status
+  writes ignore everything else), ``generation`` bumps on spec changes, and
+  no-op writes that do not bump ``resourceVersion`` or emit events;
+* JSON merge patch, JSON patch, optimistic concurrency (409 Conflict),
+  AlreadyExists/NotFound, ``generateName``, finalizers + ``deletionTimestamp``;
+* CRD installation through the API with structural-schema pruning, defaulting
+  and validation (:mod:`.schema`);
+* optional ownerReference garbage collection (background / foreground /
+  orphan) -- envtest has none, so it is opt-in;
+* fault injection and per-verb latency (:class:`FaultInjector`), and request
+  accounting for the benchmark's API-request model;
+* an injectable :class:`~cron_operator_amd.utils.clock.Clock` for timestamps.
+
+Transports: :mod:`.http` serves it over the real Kubernetes REST paths;
+:class:`cron_operator_amd.runtime.client.InMemoryTransport` calls it directly.
+The core is synchronous and must be driven from one thread (one asyncio loop).
+"""
+from __future__ import annotations
+
+import asyncio
+import base64
+import random
+import string
+import uuid
+from collections import defaultdict, deque
+from dataclasses import dataclass, field
+from typing import Any, Callable, Deque, Dict, Iterable, List, Optional, Set, Tuple
+
+from ..api import errors
+from ..api.meta import GroupVersionResource
+from ..api.selectors import compile_selectors
+from ..utils import jsonutil
+from ..utils.clock import Clock, RealClock
+from ..utils.gotime import GoTime, UTC
+from . import schema as sch
+from .registry import ResourceInfo, builtin_resources, resources_from_crd
+
+_NAME_CHARS = "bcdfghjklmnpqrstvwxz2456789"
+_DNS1123_SUB = set(string.ascii_lowercase + string.digits + "-.")
+
+
+def _ts(clock: Clock) -> str:
+    return GoTime(clock.now_ns() // 1_000_000_000, 0, UTC).rfc3339()
+
+
+# --------------------------------------------------------------------------- faults
+
+
+@dataclass
+class Fault:
+    verb: str = "*"            # get list create update patch delete watch, or *
+    resource: str = "*"        # plural resource name or *
+    subresource: Optional[str] = None  # None = any
+    code: int = 500
+    reason: str = "InternalError"
+    message: str = "injected fault"
+    times: int = -1            # -1 = unlimited
+    probability: float = 1.0
+    name: Optional[str] = None
+
+    def matches(self, verb: str, resource: str, sub: Optional[str], name: Optional[str]) -> bool:
+        if self.times == 0:
+            return False
+        if self.verb != "*" and self.verb != verb:
+            return False
+        if self.resource != "*" and self.resource != resource:
+            return False
+        if self.subresource is not None and self.subresource != (sub or ""):
+            return False
+        if self.name is not None and self.name != name:
+            return False
+        return True
+
+
+class FaultInjector:
+    """Per-verb error injection and latency (the reference has none)."""
+
+    def __init__(self, seed: int = 0):
+        self.faults: List[Fault] = []
+        self.latency: Dict[str, float] = {}  # verb -> seconds ("*" default)
+        self._rng = random.Random(seed)
+
+    def add(self, **kw: Any) -> Fault:
+        f = Fault(**kw)
+        self.faults.append(f)
+        return f
+
+    def clear(self) -> None:
+        self.faults.clear()
+        self.latency.clear()
+
+    def check(self, verb: str, resource: str, sub: Optional[str] = None, name: Optional[str] = None) -> None:
+        for f in self.faults:
+            if f.matches(verb, resource, sub, name) and self._rng.random() < f.probability:
+                if f.times > 0:
+                    f.times -= 1
+                raise errors.ApiError(f.code, f.reason, f.message)
+
+    def delay_for(self, verb: str) -> float:
+        return self.latency.get(verb, self.latency.get("*", 0.0))
+
+
+# --------------------------------------------------------------------------- watch
+
+
+class Watcher:
+    """One WATCH stream.  Events are ``(type, object)``; ``None`` ends the stream."""
+
+    def __init__(self, server: "APIServer", info: ResourceInfo, namespace: Optional[str],
+                 pred: Callable[[Dict[str, Any]], bool], bookmarks: bool):
+        self.server = server
+        self.info = info
+        self.namespace = namespace or None
+        self.pred = pred
+        self.bookmarks = bookmarks
+        self.queue: "asyncio.Queue[Optional[Tuple[str, Dict[str, Any]]]]" = asyncio.Queue()
+        self.closed = False
+        self.sent = 0
+
+    def _in_scope(self, obj: Dict[str, Any]) -> bool:
+        if self.namespace is not None and (obj.get("metadata") or {}).get("namespace") != self.namespace:
+            return False
+        return self.pred(obj)
+
+    def offer(self, etype: str, obj: Dict[str, Any], old: Optional[Dict[str, Any]]) -> None:
+        if self.closed:
+            return
+        now_in = self._in_scope(obj)
+        if etype == "MODIFIED" and old is not None:
+            was_in = self._in_scope(old)
+            if was_in and not now_in:
+                self._put("DELETED", obj)
+            elif now_in and not was_in:
+                self._put("ADDED", obj)
+            elif now_in:
+                self._put("MODIFIED", obj)
+            return
+        if now_in:
+            self._put(etype, obj)
+
+    def _put(self, etype: str, obj: Dict[str, Any]) -> None:
+        self.sent += 1
+        self.queue.put_nowait((etype, jsonutil.deepcopy(obj)))
+
+    def bookmark(self, rv: int) -> None:
+        if self.bookmarks and not self.closed:
+            self.queue.put_nowait(("BOOKMARK", {"kind": self.info.kind, "apiVersion": self.info.api_version,
+                                                "metadata": {"resourceVersion": str(rv)}}))
+
+    def stop(self) -> None:
+        if not self.closed:
+            self.closed = True
+            self.server._remove_watcher(self)
+            self.queue.put_nowait(None)
+
+    def __aiter__(self):
+        return self
+
+    async def __anext__(self) -> Tuple[str, Dict[str, Any]]:
+        if self.closed and self.queue.empty():
+            raise StopAsyncIteration
+        ev = await self.queue.get()
+        if ev is None:
+            raise StopAsyncIteration
+        return ev
+
+
+# --------------------------------------------------------------------------- server
+
+
+@dataclass
+class RequestStats:
+    by_verb: Dict[str, int] = field(default_factory=lambda: defaultdict(int))
+    by_resource_verb: Dict[Tuple[str, str], int] = field(default_factory=lambda: defaultdict(int))
+    total: int = 0
+
+    def record(self, verb: str, resource: str) -> None:
+        self.by_verb[verb] += 1
+        self.by_resource_verb[(resource, verb)] += 1
+        self.total += 1
+
+    def snapshot(self) -> Dict[str, Any]:
+        return {"total": self.total, "by_verb": dict(self.by_verb),
+                "by_resource_verb": {f"{r}:{v}": n for (r, v), n in self.by_resource_verb.items()}}
+
+
+class APIServer:
+    def __init__(self, clock: Optional[Clock] = None, gc: bool = False, watch_window: int = 200_000,
+                 auto_create_namespaces: bool = False, tokens: Optional[Dict[str, Dict[str, Any]]] = None):
+        self.clock = clock or RealClock()
+        self.gc_enabled = gc
+        self.auto_create_namespaces = auto_create_namespaces
+        self.faults = FaultInjector()
+        self.stats = RequestStats()
+        # bearer token -> user info ({"username", "groups"}); None disables authn in HTTP mode
+        self.tokens = tokens
+        self.authorizer: Optional[Callable[[Dict[str, Any], Dict[str, Any]], bool]] = None
+        self._rv = 0
+        self._resources: Dict[Tuple[str, str, str], ResourceInfo] = {}
+        self._by_kind: Dict[Tuple[str, str, str], ResourceInfo] = {}
+        # (group, resource) -> namespace -> name -> stored object (never mutated in place)
+        self._data: Dict[Tuple[str, str], Dict[str, Dict[str, Dict[str, Any]]]] = defaultdict(dict)
+        self._watchers: Dict[Tuple[str, str], List[Watcher]] = defaultdict(list)
+        self._log: Dict[Tuple[str, str], Deque[Tuple[int, str, Dict[str, Any], Optional[Dict[str, Any]]]]] = {}
+        self._log_floor: Dict[Tuple[str, str], int] = defaultdict(int)
+        self._watch_window = watch_window
+        self._owners: Dict[str, Set[Tuple[str, str, str, str]]] = defaultdict(set)  # owner uid -> dependents
+        self._gc_pending: List[Tuple[str, str]] = []
+        self.create_hooks: List[Callable[[ResourceInfo, Dict[str, Any]], None]] = []
+        self._rng = random.Random(7)
+        for ri in builtin_resources():
+            self.register(ri)
+        for ns in ("default", "kube-system", "kube-public", "kube-node-lease"):
+            self._put_raw(self._resources[("", "v1", "namespaces")], "", self._new_namespace(ns))
+
+    # ------------------------------------------------------------------ registry
+    def register(self, ri: ResourceInfo) -> None:
+        self._resources[(ri.group, ri.version, ri.resource)] = ri
+        self._by_kind[(ri.group, ri.version, ri.kind)] = ri
+
+    def resources(self) -> List[ResourceInfo]:
+        return list(self._resources.values())
+
+    def resource(self, gvr: GroupVersionResource) -> ResourceInfo:
+        ri = self._resources.get((gvr.group, gvr.version, gvr.resource))
+        if ri is None:
+            raise errors.ApiError(404, "NotFound", f"the server could not find the requested resource "
+                                                   f"({gvr.resource}.{gvr.group})" if gvr.group else
+                                  f"the server could not find the requested resource ({gvr.resource})")
+        return ri
+
+    def resource_for_kind(self, group: str, version: str, kind: str) -> Optional[ResourceInfo]:
+        return self._by_kind.get((group, version, kind))
+
+    def install_crd(self, crd: Dict[str, Any]) -> Dict[str, Any]:
+        """Create (or replace) a CRD object and register its resources."""
+        ri = self._resources[("apiextensions.k8s.io", "v1", "customresourcedefinitions")]
+        name = (crd.get("metadata") or {}).get("name", "")
+        existing = self._get_raw(ri, "", name)
+        if existing is None:
+            return self.create(ri.gvr, "", crd)
+        body = jsonutil.deepcopy(crd)
+        body.setdefault("metadata", {})["resourceVersion"] = existing["metadata"]["resourceVersion"]
+        return self.update(ri.gvr, "", name, body)
+
+    def _on_crd_written(self, crd: Dict[str, Any]) -> None:
+        for r in resources_from_crd(crd):
+            self.register(r)
+        # mark Established like the real apiextensions controller
+        st = crd.setdefault("status", {})
+        st["conditions"] = [{"type": "NamesAccepted", "status": "True", "reason": "NoConflicts"},
+                            {"type": "Established", "status": "True", "reason": "InitialNamesAccepted"}]
+        st["acceptedNames"] = dict((crd.get("spec") or {}).get("names") or {})
+
+    # ------------------------------------------------------------------ helpers
+    def current_rv(self) -> int:
+        return self._rv
+
+    def _next_rv(self) -> int:
+        self._rv += 1
+        return self._rv
+
+    def _bucket(self, ri: ResourceInfo) -> Dict[str, Dict[str, Dict[str, Any]]]:
+        return self._data[(ri.group, ri.resource)]
+
+    def _get_raw(self, ri: ResourceInfo, ns: str, name: str) -> Optional[Dict[str, Any]]:
+        return self._bucket(ri).get(ns if ri.namespaced else "", {}).get(name)
+
+    def _put_raw(self, ri: ResourceInfo, ns: str, obj: Dict[str, Any]) -> None:
+        self._bucket(ri).setdefault(ns if ri.namespaced else "", {})[obj["metadata"]["name"]] = obj
+
+    def _new_namespace(self, name: str) -> Dict[str, Any]:
+        return {"apiVersion": "v1", "kind": "Namespace",
+                "metadata": {"name": name, "uid": str(uuid.uuid4()), "resourceVersion": str(self._next_rv()),
+                             "creationTimestamp": _ts(self.clock)},
+                "spec": {"finalizers": ["kubernetes"]}, "status": {"phase": "Active"}}
+
+    def _check_namespace(self, ri: ResourceInfo, ns: str) -> None:
+        if not ri.namespaced:
+            return
+        if not ns:
+            raise errors.bad_request("an empty namespace may not be set during creation")
+        nsri = self._resources[("", "v1", "namespaces")]
+        if self._get_raw(nsri, "", ns) is None:
+            if self.auto_create_namespaces:
+                self._put_raw(nsri, "", self._new_namespace(ns))
+                return
+            raise errors.not_found("namespaces", "", ns)
+
+    def _emit(self, ri: ResourceInfo, etype: str, obj: Dict[str, Any], old: Optional[Dict[str, Any]],
+              rv: int) -> None:
+        key = (ri.group, ri.resource)
+        log = self._log.get(key)
+        if log is None:
+            log = self._log[key] = deque()
+        log.append((rv, etype, obj, old))
+        if len(log) > self._watch_window:
+            dropped = log.popleft()
+            self._log_floor[key] = dropped[0]
+        for w in list(self._watchers.get(key, ())):
+            w.offer(etype, obj, old)
+
+    def _remove_watcher(self, w: Watcher) -> None:
+        lst = self._watchers.get((w.info.group, w.info.resource))
+        if lst and w in lst:
+            lst.remove(w)
+
+    def _index_owners(self, ri: ResourceInfo, obj: Optional[Dict[str, Any]], old: Optional[Dict[str, Any]]) -> None:
+        if old is not None:
+            m = old.get("metadata") or {}
+            ref = (ri.group, ri.resource, m.get("namespace", ""), m.get("name", ""))
+            for o in m.get("ownerReferences") or []:
+                s = self._owners.get(o.get("uid", ""))
+                if s is not None:
+                    s.discard(ref)
+        if obj is not None:
+            m = obj.get("metadata") or {}
+            ref = (ri.group, ri.resource, m.get("namespace", ""), m.get("name", ""))
+            for o in m.get("ownerReferences") or []:
+                self._owners[o.get("uid", "")].add(ref)
+
+    def _admit(self, ri: ResourceInfo, obj: Dict[str, Any], name: str) -> None:
+        if ri.schema is not None:
+            sch.prune(obj, ri.schema)
+            sch.apply_defaults(obj, ri.schema)
+            errs = sch.validate(obj, ri.schema)
+            if errs:
+                raise errors.invalid(ri.kind, ri.group, name, errs)
+
+    def _validate_name(self, ri: ResourceInfo, name: str) -> None:
+        if not name:
+            raise errors.invalid(ri.kind, ri.group, name, [{"field": "metadata.name", "reason": "FieldValueRequired",
+                                                           "message": "Required value: name or generateName is "
+                                                                      "required"}])
+        bad = (len(name) > 253 or any(c not in _DNS1123_SUB for c in name) or not name[0].isalnum()
+               or not name[-1].isalnum())
+        if bad and ri.kind not in ("Event",):
+            raise errors.invalid(ri.kind, ri.group, name, [{
+                "field": "metadata.name", "reason": "FieldValueInvalid",
+                "message": f'Invalid value: "{name}": a lowercase RFC 1123 subdomain must consist of lower case '
+                           f"alphanumeric characters, '-' or '.', and must start and end with an alphanumeric "
+                           f"character"}])
+
+    # ------------------------------------------------------------------ verbs
+    def get(self, gvr: GroupVersionResource, namespace: str, name: str) -> Dict[str, Any]:
+        ri = self.resource(gvr)
+        self.stats.record("get", ri.resource)
+        obj = self._get_raw(ri, namespace, name)
+        if obj is None:
+            raise errors.not_found(ri.resource, ri.group, name)
+        return jsonutil.deepcopy(obj)
+
+    def list(self, gvr: GroupVersionResource, namespace: Optional[str] = None, label_selector: Optional[str] = None,
+             field_selector: Optional[str] = None, limit: int = 0, continue_: Optional[str] = None,
+             copy: bool = True) -> Dict[str, Any]:
+        ri = self.resource(gvr)
+        self.stats.record("list", ri.resource)
+        pred = compile_selectors(label_selector, field_selector)
+        bucket = self._bucket(ri)
+        if ri.namespaced and namespace:
+            spaces = [namespace]
+        else:
+            spaces = sorted(bucket.keys())
+        start_after = None
+        list_rv = self._rv
+        if continue_:
+            try:
+                tok = jsonutil.loads(base64.urlsafe_b64decode(continue_.encode()).decode())
+                start_after = tok["k"]
+                list_rv = int(tok["rv"])
+            except Exception:
+                raise errors.bad_request("invalid continue token") from None
+        items: List[Dict[str, Any]] = []
+        more = None
+        for ns in spaces:
+            objs = bucket.get(ns) or {}
+            for name in sorted(objs.keys()) if (limit or continue_) else objs.keys():
+                if start_after is not None and f"{ns}/{name}" <= start_after:
+                    continue
+                obj = objs[name]
+                if not pred(obj):
+                    continue
+                if limit and len(items) >= limit:
+                    more = f"{ns}/{name}"
+                    break
+                items.append(jsonutil.deepcopy(obj) if copy else obj)
+            if more:
+                break
+        meta: Dict[str, Any] = {"resourceVersion": str(list_rv)}
+        if more is not None:
+            last = items[-1]["metadata"]
+            tok = {"k": f"{last.get('namespace', '')}/{last['name']}", "rv": list_rv}
+            meta["continue"] = base64.urlsafe_b64encode(jsonutil.dumpb(tok)).decode()
+            meta["remainingItemCount"] = 0
+        return {"apiVersion": ri.api_version, "kind": ri.list_kind, "metadata": meta, "items": items}
+
+    def create(self, gvr: GroupVersionResource, namespace: str, obj: Dict[str, Any],
+               dry_run: bool = False) -> Dict[str, Any]:
+        ri = self.resource(gvr)
+        self.stats.record("create", ri.resource)
+        body = jsonutil.deepcopy(obj)
+        m = body.get("metadata")
+        if not isinstance(m, dict):
+            m = body["metadata"] = {}
+        if ri.namespaced:
+            bns = m.get("namespace", "")
+            if bns and namespace and bns != namespace:
+                raise errors.bad_request("the namespace of the provided object does not match the namespace "
+                                         "sent on the request")
+            namespace = namespace or bns
+            m["namespace"] = namespace
+        else:
+            m.pop("namespace", None)
+            namespace = ""
+        if ri.virtual:
+            return self._review(ri, body)
+        body["apiVersion"] = ri.api_version
+        body["kind"] = ri.kind
+        name = m.get("name", "")
+        if not name and m.get("generateName"):
+            for _ in range(16):
+                cand = m["generateName"] + "".join(self._rng.choice(_NAME_CHARS) for _ in range(5))
+                if self._get_raw(ri, namespace, cand) is None:
+                    name = cand
+                    break
+            m["name"] = name
+        self._validate_name(ri, name)
+        self._check_namespace(ri, namespace)
+        if self._get_raw(ri, namespace, name) is not None:
+            raise errors.already_exists(ri.resource, ri.group, name)
+        if ri.status_subresource and ri.is_crd:
+            body.pop("status", None)
+        self._admit(ri, body, name)
+        for k in ("resourceVersion", "deletionTimestamp", "deletionGracePeriodSeconds", "selfLink"):
+            m.pop(k, None)
+        m["uid"] = str(uuid.uuid4())
+        m["creationTimestamp"] = _ts(self.clock)
+        m["generation"] = 1
+        for hook in self.create_hooks:
+            hook(ri, body)
+        if dry_run:
+            return body
+        rv = self._next_rv()
+        m["resourceVersion"] = str(rv)
+        if ri.kind == "CustomResourceDefinition":
+            self._on_crd_written(body)
+        self._put_raw(ri, namespace, body)
+        self._index_owners(ri, body, None)
+        self._emit(ri, "ADDED", body, None, rv)
+        return jsonutil.deepcopy(body)
+
+    def _review(self, ri: ResourceInfo, body: Dict[str, Any]) -> Dict[str, Any]:
+        body["apiVersion"] = ri.api_version
+        body["kind"] = ri.kind
+        spec = body.get("spec") or {}
+        if ri.kind == "TokenReview":
+            user = (self.tokens or {}).get(spec.get("token", ""))
+            body["status"] = {"authenticated": user is not None, "user": user or {}}
+        elif ri.kind == "SubjectAccessReview":
+            allowed = True
+            if self.authorizer is not None:
+                allowed = bool(self.authorizer({"user": spec.get("user"), "groups": spec.get("groups")}, spec))
+            body["status"] = {"allowed": allowed}
+        return body
+
+    def _finish_write(self, ri: ResourceInfo, ns: str, name: str, old: Dict[str, Any],
+                      new: Dict[str, Any]) -> Dict[str, Any]:
+        """Store ``new`` unless it equals ``old`` (no-op writes keep the RV, emit nothing)."""
+        nm = new["metadata"]
+        nm["resourceVersion"] = old["metadata"]["resourceVersion"]
+        if jsonutil.json_equal(old, new):
+            return jsonutil.deepcopy(old)
+        # finalizers drained on a terminating object -> delete it now
+        if nm.get("deletionTimestamp") and not nm.get("finalizers"):
+            return self._remove(ri, ns, name, old)
+        rv = self._next_rv()
+        nm["resourceVersion"] = str(rv)
+        if ri.kind == "CustomResourceDefinition":
+            self._on_crd_written(new)
+        self._put_raw(ri, ns, new)
+        self._index_owners(ri, new, old)
+        self._emit(ri, "MODIFIED", new, old, rv)
+        return jsonutil.deepcopy(new)
+
+    def _prepare_update(self, ri: ResourceInfo, old: Dict[str, Any], body: Dict[str, Any],
+                        subresource: Optional[str]) -> Dict[str, Any]:
+        om = old["metadata"]
+        if subresource == "status":
+            new = jsonutil.deepcopy(old)
+            if "status" in body:
+                new["status"] = body["status"]
+            else:
+                new.pop("status", None)
+            if ri.schema is not None:
+                self._admit(ri, new, om["name"])
+            return new
+        if subresource not in (None, ""):
+            raise errors.ApiError(404, "NotFound", f"the server could not find the requested resource "
+                                                   f"({subresource})")
+        new = body
+        new["apiVersion"] = ri.api_version
+        new["kind"] = ri.kind
+        nm = new.setdefault("metadata", {})
+        # immutable / server-owned metadata
+        for k in ("uid", "creationTimestamp", "namespace", "name", "generation", "deletionTimestamp",
+                  "deletionGracePeriodSeconds"):
+            if k in om:
+                nm[k] = om[k]
+            else:
+                nm.pop(k, None)
+        if ri.status_subresource:
+            if "status" in old:
+                new["status"] = old["status"]
+            else:
+                new.pop("status", None)
+        self._admit(ri, new, om["name"])
+        spec_changed = any(not jsonutil.json_equal(old.get(k), new.get(k))
+                           for k in set(old) | set(new) if k not in ("metadata", "status", "apiVersion", "kind"))
+        if spec_changed:
+            nm["generation"] = int(om.get("generation", 1)) + 1
+        return new
+
+    def update(self, gvr: GroupVersionResource, namespace: str, name: str, obj: Dict[str, Any],
+               subresource: Optional[str] = None) -> Dict[str, Any]:
+        ri = self.resource(gvr)
+        self.stats.record("update", ri.resource)
+        ns = namespace if ri.namespaced else ""
+        old = self._get_raw(ri, ns, name)
+        body = jsonutil.deepcopy(obj)
+        bm = body.get("metadata") or {}
+        if bm.get("name") and bm["name"] != name:
+            raise errors.bad_request("the name of the object does not match the name on the URL")
+        if old is None:
+            raise errors.not_found(ri.resource, ri.group, name)
+        rv = bm.get("resourceVersion", "")
+        if rv and rv != old["metadata"]["resourceVersion"]:
+            raise errors.conflict(ri.resource, ri.group, name, "the object has been modified; please apply your "
+                                                              "changes to the latest version and try again")
+        new = self._prepare_update(ri, old, body, subresource)
+        return self._finish_write(ri, ns, name, old, new)
+
+    def patch(self, gvr: GroupVersionResource, namespace: str, name: str, patch: Any,
+              patch_type: str = "merge", subresource: Optional[str] = None) -> Dict[str, Any]:
+        ri = self.resource(gvr)
+        self.stats.record("patch", ri.resource)
+        ns = namespace if ri.namespaced else ""
+        old = self._get_raw(ri, ns, name)
+        if old is None:
+            raise errors.not_found(ri.resource, ri.group, name)
+        if patch_type in ("merge", "strategic"):
+            if patch_type == "strategic" and ri.is_crd:
+                raise errors.ApiError(415, "UnsupportedMediaType", "the body of the request was in an unknown "
+                                                                   "format - accepted media types include: "
+                                                                   "application/json-patch+json, "
+                                                                   "application/merge-patch+json")
+            if not isinstance(patch, dict):
+                raise errors.bad_request("merge patch must be a JSON object")
+            merged = jsonutil.apply_merge_patch(old, patch)
+        elif patch_type == "json":
+            try:
+                merged = jsonutil.apply_json_patch(old, patch)
+            except (KeyError, IndexError, ValueError, TypeError) as e:
+                raise errors.ApiError(422, "Invalid", f"the server rejected our request due to an error in our "
+                                                      f"request: {e}") from None
+        else:
+            raise errors.ApiError(415, "UnsupportedMediaType", f"unsupported patch type {patch_type}")
+        pm = (patch.get("metadata") or {}) if isinstance(patch, dict) else {}
+        prv = pm.get("resourceVersion")
+        if prv and prv != old["metadata"]["resourceVersion"]:
+            raise errors.conflict(ri.resource, ri.group, name, "the object has been modified; please apply your "
+                                                              "changes to the latest version and try again")
+        merged.setdefault("metadata", {})["resourceVersion"] = old["metadata"]["resourceVersion"]
+        new = self._prepare_update(ri, old, merged, subresource)
+        return self._finish_write(ri, ns, name, old, new)
+
+    def delete(self, gvr: GroupVersionResource, namespace: str, name: str,
+               propagation_policy: Optional[str] = None,
+               preconditions: Optional[Dict[str, str]] = None) -> Dict[str, Any]:
+        ri = self.resource(gvr)
+        self.stats.record("delete", ri.resource)
+        ns = namespace if ri.namespaced else ""
+        old = self._get_raw(ri, ns, name)
+        if old is None:
+            raise errors.not_found(ri.resource, ri.group, name)
+        om = old["metadata"]
+        if preconditions:
+            if preconditions.get("uid") and preconditions["uid"] != om.get("uid"):
+                raise errors.conflict(ri.resource, ri.group, name,
+                                      f"Precondition failed: UID in precondition: {preconditions['uid']}, "
+                                      f"UID in object meta: {om.get('uid')}")
+            if preconditions.get("resourceVersion") and preconditions["resourceVersion"] != om.get("resourceVersion"):
+                raise errors.conflict(ri.resource, ri.group, name, "Precondition failed: ResourceVersion mismatch")
+        finalizers = list(om.get("finalizers") or [])
+        policy = propagation_policy or "Background"
+        if policy == "Foreground" and self.gc_enabled and self._owners.get(om.get("uid", "")):
+            finalizers.append("foregroundDeletion")
+        if policy == "Orphan" and self.gc_enabled:
+            self._orphan_dependents(om.get("uid", ""))
+        if finalizers:
+            if om.get("deletionTimestamp"):
+                return jsonutil.deepcopy(old)
+            new = jsonutil.deepcopy(old)
+            new["metadata"]["deletionTimestamp"] = _ts(self.clock)
+            new["metadata"]["deletionGracePeriodSeconds"] = 0
+            new["metadata"]["finalizers"] = finalizers
+            rv = self._next_rv()
+            new["metadata"]["resourceVersion"] = str(rv)
+            self._put_raw(ri, ns, new)
+            self._emit(ri, "MODIFIED", new, old, rv)
+            if "foregroundDeletion" in finalizers:
+                self._schedule_gc(ri, new)
+            return jsonutil.deepcopy(new)
+        return self._remove(ri, ns, name, old)
+
+    def _remove(self, ri: ResourceInfo, ns: str, name: str, old: Dict[str, Any]) -> Dict[str, Any]:
+        self._bucket(ri).get(ns, {}).pop(name, None)
+        rv = self._next_rv()
+        gone_obj = jsonutil.deepcopy(old)
+        gone_obj["metadata"]["resourceVersion"] = str(rv)
+        self._index_owners(ri, None, old)
+        self._emit(ri, "DELETED", gone_obj, None, rv)
+        if self.gc_enabled:
+            self._schedule_gc(ri, old)
+        return gone_obj
+
+    def delete_collection(self, gvr: GroupVersionResource, namespace: Optional[str],
+                          label_selector: Optional[str] = None) -> int:
+        lst = self.list(gvr, namespace, label_selector, copy=False)
+        n = 0
+        for item in lst["items"]:
+            m = item["metadata"]
+            try:
+                self.delete(gvr, m.get("namespace", ""), m["name"])
+                n += 1
+            except errors.ApiError:
+                pass
+        return n
+
+    # ------------------------------------------------------------------ garbage collection
+    def _schedule_gc(self, ri: ResourceInfo, owner: Dict[str, Any]) -> None:
+        uid = (owner.get("metadata") or {}).get("uid", "")
+        if not uid:
+            return
+        self._gc_pending.append((uid, (owner.get("metadata") or {}).get("name", "")))
+        try:
+            loop = asyncio.get_running_loop()
+            loop.call_soon(self.run_gc)
+        except RuntimeError:
+            self.run_gc()
+
+    def run_gc(self) -> int:
+        """Process pending owner deletions; returns the number of dependents deleted."""
+        n = 0
+        while self._gc_pending:
+            uid, _ = self._gc_pending.pop(0)
+            for (g, r, ns, name) in list(self._owners.get(uid, ())):
+                ri = next((x for x in self._resources.values() if x.group == g and x.resource == r), None)
+                if ri is None:
+                    continue
+                dep = self._get_raw(ri, ns, name)
+                if dep is None:
+                    continue
+                refs = (dep.get("metadata") or {}).get("ownerReferences") or []
+                # only collect when no other live owner remains
+                others = [o for o in refs if o.get("uid") != uid and self._owner_alive(o, ns)]
+                if others:
+                    continue
+                try:
+                    self.delete(ri.gvr, ns, name, propagation_policy="Background")
+                    n += 1
+                except errors.ApiError:
+                    pass
+            self._owners.pop(uid, None)
+            self._finish_foreground(uid)
+        return n
+
+    def _owner_alive(self, ref: Dict[str, Any], ns: str) -> bool:
+        for ri in self._resources.values():
+            if ri.kind == ref.get("kind") and ri.api_version == ref.get("apiVersion"):
+                o = self._get_raw(ri, ns, ref.get("name", ""))
+                return o is not None and o["metadata"].get("uid") == ref.get("uid")
+        return False
+
+    def _finish_foreground(self, uid: str) -> None:
+        for (g, r), spaces in self._data.items():
+            for ns, objs in spaces.items():
+                for name, obj in list(objs.items()):
+                    m = obj["metadata"]
+                    if m.get("uid") == uid and "foregroundDeletion" in (m.get("finalizers") or []):
+                        ri = next(x for x in self._resources.values() if x.group == g and x.resource == r)
+                        new = jsonutil.deepcopy(obj)
+                        new["metadata"]["finalizers"] = [f for f in m["finalizers"] if f != "foregroundDeletion"]
+                        self._finish_write(ri, ns, name, obj, new)
+                        return
+
+    def _orphan_dependents(self, uid: str) -> None:
+        for (g, r, ns, name) in list(self._owners.get(uid, ())):
+            ri = next((x for x in self._resources.values() if x.group == g and x.resource == r), None)
+            if ri is None:
+                continue
+            dep = self._get_raw(ri, ns, name)
+            if dep is None:
+                continue
+            new = jsonutil.deepcopy(dep)
+            new["metadata"]["ownerReferences"] = [o for o in new["metadata"].get("ownerReferences") or []
+                                                  if o.get("uid") != uid]
+            if not new["metadata"]["ownerReferences"]:
+                del new["metadata"]["ownerReferences"]
+            self._finish_write(ri, ns, name, dep, new)
+        self._owners.pop(uid, None)
+
+    # ------------------------------------------------------------------ watch
+    def watch(self, gvr: GroupVersionResource, namespace: Optional[str] = None, resource_version: str = "",
+              label_selector: Optional[str] = None, field_selector: Optional[str] = None,
+              allow_bookmarks: bool = False, send_initial_events: Optional[bool] = None) -> Watcher:
+        ri = self.resource(gvr)
+        self.stats.record("watch", ri.resource)
+        pred = compile_selectors(label_selector, field_selector)
+        w = Watcher(self, ri, namespace if ri.namespaced else None, pred, allow_bookmarks)
+        key = (ri.group, ri.resource)
+        if resource_version in ("", "0") or send_initial_events:
+            for ns, objs in self._bucket(ri).items():
+                if w.namespace is not None and ns != w.namespace:
+                    continue
+                for obj in objs.values():
+                    if pred(obj):
+                        w._put("ADDED", obj)
+        else:
+            try:
+                since = int(resource_version)
+            except ValueError:
+                raise errors.bad_request(f"invalid resourceVersion {resource_version!r}") from None
+            floor = self._log_floor.get(key, 0)
+            if since < floor:
+                raise errors.gone(f"too old resource version: {since} ({floor + 1})")
+            for (rv, etype, obj, old) in self._log.get(key, ()):
+                if rv > since:
+                    w.offer(etype, obj, old)
+        self._watchers[key].append(w)
+        return w
+
+    def send_bookmarks(self) -> None:
+        for lst in self._watchers.values():
+            for w in lst:
+                w.bookmark(self._rv)
+
+    def close_all_watches(self) -> None:
+        for lst in list(self._watchers.values()):
+            for w in list(lst):
+                w.stop()
+
+    # ------------------------------------------------------------------ conveniences
+    def create_namespace(self, name: str) -> Dict[str, Any]:
+        ri = self._resources[("", "v1", "namespaces")]
+        if self._get_raw(ri, "", name) is not None:
+            return jsonutil.deepcopy(self._get_raw(ri, "", name))
+        return self.create(ri.gvr, "", {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": name}})
+
+    def objects(self, gvr: GroupVersionResource, namespace: Optional[str] = None) -> Iterable[Dict[str, Any]]:
+        """Read-only view of stored objects (no copies; do not mutate)."""
+        ri = self.resource(gvr)
+        for ns, objs in self._bucket(ri).items():
+            if namespace is None or ns == namespace:
+                yield from objs.values()
+
+    def count(self, gvr: GroupVersionResource, namespace: Optional[str] = None) -> int:
+        ri = self.resource(gvr)
+        if namespace is not None:
+            return len(self._bucket(ri).get(namespace, {}))
+        return sum(len(v) for v in self._bucket(ri).values())

@@ -1,0 +1,270 @@
+"""Command line: ``cron-operator start [flags]`` and helper subcommands.
+
+Reference: ``cmd/main.go:31-55`` (cobra root that prints help without a
+subcommand) and ``cmd/operator/start.go:61-265`` (the ``start`` command).  Every
+flag of the reference keeps its name, default and meaning:
+
+==============================  ===========  ==========================================
+flag                            default      reference
+==============================  ===========  ==========================================
+--max-concurrent-reconciles     10           start.go:215
+--qps / --burst                 30 / 50      start.go:218-219
+--metrics-bind-address          "0"          start.go:220 (0 disables)
+--health-probe-bind-address     ":8081"      start.go:222
+--leader-elect                  false        start.go:223
+--metrics-secure                true         start.go:226
+--webhook-cert-path/-name/-key  ""/tls.crt/tls.key   start.go:228-234
+--metrics-cert-path/-name/-key  ""/tls.crt/tls.key   start.go:235-240
+--enable-http2                  false        start.go:241
+--zap-devel/-encoder/-log-level/-stacktrace-level/-time-encoding      start.go:244-247
+==============================  ===========  ==========================================
+
+Additions: ``--kubeconfig``, ``--namespace`` (restrict the cache),
+``--leader-elect-namespace``, ``--compat-mode`` (``reference`` restores every
+reference quirk, see :class:`~cron_operator_amd.controller.reconciler.ReconcilerOptions`),
+``--cron-engine``.  Extra subcommands: ``fake-apiserver`` (serve the in-process
+apiserver over HTTP with the CRDs installed), ``crd`` (print the CRD) and
+``version``.
+
+Flag syntax follows pflag: ``--flag value``, ``--flag=value`` and bare boolean
+flags (``--leader-elect``, ``--metrics-secure=false``).
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import os
+import signal
+import sys
+from typing import List, Optional
+
+from .. import __version__
+
+
+def _bool(v: Optional[str]) -> bool:
+    if v is None:
+        return True
+    s = str(v).strip().lower()
+    if s in ("1", "t", "true", "yes", "y", "on"):
+        return True
+    if s in ("0", "f", "false", "no", "n", "off"):
+        return False
+    raise argparse.ArgumentTypeError(f'invalid boolean value "{v}"')
+
+
+def _add_bool(p: argparse.ArgumentParser, name: str, default: bool, help_: str) -> None:
+    p.add_argument(name, nargs="?", const=True, default=default, type=_bool, metavar="true|false", help=help_)
+
+
+def build_parser() -> argparse.ArgumentParser:
+    root = argparse.ArgumentParser(prog="cron-operator", description="Cron operator for scheduled ML training jobs "
+                                                                     "(apps.kubedl.io/v1alpha1 Cron).")
+    sub = root.add_subparsers(dest="command")
+
+    st = sub.add_parser("start", help="Start manager")
+    st.add_argument("--max-concurrent-reconciles", type=int, default=10,
+                    help="The maximum number of concurrent reconciles for controller.")
+    st.add_argument("--qps", type=float, default=30.0, help="Maximum QPS to the Kubernetes API server from this "
+                                                            "client.")
+    st.add_argument("--burst", type=int, default=50, help="Maximum burst for throttle.")
+    st.add_argument("--metrics-bind-address", default="0", help="The address the metrics endpoint binds to. Use "
+                                                                ":8443 for HTTPS or :8080 for HTTP, or leave as 0 to "
+                                                                "disable the metrics service.")
+    st.add_argument("--health-probe-bind-address", default=":8081", help="The address the probe endpoint binds to.")
+    _add_bool(st, "--leader-elect", False, "Enable leader election for controller manager. Enabling this will "
+                                           "ensure there is only one active controller manager.")
+    _add_bool(st, "--metrics-secure", True, "If set, the metrics endpoint is served securely via HTTPS. Use "
+                                            "--metrics-secure=false to use HTTP instead.")
+    st.add_argument("--webhook-cert-path", default="", help="The directory that contains the webhook certificate.")
+    st.add_argument("--webhook-cert-name", default="tls.crt", help="The name of the webhook certificate file.")
+    st.add_argument("--webhook-cert-key", default="tls.key", help="The name of the webhook key file.")
+    st.add_argument("--metrics-cert-path", default="", help="The directory that contains the metrics server "
+                                                            "certificate.")
+    st.add_argument("--metrics-cert-name", default="tls.crt", help="The name of the metrics server certificate file.")
+    st.add_argument("--metrics-cert-key", default="tls.key", help="The name of the metrics server key file.")
+    _add_bool(st, "--enable-http2", False, "If set, HTTP/2 will be enabled for the metrics and webhook servers")
+    # zap flags (controller-runtime logzap.Options.BindFlags)
+    _add_bool(st, "--zap-devel", False, "Development Mode defaults(encoder=consoleEncoder,logLevel=Debug,"
+                                        "stackTraceLevel=Warn). Production Mode defaults(encoder=jsonEncoder,"
+                                        "logLevel=Info,stackTraceLevel=Error)")
+    st.add_argument("--zap-encoder", default=None, help="Zap log encoding (one of 'json' or 'console')")
+    st.add_argument("--zap-log-level", default=None, help="Zap Level to configure the verbosity of logging. Can be "
+                                                          "one of 'debug', 'info', 'error', 'panic'or any integer "
+                                                          "value > 0 which corresponds to custom debug levels of "
+                                                          "increasing verbosity")
+    st.add_argument("--zap-stacktrace-level", default=None, help="Zap Level at and above which stacktraces are "
+                                                                 "captured (one of 'info', 'error', 'panic').")
+    st.add_argument("--zap-time-encoding", default=None, help="Zap time encoding (one of 'epoch', 'millis', 'nano', "
+                                                              "'iso8601', 'rfc3339' or 'rfc3339nano'). Defaults to "
+                                                              "'epoch'.")
+    # additions
+    st.add_argument("--kubeconfig", default="", help="Path to a kubeconfig. Only required if out-of-cluster.")
+    st.add_argument("--namespace", default="", help="Only watch Crons in this namespace (default: all).")
+    st.add_argument("--leader-elect-namespace", default="", help="Namespace of the leader-election Lease "
+                                                                 "(default: the pod's namespace).")
+    st.add_argument("--compat-mode", choices=["optimized", "reference"], default="optimized",
+                    help="'reference' reproduces every reference behaviour (live child LIST, finished=now, ...).")
+    st.add_argument("--cron-engine", choices=["auto", "native", "python"], default="auto",
+                    help="Cron next-fire engine implementation.")
+
+    fa = sub.add_parser("fake-apiserver", help="Serve the in-process fake Kubernetes API server over HTTP")
+    fa.add_argument("--bind-address", default="127.0.0.1")
+    fa.add_argument("--port", type=int, default=6443)
+    fa.add_argument("--kubeconfig-out", default="", help="Write a kubeconfig pointing at the server here.")
+    _add_bool(fa, "--gc", True, "Run ownerReference garbage collection.")
+    _add_bool(fa, "--fake-clock", False, "Use a settable clock (POST /debug/fake/clock).")
+    fa.add_argument("--token", default="", help="Require this bearer token.")
+    _add_bool(fa, "--training-operator", False, "Also run the fake training-operator (timed mode).")
+    fa.add_argument("--job-duration", type=float, default=30.0, help="Seconds a job runs in timed mode.")
+
+    sub.add_parser("crd", help="Print the Cron CustomResourceDefinition")
+    sub.add_parser("version", help="Print the version")
+    return root
+
+
+def _setup_log(a: argparse.Namespace):
+    from ..utils.logging import new_from_options, set_logger
+
+    logger = new_from_options(encoder=a.zap_encoder, level=a.zap_log_level, devel=a.zap_devel,
+                              stacktrace_level=a.zap_stacktrace_level, time_encoding=a.zap_time_encoding)
+    set_logger(logger)
+    return logger
+
+
+async def run_start(a: argparse.Namespace) -> int:
+    from ..controller.reconciler import ReconcilerOptions
+    from ..controller.setup import setup_with_manager
+    from ..cron.engine import make_engine
+    from ..runtime.client import Client
+    from ..runtime.http import HttpTransport
+    from ..runtime.kubeconfig import ConfigError, get_config
+    from ..runtime.manager import LeaderElectionLost, Manager, ManagerOptions
+    from ..utils.logging import get_logger
+
+    log = get_logger("setup")
+    if not a.enable_http2:
+        log.info("disabling http/2")
+    if a.webhook_cert_path:
+        log.info("Initializing webhook certificate watcher using provided certificates",
+                 **{"webhook-cert-path": a.webhook_cert_path, "webhook-cert-name": a.webhook_cert_name,
+                    "webhook-cert-key": a.webhook_cert_key})
+    if a.metrics_cert_path:
+        log.info("Initializing metrics certificate watcher using provided certificates",
+                 **{"metrics-cert-path": a.metrics_cert_path, "metrics-cert-name": a.metrics_cert_name,
+                    "metrics-cert-key": a.metrics_cert_key})
+    try:
+        cfg = get_config(a.kubeconfig)
+    except ConfigError as e:
+        log.error(e, "unable to get kubeconfig")
+        return 1
+    cfg.qps, cfg.burst = a.qps, a.burst
+    client = Client(HttpTransport(cfg), qps=a.qps, burst=a.burst)
+    mopts = ManagerOptions(namespace=a.namespace, leader_election=a.leader_elect,
+                           leader_election_namespace=a.leader_elect_namespace,
+                           metrics_bind_address=a.metrics_bind_address, secure_metrics=a.metrics_secure,
+                           metrics_cert_path=a.metrics_cert_path, metrics_cert_name=a.metrics_cert_name,
+                           metrics_cert_key=a.metrics_cert_key,
+                           health_probe_bind_address=a.health_probe_bind_address, enable_http2=a.enable_http2,
+                           max_concurrent_reconciles=a.max_concurrent_reconciles)
+    try:
+        mgr = Manager(client, mopts)
+        opts = ReconcilerOptions.reference() if a.compat_mode == "reference" else ReconcilerOptions()
+        await setup_with_manager(mgr, opts, make_engine(a.cron_engine))
+    except Exception as e:  # noqa: BLE001
+        log.error(e, "unable to create controller", controller="Cron")
+        await client.close()
+        return 1
+    mgr.add_healthz_check("healthz")
+    mgr.add_readyz_check("readyz")
+    loop = asyncio.get_running_loop()
+    for sig in (signal.SIGINT, signal.SIGTERM):
+        try:
+            loop.add_signal_handler(sig, mgr.stop)
+        except (NotImplementedError, RuntimeError):
+            pass
+    log.info("starting manager")
+    try:
+        await mgr.start()
+    except LeaderElectionLost:
+        log.info("leader election lost")
+        return 1
+    except Exception as e:  # noqa: BLE001
+        log.error(e, "problem running manager")
+        return 1
+    finally:
+        await client.close()
+    return 0
+
+
+async def run_fake_apiserver(a: argparse.Namespace) -> int:
+    from ..api.v1alpha1.crd import crd
+    from ..apiserver.http import APIServerApp
+    from ..apiserver.server import APIServer
+    from ..runtime.client import Client, InMemoryTransport
+    from ..runtime.kubeconfig import write_kubeconfig
+    from ..trainingop.crds import kubeflow_crds
+    from ..trainingop.operator import FakeTrainingOperator
+    from ..utils.clock import FakeClock, RealClock
+
+    clock = FakeClock() if a.fake_clock else RealClock()
+    tokens = {a.token: {"username": "admin", "groups": ["system:masters"]}} if a.token else None
+    server = APIServer(clock, gc=a.gc, tokens=tokens)
+    server.install_crd(crd())
+    for c in kubeflow_crds():
+        server.install_crd(c)
+    app = APIServerApp(server)
+    port = await app.start(a.bind_address, a.port)
+    url = f"http://{a.bind_address}:{port}"
+    if a.kubeconfig_out:
+        write_kubeconfig(a.kubeconfig_out, url, a.token)
+    print(f"fake apiserver listening on {url}", flush=True)
+    top = None
+    if a.training_operator:
+        top = FakeTrainingOperator(Client(InMemoryTransport(server), qps=-1), clock, mode="timed",
+                                   duration=a.job_duration)
+        await top.start()
+    stop = asyncio.Event()
+    loop = asyncio.get_running_loop()
+    for sig in (signal.SIGINT, signal.SIGTERM):
+        try:
+            loop.add_signal_handler(sig, stop.set)
+        except (NotImplementedError, RuntimeError):
+            pass
+    await stop.wait()
+    if top is not None:
+        await top.stop()
+    await app.stop()
+    return 0
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    parser = build_parser()
+    a = parser.parse_args(argv)
+    if a.command is None:
+        parser.print_help()
+        return 0
+    if a.command == "version":
+        print(__version__)
+        return 0
+    if a.command == "crd":
+        from ..api.v1alpha1.crd import crd_yaml
+
+        sys.stdout.write(crd_yaml())
+        return 0
+    if a.command == "fake-apiserver":
+        return asyncio.run(run_fake_apiserver(a))
+    if a.command == "start":
+        try:
+            _setup_log(a)
+        except ValueError as e:
+            print(f"invalid argument: {e}", file=sys.stderr)
+            return 2
+        if a.cron_engine != "auto":
+            os.environ["CRON_OPERATOR_ENGINE"] = a.cron_engine
+        return asyncio.run(run_start(a))
+    parser.print_help()
+    return 2
+
+
+if __name__ == "__main__":
+    sys.exit(main())

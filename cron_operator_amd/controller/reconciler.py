@@ -1,0 +1,540 @@
+"""CronReconciler -- the controller logic (reference layer L4).
+
+Reference: ``internal/controller/cron_controller.go:48-437``.  The reconcile
+algorithm and its observable behaviour are
+reproduced step by step; each step below cites the reference lines.
+
+Where this implementation deliberately differs from the reference, the
+difference is a :class:`ReconcilerOptions` switch and
+``ReconcilerOptions.reference()`` restores the reference behaviour exactly
+(the benchmark's "reference mode" uses it):
+
+=========================  =====================================  =======================================
+option                     default here                           reference
+=========================  =====================================  =======================================
+``list_mode``              ``cache``: children from a label-      ``live``: LIST on every reconcile
+                           indexed informer (+ expectations)      (``cron_controller.go:241-266``)
+``finished_time``          ``completion``: the job's own           ``now``: ``metav1.Now()`` on every
+                           completion time, else first seen       reconcile (Appendix B #3)
+``skip_noop_patch``        no PATCH when the merge patch is empty  PATCH sent whenever DeepEqual differs
+``own_write_filter``       our own status writes do not requeue   every Cron update requeues (B22)
+``workload``               Pod/batch Job/MPIJob adapters on        kubeflow conditions only (B5, App. B #6-7)
+``dynamic_watches``        watch whatever kind templates use      PyTorchJob + TFJob only (B22)
+=========================  =====================================  =======================================
+
+Time comes from the injected clock (the reference calls ``time.Now()``,
+``cron_controller.go:160``), which makes every path deterministic in tests.
+"""
+from __future__ import annotations
+
+import json
+import math
+import time
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional, Tuple
+
+from ..api import errors
+from ..api.meta import (
+    GroupVersionKind,
+    creation_timestamp,
+    set_controller_reference,
+)
+from ..api.v1alpha1 import (
+    CRON_GVK,
+    CRON_GVR,
+    LABEL_CRON_NAME,
+    ConcurrentPolicyForbid,
+    ConcurrentPolicyReplace,
+    Cron,
+    CronHistory,
+    ObjectReference,
+    TypedLocalObjectReference,
+)
+from ..cron.engine import CronEngine, ScheduleError, default_engine
+from ..models import kubeflow as kf
+from ..models.workload import (
+    Classification,
+    WorkloadError,
+    WorkloadPolicy,
+    classify,
+    get_default_job_name,
+    new_empty_workload,
+)
+from ..runtime import metrics
+from ..runtime.client import Client
+from ..runtime.controller import Reconciler, Request, Result
+from ..runtime.events import Normal, Warning, EventRecorder
+from ..runtime.informer import Cache, Informer
+from ..utils import jsonutil
+from ..utils.clock import Clock, RealClock
+from ..utils.gotime import LOCAL, GoTime
+from ..utils.logging import Logger, ObjectRef
+
+CHILD_INDEX = "cron-name"
+MAX_INT = 2**63 - 1
+
+
+def go_quote(s: str) -> str:
+    """Go's ``%q`` for the strings we format (JSON escaping is a close match)."""
+    return json.dumps(s, ensure_ascii=False)
+
+
+class JoinedError(Exception):
+    """``errors.Join`` of a reconcile error and a status-patch error."""
+
+    def __init__(self, *errs: BaseException):
+        self.errors = [e for e in errs if e is not None]
+        super().__init__("\n".join(str(e) for e in self.errors))
+
+
+@dataclass
+class ReconcilerOptions:
+    list_mode: str = "cache"                 # "cache" | "live"
+    finished_time: str = "completion"        # "completion" | "now"
+    skip_noop_patch: bool = True
+    own_write_filter: bool = True
+    dynamic_watches: bool = True
+    active_ref_resource_version: bool = True
+    expectations: bool = True
+    expectation_ttl: float = 300.0           # seconds (wall)
+    workload: WorkloadPolicy = field(default_factory=WorkloadPolicy)
+    static_owned_kinds: Tuple[GroupVersionKind, ...] = (
+        GroupVersionKind("kubeflow.org", "v1", "PyTorchJob"),
+        GroupVersionKind("kubeflow.org", "v1", "TFJob"),
+    )
+
+    @staticmethod
+    def reference() -> "ReconcilerOptions":
+        return ReconcilerOptions(list_mode="live", finished_time="now", skip_noop_patch=False,
+                                 own_write_filter=False, dynamic_watches=False, expectations=False,
+                                 workload=WorkloadPolicy.reference())
+
+
+class Expectations:
+    """Children we created/deleted that the informer has not observed yet.
+
+    Keyed by ``namespace/cron``.  Entries are dropped when the informer catches
+    up (``observe_*``) or after ``ttl`` seconds.
+    """
+
+    def __init__(self, ttl: float):
+        self.ttl = ttl
+        self.created: Dict[str, Dict[str, Tuple[float, Dict[str, Any]]]] = {}
+        self.deleted: Dict[str, Dict[str, float]] = {}
+
+    def expect_create(self, key: str, obj: Dict[str, Any]) -> None:
+        uid = (obj.get("metadata") or {}).get("uid", "")
+        if uid:
+            self.created.setdefault(key, {})[uid] = (time.monotonic() + self.ttl, obj)
+
+    def expect_delete(self, key: str, uid: str) -> None:
+        if uid:
+            self.deleted.setdefault(key, {})[uid] = time.monotonic() + self.ttl
+
+    def observe_add(self, key: str, uid: str) -> None:
+        d = self.created.get(key)
+        if d is not None and d.pop(uid, None) is not None and not d:
+            del self.created[key]
+
+    def observe_delete(self, key: str, uid: str) -> None:
+        self.observe_add(key, uid)
+        d = self.deleted.get(key)
+        if d is not None and d.pop(uid, None) is not None and not d:
+            del self.deleted[key]
+
+    def adjust(self, key: str, children: List[Dict[str, Any]]) -> List[Dict[str, Any]]:
+        cr = self.created.get(key)
+        dl = self.deleted.get(key)
+        if not cr and not dl:
+            return children
+        now = time.monotonic()
+        if dl:
+            for uid in [u for u, exp in dl.items() if exp < now]:
+                del dl[uid]
+            children = [c for c in children if (c.get("metadata") or {}).get("uid") not in dl]
+        if cr:
+            for uid in [u for u, (exp, _) in cr.items() if exp < now]:
+                del cr[uid]
+            present = {(c.get("metadata") or {}).get("uid") for c in children}
+            extra = [o for u, (_, o) in cr.items() if u not in present and not (dl and u in dl)]
+            if extra:
+                children = children + extra
+        return children
+
+
+class CronReconciler(Reconciler):
+    def __init__(self, client: Client, cache: Optional[Cache], recorder: EventRecorder,
+                 clock: Optional[Clock] = None, engine: Optional[CronEngine] = None,
+                 options: Optional[ReconcilerOptions] = None, cron_informer: Optional[Informer] = None):
+        self.client = client
+        self.cache = cache
+        self.recorder = recorder
+        self.clock = clock or RealClock()
+        self.engine = engine or default_engine()
+        self.opts = options or ReconcilerOptions()
+        self.cron_informer = cron_informer
+        self.expect = Expectations(self.opts.expectation_ttl)
+        self.child_informers: Dict[GroupVersionKind, Informer] = {}
+        self.on_child_informer: Optional[Callable[[GroupVersionKind, Informer], None]] = None
+        # key -> resourceVersion of the Cron object produced by our last status write
+        self.own_writes: Dict[str, str] = {}
+        self.stats = {"creates": 0, "deletes": 0, "patches": 0, "noop_patches_skipped": 0, "lists": 0}
+        # tick bookkeeping for latency: key -> (tick unix ns, wall perf_counter when it became due)
+        self.latency_observer: Optional[Callable[[str, GoTime, Dict[str, Any]], None]] = None
+
+    # ------------------------------------------------------------------ entry point
+    async def reconcile(self, req: Request, log: Logger) -> Result:
+        """``Reconcile`` (``cron_controller.go:90-239``)."""
+        log.info("Start reconciling Cron")
+        try:
+            return await self._reconcile(req, log)
+        finally:
+            log.info("Finish reconciling Cron")
+
+    async def _get_cron(self, req: Request) -> Optional[Dict[str, Any]]:
+        if self.cron_informer is not None:
+            return self.cron_informer.get(req.namespace, req.name, copy=False)
+        try:
+            return await self.client.get(CRON_GVR, req.namespace, req.name)
+        except errors.ApiError as e:
+            if errors.is_not_found(e):
+                return None
+            raise
+
+    async def _reconcile(self, req: Request, log: Logger) -> Result:
+        # B1: cache read; NotFound -> no-op (cron_controller.go:95-104)
+        old_obj = await self._get_cron(req)
+        if old_obj is None:
+            log.info("Skip reconciling Cron for it may have been deleted")
+            return Result()
+        cron = Cron.from_dict(old_obj)
+        old_status = cron.status.deepcopy()
+
+        result = Result()
+        err: Optional[BaseException] = None
+        try:
+            result = await self._sync(cron, log)
+        except Exception as e:  # noqa: BLE001 - joined with the patch error below
+            err = e
+        # B2: deferred status patch when status changed semantically (cron_controller.go:107-120)
+        if not old_status.semantic_equal(cron.status):
+            try:
+                await self._patch_status(old_obj, cron, log)
+            except Exception as pe:  # noqa: BLE001
+                perr = RuntimeError(f"failed to patch Cron status: {pe}")
+                perr.__cause__ = pe
+                err = JoinedError(err, perr) if err is not None else perr
+            if err is not None:
+                result = Result()
+        if err is not None:
+            raise err
+        return result
+
+    async def _patch_status(self, old_obj: Dict[str, Any], cron: Cron, log: Logger) -> None:
+        new_status = cron.status.to_dict()
+        old_status = old_obj.get("status") or {}
+        patch = jsonutil.create_merge_patch({"status": old_status}, {"status": new_status} if new_status else {})
+        if not patch and self.opts.skip_noop_patch:
+            self.stats["noop_patches_skipped"] += 1
+            metrics.STATUS_PATCHES.labels("skipped").inc()
+            return
+        m = old_obj.get("metadata") or {}
+        out = await self.client.patch(CRON_GVR, m.get("namespace", ""), m.get("name", ""), patch, "merge", "status")
+        self.stats["patches"] += 1
+        metrics.STATUS_PATCHES.labels("ok").inc()
+        if self.opts.own_write_filter:
+            om = out.get("metadata") or {}
+            self.own_writes[f"{om.get('namespace', '')}/{om.get('name', '')}"] = om.get("resourceVersion", "")
+
+    def is_own_write(self, obj: Dict[str, Any]) -> bool:
+        """Predicate helper: was this Cron version produced by our last status write?"""
+        m = obj.get("metadata") or {}
+        key = f"{m.get('namespace', '')}/{m.get('name', '')}"
+        return self.own_writes.get(key) == m.get("resourceVersion")
+
+    # ------------------------------------------------------------------ the algorithm
+    async def _sync(self, cron: Cron, log: Logger) -> Result:
+        policy = self.opts.workload
+        # B3 (cron_controller.go:122-126)
+        try:
+            gvk = GroupVersionKind.from_object(new_empty_workload(cron.spec.template.workload, policy))
+        except WorkloadError as e:
+            log.error(e, "Failed to get workload GVK")
+            return Result()
+
+        # B4 (cron_controller.go:129-133)
+        try:
+            workloads = await self.list_workloads(cron, gvk, log)
+        except Exception as e:
+            log.error(e, f"Failed to list {gvk.kind}")
+            raise
+
+        # B5 (cron_controller.go:136-152)
+        active: List[Tuple[Dict[str, Any], Classification]] = []
+        terminated: List[Tuple[Dict[str, Any], Classification]] = []
+        for w in workloads:
+            try:
+                c = classify(w, gvk, policy)
+            except kf.ConversionError as e:
+                log.error(e, f"Failed to get {gvk.kind} status")
+                continue
+            (terminated if c.finished else active).append((w, c))
+        log.info(f"{gvk.kind} count", active=len(active), terminated=len(terminated))
+
+        # B6/B7/B8 (cron_controller.go:155-158)
+        await self.sync_status(cron, gvk, active, terminated, log)
+
+        now = self.clock.now(LOCAL)
+
+        # B9 (cron_controller.go:163-166)
+        if cron.deletion_timestamp is not None:
+            log.info("Cron has been deleted", deletionTimestamp=cron.metadata.get("deletionTimestamp"))
+            return Result()
+        # B10 (cron_controller.go:169-173)
+        if cron.spec.suspend:
+            log.info("Cron has been suspended")
+            return Result()
+        # B11 (cron_controller.go:176-180)
+        if cron.spec.deadline is not None and now.after(cron.spec.deadline):
+            log.info("Cron has reached deadline and will not trigger scheduling anymore")
+            self.recorder.event(cron.to_dict(), Normal, "Deadline", "cron has reach deadline and stop scheduling")
+            return Result()
+
+        # B12/B21 (cron_controller.go:184-190, 389-437)
+        try:
+            missed_run, next_run = self.get_next_schedule(cron, now, log)
+        except ScheduleError as e:
+            log.error(e, "Failed to figure out CronJob schedule")
+            return Result()
+
+        # B13 (cron_controller.go:192)
+        scheduled = Result(requeue_after_ns=next_run.sub(now))
+        if log.enabled():
+            log = log.with_values(now=now.rfc3339(nanos=True), **{"next run": next_run.rfc3339()})
+
+        # B14 (cron_controller.go:196-199)
+        if missed_run.is_zero():
+            log.v(1).info("No upcoming schedules, wait until next")
+            return scheduled
+        if log.enabled():
+            log = log.with_values(**{"current run": missed_run.rfc3339()})
+
+        # B15 (cron_controller.go:204-207)
+        if cron.spec.concurrency_policy == ConcurrentPolicyForbid and active:
+            log.v(1).info(f"Skip creating new {gvk.kind} due to concurrency policy forbid", active=len(active))
+            return scheduled
+
+        # B16 (cron_controller.go:210-220)
+        if cron.spec.concurrency_policy == ConcurrentPolicyReplace:
+            for w, _ in active:
+                m = w.get("metadata") or {}
+                ref = ObjectRef(m.get("namespace", ""), m.get("name", ""))
+                log.info(f"Deleting active {gvk.kind}", **{gvk.kind: ref})
+                try:
+                    await self.client.delete(gvk, m.get("namespace", ""), m.get("name", ""),
+                                             propagation_policy="Background")
+                    self.stats["deletes"] += 1
+                    metrics.WORKLOADS_DELETED.labels(gvk.kind, "replace").inc()
+                    if self.opts.expectations:
+                        self.expect.expect_delete(self._ckey(cron), m.get("uid", ""))
+                except errors.ApiError as e:
+                    if not errors.is_not_found(e):
+                        log.error(e, f"Failed to delete active {gvk.kind}", **{gvk.kind: ref})
+                        raise
+
+        # B18 (cron_controller.go:222-225, 349-387)
+        try:
+            workload = self.new_workload_from_template(cron, next_run)
+        except Exception as e:
+            raise RuntimeError(f"unable to initialize {gvk.kind} from cron template: {e}") from e
+
+        # B19 (cron_controller.go:227-236)
+        wm = workload["metadata"]
+        ref = ObjectRef(wm.get("namespace", ""), wm.get("name", ""))
+        log.info(f"Creating {gvk.kind}", **{gvk.kind: ref})
+        try:
+            created = await self.client.create(gvk, workload, wm.get("namespace", ""))
+            self.stats["creates"] += 1
+            metrics.WORKLOADS_CREATED.labels(gvk.kind).inc()
+            if self.opts.expectations:
+                self.expect.expect_create(self._ckey(cron), created)
+            if self.latency_observer is not None:
+                self.latency_observer(self._ckey(cron), missed_run, created)
+            metrics.SCHEDULE_LATENCY.labels("cron").observe(
+                max(0.0, (self.clock.now_ns() - missed_run.unix_nano()) / 1e9))
+        except errors.ApiError as e:
+            if errors.is_already_exists(e):
+                log.info(f"{gvk.kind} already exists", **{gvk.kind: ref})
+            else:
+                self.recorder.eventf(cron.to_dict(), Warning, "FailedCreate", "Error creating %s: %s", gvk.kind, e)
+                raise
+        # B20 (cron_controller.go:237)
+        cron.status.last_schedule_time = now
+        return scheduled
+
+    # ------------------------------------------------------------------ children
+    @staticmethod
+    def _ckey(cron: Cron) -> str:
+        return f"{cron.namespace}/{cron.name}"
+
+    async def child_informer(self, gvk: GroupVersionKind) -> Informer:
+        inf = self.child_informers.get(gvk)
+        if inf is None:
+            assert self.cache is not None
+            from ..runtime.informer import label_index
+
+            inf = await self.cache.get_informer(gvk, label_selector=LABEL_CRON_NAME,
+                                                indexers={CHILD_INDEX: label_index(LABEL_CRON_NAME)})
+            self.child_informers[gvk] = inf
+            inf.start()
+            if self.on_child_informer is not None:
+                self.on_child_informer(gvk, inf)
+        if not inf.synced.is_set():
+            await inf.synced.wait()
+        return inf
+
+    async def list_workloads(self, cron: Cron, gvk: GroupVersionKind, log: Logger) -> List[Dict[str, Any]]:
+        """``listWorkloads`` (``cron_controller.go:241-266``): children of the template GVK in
+        the Cron's namespace labelled ``kubedl.io/cron-name=<name>``."""
+        log.v(1).info(f"Listing {gvk.kind}")
+        self.stats["lists"] += 1
+        if self.opts.list_mode == "live" or self.cache is None:
+            lst = await self.client.list(gvk, cron.namespace, label_selector=f"{LABEL_CRON_NAME}={cron.name}")
+            items = lst.get("items") or []
+            for it in items:
+                # list items may omit apiVersion/kind (built-in kinds); the reference reads them off the GVK
+                it.setdefault("apiVersion", gvk.api_version)
+                it.setdefault("kind", gvk.kind)
+            return items
+        inf = await self.child_informer(gvk)
+        children = inf.by_index(CHILD_INDEX, f"{cron.namespace}/{cron.name}", copy=False)
+        if self.opts.expectations:
+            children = self.expect.adjust(self._ckey(cron), children)
+        return children
+
+    # ------------------------------------------------------------------ status
+    async def sync_status(self, cron: Cron, gvk: GroupVersionKind, active: List[Tuple[Dict[str, Any], Classification]],
+                          terminated: List[Tuple[Dict[str, Any], Classification]], log: Logger) -> None:
+        """``syncStatus`` (``cron_controller.go:268-282``)."""
+        log.v(1).info("Syncing Cron status")
+        self.sync_active_list(cron, gvk, active, log)
+        await self.sync_cron_history(cron, gvk, terminated, log)
+
+    @staticmethod
+    def _sort(items: List[Tuple[Dict[str, Any], Classification]]) -> None:
+        items.sort(key=lambda wc: creation_timestamp(wc[0]).key())
+
+    def sync_active_list(self, cron: Cron, gvk: GroupVersionKind, active: List[Tuple[Dict[str, Any], Classification]],
+                         log: Logger) -> None:
+        """``syncActiveList`` (``cron_controller.go:284-304``)."""
+        log.v(1).info("Syncing active list")
+        self._sort(active)
+        refs = []
+        with_rv = self.opts.active_ref_resource_version
+        for w, _ in active:
+            m = w.get("metadata") or {}
+            wgvk = GroupVersionKind.from_object(w)
+            refs.append(ObjectReference(api_version=wgvk.api_version, kind=wgvk.kind, name=m.get("name", ""),
+                                        namespace=m.get("namespace", ""), uid=m.get("uid", ""),
+                                        resource_version=m.get("resourceVersion", "") if with_rv else ""))
+        cron.status.active = refs
+
+    async def sync_cron_history(self, cron: Cron, gvk: GroupVersionKind,
+                                terminated: List[Tuple[Dict[str, Any], Classification]], log: Logger) -> None:
+        """``syncCronHistory`` incl. history-limit GC (``cron_controller.go:306-346``)."""
+        log.v(1).info("Syncing Cron history")
+        self._sort(terminated)
+        n = len(terminated)
+        limit = cron.spec.history_limit if cron.spec.history_limit is not None else MAX_INT
+        previous = {h.uid: h for h in cron.status.history if h.uid}
+        history: List[CronHistory] = []
+        now: Optional[GoTime] = None
+        for i, (w, c) in enumerate(terminated):
+            m = w.get("metadata") or {}
+            wgvk = GroupVersionKind.from_object(w)
+            ref = ObjectRef(m.get("namespace", ""), m.get("name", ""))
+            if i < n - limit:
+                log.info(f"Deleting terminated {wgvk.kind}", **{wgvk.kind: ref})
+                try:
+                    await self.client.delete(wgvk, m.get("namespace", ""), m.get("name", ""),
+                                             propagation_policy="Background")
+                    self.stats["deletes"] += 1
+                    metrics.WORKLOADS_DELETED.labels(wgvk.kind, "history").inc()
+                    if self.opts.expectations:
+                        self.expect.expect_delete(self._ckey(cron), m.get("uid", ""))
+                except errors.ApiError as e:
+                    if not errors.is_not_found(e):
+                        log.error(e, f"Failed to delete terminated {wgvk.kind}", **{wgvk.kind: ref})
+                continue
+            entry = CronHistory(uid=m.get("uid", ""),
+                                object=TypedLocalObjectReference(api_group=wgvk.group_version().__str__(),
+                                                                 kind=wgvk.kind, name=m.get("name", "")),
+                                status=c.status, created=creation_timestamp(w))
+            if c.finished:
+                if self.opts.finished_time == "now":
+                    if now is None:
+                        now = self.clock.now(LOCAL)
+                    entry.finished = now
+                else:
+                    prev = previous.get(entry.uid)
+                    if c.finished_at is not None:
+                        entry.finished = c.finished_at
+                    elif prev is not None and prev.finished is not None:
+                        entry.finished = prev.finished
+                    else:
+                        # first observation: second precision so it survives the JSON round trip
+                        t = self.clock.now(LOCAL)
+                        entry.finished = GoTime(t.sec, 0, t.loc)
+            history.append(entry)
+        cron.status.history = history
+
+    # ------------------------------------------------------------------ workload creation
+    def new_workload_from_template(self, cron: Cron, schedule_time: GoTime) -> Dict[str, Any]:
+        """``newWorkloadFromTemplate`` (``cron_controller.go:348-387``)."""
+        w = new_empty_workload(cron.spec.template.workload, self.opts.workload)
+        m = w.get("metadata")
+        if not isinstance(m, dict):
+            m = w["metadata"] = {}
+        # generateName is forbidden: a retried create must hit AlreadyExists (:355-362)
+        if m.get("generateName"):
+            m["generateName"] = ""
+            del m["generateName"]
+        if not m.get("name"):
+            m["name"] = get_default_job_name(cron.name, schedule_time)
+        else:
+            self.recorder.event(cron.to_dict(), Normal, "OverridePolicy",
+                                "metadata.name has been specified in workload template, override cron concurrency "
+                                "policy as Forbidden")
+            cron.spec.concurrency_policy = ConcurrentPolicyForbid
+        m["namespace"] = cron.namespace
+        labels = m.get("labels")
+        if not isinstance(labels, dict):
+            labels = m["labels"] = {}
+        labels[LABEL_CRON_NAME] = cron.name
+        set_controller_reference({"metadata": cron.metadata}, CRON_GVK, w)
+        return w
+
+    # ------------------------------------------------------------------ schedule
+    def get_next_schedule(self, cron: Cron, now: GoTime, log: Optional[Logger] = None) -> Tuple[GoTime, GoTime]:
+        """``getNextSchedule`` (``cron_controller.go:389-437``) -> (last missed, next)."""
+        spec = cron.spec.schedule
+        try:
+            sched = self.engine.parse(spec)
+        except ScheduleError as e:
+            raise ScheduleError(f"unparsable cron {go_quote(spec)}: {e}") from None
+        earliest = cron.status.last_schedule_time
+        if earliest is None:
+            earliest = cron.creation_timestamp
+        if earliest.after(now):
+            return GoTime.zero(), self.engine.next(sched, now)
+        last, missed, bad = self.engine.missed(sched, earliest, now)
+        if bad:
+            raise ScheduleError(f"unschedulable cron {go_quote(spec)}: no matching time within five years")
+        if missed > 1:
+            metrics.MISSED_TICKS.inc(missed - 1)
+        if missed > 100:
+            self.recorder.eventf(cron.to_dict(), Warning, "TooManyMissedTimes",
+                                 "too many missed start times: %d. Check clock skew", missed)
+            if log is not None:
+                log.info("Too many missed times", **{"missed times": missed})
+        return last, self.engine.next(sched, now)

@@ -1,0 +1,87 @@
+"""Controller wiring -- ``SetupWithManager`` (``internal/controller/cron_controller.go:69-77``).
+
+* ``For(&Cron{})`` -- the Cron informer feeds the queue; with
+  ``own_write_filter`` the update events produced by our own status patches
+  are dropped (the reconcile they would trigger recomputes the same status);
+* ``Owns(PyTorchJob)``, ``Owns(TFJob)`` -- as in the reference; the informers are
+  label-selected on ``kubedl.io/cron-name`` in cache mode (we only ever need
+  children), unfiltered in reference/live mode;
+* with ``dynamic_watches`` any other template kind (MPIJob, batch Job, Pod, ...)
+  gets an owned watch the first time a Cron uses it, so its completion is
+  noticed (the reference never watches MPIJob);
+* ``WithLogConstructor(logConstructor(..., "cron"))`` (``util.go:27-41``).
+
+RBAC (the reference's markers at ``cron_controller.go:79-85`` name the wrong
+group ``kubedl.io``) is generated with the correct group
+by :mod:`cron_operator_amd.controller.rbac`.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional, Tuple
+
+from ..api import errors
+from ..api.meta import GroupVersionKind
+from ..api.v1alpha1 import CRON_GVK, LABEL_CRON_NAME
+from ..cron.engine import CronEngine
+from ..runtime.controller import Controller
+from ..runtime.informer import EventHandler, Informer, label_index
+from ..runtime.manager import Manager
+from ..utils.logging import get_logger, log_constructor
+from .reconciler import CHILD_INDEX, CronReconciler, ReconcilerOptions
+
+CONTROLLER_NAME = "cron"
+
+
+async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] = None,
+                             engine: Optional[CronEngine] = None) -> Tuple[Controller, CronReconciler]:
+    opts = options or ReconcilerOptions()
+    log = get_logger()
+    cron_inf = await mgr.cache.get_informer(CRON_GVK)
+    rec = CronReconciler(mgr.client, mgr.cache, mgr.get_event_recorder_for(CONTROLLER_NAME), mgr.clock, engine,
+                         opts, cron_inf)
+    ctrl = Controller(CONTROLLER_NAME, rec, mgr.clock, mgr.opts.max_concurrent_reconciles, log)
+    ctrl.set_log_constructor(log_constructor(log, "Cron"))
+
+    preds = []
+    if opts.own_write_filter:
+        def not_own_write(event: str, old, new) -> bool:
+            return not (event == "update" and rec.is_own_write(new))
+        preds.append(not_own_write)
+    ctrl.watch_for(cron_inf, CRON_GVK, preds)
+
+    watched: Dict[GroupVersionKind, Informer] = {}
+
+    def attach(gvk: GroupVersionKind, inf: Informer) -> None:
+        if gvk in watched:
+            return
+        watched[gvk] = inf
+        ctrl.watch_owned(inf, CRON_GVK)
+        if opts.expectations:
+            def key_of(obj) -> str:
+                m = obj.get("metadata") or {}
+                return f"{m.get('namespace', '')}/{(m.get('labels') or {}).get(LABEL_CRON_NAME, '')}"
+
+            inf.add_handler(EventHandler(
+                on_add=lambda o: rec.expect.observe_add(key_of(o), (o.get("metadata") or {}).get("uid", "")),
+                on_update=lambda old, o: rec.expect.observe_add(key_of(o), (o.get("metadata") or {}).get("uid", "")),
+                on_delete=lambda o: rec.expect.observe_delete(key_of(o), (o.get("metadata") or {}).get("uid", ""))))
+
+    for gvk in opts.static_owned_kinds:
+        try:
+            if opts.list_mode == "cache":
+                inf = await mgr.cache.get_informer(gvk, label_selector=LABEL_CRON_NAME,
+                                                   indexers={CHILD_INDEX: label_index(LABEL_CRON_NAME)})
+                rec.child_informers[gvk] = inf
+            else:
+                inf = await mgr.cache.get_informer(gvk)
+        except errors.ApiError as e:
+            # the reference fails to start without these CRDs; we keep running and
+            # pick the kind up lazily once a Cron uses it
+            log.info("owned kind not served by the apiserver, watching lazily", kind=gvk.kind, error=str(e))
+            continue
+        attach(gvk, inf)
+
+    if opts.dynamic_watches:
+        rec.on_child_informer = attach
+    mgr.add_controller(ctrl)
+    return ctrl, rec

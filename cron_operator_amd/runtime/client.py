@@ -1,0 +1,352 @@
+"""Kubernetes API client: transports, REST mapping, throttling, request metrics.
+
+Counterpart of the client-go/controller-runtime client the reference talks to
+the apiserver with (the only process boundary).  Layers:
+
+* :class:`Transport` -- raw verbs against one apiserver.  :class:`InMemoryTransport`
+  calls the fake :class:`~cron_operator_amd.apiserver.server.APIServer` directly
+  (tests, single-process bench); :class:`~cron_operator_amd.runtime.http.HttpTransport`
+  speaks the Kubernetes REST protocol to any apiserver (real clusters, the fake
+  apiserver served over HTTP).
+* :class:`RESTMapper` -- GVK -> resource via discovery, cached.
+* :class:`Client` -- typed-ish convenience on top: ``get/list/create/update/patch/
+  delete/watch`` by GVR or GVK, a ``status`` sub-client (``client.Status()``),
+  merge-patch from an old object (``client.MergeFrom``), the client-side token
+  bucket (``--qps``/``--burst``) and ``rest_client_*`` metrics.
+"""
+from __future__ import annotations
+
+import asyncio
+import time
+from typing import Any, AsyncIterator, Dict, List, Optional, Tuple, Union
+
+from ..api import errors
+from ..api.meta import GroupVersion, GroupVersionKind, GroupVersionResource
+from ..utils import jsonutil
+from . import metrics
+from .ratelimit import TokenBucket, make_client_limiter
+
+GVRorGVK = Union[GroupVersionResource, GroupVersionKind]
+
+MERGE = "merge"
+JSON_PATCH = "json"
+STRATEGIC = "strategic"
+
+PATCH_CONTENT_TYPES = {
+    MERGE: "application/merge-patch+json",
+    JSON_PATCH: "application/json-patch+json",
+    STRATEGIC: "application/strategic-merge-patch+json",
+}
+
+
+class Transport:
+    host = "in-memory"
+
+    async def request(self, verb: str, gvr: GroupVersionResource, namespace: str = "", name: str = "",
+                      subresource: str = "", body: Any = None, params: Optional[Dict[str, Any]] = None) -> Any:
+        raise NotImplementedError
+
+    async def watch(self, gvr: GroupVersionResource, namespace: str = "",
+                    params: Optional[Dict[str, Any]] = None) -> "WatchStream":
+        raise NotImplementedError
+
+    async def discover(self, group_version: GroupVersion) -> List[Dict[str, Any]]:
+        raise NotImplementedError
+
+    async def close(self) -> None:
+        pass
+
+
+class WatchStream:
+    """Async iterator of ``(type, object)``; ``stop()`` ends it."""
+
+    def __aiter__(self):
+        return self
+
+    async def __anext__(self) -> Tuple[str, Dict[str, Any]]:
+        raise NotImplementedError
+
+    def stop(self) -> None:
+        raise NotImplementedError
+
+
+class _MemWatch(WatchStream):
+    def __init__(self, w):
+        self._w = w
+
+    async def __anext__(self) -> Tuple[str, Dict[str, Any]]:
+        return await self._w.__anext__()
+
+    def stop(self) -> None:
+        self._w.stop()
+
+
+class InMemoryTransport(Transport):
+    """Direct calls into an in-process fake APIServer (same event loop)."""
+
+    host = "in-memory"
+
+    def __init__(self, server, yield_every: int = 1):
+        self.server = server
+        self._yield_every = max(1, yield_every)
+        self._n = 0
+
+    async def _gate(self, verb: str, resource: str, sub: str, name: str) -> None:
+        faults = self.server.faults
+        delay = faults.delay_for(verb) if faults.latency else 0.0
+        if delay > 0:
+            await asyncio.sleep(delay)
+        else:
+            self._n += 1
+            if self._n % self._yield_every == 0:
+                await asyncio.sleep(0)  # a real round trip yields to other tasks
+        if faults.faults:
+            faults.check(verb, resource, sub or None, name or None)
+
+    async def request(self, verb: str, gvr: GroupVersionResource, namespace: str = "", name: str = "",
+                      subresource: str = "", body: Any = None, params: Optional[Dict[str, Any]] = None) -> Any:
+        params = params or {}
+        s = self.server
+        await self._gate(verb, gvr.resource, subresource, name)
+        if verb == "get":
+            return s.get(gvr, namespace, name)
+        if verb == "list":
+            return s.list(gvr, namespace or None, params.get("labelSelector"), params.get("fieldSelector"),
+                          int(params.get("limit") or 0), params.get("continue"))
+        if verb == "create":
+            return s.create(gvr, namespace, body, dry_run=bool(params.get("dryRun")))
+        if verb == "update":
+            return s.update(gvr, namespace, name, body, subresource or None)
+        if verb == "patch":
+            return s.patch(gvr, namespace, name, body, params.get("patchType", MERGE), subresource or None)
+        if verb == "delete":
+            opts = body or {}
+            return s.delete(gvr, namespace, name, opts.get("propagationPolicy"), opts.get("preconditions"))
+        if verb == "deletecollection":
+            return s.delete_collection(gvr, namespace or None, params.get("labelSelector"))
+        raise ValueError(f"unknown verb {verb}")
+
+    async def watch(self, gvr: GroupVersionResource, namespace: str = "",
+                    params: Optional[Dict[str, Any]] = None) -> WatchStream:
+        params = params or {}
+        await self._gate("watch", gvr.resource, "", "")
+        w = self.server.watch(gvr, namespace or None, str(params.get("resourceVersion") or ""),
+                              params.get("labelSelector"), params.get("fieldSelector"),
+                              bool(params.get("allowWatchBookmarks")))
+        return _MemWatch(w)
+
+    async def discover(self, group_version: GroupVersion) -> List[Dict[str, Any]]:
+        return [ri.discovery_entry() for ri in self.server.resources()
+                if ri.group == group_version.group and ri.version == group_version.version]
+
+
+class NoKindMatchError(errors.ApiError):
+    def __init__(self, gvk: GroupVersionKind):
+        super().__init__(404, "NotFound", f'no matches for kind "{gvk.kind}" in version "{gvk.api_version}"')
+        self.gvk = gvk
+
+
+class RESTMapper:
+    """GVK <-> GVR via discovery (``meta.RESTMapper``), with a negative cache that
+    is refreshed on miss (CRDs may be installed after start)."""
+
+    def __init__(self, transport: Transport):
+        self.transport = transport
+        self._gvk: Dict[GroupVersionKind, Tuple[GroupVersionResource, bool]] = {}
+        self._gvr: Dict[GroupVersionResource, Tuple[GroupVersionKind, bool]] = {}
+        self._loaded: Dict[GroupVersion, float] = {}
+
+    async def _load(self, gv: GroupVersion, force: bool = False) -> None:
+        if not force and gv in self._loaded:
+            return
+        try:
+            entries = await self.transport.discover(gv)
+        except errors.ApiError as e:
+            if e.code == 404:
+                entries = []
+            else:
+                raise
+        for e in entries:
+            name = e.get("name", "")
+            if "/" in name:
+                continue
+            gvr = GroupVersionResource(gv.group, gv.version, name)
+            gvk = GroupVersionKind(gv.group, gv.version, e.get("kind", ""))
+            self._gvk[gvk] = (gvr, bool(e.get("namespaced", True)))
+            self._gvr[gvr] = (gvk, bool(e.get("namespaced", True)))
+        self._loaded[gv] = time.monotonic()
+
+    async def resource_for(self, gvk: GroupVersionKind) -> Tuple[GroupVersionResource, bool]:
+        hit = self._gvk.get(gvk)
+        if hit is not None:
+            return hit
+        await self._load(gvk.group_version())
+        hit = self._gvk.get(gvk)
+        if hit is None:
+            await self._load(gvk.group_version(), force=True)
+            hit = self._gvk.get(gvk)
+        if hit is None:
+            raise NoKindMatchError(gvk)
+        return hit
+
+    async def kind_for(self, gvr: GroupVersionResource) -> Tuple[GroupVersionKind, bool]:
+        hit = self._gvr.get(gvr)
+        if hit is None:
+            await self._load(GroupVersion(gvr.group, gvr.version), force=True)
+            hit = self._gvr.get(gvr)
+        if hit is None:
+            raise errors.ApiError(404, "NotFound", f"no matches for {gvr}")
+        return hit
+
+    def register(self, gvk: GroupVersionKind, gvr: GroupVersionResource, namespaced: bool = True) -> None:
+        self._gvk[gvk] = (gvr, namespaced)
+        self._gvr[gvr] = (gvk, namespaced)
+
+
+class Client:
+    """The controller's API client (controller-runtime ``client.Client`` analog)."""
+
+    def __init__(self, transport: Transport, qps: float = 30.0, burst: int = 50,
+                 limiter: Optional[TokenBucket] = None, mapper: Optional[RESTMapper] = None):
+        self.transport = transport
+        self.limiter = limiter if limiter is not None else make_client_limiter(qps, burst)
+        self.mapper = mapper or RESTMapper(transport)
+        self.host = getattr(transport, "host", "in-memory")
+        self.requests = 0
+        self.requests_by_verb: Dict[str, int] = {}
+
+    # -- plumbing
+    async def _gvr(self, target: GVRorGVK) -> GroupVersionResource:
+        if isinstance(target, GroupVersionResource):
+            return target
+        return (await self.mapper.resource_for(target))[0]
+
+    async def _throttle(self, verb: str) -> None:
+        if self.limiter is not None:
+            d = await self.limiter.wait()
+            metrics.REST_RATE_LIMIT.labels(verb, self.host).observe(d)
+
+    _METHOD = {"get": "GET", "list": "GET", "watch": "GET", "create": "POST", "update": "PUT", "patch": "PATCH",
+               "delete": "DELETE", "deletecollection": "DELETE"}
+
+    async def _do(self, verb: str, gvr: GroupVersionResource, namespace: str = "", name: str = "",
+                  subresource: str = "", body: Any = None, params: Optional[Dict[str, Any]] = None) -> Any:
+        await self._throttle(verb)
+        self.requests += 1
+        self.requests_by_verb[verb] = self.requests_by_verb.get(verb, 0) + 1
+        t0 = time.perf_counter()
+        code = "200"
+        try:
+            return await self.transport.request(verb, gvr, namespace, name, subresource, body, params)
+        except errors.ApiError as e:
+            code = str(e.code)
+            raise
+        except Exception:
+            code = "<error>"
+            raise
+        finally:
+            metrics.REST_REQUESTS.labels(code, self.host, self._METHOD.get(verb, verb.upper())).inc()
+            metrics.REST_LATENCY.labels(verb.upper(), self.host).observe(time.perf_counter() - t0)
+
+    # -- verbs
+    async def get(self, target: GVRorGVK, namespace: str, name: str) -> Dict[str, Any]:
+        return await self._do("get", await self._gvr(target), namespace, name)
+
+    async def list(self, target: GVRorGVK, namespace: str = "", label_selector: Optional[str] = None,
+                   field_selector: Optional[str] = None, limit: int = 0,
+                   continue_: Optional[str] = None) -> Dict[str, Any]:
+        params: Dict[str, Any] = {}
+        if label_selector:
+            params["labelSelector"] = label_selector
+        if field_selector:
+            params["fieldSelector"] = field_selector
+        if limit:
+            params["limit"] = limit
+        if continue_:
+            params["continue"] = continue_
+        return await self._do("list", await self._gvr(target), namespace, params=params)
+
+    async def list_all(self, target: GVRorGVK, namespace: str = "", label_selector: Optional[str] = None,
+                       page_size: int = 500) -> Dict[str, Any]:
+        """Paged LIST (client-go pager) returning one merged list."""
+        out: Optional[Dict[str, Any]] = None
+        cont = None
+        while True:
+            page = await self.list(target, namespace, label_selector, limit=page_size, continue_=cont)
+            if out is None:
+                out = page
+            else:
+                out["items"].extend(page["items"])
+                out["metadata"]["resourceVersion"] = page["metadata"].get("resourceVersion")
+            cont = (page.get("metadata") or {}).get("continue")
+            if not cont:
+                break
+        assert out is not None
+        out["metadata"].pop("continue", None)
+        return out
+
+    async def create(self, target: GVRorGVK, obj: Dict[str, Any], namespace: Optional[str] = None,
+                     dry_run: bool = False) -> Dict[str, Any]:
+        ns = namespace if namespace is not None else (obj.get("metadata") or {}).get("namespace", "")
+        return await self._do("create", await self._gvr(target), ns, body=obj,
+                              params={"dryRun": "All"} if dry_run else None)
+
+    async def update(self, target: GVRorGVK, obj: Dict[str, Any], subresource: str = "") -> Dict[str, Any]:
+        m = obj.get("metadata") or {}
+        return await self._do("update", await self._gvr(target), m.get("namespace", ""), m.get("name", ""),
+                              subresource, body=obj)
+
+    async def patch(self, target: GVRorGVK, namespace: str, name: str, patch: Any, patch_type: str = MERGE,
+                    subresource: str = "") -> Dict[str, Any]:
+        return await self._do("patch", await self._gvr(target), namespace, name, subresource, body=patch,
+                              params={"patchType": patch_type})
+
+    async def delete(self, target: GVRorGVK, namespace: str, name: str, propagation_policy: Optional[str] = None,
+                     preconditions: Optional[Dict[str, str]] = None) -> Any:
+        opts: Dict[str, Any] = {}
+        if propagation_policy:
+            opts["propagationPolicy"] = propagation_policy
+        if preconditions:
+            opts["preconditions"] = preconditions
+        return await self._do("delete", await self._gvr(target), namespace, name, body=opts or None)
+
+    async def delete_all_of(self, target: GVRorGVK, namespace: str = "", label_selector: Optional[str] = None) -> Any:
+        params = {"labelSelector": label_selector} if label_selector else {}
+        return await self._do("deletecollection", await self._gvr(target), namespace, params=params)
+
+    async def watch(self, target: GVRorGVK, namespace: str = "", resource_version: str = "",
+                    label_selector: Optional[str] = None, field_selector: Optional[str] = None,
+                    allow_bookmarks: bool = True, timeout_seconds: Optional[int] = None) -> WatchStream:
+        gvr = await self._gvr(target)
+        await self._throttle("watch")
+        self.requests += 1
+        self.requests_by_verb["watch"] = self.requests_by_verb.get("watch", 0) + 1
+        params: Dict[str, Any] = {"watch": "true", "resourceVersion": resource_version,
+                                  "allowWatchBookmarks": "true" if allow_bookmarks else "false"}
+        if label_selector:
+            params["labelSelector"] = label_selector
+        if field_selector:
+            params["fieldSelector"] = field_selector
+        if timeout_seconds:
+            params["timeoutSeconds"] = timeout_seconds
+        try:
+            w = await self.transport.watch(gvr, namespace, params)
+        except errors.ApiError as e:
+            metrics.REST_REQUESTS.labels(str(e.code), self.host, "GET").inc()
+            raise
+        metrics.REST_REQUESTS.labels("200", self.host, "GET").inc()
+        return w
+
+    # -- controller-runtime idioms
+    async def patch_status_from(self, target: GVRorGVK, old: Dict[str, Any], new: Dict[str, Any]) -> Dict[str, Any]:
+        """``client.Status().Patch(ctx, new, client.MergeFrom(old))``."""
+        patch = jsonutil.create_merge_patch(old, new)
+        m = new.get("metadata") or {}
+        return await self.patch(target, m.get("namespace", ""), m.get("name", ""), patch, MERGE, "status")
+
+    async def update_status(self, target: GVRorGVK, obj: Dict[str, Any]) -> Dict[str, Any]:
+        """``client.Status().Update(ctx, obj)``."""
+        return await self.update(target, obj, "status")
+
+    async def close(self) -> None:
+        await self.transport.close()

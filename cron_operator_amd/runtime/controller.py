@@ -1,0 +1,269 @@
+"""Controller: watches -> work queue -> N reconcile workers.
+
+Equivalent of ``ctrl.NewControllerManagedBy(mgr).For(&Cron{}).Owns(...)``
+(``internal/controller/cron_controller.go:70-77``) plus the controller-runtime
+worker loop it drives [ext]:
+
+* ``for_(gvk)`` enqueues the object's own key on add/update/delete;
+* ``owns(gvk)`` maps a child event to its *controller* owner of the For kind;
+* ``watches(gvk, map_fn)`` is the generic map-function source;
+* predicates filter events before they reach the queue;
+* result handling matches controller-runtime: error -> rate-limited requeue
+  (``result=error``), ``requeue_after`` -> forget + delayed add
+  (``requeue_after``), ``requeue`` -> rate-limited (``requeue``), else forget
+  (``success``); panics are recovered and counted;
+* ``controller_runtime_*`` and ``workqueue_*`` metrics, per-request loggers from
+  a log constructor (``internal/controller/util.go:27-41``) with a
+  ``reconcileID``.
+"""
+from __future__ import annotations
+
+import asyncio
+import time
+import traceback
+import uuid
+from dataclasses import dataclass
+from typing import Any, Awaitable, Callable, Dict, List, Optional, Tuple
+
+from ..api.meta import GroupVersionKind, NamespacedName, controller_ref
+from ..parallel.workqueue import ShutDown, WorkQueue
+from ..utils.clock import Clock
+from ..utils.logging import Logger, get_logger, log_constructor
+from . import metrics
+from .informer import EventHandler, Informer
+
+Request = NamespacedName
+
+PRIORITY_EVENT = 0
+PRIORITY_SCHEDULE = 10
+
+
+@dataclass
+class Result:
+    requeue: bool = False
+    requeue_after: float = 0.0  # seconds
+    requeue_after_ns: int = 0   # exact form (schedule requeues land on the tick)
+
+    def after_ns(self) -> int:
+        return self.requeue_after_ns or int(self.requeue_after * 1e9)
+
+    def is_zero(self) -> bool:
+        return not self.requeue and self.after_ns() == 0
+
+
+class TerminalError(Exception):
+    """An error that should not be retried (``reconcile.TerminalError``)."""
+
+
+class Reconciler:
+    async def reconcile(self, req: Request, log: Logger) -> Result:
+        raise NotImplementedError
+
+
+Predicate = Callable[[str, Optional[Dict[str, Any]], Dict[str, Any]], bool]  # (event, old, new) -> keep?
+
+
+def generation_changed(event: str, old: Optional[Dict[str, Any]], new: Dict[str, Any]) -> bool:
+    if event != "update" or old is None:
+        return True
+    return (old.get("metadata") or {}).get("generation") != (new.get("metadata") or {}).get("generation")
+
+
+def _key(obj: Dict[str, Any]) -> Request:
+    m = obj.get("metadata") or {}
+    return Request(m.get("namespace", ""), m.get("name", ""))
+
+
+class Controller:
+    def __init__(self, name: str, reconciler: Reconciler, clock: Clock, max_concurrent_reconciles: int = 1,
+                 logger: Optional[Logger] = None, recover_panic: bool = True, queue: Optional[WorkQueue] = None):
+        self.name = name
+        self.reconciler = reconciler
+        self.clock = clock
+        self.max_concurrent = max(1, max_concurrent_reconciles)
+        base = logger or get_logger()
+        self.log = base.with_values(controller=name)
+        self._log_ctor = log_constructor(base, "Cron") if name == "cron" else None
+        self.recover_panic = recover_panic
+        self.queue = queue or WorkQueue(name, clock, controller=name)
+        self._sources: List[Tuple[Informer, EventHandler]] = []
+        self._workers: List[asyncio.Task] = []
+        self.active = 0
+        self.reconciles = 0
+        self.errors = 0
+        self.started = False
+        self.result_counts: Dict[str, int] = {}
+        self.on_result: Optional[Callable[[Request, Optional[Result], Optional[BaseException]], None]] = None
+        self._m_active = metrics.ACTIVE_WORKERS.labels(name)
+        self._m_time = metrics.RECONCILE_TIME.labels(name)
+        metrics.MAX_CONCURRENT.labels(name).set(self.max_concurrent)
+        self.for_kind: Optional[GroupVersionKind] = None
+
+    def set_log_constructor(self, ctor: Callable[[Optional[Request]], Logger]) -> None:
+        self._log_ctor = ctor
+
+    # ------------------------------------------------------------------ sources
+    def _handler(self, mapper: Callable[[Dict[str, Any]], List[Request]],
+                 predicates: List[Predicate]) -> EventHandler:
+        q = self.queue
+
+        def ok(event: str, old: Optional[Dict[str, Any]], new: Dict[str, Any]) -> bool:
+            return all(p(event, old, new) for p in predicates)
+
+        def on_add(obj: Dict[str, Any]) -> None:
+            if ok("create", None, obj):
+                for r in mapper(obj):
+                    q.add(r, PRIORITY_EVENT)
+
+        def on_update(old: Dict[str, Any], new: Dict[str, Any]) -> None:
+            if ok("update", old, new):
+                for r in mapper(new):
+                    q.add(r, PRIORITY_EVENT)
+                # an owner change moves the child: also wake the previous owner
+                for r in mapper(old):
+                    q.add(r, PRIORITY_EVENT)
+
+        def on_delete(obj: Dict[str, Any]) -> None:
+            if ok("delete", None, obj):
+                for r in mapper(obj):
+                    q.add(r, PRIORITY_EVENT)
+
+        return EventHandler(on_add, on_update, on_delete)
+
+    def watch_for(self, informer: Informer, gvk: GroupVersionKind, predicates: Optional[List[Predicate]] = None) -> None:
+        """``For(&Cron{})``: enqueue the object itself."""
+        self.for_kind = gvk
+        h = self._handler(lambda o: [_key(o)], list(predicates or []))
+        self._sources.append((informer, h))
+        informer.add_handler(h)
+
+    def watch_owned(self, informer: Informer, owner: GroupVersionKind,
+                    predicates: Optional[List[Predicate]] = None) -> None:
+        """``Owns(&Child{})``: enqueue the child's controller owner of kind ``owner``."""
+
+        def mapper(obj: Dict[str, Any]) -> List[Request]:
+            ref = controller_ref(obj)
+            if ref is None or ref.get("kind") != owner.kind:
+                return []
+            if (ref.get("apiVersion", "").split("/")[0]) != owner.group:
+                return []
+            return [Request((obj.get("metadata") or {}).get("namespace", ""), ref.get("name", ""))]
+
+        h = self._handler(mapper, list(predicates or []))
+        self._sources.append((informer, h))
+        informer.add_handler(h)
+
+    def watch_map(self, informer: Informer, fn: Callable[[Dict[str, Any]], List[Request]],
+                  predicates: Optional[List[Predicate]] = None) -> None:
+        h = self._handler(fn, list(predicates or []))
+        self._sources.append((informer, h))
+        informer.add_handler(h)
+
+    # ------------------------------------------------------------------ workers
+    def _logger_for(self, req: Request) -> Logger:
+        base = self._log_ctor(req) if self._log_ctor else self.log.with_values(
+            **{"namespace": req.namespace, "name": req.name})
+        if base.sink.level > 0:  # info disabled: skip the per-request ID
+            return base
+        return base.with_values(reconcileID=str(uuid.uuid4()))
+
+    def _count(self, label: str) -> None:
+        self.result_counts[label] = self.result_counts.get(label, 0) + 1
+        metrics.RECONCILE_TOTAL.labels(self.name, label).inc()
+
+    async def process_one(self, req: Request) -> None:
+        q = self.queue
+        log = self._logger_for(req)
+        self.active += 1
+        self._m_active.set(self.active)
+        t0 = time.perf_counter()
+        result: Optional[Result] = None
+        err: Optional[BaseException] = None
+        try:
+            result = await self.reconciler.reconcile(req, log)
+            if result is None:
+                result = Result()
+        except asyncio.CancelledError:
+            raise
+        except Exception as e:  # noqa: BLE001 - recover like RecoverPanic
+            err = e
+            if not self.recover_panic:
+                raise
+        finally:
+            self.active -= 1
+            self._m_active.set(self.active)
+            self._m_time.observe(time.perf_counter() - t0)
+        self.reconciles += 1
+        if err is not None:
+            self.errors += 1
+            if isinstance(err, TerminalError):
+                metrics.TERMINAL_ERRORS.labels(self.name).inc()
+            else:
+                q.add_rate_limited(req, PRIORITY_EVENT)
+            metrics.RECONCILE_ERRORS.labels(self.name).inc()
+            self._count("error")
+            if not isinstance(err, Exception) or type(err).__name__ in ("AttributeError", "TypeError", "KeyError"):
+                metrics.RECONCILE_PANICS.labels(self.name).inc()
+                log.error(err, "Observed a panic", stacktrace="".join(traceback.format_exception(err))[-2000:])
+            else:
+                log.error(err, "Reconciler error")
+        elif result.after_ns() > 0:
+            q.forget(req)
+            q.add_at(req, self.clock.now_ns() + result.after_ns(), PRIORITY_SCHEDULE)
+            self._count("requeue_after")
+        elif result.requeue:
+            q.add_rate_limited(req, PRIORITY_EVENT)
+            self._count("requeue")
+        else:
+            q.forget(req)
+            self._count("success")
+        if self.on_result is not None:
+            self.on_result(req, result, err)
+
+    async def _worker(self) -> None:
+        q = self.queue
+        while True:
+            try:
+                req = await q.get()
+            except ShutDown:
+                return
+            try:
+                await self.process_one(req)
+            finally:
+                q.done(req)
+
+    def start(self) -> None:
+        if self.started:
+            return
+        self.started = True
+        loop = asyncio.get_running_loop()
+        for i in range(self.max_concurrent):
+            self._workers.append(loop.create_task(self._worker(), name=f"{self.name}-worker-{i}"))
+
+    async def stop(self) -> None:
+        self.queue.shutdown()
+        for t in self._workers:
+            t.cancel()
+        for t in self._workers:
+            try:
+                await t
+            except (asyncio.CancelledError, Exception):
+                pass
+        self._workers.clear()
+        self.started = False
+
+    async def wait_idle(self, settle: float = 0.0, timeout: float = 60.0) -> bool:
+        """Wait until the queue has nothing queued or in flight (delayed items excluded)."""
+        deadline = time.monotonic() + timeout
+        while time.monotonic() < deadline:
+            if self.queue.idle():
+                if settle <= 0:
+                    return True
+                await asyncio.sleep(settle)
+                if self.queue.idle():
+                    return True
+            await asyncio.sleep(0.001)
+        return False
+
+
+ReconcileFunc = Callable[[Request, Logger], Awaitable[Result]]

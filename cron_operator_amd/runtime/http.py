@@ -1,0 +1,155 @@
+"""HTTP transport: the Kubernetes REST protocol over aiohttp.
+
+Works against a real kube-apiserver (kubeconfig / in-cluster config) and the
+framework's fake apiserver served by :mod:`cron_operator_amd.apiserver.http`.
+Connections are pooled and kept alive; watch streams are read line by line
+(newline-delimited JSON) with a large line limit so big objects fit.
+"""
+from __future__ import annotations
+
+import asyncio
+import json
+from typing import Any, Dict, List, Optional, Tuple
+from urllib.parse import quote
+
+import aiohttp
+
+from ..api import errors
+from ..api.meta import GroupVersion, GroupVersionResource
+from ..utils import jsonutil
+from .client import PATCH_CONTENT_TYPES, Transport, WatchStream
+from .kubeconfig import RestConfig
+
+
+def resource_path(gvr: GroupVersionResource, namespace: str = "", name: str = "", sub: str = "") -> str:
+    base = f"/api/{gvr.version}" if not gvr.group else f"/apis/{gvr.group}/{gvr.version}"
+    if namespace:
+        base += f"/namespaces/{quote(namespace, safe='')}"
+    base += f"/{gvr.resource}"
+    if name:
+        base += f"/{quote(name, safe='')}"
+    if sub:
+        base += f"/{sub}"
+    return base
+
+
+def _clean(params: Optional[Dict[str, Any]]) -> Dict[str, str]:
+    out = {}
+    for k, v in (params or {}).items():
+        if k == "patchType" or v is None or v == "":
+            continue
+        out[k] = str(v)
+    return out
+
+
+class _HttpWatch(WatchStream):
+    def __init__(self, resp: aiohttp.ClientResponse):
+        self._resp = resp
+        self._done = False
+
+    async def __anext__(self) -> Tuple[str, Dict[str, Any]]:
+        if self._done:
+            raise StopAsyncIteration
+        while True:
+            try:
+                line = await self._resp.content.readline()
+            except (aiohttp.ClientError, asyncio.TimeoutError, ValueError):
+                self.stop()
+                raise StopAsyncIteration
+            if not line:
+                self.stop()
+                raise StopAsyncIteration
+            line = line.strip()
+            if not line:
+                continue
+            ev = json.loads(line)
+            return ev.get("type", ""), ev.get("object") or {}
+
+    def stop(self) -> None:
+        if not self._done:
+            self._done = True
+            self._resp.close()
+
+
+class HttpTransport(Transport):
+    def __init__(self, config: RestConfig, pool_size: int = 64, timeout: float = 60.0):
+        self.config = config
+        self.host = config.host.split("://", 1)[-1]
+        self._pool_size = pool_size
+        self._timeout = timeout
+        self._session: Optional[aiohttp.ClientSession] = None
+
+    def _sess(self) -> aiohttp.ClientSession:
+        if self._session is None or self._session.closed:
+            conn = aiohttp.TCPConnector(limit=self._pool_size, ssl=self.config.ssl_context() or False,
+                                        keepalive_timeout=120)
+            self._session = aiohttp.ClientSession(connector=conn, headers=self.config.auth_headers(),
+                                                  read_bufsize=1 << 20, json_serialize=jsonutil.dumps)
+        return self._session
+
+    async def _raise(self, resp: aiohttp.ClientResponse) -> None:
+        raw = await resp.read()
+        try:
+            body: Any = json.loads(raw)
+        except ValueError:
+            body = raw.decode(errors="replace")
+        raise errors.ApiError.from_status(resp.status, body)
+
+    async def request(self, verb: str, gvr: GroupVersionResource, namespace: str = "", name: str = "",
+                      subresource: str = "", body: Any = None, params: Optional[Dict[str, Any]] = None) -> Any:
+        params = params or {}
+        method = {"get": "GET", "list": "GET", "create": "POST", "update": "PUT", "patch": "PATCH",
+                  "delete": "DELETE", "deletecollection": "DELETE"}[verb]
+        url = self.config.host + resource_path(gvr, namespace, name if verb not in ("list", "create",
+                                                                                    "deletecollection") else "",
+                                                subresource)
+        headers = {"Accept": "application/json"}
+        data = None
+        if body is not None:
+            data = jsonutil.dumpb(body)
+            headers["Content-Type"] = PATCH_CONTENT_TYPES[params.get("patchType", "merge")] if verb == "patch" \
+                else "application/json"
+        timeout = aiohttp.ClientTimeout(total=self._timeout)
+        try:
+            async with self._sess().request(method, url, params=_clean(params), data=data, headers=headers,
+                                            timeout=timeout) as resp:
+                if resp.status >= 400:
+                    await self._raise(resp)
+                raw = await resp.read()
+        except aiohttp.ClientConnectionError as e:
+            raise errors.ApiError(503, "ServiceUnavailable", f"connection error: {e}") from None
+        return json.loads(raw) if raw else None
+
+    async def watch(self, gvr: GroupVersionResource, namespace: str = "",
+                    params: Optional[Dict[str, Any]] = None) -> WatchStream:
+        url = self.config.host + resource_path(gvr, namespace)
+        p = _clean(params)
+        p["watch"] = "true"
+        timeout = aiohttp.ClientTimeout(total=None, sock_connect=self._timeout)
+        try:
+            resp = await self._sess().get(url, params=p, timeout=timeout)
+        except aiohttp.ClientConnectionError as e:
+            raise errors.ApiError(503, "ServiceUnavailable", f"connection error: {e}") from None
+        if resp.status >= 400:
+            try:
+                await self._raise(resp)
+            finally:
+                resp.release()
+        return _HttpWatch(resp)
+
+    async def discover(self, group_version: GroupVersion) -> List[Dict[str, Any]]:
+        path = f"/api/{group_version.version}" if not group_version.group else \
+            f"/apis/{group_version.group}/{group_version.version}"
+        try:
+            async with self._sess().get(self.config.host + path) as resp:
+                if resp.status >= 400:
+                    await self._raise(resp)
+                doc = json.loads(await resp.read())
+        except aiohttp.ClientConnectionError as e:
+            raise errors.ApiError(503, "ServiceUnavailable", f"connection error: {e}") from None
+        return doc.get("resources") or []
+
+    async def close(self) -> None:
+        if self._session is not None:
+            await self._session.close()
+            self._session = None

@@ -1,0 +1,225 @@
+"""Health-probe and metrics HTTP servers.
+
+* Probes: ``/healthz`` and ``/readyz`` (plus ``/healthz/<check>``), answered from
+  registered checks like controller-runtime's ``healthz.Ping``
+  (``cmd/operator/start.go:195-203``; probed on :8081 by the chart,
+  ``charts/cron-operator/templates/deployment.yaml:74-83``).
+* Metrics: ``/metrics`` in Prometheus text format.  ``--metrics-secure`` (default
+  true, ``start.go:226``) serves HTTPS and guards the endpoint with the
+  authn/authz filter: the bearer token is checked with a TokenReview and the
+  caller must be allowed ``get`` on the ``/metrics`` non-resource URL by a
+  SubjectAccessReview (``start.go:127-133``).  Without ``--metrics-cert-path`` a
+  self-signed certificate is generated (openssl), as controller-runtime does.
+  ``--metrics-bind-address=0`` disables the server.
+"""
+from __future__ import annotations
+
+import asyncio
+import os
+import ssl
+import subprocess
+import tempfile
+from typing import Any, Awaitable, Callable, Dict, Optional, Tuple
+
+from aiohttp import web
+
+from ..api import errors
+from ..api.meta import GroupVersionResource
+from ..utils.logging import get_logger
+from . import metrics
+
+Check = Callable[[], Optional[str]]  # returns None when healthy, else a reason
+
+TOKENREVIEWS = GroupVersionResource("authentication.k8s.io", "v1", "tokenreviews")
+SUBJECTACCESSREVIEWS = GroupVersionResource("authorization.k8s.io", "v1", "subjectaccessreviews")
+
+
+def ping() -> Optional[str]:
+    return None
+
+
+def parse_bind_address(addr: str) -> Optional[Tuple[str, int]]:
+    """":8080" -> ("0.0.0.0", 8080); "0" -> None (disabled)."""
+    if addr in ("", "0"):
+        return None
+    host, _, port = addr.rpartition(":")
+    if not port:
+        raise ValueError(f"invalid bind address {addr!r}")
+    return (host or "0.0.0.0", int(port))
+
+
+def _render(checks: Dict[str, Check], kind: str, verbose: bool) -> Tuple[int, str]:
+    lines = []
+    failed = False
+    for name, fn in sorted(checks.items()):
+        try:
+            reason = fn()
+        except Exception as e:  # noqa: BLE001
+            reason = str(e)
+        if reason is None:
+            lines.append(f"[+]{name} ok")
+        else:
+            failed = True
+            lines.append(f"[-]{name} failed: {reason}")
+    if failed:
+        return 500, "\n".join(lines) + f"\n{kind} check failed\n"
+    if verbose:
+        return 200, "\n".join(lines) + f"\n{kind} check passed\n"
+    return 200, "ok"
+
+
+class ProbeServer:
+    def __init__(self, bind: str):
+        self.bind = bind
+        self.healthz: Dict[str, Check] = {}
+        self.readyz: Dict[str, Check] = {}
+        self._runner: Optional[web.AppRunner] = None
+        self.port: Optional[int] = None
+
+    def app(self) -> web.Application:
+        app = web.Application()
+
+        def handler(checks: Dict[str, Check], kind: str):
+            async def h(req: web.Request) -> web.Response:
+                sub = req.match_info.get("check")
+                if sub:
+                    if sub not in checks:
+                        return web.Response(status=404, text=f"no such check {sub}\n")
+                    code, body = _render({sub: checks[sub]}, kind, False)
+                    return web.Response(status=code, text=body)
+                code, body = _render(checks, kind, "verbose" in req.query)
+                return web.Response(status=code, text=body)
+            return h
+
+        app.router.add_get("/healthz", handler(self.healthz, "healthz"))
+        app.router.add_get("/healthz/{check}", handler(self.healthz, "healthz"))
+        app.router.add_get("/readyz", handler(self.readyz, "readyz"))
+        app.router.add_get("/readyz/{check}", handler(self.readyz, "readyz"))
+        return app
+
+    async def start(self) -> None:
+        addr = parse_bind_address(self.bind)
+        if addr is None:
+            return
+        self._runner = web.AppRunner(self.app(), access_log=None)
+        await self._runner.setup()
+        site = web.TCPSite(self._runner, addr[0], addr[1])
+        await site.start()
+        self.port = _bound_port(site)
+
+    async def stop(self) -> None:
+        if self._runner is not None:
+            await self._runner.cleanup()
+            self._runner = None
+
+
+def _bound_port(site: web.TCPSite) -> Optional[int]:
+    server = getattr(site, "_server", None)
+    if server is not None and server.sockets:
+        return server.sockets[0].getsockname()[1]
+    return None
+
+
+def self_signed_cert(directory: str, host: str = "localhost") -> Tuple[str, str]:
+    crt = os.path.join(directory, "tls.crt")
+    key = os.path.join(directory, "tls.key")
+    subprocess.run(["openssl", "req", "-x509", "-newkey", "rsa:2048", "-nodes", "-days", "365",
+                    "-subj", f"/CN={host}", "-keyout", key, "-out", crt],
+                   check=True, capture_output=True)
+    return crt, key
+
+
+class MetricsServer:
+    def __init__(self, bind: str, secure: bool = True, cert_dir: str = "", cert_name: str = "tls.crt",
+                 key_name: str = "tls.key", client=None, enable_http2: bool = False):
+        self.bind = bind
+        self.secure = secure
+        self.cert_dir = cert_dir
+        self.cert_name = cert_name
+        self.key_name = key_name
+        self.client = client  # for TokenReview / SubjectAccessReview
+        self.enable_http2 = enable_http2
+        self._runner: Optional[web.AppRunner] = None
+        self._tmp: Optional[tempfile.TemporaryDirectory] = None
+        self.port: Optional[int] = None
+        self.extra_handlers: Dict[str, Callable[[web.Request], Awaitable[web.Response]]] = {}
+        self.log = get_logger("controller-runtime.metrics")
+
+    async def _authorize(self, req: web.Request) -> Optional[web.Response]:
+        if not self.secure or self.client is None:
+            return None
+        auth = req.headers.get("Authorization", "")
+        if not auth.startswith("Bearer "):
+            return web.Response(status=401, text="Unauthorized\n")
+        token = auth[len("Bearer "):].strip()
+        try:
+            tr = await self.client.create(TOKENREVIEWS, {"apiVersion": "authentication.k8s.io/v1",
+                                                         "kind": "TokenReview", "spec": {"token": token}}, "")
+        except errors.ApiError as e:
+            return web.Response(status=500, text=f"authentication failed: {e}\n")
+        st = tr.get("status") or {}
+        if not st.get("authenticated"):
+            return web.Response(status=401, text="Unauthorized\n")
+        user = st.get("user") or {}
+        sar = {"apiVersion": "authorization.k8s.io/v1", "kind": "SubjectAccessReview",
+               "spec": {"user": user.get("username", ""), "groups": user.get("groups") or [],
+                        "nonResourceAttributes": {"path": req.path, "verb": "get"}}}
+        try:
+            res = await self.client.create(SUBJECTACCESSREVIEWS, sar, "")
+        except errors.ApiError as e:
+            return web.Response(status=500, text=f"authorization failed: {e}\n")
+        if not (res.get("status") or {}).get("allowed"):
+            return web.Response(status=403, text=f'Authorization denied for user {user.get("username", "")}\n')
+        return None
+
+    def app(self) -> web.Application:
+        app = web.Application()
+
+        async def handle(req: web.Request) -> web.Response:
+            denied = await self._authorize(req)
+            if denied is not None:
+                return denied
+            body = metrics.exposition()
+            return web.Response(body=body, headers={"Content-Type": "text/plain; version=0.0.4; charset=utf-8"})
+
+        app.router.add_get("/metrics", handle)
+        for path, h in self.extra_handlers.items():
+            app.router.add_get(path, h)
+        return app
+
+    def _ssl(self) -> Optional[ssl.SSLContext]:
+        if not self.secure:
+            return None
+        if self.cert_dir:
+            crt = os.path.join(self.cert_dir, self.cert_name)
+            key = os.path.join(self.cert_dir, self.key_name)
+        else:
+            self._tmp = tempfile.TemporaryDirectory(prefix="cron-operator-metrics-")
+            crt, key = self_signed_cert(self._tmp.name)
+        ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+        ctx.load_cert_chain(crt, key)
+        # HTTP/2 is off unless --enable-http2 (start.go:83-98); aiohttp speaks HTTP/1.1 only
+        ctx.set_alpn_protocols(["http/1.1"])
+        return ctx
+
+    async def start(self) -> None:
+        addr = parse_bind_address(self.bind)
+        if addr is None:
+            return
+        if self.enable_http2:
+            self.log.info("HTTP/2 requested but the metrics server only serves HTTP/1.1")
+        self._runner = web.AppRunner(self.app(), access_log=None)
+        await self._runner.setup()
+        site = web.TCPSite(self._runner, addr[0], addr[1], ssl_context=self._ssl())
+        await site.start()
+        self.port = _bound_port(site)
+        self.log.info("Serving metrics server", bindAddress=self.bind, secure=self.secure)
+
+    async def stop(self) -> None:
+        if self._runner is not None:
+            await self._runner.cleanup()
+            self._runner = None
+        if self._tmp is not None:
+            self._tmp.cleanup()
+            self._tmp = None
+

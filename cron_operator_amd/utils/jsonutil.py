@@ -1,0 +1,196 @@
+"""JSON-tree helpers: copy, semantic equality, RFC 7386 merge patch.
+
+Kubernetes objects travel as JSON object trees (``dict``/``list``/``str``/
+``int``/``float``/``bool``/``None``) everywhere in this framework: the fake
+apiserver stores them, the informer caches them, the reconciler reads them.
+These helpers are on the hot path of every request, so the native
+``_fastjson`` extension (``ops/csrc/fastjson.cpp``) provides drop-in versions
+of :func:`deepcopy`, :func:`json_equal` and :func:`create_merge_patch`; the
+pure-Python implementations below are the fallback and the test oracle.
+
+``create_merge_patch(old, new)`` reproduces what controller-runtime's
+``client.MergeFrom(old)`` sends (``CreateMergePatch`` of the two JSON
+documents), which the reference uses for its deferred status write
+(``internal/controller/cron_controller.go:107-120``).
+"""
+from __future__ import annotations
+
+import json
+from typing import Any
+
+_SCALARS = (str, int, float, bool, type(None))
+
+
+def py_deepcopy(x: Any) -> Any:
+    t = type(x)
+    if t is dict:
+        return {k: (v if type(v) in _SCALARS else py_deepcopy(v)) for k, v in x.items()}
+    if t is list:
+        return [v if type(v) in _SCALARS else py_deepcopy(v) for v in x]
+    return x
+
+
+def py_json_equal(a: Any, b: Any) -> bool:
+    if a is b:
+        return True
+    ta, tb = type(a), type(b)
+    if ta is dict and tb is dict:
+        if len(a) != len(b):
+            return False
+        for k, v in a.items():
+            if k not in b or not py_json_equal(v, b[k]):
+                return False
+        return True
+    if ta is list and tb is list:
+        if len(a) != len(b):
+            return False
+        return all(py_json_equal(x, y) for x, y in zip(a, b))
+    if ta is bool or tb is bool:
+        return ta is tb and a == b
+    return a == b
+
+
+def py_create_merge_patch(old: Any, new: Any) -> Any:
+    """Minimal RFC 7386 patch turning ``old`` into ``new`` (objects only recurse)."""
+    if type(old) is not dict or type(new) is not dict:
+        return py_deepcopy(new)
+    patch = {}
+    for k, v in new.items():
+        if k not in old:
+            patch[k] = py_deepcopy(v)
+        else:
+            ov = old[k]
+            if type(ov) is dict and type(v) is dict:
+                sub = py_create_merge_patch(ov, v)
+                if sub:
+                    patch[k] = sub
+            elif not py_json_equal(ov, v):
+                patch[k] = py_deepcopy(v)
+    for k in old:
+        if k not in new:
+            patch[k] = None
+    return patch
+
+
+def apply_merge_patch(target: Any, patch: Any) -> Any:
+    """RFC 7386 apply; returns a new tree (inputs untouched)."""
+    if type(patch) is not dict:
+        return deepcopy(patch)
+    out = deepcopy(target) if type(target) is dict else {}
+    for k, v in patch.items():
+        if v is None:
+            out.pop(k, None)
+        elif type(v) is dict:
+            out[k] = apply_merge_patch(out.get(k), v)
+        else:
+            out[k] = deepcopy(v)
+    return out
+
+
+def apply_json_patch(target: Any, ops: list) -> Any:
+    """RFC 6902 JSON patch (add/remove/replace/test/move/copy)."""
+    doc = deepcopy(target)
+
+    def parse_ptr(p: str):
+        if p == "":
+            return []
+        if not p.startswith("/"):
+            raise ValueError(f"invalid JSON pointer {p!r}")
+        return [s.replace("~1", "/").replace("~0", "~") for s in p[1:].split("/")]
+
+    def walk(d, parts):
+        for s in parts:
+            if type(d) is list:
+                d = d[int(s)]
+            else:
+                d = d[s]
+        return d
+
+    for op in ops:
+        kind = op.get("op")
+        path = parse_ptr(op.get("path", ""))
+        if kind == "test":
+            if not py_json_equal(walk(doc, path), op.get("value")):
+                raise ValueError(f"test operation failed at {op.get('path')}")
+            continue
+        if kind in ("move", "copy"):
+            src = parse_ptr(op["from"])
+            val = deepcopy(walk(doc, src))
+            if kind == "move":
+                parent = walk(doc, src[:-1])
+                if type(parent) is list:
+                    parent.pop(int(src[-1]))
+                else:
+                    del parent[src[-1]]
+            kind, op = "add", {"value": val}
+        if not path:
+            if kind in ("add", "replace"):
+                doc = deepcopy(op.get("value"))
+                continue
+            raise ValueError("cannot remove the document root")
+        parent = walk(doc, path[:-1])
+        last = path[-1]
+        if kind == "add":
+            if type(parent) is list:
+                if last == "-":
+                    parent.append(deepcopy(op.get("value")))
+                else:
+                    parent.insert(int(last), deepcopy(op.get("value")))
+            else:
+                parent[last] = deepcopy(op.get("value"))
+        elif kind == "remove":
+            if type(parent) is list:
+                parent.pop(int(last))
+            else:
+                del parent[last]
+        elif kind == "replace":
+            if type(parent) is list:
+                parent[int(last)] = deepcopy(op.get("value"))
+            else:
+                if last not in parent:
+                    raise KeyError(last)
+                parent[last] = deepcopy(op.get("value"))
+        else:
+            raise ValueError(f"unsupported JSON patch op {kind!r}")
+    return doc
+
+
+def dumps(x: Any) -> str:
+    return json.dumps(x, separators=(",", ":"), ensure_ascii=False)
+
+
+def dumpb(x: Any) -> bytes:
+    return json.dumps(x, separators=(",", ":"), ensure_ascii=False).encode()
+
+
+loads = json.loads
+
+# --------------------------------------------------------------------------- native dispatch
+
+deepcopy = py_deepcopy
+json_equal = py_json_equal
+create_merge_patch = py_create_merge_patch
+NATIVE = False
+
+
+def _try_native() -> None:
+    global deepcopy, json_equal, create_merge_patch, NATIVE
+    import os
+
+    if os.environ.get("CRON_OPERATOR_FASTJSON", "auto").lower() == "python":
+        return
+    try:
+        from ..ops import fastjson_native
+
+        mod = fastjson_native.load()
+    except Exception:  # noqa: BLE001 - fall back to Python
+        if os.environ.get("CRON_OPERATOR_FASTJSON", "auto").lower() == "native":
+            raise
+        return
+    deepcopy = mod.deepcopy
+    json_equal = mod.json_equal
+    create_merge_patch = mod.create_merge_patch
+    NATIVE = True
+
+
+_try_native()
