@@ -1,0 +1,142 @@
+#!/usr/bin/env python3
+"""Headline benchmark: reconcile throughput + tick->create latency @ 1000 Cron CRs.
+
+BASELINE.json names the metric "reconciles/sec + p50 schedule->create latency
+@1000 Cron CRs" on the config "1000 Cron CRs at ``* * * * *``, historyLimit=10
+-- reconcile-throughput + GC stress".  This runs exactly that (see
+``cron_operator_amd/bench/harness.py`` for the step definition): every timed
+step is one schedule tick in virtual time in which all 1000 Crons move their
+finished job into history, garbage-collect the overflow, create the tick's
+PyTorchJob and update status -- against a fake Kubernetes apiserver running in
+its own process, over HTTP + watch streams.  Synthetic objects, no cluster.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
+it runs under ``torch.distributed.run`` with one rank per GPU.  The operator is
+pure control plane, so ranks do not use the GPU: each
+rank is one operator shard (its own apiserver process and 1000 Crons, weak
+scaling) and rank 0 reports the whole-job aggregate.  Ranks synchronise with
+gloo barriers; there is no device work to ``torch.cuda.synchronize()``.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+# BASELINE.md row "reference algorithm, measured in this harness" (reconciles/s @1000 Crons,
+# see BASELINE.md).  None until a measured value is recorded there.
+BASELINE_VALUE = None
+
+
+def _dist():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    if ws <= 1:
+        return None, 0, 1
+    import torch.distributed as dist  # only multi-rank runs pay for importing torch
+
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("gloo")
+    return dist, dist.get_rank(), dist.get_world_size()
+
+
+def _barrier(dist) -> None:
+    if dist is not None:
+        dist.barrier()
+
+
+def _sync_device() -> None:
+    """No kernels are launched by the operator; synchronise only if a device was touched."""
+    if "torch" in sys.modules:
+        import torch
+
+        if torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[1])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--crons", type=int, default=1000)
+    ap.add_argument("--history-limit", type=int, default=10)
+    ap.add_argument("--workers", type=int, default=10, help="--max-concurrent-reconciles")
+    ap.add_argument("--qps", type=float, default=-1.0, help="client QPS (-1: unthrottled)")
+    ap.add_argument("--burst", type=int, default=50)
+    ap.add_argument("--transport", choices=["http", "memory"], default="http")
+    ap.add_argument("--mode", choices=["optimized", "reference"], default="optimized")
+    ap.add_argument("--out", default="", help="also write the full result JSON here")
+    a = ap.parse_args()
+
+    dist, rank, world = _dist()
+    from cron_operator_amd.bench.harness import BenchConfig, run_sync
+
+    cfg = BenchConfig(n_crons=a.crons, steps=a.steps, warmup=a.warmup, history_limit=a.history_limit,
+                      mode=a.mode, transport=a.transport, qps=a.qps, burst=a.burst, workers=a.workers,
+                      namespace=f"bench-r{rank}")
+    _barrier(dist)
+    _sync_device()
+    t0 = time.perf_counter()
+    res = run_sync(cfg)
+    _sync_device()
+    _barrier(dist)
+    wall = time.perf_counter() - t0
+
+    mine = {"elapsed_s": res.elapsed_s, "fires": cfg.n_crons * cfg.steps,
+            "reconciles": res.raw_reconciles_per_s * res.elapsed_s, "p50": res.p50_latency_ms,
+            "p99": res.p99_latency_ms, "req_per_fire": res.api_requests_per_fire}
+    if dist is not None:
+        allr = [None] * world
+        dist.all_gather_object(allr, mine)
+    else:
+        allr = [mine]
+    if rank == 0:
+        t_max = max(r["elapsed_s"] for r in allr)  # timed region: max over ranks
+        fires = sum(r["fires"] for r in allr)
+        value = fires / t_max
+        out = {
+            "metric": "reconciles/sec + p50 schedule→create latency @1000 Cron CRs",
+            "value": round(value, 2),
+            "unit": "cron_reconciles/s",
+            "n_gpus": a.gpus,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(t_max * 1000 / a.steps, 2),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_VALUE, 3) if BASELINE_VALUE else None,
+            "dtype": "n/a (control plane; no tensor compute)",
+            "data": "synthetic: 1000 random-free Cron CRs (* * * * *, historyLimit=10) + PyTorchJob children on a "
+                    "fake apiserver process per rank",
+            "config": {"model": "cron-operator Cron reconciler (apps.kubedl.io/v1alpha1)",
+                       "global_batch": fires // a.steps, "seq_len": None,
+                       "parallelism": f"shard{world}", "crons_per_rank": cfg.n_crons,
+                       "history_limit": cfg.history_limit, "schedule": "* * * * *",
+                       "transport": cfg.transport, "mode": cfg.mode, "workers": cfg.workers,
+                       "qps": cfg.qps},
+            "p50_schedule_to_create_ms": round(max(r["p50"] for r in allr), 2),
+            "p99_schedule_to_create_ms": round(max(r["p99"] for r in allr), 2),
+            "raw_reconciles_per_s": round(sum(r["reconciles"] for r in allr) / t_max, 2),
+            "api_requests_per_fire": round(sum(r["req_per_fire"] for r in allr) / len(allr), 3),
+            "cron_engine": res.engine,
+            "wall_s": round(wall, 2),
+        }
+        print(json.dumps(out), flush=True)
+        if a.out:
+            with open(a.out, "w") as fh:
+                json.dump({"summary": out, "rank0": res.to_dict()}, fh, indent=1)
+    if dist is not None:
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -38,8 +38,35 @@ PATCH_TYPES = {
 }
 
 
+class _EncodeCache:
+    """Serialised bytes of stored objects.  A write's response and its watch events
+    carry the same (immutable) stored object, so it is encoded once."""
+
+    def __init__(self, size: int = 8192):
+        self._d: Dict[int, Tuple[Any, bytes]] = {}
+        self._size = size
+
+    def encode(self, obj: Any) -> bytes:
+        hit = self._d.get(id(obj))
+        if hit is not None and hit[0] is obj:
+            return hit[1]
+        b = jsonutil.dumpb(obj)
+        if len(self._d) >= self._size:
+            self._d.clear()
+        self._d[id(obj)] = (obj, b)
+        return b
+
+
+_ENC = _EncodeCache()
+
+
 def _json(data: Any, status: int = 200) -> web.Response:
-    return web.Response(body=jsonutil.dumpb(data), status=status, content_type="application/json")
+    return web.Response(body=_ENC.encode(data) if status < 300 else jsonutil.dumpb(data), status=status,
+                        content_type="application/json")
+
+
+def _event_line(etype: str, obj: Any) -> bytes:
+    return b'{"type":"' + etype.encode() + b'","object":' + _ENC.encode(obj) + b"}"
 
 
 def _err(e: errors.ApiError) -> web.Response:
@@ -186,40 +213,48 @@ class APIServerApp:
             s.faults.check(verb, gvr.resource, sub or None, name or None)
         if verb == "watch":
             return await self._watch(req, gvr, ns)
-        if verb == "list":
-            return _json(s.list(gvr, ns or None, q.get("labelSelector"), q.get("fieldSelector"),
-                                int(q.get("limit") or 0), q.get("continue")))
-        if verb == "get":
-            return _json(s.get(gvr, ns, name) if not sub else s.get(gvr, ns, name))
-        if verb == "create":
+        body: Any = None
+        ptype = "merge"
+        if verb in ("create", "update", "patch", "delete"):
+            if verb == "patch":
+                ptype = PATCH_TYPES.get(req.content_type)
+                if ptype is None or ptype == "apply":
+                    accepted = ", ".join(k for k in PATCH_TYPES if k != "application/apply-patch+yaml")
+                    raise errors.ApiError(415, "UnsupportedMediaType", "the body of the request was in an unknown "
+                                                                       f"format - accepted media types include: "
+                                                                       f"{accepted}")
             body = await self._body(req)
-            if not isinstance(body, dict):
+            if verb in ("create", "update") and not isinstance(body, dict):
                 raise errors.bad_request("request body must be a JSON object")
-            return _json(s.create(gvr, ns, body, dry_run=q.get("dryRun") == "All"), 201)
-        if verb == "update":
-            body = await self._body(req)
-            if not isinstance(body, dict):
-                raise errors.bad_request("request body must be a JSON object")
-            return _json(s.update(gvr, ns, name, body, sub or None))
-        if verb == "patch":
-            ptype = PATCH_TYPES.get(req.content_type)
-            if ptype is None or ptype == "apply":
-                raise errors.ApiError(415, "UnsupportedMediaType", f"the body of the request was in an unknown "
-                                                                   f"format - accepted media types include: "
-                                                                   f"{', '.join(k for k in PATCH_TYPES if k != 'application/apply-patch+yaml')}")
-            body = await self._body(req)
-            return _json(s.patch(gvr, ns, name, body, ptype, sub or None))
-        if verb == "delete":
-            body = await self._body(req) or {}
-            policy = body.get("propagationPolicy") or q.get("propagationPolicy")
-            return _json(s.delete(gvr, ns, name, policy, body.get("preconditions")))
-        n = s.delete_collection(gvr, ns or None, q.get("labelSelector"))
-        return _json({"kind": "Status", "apiVersion": "v1", "status": "Success", "details": {"deleted": n}})
+        # The verb runs synchronously and its result is serialised right here, so the
+        # stored object can be returned without a defensive copy.
+        s.copy_responses = False
+        try:
+            if verb == "list":
+                return _json(s.list(gvr, ns or None, q.get("labelSelector"), q.get("fieldSelector"),
+                                    int(q.get("limit") or 0), q.get("continue"), copy=False))
+            if verb == "get":
+                return _json(s.get(gvr, ns, name))
+            if verb == "create":
+                return _json(s.create(gvr, ns, body, dry_run=q.get("dryRun") == "All"), 201)
+            if verb == "update":
+                return _json(s.update(gvr, ns, name, body, sub or None))
+            if verb == "patch":
+                return _json(s.patch(gvr, ns, name, body, ptype, sub or None))
+            if verb == "delete":
+                opts = body or {}
+                policy = opts.get("propagationPolicy") or q.get("propagationPolicy")
+                return _json(s.delete(gvr, ns, name, policy, opts.get("preconditions")))
+            n = s.delete_collection(gvr, ns or None, q.get("labelSelector"))
+            return _json({"kind": "Status", "apiVersion": "v1", "status": "Success", "details": {"deleted": n}})
+        finally:
+            s.copy_responses = True
 
     async def _watch(self, req: web.Request, gvr: GroupVersionResource, ns: str) -> web.StreamResponse:
         q = req.query
         w = self.server.watch(gvr, ns or None, q.get("resourceVersion", ""), q.get("labelSelector"),
-                              q.get("fieldSelector"), q.get("allowWatchBookmarks") in ("true", "1"))
+                              q.get("fieldSelector"), q.get("allowWatchBookmarks") in ("true", "1"),
+                              copy_events=False)
         resp = web.StreamResponse(status=200, headers={"Content-Type": "application/json",
                                                        "Transfer-Encoding": "chunked"})
         await resp.prepare(req)
@@ -237,14 +272,14 @@ class APIServerApp:
                     break
                 if ev is None:
                     break
-                buf = [jsonutil.dumpb({"type": ev[0], "object": ev[1]})]
+                buf = [_event_line(ev[0], ev[1])]
                 # coalesce whatever is already queued into one write
                 while not w.queue.empty() and len(buf) < 512:
                     nxt = w.queue.get_nowait()
                     if nxt is None:
                         w.closed = True
                         break
-                    buf.append(jsonutil.dumpb({"type": nxt[0], "object": nxt[1]}))
+                    buf.append(_event_line(nxt[0], nxt[1]))
                 await resp.write(b"\n".join(buf) + b"\n")
                 if w.closed:
                     break

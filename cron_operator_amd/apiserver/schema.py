@@ -46,6 +46,94 @@ def _go_type_name(v: Any) -> str:
     return "null"
 
 
+class CompiledSchema:
+    """One-pass prune + default + validity check, compiled from a structural schema.
+
+    The three tree walks below (:func:`prune`, :func:`apply_defaults`,
+    :func:`validate`) build path strings at every node; the fake apiserver runs
+    them on every custom-resource write, so this compiles the schema once into
+    nested closures that do all three in a single walk without paths.  It
+    returns ``True`` when the object is valid; on ``False`` the caller re-runs
+    :func:`validate` to produce the field errors (the rare path).
+    """
+
+    def __init__(self, schema: Dict[str, Any], root: bool = True):
+        self.fn = self._compile(schema, root)
+
+    def __call__(self, obj: Any) -> bool:
+        return self.fn(obj)
+
+    def _compile(self, s: Dict[str, Any], root: bool = False):
+        if not isinstance(s, dict):
+            return lambda v: True
+        t = s.get("type")
+        tcheck = _TYPES.get(t) if t else None
+        enum = tuple(s["enum"]) if "enum" in s else None
+        is_dt = s.get("format") == "date-time"
+        minimum = s.get("minimum")
+        maximum = s.get("maximum")
+        nullable = bool(s.get("nullable"))
+        preserve = bool(s.get("x-kubernetes-preserve-unknown-fields"))
+        props_s = s.get("properties")
+        addl_s = s.get("additionalProperties")
+        props = {k: self._compile(v) for k, v in (props_s or {}).items()}
+        defaults = [(k, v["default"]) for k, v in (props_s or {}).items() if isinstance(v, dict) and "default" in v]
+        required = tuple(s.get("required") or ())
+        addl = self._compile(addl_s) if isinstance(addl_s, dict) else None
+        addl_true = addl_s is True
+        keep_unknown = preserve or (props_s is None and addl_s is None)
+        items_s = s.get("items")
+        items = self._compile(items_s) if isinstance(items_s, dict) else None
+        skip_meta = root
+        deep = jsonutil.deepcopy
+
+        def check(v: Any) -> bool:
+            if v is None:
+                return nullable or root or t is None
+            if tcheck is not None and not tcheck(v):
+                return False
+            ok = True
+            if enum is not None and v not in enum:
+                ok = False
+            if is_dt and isinstance(v, str) and not _DATE_TIME.match(v):
+                ok = False
+            if minimum is not None and isinstance(v, (int, float)) and not isinstance(v, bool) and v < minimum:
+                ok = False
+            if maximum is not None and isinstance(v, (int, float)) and not isinstance(v, bool) and v > maximum:
+                ok = False
+            if type(v) is dict:
+                if not keep_unknown:
+                    for k in [k for k in v if k not in props]:
+                        if skip_meta and k in ("apiVersion", "kind", "metadata"):
+                            continue
+                        if addl is not None:
+                            continue
+                        if addl_true:
+                            continue
+                        del v[k]
+                for k, d in defaults:
+                    if k not in v:
+                        v[k] = deep(d)
+                for k in required:
+                    if k not in v:
+                        ok = False
+                for k, sub in props.items():
+                    if k in v and not (skip_meta and k == "metadata"):
+                        if not sub(v[k]):
+                            ok = False
+                if addl is not None:
+                    for k, val in v.items():
+                        if k not in props and not addl(val):
+                            ok = False
+            elif type(v) is list and items is not None:
+                for it in v:
+                    if not items(it):
+                        ok = False
+            return ok
+
+        return check
+
+
 def prune(obj: Any, schema: Dict[str, Any], root: bool = True) -> Any:
     """Drop fields not declared in ``schema`` (in place; returns obj)."""
     if not isinstance(schema, dict):

@@ -119,7 +119,8 @@ class Watcher:
     """One WATCH stream.  Events are ``(type, object)``; ``None`` ends the stream."""
 
     def __init__(self, server: "APIServer", info: ResourceInfo, namespace: Optional[str],
-                 pred: Callable[[Dict[str, Any]], bool], bookmarks: bool):
+                 pred: Callable[[Dict[str, Any]], bool], bookmarks: bool, copy_events: bool = True):
+        self.copy_events = copy_events  # False: consumer serialises immediately (HTTP), stored objects are immutable
         self.server = server
         self.info = info
         self.namespace = namespace or None
@@ -152,7 +153,7 @@ class Watcher:
 
     def _put(self, etype: str, obj: Dict[str, Any]) -> None:
         self.sent += 1
-        self.queue.put_nowait((etype, jsonutil.deepcopy(obj)))
+        self.queue.put_nowait((etype, jsonutil.deepcopy(obj) if self.copy_events else obj))
 
     def bookmark(self, rv: int) -> None:
         if self.bookmarks and not self.closed:
@@ -219,6 +220,9 @@ class APIServer:
         self._owners: Dict[str, Set[Tuple[str, str, str, str]]] = defaultdict(set)  # owner uid -> dependents
         self._gc_pending: List[Tuple[str, str]] = []
         self.create_hooks: List[Callable[[ResourceInfo, Dict[str, Any]], None]] = []
+        self._compiled_schemas: Dict[Tuple[str, str, str, int], Tuple[Any, Any]] = {}
+        # verbs return deep copies unless a caller that serialises immediately opts out
+        self.copy_responses = True
         self._rng = random.Random(7)
         for ri in builtin_resources():
             self.register(ri)
@@ -331,13 +335,41 @@ class APIServer:
             for o in m.get("ownerReferences") or []:
                 self._owners[o.get("uid", "")].add(ref)
 
+    def _out(self, obj: Dict[str, Any]) -> Dict[str, Any]:
+        """Response object: a private copy, or the stored (immutable) object itself when the
+        caller serialises it straight away (HTTP front end)."""
+        return jsonutil.deepcopy(obj) if self.copy_responses else obj
+
+    def _compiled(self, ri: ResourceInfo) -> Tuple[sch.CompiledSchema, Optional[sch.CompiledSchema]]:
+        key = (ri.group, ri.version, ri.resource, id(ri.schema))
+        hit = self._compiled_schemas.get(key)
+        if hit is None:
+            st = ((ri.schema or {}).get("properties") or {}).get("status")
+            hit = (sch.CompiledSchema(ri.schema or {}, root=True),
+                   sch.CompiledSchema(st, root=False) if isinstance(st, dict) else None)
+            self._compiled_schemas[key] = hit
+        return hit
+
     def _admit(self, ri: ResourceInfo, obj: Dict[str, Any], name: str) -> None:
         if ri.schema is not None:
-            sch.prune(obj, ri.schema)
-            sch.apply_defaults(obj, ri.schema)
+            if self._compiled(ri)[0](obj):
+                return
             errs = sch.validate(obj, ri.schema)
             if errs:
                 raise errors.invalid(ri.kind, ri.group, name, errs)
+
+    def _admit_status(self, ri: ResourceInfo, obj: Dict[str, Any], name: str) -> None:
+        """Status-subresource writes only change ``status``: admit just that subtree."""
+        st_schema = ((ri.schema or {}).get("properties") or {}).get("status")
+        if st_schema is None:
+            return
+        st = obj["status"]
+        fast = self._compiled(ri)[1]
+        if fast is not None and fast(st):
+            return
+        errs = sch.validate(st, st_schema, "status")
+        if errs:
+            raise errors.invalid(ri.kind, ri.group, name, errs)
 
     def _validate_name(self, ri: ResourceInfo, name: str) -> None:
         if not name:
@@ -360,7 +392,7 @@ class APIServer:
         obj = self._get_raw(ri, namespace, name)
         if obj is None:
             raise errors.not_found(ri.resource, ri.group, name)
-        return jsonutil.deepcopy(obj)
+        return self._out(obj)
 
     def list(self, gvr: GroupVersionResource, namespace: Optional[str] = None, label_selector: Optional[str] = None,
              field_selector: Optional[str] = None, limit: int = 0, continue_: Optional[str] = None,
@@ -395,7 +427,7 @@ class APIServer:
                 if limit and len(items) >= limit:
                     more = f"{ns}/{name}"
                     break
-                items.append(jsonutil.deepcopy(obj) if copy else obj)
+                items.append(jsonutil.deepcopy(obj) if (copy and self.copy_responses) else obj)
             if more:
                 break
         meta: Dict[str, Any] = {"resourceVersion": str(list_rv)}
@@ -459,7 +491,7 @@ class APIServer:
         self._put_raw(ri, namespace, body)
         self._index_owners(ri, body, None)
         self._emit(ri, "ADDED", body, None, rv)
-        return jsonutil.deepcopy(body)
+        return self._out(body)
 
     def _review(self, ri: ResourceInfo, body: Dict[str, Any]) -> Dict[str, Any]:
         body["apiVersion"] = ri.api_version
@@ -481,7 +513,7 @@ class APIServer:
         nm = new["metadata"]
         nm["resourceVersion"] = old["metadata"]["resourceVersion"]
         if jsonutil.json_equal(old, new):
-            return jsonutil.deepcopy(old)
+            return self._out(old)
         # finalizers drained on a terminating object -> delete it now
         if nm.get("deletionTimestamp") and not nm.get("finalizers"):
             return self._remove(ri, ns, name, old)
@@ -492,19 +524,20 @@ class APIServer:
         self._put_raw(ri, ns, new)
         self._index_owners(ri, new, old)
         self._emit(ri, "MODIFIED", new, old, rv)
-        return jsonutil.deepcopy(new)
+        return self._out(new)
 
     def _prepare_update(self, ri: ResourceInfo, old: Dict[str, Any], body: Dict[str, Any],
                         subresource: Optional[str]) -> Dict[str, Any]:
         om = old["metadata"]
         if subresource == "status":
-            new = jsonutil.deepcopy(old)
+            new = dict(old)  # shallow: only "status" is replaced, the rest is shared immutable storage
+            new["metadata"] = dict(old["metadata"])
             if "status" in body:
                 new["status"] = body["status"]
             else:
                 new.pop("status", None)
-            if ri.schema is not None:
-                self._admit(ri, new, om["name"])
+            if ri.schema is not None and new.get("status") is not None:
+                self._admit_status(ri, new, om["name"])
             return new
         if subresource not in (None, ""):
             raise errors.ApiError(404, "NotFound", f"the server could not find the requested resource "
@@ -610,7 +643,7 @@ class APIServer:
             self._orphan_dependents(om.get("uid", ""))
         if finalizers:
             if om.get("deletionTimestamp"):
-                return jsonutil.deepcopy(old)
+                return self._out(old)
             new = jsonutil.deepcopy(old)
             new["metadata"]["deletionTimestamp"] = _ts(self.clock)
             new["metadata"]["deletionGracePeriodSeconds"] = 0
@@ -621,7 +654,7 @@ class APIServer:
             self._emit(ri, "MODIFIED", new, old, rv)
             if "foregroundDeletion" in finalizers:
                 self._schedule_gc(ri, new)
-            return jsonutil.deepcopy(new)
+            return self._out(new)
         return self._remove(ri, ns, name, old)
 
     def _remove(self, ri: ResourceInfo, ns: str, name: str, old: Dict[str, Any]) -> Dict[str, Any]:
@@ -724,11 +757,12 @@ class APIServer:
     # ------------------------------------------------------------------ watch
     def watch(self, gvr: GroupVersionResource, namespace: Optional[str] = None, resource_version: str = "",
               label_selector: Optional[str] = None, field_selector: Optional[str] = None,
-              allow_bookmarks: bool = False, send_initial_events: Optional[bool] = None) -> Watcher:
+              allow_bookmarks: bool = False, send_initial_events: Optional[bool] = None,
+              copy_events: bool = True) -> Watcher:
         ri = self.resource(gvr)
         self.stats.record("watch", ri.resource)
         pred = compile_selectors(label_selector, field_selector)
-        w = Watcher(self, ri, namespace if ri.namespaced else None, pred, allow_bookmarks)
+        w = Watcher(self, ri, namespace if ri.namespaced else None, pred, allow_bookmarks, copy_events)
         key = (ri.group, ri.resource)
         if resource_version in ("", "0") or send_initial_events:
             for ns, objs in self._bucket(ri).items():

@@ -97,6 +97,9 @@ class ReconcilerOptions:
     active_ref_resource_version: bool = True
     expectations: bool = True
     expectation_ttl: float = 300.0           # seconds (wall)
+    fold_created_into_active: bool = True    # add the just-created child to status.active right away
+    skip_expected_events: bool = True        # child add/delete events we caused do not requeue the Cron
+    classification_cache: bool = True
     workload: WorkloadPolicy = field(default_factory=WorkloadPolicy)
     static_owned_kinds: Tuple[GroupVersionKind, ...] = (
         GroupVersionKind("kubeflow.org", "v1", "PyTorchJob"),
@@ -107,7 +110,8 @@ class ReconcilerOptions:
     def reference() -> "ReconcilerOptions":
         return ReconcilerOptions(list_mode="live", finished_time="now", skip_noop_patch=False,
                                  own_write_filter=False, dynamic_watches=False, expectations=False,
-                                 workload=WorkloadPolicy.reference())
+                                 fold_created_into_active=False, skip_expected_events=False,
+                                 classification_cache=False, workload=WorkloadPolicy.reference())
 
 
 class Expectations:
@@ -121,8 +125,18 @@ class Expectations:
         self.ttl = ttl
         self.created: Dict[str, Dict[str, Tuple[float, Dict[str, Any]]]] = {}
         self.deleted: Dict[str, Dict[str, float]] = {}
+        self.pending: Dict[str, Dict[str, float]] = {}  # key -> {name: expiry} for in-flight CREATEs
+
+    def expect_pending(self, key: str, name: str) -> None:
+        self.pending.setdefault(key, {})[name] = time.monotonic() + self.ttl
+
+    def drop_pending(self, key: str, name: str) -> None:
+        d = self.pending.get(key)
+        if d is not None and d.pop(name, None) is not None and not d:
+            del self.pending[key]
 
     def expect_create(self, key: str, obj: Dict[str, Any]) -> None:
+        self.drop_pending(key, (obj.get("metadata") or {}).get("name", ""))
         uid = (obj.get("metadata") or {}).get("uid", "")
         if uid:
             self.created.setdefault(key, {})[uid] = (time.monotonic() + self.ttl, obj)
@@ -141,6 +155,22 @@ class Expectations:
         d = self.deleted.get(key)
         if d is not None and d.pop(uid, None) is not None and not d:
             del self.deleted[key]
+
+    def matches_created(self, key: str, obj: Dict[str, Any]) -> bool:
+        """Is ``obj`` exactly the object our CREATE returned (same uid and resourceVersion)?"""
+        m = obj.get("metadata") or {}
+        p = self.pending.get(key)
+        if p and m.get("name", "") in p:
+            return True  # the watch event overtook our CREATE response
+        d = self.created.get(key)
+        if not d:
+            return False
+        hit = d.get(m.get("uid", ""))
+        return hit is not None and (hit[1].get("metadata") or {}).get("resourceVersion") == m.get("resourceVersion")
+
+    def matches_deleted(self, key: str, obj: Dict[str, Any]) -> bool:
+        d = self.deleted.get(key)
+        return bool(d) and (obj.get("metadata") or {}).get("uid", "") in d
 
     def adjust(self, key: str, children: List[Dict[str, Any]]) -> List[Dict[str, Any]]:
         cr = self.created.get(key)
@@ -177,8 +207,10 @@ class CronReconciler(Reconciler):
         self.child_informers: Dict[GroupVersionKind, Informer] = {}
         self.on_child_informer: Optional[Callable[[GroupVersionKind, Informer], None]] = None
         # key -> resourceVersion of the Cron object produced by our last status write
-        self.own_writes: Dict[str, str] = {}
+        self.own_writes: Dict[str, Tuple[Any, Dict[str, Any]]] = {}  # key -> (generation, status we wrote)
         self.stats = {"creates": 0, "deletes": 0, "patches": 0, "noop_patches_skipped": 0, "lists": 0}
+        # child uid -> (resourceVersion, Classification): objects are immutable per resourceVersion
+        self._class_cache: Dict[str, Tuple[str, Classification]] = {}
         # tick bookkeeping for latency: key -> (tick unix ns, wall perf_counter when it became due)
         self.latency_observer: Optional[Callable[[str, GoTime, Dict[str, Any]], None]] = None
 
@@ -239,18 +271,36 @@ class CronReconciler(Reconciler):
             metrics.STATUS_PATCHES.labels("skipped").inc()
             return
         m = old_obj.get("metadata") or {}
-        out = await self.client.patch(CRON_GVR, m.get("namespace", ""), m.get("name", ""), patch, "merge", "status")
+        key = f"{m.get('namespace', '')}/{m.get('name', '')}"
+        if self.opts.own_write_filter:
+            # recorded before the call: the watch event can overtake the PATCH response
+            self.own_writes[key] = (m.get("generation"), new_status)
+        try:
+            await self.client.patch(CRON_GVR, m.get("namespace", ""), m.get("name", ""), patch, "merge", "status")
+        except Exception:
+            self.own_writes.pop(key, None)
+            raise
         self.stats["patches"] += 1
         metrics.STATUS_PATCHES.labels("ok").inc()
-        if self.opts.own_write_filter:
-            om = out.get("metadata") or {}
-            self.own_writes[f"{om.get('namespace', '')}/{om.get('name', '')}"] = om.get("resourceVersion", "")
 
-    def is_own_write(self, obj: Dict[str, Any]) -> bool:
-        """Predicate helper: was this Cron version produced by our last status write?"""
-        m = obj.get("metadata") or {}
-        key = f"{m.get('namespace', '')}/{m.get('name', '')}"
-        return self.own_writes.get(key) == m.get("resourceVersion")
+    def is_own_write(self, old: Optional[Dict[str, Any]], new: Dict[str, Any]) -> bool:
+        """Predicate helper: is this Cron update exactly our last status write?
+
+        True when the new object's status equals the status we sent and nothing
+        a reconcile reads besides status changed (same generation, so same spec,
+        and no deletion started).  Such an event would only recompute what we
+        just wrote.
+        """
+        m = new.get("metadata") or {}
+        hit = self.own_writes.get(f"{m.get('namespace', '')}/{m.get('name', '')}")
+        if hit is None:
+            return False
+        gen, status = hit
+        if m.get("generation") != gen or m.get("deletionTimestamp"):
+            return False
+        if old is not None and (old.get("metadata") or {}).get("deletionTimestamp") != m.get("deletionTimestamp"):
+            return False
+        return jsonutil.json_equal(new.get("status") or {}, status)
 
     # ------------------------------------------------------------------ the algorithm
     async def _sync(self, cron: Cron, log: Logger) -> Result:
@@ -272,9 +322,22 @@ class CronReconciler(Reconciler):
         # B5 (cron_controller.go:136-152)
         active: List[Tuple[Dict[str, Any], Classification]] = []
         terminated: List[Tuple[Dict[str, Any], Classification]] = []
+        cache = self._class_cache if self.opts.classification_cache else None
         for w in workloads:
             try:
-                c = classify(w, gvk, policy)
+                if cache is not None:
+                    m = w.get("metadata") or {}
+                    uid, rv = m.get("uid", ""), m.get("resourceVersion", "")
+                    hit = cache.get(uid)
+                    if hit is not None and hit[0] == rv:
+                        c = hit[1]
+                    else:
+                        c = classify(w, gvk, policy)
+                        if len(cache) > 500_000:
+                            cache.clear()
+                        cache[uid] = (rv, c)
+                else:
+                    c = classify(w, gvk, policy)
             except kf.ConversionError as e:
                 log.error(e, f"Failed to get {gvk.kind} status")
                 continue
@@ -330,17 +393,22 @@ class CronReconciler(Reconciler):
                 m = w.get("metadata") or {}
                 ref = ObjectRef(m.get("namespace", ""), m.get("name", ""))
                 log.info(f"Deleting active {gvk.kind}", **{gvk.kind: ref})
+                uid = m.get("uid", "")
+                if self.opts.expectations:  # before the call: the watch event may beat the response
+                    self.expect.expect_delete(self._ckey(cron), uid)
                 try:
                     await self.client.delete(gvk, m.get("namespace", ""), m.get("name", ""),
                                              propagation_policy="Background")
                     self.stats["deletes"] += 1
                     metrics.WORKLOADS_DELETED.labels(gvk.kind, "replace").inc()
-                    if self.opts.expectations:
-                        self.expect.expect_delete(self._ckey(cron), m.get("uid", ""))
                 except errors.ApiError as e:
                     if not errors.is_not_found(e):
+                        if self.opts.expectations:
+                            self.expect.observe_delete(self._ckey(cron), uid)
                         log.error(e, f"Failed to delete active {gvk.kind}", **{gvk.kind: ref})
                         raise
+                if self.opts.fold_created_into_active:
+                    cron.status.active = [a for a in cron.status.active if a.uid != uid]
 
         # B18 (cron_controller.go:222-225, 349-387)
         try:
@@ -352,17 +420,28 @@ class CronReconciler(Reconciler):
         wm = workload["metadata"]
         ref = ObjectRef(wm.get("namespace", ""), wm.get("name", ""))
         log.info(f"Creating {gvk.kind}", **{gvk.kind: ref})
+        if self.opts.expectations:
+            self.expect.expect_pending(self._ckey(cron), wm.get("name", ""))
         try:
             created = await self.client.create(gvk, workload, wm.get("namespace", ""))
             self.stats["creates"] += 1
             metrics.WORKLOADS_CREATED.labels(gvk.kind).inc()
             if self.opts.expectations:
                 self.expect.expect_create(self._ckey(cron), created)
+            if self.opts.fold_created_into_active:
+                cm = created.get("metadata") or {}
+                cgvk = GroupVersionKind.from_object(created)
+                cron.status.active.append(ObjectReference(
+                    api_version=cgvk.api_version, kind=cgvk.kind, name=cm.get("name", ""),
+                    namespace=cm.get("namespace", ""), uid=cm.get("uid", ""),
+                    resource_version=cm.get("resourceVersion", "") if self.opts.active_ref_resource_version else ""))
             if self.latency_observer is not None:
                 self.latency_observer(self._ckey(cron), missed_run, created)
             metrics.SCHEDULE_LATENCY.labels("cron").observe(
                 max(0.0, (self.clock.now_ns() - missed_run.unix_nano()) / 1e9))
         except errors.ApiError as e:
+            if self.opts.expectations:
+                self.expect.drop_pending(self._ckey(cron), wm.get("name", ""))
             if errors.is_already_exists(e):
                 log.info(f"{gvk.kind} already exists", **{gvk.kind: ref})
             else:
@@ -455,15 +534,18 @@ class CronReconciler(Reconciler):
             ref = ObjectRef(m.get("namespace", ""), m.get("name", ""))
             if i < n - limit:
                 log.info(f"Deleting terminated {wgvk.kind}", **{wgvk.kind: ref})
+                uid = m.get("uid", "")
+                if self.opts.expectations:  # before the call: the watch event may beat the response
+                    self.expect.expect_delete(self._ckey(cron), uid)
                 try:
                     await self.client.delete(wgvk, m.get("namespace", ""), m.get("name", ""),
                                              propagation_policy="Background")
                     self.stats["deletes"] += 1
                     metrics.WORKLOADS_DELETED.labels(wgvk.kind, "history").inc()
-                    if self.opts.expectations:
-                        self.expect.expect_delete(self._ckey(cron), m.get("uid", ""))
                 except errors.ApiError as e:
                     if not errors.is_not_found(e):
+                        if self.opts.expectations:
+                            self.expect.observe_delete(self._ckey(cron), uid)
                         log.error(e, f"Failed to delete terminated {wgvk.kind}", **{wgvk.kind: ref})
                 continue
             entry = CronHistory(uid=m.get("uid", ""),

@@ -45,7 +45,7 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
     preds = []
     if opts.own_write_filter:
         def not_own_write(event: str, old, new) -> bool:
-            return not (event == "update" and rec.is_own_write(new))
+            return not (event == "update" and rec.is_own_write(old, new))
         preds.append(not_own_write)
     ctrl.watch_for(cron_inf, CRON_GVK, preds)
 
@@ -55,12 +55,23 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
         if gvk in watched:
             return
         watched[gvk] = inf
-        ctrl.watch_owned(inf, CRON_GVK)
-        if opts.expectations:
-            def key_of(obj) -> str:
-                m = obj.get("metadata") or {}
-                return f"{m.get('namespace', '')}/{(m.get('labels') or {}).get(LABEL_CRON_NAME, '')}"
 
+        def key_of(obj) -> str:
+            m = obj.get("metadata") or {}
+            return f"{m.get('namespace', '')}/{(m.get('labels') or {}).get(LABEL_CRON_NAME, '')}"
+
+        owned_preds = []
+        if opts.expectations and opts.skip_expected_events:
+            # events that only confirm what the reconciler already folded into status
+            def not_expected(event: str, old, new) -> bool:
+                if event == "create":
+                    return not rec.expect.matches_created(key_of(new), new)
+                if event == "delete":
+                    return not rec.expect.matches_deleted(key_of(new), new)
+                return True
+            owned_preds.append(not_expected)
+        ctrl.watch_owned(inf, CRON_GVK, owned_preds)
+        if opts.expectations:
             inf.add_handler(EventHandler(
                 on_add=lambda o: rec.expect.observe_add(key_of(o), (o.get("metadata") or {}).get("uid", "")),
                 on_update=lambda old, o: rec.expect.observe_add(key_of(o), (o.get("metadata") or {}).get("uid", "")),

@@ -214,6 +214,9 @@ class Client:
         self.host = getattr(transport, "host", "in-memory")
         self.requests = 0
         self.requests_by_verb: Dict[str, int] = {}
+        self._m_req: Dict[Tuple[str, str], Any] = {}
+        self._m_lat: Dict[str, Any] = {}
+        self._m_rl: Dict[str, Any] = {}
 
     # -- plumbing
     async def _gvr(self, target: GVRorGVK) -> GroupVersionResource:
@@ -224,7 +227,10 @@ class Client:
     async def _throttle(self, verb: str) -> None:
         if self.limiter is not None:
             d = await self.limiter.wait()
-            metrics.REST_RATE_LIMIT.labels(verb, self.host).observe(d)
+            m = self._m_rl.get(verb)
+            if m is None:
+                m = self._m_rl[verb] = metrics.REST_RATE_LIMIT.labels(verb, self.host)
+            m.observe(d)
 
     _METHOD = {"get": "GET", "list": "GET", "watch": "GET", "create": "POST", "update": "PUT", "patch": "PATCH",
                "delete": "DELETE", "deletecollection": "DELETE"}
@@ -245,8 +251,16 @@ class Client:
             code = "<error>"
             raise
         finally:
-            metrics.REST_REQUESTS.labels(code, self.host, self._METHOD.get(verb, verb.upper())).inc()
-            metrics.REST_LATENCY.labels(verb.upper(), self.host).observe(time.perf_counter() - t0)
+            key = (code, verb)
+            m = self._m_req.get(key)
+            if m is None:
+                m = self._m_req[key] = metrics.REST_REQUESTS.labels(code, self.host,
+                                                                    self._METHOD.get(verb, verb.upper()))
+            m.inc()
+            lm = self._m_lat.get(verb)
+            if lm is None:
+                lm = self._m_lat[verb] = metrics.REST_LATENCY.labels(verb.upper(), self.host)
+            lm.observe(time.perf_counter() - t0)
 
     # -- verbs
     async def get(self, target: GVRorGVK, namespace: str, name: str) -> Dict[str, Any]:

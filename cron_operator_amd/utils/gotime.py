@@ -383,8 +383,29 @@ def parse_rfc3339(s: str, loc: Location = LOCAL) -> GoTime:
 
     ``metav1.Time.UnmarshalJSON`` calls ``.Local()`` on the parsed value.
     Fractional seconds are accepted (Go accepts them on parse even though the
-    layout has none).
+    layout has none).  Results are cached: the same timestamps are parsed over
+    and over (every reconcile re-reads a Cron's history and its children's
+    conditions), and GoTime values are immutable.
     """
+    return _parse_cached(s, loc)
+
+
+@lru_cache(maxsize=1 << 16)
+def _parse_cached(s: str, loc: Location) -> GoTime:
+    # fast path: "YYYY-MM-DDTHH:MM:SSZ" (what metav1.Time always writes)
+    if len(s) == 20 and s[19] == "Z" and s[10] == "T" and s[4] == "-" and s[13] == ":":
+        try:
+            y, mo, d = int(s[0:4]), int(s[5:7]), int(s[8:10])
+            hh, mi, ss = int(s[11:13]), int(s[14:16]), int(s[17:19])
+        except ValueError:
+            y = -1
+        if y >= 0 and 1 <= mo <= 12 and 1 <= d <= 31 and hh < 24 and mi < 60 and ss < 60 and \
+                s[7] == "-" and s[16] == ":":
+            return GoTime(days_from_civil(y, mo, d) * 86400 + hh * 3600 + mi * 60 + ss, 0, loc)
+    return _parse_slow(s, loc)
+
+
+def _parse_slow(s: str, loc: Location) -> GoTime:
     mt = _RFC3339_RE.match(s)
     if not mt:
         raise ValueError(f'parsing time "{s}" as RFC3339: cannot parse')
