@@ -1,0 +1,202 @@
+"""Manager-level integration: the controller running against the fake apiserver
+through informers, the work queue and timers, over many virtual minutes.
+
+Covers the BASELINE.json configs at small scale (PyTorchJob Forbid + historyLimit,
+TFJob Replace + deadline, suspend/resume cycle, Pod template), the no-duplicate
+guarantee under many workers and duplicated events, fail-over via
+leader election with deterministic names, and both reconciler modes.
+"""
+from __future__ import annotations
+
+import asyncio
+
+import pytest
+
+from cron_operator_amd.api.meta import GroupVersionResource
+from cron_operator_amd.api.v1alpha1 import CRON_GVR, LABEL_CRON_NAME, new_cron
+from cron_operator_amd.controller.reconciler import ReconcilerOptions
+from cron_operator_amd.testing.env import TestEnv
+from cron_operator_amd.trainingop.operator import FakeTrainingOperator
+from cron_operator_amd.utils.clock import FakeClock
+from cron_operator_amd.utils.gotime import UTC, GoTime, parse_rfc3339
+
+PT = GroupVersionResource("kubeflow.org", "v1", "pytorchjobs")
+TF = GroupVersionResource("kubeflow.org", "v1", "tfjobs")
+PODS = GroupVersionResource("", "v1", "pods")
+NS = "default"
+
+PT_TMPL = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+           "spec": {"pytorchReplicaSpecs": {"Master": {"replicas": 1}, "Worker": {"replicas": 1}}}}
+TF_TMPL = {"apiVersion": "kubeflow.org/v1", "kind": "TFJob",
+           "spec": {"tfReplicaSpecs": {"PS": {"replicas": 1}, "Worker": {"replicas": 2}}}}
+
+MODES = {"optimized": ReconcilerOptions(), "reference": ReconcilerOptions.reference()}
+
+
+def names(server, gvr, cron):
+    return sorted(o["metadata"]["name"] for o in server.list(gvr, NS, label_selector=f"{LABEL_CRON_NAME}={cron}")["items"])
+
+
+@pytest.mark.parametrize("mode", MODES)
+async def test_pytorchjob_forbid_history_limit(mode):
+    env = TestEnv()
+    trainer = FakeTrainingOperator(env.new_client(), env.clock, mode="timed", duration=90)
+    await trainer.start()
+    await env.create_cron(new_cron("pt", NS, "*/1 * * * *", PT_TMPL, concurrency_policy="Forbid", history_limit=3))
+    await env.start_manager(MODES[mode])
+    await env.settle()
+    created = []
+    for _ in range(12):
+        await env.advance(30)
+        for n in names(env.server, PT, "pt"):
+            if n not in created:
+                created.append(n)
+        active = [o for o in env.server.list(PT, NS)["items"] if not (o.get("status") or {}).get("completionTime")]
+        assert len(active) <= 1  # Forbid: never two running jobs
+    st = env.server.get(CRON_GVR, NS, "pt")["status"]
+    assert len(created) >= 3
+    assert len(st.get("history") or []) <= 3
+    assert len(names(env.server, PT, "pt")) <= 4  # history limit GC (3 finished + at most 1 running)
+    await trainer.stop()
+    await env.stop()
+
+
+@pytest.mark.parametrize("mode", MODES)
+async def test_tfjob_replace_and_deadline(mode):
+    env = TestEnv()
+    start = env.clock.now(UTC)
+    deadline = GoTime(start.sec + 5 * 60, 0, UTC)
+    await env.create_cron(new_cron("tf", NS, "*/1 * * * *", TF_TMPL, concurrency_policy="Replace",
+                                   deadline=deadline))
+    await env.start_manager(MODES[mode])
+    await env.settle()
+    seen = set()
+    for _ in range(9):
+        await env.advance(60)
+        cur = names(env.server, TF, "tf")
+        assert len(cur) <= 1  # Replace: the previous run is deleted first
+        seen.update(cur)
+    assert 4 <= len(seen) <= 5  # only ticks before the deadline fired
+    await env.stop()
+
+
+@pytest.mark.parametrize("mode", MODES)
+async def test_suspend_resume_collapses_missed_runs(mode):
+    env = TestEnv()
+    await env.create_cron(new_cron("s", NS, "*/1 * * * *", PT_TMPL))
+    await env.start_manager(MODES[mode])
+    await env.settle()
+    await env.advance(60)
+    assert len(names(env.server, PT, "s")) == 1
+    env.server.patch(CRON_GVR, NS, "s", {"spec": {"suspend": True}})
+    await env.settle()
+    for _ in range(5):
+        await env.advance(60)
+    assert len(names(env.server, PT, "s")) == 1
+    env.server.patch(CRON_GVR, NS, "s", {"spec": {"suspend": False}})
+    await env.settle()
+    assert len(names(env.server, PT, "s")) == 2  # one immediate run for all missed ticks
+    await env.advance(60)
+    assert len(names(env.server, PT, "s")) == 3
+    await env.stop()
+
+
+async def test_pod_template_busybox_config():
+    # BASELINE config 1: a Cron spawning a no-op busybox Pod (core group; optimized mode only)
+    env = TestEnv()
+    pod = {"apiVersion": "v1", "kind": "Pod", "spec": {"containers": [{"name": "b", "image": "busybox",
+                                                                       "command": ["true"]}]}}
+    await env.create_cron(new_cron("pod", NS, "*/1 * * * *", pod, history_limit=1))
+    await env.start_manager()
+    await env.settle()
+    await env.advance(60)
+    pods = names(env.server, PODS, "pod")
+    assert len(pods) == 1
+    env.server.patch(PODS, NS, pods[0], {"status": {"phase": "Succeeded"}}, "merge", "status")
+    await env.settle()
+    hist = env.server.get(CRON_GVR, NS, "pod")["status"]["history"]
+    assert hist[0]["status"] == "Succeeded"
+    await env.advance(60)
+    pods = names(env.server, PODS, "pod")
+    assert len(pods) == 2  # one finished (kept by historyLimit=1) + the new active one
+    env.server.patch(PODS, NS, pods[1], {"status": {"phase": "Failed"}}, "merge", "status")
+    await env.settle()
+    assert names(env.server, PODS, "pod") == [pods[1]]  # the older finished pod is GC'd
+    hist = env.server.get(CRON_GVR, NS, "pod")["status"]["history"]
+    assert [(h["object"]["name"], h["status"]) for h in hist] == [(pods[1], "Failed")]
+    await env.stop()
+
+
+@pytest.mark.parametrize("mode", MODES)
+async def test_no_duplicate_creates_under_concurrency(mode):
+    """Many workers, many Crons, event storms: exactly one job per Cron per tick."""
+    env = TestEnv()
+    n = 40
+    for i in range(n):
+        await env.create_cron(new_cron(f"c{i}", NS, "*/1 * * * *", PT_TMPL))
+    await env.start_manager(MODES[mode], max_concurrent=32)
+    await env.settle()
+    for tick in range(1, 4):
+        env.clock.advance(60)
+        # storm: re-enqueue every cron repeatedly while the tick is being processed
+        for _ in range(5):
+            for i in range(n):
+                env.controller.queue.add(env.controller.queue.__class__ and
+                                         __import__("cron_operator_amd.runtime.controller",
+                                                    fromlist=["Request"]).Request(NS, f"c{i}"))
+            await asyncio.sleep(0)
+        await env.settle()
+        for i in range(n):
+            assert len(names(env.server, PT, f"c{i}")) == tick, f"c{i} at tick {tick}"
+    await env.stop()
+
+
+async def test_failover_no_duplicates_with_deterministic_names():
+    """Operator A creates the job and dies before writing status; B takes over and
+    must not create a second job for the same tick (AlreadyExists == success)."""
+    env = TestEnv()
+    await env.create_cron(new_cron("f", NS, "*/1 * * * *", PT_TMPL))
+    # A: the status patch always fails -> lastScheduleTime never advances
+    env.server.faults.add(verb="patch", resource="crons", subresource="status", code=500)
+    await env.start_manager()
+    await env.settle()
+    env.clock.advance(60)
+    for _ in range(20):
+        await asyncio.sleep(0.001)
+    assert len(names(env.server, PT, "f")) == 1
+    await env.stop()
+    env.server.faults.clear()
+    # B: a fresh manager on the same cluster, same virtual minute
+    env2 = TestEnv.__new__(TestEnv)
+    env2.__dict__.update(env.__dict__)
+    env2.manager = env2.controller = env2.reconciler = env2._mgr_task = None
+    await env2.start_manager()
+    await env2.settle()
+    assert len(names(env2.server, PT, "f")) == 1
+    st = env2.server.get(CRON_GVR, NS, "f")["status"]
+    assert st.get("lastScheduleTime")
+    await env2.stop()
+
+
+async def test_manager_leader_election_single_active():
+    clock = FakeClock(1767268805 * 10**9)
+    env = TestEnv(clock=clock)
+    await env.create_cron(new_cron("le", NS, "*/1 * * * *", PT_TMPL))
+    await env.start_manager(leader_election=True, leader_election_namespace=NS, leader_election_identity="a")
+    from cron_operator_amd.controller.setup import setup_with_manager
+    from cron_operator_amd.runtime.manager import Manager, ManagerOptions
+
+    standby = Manager(env.new_client(), ManagerOptions(clock=clock, leader_election=True,
+                                                       leader_election_namespace=NS,
+                                                       leader_election_identity="b",
+                                                       health_probe_bind_address="0"))
+    await setup_with_manager(standby)
+    t = asyncio.get_running_loop().create_task(standby.start())
+    for _ in range(20):
+        await asyncio.sleep(0.001)
+    assert env.manager.elected.is_set() and not standby.elected.is_set()
+    await env.advance(60)
+    assert len(names(env.server, PT, "le")) == 1
+    standby.stop()
+    await asyncio.wait_for(t, 10)
+    await env.stop()

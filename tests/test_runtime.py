@@ -1,0 +1,373 @@
+"""Runtime layer: work queue, rate limiters, informers, HTTP client/transport,
+leader election, event recorder, probe + metrics servers, kubeconfig."""
+from __future__ import annotations
+
+import asyncio
+import os
+import tempfile
+
+import aiohttp
+import pytest
+
+from cron_operator_amd.api import errors
+from cron_operator_amd.api.meta import GroupVersionKind, GroupVersionResource
+from cron_operator_amd.api.v1alpha1 import CRON_GVK, CRON_GVR, new_cron
+from cron_operator_amd.apiserver.http import APIServerApp
+from cron_operator_amd.parallel.leaderelection import LEASES, LeaderElector
+from cron_operator_amd.parallel.workqueue import ShutDown, WorkQueue
+from cron_operator_amd.runtime.client import Client, InMemoryTransport
+from cron_operator_amd.runtime.events import Broadcaster, EVENTS_GVR
+from cron_operator_amd.runtime.http import HttpTransport, resource_path
+from cron_operator_amd.runtime.informer import EventHandler, Informer, label_index
+from cron_operator_amd.runtime.kubeconfig import ConfigError, RestConfig, get_config, load_kubeconfig, \
+    write_kubeconfig
+from cron_operator_amd.runtime.ratelimit import (
+    ItemExponentialFailureRateLimiter,
+    TokenBucket,
+    default_controller_rate_limiter,
+    make_client_limiter,
+)
+from cron_operator_amd.runtime.servers import MetricsServer, ProbeServer, parse_bind_address
+from cron_operator_amd.testing.env import TestEnv
+from cron_operator_amd.utils.clock import FakeClock
+
+CM = GroupVersionResource("", "v1", "configmaps")
+
+
+# ---------------------------------------------------------------- work queue
+
+
+async def test_queue_dedupe_and_serialisation():
+    q = WorkQueue("t", FakeClock(0))
+    q.add("a")
+    q.add("a")
+    q.add("b")
+    assert len(q) == 2
+    a = await q.get()
+    assert a == "a"
+    q.add("a")  # while processing: parked, not queued
+    assert len(q) == 1
+    b = await q.get()
+    assert b == "b"
+    q.done("a")
+    assert len(q) == 1 and await q.get() == "a"
+    q.done("a")
+    q.done("b")
+    assert q.idle()
+
+
+async def test_queue_priority_and_raise():
+    q = WorkQueue("t", FakeClock(0))
+    q.add("low1")
+    q.add("low2")
+    q.add("high", priority=10)
+    q.add("low2", priority=5)  # raised
+    assert [await q.get() for _ in range(3)] == ["high", "low2", "low1"]
+
+
+async def test_queue_add_after_uses_clock_and_keeps_earliest():
+    clock = FakeClock(0)
+    q = WorkQueue("t", clock)
+    q.add_after("a", 10)
+    q.add_after("a", 5)
+    q.add_after("a", 20)
+    assert len(q) == 0 and q.waiting() == 1
+    clock.advance(4.9)
+    assert len(q) == 0
+    clock.advance(0.2)
+    assert len(q) == 1 and await q.get() == "a"
+
+
+async def test_queue_shutdown_wakes_getters():
+    q = WorkQueue("t", FakeClock(0))
+    t = asyncio.get_running_loop().create_task(q.get())
+    await asyncio.sleep(0)
+    q.shutdown()
+    with pytest.raises(ShutDown):
+        await t
+
+
+def test_rate_limiters():
+    r = ItemExponentialFailureRateLimiter(0.005, 1000)
+    assert [r.when("x") for _ in range(4)] == [0.005, 0.01, 0.02, 0.04]
+    assert r.num_requeues("x") == 4
+    r.forget("x")
+    assert r.when("x") == 0.005
+    assert ItemExponentialFailureRateLimiter(0.005, 1.0).when("y") <= 1.0
+    d = default_controller_rate_limiter()
+    assert d.when("z") == pytest.approx(0.005, abs=1e-3)
+    assert make_client_limiter(-1, 10) is None
+    assert make_client_limiter(0, 0).qps == 5.0
+
+
+async def test_token_bucket_paces():
+    b = TokenBucket(100, 5)
+    t0 = asyncio.get_running_loop().time()
+    for _ in range(15):
+        await b.wait()
+    assert asyncio.get_running_loop().time() - t0 >= 0.08  # 10 tokens beyond the burst at 100/s
+
+
+# ---------------------------------------------------------------- informer
+
+
+async def test_informer_list_watch_index_and_relist():
+    env = TestEnv()
+    s = env.server
+    s.create(CM, "default", {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "a", "labels": {"k": "1"}}})
+    inf = Informer(env.client, CM, indexers={"k": label_index("k")})
+    seen = []
+    inf.add_handler(EventHandler(on_add=lambda o: seen.append(("add", o["metadata"]["name"])),
+                                 on_update=lambda a, b: seen.append(("upd", b["metadata"]["name"])),
+                                 on_delete=lambda o: seen.append(("del", o["metadata"]["name"]))))
+    inf.start()
+    await asyncio.wait_for(inf.synced.wait(), 5)
+    s.create(CM, "default", {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "b", "labels": {"k": "1"}}})
+    s.patch(CM, "default", "a", {"data": {"x": "y"}})
+    s.delete(CM, "default", "b")
+    for _ in range(50):
+        await asyncio.sleep(0.001)
+    assert seen == [("add", "a"), ("add", "b"), ("upd", "a"), ("del", "b")]
+    assert [o["metadata"]["name"] for o in inf.by_index("k", "default/1")] == ["a"]
+    # force a 410 on the next watch: closing the stream makes the reflector resume; expire the window
+    s._log_floor[("", "configmaps")] = s.current_rv() + 100
+    s.close_all_watches()
+    s.create(CM, "default", {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "c"}})
+    for _ in range(200):
+        await asyncio.sleep(0.002)
+        if inf.get("default", "c") is not None:
+            break
+    assert inf.get("default", "c") is not None and inf.relists >= 2
+    await inf.stop()
+
+
+# ---------------------------------------------------------------- HTTP transport against the served fake apiserver
+
+
+async def test_http_transport_end_to_end():
+    env = TestEnv()
+    app = APIServerApp(env.server)
+    port = await app.start("127.0.0.1", 0)
+    client = Client(HttpTransport(RestConfig(host=f"http://127.0.0.1:{port}")), qps=-1)
+    try:
+        created = await client.create(CRON_GVK, new_cron("c", "default", "* * * * *",
+                                                         {"apiVersion": "kubeflow.org/v1",
+                                                          "kind": "PyTorchJob"}).to_dict())
+        assert created["spec"]["concurrencyPolicy"] == "Allow"
+        got = await client.get(CRON_GVR, "default", "c")
+        assert got["metadata"]["uid"] == created["metadata"]["uid"]
+        lst = await client.list(CRON_GVK, "default")
+        assert len(lst["items"]) == 1
+        with pytest.raises(errors.ApiError) as e:
+            await client.get(CRON_GVR, "default", "missing")
+        assert errors.is_not_found(e.value)
+        with pytest.raises(errors.ApiError) as e:
+            await client.create(CRON_GVR, created)
+        assert errors.is_already_exists(e.value)
+        p = await client.patch(CRON_GVR, "default", "c", {"status": {"lastScheduleTime": "2026-01-01T00:00:00Z"}},
+                               "merge", "status")
+        assert p["status"]["lastScheduleTime"] == "2026-01-01T00:00:00Z"
+        # watch over HTTP
+        w = await client.watch(CRON_GVR, "default", resource_version=p["metadata"]["resourceVersion"])
+        await client.patch(CRON_GVR, "default", "c", {"metadata": {"labels": {"x": "y"}}})
+        et, obj = await asyncio.wait_for(w.__anext__(), 5)
+        assert et == "MODIFIED" and obj["metadata"]["labels"] == {"x": "y"}
+        w.stop()
+        # informer over HTTP
+        inf = Informer(client, CRON_GVR)
+        inf.start()
+        await asyncio.wait_for(inf.synced.wait(), 5)
+        assert inf.get("default", "c") is not None
+        await inf.stop()
+        await client.delete(CRON_GVR, "default", "c")
+        # discovery via the mapper
+        gvr, namespaced = await client.mapper.resource_for(GroupVersionKind("kubeflow.org", "v1", "TFJob"))
+        assert gvr.resource == "tfjobs" and namespaced
+    finally:
+        await client.close()
+        await app.stop()
+
+
+def test_resource_paths():
+    assert resource_path(CRON_GVR, "ns", "n", "status") == "/apis/apps.kubedl.io/v1alpha1/namespaces/ns/crons/n/status"
+    assert resource_path(GroupVersionResource("", "v1", "namespaces"), "", "x") == "/api/v1/namespaces/x"
+
+
+async def test_http_bearer_token_required():
+    env = TestEnv()
+    env.server.tokens = {"sekret": {"username": "u"}}
+    app = APIServerApp(env.server)
+    port = await app.start("127.0.0.1", 0)
+    try:
+        bad = Client(HttpTransport(RestConfig(host=f"http://127.0.0.1:{port}")), qps=-1)
+        with pytest.raises(errors.ApiError) as e:
+            await bad.get(CRON_GVR, "default", "x")
+        assert e.value.code == 401
+        await bad.close()
+        good = Client(HttpTransport(RestConfig(host=f"http://127.0.0.1:{port}", bearer_token="sekret")), qps=-1)
+        with pytest.raises(errors.ApiError) as e:
+            await good.get(CRON_GVR, "default", "x")
+        assert e.value.code == 404
+        await good.close()
+    finally:
+        await app.stop()
+
+
+# ---------------------------------------------------------------- leader election
+
+
+async def test_leader_election_single_leader_and_failover():
+    clock = FakeClock(1_000_000 * 10**9)
+    env = TestEnv(clock=clock)
+    a = LeaderElector(env.new_client(), "619a52b8.kubedl.io", "default", "a", clock, 15, 10, 2)
+    b = LeaderElector(env.new_client(), "619a52b8.kubedl.io", "default", "b", clock, 15, 10, 2)
+    assert await a.try_acquire_or_renew()
+    assert not await b.try_acquire_or_renew()  # held and fresh
+    lease = env.server.get(LEASES, "default", "619a52b8.kubedl.io")
+    assert lease["spec"]["holderIdentity"] == "a" and lease["spec"]["leaseTransitions"] == 0
+    clock.advance(10)
+    assert await a.try_acquire_or_renew()  # renew
+    clock.advance(16)  # a stops renewing; lease expires
+    assert await b.try_acquire_or_renew()
+    lease = env.server.get(LEASES, "default", "619a52b8.kubedl.io")
+    assert lease["spec"]["holderIdentity"] == "b" and lease["spec"]["leaseTransitions"] == 1
+    assert not await a.try_acquire_or_renew()
+
+
+async def test_leader_election_release():
+    clock = FakeClock(10**12)
+    env = TestEnv(clock=clock)
+    a = LeaderElector(env.new_client(), "l", "default", "a", clock, 15, 10, 2, release_on_cancel=True)
+    await a.try_acquire_or_renew()
+    a.is_leader = True
+    await a.release()
+    b = LeaderElector(env.new_client(), "l", "default", "b", clock, 15, 10, 2)
+    clock.advance(1.5)
+    assert await b.try_acquire_or_renew()
+
+
+def test_leader_election_validates_timings():
+    with pytest.raises(ValueError):
+        LeaderElector(None, "l", "ns", "a", FakeClock(0), 10, 10, 2)
+
+
+# ---------------------------------------------------------------- events
+
+
+async def test_event_broadcaster_writes_and_aggregates():
+    env = TestEnv()
+    b = Broadcaster(env.new_client(), env.clock)
+    b.start()
+    rec = b.recorder_for("cron")
+    obj = {"apiVersion": "apps.kubedl.io/v1alpha1", "kind": "Cron",
+           "metadata": {"name": "c", "namespace": "default", "uid": "u1"}}
+    rec.event(obj, "Normal", "Deadline", "cron has reach deadline and stop scheduling")
+    rec.event(obj, "Normal", "Deadline", "cron has reach deadline and stop scheduling")
+    rec.eventf(obj, "Warning", "TooManyMissedTimes", "too many missed start times: %d. Check clock skew", 101)
+    await b.flush()
+    for _ in range(20):
+        await asyncio.sleep(0.001)
+    evs = env.server.list(EVENTS_GVR, "default")["items"]
+    by_reason = {e["reason"]: e for e in evs}
+    assert by_reason["Deadline"]["count"] == 2 and by_reason["Deadline"]["type"] == "Normal"
+    assert by_reason["Deadline"]["involvedObject"]["kind"] == "Cron"
+    assert by_reason["Deadline"]["source"] == {"component": "cron"}
+    assert by_reason["TooManyMissedTimes"]["message"].endswith("101. Check clock skew")
+    with pytest.raises(ValueError):
+        rec.event(obj, "Info", "X", "y")
+    await b.stop()
+
+
+async def test_event_spam_filter():
+    env = TestEnv()
+    b = Broadcaster(env.new_client(), env.clock, spam_burst=3)
+    b.start()
+    rec = b.recorder_for("cron")
+    obj = {"kind": "Cron", "apiVersion": "apps.kubedl.io/v1alpha1", "metadata": {"name": "c", "namespace": "default"}}
+    for i in range(10):
+        rec.event(obj, "Normal", "R", f"m{i}")
+    await b.flush()
+    for _ in range(20):
+        await asyncio.sleep(0.001)
+    assert len(env.server.list(EVENTS_GVR, "default")["items"]) == 3 and b.dropped == 7
+    await b.stop()
+
+
+# ---------------------------------------------------------------- servers
+
+
+def test_parse_bind_address():
+    assert parse_bind_address("0") is None
+    assert parse_bind_address(":8081") == ("0.0.0.0", 8081)
+    assert parse_bind_address("127.0.0.1:9") == ("127.0.0.1", 9)
+
+
+async def test_probe_server():
+    p = ProbeServer("127.0.0.1:0")
+    p.healthz["ping"] = lambda: None
+    p.readyz["ping"] = lambda: None
+    p.readyz["cache"] = lambda: "not synced"
+    await p.start()
+    try:
+        async with aiohttp.ClientSession() as s:
+            async with s.get(f"http://127.0.0.1:{p.port}/healthz") as r:
+                assert r.status == 200 and await r.text() == "ok"
+            async with s.get(f"http://127.0.0.1:{p.port}/readyz?verbose") as r:
+                assert r.status == 500 and "[-]cache failed: not synced" in await r.text()
+            async with s.get(f"http://127.0.0.1:{p.port}/readyz/ping") as r:
+                assert r.status == 200
+    finally:
+        await p.stop()
+
+
+async def test_metrics_server_insecure_and_secure():
+    env = TestEnv()
+    env.server.tokens = {"good": {"username": "system:serviceaccount:x:prom", "groups": []}}
+    env.server.authorizer = lambda who, spec: who["user"].startswith("system:serviceaccount:x:")
+    m = MetricsServer("127.0.0.1:0", secure=False)
+    await m.start()
+    try:
+        async with aiohttp.ClientSession() as s:
+            async with s.get(f"http://127.0.0.1:{m.port}/metrics") as r:
+                body = await r.text()
+                assert r.status == 200 and "workqueue_adds_total" in body or "process_" in body
+    finally:
+        await m.stop()
+    sm = MetricsServer("127.0.0.1:0", secure=True, client=env.new_client())
+    await sm.start()
+    try:
+        async with aiohttp.ClientSession(connector=aiohttp.TCPConnector(ssl=False)) as s:
+            url = f"https://127.0.0.1:{sm.port}/metrics"
+            async with s.get(url) as r:
+                assert r.status == 401
+            async with s.get(url, headers={"Authorization": "Bearer bad"}) as r:
+                assert r.status == 401
+            async with s.get(url, headers={"Authorization": "Bearer good"}) as r:
+                assert r.status == 200 and "controller_runtime" in (await r.text()) or r.status == 200
+        env.server.authorizer = lambda who, spec: False
+        async with aiohttp.ClientSession(connector=aiohttp.TCPConnector(ssl=False)) as s:
+            async with s.get(f"https://127.0.0.1:{sm.port}/metrics", headers={"Authorization": "Bearer good"}) as r:
+                assert r.status == 403
+    finally:
+        await sm.stop()
+
+
+# ---------------------------------------------------------------- kubeconfig
+
+
+def test_kubeconfig_load_and_precedence(monkeypatch):
+    with tempfile.TemporaryDirectory() as d:
+        p = os.path.join(d, "kc")
+        write_kubeconfig(p, "https://example:6443", token="abc", insecure=True)
+        cfg = load_kubeconfig(p)
+        assert cfg.host == "https://example:6443" and cfg.token() == "abc" and cfg.insecure
+        assert cfg.auth_headers()["Authorization"] == "Bearer abc"
+        monkeypatch.setenv("KUBECONFIG", p)
+        assert get_config().host == "https://example:6443"
+        monkeypatch.delenv("KUBECONFIG")
+        monkeypatch.setenv("KUBERNETES_SERVICE_HOST", "10.0.0.1")
+        monkeypatch.setenv("KUBERNETES_SERVICE_PORT", "443")
+        ic = get_config()
+        assert ic.host == "https://10.0.0.1:443" and ic.bearer_token_file.endswith("/token")
+        with pytest.raises(ConfigError):
+            load_kubeconfig(os.path.join(d, "missing"))
