@@ -1,0 +1,173 @@
+"""Helm chart rendering tests (helm-unittest analog).
+
+The reference tests its chart with helm-unittest
+(``charts/cron-operator/tests/{deployment,service,cluster_role,cluster_role_binding}_test.yaml``):
+image composition, replicas, pull policy, zap flags, leader election on/off,
+concurrency/QPS/burst flags, resources, nodeSelector merge and override,
+affinity, tolerations concatenation, host-timezone mount, the Edge profile,
+service type/port, RBAC rules and the binding.  Helm is not installed here, so
+the templates are rendered with :mod:`cron_operator_amd.utils.gotemplate`.
+"""
+from __future__ import annotations
+
+import os
+
+import pytest
+
+from cron_operator_amd.controller.rbac import RULES
+from cron_operator_amd.utils.gotemplate import Engine, TemplateError, render_chart
+
+CHART = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "charts", "cron-operator")
+
+
+def deployment(values=None, release="cron-operator"):
+    return render_chart(CHART, values, release=release)["deployment.yaml"][0]
+
+
+def container(values=None):
+    d = deployment(values)
+    return [c for c in d["spec"]["template"]["spec"]["containers"] if c["name"] == "cron-operator"][0]
+
+
+def test_image_composition():
+    c = container({"image": {"registry": "test-registry", "repository": "test-repository", "tag": "test-tag"}})
+    assert c["image"] == "test-registry/test-repository:test-tag"
+    assert container()["image"].endswith(":0.3.0")  # defaults to appVersion
+
+
+def test_replicas_and_pull_policy():
+    d = deployment({"replicas": 3, "image": {"pullPolicy": "Always"}})
+    assert d["spec"]["replicas"] == 3
+    assert d["spec"]["template"]["spec"]["containers"][0]["imagePullPolicy"] == "Always"
+
+
+@pytest.mark.parametrize("values,arg", [
+    ({"logEncoder": "json"}, "--zap-encoder=json"),
+    ({"logLevel": "debug"}, "--zap-log-level=debug"),
+    ({"leaderElection": {"enable": True}}, "--leader-elect=true"),
+    ({"leaderElection": {"enable": False}}, "--leader-elect=false"),
+    ({"maxConcurrentReconciles": 20}, "--max-concurrent-reconciles=20"),
+    ({"qps": 100}, "--qps=100"),
+    ({"burst": 200}, "--burst=200"),
+    ({"compatMode": "reference"}, "--compat-mode=reference"),
+    ({"extraArgs": ["--namespace=team-a"]}, "--namespace=team-a"),
+])
+def test_args(values, arg):
+    assert arg in container(values)["args"]
+
+
+def test_args_are_parsed_by_the_cli():
+    from cron_operator_amd.cmd.main import build_parser
+
+    args = container()["args"]
+    a = build_parser().parse_args(args)
+    assert a.command == "start" and a.leader_elect is True and a.metrics_secure is False
+    assert a.metrics_bind_address == ":8080" and a.health_probe_bind_address == ":8081"
+
+
+def test_resources():
+    res = {"requests": {"cpu": "1", "memory": "1Gi"}, "limits": {"cpu": "2", "memory": "2Gi"}}
+    assert container({"resources": res})["resources"] == res
+
+
+def spec(values):
+    return deployment(values)["spec"]["template"]["spec"]
+
+
+def test_node_selector_merge_and_override():
+    assert "nodeSelector" not in spec({})
+    assert spec({"global": {"nodeSelector": {"key1": "value1"}}})["nodeSelector"] == {"key1": "value1"}
+    assert spec({"nodeSelector": {"key2": "value2"}})["nodeSelector"] == {"key2": "value2"}
+    both = spec({"global": {"nodeSelector": {"key1": "value1", "key2": "value2"}},
+                 "nodeSelector": {"key1": "value1-override", "key3": "value3"}})["nodeSelector"]
+    assert both == {"key1": "value1-override", "key2": "value2", "key3": "value3"}
+
+
+def test_affinity():
+    aff = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": [
+        {"matchExpressions": [{"key": "k", "operator": "In", "values": ["v"]}]}]}}}
+    assert spec({"affinity": aff})["affinity"] == aff
+
+
+def test_tolerations_concat():
+    g = [{"key": "key1", "operator": "Equal", "value": "value1", "effect": "NoSchedule"}]
+    t = [{"key": "key2", "operator": "Exists", "effect": "NoExecute"}]
+    assert "tolerations" not in spec({})
+    assert spec({"global": {"tolerations": g}})["tolerations"] == g
+    assert spec({"global": {"tolerations": g}, "tolerations": t})["tolerations"] == g + t
+
+
+def test_host_timezone_mount():
+    s = spec({"useHostTimezone": True})
+    assert s["volumes"] == [{"name": "host-localtime", "hostPath": {"path": "/etc/localtime"}}]
+    assert s["containers"][0]["volumeMounts"][0]["mountPath"] == "/etc/localtime"
+    assert "volumes" not in spec({})
+
+
+def test_edge_profile():
+    s = spec({"global": {"clusterProfile": "Edge"}, "tolerations": [{"key": "x", "operator": "Exists"}]})
+    assert s["nodeSelector"] == {"alibabacloud.com/is-edge-worker": "false"}
+    assert {"key": "node-role.alibabacloud.com/addon", "operator": "Exists", "effect": "NoSchedule"} in \
+        s["tolerations"]
+    assert {"key": "x", "operator": "Exists"} in s["tolerations"]
+
+
+def test_probes_and_security_context():
+    c = container()
+    assert c["livenessProbe"]["httpGet"]["path"] == "/healthz"
+    assert c["readinessProbe"]["httpGet"]["path"] == "/readyz"
+    assert c["securityContext"]["readOnlyRootFilesystem"] is True
+    assert c["securityContext"]["runAsNonRoot"] is True
+
+
+def test_service():
+    out = render_chart(CHART, {"service": {"type": "NodePort"}})["service.yaml"][0]
+    assert out["spec"]["type"] == "NodePort"
+    assert out["spec"]["ports"] == [{"name": "metrics", "port": 8080, "targetPort": "metrics", "protocol": "TCP"}]
+
+
+def test_rbac_rules_match_generator_and_group_is_correct():
+    docs = render_chart(CHART)["rbac.yaml"]
+    role = [d for d in docs if d["kind"] == "ClusterRole"][0]
+    assert role["rules"] == RULES
+    assert any("apps.kubedl.io" in r["apiGroups"] and "crons" in r["resources"] for r in role["rules"])
+    binding = [d for d in docs if d["kind"] == "ClusterRoleBinding"][0]
+    assert binding["roleRef"] == {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole",
+                                  "name": "cron-operator"}
+    assert binding["subjects"] == [{"kind": "ServiceAccount", "name": "cron-operator", "namespace": "cron-operator"}]
+
+
+def test_extra_workload_rules():
+    docs = render_chart(CHART, {"rbac": {"extraWorkloadRules": [{"apiGroups": ["ray.io"],
+                                                                 "resources": ["rayjobs"]}]}})["rbac.yaml"]
+    role = [d for d in docs if d["kind"] == "ClusterRole"][0]
+    assert role["rules"][-1]["apiGroups"] == ["ray.io"]
+
+
+def test_fullname_rules():
+    assert deployment(release="cron-operator")["metadata"]["name"] == "cron-operator"
+    assert deployment(release="prod")["metadata"]["name"] == "prod-cron-operator"
+    assert render_chart(CHART, {"fullnameOverride": "x"})["deployment.yaml"][0]["metadata"]["name"] == "x"
+
+
+# ---------------------------------------------------------------- the template engine itself
+
+
+def _r(src, dot=None):
+    e = Engine()
+    return e.render(e.add_template(src), dot if dot is not None else {})
+
+
+def test_engine_basics():
+    assert _r("{{ .a }}-{{ .b.c }}", {"a": 1, "b": {"c": "x"}}) == "1-x"
+    assert _r("{{- if .a }}yes{{ else }}no{{ end -}}", {"a": ""}) == "no"
+    assert _r("{{ range $i, $v := .l }}{{ $i }}={{ $v }};{{ end }}", {"l": ["a", "b"]}) == "0=a;1=b;"
+    assert _r("{{ range $k, $v := .m }}{{ $k }}{{ $v }}{{ end }}", {"m": {"b": 2, "a": 1}}) == "a1b2"
+    assert _r('{{ printf "%s-%d" "x" 3 | upper }}') == "X-3"
+    assert _r('{{ $x := 1 }}{{ if true }}{{ $x = 2 }}{{ end }}{{ $x }}') == "2"
+    assert _r('{{ define "t" }}[{{ . }}]{{ end }}{{ include "t" "v" }}') == "[v]"
+    assert _r("{{ .missing }}") == "<no value>"
+    assert _r('{{ default "d" .x }}', {"x": ""}) == "d"
+    assert _r("{{ and 1 0 }}{{ or 0 2 }}") == "02"
+    with pytest.raises(TemplateError):
+        _r('{{ required "need x" .x }}')
