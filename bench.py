@@ -31,9 +31,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
-# BASELINE.md row "reference algorithm, measured in this harness" (reconciles/s @1000 Crons,
-# see BASELINE.md).  None until a measured value is recorded there.
-BASELINE_VALUE = None
+# BASELINE.md row "Reference algorithm, measured in this harness" (cron-reconciles/s @1000 Crons,
+# `bench.py --mode reference`, MI355X box, profiles/bench_reference_algorithm_mi355x_box_r1b.json).
+BASELINE_VALUE = 42.41
 
 
 def _dist():

@@ -69,6 +69,9 @@ def _event_line(etype: str, obj: Any) -> bytes:
     return b'{"type":"' + etype.encode() + b'","object":' + _ENC.encode(obj) + b"}"
 
 
+_USER = web.RequestKey("user", dict) if hasattr(web, "RequestKey") else "user"
+
+
 def _err(e: errors.ApiError) -> web.Response:
     return _json(e.status(), e.code)
 
@@ -112,9 +115,21 @@ class APIServerApp:
             return None
         auth = req.headers.get("Authorization", "")
         token = auth[7:].strip() if auth.startswith("Bearer ") else ""
-        if token not in self.server.tokens:
+        user = self.server.tokens.get(token)
+        if user is None:
             return _json(errors.ApiError(401, "Unauthorized", "Unauthorized").status(), 401)
+        req[_USER] = user
         return None
+
+    def _authorize(self, req: web.Request, attrs: Dict[str, Any]) -> None:
+        rbac = self.server.rbac
+        user = req.get(_USER)
+        if rbac is None or user is None:
+            return
+        if not rbac.authorize(user.get("username", ""), user.get("groups") or [], attrs):
+            from .rbac import forbidden_message
+
+            raise errors.ApiError(403, "Forbidden", forbidden_message(user.get("username", ""), attrs))
 
     # ------------------------------------------------------------------ routing
     @staticmethod
@@ -164,6 +179,11 @@ class APIServerApp:
             return _json(self._groups())
         if path.startswith("/debug/fake/"):
             return await self._debug(req)
+        if self.server.rbac is not None and req.get(_USER) is not None and not path.startswith(("/api/", "/apis/")):
+            try:
+                self._authorize(req, {"verb": req.method.lower(), "path": path})
+            except errors.ApiError as e:
+                return _err(e)
         parts = [p for p in path.split("/") if p]
         if len(parts) == 3 and parts[0] == "apis":
             gv = self._group_version(parts[1], parts[2])
@@ -208,6 +228,9 @@ class APIServerApp:
                 "DELETE": "delete" if name else "deletecollection"}.get(m)
         if verb is None:
             raise errors.ApiError(405, "MethodNotAllowed", f"method {m} not allowed")
+        if s.rbac is not None:
+            self._authorize(req, {"verb": verb, "group": gvr.group, "resource": gvr.resource, "subresource": sub,
+                                  "namespace": ns, "name": name})
         await self._delay(verb)
         if s.faults.faults:
             s.faults.check(verb, gvr.resource, sub or None, name or None)

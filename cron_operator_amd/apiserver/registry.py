@@ -2,8 +2,10 @@
 
 Built-in resources cover what the operator and its tests touch: namespaces,
 pods, events, configmaps, leases (leader election), batch Jobs, events.k8s.io
-Events, TokenReview/SubjectAccessReview (metrics authn/authz filter) and
-CustomResourceDefinitions.  Custom resources are added by creating a CRD
+Events, TokenReview/SubjectAccessReview (metrics authn/authz filter),
+CustomResourceDefinitions, the RBAC kinds (enforced with
+``authorization="RBAC"``, see :mod:`.rbac`) and the Deployment /
+NetworkPolicy kinds an install applies.  Custom resources are added by creating a CRD
 object (exactly how envtest installs ``charts/cron-operator/crds`` and
 ``test/crds``, reference ``internal/controller/suite_test.go:73-79``).
 """
@@ -74,6 +76,12 @@ def builtin_resources() -> List[ResourceInfo]:
           virtual=True, verbs=("create",)),
         R("apiextensions.k8s.io", "v1", "customresourcedefinitions", "CustomResourceDefinition", namespaced=False,
           status_subresource=True, short_names=["crd", "crds"]),
+        R("rbac.authorization.k8s.io", "v1", "roles", "Role"),
+        R("rbac.authorization.k8s.io", "v1", "rolebindings", "RoleBinding"),
+        R("rbac.authorization.k8s.io", "v1", "clusterroles", "ClusterRole", namespaced=False),
+        R("rbac.authorization.k8s.io", "v1", "clusterrolebindings", "ClusterRoleBinding", namespaced=False),
+        R("apps", "v1", "deployments", "Deployment", status_subresource=True, short_names=["deploy"]),
+        R("networking.k8s.io", "v1", "networkpolicies", "NetworkPolicy", short_names=["netpol"]),
     ]
 
 

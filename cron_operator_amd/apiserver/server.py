@@ -199,7 +199,8 @@ class RequestStats:
 
 class APIServer:
     def __init__(self, clock: Optional[Clock] = None, gc: bool = False, watch_window: int = 200_000,
-                 auto_create_namespaces: bool = False, tokens: Optional[Dict[str, Dict[str, Any]]] = None):
+                 auto_create_namespaces: bool = False, tokens: Optional[Dict[str, Dict[str, Any]]] = None,
+                 authorization: str = "AlwaysAllow"):
         self.clock = clock or RealClock()
         self.gc_enabled = gc
         self.auto_create_namespaces = auto_create_namespaces
@@ -208,6 +209,15 @@ class APIServer:
         # bearer token -> user info ({"username", "groups"}); None disables authn in HTTP mode
         self.tokens = tokens
         self.authorizer: Optional[Callable[[Dict[str, Any], Dict[str, Any]], bool]] = None
+        # "RBAC": HTTP requests are authorized against stored (Cluster)Roles/Bindings
+        self.rbac = None
+        if authorization == "RBAC":
+            from .rbac import RBACAuthorizer
+
+            self.rbac = RBACAuthorizer(self)
+            self.authorizer = self.rbac
+        elif authorization != "AlwaysAllow":
+            raise ValueError(f"unknown authorization mode {authorization!r}")
         self._rv = 0
         self._resources: Dict[Tuple[str, str, str], ResourceInfo] = {}
         self._by_kind: Dict[Tuple[str, str, str], ResourceInfo] = {}

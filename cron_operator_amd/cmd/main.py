@@ -113,11 +113,24 @@ def build_parser() -> argparse.ArgumentParser:
     fa.add_argument("--kubeconfig-out", default="", help="Write a kubeconfig pointing at the server here.")
     _add_bool(fa, "--gc", True, "Run ownerReference garbage collection.")
     _add_bool(fa, "--fake-clock", False, "Use a settable clock (POST /debug/fake/clock).")
-    fa.add_argument("--token", default="", help="Require this bearer token.")
+    fa.add_argument("--token", default="", help="Require this bearer token (an admin: group system:masters).")
+    fa.add_argument("--sa-token", action="append", default=[], metavar="TOKEN=NAMESPACE:NAME",
+                    help="Also accept TOKEN as ServiceAccount NAMESPACE/NAME (repeatable).")
+    fa.add_argument("--authorization-mode", choices=["AlwaysAllow", "RBAC"], default="AlwaysAllow",
+                    help="RBAC: authorize requests against stored (Cluster)Roles and bindings.")
     _add_bool(fa, "--training-operator", False, "Also run the fake training-operator (timed mode).")
     fa.add_argument("--job-duration", type=float, default=30.0, help="Seconds a job runs in timed mode.")
 
     sub.add_parser("crd", help="Print the Cron CustomResourceDefinition")
+    kz = sub.add_parser("kustomize", help="Render a kustomization directory (kustomize build)")
+    kz.add_argument("dir", nargs="?", default="deploy/kustomize/default")
+    kz.add_argument("-o", "--output", default="", help="Write here instead of stdout (e.g. dist/install.yaml).")
+    hm = sub.add_parser("helm-template", help="Render the Helm chart (helm template)")
+    hm.add_argument("chart", nargs="?", default="charts/cron-operator")
+    hm.add_argument("--release", default="cron-operator")
+    hm.add_argument("--namespace", default="cron-operator")
+    hm.add_argument("--set", action="append", default=[], help="key.path=value overrides")
+    hm.add_argument("-f", "--values", action="append", default=[], help="values file(s)")
     sub.add_parser("version", help="Print the version")
     return root
 
@@ -207,8 +220,18 @@ async def run_fake_apiserver(a: argparse.Namespace) -> int:
     from ..utils.clock import FakeClock, RealClock
 
     clock = FakeClock() if a.fake_clock else RealClock()
+    from ..apiserver.rbac import service_account_user
+
     tokens = {a.token: {"username": "admin", "groups": ["system:masters"]}} if a.token else None
-    server = APIServer(clock, gc=a.gc, tokens=tokens)
+    for spec in a.sa_token:
+        tok, _, who = spec.partition("=")
+        ns, _, name = who.partition(":")
+        if not (tok and ns and name):
+            print(f"invalid --sa-token {spec!r} (want TOKEN=NAMESPACE:NAME)", file=sys.stderr)
+            return 2
+        tokens = tokens or {}
+        tokens[tok] = service_account_user(ns, name)
+    server = APIServer(clock, gc=a.gc, tokens=tokens, authorization=a.authorization_mode)
     server.install_crd(crd())
     for c in kubeflow_crds():
         server.install_crd(c)
@@ -237,6 +260,40 @@ async def run_fake_apiserver(a: argparse.Namespace) -> int:
     return 0
 
 
+def _helm_template(a: argparse.Namespace) -> int:
+    import yaml
+
+    from ..utils.gotemplate import render_chart
+
+    values: dict = {}
+
+    def put(path: str, val) -> None:
+        cur = values
+        keys = path.split(".")
+        for k in keys[:-1]:
+            cur = cur.setdefault(k, {})
+        cur[keys[-1]] = val
+
+    def merge(dst: dict, src: dict) -> None:
+        for k, v in src.items():
+            if isinstance(v, dict) and isinstance(dst.get(k), dict):
+                merge(dst[k], v)
+            else:
+                dst[k] = v
+
+    for f in a.values:
+        with open(f) as fh:
+            merge(values, yaml.safe_load(fh) or {})
+    for kv in a.set:
+        k, _, v = kv.partition("=")
+        put(k, yaml.safe_load(v) if v else "")
+    docs = render_chart(a.chart, values, release=a.release, namespace=a.namespace)
+    for name, objs in docs.items():
+        for obj in objs:
+            sys.stdout.write(f"---\n# Source: {name}\n" + yaml.safe_dump(obj, sort_keys=False))
+    return 0
+
+
 def main(argv: Optional[List[str]] = None) -> int:
     parser = build_parser()
     a = parser.parse_args(argv)
@@ -251,6 +308,19 @@ def main(argv: Optional[List[str]] = None) -> int:
 
         sys.stdout.write(crd_yaml())
         return 0
+    if a.command == "kustomize":
+        from ..utils.kustomize import build_yaml
+
+        out = build_yaml(a.dir)
+        if a.output:
+            os.makedirs(os.path.dirname(a.output) or ".", exist_ok=True)
+            with open(a.output, "w") as fh:
+                fh.write(out)
+        else:
+            sys.stdout.write(out)
+        return 0
+    if a.command == "helm-template":
+        return _helm_template(a)
     if a.command == "fake-apiserver":
         return asyncio.run(run_fake_apiserver(a))
     if a.command == "start":

@@ -1,0 +1,56 @@
+#!/usr/bin/env python3
+"""Host-side profile of the operator process during the headline bench.
+
+The operator is CPU control plane, so its "kernel trace" is a cProfile of the
+reconcile hot path (the fake apiserver runs in its own process and is not
+included).  Writes the top functions by self time and by cumulative time.
+"""
+from __future__ import annotations
+
+import argparse
+import cProfile
+import io
+import os
+import pstats
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--crons", type=int, default=1000)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--transport", default="http")
+    ap.add_argument("--mode", default="optimized")
+    ap.add_argument("--top", type=int, default=45)
+    ap.add_argument("--out", required=True)
+    a = ap.parse_args()
+
+    from cron_operator_amd.bench.harness import BenchConfig, run_sync, summarize
+
+    cfg = BenchConfig(n_crons=a.crons, steps=a.steps, warmup=a.warmup, transport=a.transport, mode=a.mode)
+    prof = cProfile.Profile()
+    t0, c0 = time.perf_counter(), time.process_time()
+    prof.enable()
+    res = run_sync(cfg)
+    prof.disable()
+    wall, cpu = time.perf_counter() - t0, time.process_time() - c0
+    buf = io.StringIO()
+    buf.write(f"# operator-process cProfile ({a.mode}/{a.transport}, {a.crons} Crons, "
+              f"{a.warmup}+{a.steps} steps; profiler overhead inflates absolute times)\n")
+    buf.write(f"# {summarize(res)}\n# wall {wall:.2f} s, operator CPU {cpu:.2f} s\n\n")
+    st = pstats.Stats(prof, stream=buf)
+    st.sort_stats("tottime").print_stats(a.top)
+    st.sort_stats("cumulative").print_stats(a.top)
+    with open(a.out, "w") as fh:
+        fh.write(buf.getvalue())
+    print(summarize(res))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,214 @@
+"""Process-level e2e tier: the operator binary against an apiserver over HTTP.
+
+Reference tier: ``test/e2e/e2e_test.go:53-347`` (kind + helm).  It asserts only
+that the controller pod reaches Running (``:156-184``) and that ``/metrics``
+answers ``HTTP/1.1 200 OK`` through an SA token (``:186-277``); its TODO at
+``:281-289`` names ``controller_runtime_reconcile_total`` as the next assertion.
+kind/helm are absent here, so "cluster" = ``cron-operator fake-apiserver`` in
+its own process (bearer-token auth, GC, fake training-operator) and "pod" =
+``cron-operator start`` in another, wired by a kubeconfig file -- the same
+process boundary the reference has.  Beyond the reference, a Cron fires
+end to end and its job lands in ``status.history`` after completing.
+"""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import ssl
+import subprocess
+import sys
+import time
+import urllib.error
+import urllib.request
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+TOKEN = "e2e-admin-token"
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _env():
+    env = dict(os.environ)
+    env["PYTHONPATH"] = ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    env.setdefault("CRON_OPERATOR_ENGINE", "python")
+    return env
+
+
+def _wait(pred, timeout: float, what: str, proc=None):
+    end = time.monotonic() + timeout
+    last = None
+    while time.monotonic() < end:
+        if proc is not None and proc.poll() is not None:
+            raise AssertionError(f"{what}: process exited rc={proc.returncode}: {proc.stdout.read()[-3000:]}")
+        try:
+            last = pred()
+            if last:
+                return last
+        except Exception as e:  # noqa: BLE001
+            last = e
+        time.sleep(0.1)
+    raise AssertionError(f"timed out waiting for {what} (last={last!r})")
+
+
+def _get(url: str, token: str = "", ctx=None):
+    req = urllib.request.Request(url, headers={"Authorization": f"Bearer {token}"} if token else {})
+    with urllib.request.urlopen(req, timeout=5, context=ctx) as r:
+        return r.status, r.read().decode()
+
+
+def _api(base: str, method: str, path: str, body=None, ctype="application/json"):
+    data = json.dumps(body).encode() if body is not None else None
+    req = urllib.request.Request(base + path, data=data, method=method,
+                                 headers={"Authorization": f"Bearer {TOKEN}", "Content-Type": ctype})
+    with urllib.request.urlopen(req, timeout=5) as r:
+        return json.loads(r.read())
+
+
+@pytest.fixture(scope="module")
+def cluster(tmp_path_factory):
+    d = tmp_path_factory.mktemp("e2e")
+    kcfg = str(d / "kubeconfig")
+    api_port = _free_port()
+    api = subprocess.Popen(
+        [sys.executable, "-m", "cron_operator_amd", "fake-apiserver", "--port", str(api_port), "--token", TOKEN,
+         "--kubeconfig-out", kcfg, "--training-operator", "--job-duration", "1"],
+        env=_env(), stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    base = f"http://127.0.0.1:{api_port}"
+    try:
+        _wait(lambda: os.path.exists(kcfg) and _api(base, "GET", "/api/v1/namespaces"), 60, "fake apiserver", api)
+        _api(base, "POST", "/api/v1/namespaces",
+             {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "cron-operator-system"}})
+        yield {"base": base, "kubeconfig": kcfg, "dir": d}
+    finally:
+        api.terminate()
+        try:
+            api.wait(10)
+        except subprocess.TimeoutExpired:
+            api.kill()
+
+
+def _start_operator(cluster, *extra):
+    probe, metrics = _free_port(), _free_port()
+    env = _env()
+    env["POD_NAMESPACE"] = "cron-operator-system"
+    proc = subprocess.Popen(
+        [sys.executable, "-m", "cron_operator_amd", "start", "--kubeconfig", cluster["kubeconfig"],
+         f"--health-probe-bind-address=127.0.0.1:{probe}", f"--metrics-bind-address=127.0.0.1:{metrics}",
+         "--zap-encoder", "json", *extra],
+        env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    return proc, probe, metrics
+
+
+def _stop(proc):
+    proc.terminate()
+    try:
+        rc = proc.wait(15)
+    except subprocess.TimeoutExpired:
+        proc.kill()
+        rc = proc.wait()
+    return rc
+
+
+def test_controller_running_metrics_and_cron_fires(cluster):
+    """e2e_test.go:156-184 (Running) + :186-277 (metrics 200) + the :281-289 TODO, plus a real fire."""
+    proc, probe, mport = _start_operator(cluster, "--leader-elect", "--metrics-secure=false")
+    try:
+        # "controller pod reaches Running": readiness probe answers 200
+        _wait(lambda: _get(f"http://127.0.0.1:{probe}/readyz")[0] == 200, 60, "readyz", proc)
+        assert _get(f"http://127.0.0.1:{probe}/healthz")[0] == 200
+        # leader election: the Lease named by the reference ID exists and names this process
+        lease = _wait(lambda: _api(cluster["base"], "GET", "/apis/coordination.k8s.io/v1/namespaces/"
+                                   "cron-operator-system/leases/619a52b8.kubedl.io"), 30, "lease", proc)
+        assert lease["spec"]["holderIdentity"]
+
+        # a Cron whose last run was 2 minutes ago fires immediately (cron_controller_test.go:93-97 trick)
+        base = cluster["base"]
+        tmpl = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+                "spec": {"pytorchReplicaSpecs": {"Master": {"replicas": 1, "template": {"spec": {"containers": [
+                    {"name": "pytorch", "image": "rocm/pytorch", "command": ["true"]}]}}}}}}
+        cron = {"apiVersion": "apps.kubedl.io/v1alpha1", "kind": "Cron",
+                "metadata": {"name": "e2e", "namespace": "default"},
+                "spec": {"schedule": "*/1 * * * *", "concurrencyPolicy": "Forbid", "historyLimit": 2,
+                         "template": {"workload": tmpl}}}
+        _api(base, "POST", "/apis/apps.kubedl.io/v1alpha1/namespaces/default/crons", cron)
+        past = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(time.time() - 120))
+        _api(base, "PATCH", "/apis/apps.kubedl.io/v1alpha1/namespaces/default/crons/e2e/status",
+             {"status": {"lastScheduleTime": past}}, "application/merge-patch+json")
+
+        def job_created():
+            items = _api(base, "GET", "/apis/kubeflow.org/v1/namespaces/default/pytorchjobs"
+                                      "?labelSelector=kubedl.io%2Fcron-name%3De2e")["items"]
+            return items or None
+
+        jobs = _wait(job_created, 30, "PyTorchJob creation", proc)
+        job = jobs[0]
+        assert job["metadata"]["name"].startswith("e2e-")
+        owner = job["metadata"]["ownerReferences"][0]
+        assert (owner["kind"], owner["name"], owner["controller"]) == ("Cron", "e2e", True)
+
+        # the fake training-operator finishes it after ~1 s; the Cron records it in history
+        def in_history():
+            st = _api(base, "GET", "/apis/apps.kubedl.io/v1alpha1/namespaces/default/crons/e2e").get("status", {})
+            hist = st.get("history") or []
+            return hist if any(h["status"] == "Succeeded" for h in hist) else None
+
+        hist = _wait(in_history, 30, "history Succeeded", proc)
+        assert hist[0]["object"]["name"] == job["metadata"]["name"]
+        assert hist[0]["object"]["apiGroup"] == "kubeflow.org/v1"
+
+        # metrics: plain HTTP like the chart (deployment.yaml:62-63), reconcile counter present
+        status, body = _get(f"http://127.0.0.1:{mport}/metrics")
+        assert status == 200
+        assert 'controller_runtime_reconcile_total{controller="cron",result="requeue_after"}' in body
+        assert 'workqueue_adds_total{controller="cron",name="cron"}' in body
+    finally:
+        rc = _stop(proc)
+    assert rc == 0, proc.stdout.read()[-3000:]
+
+
+def test_secure_metrics_require_authorized_token(cluster):
+    """Binary default --metrics-secure=true: HTTPS + TokenReview/SubjectAccessReview filter (start.go:127-133)."""
+    proc, probe, mport = _start_operator(cluster, "--leader-elect=false")
+    try:
+        _wait(lambda: _get(f"http://127.0.0.1:{probe}/readyz")[0] == 200, 60, "readyz", proc)
+        ctx = ssl.create_default_context()
+        ctx.check_hostname = False
+        ctx.verify_mode = ssl.CERT_NONE
+        url = f"https://127.0.0.1:{mport}/metrics"
+        _wait(lambda: _get(url, TOKEN, ctx)[0] == 200, 30, "secure metrics", proc)
+        with pytest.raises(urllib.error.HTTPError) as ei:
+            _get(url, "", ctx)
+        assert ei.value.code in (401, 403)
+        with pytest.raises(urllib.error.HTTPError) as ei:
+            _get(url, "not-a-token", ctx)
+        assert ei.value.code in (401, 403)
+    finally:
+        _stop(proc)
+
+
+def test_bad_kubeconfig_fails_fast(tmp_path):
+    """GetConfigOrDie analog: no reachable config -> non-zero exit, no hang."""
+    env = _env()
+    env.pop("KUBERNETES_SERVICE_HOST", None)
+    env["KUBECONFIG"] = str(tmp_path / "missing")
+    env["HOME"] = str(tmp_path)
+    r = subprocess.run([sys.executable, "-m", "cron_operator_amd", "start", "--kubeconfig", str(tmp_path / "nope"),
+                        "--health-probe-bind-address=0"], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0
+
+
+def test_cli_help_version_crd():
+    env = _env()
+    r = subprocess.run([sys.executable, "-m", "cron_operator_amd"], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0 and "start" in r.stdout
+    r = subprocess.run([sys.executable, "-m", "cron_operator_amd", "crd"], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0 and "crons.apps.kubedl.io" in r.stdout

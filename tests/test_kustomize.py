@@ -1,0 +1,175 @@
+"""``kustomize build`` of the shipped tree (reference: ``make build-installer``,
+``Makefile:112-150``, which renders ``config/default`` into ``dist/install.yaml``).
+
+Checks the transformers the install relies on -- namespace, namePrefix with
+reference fix-ups, image override, JSON6902 patch -- plus strategic-merge and
+6902 semantics on small inputs, and that every rendered object is accepted by
+the fake apiserver (the "kubectl apply" smoke of the installer).
+"""
+from __future__ import annotations
+
+import os
+
+import pytest
+import yaml
+
+from cron_operator_amd.api.meta import GroupVersionResource
+from cron_operator_amd.apiserver.server import APIServer
+from cron_operator_amd.cmd.main import main as cli
+from cron_operator_amd.utils.clock import FakeClock
+from cron_operator_amd.utils.kustomize import KustomizeError, apply_json6902, build, build_sorted, strategic_merge
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+DEFAULT = os.path.join(ROOT, "deploy", "kustomize", "default")
+
+
+def by_kind(objs, kind):
+    return [o for o in objs if o["kind"] == kind]
+
+
+def test_default_install_namespace_prefix_and_refs():
+    objs = build_sorted(DEFAULT)
+    kinds = [o["kind"] for o in objs]
+    assert kinds[:2] == ["Namespace", "CustomResourceDefinition"]  # legacy order, as `kubectl apply` needs
+    assert kinds[-2:] == ["Service", "Deployment"]
+    crd = objs[1]
+    assert crd["metadata"]["name"] == "crons.apps.kubedl.io"  # CRDs are never prefixed
+    ns = by_kind(objs, "Namespace")
+    assert [n["metadata"]["name"] for n in ns] == ["cron-operator-system"]
+    for o in objs:
+        if o["kind"] not in ("CustomResourceDefinition", "ClusterRole", "ClusterRoleBinding", "Namespace"):
+            assert o["metadata"]["namespace"] == "cron-operator-system", o["metadata"]
+        if o["kind"] != "CustomResourceDefinition":
+            assert o["metadata"]["name"].startswith("cron-operator-")
+    names = {(o["kind"], o["metadata"]["name"]) for o in objs}
+    sa = by_kind(objs, "ServiceAccount")[0]["metadata"]["name"]
+    for b in by_kind(objs, "ClusterRoleBinding") + by_kind(objs, "RoleBinding"):
+        assert (b["roleRef"]["kind"], b["roleRef"]["name"]) in names
+        for s in b["subjects"]:
+            if s["kind"] == "ServiceAccount":
+                assert s["name"] == sa and s["namespace"] == "cron-operator-system"
+    dep = by_kind(objs, "Deployment")[0]
+    pod = dep["spec"]["template"]["spec"]
+    assert pod["serviceAccountName"] == sa
+    c = pod["containers"][0]
+    assert c["image"] == "docker.io/cron-operator-amd/cron-operator:0.3.0"
+    # metrics patch (config/default/manager_metrics_patch.yaml analog) applied
+    assert "--metrics-bind-address=:8443" in c["args"]
+    assert "--leader-elect" in c["args"]
+    assert {"name": "https", "containerPort": 8443} in c["ports"]
+    # the user-facing aggregated roles keep the reference names under the prefix
+    assert {"cron-operator-cron-admin-role", "cron-operator-cron-editor-role", "cron-operator-cron-viewer-role"} <= \
+        {o["metadata"]["name"] for o in by_kind(objs, "ClusterRole")}
+    # the manager role grants the right group (reference Appendix B #1 fixed)
+    mgr = next(o for o in by_kind(objs, "ClusterRole") if o["metadata"]["name"] == "cron-operator-manager-role")
+    assert any("apps.kubedl.io" in r.get("apiGroups", []) for r in mgr["rules"])
+
+
+@pytest.mark.parametrize("overlay", ["prometheus", "network-policy", "crd", "rbac", "manager"])
+def test_component_dirs_build(overlay):
+    assert build(os.path.join(ROOT, "deploy", "kustomize", overlay))
+
+
+def test_examples_kustomization_builds():
+    objs = build(os.path.join(ROOT, "examples"))
+    assert {o["kind"] for o in objs} == {"Cron"}
+    assert len(objs) >= 5
+
+
+def test_install_objects_accepted_by_apiserver():
+    """`kubectl apply -f dist/install.yaml` against the fake apiserver."""
+    srv = APIServer(FakeClock(0), gc=False)
+    objs = build_sorted(DEFAULT)
+    plural = {"CustomResourceDefinition": ("apiextensions.k8s.io", "customresourcedefinitions"),
+              "Namespace": ("", "namespaces"), "ServiceAccount": ("", "serviceaccounts"),
+              "ClusterRole": ("rbac.authorization.k8s.io", "clusterroles"),
+              "ClusterRoleBinding": ("rbac.authorization.k8s.io", "clusterrolebindings"),
+              "Role": ("rbac.authorization.k8s.io", "roles"), "RoleBinding": ("rbac.authorization.k8s.io", "rolebindings"),
+              "Deployment": ("apps", "deployments"), "Service": ("", "services")}
+    for o in objs:
+        g, r = plural[o["kind"]]
+        gvr = GroupVersionResource(g, o["apiVersion"].rpartition("/")[2], r)
+        if o["kind"] == "CustomResourceDefinition":
+            srv.install_crd(o)
+            continue
+        srv.create(gvr, o["metadata"].get("namespace", ""), o)
+    # the CRD from the installer is live: a Cron can be created
+    srv.create_namespace("d")
+    srv.create(GroupVersionResource("apps.kubedl.io", "v1alpha1", "crons"),
+               "d", {"apiVersion": "apps.kubedl.io/v1alpha1", "kind": "Cron", "metadata": {"name": "c", "namespace": "d"},
+                "spec": {"schedule": "@hourly", "template": {"workload": {"apiVersion": "kubeflow.org/v1",
+                                                                           "kind": "PyTorchJob"}}}})
+
+
+def test_cli_kustomize_writes_installer(tmp_path, capsys):
+    out = tmp_path / "dist" / "install.yaml"
+    assert cli(["kustomize", DEFAULT, "-o", str(out)]) == 0
+    docs = [d for d in yaml.safe_load_all(out.read_text()) if d]
+    assert docs == build_sorted(DEFAULT)
+
+
+def test_cli_helm_template_set(capsys):
+    assert cli(["helm-template", os.path.join(ROOT, "charts", "cron-operator"), "--set", "qps=99",
+                "--set", "leaderElection.enable=false"]) == 0
+    text = capsys.readouterr().out
+    assert "--qps=99" in text and "--leader-elect=false" in text
+
+
+def test_json6902_ops():
+    doc = {"a": {"b": [1, 2]}, "c": 1}
+    out = apply_json6902(doc, [
+        {"op": "add", "path": "/a/b/-", "value": 3},
+        {"op": "add", "path": "/a/b/0", "value": 0},
+        {"op": "replace", "path": "/c", "value": 2},
+        {"op": "copy", "from": "/c", "path": "/d"},
+        {"op": "move", "from": "/d", "path": "/e"},
+        {"op": "remove", "path": "/a/b/1"},
+        {"op": "test", "path": "/e", "value": 2},
+        {"op": "add", "path": "/x~1y", "value": True},
+    ])
+    assert out == {"a": {"b": [0, 2, 3]}, "c": 2, "e": 2, "x/y": True}
+    assert doc == {"a": {"b": [1, 2]}, "c": 1}  # input untouched
+    with pytest.raises(KustomizeError):
+        apply_json6902(doc, [{"op": "replace", "path": "/nope", "value": 1}])
+    with pytest.raises(KustomizeError):
+        apply_json6902(doc, [{"op": "test", "path": "/c", "value": 5}])
+
+
+def test_strategic_merge_containers_by_name():
+    base = {"spec": {"containers": [{"name": "a", "image": "x", "args": ["1"]}, {"name": "b", "image": "y"}],
+                     "nodeSelector": {"k": "v"}}}
+    patch = {"spec": {"containers": [{"name": "a", "image": "x2"}, {"name": "c", "image": "z"},
+                                     {"name": "b", "$patch": "delete"}],
+                      "nodeSelector": {"k": None, "k2": "v2"}}}
+    out = strategic_merge(base, patch)
+    assert out["spec"]["containers"] == [{"name": "a", "image": "x2", "args": ["1"]}, {"name": "c", "image": "z"}]
+    assert out["spec"]["nodeSelector"] == {"k2": "v2"}
+
+
+def test_overlay_with_labels_images_and_inline_patch(tmp_path):
+    base = tmp_path / "base"
+    base.mkdir()
+    (base / "kustomization.yaml").write_text("resources: [dep.yaml]\n")
+    (base / "dep.yaml").write_text(yaml.safe_dump({
+        "apiVersion": "apps/v1", "kind": "Deployment", "metadata": {"name": "m"},
+        "spec": {"selector": {"matchLabels": {"app": "m"}}, "template": {"metadata": {"labels": {"app": "m"}},
+                 "spec": {"containers": [{"name": "c", "image": "controller:latest"}]}}}}))
+    ov = tmp_path / "ov"
+    ov.mkdir()
+    (ov / "kustomization.yaml").write_text(yaml.safe_dump({
+        "resources": ["../base"], "nameSuffix": "-x", "namespace": "n",
+        "labels": [{"pairs": {"tier": "ops"}, "includeSelectors": True}],
+        "images": [{"name": "controller", "newName": "reg/op", "newTag": "v9"}],
+        "patches": [{"patch": "apiVersion: apps/v1\nkind: Deployment\nmetadata: {name: m}\nspec: {replicas: 3}\n"}]}))
+    (o,) = build(str(ov))
+    assert o["metadata"] == {"name": "m-x", "namespace": "n", "labels": {"tier": "ops"}}
+    assert o["spec"]["replicas"] == 3
+    assert o["spec"]["selector"]["matchLabels"] == {"app": "m", "tier": "ops"}
+    assert o["spec"]["template"]["spec"]["containers"][0]["image"] == "reg/op:v9"
+
+
+def test_patch_target_must_match(tmp_path):
+    (tmp_path / "kustomization.yaml").write_text(yaml.safe_dump({
+        "resources": [], "patches": [{"patch": "[]", "target": {"kind": "Deployment"}}]}))
+    with pytest.raises(KustomizeError):
+        build(str(tmp_path))
