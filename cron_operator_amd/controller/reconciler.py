@@ -28,7 +28,6 @@ Time comes from the injected clock (the reference calls ``time.Now()``,
 from __future__ import annotations
 
 import json
-import math
 import time
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional, Tuple

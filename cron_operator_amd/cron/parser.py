@@ -149,7 +149,8 @@ def _parse_descriptor(desc: str, loc: Location) -> Schedule:
     if desc in ("@daily", "@midnight"):
         return SpecSchedule(one(SECONDS), one(MINUTES), one(HOURS), all_bits(DOM), all_bits(MONTHS), all_bits(DOW), loc)
     if desc == "@hourly":
-        return SpecSchedule(one(SECONDS), one(MINUTES), all_bits(HOURS), all_bits(DOM), all_bits(MONTHS), all_bits(DOW), loc)
+        return SpecSchedule(one(SECONDS), one(MINUTES), all_bits(HOURS), all_bits(DOM), all_bits(MONTHS),
+                            all_bits(DOW), loc)
     prefix = "@every "
     if desc.startswith(prefix):
         try:

@@ -28,7 +28,7 @@ import heapq
 import itertools
 import time
 from collections import deque
-from typing import Any, Deque, Dict, Hashable, List, Optional, Set, Tuple
+from typing import Deque, Dict, Hashable, List, Optional, Set, Tuple
 
 from ..runtime import metrics
 from ..runtime.ratelimit import RateLimiter, default_controller_rate_limiter

@@ -130,7 +130,8 @@ class Controller:
 
         return EventHandler(on_add, on_update, on_delete)
 
-    def watch_for(self, informer: Informer, gvk: GroupVersionKind, predicates: Optional[List[Predicate]] = None) -> None:
+    def watch_for(self, informer: Informer, gvk: GroupVersionKind,
+                  predicates: Optional[List[Predicate]] = None) -> None:
         """``For(&Cron{})``: enqueue the object itself."""
         self.for_kind = gvk
         h = self._handler(lambda o: [_key(o)], list(predicates or []))

@@ -15,7 +15,7 @@ from __future__ import annotations
 
 import asyncio
 from dataclasses import dataclass, field
-from typing import Awaitable, Callable, Dict, List, Optional
+from typing import Awaitable, Callable, List, Optional
 
 from ..parallel.leaderelection import LeaderElector, in_cluster_namespace
 from ..utils.clock import Clock, RealClock

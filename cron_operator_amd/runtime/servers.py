@@ -14,12 +14,11 @@
 """
 from __future__ import annotations
 
-import asyncio
 import os
 import ssl
 import subprocess
 import tempfile
-from typing import Any, Awaitable, Callable, Dict, Optional, Tuple
+from typing import Awaitable, Callable, Dict, Optional, Tuple
 
 from aiohttp import web
 

@@ -27,7 +27,7 @@ import sys
 from typing import Any, Dict, List, Optional, Tuple
 
 from ..api import errors
-from ..api.meta import GroupVersionKind, GroupVersionResource
+from ..api.meta import GroupVersionResource
 from ..runtime.client import Client
 from ..runtime.informer import EventHandler, Informer
 from ..utils.clock import Clock, RealClock

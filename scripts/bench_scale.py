@@ -1,0 +1,62 @@
+#!/usr/bin/env python3
+"""Scaling curve: the headline bench at 1 / 10 / 100 / 1000 Cron CRs.
+
+BASELINE.json asks for reconciles/sec and tick->create latency "at 1, 10, 100
+and 1000 concurrent Cron CRs with the scaling curve reported".  This runs
+``cron_operator_amd.bench.harness`` for each size, in both modes
+(``optimized`` = this operator, ``reference`` = the reference algorithm), and
+prints a Markdown table plus one JSON document (``--out``).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sizes", default="1,10,100,1000")
+    ap.add_argument("--modes", default="optimized,reference")
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--transport", default="http")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+
+    from cron_operator_amd.bench.harness import BenchConfig, run_sync
+
+    rows = []
+    for mode in a.modes.split(","):
+        for n in (int(x) for x in a.sizes.split(",")):
+            t0 = time.perf_counter()
+            r = run_sync(BenchConfig(n_crons=n, steps=a.steps, warmup=a.warmup, mode=mode, transport=a.transport))
+            rows.append({"mode": mode, "n_crons": n, "cron_reconciles_per_s": r.cron_reconciles_per_s,
+                         "raw_reconciles_per_s": r.raw_reconciles_per_s, "p50_ms": r.p50_latency_ms,
+                         "p99_ms": r.p99_latency_ms, "ms_per_step": r.ms_per_step,
+                         "api_requests_per_fire": r.api_requests_per_fire,
+                         "reconciles_per_fire": r.reconciles_per_fire, "wall_s": time.perf_counter() - t0})
+            print(f"{mode:>9} n={n:>5}: {r.cron_reconciles_per_s:9.1f} cron-reconciles/s  "
+                  f"p50 {r.p50_latency_ms:8.1f} ms  p99 {r.p99_latency_ms:8.1f} ms  "
+                  f"{r.api_requests_per_fire:.1f} req/fire", flush=True)
+    print()
+    print("| mode | Crons | cron-reconciles/s | p50 tick→create ms | p99 ms | ms/tick | API req/fire "
+          "| reconciles/fire |")
+    print("|---|---:|---:|---:|---:|---:|---:|---:|")
+    for x in rows:
+        print(f"| {x['mode']} | {x['n_crons']} | {x['cron_reconciles_per_s']:.1f} | {x['p50_ms']:.1f} | "
+              f"{x['p99_ms']:.1f} | {x['ms_per_step']:.0f} | {x['api_requests_per_fire']:.1f} | "
+              f"{x['reconciles_per_fire']:.1f} |")
+    if a.out:
+        with open(a.out, "w") as fh:
+            json.dump({"transport": a.transport, "steps": a.steps, "warmup": a.warmup, "rows": rows}, fh, indent=1)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

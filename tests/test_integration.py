@@ -18,7 +18,7 @@ from cron_operator_amd.controller.reconciler import ReconcilerOptions
 from cron_operator_amd.testing.env import TestEnv
 from cron_operator_amd.trainingop.operator import FakeTrainingOperator
 from cron_operator_amd.utils.clock import FakeClock
-from cron_operator_amd.utils.gotime import UTC, GoTime, parse_rfc3339
+from cron_operator_amd.utils.gotime import UTC, GoTime
 
 PT = GroupVersionResource("kubeflow.org", "v1", "pytorchjobs")
 TF = GroupVersionResource("kubeflow.org", "v1", "tfjobs")
@@ -34,7 +34,8 @@ MODES = {"optimized": ReconcilerOptions(), "reference": ReconcilerOptions.refere
 
 
 def names(server, gvr, cron):
-    return sorted(o["metadata"]["name"] for o in server.list(gvr, NS, label_selector=f"{LABEL_CRON_NAME}={cron}")["items"])
+    items = server.list(gvr, NS, label_selector=f"{LABEL_CRON_NAME}={cron}")["items"]
+    return sorted(o["metadata"]["name"] for o in items)
 
 
 @pytest.mark.parametrize("mode", MODES)

@@ -84,7 +84,8 @@ def test_install_objects_accepted_by_apiserver():
               "Namespace": ("", "namespaces"), "ServiceAccount": ("", "serviceaccounts"),
               "ClusterRole": ("rbac.authorization.k8s.io", "clusterroles"),
               "ClusterRoleBinding": ("rbac.authorization.k8s.io", "clusterrolebindings"),
-              "Role": ("rbac.authorization.k8s.io", "roles"), "RoleBinding": ("rbac.authorization.k8s.io", "rolebindings"),
+              "Role": ("rbac.authorization.k8s.io", "roles"),
+              "RoleBinding": ("rbac.authorization.k8s.io", "rolebindings"),
               "Deployment": ("apps", "deployments"), "Service": ("", "services")}
     for o in objs:
         g, r = plural[o["kind"]]
@@ -96,9 +97,10 @@ def test_install_objects_accepted_by_apiserver():
     # the CRD from the installer is live: a Cron can be created
     srv.create_namespace("d")
     srv.create(GroupVersionResource("apps.kubedl.io", "v1alpha1", "crons"),
-               "d", {"apiVersion": "apps.kubedl.io/v1alpha1", "kind": "Cron", "metadata": {"name": "c", "namespace": "d"},
-                "spec": {"schedule": "@hourly", "template": {"workload": {"apiVersion": "kubeflow.org/v1",
-                                                                           "kind": "PyTorchJob"}}}})
+               "d", {"apiVersion": "apps.kubedl.io/v1alpha1", "kind": "Cron",
+                     "metadata": {"name": "c", "namespace": "d"},
+                     "spec": {"schedule": "@hourly", "template": {"workload": {"apiVersion": "kubeflow.org/v1",
+                                                                                "kind": "PyTorchJob"}}}})
 
 
 def test_cli_kustomize_writes_installer(tmp_path, capsys):

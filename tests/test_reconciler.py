@@ -21,7 +21,7 @@ from cron_operator_amd.runtime.controller import Request
 from cron_operator_amd.runtime.events import FakeRecorder
 from cron_operator_amd.testing.env import TestEnv
 from cron_operator_amd.trainingop.operator import finished_status, running_status
-from cron_operator_amd.utils.gotime import MINUTE, NANOS, UTC, GoTime, parse_rfc3339
+from cron_operator_amd.utils.gotime import MINUTE, UTC, GoTime, parse_rfc3339
 from cron_operator_amd.utils.logging import get_logger
 
 PT = GroupVersionResource("kubeflow.org", "v1", "pytorchjobs")

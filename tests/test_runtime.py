@@ -15,7 +15,7 @@ from cron_operator_amd.api.v1alpha1 import CRON_GVK, CRON_GVR, new_cron
 from cron_operator_amd.apiserver.http import APIServerApp
 from cron_operator_amd.parallel.leaderelection import LEASES, LeaderElector
 from cron_operator_amd.parallel.workqueue import ShutDown, WorkQueue
-from cron_operator_amd.runtime.client import Client, InMemoryTransport
+from cron_operator_amd.runtime.client import Client
 from cron_operator_amd.runtime.events import Broadcaster, EVENTS_GVR
 from cron_operator_amd.runtime.http import HttpTransport, resource_path
 from cron_operator_amd.runtime.informer import EventHandler, Informer, label_index
