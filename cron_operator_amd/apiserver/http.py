@@ -253,25 +253,33 @@ class APIServerApp:
         # stored object can be returned without a defensive copy.
         s.copy_responses = False
         try:
-            if verb == "list":
-                return _json(s.list(gvr, ns or None, q.get("labelSelector"), q.get("fieldSelector"),
-                                    int(q.get("limit") or 0), q.get("continue"), copy=False))
-            if verb == "get":
-                return _json(s.get(gvr, ns, name))
-            if verb == "create":
-                return _json(s.create(gvr, ns, body, dry_run=q.get("dryRun") == "All"), 201)
-            if verb == "update":
-                return _json(s.update(gvr, ns, name, body, sub or None))
-            if verb == "patch":
-                return _json(s.patch(gvr, ns, name, body, ptype, sub or None))
-            if verb == "delete":
-                opts = body or {}
-                policy = opts.get("propagationPolicy") or q.get("propagationPolicy")
-                return _json(s.delete(gvr, ns, name, policy, opts.get("preconditions")))
-            n = s.delete_collection(gvr, ns or None, q.get("labelSelector"))
-            return _json({"kind": "Status", "apiVersion": "v1", "status": "Success", "details": {"deleted": n}})
+            resp = self._apply(verb, gvr, ns, name, sub, body, ptype, q)
         finally:
             s.copy_responses = True
+        if s.faults.faults:  # "lost response" faults fire after the verb was applied
+            s.faults.check(verb, gvr.resource, sub or None, name or None, after=True)
+        return resp
+
+    def _apply(self, verb: str, gvr: GroupVersionResource, ns: str, name: str, sub: str, body: Any, ptype: Any,
+               q: Any) -> web.Response:
+        s = self.server
+        if verb == "list":
+            return _json(s.list(gvr, ns or None, q.get("labelSelector"), q.get("fieldSelector"),
+                                int(q.get("limit") or 0), q.get("continue"), copy=False))
+        if verb == "get":
+            return _json(s.get(gvr, ns, name))
+        if verb == "create":
+            return _json(s.create(gvr, ns, body, dry_run=q.get("dryRun") == "All"), 201)
+        if verb == "update":
+            return _json(s.update(gvr, ns, name, body, sub or None))
+        if verb == "patch":
+            return _json(s.patch(gvr, ns, name, body, ptype, sub or None))
+        if verb == "delete":
+            opts = body or {}
+            policy = opts.get("propagationPolicy") or q.get("propagationPolicy")
+            return _json(s.delete(gvr, ns, name, policy, opts.get("preconditions")))
+        n = s.delete_collection(gvr, ns or None, q.get("labelSelector"))
+        return _json({"kind": "Status", "apiVersion": "v1", "status": "Success", "details": {"deleted": n}})
 
     async def _watch(self, req: web.Request, gvr: GroupVersionResource, ns: str) -> web.StreamResponse:
         q = req.query

@@ -69,6 +69,9 @@ class Fault:
     times: int = -1            # -1 = unlimited
     probability: float = 1.0
     name: Optional[str] = None
+    # True: the verb is applied and *then* the error is returned -- a lost response
+    # (timeout after commit), the case deterministic job names exist for
+    after: bool = False
 
     def matches(self, verb: str, resource: str, sub: Optional[str], name: Optional[str]) -> bool:
         if self.times == 0:
@@ -101,9 +104,10 @@ class FaultInjector:
         self.faults.clear()
         self.latency.clear()
 
-    def check(self, verb: str, resource: str, sub: Optional[str] = None, name: Optional[str] = None) -> None:
+    def check(self, verb: str, resource: str, sub: Optional[str] = None, name: Optional[str] = None,
+              after: bool = False) -> None:
         for f in self.faults:
-            if f.matches(verb, resource, sub, name) and self._rng.random() < f.probability:
+            if f.after == after and f.matches(verb, resource, sub, name) and self._rng.random() < f.probability:
                 if f.times > 0:
                     f.times -= 1
                 raise errors.ApiError(f.code, f.reason, f.message)

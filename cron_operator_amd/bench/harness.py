@@ -102,6 +102,9 @@ class BenchResult:
     phase_ms: Dict[str, List[float]] = field(default_factory=dict)
     engine: str = ""
     fastjson_native: bool = False
+    # CPU seconds burnt in the timed region by the operator process and the apiserver process
+    cpu_s_operator: float = 0.0
+    cpu_s_apiserver: float = 0.0
 
     def to_dict(self) -> Dict[str, Any]:
         return asdict(self)
@@ -145,6 +148,20 @@ class _RemoteServer:
             except subprocess.TimeoutExpired:
                 self.proc.kill()
                 self.proc.wait()
+
+
+def _cpu_times(remote: Optional["_RemoteServer"]) -> "tuple[float, float]":
+    """(operator process CPU s, apiserver process CPU s) -- the apiserver shares our process in memory mode."""
+    me = time.process_time()
+    other = 0.0
+    if remote is not None and remote.proc is not None:
+        try:
+            with open(f"/proc/{remote.proc.pid}/stat") as fh:
+                f = fh.read().rsplit(")", 1)[1].split()
+            other = (int(f[11]) + int(f[12])) / os.sysconf("SC_CLK_TCK")
+        except (OSError, IndexError, ValueError):
+            other = float("nan")
+    return me, other
 
 
 async def run(cfg: BenchConfig, on_step=None) -> BenchResult:
@@ -324,6 +341,7 @@ async def run(cfg: BenchConfig, on_step=None) -> BenchResult:
         for k in range(1, total + 1):
             tick_ns = T0_NS + k * 60 * NANOS
             if k == cfg.warmup + 1:
+                cpu0 = _cpu_times(remote)
                 rec0 = ctrl.reconciles
                 req0 = client.requests
                 reqv0 = dict(client.requests_by_verb)
@@ -352,6 +370,7 @@ async def run(cfg: BenchConfig, on_step=None) -> BenchResult:
             if on_step is not None:
                 on_step(k, dt, k > cfg.warmup)
         elapsed = time.perf_counter() - t_start
+        cpu1 = _cpu_times(remote)
         reconciles = ctrl.reconciles - rec0
         requests = client.requests - req0
         by_verb = {v: n - reqv0.get(v, 0) for v, n in client.requests_by_verb.items()}
@@ -364,7 +383,8 @@ async def run(cfg: BenchConfig, on_step=None) -> BenchResult:
             max_latency_ms=max(timed_lat) * 1000 if timed_lat else float("nan"),
             api_requests_per_fire=requests / fires, api_requests_by_verb=by_verb,
             reconciles_per_fire=reconciles / fires, step_ms=step_ms, phase_ms=phase_ms,
-            engine=default_engine().name, fastjson_native=jsonutil.NATIVE)
+            engine=default_engine().name, fastjson_native=jsonutil.NATIVE,
+            cpu_s_operator=cpu1[0] - cpu0[0], cpu_s_apiserver=cpu1[1] - cpu0[1])
         mgr.stop()
         try:
             await asyncio.wait_for(mgr_task, 30)
@@ -388,4 +408,5 @@ def summarize(r: BenchResult) -> str:
             f"{r.cron_reconciles_per_s:,.0f} cron-reconciles/s, {r.raw_reconciles_per_s:,.0f} raw reconciles/s, "
             f"p50 {r.p50_latency_ms:.1f} ms p99 {r.p99_latency_ms:.1f} ms, {r.ms_per_step:.0f} ms/step, "
             f"{r.api_requests_per_fire:.2f} req/fire, {r.reconciles_per_fire:.2f} reconciles/fire "
-            f"(median step {statistics.median(r.step_ms):.0f} ms)")
+            f"(median step {statistics.median(r.step_ms):.0f} ms; CPU operator {r.cpu_s_operator:.2f} s, "
+            f"apiserver {r.cpu_s_apiserver:.2f} s)")

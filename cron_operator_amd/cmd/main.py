@@ -106,6 +106,10 @@ def build_parser() -> argparse.ArgumentParser:
                     help="'reference' reproduces every reference behaviour (live child LIST, finished=now, ...).")
     st.add_argument("--cron-engine", choices=["auto", "native", "python"], default="auto",
                     help="Cron next-fire engine implementation.")
+    _add_bool(st, "--enable-tracing", False, "Record per-reconcile spans (served at /debug/traces on the probe port).")
+    st.add_argument("--trace-file", default="", help="Also append finished spans here as JSON lines "
+                                                     "(implies --enable-tracing).")
+    st.add_argument("--trace-sample-rate", type=float, default=1.0, help="Fraction of reconciles traced.")
 
     fa = sub.add_parser("fake-apiserver", help="Serve the in-process fake Kubernetes API server over HTTP")
     fa.add_argument("--bind-address", default="127.0.0.1")
@@ -155,6 +159,11 @@ async def run_start(a: argparse.Namespace) -> int:
     from ..utils.logging import get_logger
 
     log = get_logger("setup")
+    if a.enable_tracing or a.trace_file:
+        from ..runtime import tracing
+
+        tracing.set_tracer(tracing.Tracer(enabled=True, sample_rate=a.trace_sample_rate, file=a.trace_file))
+        log.info("tracing enabled", sampleRate=a.trace_sample_rate, file=a.trace_file or None)
     if not a.enable_http2:
         log.info("disabling http/2")
     if a.webhook_cert_path:

@@ -20,7 +20,19 @@ option                     default here                           reference
 ``own_write_filter``       our own status writes do not requeue   every Cron update requeues (B22)
 ``workload``               Pod/batch Job/MPIJob adapters on        kubeflow conditions only (B5, App. B #6-7)
 ``dynamic_watches``        watch whatever kind templates use      PyTorchJob + TFJob only (B22)
+``dedupe_ran_tick``        a tick whose job already exists is     the tick runs again when the status
+                           recorded, not run again                 write after its CREATE was lost
 =========================  =====================================  =======================================
+
+``dedupe_ran_tick``: the reference advances ``lastScheduleTime`` only in the
+deferred status patch after a successful CREATE (B20).  If that patch fails, or
+the CREATE's response is lost after the object was stored, the next reconcile
+sees the same missed tick again: under ``Replace`` it deletes the job it just
+created and creates it anew, and under ``Forbid`` it waits for the job to finish
+and then runs the tick a second time under a new name.  Job names are
+``<cron>-<unix(Next(tick))>`` (B18), so the job a tick produced is recognisable;
+when it already exists the tick is recorded as run instead
+(``tests/test_chaos.py`` drives exactly these faults).
 
 Time comes from the injected clock (the reference calls ``time.Now()``,
 ``cron_controller.go:160``), which makes every path deterministic in tests.
@@ -59,7 +71,7 @@ from ..models.workload import (
     get_default_job_name,
     new_empty_workload,
 )
-from ..runtime import metrics
+from ..runtime import metrics, tracing
 from ..runtime.client import Client
 from ..runtime.controller import Reconciler, Request, Result
 from ..runtime.events import Normal, Warning, EventRecorder
@@ -99,6 +111,7 @@ class ReconcilerOptions:
     fold_created_into_active: bool = True    # add the just-created child to status.active right away
     skip_expected_events: bool = True        # child add/delete events we caused do not requeue the Cron
     classification_cache: bool = True
+    dedupe_ran_tick: bool = True
     workload: WorkloadPolicy = field(default_factory=WorkloadPolicy)
     static_owned_kinds: Tuple[GroupVersionKind, ...] = (
         GroupVersionKind("kubeflow.org", "v1", "PyTorchJob"),
@@ -110,7 +123,8 @@ class ReconcilerOptions:
         return ReconcilerOptions(list_mode="live", finished_time="now", skip_noop_patch=False,
                                  own_write_filter=False, dynamic_watches=False, expectations=False,
                                  fold_created_into_active=False, skip_expected_events=False,
-                                 classification_cache=False, workload=WorkloadPolicy.reference())
+                                 classification_cache=False, dedupe_ran_tick=False,
+                                 workload=WorkloadPolicy.reference())
 
 
 class Expectations:
@@ -275,7 +289,9 @@ class CronReconciler(Reconciler):
             # recorded before the call: the watch event can overtake the PATCH response
             self.own_writes[key] = (m.get("generation"), new_status)
         try:
-            await self.client.patch(CRON_GVR, m.get("namespace", ""), m.get("name", ""), patch, "merge", "status")
+            with tracing.span("patch_status", bytes=len(jsonutil.dumps(patch)) if tracing.get_tracer().enabled else 0):
+                await self.client.patch(CRON_GVR, m.get("namespace", ""), m.get("name", ""), patch, "merge",
+                                        "status")
         except Exception:
             self.own_writes.pop(key, None)
             raise
@@ -313,7 +329,9 @@ class CronReconciler(Reconciler):
 
         # B4 (cron_controller.go:129-133)
         try:
-            workloads = await self.list_workloads(cron, gvk, log)
+            with tracing.span("list_children", kind=gvk.kind, mode=self.opts.list_mode) as sp:
+                workloads = await self.list_workloads(cron, gvk, log)
+                sp.set(count=len(workloads))
         except Exception as e:
             log.error(e, f"Failed to list {gvk.kind}")
             raise
@@ -344,7 +362,8 @@ class CronReconciler(Reconciler):
         log.info(f"{gvk.kind} count", active=len(active), terminated=len(terminated))
 
         # B6/B7/B8 (cron_controller.go:155-158)
-        await self.sync_status(cron, gvk, active, terminated, log)
+        with tracing.span("sync_status", active=len(active), terminated=len(terminated)):
+            await self.sync_status(cron, gvk, active, terminated, log)
 
         now = self.clock.now(LOCAL)
 
@@ -380,6 +399,11 @@ class CronReconciler(Reconciler):
             return scheduled
         if log.enabled():
             log = log.with_values(**{"current run": missed_run.rfc3339()})
+
+        if self.opts.dedupe_ran_tick and self._tick_already_ran(cron, missed_run, active, terminated):
+            log.info(f"{gvk.kind} for this run already exists; recording it as scheduled")
+            cron.status.last_schedule_time = now
+            return scheduled
 
         # B15 (cron_controller.go:204-207)
         if cron.spec.concurrency_policy == ConcurrentPolicyForbid and active:
@@ -422,7 +446,10 @@ class CronReconciler(Reconciler):
         if self.opts.expectations:
             self.expect.expect_pending(self._ckey(cron), wm.get("name", ""))
         try:
-            created = await self.client.create(gvk, workload, wm.get("namespace", ""))
+            with tracing.span("create_workload", kind=gvk.kind, name=wm.get("name", ""),
+                              tick=missed_run.rfc3339()) as sp:
+                created = await self.client.create(gvk, workload, wm.get("namespace", ""))
+                sp.set(tick_to_create_ms=(self.clock.now_ns() - missed_run.unix_nano()) / 1e6)
             self.stats["creates"] += 1
             metrics.WORKLOADS_CREATED.labels(gvk.kind).inc()
             if self.opts.expectations:
@@ -449,6 +476,27 @@ class CronReconciler(Reconciler):
         # B20 (cron_controller.go:237)
         cron.status.last_schedule_time = now
         return scheduled
+
+    def _tick_already_ran(self, cron: Cron, missed_run: GoTime, active: List[Tuple[Dict[str, Any], Classification]],
+                          terminated: List[Tuple[Dict[str, Any], Classification]]) -> bool:
+        """Does a child named for ``missed_run``'s run exist?  Only for generated names: a
+        template with a fixed ``metadata.name`` reuses one name for every run."""
+        tmpl_meta = (cron.spec.template.workload or {}).get("metadata") if isinstance(
+            cron.spec.template.workload, dict) else None
+        if isinstance(tmpl_meta, dict) and tmpl_meta.get("name"):
+            return False
+        try:
+            ran_name = get_default_job_name(cron.name, self.engine.next(self.engine.parse(cron.spec.schedule),
+                                                                        missed_run))
+        except ScheduleError:
+            return False
+        for w, _ in active:
+            if (w.get("metadata") or {}).get("name") == ran_name:
+                return True
+        for w, _ in terminated:
+            if (w.get("metadata") or {}).get("name") == ran_name:
+                return True
+        return False
 
     # ------------------------------------------------------------------ children
     @staticmethod

@@ -23,7 +23,7 @@ from typing import Any, Dict, List, Optional, Tuple, Union
 from ..api import errors
 from ..api.meta import GroupVersion, GroupVersionKind, GroupVersionResource
 from ..utils import jsonutil
-from . import metrics
+from . import metrics, tracing
 from .ratelimit import TokenBucket, make_client_limiter
 
 GVRorGVK = Union[GroupVersionResource, GroupVersionKind]
@@ -106,8 +106,16 @@ class InMemoryTransport(Transport):
     async def request(self, verb: str, gvr: GroupVersionResource, namespace: str = "", name: str = "",
                       subresource: str = "", body: Any = None, params: Optional[Dict[str, Any]] = None) -> Any:
         params = params or {}
-        s = self.server
         await self._gate(verb, gvr.resource, subresource, name)
+        out = self._apply(verb, gvr, namespace, name, subresource, body, params)
+        faults = self.server.faults
+        if faults.faults:
+            faults.check(verb, gvr.resource, subresource or None, name or None, after=True)
+        return out
+
+    def _apply(self, verb: str, gvr: GroupVersionResource, namespace: str, name: str, subresource: str, body: Any,
+               params: Dict[str, Any]) -> Any:
+        s = self.server
         if verb == "get":
             return s.get(gvr, namespace, name)
         if verb == "list":
@@ -242,10 +250,14 @@ class Client:
         self.requests_by_verb[verb] = self.requests_by_verb.get(verb, 0) + 1
         t0 = time.perf_counter()
         code = "200"
+        sp = tracing.span("http." + verb, resource=gvr.resource + ("/" + subresource if subresource else ""),
+                          namespace=namespace, name=name)
         try:
-            return await self.transport.request(verb, gvr, namespace, name, subresource, body, params)
+            with sp:
+                return await self.transport.request(verb, gvr, namespace, name, subresource, body, params)
         except errors.ApiError as e:
             code = str(e.code)
+            sp.set(code=e.code)
             raise
         except Exception:
             code = "<error>"

@@ -29,7 +29,7 @@ from ..api.meta import GroupVersionKind, NamespacedName, controller_ref
 from ..parallel.workqueue import ShutDown, WorkQueue
 from ..utils.clock import Clock
 from ..utils.logging import Logger, get_logger, log_constructor
-from . import metrics
+from . import metrics, tracing
 from .informer import EventHandler, Informer
 
 Request = NamespacedName
@@ -181,9 +181,11 @@ class Controller:
         result: Optional[Result] = None
         err: Optional[BaseException] = None
         try:
-            result = await self.reconciler.reconcile(req, log)
-            if result is None:
-                result = Result()
+            with tracing.span("reconcile", controller=self.name, namespace=req.namespace, name=req.name) as sp:
+                result = await self.reconciler.reconcile(req, log)
+                if result is None:
+                    result = Result()
+                sp.set(requeue_after_ms=result.after_ns() / 1e6)
         except asyncio.CancelledError:
             raise
         except Exception as e:  # noqa: BLE001 - recover like RecoverPanic

@@ -3,7 +3,8 @@
 * Probes: ``/healthz`` and ``/readyz`` (plus ``/healthz/<check>``), answered from
   registered checks like controller-runtime's ``healthz.Ping``
   (``cmd/operator/start.go:195-203``; probed on :8081 by the chart,
-  ``charts/cron-operator/templates/deployment.yaml:74-83``).
+  ``charts/cron-operator/templates/deployment.yaml:74-83``).  The same port serves
+  ``/debug/traces`` (Chrome trace JSON of recent reconciles) when tracing is on.
 * Metrics: ``/metrics`` in Prometheus text format.  ``--metrics-secure`` (default
   true, ``start.go:226``) serves HTTPS and guards the endpoint with the
   authn/authz filter: the bearer token is checked with a TokenReview and the
@@ -94,6 +95,18 @@ class ProbeServer:
         app.router.add_get("/healthz/{check}", handler(self.healthz, "healthz"))
         app.router.add_get("/readyz", handler(self.readyz, "readyz"))
         app.router.add_get("/readyz/{check}", handler(self.readyz, "readyz"))
+
+        async def traces(req: web.Request) -> web.Response:
+            from . import tracing
+
+            t = tracing.get_tracer()
+            if not t.enabled:
+                return web.Response(status=404, text="tracing disabled (start with --enable-tracing)\n")
+            if req.query.get("format") == "spans":
+                return web.json_response({"spans": t.spans()})
+            return web.json_response(t.chrome_trace())
+
+        app.router.add_get("/debug/traces", traces)
         return app
 
     async def start(self) -> None:

@@ -1,0 +1,141 @@
+"""Fault injection: the operator converges under API errors, lost responses and
+dropped watches, and never breaks its scheduling invariants.
+
+The reference has no fault-injection tests ("no fault
+injection", "no Replace, history-GC, deadline, Forbid-with-active ... tests").
+Here a mixed fleet of Allow / Forbid / Replace Crons runs for several virtual
+minutes while the fake apiserver
+
+* fails ~20% of every verb the operator uses (500s before the write),
+* *applies* ~15% of CREATEs and DELETEs and then fails them anyway (a lost
+  response -- the case deterministic job names exist for,
+  ``cron_controller.go:229-231``),
+* drops every watch stream once per minute (informers must relist),
+
+and the training-operator side finishes jobs half a minute after they start.
+Checked at every step: a Forbid Cron never has two unfinished jobs; no tick is
+ever run twice. After the faults stop: every Cron converges -- status matches
+the cluster, GC has trimmed finished jobs to ``historyLimit``, the last tick ran.
+"""
+from __future__ import annotations
+
+import random
+
+import pytest
+
+from cron_operator_amd.api.meta import GroupVersionResource
+from cron_operator_amd.api.v1alpha1 import CRON_GVR, LABEL_CRON_NAME, new_cron
+from cron_operator_amd.controller.reconciler import ReconcilerOptions
+from cron_operator_amd.testing.env import TestEnv
+from cron_operator_amd.trainingop.operator import finished_status
+from cron_operator_amd.utils.gotime import NANOS, UTC, GoTime
+
+PT = GroupVersionResource("kubeflow.org", "v1", "pytorchjobs")
+NS = "default"
+TMPL = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+        "spec": {"pytorchReplicaSpecs": {"Master": {"replicas": 1}}}}
+POLICIES = ["Allow", "Forbid", "Replace"]
+HISTORY = 2
+
+
+def jobs_of(env, cron):
+    return env.server.list(PT, NS, label_selector=f"{LABEL_CRON_NAME}={cron}")["items"]
+
+
+def finished(job):
+    return any(c.get("type") in ("Succeeded", "Failed") and c.get("status") == "True"
+               for c in (job.get("status") or {}).get("conditions") or [])
+
+
+def inject(env, seed):
+    f = env.server.faults
+    f._rng = random.Random(seed)
+    for verb, res, sub in (("patch", "crons", "status"), ("create", "pytorchjobs", None),
+                           ("delete", "pytorchjobs", None), ("list", "pytorchjobs", None),
+                           ("list", "crons", None), ("create", "events", None)):
+        f.add(verb=verb, resource=res, subresource=sub, code=500, probability=0.2)
+    f.add(verb="create", resource="pytorchjobs", code=504, reason="Timeout", probability=0.15, after=True)
+    f.add(verb="delete", resource="pytorchjobs", code=504, reason="Timeout", probability=0.15, after=True)
+
+
+def complete_running(env, now_ns):
+    ts = GoTime(now_ns // NANOS, 0, UTC).rfc3339()
+    for j in env.server.list(PT, NS)["items"]:
+        if not finished(j):
+            env.server.patch(PT, NS, j["metadata"]["name"], {"status": finished_status("PyTorchJob",
+                                                                                       j["metadata"]["name"], ts,
+                                                                                       True)},
+                             "merge", "status")
+
+
+def check_invariants(env, crons, seen, once=True):
+    for name, policy in crons.items():
+        jobs = jobs_of(env, name)
+        running = [j for j in jobs if not finished(j)]
+        if policy == "Forbid":
+            assert len(running) <= 1, f"{name}: Forbid with {len(running)} running jobs"
+        if not once:
+            continue
+        for j in jobs:
+            uid, jname = j["metadata"]["uid"], j["metadata"]["name"]
+            prev = seen.setdefault(jname, uid)
+            # a tick's job is created once: the same name never reappears as a new object
+            assert prev == uid, f"{jname} was created twice"
+
+
+@pytest.mark.parametrize("mode", ["optimized", "reference"])
+@pytest.mark.timeout(300)
+async def test_converges_under_faults(mode):
+    opts = ReconcilerOptions() if mode == "optimized" else ReconcilerOptions.reference()
+    env = TestEnv(gc=True)
+    crons = {}
+    for i in range(18):
+        policy = POLICIES[i % 3]
+        name = f"chaos-{policy.lower()}-{i}"
+        crons[name] = policy
+        await env.create_cron(new_cron(name, NS, "*/1 * * * *", TMPL, concurrency_policy=policy,
+                                       history_limit=HISTORY))
+    await env.start_manager(opts, max_concurrent=8)
+    await env.settle()
+    inject(env, seed=11 if mode == "optimized" else 12)
+    seen = {}
+    minutes = 6
+    for minute in range(minutes):
+        for sec in range(60):
+            env.clock.advance(1)
+            if sec == 30:
+                complete_running(env, env.clock.now_ns())
+            if sec == 45:
+                env.server.close_all_watches()  # every informer must relist and resume
+            await env.settle(timeout=60)
+            if sec % 10 == 0:
+                check_invariants(env, crons, seen, once=mode == "optimized")
+    # faults stop: everything must converge within a couple of minutes of backoff
+    env.server.faults.clear()
+    for _ in range(180):
+        env.clock.advance(1)
+        await env.settle(timeout=60)
+    complete_running(env, env.clock.now_ns())
+    for _ in range(30):
+        env.clock.advance(1)
+        await env.settle(timeout=60)
+    check_invariants(env, crons, seen, once=mode == "optimized")
+
+    last_tick = GoTime((env.clock.now_ns() // NANOS) // 60 * 60, 0, UTC)
+    for name, policy in crons.items():
+        st = env.server.get(CRON_GVR, NS, name).get("status") or {}
+        jobs = jobs_of(env, name)
+        done = [j for j in jobs if finished(j)]
+        running = [j for j in jobs if not finished(j)]
+        assert st.get("lastScheduleTime"), name
+        # the most recent tick ran (reference B20 stamps wall time, so compare at minute granularity)
+        ls = st["lastScheduleTime"]
+        assert ls[:16] == last_tick.rfc3339()[:16], (name, ls, last_tick.rfc3339())
+        assert len(done) <= HISTORY, f"{name}: GC left {len(done)} finished jobs"
+        assert sorted(a["name"] for a in st.get("active") or []) == sorted(j["metadata"]["name"] for j in running)
+        assert sorted(h["object"]["name"] for h in st.get("history") or []) == \
+            sorted(j["metadata"]["name"] for j in done)
+        names = [j["metadata"]["name"] for j in jobs]
+        assert len(names) == len(set(names))
+    assert env.controller.errors > 0  # the faults really hit the operator
+    await env.stop()
