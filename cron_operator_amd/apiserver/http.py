@@ -1,4 +1,4 @@
-"""Serve the fake :class:`APIServer` over the Kubernetes REST protocol (aiohttp).
+"""Serve the fake :class:`APIServer` over the Kubernetes REST protocol.
 
 Paths follow kube-apiserver: ``/api/v1/...`` for the core group and
 ``/apis/<group>/<version>/...`` otherwise, with ``namespaces/<ns>/`` scoping,
@@ -6,29 +6,35 @@ Paths follow kube-apiserver: ``/api/v1/...`` for the core group and
 ``/apis/<g>/<v>``), ``/version`` and ``/healthz``.  LIST/WATCH take
 ``labelSelector``, ``fieldSelector``, ``resourceVersion``, ``limit``,
 ``continue``, ``allowWatchBookmarks`` and ``timeoutSeconds``; watches stream
-newline-delimited JSON events.  PATCH honours the content type
+newline-delimited JSON events (chunked).  PATCH honours the content type
 (merge / json / strategic); DELETE reads ``DeleteOptions`` from the body or
 ``propagationPolicy`` from the query.  Errors are ``metav1.Status`` bodies.
 
-Optional bearer-token authentication (``tokens``) mirrors what the metrics
-authn/authz filter needs.  ``/debug/fake/*`` endpoints expose test controls
-(clock, request stats, faults, bulk job completion) to out-of-process drivers
-such as the benchmark.
+Optional bearer-token authentication (``tokens``) and RBAC authorization
+(``APIServer(authorization="RBAC")``).  ``/debug/fake/*`` endpoints expose test
+controls (clock, request stats, faults, bulk job completion) to out-of-process
+drivers such as the benchmark.
+
+The HTTP/1.1 front end is a small ``asyncio.Protocol`` server (keep-alive,
+pipelining, ``Content-Length`` and chunked request bodies, ``Expect:
+100-continue``, optional TLS).  It replaced aiohttp's web stack because in the
+1000-Cron benchmark the apiserver process sits on the critical path and
+aiohttp's per-request machinery was a third of its CPU; request handling is
+synchronous except for watches and injected latency.
 """
 from __future__ import annotations
 
 import asyncio
 import json
 import time
-from typing import Any, Dict, List, Optional, Tuple
-
-from aiohttp import web
+from typing import Any, Dict, List, Optional, Tuple, Union
+from urllib.parse import parse_qsl, unquote
 
 from ..api import errors
 from ..api.meta import GroupVersionResource
 from ..utils import jsonutil
 from ..utils.clock import FakeClock
-from .server import APIServer
+from .server import APIServer, Watcher
 
 PATCH_TYPES = {
     "application/merge-patch+json": "merge",
@@ -36,6 +42,12 @@ PATCH_TYPES = {
     "application/strategic-merge-patch+json": "strategic",
     "application/apply-patch+yaml": "apply",
 }
+_REASONS = {200: "OK", 201: "Created", 202: "Accepted", 204: "No Content", 400: "Bad Request",
+            401: "Unauthorized", 403: "Forbidden", 404: "Not Found", 405: "Method Not Allowed", 409: "Conflict",
+            410: "Gone", 413: "Payload Too Large", 415: "Unsupported Media Type", 422: "Unprocessable Entity",
+            429: "Too Many Requests", 431: "Request Header Fields Too Large", 500: "Internal Server Error",
+            503: "Service Unavailable", 504: "Gateway Timeout"}
+MAX_BODY = 64 * 1024 * 1024
 
 
 class _EncodeCache:
@@ -60,19 +72,56 @@ class _EncodeCache:
 _ENC = _EncodeCache()
 
 
-def _json(data: Any, status: int = 200) -> web.Response:
-    return web.Response(body=_ENC.encode(data) if status < 300 else jsonutil.dumpb(data), status=status,
-                        content_type="application/json")
+class Request:
+    """What a handler sees: method, decoded path, query (first value per key),
+    lower-cased headers, the raw body and the authenticated user."""
+
+    __slots__ = ("method", "path", "query", "headers", "body", "user")
+
+    def __init__(self, method: str, path: str, query: Dict[str, str], headers: Dict[str, str], body: bytes):
+        self.method = method
+        self.path = path
+        self.query = query
+        self.headers = headers
+        self.body = body
+        self.user: Optional[Dict[str, Any]] = None
+
+    @property
+    def content_type(self) -> str:
+        return self.headers.get("content-type", "").split(";", 1)[0].strip().lower()
+
+
+class Response:
+    __slots__ = ("status", "body", "content_type")
+
+    def __init__(self, status: int, body: bytes, content_type: str = "application/json"):
+        self.status = status
+        self.body = body
+        self.content_type = content_type
+
+
+class WatchResponse:
+    """A streaming response: newline-delimited watch events until timeout/stop."""
+
+    __slots__ = ("watcher", "timeout")
+
+    def __init__(self, watcher: Watcher, timeout: float):
+        self.watcher = watcher
+        self.timeout = timeout
+
+
+Reply = Union[Response, WatchResponse]
+
+
+def _json(data: Any, status: int = 200) -> Response:
+    return Response(status, _ENC.encode(data) if status < 300 else jsonutil.dumpb(data))
 
 
 def _event_line(etype: str, obj: Any) -> bytes:
     return b'{"type":"' + etype.encode() + b'","object":' + _ENC.encode(obj) + b"}"
 
 
-_USER = web.RequestKey("user", dict) if hasattr(web, "RequestKey") else "user"
-
-
-def _err(e: errors.ApiError) -> web.Response:
+def _err(e: errors.ApiError) -> Response:
     return _json(e.status(), e.code)
 
 
@@ -80,9 +129,11 @@ class APIServerApp:
     def __init__(self, server: APIServer, request_log: bool = False):
         self.server = server
         self.request_log = request_log
-        self._runner: Optional[web.AppRunner] = None
         self.port: Optional[int] = None
-        self._streams: List[Any] = []
+        self._srv: Optional[asyncio.AbstractServer] = None
+        self._conns: "set[_ServerConn]" = set()
+        self._streams: List[Watcher] = []
+        self.requests = 0
 
     # ------------------------------------------------------------------ discovery
     def _core_list(self) -> Dict[str, Any]:
@@ -110,20 +161,20 @@ class APIServerApp:
                 "resources": res}
 
     # ------------------------------------------------------------------ auth
-    def _authenticate(self, req: web.Request) -> Optional[web.Response]:
+    def _authenticate(self, req: Request) -> Optional[Response]:
         if self.server.tokens is None:
             return None
-        auth = req.headers.get("Authorization", "")
+        auth = req.headers.get("authorization", "")
         token = auth[7:].strip() if auth.startswith("Bearer ") else ""
         user = self.server.tokens.get(token)
         if user is None:
             return _json(errors.ApiError(401, "Unauthorized", "Unauthorized").status(), 401)
-        req[_USER] = user
+        req.user = user
         return None
 
-    def _authorize(self, req: web.Request, attrs: Dict[str, Any]) -> None:
+    def _authorize(self, req: Request, attrs: Dict[str, Any]) -> None:
         rbac = self.server.rbac
-        user = req.get(_USER)
+        user = req.user
         if rbac is None or user is None:
             return
         if not rbac.authorize(user.get("username", ""), user.get("groups") or [], attrs):
@@ -161,13 +212,16 @@ class APIServerApp:
             return None
         return GroupVersionResource(group, version, resource), ns, name, sub, namespaced
 
-    async def handle(self, req: web.Request) -> web.StreamResponse:
+    def dispatch(self, req: Request) -> Union[Reply, "asyncio.Future[Reply]"]:
+        """Handle one request: a reply, or an awaitable one when the verb must wait
+        (injected latency)."""
+        self.requests += 1
         denied = self._authenticate(req)
         if denied is not None:
             return denied
         path = req.path
         if path in ("/healthz", "/readyz", "/livez"):
-            return web.Response(text="ok")
+            return Response(200, b"ok", "text/plain")
         if path == "/version":
             return _json({"major": "1", "minor": "34", "gitVersion": "v1.34.0-cron-operator-amd-fake",
                           "platform": "linux/amd64"})
@@ -177,46 +231,39 @@ class APIServerApp:
             return _json(self._core_list())
         if path == "/apis":
             return _json(self._groups())
-        if path.startswith("/debug/fake/"):
-            return await self._debug(req)
-        if self.server.rbac is not None and req.get(_USER) is not None and not path.startswith(("/api/", "/apis/")):
-            try:
-                self._authorize(req, {"verb": req.method.lower(), "path": path})
-            except errors.ApiError as e:
-                return _err(e)
-        parts = [p for p in path.split("/") if p]
-        if len(parts) == 3 and parts[0] == "apis":
-            gv = self._group_version(parts[1], parts[2])
-            if gv is None:
-                return _err(errors.ApiError(404, "NotFound", "the server could not find the requested resource"))
-            return _json(gv)
-        parsed = self._parse(path)
-        if parsed is None:
-            return _err(errors.ApiError(404, "NotFound", "the server could not find the requested resource"))
-        gvr, ns, name, sub, _ = parsed
         try:
-            return await self._resource(req, gvr, ns, name, sub)
+            if path.startswith("/debug/fake/"):
+                return self._debug(req)
+            if self.server.rbac is not None and req.user is not None and not path.startswith(("/api/", "/apis/")):
+                self._authorize(req, {"verb": req.method.lower(), "path": path})
+            parts = [p for p in path.split("/") if p]
+            if len(parts) == 3 and parts[0] == "apis":
+                gv = self._group_version(parts[1], parts[2])
+                if gv is None:
+                    return _err(errors.ApiError(404, "NotFound", "the server could not find the requested resource"))
+                return _json(gv)
+            parsed = self._parse(path)
+            if parsed is None:
+                return _err(errors.ApiError(404, "NotFound", "the server could not find the requested resource"))
+            gvr, ns, name, sub, _ = parsed
+            return self._resource(req, gvr, ns, name, sub)
         except errors.ApiError as e:
             return _err(e)
         except (ValueError, KeyError, TypeError) as e:
             return _err(errors.bad_request(str(e)))
 
-    async def _body(self, req: web.Request) -> Any:
-        raw = await req.read()
+    @staticmethod
+    def _body(req: Request) -> Any:
+        raw = req.body
         if not raw:
             return None
         try:
-            return json.loads(raw)
+            return jsonutil.loads(raw)
         except ValueError as e:
             raise errors.bad_request(f"invalid JSON body: {e}") from None
 
-    async def _delay(self, verb: str) -> None:
-        d = self.server.faults.delay_for(verb) if self.server.faults.latency else 0.0
-        if d > 0:
-            await asyncio.sleep(d)
-
-    async def _resource(self, req: web.Request, gvr: GroupVersionResource, ns: str, name: str,
-                        sub: str) -> web.StreamResponse:
+    def _resource(self, req: Request, gvr: GroupVersionResource, ns: str, name: str,
+                  sub: str) -> Union[Reply, "asyncio.Future[Reply]"]:
         s = self.server
         q = req.query
         m = req.method
@@ -231,11 +278,30 @@ class APIServerApp:
         if s.rbac is not None:
             self._authorize(req, {"verb": verb, "group": gvr.group, "resource": gvr.resource, "subresource": sub,
                                   "namespace": ns, "name": name})
-        await self._delay(verb)
+        delay = s.faults.delay_for(verb) if s.faults.latency else 0.0
+        if delay > 0:
+            return asyncio.ensure_future(self._delayed(delay, req, gvr, ns, name, sub, verb))
+        return self._verb(req, gvr, ns, name, sub, verb)
+
+    async def _delayed(self, delay: float, req: Request, gvr: GroupVersionResource, ns: str, name: str, sub: str,
+                       verb: str) -> Reply:
+        await asyncio.sleep(delay)
+        try:
+            return self._verb(req, gvr, ns, name, sub, verb)
+        except errors.ApiError as e:
+            return _err(e)
+        except (ValueError, KeyError, TypeError) as e:
+            return _err(errors.bad_request(str(e)))
+
+    def _verb(self, req: Request, gvr: GroupVersionResource, ns: str, name: str, sub: str, verb: str) -> Reply:
+        s = self.server
+        q = req.query
         if s.faults.faults:
             s.faults.check(verb, gvr.resource, sub or None, name or None)
         if verb == "watch":
-            return await self._watch(req, gvr, ns)
+            w = s.watch(gvr, ns or None, q.get("resourceVersion", ""), q.get("labelSelector"), q.get("fieldSelector"),
+                        q.get("allowWatchBookmarks") in ("true", "1"), copy_events=False)
+            return WatchResponse(w, float(q.get("timeoutSeconds") or 1800))
         body: Any = None
         ptype = "merge"
         if verb in ("create", "update", "patch", "delete"):
@@ -246,7 +312,7 @@ class APIServerApp:
                     raise errors.ApiError(415, "UnsupportedMediaType", "the body of the request was in an unknown "
                                                                        f"format - accepted media types include: "
                                                                        f"{accepted}")
-            body = await self._body(req)
+            body = self._body(req)
             if verb in ("create", "update") and not isinstance(body, dict):
                 raise errors.bad_request("request body must be a JSON object")
         # The verb runs synchronously and its result is serialised right here, so the
@@ -261,7 +327,7 @@ class APIServerApp:
         return resp
 
     def _apply(self, verb: str, gvr: GroupVersionResource, ns: str, name: str, sub: str, body: Any, ptype: Any,
-               q: Any) -> web.Response:
+               q: Dict[str, str]) -> Response:
         s = self.server
         if verb == "list":
             return _json(s.list(gvr, ns or None, q.get("labelSelector"), q.get("fieldSelector"),
@@ -281,49 +347,8 @@ class APIServerApp:
         n = s.delete_collection(gvr, ns or None, q.get("labelSelector"))
         return _json({"kind": "Status", "apiVersion": "v1", "status": "Success", "details": {"deleted": n}})
 
-    async def _watch(self, req: web.Request, gvr: GroupVersionResource, ns: str) -> web.StreamResponse:
-        q = req.query
-        w = self.server.watch(gvr, ns or None, q.get("resourceVersion", ""), q.get("labelSelector"),
-                              q.get("fieldSelector"), q.get("allowWatchBookmarks") in ("true", "1"),
-                              copy_events=False)
-        resp = web.StreamResponse(status=200, headers={"Content-Type": "application/json",
-                                                       "Transfer-Encoding": "chunked"})
-        await resp.prepare(req)
-        timeout = float(q.get("timeoutSeconds") or 1800)
-        deadline = time.monotonic() + timeout
-        self._streams.append(w)
-        try:
-            while True:
-                remaining = deadline - time.monotonic()
-                if remaining <= 0:
-                    break
-                try:
-                    ev = await asyncio.wait_for(w.queue.get(), remaining)
-                except asyncio.TimeoutError:
-                    break
-                if ev is None:
-                    break
-                buf = [_event_line(ev[0], ev[1])]
-                # coalesce whatever is already queued into one write
-                while not w.queue.empty() and len(buf) < 512:
-                    nxt = w.queue.get_nowait()
-                    if nxt is None:
-                        w.closed = True
-                        break
-                    buf.append(_event_line(nxt[0], nxt[1]))
-                await resp.write(b"\n".join(buf) + b"\n")
-                if w.closed:
-                    break
-        except (ConnectionResetError, asyncio.CancelledError):
-            pass
-        finally:
-            w.stop()
-            if w in self._streams:
-                self._streams.remove(w)
-        return resp
-
     # ------------------------------------------------------------------ debug / test controls
-    async def _debug(self, req: web.Request) -> web.Response:
+    def _debug(self, req: Request) -> Response:
         s = self.server
         what = req.path[len("/debug/fake/"):]
         if what == "stats":
@@ -332,13 +357,13 @@ class APIServerApp:
             return _json(snap)
         if what == "clock":
             if req.method == "POST":
-                body = await self._body(req) or {}
+                body = self._body(req) or {}
                 if not isinstance(s.clock, FakeClock):
                     raise errors.bad_request("server clock is not settable")
                 s.clock.set(int(body["nowNs"]))
             return _json({"nowNs": s.clock.now_ns()})
         if what == "faults" and req.method == "POST":
-            body = await self._body(req) or {}
+            body = self._body(req) or {}
             if body.get("clear"):
                 s.faults.clear()
             for f in body.get("faults") or []:
@@ -348,7 +373,7 @@ class APIServerApp:
             return _json({"faults": len(s.faults.faults)})
         if what == "complete" and req.method == "POST":
             # bench helper: mark every job (of the given resource) without completionTime as finished
-            body = await self._body(req) or {}
+            body = self._body(req) or {}
             from ..trainingop.operator import finished_status
 
             gvr = GroupVersionResource(body.get("group", "kubeflow.org"), body.get("version", "v1"),
@@ -371,23 +396,211 @@ class APIServerApp:
         return _err(errors.ApiError(404, "NotFound", f"unknown debug endpoint {what}"))
 
     # ------------------------------------------------------------------ lifecycle
-    def app(self) -> web.Application:
-        app = web.Application(client_max_size=64 * 1024 * 1024)
-        app.router.add_route("*", "/{tail:.*}", self.handle)
-        return app
-
     async def start(self, host: str = "127.0.0.1", port: int = 0, ssl_context=None) -> int:
-        self._runner = web.AppRunner(self.app(), access_log=None, handle_signals=False)
-        await self._runner.setup()
-        site = web.TCPSite(self._runner, host, port, ssl_context=ssl_context, backlog=1024)
-        await site.start()
-        server = getattr(site, "_server", None)
-        self.port = server.sockets[0].getsockname()[1] if server is not None else port
+        loop = asyncio.get_running_loop()
+        self._srv = await loop.create_server(lambda: _ServerConn(self), host, port, ssl=ssl_context, backlog=1024)
+        self.port = self._srv.sockets[0].getsockname()[1]
         return self.port
 
     async def stop(self) -> None:
         for w in list(self._streams):
             w.stop()
-        if self._runner is not None:
-            await self._runner.cleanup()
-            self._runner = None
+        if self._srv is not None:
+            self._srv.close()
+            for c in list(self._conns):
+                c.close()
+            try:
+                await asyncio.wait_for(self._srv.wait_closed(), 5)
+            except asyncio.TimeoutError:
+                pass
+            self._srv = None
+
+
+class _ServerConn(asyncio.Protocol):
+    """One client connection: parse requests, dispatch in order, write replies."""
+
+    def __init__(self, app: APIServerApp):
+        self.app = app
+        self.transport: Optional[asyncio.Transport] = None
+        self.buf = bytearray()
+        self.busy = False               # a reply (watch / delayed) is pending; later requests wait
+        self.closed = False
+        self._continued = False         # "100 Continue" already sent for the pending request
+        self._watch_task: Optional[asyncio.Task] = None
+
+    def connection_made(self, transport: asyncio.BaseTransport) -> None:
+        self.transport = transport  # type: ignore[assignment]
+        self.app._conns.add(self)
+
+    def connection_lost(self, exc: Optional[BaseException]) -> None:
+        self.closed = True
+        self.app._conns.discard(self)
+        if self._watch_task is not None:
+            self._watch_task.cancel()
+
+    def close(self) -> None:
+        if self.transport is not None and not self.closed:
+            self.transport.close()
+
+    def data_received(self, data: bytes) -> None:
+        self.buf += data
+        if not self.busy:
+            self._drain()
+
+    # --------------------------------------------------------------- parsing
+    def _next_request(self) -> Optional[Tuple[Request, bool]]:
+        buf = self.buf
+        end = buf.find(b"\r\n\r\n")
+        if end < 0:
+            if len(buf) > 1 << 20:
+                self._reply_raw(431, b"request header too large", "text/plain", close=True)
+            return None
+        head = bytes(buf[:end]).decode("latin-1")
+        lines = head.split("\r\n")
+        try:
+            method, target, version = lines[0].split(" ", 2)
+        except ValueError:
+            self._reply_raw(400, b"bad request line", "text/plain", close=True)
+            return None
+        headers: Dict[str, str] = {}
+        for line in lines[1:]:
+            k, _, v = line.partition(":")
+            headers[k.strip().lower()] = v.strip()
+        pos = end + 4
+        te = headers.get("transfer-encoding", "").lower()
+        if "chunked" in te:
+            body = bytearray()
+            while True:
+                nl = buf.find(b"\r\n", pos)
+                if nl < 0:
+                    return None
+                size = int(bytes(buf[pos:nl]).split(b";", 1)[0], 16)
+                if size == 0:
+                    tend = buf.find(b"\r\n\r\n", nl)
+                    if tend < 0:
+                        return None
+                    pos = tend + 4
+                    break
+                if len(buf) < nl + 2 + size + 2:
+                    return None
+                body += buf[nl + 2:nl + 2 + size]
+                pos = nl + 2 + size + 2
+            raw = bytes(body)
+        else:
+            clen = int(headers.get("content-length") or 0)
+            if clen > MAX_BODY:
+                self._reply_raw(413, b"request body too large", "text/plain", close=True)
+                return None
+            if len(buf) < pos + clen:
+                if headers.get("expect", "").lower() == "100-continue" and not self._continued:
+                    self._continued = True
+                    assert self.transport is not None
+                    self.transport.write(b"HTTP/1.1 100 Continue\r\n\r\n")
+                return None
+            raw = bytes(buf[pos:pos + clen])
+            pos += clen
+        del buf[:pos]
+        self._continued = False
+        path, _, qs = target.partition("?")
+        query: Dict[str, str] = {}
+        if qs:
+            for k, v in parse_qsl(qs, keep_blank_values=True):
+                query.setdefault(k, v)
+        conn_hdr = headers.get("connection", "").lower()
+        keep = (conn_hdr != "close") if version == "HTTP/1.1" else (conn_hdr == "keep-alive")
+        return Request(method.upper(), unquote(path), query, headers, raw), keep
+
+    def _drain(self) -> None:
+        while not self.busy and not self.closed:
+            nxt = self._next_request()
+            if nxt is None:
+                return
+            req, keep = nxt
+            try:
+                reply = self.app.dispatch(req)
+            except Exception as e:  # noqa: BLE001 - never kill the connection on a handler bug
+                reply = _err(errors.ApiError(500, "InternalError", f"{type(e).__name__}: {e}"))
+            if isinstance(reply, Response):
+                self._reply(reply, keep)
+                continue
+            self.busy = True
+            if isinstance(reply, WatchResponse):
+                self._watch_task = asyncio.ensure_future(self._stream(reply, keep))
+            else:
+                reply.add_done_callback(lambda f, keep=keep: self._delayed_done(f, keep))
+
+    def _delayed_done(self, fut: "asyncio.Future[Reply]", keep: bool) -> None:
+        self.busy = False
+        if self.closed:
+            return
+        try:
+            reply = fut.result()
+        except Exception as e:  # noqa: BLE001
+            reply = _err(errors.ApiError(500, "InternalError", str(e)))
+        if isinstance(reply, WatchResponse):
+            self.busy = True
+            self._watch_task = asyncio.ensure_future(self._stream(reply, keep))
+            return
+        self._reply(reply, keep)
+        self._drain()
+
+    # --------------------------------------------------------------- replies
+    def _reply(self, r: Response, keep: bool) -> None:
+        self._reply_raw(r.status, r.body, r.content_type, close=not keep)
+
+    def _reply_raw(self, status: int, body: bytes, ctype: str, close: bool = False) -> None:
+        if self.transport is None or self.closed:
+            return
+        head = (f"HTTP/1.1 {status} {_REASONS.get(status, 'Unknown')}\r\nContent-Type: {ctype}\r\n"
+                f"Content-Length: {len(body)}\r\n" + ("Connection: close\r\n" if close else "") + "\r\n")
+        self.transport.write(head.encode("latin-1") + body)
+        if close:
+            self.transport.close()
+            self.closed = True
+
+    async def _stream(self, wr: WatchResponse, keep: bool) -> None:
+        w = wr.watcher
+        app = self.app
+        app._streams.append(w)
+        t = self.transport
+        assert t is not None
+        t.write(b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nTransfer-Encoding: chunked\r\n\r\n")
+        deadline = time.monotonic() + wr.timeout
+        try:
+            while not self.closed:
+                remaining = deadline - time.monotonic()
+                if remaining <= 0:
+                    break
+                try:
+                    ev = await asyncio.wait_for(w.queue.get(), remaining)
+                except asyncio.TimeoutError:
+                    break
+                if ev is None:
+                    break
+                buf = [_event_line(ev[0], ev[1])]
+                # coalesce whatever is already queued into one chunk
+                while not w.queue.empty() and len(buf) < 512:
+                    nxt = w.queue.get_nowait()
+                    if nxt is None:
+                        w.closed = True
+                        break
+                    buf.append(_event_line(nxt[0], nxt[1]))
+                chunk = b"\n".join(buf) + b"\n"
+                t.write(b"%x\r\n" % len(chunk) + chunk + b"\r\n")
+                if w.closed:
+                    break
+        except asyncio.CancelledError:
+            pass
+        finally:
+            w.stop()
+            if w in app._streams:
+                app._streams.remove(w)
+        if not self.closed:
+            t.write(b"0\r\n\r\n")
+            if not keep:
+                t.close()
+                self.closed = True
+                return
+            self.busy = False
+            self._watch_task = None
+            self._drain()

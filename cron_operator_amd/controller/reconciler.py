@@ -291,7 +291,7 @@ class CronReconciler(Reconciler):
         try:
             with tracing.span("patch_status", bytes=len(jsonutil.dumps(patch)) if tracing.get_tracer().enabled else 0):
                 await self.client.patch(CRON_GVR, m.get("namespace", ""), m.get("name", ""), patch, "merge",
-                                        "status")
+                                        "status", discard_response=True)
         except Exception:
             self.own_writes.pop(key, None)
             raise
@@ -421,7 +421,7 @@ class CronReconciler(Reconciler):
                     self.expect.expect_delete(self._ckey(cron), uid)
                 try:
                     await self.client.delete(gvk, m.get("namespace", ""), m.get("name", ""),
-                                             propagation_policy="Background")
+                                             propagation_policy="Background", discard_response=True)
                     self.stats["deletes"] += 1
                     metrics.WORKLOADS_DELETED.labels(gvk.kind, "replace").inc()
                 except errors.ApiError as e:
@@ -586,7 +586,7 @@ class CronReconciler(Reconciler):
                     self.expect.expect_delete(self._ckey(cron), uid)
                 try:
                     await self.client.delete(wgvk, m.get("namespace", ""), m.get("name", ""),
-                                             propagation_policy="Background")
+                                             propagation_policy="Background", discard_response=True)
                     self.stats["deletes"] += 1
                     metrics.WORKLOADS_DELETED.labels(wgvk.kind, "history").inc()
                 except errors.ApiError as e:

@@ -39,6 +39,10 @@ PATCH_CONTENT_TYPES = {
 }
 
 
+# request-parameter key (never sent): the caller ignores the response body
+DISCARD = "_discardResponse"
+
+
 class Transport:
     host = "in-memory"
 
@@ -323,18 +327,24 @@ class Client:
                               subresource, body=obj)
 
     async def patch(self, target: GVRorGVK, namespace: str, name: str, patch: Any, patch_type: str = MERGE,
-                    subresource: str = "") -> Dict[str, Any]:
+                    subresource: str = "", discard_response: bool = False) -> Dict[str, Any]:
+        """``discard_response``: the caller does not read the result, so an HTTP transport
+        need not decode the returned object (it is still received, and errors still raise)."""
+        params: Dict[str, Any] = {"patchType": patch_type}
+        if discard_response:
+            params[DISCARD] = True
         return await self._do("patch", await self._gvr(target), namespace, name, subresource, body=patch,
-                              params={"patchType": patch_type})
+                              params=params)
 
     async def delete(self, target: GVRorGVK, namespace: str, name: str, propagation_policy: Optional[str] = None,
-                     preconditions: Optional[Dict[str, str]] = None) -> Any:
+                     preconditions: Optional[Dict[str, str]] = None, discard_response: bool = False) -> Any:
         opts: Dict[str, Any] = {}
         if propagation_policy:
             opts["propagationPolicy"] = propagation_policy
         if preconditions:
             opts["preconditions"] = preconditions
-        return await self._do("delete", await self._gvr(target), namespace, name, body=opts or None)
+        return await self._do("delete", await self._gvr(target), namespace, name, body=opts or None,
+                              params={DISCARD: True} if discard_response else None)
 
     async def delete_all_of(self, target: GVRorGVK, namespace: str = "", label_selector: Optional[str] = None) -> Any:
         params = {"labelSelector": label_selector} if label_selector else {}

@@ -1,0 +1,295 @@
+"""Lean HTTP/1.1 keep-alive client for the request/response verbs.
+
+Profiling the operator during the 1000-Cron bench (``profiles/operator_cprofile_r1b.txt``)
+put aiohttp's client machinery (request/response objects, header multidicts,
+timers, stream readers) at roughly a third of the operator's CPU per API call.
+A Kubernetes client needs far less: one request in flight per connection, a
+fixed header set, ``Content-Length`` or ``chunked`` responses, keep-alive.
+This module is exactly that, on ``asyncio.Protocol``:
+
+* a pool of persistent connections per host (TLS via the kubeconfig's
+  ``ssl.SSLContext``; plain TCP for ``http://``);
+* request bytes built once per call (method, path, fixed auth headers,
+  ``Content-Length``);
+* an incremental response parser (status line, headers, ``Content-Length`` /
+  ``chunked`` / read-to-close bodies) that completes a future with
+  ``(status, body bytes)``;
+* a request that dies on a *reused* connection before any response byte
+  arrived (the server closed an idle keep-alive socket) is retried once on a
+  fresh connection, as Go's ``net/http`` does; the operator's writes are
+  idempotent anyway (deterministic names, merge patches).
+
+Watch streams stay on aiohttp (few, long-lived); see :mod:`.http`.
+"""
+from __future__ import annotations
+
+import asyncio
+import ssl as _ssl
+from collections import deque
+from typing import Deque, Dict, List, Optional, Tuple
+from urllib.parse import urlsplit
+
+
+class ConnectionFailed(Exception):
+    """The connection broke; ``no_response`` + ``reused`` tell whether a retry is safe."""
+
+    def __init__(self, msg: str, no_response: bool, reused: bool):
+        super().__init__(msg)
+        self.no_response = no_response
+        self.reused = reused
+
+
+class _Conn(asyncio.Protocol):
+    __slots__ = ("transport", "buf", "fut", "alive", "used", "_state", "_status", "_clen", "_chunked",
+                 "_close_after", "_body", "_got_any")
+
+    def __init__(self) -> None:
+        self.transport: Optional[asyncio.Transport] = None
+        self.buf = bytearray()
+        self.fut: Optional[asyncio.Future] = None
+        self.alive = True
+        self.used = 0
+        self._reset()
+
+    def _reset(self) -> None:
+        self._state = 0          # 0 headers, 1 body by length, 2 chunked, 3 until close
+        self._status = 0
+        self._clen = -1
+        self._chunked = False
+        self._close_after = False
+        self._body = bytearray()
+        self._got_any = False
+
+    # --------------------------------------------------------------- protocol
+    def connection_made(self, transport: asyncio.BaseTransport) -> None:
+        self.transport = transport  # type: ignore[assignment]
+
+    def connection_lost(self, exc: Optional[BaseException]) -> None:
+        self.alive = False
+        fut = self.fut
+        if fut is not None and not fut.done():
+            if self._state == 3:
+                self._finish()
+                return
+            fut.set_exception(ConnectionFailed(f"connection lost: {exc or 'closed by peer'}",
+                                               not self._got_any, self.used > 1))
+
+    def eof_received(self) -> Optional[bool]:
+        return False
+
+    def data_received(self, data: bytes) -> None:
+        self._got_any = True
+        self.buf += data
+        try:
+            self._parse()
+        except Exception as e:  # noqa: BLE001 - malformed response
+            self.alive = False
+            if self.fut is not None and not self.fut.done():
+                self.fut.set_exception(ConnectionFailed(f"bad HTTP response: {e}", False, False))
+            if self.transport is not None:
+                self.transport.close()
+
+    def _parse(self) -> None:
+        buf = self.buf
+        while True:
+            if self._state == 0:
+                end = buf.find(b"\r\n\r\n")
+                if end < 0:
+                    return
+                head = bytes(buf[:end]).decode("latin-1")
+                del buf[:end + 4]
+                lines = head.split("\r\n")
+                parts = lines[0].split(" ", 2)
+                self._status = int(parts[1])
+                clen = -1
+                chunked = False
+                close = parts[0] == "HTTP/1.0"
+                for line in lines[1:]:
+                    k, _, v = line.partition(":")
+                    k = k.strip().lower()
+                    if k == "content-length":
+                        clen = int(v.strip())
+                    elif k == "transfer-encoding":
+                        chunked = "chunked" in v.lower()
+                    elif k == "connection":
+                        lv = v.strip().lower()
+                        close = lv == "close" if lv in ("close", "keep-alive") else close
+                self._close_after = close
+                if self._status in (204, 304) or 100 <= self._status < 200:
+                    if 100 <= self._status < 200:  # interim response: parse the next head
+                        continue
+                    self._finish()
+                    return
+                if chunked:
+                    self._state = 2
+                elif clen >= 0:
+                    self._clen = clen
+                    self._state = 1
+                else:
+                    self._state = 3
+                    self._close_after = True
+            if self._state == 1:
+                if len(buf) < self._clen:
+                    return
+                self._body = buf[:self._clen]
+                del buf[:self._clen]
+                self._finish()
+                return
+            if self._state == 2:
+                while True:
+                    nl = buf.find(b"\r\n")
+                    if nl < 0:
+                        return
+                    size = int(bytes(buf[:nl]).split(b";", 1)[0], 16)
+                    if size == 0:
+                        # trailers end with an empty line
+                        end = buf.find(b"\r\n\r\n", nl)
+                        if end < 0:
+                            if len(buf) >= nl + 4 and buf[nl:nl + 4] == b"\r\n\r\n":
+                                end = nl
+                            else:
+                                return
+                        del buf[:end + 4]
+                        self._finish()
+                        return
+                    if len(buf) < nl + 2 + size + 2:
+                        return
+                    self._body += buf[nl + 2:nl + 2 + size]
+                    del buf[:nl + 2 + size + 2]
+            if self._state == 3:
+                self._body += buf
+                buf.clear()
+                return
+
+    def _finish(self) -> None:
+        fut = self.fut
+        status, body = self._status, bytes(self._body)
+        if self._close_after:
+            self.alive = False
+            if self.transport is not None:
+                self.transport.close()
+        self._reset()
+        self.fut = None
+        if fut is not None and not fut.done():
+            fut.set_result((status, body))
+
+    # --------------------------------------------------------------- client side
+    def send(self, data: bytes) -> asyncio.Future:
+        loop = asyncio.get_running_loop()
+        self.fut = loop.create_future()
+        self.used += 1
+        self._got_any = False
+        assert self.transport is not None
+        self.transport.write(data)
+        return self.fut
+
+
+def _expire(fut: asyncio.Future) -> None:
+    if not fut.done():
+        fut.set_exception(asyncio.TimeoutError())
+
+
+class HttpPool:
+    """Keep-alive connection pool to one ``scheme://host:port``."""
+
+    def __init__(self, base_url: str, ssl_context: Optional[_ssl.SSLContext] = None,
+                 headers: Optional[Dict[str, str]] = None, max_idle: int = 64, timeout: float = 60.0,
+                 server_hostname: Optional[str] = None):
+        u = urlsplit(base_url)
+        self.scheme = u.scheme or "http"
+        self.host = u.hostname or "127.0.0.1"
+        self.port = u.port or (443 if self.scheme == "https" else 80)
+        self.base_path = (u.path or "").rstrip("/")
+        self.ssl = ssl_context if self.scheme == "https" else None
+        if self.scheme == "https" and self.ssl is None:
+            self.ssl = _ssl.create_default_context()
+        self.server_hostname = server_hostname
+        hosthdr = self.host if (self.port in (80, 443)) else f"{self.host}:{self.port}"
+        hdrs = {"User-Agent": "cron-operator-amd", "Accept": "application/json"}
+        hdrs.update(headers or {})
+        extra = "".join(f"{k}: {v}\r\n" for k, v in hdrs.items())
+        self._fixed = f"Host: {hosthdr}\r\n{extra}"
+        self._idle: Deque[_Conn] = deque()
+        self.max_idle = max_idle
+        self.timeout = timeout
+        self.connects = 0
+        self._closed = False
+
+    async def _connect(self) -> _Conn:
+        loop = asyncio.get_running_loop()
+        kw = {}
+        if self.ssl is not None:
+            kw["ssl"] = self.ssl
+            kw["server_hostname"] = self.server_hostname or self.host
+        _, proto = await asyncio.wait_for(loop.create_connection(_Conn, self.host, self.port, **kw), self.timeout)
+        self.connects += 1
+        return proto  # type: ignore[return-value]
+
+    def _take_idle(self) -> Optional[_Conn]:
+        while self._idle:
+            c = self._idle.pop()
+            if c.alive and c.transport is not None and not c.transport.is_closing():
+                return c
+        return None
+
+    def _give_back(self, c: _Conn) -> None:
+        if c.alive and not self._closed and len(self._idle) < self.max_idle and c.fut is None:
+            self._idle.append(c)
+        elif c.transport is not None:
+            c.transport.close()
+
+    async def request(self, method: str, path: str, body: Optional[bytes] = None,
+                      content_type: str = "application/json") -> Tuple[int, bytes]:
+        head = f"{method} {self.base_path}{path} HTTP/1.1\r\n{self._fixed}"
+        if body is not None:
+            head += f"Content-Type: {content_type}\r\nContent-Length: {len(body)}\r\n\r\n"
+            data = head.encode("latin-1") + body
+        else:
+            data = (head + ("Content-Length: 0\r\n\r\n" if method in ("POST", "PUT", "PATCH") else "\r\n")
+                    ).encode("latin-1")
+        for attempt in (0, 1):
+            conn = self._take_idle() if attempt == 0 else None
+            if conn is None:
+                conn = await self._connect()
+            fut = conn.send(data)
+            timer = asyncio.get_running_loop().call_later(self.timeout, _expire, fut)
+            try:
+                status, raw = await fut
+            except ConnectionFailed as e:
+                conn.alive = False
+                if attempt == 0 and e.no_response and e.reused:
+                    continue  # stale keep-alive connection: retry once on a fresh one
+                raise
+            except asyncio.TimeoutError:
+                conn.alive = False
+                if conn.transport is not None:
+                    conn.transport.close()
+                raise
+            except BaseException:
+                conn.alive = False
+                if conn.transport is not None:
+                    conn.transport.close()
+                raise
+            finally:
+                timer.cancel()
+            self._give_back(conn)
+            return status, raw
+        raise ConnectionFailed("unreachable", True, False)  # pragma: no cover
+
+    async def close(self) -> None:
+        self._closed = True
+        while self._idle:
+            c = self._idle.pop()
+            if c.transport is not None:
+                c.transport.close()
+
+
+def encode_query(params: Dict[str, str]) -> str:
+    if not params:
+        return ""
+    from urllib.parse import urlencode
+
+    return "?" + urlencode(params)
+
+
+__all__: List[str] = ["HttpPool", "ConnectionFailed", "encode_query"]

@@ -1,9 +1,11 @@
-"""HTTP transport: the Kubernetes REST protocol over aiohttp.
+"""HTTP transport: the Kubernetes REST protocol.
 
 Works against a real kube-apiserver (kubeconfig / in-cluster config) and the
 framework's fake apiserver served by :mod:`cron_operator_amd.apiserver.http`.
-Connections are pooled and kept alive; watch streams are read line by line
-(newline-delimited JSON) with a large line limit so big objects fit.
+Request/response verbs go through the lean keep-alive pool of
+:mod:`.fasthttp` (``fast=True``, the default) or aiohttp (``fast=False``);
+watch streams use aiohttp and are read line by line (newline-delimited JSON)
+with a large line limit so big objects fit.
 """
 from __future__ import annotations
 
@@ -17,7 +19,8 @@ import aiohttp
 from ..api import errors
 from ..api.meta import GroupVersion, GroupVersionResource
 from ..utils import jsonutil
-from .client import PATCH_CONTENT_TYPES, Transport, WatchStream
+from .client import DISCARD, PATCH_CONTENT_TYPES, Transport, WatchStream
+from .fasthttp import ConnectionFailed, HttpPool, encode_query
 from .kubeconfig import RestConfig
 
 
@@ -36,7 +39,7 @@ def resource_path(gvr: GroupVersionResource, namespace: str = "", name: str = ""
 def _clean(params: Optional[Dict[str, Any]]) -> Dict[str, str]:
     out = {}
     for k, v in (params or {}).items():
-        if k == "patchType" or v is None or v == "":
+        if k == "patchType" or k.startswith("_") or v is None or v == "":
             continue
         out[k] = str(v)
     return out
@@ -62,7 +65,7 @@ class _HttpWatch(WatchStream):
             line = line.strip()
             if not line:
                 continue
-            ev = json.loads(line)
+            ev = jsonutil.loads(line)
             return ev.get("type", ""), ev.get("object") or {}
 
     def stop(self) -> None:
@@ -71,13 +74,26 @@ class _HttpWatch(WatchStream):
             self._resp.close()
 
 
+_METHODS = {"get": "GET", "list": "GET", "create": "POST", "update": "PUT", "patch": "PATCH",
+            "delete": "DELETE", "deletecollection": "DELETE"}
+
+
 class HttpTransport(Transport):
-    def __init__(self, config: RestConfig, pool_size: int = 64, timeout: float = 60.0):
+    def __init__(self, config: RestConfig, pool_size: int = 64, timeout: float = 60.0, fast: bool = True):
         self.config = config
         self.host = config.host.split("://", 1)[-1]
         self._pool_size = pool_size
         self._timeout = timeout
         self._session: Optional[aiohttp.ClientSession] = None
+        self.fast = fast
+        self._pool: Optional[HttpPool] = None
+
+    def _fast_pool(self) -> HttpPool:
+        if self._pool is None:
+            self._pool = HttpPool(self.config.host, ssl_context=self.config.ssl_context() or None,
+                                  headers=self.config.auth_headers(), max_idle=self._pool_size,
+                                  timeout=self._timeout, server_hostname=self.config.tls_server_name or None)
+        return self._pool
 
     def _sess(self) -> aiohttp.ClientSession:
         if self._session is None or self._session.closed:
@@ -98,11 +114,27 @@ class HttpTransport(Transport):
     async def request(self, verb: str, gvr: GroupVersionResource, namespace: str = "", name: str = "",
                       subresource: str = "", body: Any = None, params: Optional[Dict[str, Any]] = None) -> Any:
         params = params or {}
-        method = {"get": "GET", "list": "GET", "create": "POST", "update": "PUT", "patch": "PATCH",
-                  "delete": "DELETE", "deletecollection": "DELETE"}[verb]
-        url = self.config.host + resource_path(gvr, namespace, name if verb not in ("list", "create",
-                                                                                    "deletecollection") else "",
-                                                subresource)
+        method = _METHODS[verb]
+        path = resource_path(gvr, namespace, name if verb not in ("list", "create", "deletecollection") else "",
+                             subresource)
+        if self.fast:
+            data = jsonutil.dumpb(body) if body is not None else None
+            ctype = PATCH_CONTENT_TYPES[params.get("patchType", "merge")] if verb == "patch" else "application/json"
+            try:
+                status, raw = await self._fast_pool().request(method, path + encode_query(_clean(params)), data,
+                                                              ctype)
+            except (ConnectionFailed, OSError, asyncio.TimeoutError) as e:
+                raise errors.ApiError(503, "ServiceUnavailable", f"connection error: {e}") from None
+            if status >= 400:
+                try:
+                    err_body: Any = jsonutil.loads(raw)
+                except ValueError:
+                    err_body = raw.decode(errors="replace")
+                raise errors.ApiError.from_status(status, err_body)
+            if params.get(DISCARD):
+                return None
+            return jsonutil.loads(raw) if raw else None
+        url = self.config.host + path
         headers = {"Accept": "application/json"}
         data = None
         if body is not None:
@@ -118,7 +150,7 @@ class HttpTransport(Transport):
                 raw = await resp.read()
         except aiohttp.ClientConnectionError as e:
             raise errors.ApiError(503, "ServiceUnavailable", f"connection error: {e}") from None
-        return json.loads(raw) if raw else None
+        return jsonutil.loads(raw) if raw else None
 
     async def watch(self, gvr: GroupVersionResource, namespace: str = "",
                     params: Optional[Dict[str, Any]] = None) -> WatchStream:
@@ -150,6 +182,9 @@ class HttpTransport(Transport):
         return doc.get("resources") or []
 
     async def close(self) -> None:
+        if self._pool is not None:
+            await self._pool.close()
+            self._pool = None
         if self._session is not None:
             await self._session.close()
             self._session = None

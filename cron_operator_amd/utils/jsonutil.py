@@ -163,6 +163,7 @@ def dumpb(x: Any) -> bytes:
     return json.dumps(x, separators=(",", ":"), ensure_ascii=False).encode()
 
 
+py_loads = json.loads
 loads = json.loads
 
 # --------------------------------------------------------------------------- native dispatch
@@ -174,7 +175,7 @@ NATIVE = False
 
 
 def _try_native() -> None:
-    global deepcopy, json_equal, create_merge_patch, NATIVE
+    global deepcopy, json_equal, create_merge_patch, loads, NATIVE
     import os
 
     if os.environ.get("CRON_OPERATOR_FASTJSON", "auto").lower() == "python":
@@ -190,6 +191,7 @@ def _try_native() -> None:
     deepcopy = mod.deepcopy
     json_equal = mod.json_equal
     create_merge_patch = mod.create_merge_patch
+    loads = mod.loads
     NATIVE = True
 
 

@@ -35,13 +35,22 @@ def main() -> int:
     cfg = BenchConfig(n_crons=a.crons, steps=a.steps, warmup=a.warmup, transport=a.transport, mode=a.mode)
     prof = cProfile.Profile()
     t0, c0 = time.perf_counter(), time.process_time()
-    prof.enable()
-    res = run_sync(cfg)
+
+    def on_step(k: int, dt: float, timed: bool) -> None:
+        # profile only the timed steps (setup and warmup excluded)
+        if k == cfg.warmup:
+            prof.enable()
+        if k == cfg.warmup + cfg.steps:
+            prof.disable()
+
+    if cfg.warmup == 0:
+        prof.enable()
+    res = run_sync(cfg, on_step)
     prof.disable()
     wall, cpu = time.perf_counter() - t0, time.process_time() - c0
     buf = io.StringIO()
-    buf.write(f"# operator-process cProfile ({a.mode}/{a.transport}, {a.crons} Crons, "
-              f"{a.warmup}+{a.steps} steps; profiler overhead inflates absolute times)\n")
+    buf.write(f"# operator-process cProfile of the {a.steps} timed steps ({a.mode}/{a.transport}, {a.crons} Crons, "
+              f"{a.warmup} warmup steps excluded; profiler overhead inflates absolute times)\n")
     buf.write(f"# {summarize(res)}\n# wall {wall:.2f} s, operator CPU {cpu:.2f} s\n\n")
     st = pstats.Stats(prof, stream=buf)
     st.sort_stats("tottime").print_stats(a.top)

@@ -1,0 +1,160 @@
+"""The lean HTTP/1.1 client (runtime/fasthttp.py) against hand-written server replies."""
+from __future__ import annotations
+
+import asyncio
+
+import pytest
+
+from cron_operator_amd.runtime.fasthttp import ConnectionFailed, HttpPool, encode_query
+
+
+async def serve(replies, record=None):
+    """A TCP server that answers successive requests on a connection with ``replies`` (bytes or callables)."""
+    it = iter(replies)
+
+    async def handle(reader, writer):
+        try:
+            while True:
+                head = await reader.readuntil(b"\r\n\r\n")
+                clen = 0
+                for line in head.split(b"\r\n"):
+                    if line.lower().startswith(b"content-length:"):
+                        clen = int(line.split(b":")[1])
+                body = await reader.readexactly(clen) if clen else b""
+                if record is not None:
+                    record.append((head, body))
+                r = next(it)
+                if r is None:  # close without answering
+                    writer.close()
+                    return
+                writer.write(r)
+                await writer.drain()
+        except (asyncio.IncompleteReadError, ConnectionResetError, StopIteration):
+            writer.close()
+
+    srv = await asyncio.start_server(handle, "127.0.0.1", 0)
+    return srv, srv.sockets[0].getsockname()[1]
+
+
+async def test_content_length_keepalive_and_headers():
+    rec = []
+    srv, port = await serve([b"HTTP/1.1 200 OK\r\nContent-Length: 2\r\n\r\n{}",
+                             b"HTTP/1.1 201 Created\r\nContent-Length: 7\r\n\r\n{\"a\":1}"], rec)
+    pool = HttpPool(f"http://127.0.0.1:{port}", headers={"Authorization": "Bearer t"})
+    try:
+        assert await pool.request("GET", "/x") == (200, b"{}")
+        assert await pool.request("POST", "/y", b'{"k":1}') == (201, b'{"a":1}')
+        assert pool.connects == 1  # kept alive
+        head0, _ = rec[0]
+        assert head0.startswith(b"GET /x HTTP/1.1\r\n") and b"Authorization: Bearer t" in head0
+        head1, body1 = rec[1]
+        assert b"Content-Type: application/json" in head1 and body1 == b'{"k":1}'
+    finally:
+        await pool.close()
+        srv.close()
+
+
+async def test_chunked_and_split_packets():
+    body = b"4\r\nWiki\r\n6;ext=1\r\npedia \r\nE\r\nin \r\n\r\nchunks.\r\n0\r\nX-Trailer: 1\r\n\r\n"
+    srv, port = await serve([b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n" + body,
+                             b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n0\r\n\r\n"])
+    pool = HttpPool(f"http://127.0.0.1:{port}")
+    try:
+        st, raw = await pool.request("GET", "/c")
+        assert st == 200 and raw == b"Wikipedia in \r\n\r\nchunks."
+        assert await pool.request("GET", "/empty") == (200, b"")
+        assert pool.connects == 1
+    finally:
+        await pool.close()
+        srv.close()
+
+
+async def test_parser_handles_byte_by_byte_delivery():
+    from cron_operator_amd.runtime.fasthttp import _Conn
+
+    loop = asyncio.get_running_loop()
+
+    class T:
+        def write(self, d):
+            pass
+
+        def is_closing(self):
+            return False
+
+        def close(self):
+            pass
+
+    c = _Conn()
+    c.connection_made(T())
+    fut = c.send(b"GET / HTTP/1.1\r\n\r\n")
+    for b in b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n3\r\nabc\r\n0\r\n\r\n":
+        c.data_received(bytes([b]))
+    assert fut.done() and fut.result() == (200, b"abc")
+    assert loop is asyncio.get_running_loop()
+
+
+async def test_connection_close_and_read_to_eof():
+    srv, port = await serve([b"HTTP/1.1 200 OK\r\nConnection: close\r\nContent-Length: 1\r\n\r\na"])
+    pool = HttpPool(f"http://127.0.0.1:{port}")
+    try:
+        assert await pool.request("GET", "/") == (200, b"a")
+        assert not pool._idle  # closed, not pooled
+    finally:
+        await pool.close()
+        srv.close()
+
+    async def eof_server(reader, writer):
+        await reader.readuntil(b"\r\n\r\n")
+        writer.write(b"HTTP/1.0 200 OK\r\n\r\nuntil-close")
+        await writer.drain()
+        writer.close()
+
+    srv2 = await asyncio.start_server(eof_server, "127.0.0.1", 0)
+    pool2 = HttpPool(f"http://127.0.0.1:{srv2.sockets[0].getsockname()[1]}")
+    try:
+        assert await pool2.request("GET", "/") == (200, b"until-close")
+    finally:
+        await pool2.close()
+        srv2.close()
+
+
+async def test_stale_keepalive_is_retried_once():
+    # first connection: one good reply then the server drops the idle connection
+    srv, port = await serve([b"HTTP/1.1 200 OK\r\nContent-Length: 1\r\n\r\n1", None,
+                             b"HTTP/1.1 200 OK\r\nContent-Length: 1\r\n\r\n2"])
+    pool = HttpPool(f"http://127.0.0.1:{port}")
+    try:
+        assert await pool.request("GET", "/") == (200, b"1")
+        assert await pool.request("GET", "/") == (200, b"2")  # retried on a fresh connection
+        assert pool.connects == 2
+    finally:
+        await pool.close()
+        srv.close()
+
+
+async def test_fresh_connection_failure_raises_and_timeout():
+    srv, port = await serve([None])
+    pool = HttpPool(f"http://127.0.0.1:{port}")
+    try:
+        with pytest.raises(ConnectionFailed):
+            await pool.request("GET", "/")
+    finally:
+        await pool.close()
+        srv.close()
+
+    async def silent(reader, writer):
+        await asyncio.sleep(5)
+
+    srv2 = await asyncio.start_server(silent, "127.0.0.1", 0)
+    pool2 = HttpPool(f"http://127.0.0.1:{srv2.sockets[0].getsockname()[1]}", timeout=0.2)
+    try:
+        with pytest.raises(asyncio.TimeoutError):
+            await pool2.request("GET", "/")
+    finally:
+        await pool2.close()
+        srv2.close()
+
+
+def test_encode_query():
+    assert encode_query({}) == ""
+    assert encode_query({"labelSelector": "kubedl.io/cron-name=a b"}) == "?labelSelector=kubedl.io%2Fcron-name%3Da+b"

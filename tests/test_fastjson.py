@@ -1,0 +1,72 @@
+"""Native JSON decoder (``_fastjson.loads``) against ``json.loads`` as the oracle."""
+from __future__ import annotations
+
+import json
+import math
+
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from cron_operator_amd.ops import fastjson_native
+
+m = fastjson_native.load()
+
+json_values = st.recursive(
+    st.none() | st.booleans() | st.integers(min_value=-(10 ** 30), max_value=10 ** 30)
+    | st.floats(allow_nan=False, allow_infinity=False) | st.text(max_size=20),
+    lambda children: st.lists(children, max_size=5) | st.dictionaries(st.text(max_size=12), children, max_size=5),
+    max_leaves=40)
+
+
+@settings(max_examples=400, deadline=None)
+@given(json_values, st.booleans(), st.booleans())
+def test_roundtrip_matches_json(v, ascii_only, pretty):
+    s = json.dumps(v, ensure_ascii=ascii_only, indent=2 if pretty else None)
+    want = json.loads(s)
+    assert m.loads(s) == want
+    assert m.loads(s.encode()) == want
+    assert m.loads(bytearray(s.encode())) == want
+    assert repr(m.loads(s)) == repr(want)  # int vs float, -0.0, key order
+
+
+@pytest.mark.parametrize("doc", [
+    '{}', '[]', '0', '-0', '-0.0', '1.5e10', '1E-5', '2.5E+3', '123456789012345678901234567890',
+    '-12345678901234567', '"a\\u00e9\\ud83d\\ude00\\ud800x"', '"\\"\\\\\\/\\b\\f\\n\\r\\t"', '"héllo ✓"',
+    '{"a":1,"a":2}', '[1,[2,[3,{"x":null,"y":true,"z":false}]]]', ' \n {"k" : [ 1 , 2 ] } \t', '1e400',
+    '"\\ud800"', '"\\udc00\\ud800"', '"\U0001F600"', '-1e-400',
+])
+def test_edge_cases(doc):
+    assert repr(m.loads(doc)) == repr(json.loads(doc))
+
+
+def test_non_finite():
+    assert math.isnan(m.loads("NaN"))
+    assert m.loads("Infinity") == math.inf and m.loads("-Infinity") == -math.inf
+    assert m.loads(b"\xef\xbb\xbf[1]") == [1]  # UTF-8 BOM on bytes is skipped, like json.loads
+    with pytest.raises(ValueError):
+        m.loads("﻿[1]")
+
+
+@pytest.mark.parametrize("bad", ['', '{', '[1,]', '{"a"}', '{"a" 1}', '01', '1.', '"abc', '"\x01"', 'tru', '{"a":1}x',
+                                 '"\\x"', '-', '[1 2]', b'"\xff"', '"\\u12"', "{'a':1}", '[1,,2]', '{"a":1,}'])
+def test_rejects_what_json_rejects(bad):
+    with pytest.raises(ValueError):
+        json.loads(bad)
+    with pytest.raises(ValueError):
+        m.loads(bad)
+
+
+def test_deep_nesting_and_types():
+    with pytest.raises((ValueError, RecursionError)):
+        m.loads("[" * 5000 + "]" * 5000)
+    with pytest.raises(TypeError):
+        m.loads(1)
+
+
+def test_keys_are_shared_and_cache_clear():
+    a = m.loads('{"metadata":{"name":"x"}}')
+    b = m.loads(b'{"metadata":{"name":"y"}}')
+    assert next(iter(a)) is next(iter(b))  # interned through the key cache
+    m.clear_key_cache()
+    assert m.loads('{"metadata":1}') == {"metadata": 1}

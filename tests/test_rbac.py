@@ -169,7 +169,14 @@ async def _operator_fires_under(srv: APIServer, clock: FakeClock, lease_ns: str)
                          "template": {"workload": {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
                                                    "spec": {"pytorchReplicaSpecs": {}}}}}}
         await admin.create(CRON_GVR, cron, "default")
-        clock.advance(60)
+
+        async def advance(seconds: int) -> None:
+            # step the fake clock like wall time so the leader keeps renewing its Lease
+            for _ in range(seconds):
+                clock.advance(1)
+                await asyncio.sleep(0.002)
+
+        await advance(60)
         for _ in range(400):
             items = (await admin.list(PT, "default", label_selector=f"{LABEL_CRON_NAME}=rbac"))["items"]
             if items:
@@ -178,7 +185,7 @@ async def _operator_fires_under(srv: APIServer, clock: FakeClock, lease_ns: str)
         assert items, f"no job created; reconcile errors={ctrl.errors}"
         # Replace: the next tick deletes the active job and creates a new one (delete verb granted)
         first = items[0]["metadata"]["name"]
-        clock.advance(60)
+        await advance(60)
         for _ in range(400):
             names = [o["metadata"]["name"] for o in
                      (await admin.list(PT, "default", label_selector=f"{LABEL_CRON_NAME}=rbac"))["items"]]
