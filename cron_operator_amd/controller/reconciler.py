@@ -90,6 +90,23 @@ def go_quote(s: str) -> str:
     return json.dumps(s, ensure_ascii=False)
 
 
+class _ChildInfo:
+    """Everything a reconcile derives from one child object.  Objects are immutable per
+    resourceVersion, so with ``classification_cache`` this is computed once per child
+    version instead of on every reconcile of its Cron (the 10 history children of a
+    Cron were re-parsed ~2x per tick otherwise)."""
+
+    __slots__ = ("rv", "cls", "sort_key", "gvk", "active_ref", "history_entry")
+
+    def __init__(self, rv: str, cls: Classification, sort_key: Any, gvk: GroupVersionKind):
+        self.rv = rv
+        self.cls = cls
+        self.sort_key = sort_key
+        self.gvk = gvk
+        self.active_ref: Optional[ObjectReference] = None
+        self.history_entry: Optional[CronHistory] = None
+
+
 class JoinedError(Exception):
     """``errors.Join`` of a reconcile error and a status-patch error."""
 
@@ -222,8 +239,8 @@ class CronReconciler(Reconciler):
         # key -> resourceVersion of the Cron object produced by our last status write
         self.own_writes: Dict[str, Tuple[Any, Dict[str, Any]]] = {}  # key -> (generation, status we wrote)
         self.stats = {"creates": 0, "deletes": 0, "patches": 0, "noop_patches_skipped": 0, "lists": 0}
-        # child uid -> (resourceVersion, Classification): objects are immutable per resourceVersion
-        self._class_cache: Dict[str, Tuple[str, Classification]] = {}
+        # child uid -> derived data for one resourceVersion (objects are immutable per resourceVersion)
+        self._class_cache: Dict[str, _ChildInfo] = {}
         # tick bookkeeping for latency: key -> (tick unix ns, wall perf_counter when it became due)
         self.latency_observer: Optional[Callable[[str, GoTime, Dict[str, Any]], None]] = None
 
@@ -346,13 +363,13 @@ class CronReconciler(Reconciler):
                     m = w.get("metadata") or {}
                     uid, rv = m.get("uid", ""), m.get("resourceVersion", "")
                     hit = cache.get(uid)
-                    if hit is not None and hit[0] == rv:
-                        c = hit[1]
+                    if hit is not None and hit.rv == rv:
+                        c = hit.cls
                     else:
                         c = classify(w, gvk, policy)
                         if len(cache) > 500_000:
                             cache.clear()
-                        cache[uid] = (rv, c)
+                        cache[uid] = _ChildInfo(rv, c, creation_timestamp(w).key(), GroupVersionKind.from_object(w))
                 else:
                     c = classify(w, gvk, policy)
             except kf.ConversionError as e:
@@ -550,32 +567,64 @@ class CronReconciler(Reconciler):
     def _sort(items: List[Tuple[Dict[str, Any], Classification]]) -> None:
         items.sort(key=lambda wc: creation_timestamp(wc[0]).key())
 
+    def _memo(self, w: Dict[str, Any]) -> Optional[_ChildInfo]:
+        """The child's cached derived data, if the classification cache holds this version."""
+        if not self.opts.classification_cache:
+            return None
+        m = w.get("metadata") or {}
+        info = self._class_cache.get(m.get("uid", ""))
+        if info is not None and info.rv == m.get("resourceVersion", ""):
+            return info
+        return None
+
+    def _sort_children(self, items: List[Tuple[Dict[str, Any], Classification]]) -> None:
+        if self.opts.classification_cache:
+            infos = [self._memo(w) for w, _ in items]
+            if all(i is not None for i in infos):
+                order = sorted(range(len(items)), key=lambda k: infos[k].sort_key)  # type: ignore[union-attr]
+                items[:] = [items[k] for k in order]
+                return
+        self._sort(items)
+
     def sync_active_list(self, cron: Cron, gvk: GroupVersionKind, active: List[Tuple[Dict[str, Any], Classification]],
                          log: Logger) -> None:
         """``syncActiveList`` (``cron_controller.go:284-304``)."""
         log.v(1).info("Syncing active list")
-        self._sort(active)
+        self._sort_children(active)
         refs = []
         with_rv = self.opts.active_ref_resource_version
         for w, _ in active:
+            info = self._memo(w)
+            if info is not None and info.active_ref is not None:
+                refs.append(info.active_ref)
+                continue
             m = w.get("metadata") or {}
             wgvk = GroupVersionKind.from_object(w)
-            refs.append(ObjectReference(api_version=wgvk.api_version, kind=wgvk.kind, name=m.get("name", ""),
-                                        namespace=m.get("namespace", ""), uid=m.get("uid", ""),
-                                        resource_version=m.get("resourceVersion", "") if with_rv else ""))
+            ref = ObjectReference(api_version=wgvk.api_version, kind=wgvk.kind, name=m.get("name", ""),
+                                  namespace=m.get("namespace", ""), uid=m.get("uid", ""),
+                                  resource_version=m.get("resourceVersion", "") if with_rv else "")
+            if info is not None:
+                info.active_ref = ref
+            refs.append(ref)
         cron.status.active = refs
 
     async def sync_cron_history(self, cron: Cron, gvk: GroupVersionKind,
                                 terminated: List[Tuple[Dict[str, Any], Classification]], log: Logger) -> None:
         """``syncCronHistory`` incl. history-limit GC (``cron_controller.go:306-346``)."""
         log.v(1).info("Syncing Cron history")
-        self._sort(terminated)
+        self._sort_children(terminated)
         n = len(terminated)
         limit = cron.spec.history_limit if cron.spec.history_limit is not None else MAX_INT
-        previous = {h.uid: h for h in cron.status.history if h.uid}
+        previous: Optional[Dict[str, CronHistory]] = None
         history: List[CronHistory] = []
         now: Optional[GoTime] = None
+        memo_ok = self.opts.finished_time != "now"
         for i, (w, c) in enumerate(terminated):
+            if memo_ok and i >= n - limit:
+                info = self._memo(w)
+                if info is not None and info.history_entry is not None:
+                    history.append(info.history_entry)
+                    continue
             m = w.get("metadata") or {}
             wgvk = GroupVersionKind.from_object(w)
             ref = ObjectRef(m.get("namespace", ""), m.get("name", ""))
@@ -595,6 +644,7 @@ class CronReconciler(Reconciler):
                             self.expect.observe_delete(self._ckey(cron), uid)
                         log.error(e, f"Failed to delete terminated {wgvk.kind}", **{wgvk.kind: ref})
                 continue
+            info = self._memo(w) if memo_ok else None
             entry = CronHistory(uid=m.get("uid", ""),
                                 object=TypedLocalObjectReference(api_group=wgvk.group_version().__str__(),
                                                                  kind=wgvk.kind, name=m.get("name", "")),
@@ -605,9 +655,13 @@ class CronReconciler(Reconciler):
                         now = self.clock.now(LOCAL)
                     entry.finished = now
                 else:
+                    if previous is None:
+                        previous = {h.uid: h for h in cron.status.history if h.uid}
                     prev = previous.get(entry.uid)
                     if c.finished_at is not None:
                         entry.finished = c.finished_at
+                        if info is not None:  # fully determined by this child version
+                            info.history_entry = entry
                     elif prev is not None and prev.finished is not None:
                         entry.finished = prev.finished
                     else:

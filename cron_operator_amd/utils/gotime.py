@@ -424,8 +424,16 @@ def _parse_slow(s: str, loc: Location) -> GoTime:
 
 
 def format_rfc3339_utc(t: GoTime) -> str:
-    """``metav1.Time.MarshalJSON``: UTC, second precision."""
-    return GoTime(t.sec, 0, UTC).rfc3339()
+    """``metav1.Time.MarshalJSON``: UTC, second precision.  Cached by unix second: a
+    reconcile re-serialises every history timestamp of its Cron."""
+    return _format_utc_cached(t.sec)
+
+
+@lru_cache(maxsize=1 << 16)
+def _format_utc_cached(sec: int) -> str:
+    days, rem = divmod(sec, 86400)
+    y, m, d = civil_from_days(days)
+    return f"{y:04d}-{m:02d}-{d:02d}T{rem // 3600:02d}:{(rem // 60) % 60:02d}:{rem % 60:02d}Z"
 
 
 # --------------------------------------------------------------------------- durations
