@@ -32,8 +32,9 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 # BASELINE.md row "Reference algorithm, measured in this harness" (cron-reconciles/s @1000 Crons,
-# `bench.py --mode reference`, MI355X box, profiles/bench_reference_algorithm_mi355x_box_r1b.json).
-BASELINE_VALUE = 42.41
+# `--mode reference` in the same harness + fake apiserver, MI355X box, profiles/scale_mi355x_box_r1c.json).
+# Re-measured whenever the harness/apiserver changes, since the reference's live LISTs load the apiserver.
+BASELINE_VALUE = 68.8
 
 
 def _dist():

@@ -107,6 +107,10 @@ class _ChildInfo:
         self.history_entry: Optional[CronHistory] = None
 
 
+# (child object, its classification, its memo record when the classification cache is on)
+Child = Tuple[Dict[str, Any], Classification, Optional[_ChildInfo]]
+
+
 class JoinedError(Exception):
     """``errors.Join`` of a reconcile error and a status-patch error."""
 
@@ -354,28 +358,29 @@ class CronReconciler(Reconciler):
             raise
 
         # B5 (cron_controller.go:136-152)
-        active: List[Tuple[Dict[str, Any], Classification]] = []
-        terminated: List[Tuple[Dict[str, Any], Classification]] = []
+        active: List[Child] = []
+        terminated: List[Child] = []
         cache = self._class_cache if self.opts.classification_cache else None
         for w in workloads:
             try:
                 if cache is not None:
                     m = w.get("metadata") or {}
                     uid, rv = m.get("uid", ""), m.get("resourceVersion", "")
-                    hit = cache.get(uid)
-                    if hit is not None and hit.rv == rv:
-                        c = hit.cls
-                    else:
-                        c = classify(w, gvk, policy)
+                    info = cache.get(uid)
+                    if info is None or info.rv != rv:
+                        info = _ChildInfo(rv, classify(w, gvk, policy), creation_timestamp(w).key(),
+                                          GroupVersionKind.from_object(w))
                         if len(cache) > 500_000:
                             cache.clear()
-                        cache[uid] = _ChildInfo(rv, c, creation_timestamp(w).key(), GroupVersionKind.from_object(w))
+                        cache[uid] = info
+                    c = info.cls
                 else:
+                    info = None
                     c = classify(w, gvk, policy)
             except kf.ConversionError as e:
                 log.error(e, f"Failed to get {gvk.kind} status")
                 continue
-            (terminated if c.finished else active).append((w, c))
+            (terminated if c.finished else active).append((w, c, info))
         log.info(f"{gvk.kind} count", active=len(active), terminated=len(terminated))
 
         # B6/B7/B8 (cron_controller.go:155-158)
@@ -429,7 +434,7 @@ class CronReconciler(Reconciler):
 
         # B16 (cron_controller.go:210-220)
         if cron.spec.concurrency_policy == ConcurrentPolicyReplace:
-            for w, _ in active:
+            for w, _, _ in active:
                 m = w.get("metadata") or {}
                 ref = ObjectRef(m.get("namespace", ""), m.get("name", ""))
                 log.info(f"Deleting active {gvk.kind}", **{gvk.kind: ref})
@@ -494,8 +499,8 @@ class CronReconciler(Reconciler):
         cron.status.last_schedule_time = now
         return scheduled
 
-    def _tick_already_ran(self, cron: Cron, missed_run: GoTime, active: List[Tuple[Dict[str, Any], Classification]],
-                          terminated: List[Tuple[Dict[str, Any], Classification]]) -> bool:
+    def _tick_already_ran(self, cron: Cron, missed_run: GoTime, active: List[Child],
+                          terminated: List[Child]) -> bool:
         """Does a child named for ``missed_run``'s run exist?  Only for generated names: a
         template with a fixed ``metadata.name`` reuses one name for every run."""
         tmpl_meta = (cron.spec.template.workload or {}).get("metadata") if isinstance(
@@ -507,10 +512,10 @@ class CronReconciler(Reconciler):
                                                                         missed_run))
         except ScheduleError:
             return False
-        for w, _ in active:
+        for w, _, _ in active:
             if (w.get("metadata") or {}).get("name") == ran_name:
                 return True
-        for w, _ in terminated:
+        for w, _, _ in terminated:
             if (w.get("metadata") or {}).get("name") == ran_name:
                 return True
         return False
@@ -556,45 +561,30 @@ class CronReconciler(Reconciler):
         return children
 
     # ------------------------------------------------------------------ status
-    async def sync_status(self, cron: Cron, gvk: GroupVersionKind, active: List[Tuple[Dict[str, Any], Classification]],
-                          terminated: List[Tuple[Dict[str, Any], Classification]], log: Logger) -> None:
+    async def sync_status(self, cron: Cron, gvk: GroupVersionKind, active: List[Child],
+                          terminated: List[Child], log: Logger) -> None:
         """``syncStatus`` (``cron_controller.go:268-282``)."""
         log.v(1).info("Syncing Cron status")
         self.sync_active_list(cron, gvk, active, log)
         await self.sync_cron_history(cron, gvk, terminated, log)
 
     @staticmethod
-    def _sort(items: List[Tuple[Dict[str, Any], Classification]]) -> None:
-        items.sort(key=lambda wc: creation_timestamp(wc[0]).key())
+    @staticmethod
+    def _sort(items: List[Child]) -> None:
+        """``sortByCreationTimestamp`` (``cron_util.go:116-129``): stable, oldest first."""
+        if all(x[2] is not None for x in items):
+            items.sort(key=lambda x: x[2].sort_key)  # type: ignore[union-attr]
+        else:
+            items.sort(key=lambda x: creation_timestamp(x[0]).key())
 
-    def _memo(self, w: Dict[str, Any]) -> Optional[_ChildInfo]:
-        """The child's cached derived data, if the classification cache holds this version."""
-        if not self.opts.classification_cache:
-            return None
-        m = w.get("metadata") or {}
-        info = self._class_cache.get(m.get("uid", ""))
-        if info is not None and info.rv == m.get("resourceVersion", ""):
-            return info
-        return None
-
-    def _sort_children(self, items: List[Tuple[Dict[str, Any], Classification]]) -> None:
-        if self.opts.classification_cache:
-            infos = [self._memo(w) for w, _ in items]
-            if all(i is not None for i in infos):
-                order = sorted(range(len(items)), key=lambda k: infos[k].sort_key)  # type: ignore[union-attr]
-                items[:] = [items[k] for k in order]
-                return
-        self._sort(items)
-
-    def sync_active_list(self, cron: Cron, gvk: GroupVersionKind, active: List[Tuple[Dict[str, Any], Classification]],
+    def sync_active_list(self, cron: Cron, gvk: GroupVersionKind, active: List[Child],
                          log: Logger) -> None:
         """``syncActiveList`` (``cron_controller.go:284-304``)."""
         log.v(1).info("Syncing active list")
-        self._sort_children(active)
+        self._sort(active)
         refs = []
         with_rv = self.opts.active_ref_resource_version
-        for w, _ in active:
-            info = self._memo(w)
+        for w, _, info in active:
             if info is not None and info.active_ref is not None:
                 refs.append(info.active_ref)
                 continue
@@ -609,19 +599,18 @@ class CronReconciler(Reconciler):
         cron.status.active = refs
 
     async def sync_cron_history(self, cron: Cron, gvk: GroupVersionKind,
-                                terminated: List[Tuple[Dict[str, Any], Classification]], log: Logger) -> None:
+                                terminated: List[Child], log: Logger) -> None:
         """``syncCronHistory`` incl. history-limit GC (``cron_controller.go:306-346``)."""
         log.v(1).info("Syncing Cron history")
-        self._sort_children(terminated)
+        self._sort(terminated)
         n = len(terminated)
         limit = cron.spec.history_limit if cron.spec.history_limit is not None else MAX_INT
         previous: Optional[Dict[str, CronHistory]] = None
         history: List[CronHistory] = []
         now: Optional[GoTime] = None
         memo_ok = self.opts.finished_time != "now"
-        for i, (w, c) in enumerate(terminated):
+        for i, (w, c, info) in enumerate(terminated):
             if memo_ok and i >= n - limit:
-                info = self._memo(w)
                 if info is not None and info.history_entry is not None:
                     history.append(info.history_entry)
                     continue
@@ -644,7 +633,8 @@ class CronReconciler(Reconciler):
                             self.expect.observe_delete(self._ckey(cron), uid)
                         log.error(e, f"Failed to delete terminated {wgvk.kind}", **{wgvk.kind: ref})
                 continue
-            info = self._memo(w) if memo_ok else None
+            if not memo_ok:
+                info = None
             entry = CronHistory(uid=m.get("uid", ""),
                                 object=TypedLocalObjectReference(api_group=wgvk.group_version().__str__(),
                                                                  kind=wgvk.kind, name=m.get("name", "")),
