@@ -83,10 +83,17 @@ def main() -> int:
     cfg = BenchConfig(n_crons=a.crons, steps=a.steps, warmup=a.warmup, history_limit=a.history_limit,
                       mode=a.mode, transport=a.transport, qps=a.qps, burst=a.burst, workers=a.workers,
                       namespace=f"bench-r{rank}")
+    def on_step(k: int, dt: float, timed: bool) -> None:
+        # bracket the K timed steps with barriers so every rank times the same window: the
+        # harness starts its clock right after step `warmup` returns and stops it after the
+        # last step, i.e. after the closing barrier (which therefore counts: max over ranks)
+        if k == cfg.warmup or k == cfg.warmup + cfg.steps:
+            _sync_device()
+            _barrier(dist)
+
     _barrier(dist)
-    _sync_device()
     t0 = time.perf_counter()
-    res = run_sync(cfg)
+    res = run_sync(cfg, on_step if cfg.warmup > 0 else None)
     _sync_device()
     _barrier(dist)
     wall = time.perf_counter() - t0
