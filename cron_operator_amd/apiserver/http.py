@@ -389,6 +389,12 @@ class APIServerApp:
                         {"status": finished_status(obj.get("kind", ""), m["name"], ts, True)}, "merge", "status")
                 n += 1
             return _json({"completed": n})
+        if what == "gc" and req.method == "POST":
+            from ..utils import gctune
+
+            gctune.tune()
+            gctune.freeze()
+            return _json({"frozen": True})
         if what == "count":
             gvr = GroupVersionResource(req.query.get("group", ""), req.query.get("version", "v1"),
                                        req.query["resource"])

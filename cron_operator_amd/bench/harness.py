@@ -267,6 +267,9 @@ async def run(cfg: BenchConfig, on_step=None) -> BenchResult:
                                              {"status": finished_status("PyTorchJob", name, ts, True)}, "merge",
                                              "status")
         await set_time(T0_NS + NANOS // 2)
+        if admin is not None:  # the apiserver process holds the seeded store for the whole run
+            async with admin.post(remote.url + "/debug/fake/gc", json={}) as r:
+                await r.read()
 
         client = Client(transport, qps=cfg.qps, burst=cfg.burst)
         opts = ReconcilerOptions.reference() if cfg.mode == "reference" else ReconcilerOptions()

@@ -76,7 +76,7 @@ from ..runtime.client import Client
 from ..runtime.controller import Reconciler, Request, Result
 from ..runtime.events import Normal, Warning, EventRecorder
 from ..runtime.informer import Cache, Informer
-from ..utils import jsonutil
+from ..utils import gctune, jsonutil
 from ..utils.clock import Clock, RealClock
 from ..utils.gotime import LOCAL, GoTime
 from ..utils.logging import Logger, ObjectRef
@@ -539,6 +539,7 @@ class CronReconciler(Reconciler):
                 self.on_child_informer(gvk, inf)
         if not inf.synced.is_set():
             await inf.synced.wait()
+            gctune.freeze()  # a newly synced child cache: long-lived, keep it out of GC scans
         return inf
 
     async def list_workloads(self, cron: Cron, gvk: GroupVersionKind, log: Logger) -> List[Dict[str, Any]]:

@@ -18,6 +18,7 @@ from dataclasses import dataclass, field
 from typing import Awaitable, Callable, List, Optional
 
 from ..parallel.leaderelection import LeaderElector, in_cluster_namespace
+from ..utils import gctune
 from ..utils.clock import Clock, RealClock
 from ..utils.logging import get_logger
 from .client import Client
@@ -107,6 +108,8 @@ class Manager:
         ok = await self.cache.wait_for_sync(self.opts.cache_sync_timeout)
         if not ok:
             raise TimeoutError("timed out waiting for cache to be synced")
+        gctune.tune()
+        gctune.freeze()  # the synced caches are long-lived: keep them out of GC scans
         for c in self.controllers:
             c.start()
         loop = asyncio.get_running_loop()

@@ -1,0 +1,39 @@
+"""Garbage-collector tuning for a long-lived cache-heavy process.
+
+The operator keeps every watched object in informer caches (1000 Crons plus 11000
+PyTorchJobs in the headline bench).  CPython's cyclic GC re-scans all of them on
+every generation-2 collection even though JSON trees are acyclic and are freed
+by reference counting; measured in the bench, that was ~1.7 s of pauses per run
+(8 full collections).  Two standard remedies, applied at startup/sync points:
+
+* :func:`freeze` -- collect once, then move everything that survived into the
+  permanent generation (``gc.freeze``), so later collections skip the synced
+  cache (objects replaced later are still freed by refcounting);
+* :func:`tune` -- a larger generation-0 threshold, so short-lived reconcile
+  garbage is collected in fewer, cheaper passes.
+
+Disabled with ``CRON_OPERATOR_GC_TUNING=0``.
+"""
+from __future__ import annotations
+
+import gc
+import os
+
+_ENABLED = os.environ.get("CRON_OPERATOR_GC_TUNING", "1") not in ("0", "false", "no")
+DEFAULT_THRESHOLDS = (50_000, 20, 100)
+
+
+def enabled() -> bool:
+    return _ENABLED
+
+
+def tune(thresholds=DEFAULT_THRESHOLDS) -> None:
+    if _ENABLED:
+        gc.set_threshold(*thresholds)
+
+
+def freeze() -> None:
+    """Collect, then exempt every surviving object from future collections."""
+    if _ENABLED:
+        gc.collect()
+        gc.freeze()
