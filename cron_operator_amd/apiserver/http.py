@@ -389,6 +389,23 @@ class APIServerApp:
                         {"status": finished_status(obj.get("kind", ""), m["name"], ts, True)}, "merge", "status")
                 n += 1
             return _json({"completed": n})
+        if what == "profile" and req.method == "POST":
+            # cProfile of this process between "start" and "stop" (the bench profiles its timed steps)
+            import cProfile
+
+            body = self._body(req) or {}
+            if body.get("action") == "start":
+                self._prof = cProfile.Profile()
+                self._prof.enable()
+                return _json({"profiling": True})
+            prof = getattr(self, "_prof", None)
+            if prof is None:
+                raise errors.bad_request("profiling was not started")
+            prof.disable()
+            self._prof = None
+            if body.get("path"):
+                prof.dump_stats(body["path"])
+            return _json({"profiling": False, "path": body.get("path", "")})
         if what == "gc" and req.method == "POST":
             from ..utils import gctune
 

@@ -82,6 +82,7 @@ class BenchConfig:
     log_level: str = "error"
     step_timeout: float = 600.0
     seed_history: bool = True  # requires history_limit >= 1
+    apiserver_profile: str = ""  # write a cProfile of the apiserver process over the timed steps here
 
 
 @dataclass
@@ -344,6 +345,9 @@ async def run(cfg: BenchConfig, on_step=None) -> BenchResult:
         for k in range(1, total + 1):
             tick_ns = T0_NS + k * 60 * NANOS
             if k == cfg.warmup + 1:
+                if cfg.apiserver_profile and admin is not None:
+                    async with admin.post(remote.url + "/debug/fake/profile", json={"action": "start"}) as r:
+                        await r.read()
                 cpu0 = _cpu_times(remote)
                 rec0 = ctrl.reconciles
                 req0 = client.requests
@@ -374,6 +378,10 @@ async def run(cfg: BenchConfig, on_step=None) -> BenchResult:
                 on_step(k, dt, k > cfg.warmup)
         elapsed = time.perf_counter() - t_start
         cpu1 = _cpu_times(remote)
+        if cfg.apiserver_profile and admin is not None:
+            async with admin.post(remote.url + "/debug/fake/profile",
+                                  json={"action": "stop", "path": os.path.abspath(cfg.apiserver_profile)}) as r:
+                await r.read()
         reconciles = ctrl.reconciles - rec0
         requests = client.requests - req0
         by_verb = {v: n - reqv0.get(v, 0) for v, n in client.requests_by_verb.items()}

@@ -12,6 +12,9 @@
 //   json_equal(a, b) -> bool         structural equality; bool is never equal to int
 //   create_merge_patch(old, new)     RFC 7386 patch turning old into new
 //   loads(bytes | str) -> tree       JSON decoder (json.loads semantics for UTF-8 input)
+//   dumpb(tree) -> bytes             compact UTF-8 JSON, byte-identical to
+//                                    json.dumps(tree, separators=(",", ":"), ensure_ascii=False).encode()
+//   dumps(tree) -> str               the same as str
 //
 // loads: every API response and watch event the operator receives is decoded,
 // and in the 1000-Cron bench that was the largest single item of operator CPU
@@ -30,6 +33,7 @@
 #include <Python.h>
 
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -581,6 +585,159 @@ PyObject* py_loads(PyObject*, PyObject* arg) {
   return v;
 }
 
+
+// ---------------------------------------------------------------------------------------- encoder
+//
+// The fake apiserver encodes every response and watch event and the operator every
+// request body; CPython's encoder re-enters Python for each container.  This writes
+// straight into one growing buffer.  Output matches json.dumps(separators=(",", ":"),
+// ensure_ascii=False): floats via repr (PyOS_double_to_string 'r'), NaN/Infinity
+// literals, non-str keys coerced like json (True -> "true", 1 -> "1", None -> "null"),
+// tuples as arrays, control characters escaped as \uXXXX except the short forms.
+
+struct Encoder {
+  std::string out;
+
+  bool str(PyObject* u) {
+    Py_ssize_t n;
+    const char* p = PyUnicode_AsUTF8AndSize(u, &n);
+    if (!p) return false;  // lone surrogates: UnicodeEncodeError, like json.dumps(...).encode()
+    out.push_back('"');
+    const char* run = p;
+    const char* e = p + n;
+    for (const char* q = p; q < e; ++q) {
+      const unsigned char c = static_cast<unsigned char>(*q);
+      if (c >= 0x20 && c != '"' && c != '\\') continue;
+      out.append(run, static_cast<size_t>(q - run));
+      run = q + 1;
+      switch (c) {
+        case '"': out.append("\\\""); break;
+        case '\\': out.append("\\\\"); break;
+        case '\n': out.append("\\n"); break;
+        case '\r': out.append("\\r"); break;
+        case '\t': out.append("\\t"); break;
+        case '\b': out.append("\\b"); break;
+        case '\f': out.append("\\f"); break;
+        default: {
+          static const char hex[] = "0123456789abcdef";
+          char buf[7] = {'\\', 'u', '0', '0', hex[c >> 4], hex[c & 15], 0};
+          out.append(buf, 6);
+        }
+      }
+    }
+    out.append(run, static_cast<size_t>(e - run));
+    out.push_back('"');
+    return true;
+  }
+
+  bool flt(double d) {
+    if (d != d) { out.append("NaN"); return true; }
+    if (d == Py_HUGE_VAL) { out.append("Infinity"); return true; }
+    if (d == -Py_HUGE_VAL) { out.append("-Infinity"); return true; }
+    char* r = PyOS_double_to_string(d, 'r', 0, Py_DTSF_ADD_DOT_0, nullptr);
+    if (!r) return false;
+    out.append(r);
+    PyMem_Free(r);
+    return true;
+  }
+
+  bool integer(PyObject* o) {
+    int overflow = 0;
+    const long long v = PyLong_AsLongLongAndOverflow(o, &overflow);
+    if (v == -1 && PyErr_Occurred()) return false;
+    if (!overflow) {
+      char buf[24];
+      const int n = std::snprintf(buf, sizeof(buf), "%lld", v);
+      out.append(buf, static_cast<size_t>(n));
+      return true;
+    }
+    PyObject* s = PyLong_Type.tp_repr(o);
+    if (!s) return false;
+    Py_ssize_t n;
+    const char* p = PyUnicode_AsUTF8AndSize(s, &n);
+    if (p) out.append(p, static_cast<size_t>(n));
+    Py_DECREF(s);
+    return p != nullptr;
+  }
+
+  bool key(PyObject* k) {
+    if (PyUnicode_Check(k)) return str(k);
+    if (k == Py_True) { out.append("\"true\""); return true; }
+    if (k == Py_False) { out.append("\"false\""); return true; }
+    if (k == Py_None) { out.append("\"null\""); return true; }
+    if (PyLong_Check(k)) {
+      out.push_back('"');
+      if (!integer(k)) return false;
+      out.push_back('"');
+      return true;
+    }
+    if (PyFloat_Check(k)) {
+      out.push_back('"');
+      if (!flt(PyFloat_AS_DOUBLE(k))) return false;
+      out.push_back('"');
+      return true;
+    }
+    PyErr_Format(PyExc_TypeError, "keys must be str, int, float, bool or None, not %s", Py_TYPE(k)->tp_name);
+    return false;
+  }
+
+  bool value(PyObject* o, int depth) {
+    if (depth > kMaxDepth) {
+      PyErr_SetString(PyExc_ValueError, "Circular reference detected");
+      return false;
+    }
+    if (o == Py_None) { out.append("null"); return true; }
+    if (o == Py_True) { out.append("true"); return true; }
+    if (o == Py_False) { out.append("false"); return true; }
+    if (PyUnicode_Check(o)) return str(o);
+    if (PyLong_Check(o)) return integer(o);
+    if (PyFloat_Check(o)) return flt(PyFloat_AS_DOUBLE(o));
+    if (PyDict_Check(o)) {
+      out.push_back('{');
+      Py_ssize_t pos = 0;
+      PyObject *k, *v;
+      bool first = true;
+      while (PyDict_Next(o, &pos, &k, &v)) {
+        if (!first) out.push_back(',');
+        first = false;
+        if (!key(k)) return false;
+        out.push_back(':');
+        if (!value(v, depth + 1)) return false;
+      }
+      out.push_back('}');
+      return true;
+    }
+    if (PyList_Check(o) || PyTuple_Check(o)) {
+      PyObject* seq = o;
+      const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+      PyObject** items = PySequence_Fast_ITEMS(seq);
+      out.push_back('[');
+      for (Py_ssize_t i = 0; i < n; ++i) {
+        if (i) out.push_back(',');
+        if (!value(items[i], depth + 1)) return false;
+      }
+      out.push_back(']');
+      return true;
+    }
+    PyErr_Format(PyExc_TypeError, "Object of type %s is not JSON serializable", Py_TYPE(o)->tp_name);
+    return false;
+  }
+};
+
+PyObject* py_dumpb(PyObject*, PyObject* o) {
+  Encoder e;
+  e.out.reserve(1024);
+  if (!e.value(o, 0)) return nullptr;
+  return PyBytes_FromStringAndSize(e.out.data(), static_cast<Py_ssize_t>(e.out.size()));
+}
+
+PyObject* py_dumps(PyObject*, PyObject* o) {
+  Encoder e;
+  e.out.reserve(1024);
+  if (!e.value(o, 0)) return nullptr;
+  return PyUnicode_DecodeUTF8(e.out.data(), static_cast<Py_ssize_t>(e.out.size()), "strict");
+}
+
 PyObject* py_clear_key_cache(PyObject*, PyObject*) {
   clear_keys();
   Py_RETURN_NONE;
@@ -613,6 +770,8 @@ PyMethodDef methods[] = {
     {"create_merge_patch", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(py_merge_patch)),
      METH_FASTCALL, "RFC 7386 merge patch from old to new"},
     {"loads", py_loads, METH_O, "decode JSON (bytes, bytearray or str)"},
+    {"dumpb", py_dumpb, METH_O, "compact JSON as UTF-8 bytes"},
+    {"dumps", py_dumps, METH_O, "compact JSON as str"},
     {"clear_key_cache", py_clear_key_cache, METH_NOARGS, "drop the interned-key cache"},
     {nullptr, nullptr, 0, nullptr}};
 

@@ -155,12 +155,16 @@ def apply_json_patch(target: Any, ops: list) -> Any:
     return doc
 
 
-def dumps(x: Any) -> str:
+def py_dumps(x: Any) -> str:
     return json.dumps(x, separators=(",", ":"), ensure_ascii=False)
 
 
-def dumpb(x: Any) -> bytes:
+def py_dumpb(x: Any) -> bytes:
     return json.dumps(x, separators=(",", ":"), ensure_ascii=False).encode()
+
+
+dumps = py_dumps
+dumpb = py_dumpb
 
 
 py_loads = json.loads
@@ -175,7 +179,7 @@ NATIVE = False
 
 
 def _try_native() -> None:
-    global deepcopy, json_equal, create_merge_patch, loads, NATIVE
+    global deepcopy, json_equal, create_merge_patch, loads, dumps, dumpb, NATIVE
     import os
 
     if os.environ.get("CRON_OPERATOR_FASTJSON", "auto").lower() == "python":
@@ -192,6 +196,8 @@ def _try_native() -> None:
     json_equal = mod.json_equal
     create_merge_patch = mod.create_merge_patch
     loads = mod.loads
+    dumps = mod.dumps
+    dumpb = mod.dumpb
     NATIVE = True
 
 

@@ -32,7 +32,9 @@ def main() -> int:
 
     from cron_operator_amd.bench.harness import BenchConfig, run_sync, summarize
 
-    cfg = BenchConfig(n_crons=a.crons, steps=a.steps, warmup=a.warmup, transport=a.transport, mode=a.mode)
+    api_prof = a.out + ".apiserver.pstats" if a.transport == "http" else ""
+    cfg = BenchConfig(n_crons=a.crons, steps=a.steps, warmup=a.warmup, transport=a.transport, mode=a.mode,
+                      apiserver_profile=api_prof)
     prof = cProfile.Profile()
     t0, c0 = time.perf_counter(), time.process_time()
 
@@ -55,6 +57,10 @@ def main() -> int:
     st = pstats.Stats(prof, stream=buf)
     st.sort_stats("tottime").print_stats(a.top)
     st.sort_stats("cumulative").print_stats(a.top)
+    if api_prof and os.path.exists(api_prof):
+        buf.write("\n\n# ===== fake apiserver process, same timed steps =====\n")
+        ast = pstats.Stats(api_prof, stream=buf)
+        ast.sort_stats("tottime").print_stats(a.top)
     with open(a.out, "w") as fh:
         fh.write(buf.getvalue())
     print(summarize(res))

@@ -70,3 +70,38 @@ def test_keys_are_shared_and_cache_clear():
     assert next(iter(a)) is next(iter(b))  # interned through the key cache
     m.clear_key_cache()
     assert m.loads('{"metadata":1}') == {"metadata": 1}
+
+
+def _ref_dumps(v):
+    return json.dumps(v, separators=(",", ":"), ensure_ascii=False)
+
+
+@settings(max_examples=400, deadline=None)
+@given(json_values)
+def test_encoder_matches_json(v):
+    assert m.dumps(v) == _ref_dumps(v)
+    assert m.dumpb(v) == _ref_dumps(v).encode()
+
+
+@pytest.mark.parametrize("v", [float("inf"), float("-inf"), -0.0, 1e-7, 2 ** 80, -(2 ** 70), "\x00\x1f\u2028\"\\",
+                               (1, [2, (3,)]), {1: "a", 2.5: "b", None: "c", False: "d"}, 123456789.123])
+def test_encoder_edge_cases(v):
+    assert m.dumps(v) == _ref_dumps(v)
+
+
+def test_encoder_nan_and_errors():
+    assert m.dumps(float("nan")) == "NaN"
+    with pytest.raises(TypeError):
+        m.dumpb(object())
+    with pytest.raises(TypeError):
+        m.dumpb({(1, 2): 3})
+    with pytest.raises(UnicodeEncodeError):
+        m.dumpb("\ud800")
+    deep = []
+    cur = deep
+    for _ in range(3000):
+        nxt = []
+        cur.append(nxt)
+        cur = nxt
+    with pytest.raises(ValueError):
+        m.dumpb(deep)
