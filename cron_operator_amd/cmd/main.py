@@ -106,6 +106,9 @@ def build_parser() -> argparse.ArgumentParser:
                     help="'reference' reproduces every reference behaviour (live child LIST, finished=now, ...).")
     st.add_argument("--cron-engine", choices=["auto", "native", "python"], default="auto",
                     help="Cron next-fire engine implementation.")
+    st.add_argument("--sync-period", default="10h", help="Minimum frequency at which every watched object is "
+                                                        "reconciled again (controller-runtime's cache SyncPeriod; "
+                                                        "Go duration, 0 disables).")
     _add_bool(st, "--enable-tracing", False, "Record per-reconcile spans (served at /debug/traces on the probe port).")
     st.add_argument("--trace-file", default="", help="Also append finished spans here as JSON lines "
                                                      "(implies --enable-tracing).")
@@ -180,6 +183,13 @@ async def run_start(a: argparse.Namespace) -> int:
         log.error(e, "unable to get kubeconfig")
         return 1
     cfg.qps, cfg.burst = a.qps, a.burst
+    from ..utils.gotime import NANOS, parse_duration
+
+    try:
+        sync_period = parse_duration(a.sync_period) / NANOS if a.sync_period not in ("", "0") else 0.0
+    except ValueError as e:
+        log.error(e, "invalid --sync-period")
+        return 2
     client = Client(HttpTransport(cfg), qps=a.qps, burst=a.burst)
     mopts = ManagerOptions(namespace=a.namespace, leader_election=a.leader_elect,
                            leader_election_namespace=a.leader_elect_namespace,
@@ -187,7 +197,8 @@ async def run_start(a: argparse.Namespace) -> int:
                            metrics_cert_path=a.metrics_cert_path, metrics_cert_name=a.metrics_cert_name,
                            metrics_cert_key=a.metrics_cert_key,
                            health_probe_bind_address=a.health_probe_bind_address, enable_http2=a.enable_http2,
-                           max_concurrent_reconciles=a.max_concurrent_reconciles)
+                           max_concurrent_reconciles=a.max_concurrent_reconciles,
+                           sync_period=sync_period)
     try:
         mgr = Manager(client, mopts)
         opts = ReconcilerOptions.reference() if a.compat_mode == "reference" else ReconcilerOptions()

@@ -327,6 +327,8 @@ class CronReconciler(Reconciler):
         and no deletion started).  Such an event would only recompute what we
         just wrote.
         """
+        if old is new:  # periodic resync: always reconcile
+            return False
         m = new.get("metadata") or {}
         hit = self.own_writes.get(f"{m.get('namespace', '')}/{m.get('name', '')}")
         if hit is None:

@@ -12,6 +12,11 @@ served from an informer, and children are indexed by the
 the list's resourceVersion; a closed watch resumes from the last seen version;
 410 Expired triggers a relist whose diff is replayed as add/update/delete
 events.  Objects in the store are read-only snapshots.
+
+Periodic resync (controller-runtime's ``SyncPeriod``, default 10 h with up to
+10% jitter): every object in the store is re-delivered to the handlers as an
+update whose old and new object are the same, so every Cron is reconciled at
+least that often even if no event arrives (a safety net against missed events).
 """
 from __future__ import annotations
 
@@ -22,6 +27,8 @@ from typing import Any, Callable, Dict, Iterable, List, Optional, Set, Tuple
 from ..api import errors
 from ..api.meta import GroupVersionKind, GroupVersionResource
 from ..utils import jsonutil
+from ..utils.clock import Clock, TimerHandle
+from ..utils.gotime import NANOS
 from ..utils.logging import get_logger
 from .client import Client
 
@@ -80,8 +87,13 @@ class EventHandler:
 class Informer:
     def __init__(self, client: Client, target: Any, namespace: str = "", label_selector: Optional[str] = None,
                  field_selector: Optional[str] = None, indexers: Optional[Dict[str, IndexFunc]] = None,
-                 page_size: int = 500, name: str = ""):
+                 page_size: int = 500, name: str = "", resync_period: float = 0.0,
+                 clock: Optional[Clock] = None):
         self.client = client
+        self.resync_period = resync_period
+        self.clock = clock
+        self._resync_timer: Optional[TimerHandle] = None
+        self.resyncs = 0
         self.target = target
         self.namespace = namespace
         self.label_selector = label_selector
@@ -179,6 +191,27 @@ class Informer:
                 if h.on_update:
                     h.on_update(old, obj)
 
+    def resync(self) -> None:
+        """Re-deliver every stored object as an update with ``old is new``."""
+        self.resyncs += 1
+        for obj in list(self.store.values()):
+            for h in self.handlers:
+                if h.on_update:
+                    h.on_update(obj, obj)
+
+    def _arm_resync(self) -> None:
+        if self.resync_period <= 0 or self.clock is None or self._stopped:
+            return
+        delay = self.resync_period * (1.0 + 0.1 * random.random())
+        self._resync_timer = self.clock.call_later(int(delay * NANOS), self._on_resync)
+
+    def _on_resync(self) -> None:
+        self._resync_timer = None
+        if self._stopped:
+            return
+        self.resync()
+        self._arm_resync()
+
     def _replace(self, items: List[Dict[str, Any]]) -> None:
         seen = set()
         for obj in items:
@@ -246,10 +279,14 @@ class Informer:
     def start(self) -> asyncio.Task:
         if self._task is None:
             self._task = asyncio.get_running_loop().create_task(self.run(), name=f"informer:{self.name}")
+            self._arm_resync()
         return self._task
 
     async def stop(self) -> None:
         self._stopped = True
+        if self._resync_timer is not None:
+            self._resync_timer.cancel()
+            self._resync_timer = None
         if self._watch is not None:
             try:
                 self._watch.stop()
@@ -266,9 +303,12 @@ class Informer:
 class Cache:
     """Shared informers keyed by (resource, namespace, selector) -- ``cache.Cache``."""
 
-    def __init__(self, client: Client, namespace: str = ""):
+    def __init__(self, client: Client, namespace: str = "", resync_period: float = 0.0,
+                 clock: Optional[Clock] = None):
         self.client = client
         self.namespace = namespace
+        self.resync_period = resync_period
+        self.clock = clock
         self._informers: Dict[Tuple[Any, str, Optional[str]], Informer] = {}
         self._started = False
 
@@ -284,7 +324,8 @@ class Cache:
         inf = self._informers.get(key)
         if inf is None:
             inf = Informer(self.client, gvr, self.namespace, label_selector, indexers=indexers,
-                           name=f"{gvr.resource}.{gvr.group}" if gvr.group else gvr.resource)
+                           name=f"{gvr.resource}.{gvr.group}" if gvr.group else gvr.resource,
+                           resync_period=self.resync_period, clock=self.clock)
             self._informers[key] = inf
             if self._started:
                 inf.start()

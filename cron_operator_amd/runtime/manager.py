@@ -55,6 +55,8 @@ class ManagerOptions:
     enable_http2: bool = False
     max_concurrent_reconciles: int = 10
     cache_sync_timeout: float = 120.0
+    # controller-runtime's cache SyncPeriod: every object is re-reconciled at least this often
+    sync_period: float = 10 * 3600.0
 
 
 class Manager:
@@ -62,7 +64,7 @@ class Manager:
         self.client = client
         self.opts = options or ManagerOptions()
         self.clock = self.opts.clock
-        self.cache = Cache(client, self.opts.namespace)
+        self.cache = Cache(client, self.opts.namespace, self.opts.sync_period, self.clock)
         self.broadcaster = Broadcaster(client, self.clock)
         self.controllers: List[Controller] = []
         self.runnables: List[Callable[[], Awaitable[None]]] = []

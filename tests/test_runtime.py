@@ -371,3 +371,41 @@ def test_kubeconfig_load_and_precedence(monkeypatch):
         assert ic.host == "https://10.0.0.1:443" and ic.bearer_token_file.endswith("/token")
         with pytest.raises(ConfigError):
             load_kubeconfig(os.path.join(d, "missing"))
+
+
+# ---------------------------------------------------------------- periodic resync (controller-runtime SyncPeriod)
+
+
+async def test_periodic_resync_reconciles_idle_crons():
+    """A suspended Cron is never requeued; only the cache resync brings it back (SyncPeriod)."""
+    from cron_operator_amd.api.v1alpha1 import new_cron
+    from cron_operator_amd.testing.env import TestEnv
+
+    env = TestEnv()
+    tmpl = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob"}
+    await env.create_cron(new_cron("idle", "default", "*/1 * * * *", tmpl, suspend=True))
+    await env.start_manager(sync_period=600.0)
+    await env.settle()
+    before = env.controller.reconciles
+    await env.advance(300)
+    assert env.controller.reconciles == before  # nothing requeues a suspended Cron
+    await env.advance(400)  # past 600 s (+ <=10% jitter)
+    assert env.controller.reconciles == before + 1
+    infs = env.manager.cache.informers()
+    assert all(i.resyncs >= 1 for i in infs if i.synced.is_set())
+    await env.stop()
+
+
+async def test_resync_disabled_with_zero_period():
+    from cron_operator_amd.api.v1alpha1 import new_cron
+    from cron_operator_amd.testing.env import TestEnv
+
+    env = TestEnv()
+    await env.create_cron(new_cron("idle", "default", "*/1 * * * *", {"apiVersion": "kubeflow.org/v1",
+                                                                      "kind": "PyTorchJob"}, suspend=True))
+    await env.start_manager(sync_period=0.0)
+    await env.settle()
+    before = env.controller.reconciles
+    await env.advance(100 * 3600)
+    assert env.controller.reconciles == before
+    await env.stop()
