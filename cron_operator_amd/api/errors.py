@@ -11,25 +11,33 @@ from typing import Any, Dict, Optional
 
 
 class ApiError(Exception):
-    def __init__(self, code: int, reason: str, message: str, details: Optional[Dict[str, Any]] = None):
+    def __init__(self, code: int, reason: str, message: str, details: Optional[Dict[str, Any]] = None,
+                 retry_after: Optional[int] = None):
         super().__init__(message)
         self.code = code
         self.reason = reason
         self.message = message
         self.details = details or {}
+        # seconds from a Retry-After header / details.retryAfterSeconds (429s, overloaded apiserver)
+        self.retry_after = retry_after
 
     def status(self) -> Dict[str, Any]:
         st: Dict[str, Any] = {"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Failure",
                               "message": self.message, "reason": self.reason, "code": self.code}
-        if self.details:
-            st["details"] = self.details
+        details = dict(self.details)
+        if self.retry_after is not None:
+            details["retryAfterSeconds"] = self.retry_after
+        if details:
+            st["details"] = details
         return st
 
     @staticmethod
     def from_status(code: int, body: Any) -> "ApiError":
         if isinstance(body, dict) and body.get("kind") == "Status":
+            det = body.get("details") or {}
+            ra = det.get("retryAfterSeconds") if isinstance(det, dict) else None
             return ApiError(int(body.get("code") or code), body.get("reason") or _reason_for(code),
-                            body.get("message") or "", body.get("details"))
+                            body.get("message") or "", body.get("details"), ra if isinstance(ra, int) else None)
         text = body if isinstance(body, str) else str(body)
         return ApiError(code, _reason_for(code), text or f"HTTP {code}")
 

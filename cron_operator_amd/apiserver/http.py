@@ -92,12 +92,14 @@ class Request:
 
 
 class Response:
-    __slots__ = ("status", "body", "content_type")
+    __slots__ = ("status", "body", "content_type", "headers")
 
-    def __init__(self, status: int, body: bytes, content_type: str = "application/json"):
+    def __init__(self, status: int, body: bytes, content_type: str = "application/json",
+                 headers: Optional[Dict[str, str]] = None):
         self.status = status
         self.body = body
         self.content_type = content_type
+        self.headers = headers
 
 
 class WatchResponse:
@@ -122,7 +124,10 @@ def _event_line(etype: str, obj: Any) -> bytes:
 
 
 def _err(e: errors.ApiError) -> Response:
-    return _json(e.status(), e.code)
+    r = _json(e.status(), e.code)
+    if e.retry_after is not None:
+        r.headers = {"Retry-After": str(e.retry_after)}
+    return r
 
 
 class APIServerApp:
@@ -569,13 +574,15 @@ class _ServerConn(asyncio.Protocol):
 
     # --------------------------------------------------------------- replies
     def _reply(self, r: Response, keep: bool) -> None:
-        self._reply_raw(r.status, r.body, r.content_type, close=not keep)
+        self._reply_raw(r.status, r.body, r.content_type, close=not keep, headers=r.headers)
 
-    def _reply_raw(self, status: int, body: bytes, ctype: str, close: bool = False) -> None:
+    def _reply_raw(self, status: int, body: bytes, ctype: str, close: bool = False,
+                   headers: Optional[Dict[str, str]] = None) -> None:
         if self.transport is None or self.closed:
             return
+        extra = "".join(f"{k}: {v}\r\n" for k, v in headers.items()) if headers else ""
         head = (f"HTTP/1.1 {status} {_REASONS.get(status, 'Unknown')}\r\nContent-Type: {ctype}\r\n"
-                f"Content-Length: {len(body)}\r\n" + ("Connection: close\r\n" if close else "") + "\r\n")
+                f"Content-Length: {len(body)}\r\n{extra}" + ("Connection: close\r\n" if close else "") + "\r\n")
         self.transport.write(head.encode("latin-1") + body)
         if close:
             self.transport.close()

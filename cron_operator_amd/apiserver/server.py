@@ -72,6 +72,7 @@ class Fault:
     # True: the verb is applied and *then* the error is returned -- a lost response
     # (timeout after commit), the case deterministic job names exist for
     after: bool = False
+    retry_after: Optional[int] = None  # seconds: sent as Retry-After (APF-style 429 throttling)
 
     def matches(self, verb: str, resource: str, sub: Optional[str], name: Optional[str]) -> bool:
         if self.times == 0:
@@ -110,7 +111,7 @@ class FaultInjector:
             if f.after == after and f.matches(verb, resource, sub, name) and self._rng.random() < f.probability:
                 if f.times > 0:
                     f.times -= 1
-                raise errors.ApiError(f.code, f.reason, f.message)
+                raise errors.ApiError(f.code, f.reason, f.message, retry_after=f.retry_after)
 
     def delay_for(self, verb: str) -> float:
         return self.latency.get(verb, self.latency.get("*", 0.0))

@@ -41,7 +41,7 @@ class ConnectionFailed(Exception):
 
 class _Conn(asyncio.Protocol):
     __slots__ = ("transport", "buf", "fut", "alive", "used", "_state", "_status", "_clen", "_chunked",
-                 "_close_after", "_body", "_got_any")
+                 "_close_after", "_body", "_got_any", "retry_after")
 
     def __init__(self) -> None:
         self.transport: Optional[asyncio.Transport] = None
@@ -52,6 +52,7 @@ class _Conn(asyncio.Protocol):
         self._reset()
 
     def _reset(self) -> None:
+        self.retry_after: Optional[int] = None   # Retry-After of the last response (seconds)
         self._state = 0          # 0 headers, 1 body by length, 2 chunked, 3 until close
         self._status = 0
         self._clen = -1
@@ -103,6 +104,7 @@ class _Conn(asyncio.Protocol):
                 self._status = int(parts[1])
                 clen = -1
                 chunked = False
+                retry_after: Optional[int] = None
                 close = parts[0] == "HTTP/1.0"
                 for line in lines[1:]:
                     k, _, v = line.partition(":")
@@ -114,7 +116,13 @@ class _Conn(asyncio.Protocol):
                     elif k == "connection":
                         lv = v.strip().lower()
                         close = lv == "close" if lv in ("close", "keep-alive") else close
+                    elif k == "retry-after":
+                        try:
+                            retry_after = int(v.strip())
+                        except ValueError:
+                            retry_after = None
                 self._close_after = close
+                self.retry_after = retry_after if self._status >= 400 else None
                 if self._status in (204, 304) or 100 <= self._status < 200:
                     if 100 <= self._status < 200:  # interim response: parse the next head
                         continue
@@ -163,7 +171,7 @@ class _Conn(asyncio.Protocol):
 
     def _finish(self) -> None:
         fut = self.fut
-        status, body = self._status, bytes(self._body)
+        status, body, ra = self._status, bytes(self._body), self.retry_after
         if self._close_after:
             self.alive = False
             if self.transport is not None:
@@ -171,7 +179,7 @@ class _Conn(asyncio.Protocol):
         self._reset()
         self.fut = None
         if fut is not None and not fut.done():
-            fut.set_result((status, body))
+            fut.set_result((status, body, ra))
 
     # --------------------------------------------------------------- client side
     def send(self, data: bytes) -> asyncio.Future:
@@ -240,6 +248,12 @@ class HttpPool:
 
     async def request(self, method: str, path: str, body: Optional[bytes] = None,
                       content_type: str = "application/json") -> Tuple[int, bytes]:
+        status, raw, _ = await self.request_full(method, path, body, content_type)
+        return status, raw
+
+    async def request_full(self, method: str, path: str, body: Optional[bytes] = None,
+                           content_type: str = "application/json") -> Tuple[int, bytes, Optional[int]]:
+        """``(status, body, Retry-After seconds or None)``."""
         head = f"{method} {self.base_path}{path} HTTP/1.1\r\n{self._fixed}"
         if body is not None:
             head += f"Content-Type: {content_type}\r\nContent-Length: {len(body)}\r\n\r\n"
@@ -254,7 +268,7 @@ class HttpPool:
             fut = conn.send(data)
             timer = asyncio.get_running_loop().call_later(self.timeout, _expire, fut)
             try:
-                status, raw = await fut
+                status, raw, retry_after = await fut
             except ConnectionFailed as e:
                 conn.alive = False
                 if attempt == 0 and e.no_response and e.reused:
@@ -273,7 +287,7 @@ class HttpPool:
             finally:
                 timer.cancel()
             self._give_back(conn)
-            return status, raw
+            return status, raw, retry_after
         raise ConnectionFailed("unreachable", True, False)  # pragma: no cover
 
     async def close(self) -> None:

@@ -19,6 +19,7 @@ import aiohttp
 from ..api import errors
 from ..api.meta import GroupVersion, GroupVersionResource
 from ..utils import jsonutil
+from . import metrics
 from .client import DISCARD, PATCH_CONTENT_TYPES, Transport, WatchStream
 from .fasthttp import ConnectionFailed, HttpPool, encode_query
 from .kubeconfig import RestConfig
@@ -79,8 +80,13 @@ _METHODS = {"get": "GET", "list": "GET", "create": "POST", "update": "PUT", "pat
 
 
 class HttpTransport(Transport):
-    def __init__(self, config: RestConfig, pool_size: int = 64, timeout: float = 60.0, fast: bool = True):
+    def __init__(self, config: RestConfig, pool_size: int = 64, timeout: float = 60.0, fast: bool = True,
+                 max_retries: int = 10):
         self.config = config
+        # client-go rest.Request: a 429/5xx carrying Retry-After is retried after that many seconds,
+        # up to maxRetries (10) times -- how an apiserver under API Priority and Fairness sheds load
+        self.max_retries = max_retries
+        self.retries = 0
         self.host = config.host.split("://", 1)[-1]
         self._pool_size = pool_size
         self._timeout = timeout
@@ -120,11 +126,19 @@ class HttpTransport(Transport):
         if self.fast:
             data = jsonutil.dumpb(body) if body is not None else None
             ctype = PATCH_CONTENT_TYPES[params.get("patchType", "merge")] if verb == "patch" else "application/json"
-            try:
-                status, raw = await self._fast_pool().request(method, path + encode_query(_clean(params)), data,
-                                                              ctype)
-            except (ConnectionFailed, OSError, asyncio.TimeoutError) as e:
-                raise errors.ApiError(503, "ServiceUnavailable", f"connection error: {e}") from None
+            target = path + encode_query(_clean(params))
+            attempt = 0
+            while True:
+                try:
+                    status, raw, retry_after = await self._fast_pool().request_full(method, target, data, ctype)
+                except (ConnectionFailed, OSError, asyncio.TimeoutError) as e:
+                    raise errors.ApiError(503, "ServiceUnavailable", f"connection error: {e}") from None
+                if retry_after is None or not (status == 429 or status >= 500) or attempt >= self.max_retries:
+                    break
+                attempt += 1
+                self.retries += 1
+                metrics.REST_RETRIES.labels(str(status), method, self.host).inc()
+                await asyncio.sleep(max(0, retry_after))
             if status >= 400:
                 try:
                     err_body: Any = jsonutil.loads(raw)

@@ -79,6 +79,9 @@ WQ_RETRIES = Counter("workqueue_retries_total", "Total number of retries handled
 REST_REQUESTS = Counter("rest_client_requests_total",
                         "Number of HTTP requests, partitioned by status code, method, and host.",
                         ["code", "host", "method"], registry=REGISTRY)
+REST_RETRIES = Counter("rest_client_request_retries_total",
+                       "Number of request retries, partitioned by status code, verb, and host.",
+                       ["code", "verb", "host"], registry=REGISTRY)
 REST_LATENCY = Histogram("rest_client_request_duration_seconds", "Request latency in seconds. Broken down by verb, "
                          "and host.", ["verb", "host"],
                          buckets=(0.005, 0.025, 0.1, 0.25, 0.5, 1.0, 2.0, 4.0, 8.0, 15.0, 30.0, 60.0),

@@ -89,7 +89,7 @@ async def test_parser_handles_byte_by_byte_delivery():
     fut = c.send(b"GET / HTTP/1.1\r\n\r\n")
     for b in b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n3\r\nabc\r\n0\r\n\r\n":
         c.data_received(bytes([b]))
-    assert fut.done() and fut.result() == (200, b"abc")
+    assert fut.done() and fut.result() == (200, b"abc", None)
     assert loop is asyncio.get_running_loop()
 
 
@@ -158,3 +158,37 @@ async def test_fresh_connection_failure_raises_and_timeout():
 def test_encode_query():
     assert encode_query({}) == ""
     assert encode_query({"labelSelector": "kubedl.io/cron-name=a b"}) == "?labelSelector=kubedl.io%2Fcron-name%3Da+b"
+
+
+async def test_retry_after_429_is_honoured_by_http_transport():
+    """client-go semantics: 429 + Retry-After is retried (here with Retry-After: 0), 429 without it is not."""
+    from cron_operator_amd.api import errors
+    from cron_operator_amd.api.v1alpha1 import CRON_GVR
+    from cron_operator_amd.apiserver.http import APIServerApp
+    from cron_operator_amd.runtime.client import Client
+    from cron_operator_amd.runtime.http import HttpTransport
+    from cron_operator_amd.runtime.kubeconfig import RestConfig
+    from cron_operator_amd.testing.env import TestEnv
+
+    env = TestEnv()
+    app = APIServerApp(env.server)
+    port = await app.start("127.0.0.1", 0)
+    tr = HttpTransport(RestConfig(host=f"http://127.0.0.1:{port}"))
+    client = Client(tr, qps=-1)
+    try:
+        env.server.faults.add(verb="list", resource="crons", code=429, reason="TooManyRequests", times=3,
+                              retry_after=0)
+        assert (await client.list(CRON_GVR, "default"))["items"] == []
+        assert tr.retries == 3
+        env.server.faults.add(verb="list", resource="crons", code=429, reason="TooManyRequests", times=1)
+        with pytest.raises(errors.ApiError) as ei:
+            await client.list(CRON_GVR, "default")
+        assert ei.value.code == 429 and tr.retries == 3
+        env.server.faults.add(verb="get", resource="crons", code=503, reason="ServiceUnavailable", retry_after=0)
+        tr.max_retries = 2
+        with pytest.raises(errors.ApiError) as ei:
+            await client.get(CRON_GVR, "default", "x")
+        assert ei.value.code == 503 and ei.value.retry_after == 0 and tr.retries == 5
+    finally:
+        await client.close()
+        await app.stop()
