@@ -307,6 +307,11 @@ class APIServerApp:
             w = s.watch(gvr, ns or None, q.get("resourceVersion", ""), q.get("labelSelector"), q.get("fieldSelector"),
                         q.get("allowWatchBookmarks") in ("true", "1"), copy_events=False)
             return WatchResponse(w, float(q.get("timeoutSeconds") or 1800))
+        if verb in ("get", "list") and "as=Table" in req.headers.get("accept", ""):
+            from .table import wants_table
+
+            if wants_table(req.headers["accept"]):
+                return self._table(req, gvr, ns, name)
         body: Any = None
         ptype = "merge"
         if verb in ("create", "update", "patch", "delete"):
@@ -330,6 +335,23 @@ class APIServerApp:
         if s.faults.faults:  # "lost response" faults fire after the verb was applied
             s.faults.check(verb, gvr.resource, sub or None, name or None, after=True)
         return resp
+
+    def _table(self, req: Request, gvr: GroupVersionResource, ns: str, name: str) -> Response:
+        """``kubectl get``'s server-side printing (see :mod:`.table`)."""
+        from .table import printer_columns_of, to_table
+
+        s = self.server
+        q = req.query
+        ri = s.resource(gvr)
+        if name:
+            objs = [s.get(gvr, ns, name)]
+            rv = objs[0]["metadata"].get("resourceVersion", "")
+        else:
+            lst = s.list(gvr, ns or None, q.get("labelSelector"), q.get("fieldSelector"), copy=False)
+            objs = lst["items"]
+            rv = lst["metadata"].get("resourceVersion", "")
+        return Response(200, jsonutil.dumpb(to_table(printer_columns_of(ri), objs, s.clock.now_ns(), rv,
+                                                      q.get("includeObject", "Metadata"))))
 
     def _apply(self, verb: str, gvr: GroupVersionResource, ns: str, name: str, sub: str, body: Any, ptype: Any,
                q: Dict[str, str]) -> Response:

@@ -33,10 +33,11 @@ from __future__ import annotations
 
 import argparse
 import asyncio
+import json
 import os
 import signal
 import sys
-from typing import List, Optional
+from typing import Any, List, Optional
 
 from .. import __version__
 
@@ -128,6 +129,15 @@ def build_parser() -> argparse.ArgumentParser:
     _add_bool(fa, "--training-operator", False, "Also run the fake training-operator (timed mode).")
     fa.add_argument("--job-duration", type=float, default=30.0, help="Seconds a job runs in timed mode.")
 
+    gt = sub.add_parser("get", help="List Crons (or one Cron) like `kubectl get crons`")
+    gt.add_argument("resource", nargs="?", default="crons", help="crons | cron (kubectl aliases accepted)")
+    gt.add_argument("name", nargs="?", default="")
+    gt.add_argument("-n", "--namespace", default="default")
+    gt.add_argument("-A", "--all-namespaces", action="store_true")
+    gt.add_argument("-l", "--selector", default="")
+    gt.add_argument("-o", "--output", default="", choices=["", "wide", "json", "yaml", "name"])
+    gt.add_argument("--kubeconfig", default="")
+    gt.add_argument("--no-headers", action="store_true")
     sub.add_parser("crd", help="Print the Cron CustomResourceDefinition")
     kz = sub.add_parser("kustomize", help="Render a kustomization directory (kustomize build)")
     kz.add_argument("dir", nargs="?", default="deploy/kustomize/default")
@@ -280,6 +290,56 @@ async def run_fake_apiserver(a: argparse.Namespace) -> int:
     return 0
 
 
+async def run_get(a: argparse.Namespace) -> int:
+    import yaml
+
+    from ..api import errors
+    from ..api.v1alpha1 import CRON_GVR
+    from ..apiserver.table import render
+    from ..runtime.client import Client
+    from ..runtime.http import HttpTransport
+    from ..runtime.kubeconfig import ConfigError, get_config
+
+    if a.resource.lower() not in ("crons", "cron", "crons.apps.kubedl.io", "cron.apps.kubedl.io"):
+        print(f'error: the server doesn\'t have a resource type "{a.resource}"', file=sys.stderr)
+        return 1
+    try:
+        cfg = get_config(a.kubeconfig)
+    except ConfigError as e:
+        print(f"error: {e}", file=sys.stderr)
+        return 1
+    client = Client(HttpTransport(cfg), qps=-1)
+    ns = "" if a.all_namespaces else a.namespace
+    try:
+        if a.output in ("json", "yaml", "name"):
+            if a.name:
+                data: Any = await client.get(CRON_GVR, ns, a.name)
+                items = [data]
+            else:
+                data = await client.list(CRON_GVR, ns, a.selector or None)
+                items = data.get("items") or []
+            if a.output == "name":
+                sys.stdout.write("".join(f"cron.apps.kubedl.io/{o['metadata']['name']}\n" for o in items))
+            elif a.output == "json":
+                sys.stdout.write(json.dumps(data, indent=4) + "\n")
+            else:
+                sys.stdout.write(yaml.safe_dump(data, sort_keys=False))
+            return 0
+        table = await client.table(CRON_GVR, ns, a.name, a.selector or None)
+        if not table.get("rows"):
+            where = "any namespace" if a.all_namespaces else f"{ns} namespace"
+            print(f"No resources found in {where}.", file=sys.stderr)
+            return 0
+        sys.stdout.write(render(table, wide=a.output == "wide", namespace_column=a.all_namespaces,
+                                no_headers=a.no_headers))
+        return 0
+    except errors.ApiError as e:
+        print(f"Error from server ({e.reason}): {e.message}", file=sys.stderr)
+        return 1
+    finally:
+        await client.close()
+
+
 def _helm_template(a: argparse.Namespace) -> int:
     import yaml
 
@@ -328,6 +388,8 @@ def main(argv: Optional[List[str]] = None) -> int:
 
         sys.stdout.write(crd_yaml())
         return 0
+    if a.command == "get":
+        return asyncio.run(run_get(a))
     if a.command == "kustomize":
         from ..utils.kustomize import build_yaml
 

@@ -39,8 +39,10 @@ PATCH_CONTENT_TYPES = {
 }
 
 
-# request-parameter key (never sent): the caller ignores the response body
-DISCARD = "_discardResponse"
+# request-parameter keys (never sent as query parameters):
+DISCARD = "_discardResponse"   # the caller ignores the response body
+ACCEPT = "_accept"             # Accept header override (server-side printing)
+TABLE_ACCEPT = "application/json;as=Table;v=v1;g=meta.k8s.io,application/json"
 
 
 class Transport:
@@ -111,6 +113,16 @@ class InMemoryTransport(Transport):
                       subresource: str = "", body: Any = None, params: Optional[Dict[str, Any]] = None) -> Any:
         params = params or {}
         await self._gate(verb, gvr.resource, subresource, name)
+        if params.get(ACCEPT) and verb in ("get", "list"):
+            from ..apiserver.table import printer_columns_of, to_table, wants_table
+
+            if wants_table(params[ACCEPT]):
+                s = self.server
+                if name:
+                    objs = [s.get(gvr, namespace, name)]
+                else:
+                    objs = s.list(gvr, namespace or None, params.get("labelSelector"))["items"]
+                return to_table(printer_columns_of(s.resource(gvr)), objs, s.clock.now_ns())
         out = self._apply(verb, gvr, namespace, name, subresource, body, params)
         faults = self.server.faults
         if faults.faults:
@@ -295,6 +307,14 @@ class Client:
         if continue_:
             params["continue"] = continue_
         return await self._do("list", await self._gvr(target), namespace, params=params)
+
+    async def table(self, target: GVRorGVK, namespace: str = "", name: str = "",
+                    label_selector: Optional[str] = None) -> Dict[str, Any]:
+        """``kubectl get`` data: a ``meta.k8s.io/v1`` Table from server-side printing (HTTP transports)."""
+        params: Dict[str, Any] = {ACCEPT: TABLE_ACCEPT}
+        if label_selector:
+            params["labelSelector"] = label_selector
+        return await self._do("get" if name else "list", await self._gvr(target), namespace, name, params=params)
 
     async def list_all(self, target: GVRorGVK, namespace: str = "", label_selector: Optional[str] = None,
                        page_size: int = 500) -> Dict[str, Any]:

@@ -213,8 +213,8 @@ class HttpPool:
             self.ssl = _ssl.create_default_context()
         self.server_hostname = server_hostname
         hosthdr = self.host if (self.port in (80, 443)) else f"{self.host}:{self.port}"
-        hdrs = {"User-Agent": "cron-operator-amd", "Accept": "application/json"}
-        hdrs.update(headers or {})
+        hdrs = {"User-Agent": "cron-operator-amd"}
+        hdrs.update({k: v for k, v in (headers or {}).items() if k.lower() != "accept"})
         extra = "".join(f"{k}: {v}\r\n" for k, v in hdrs.items())
         self._fixed = f"Host: {hosthdr}\r\n{extra}"
         self._idle: Deque[_Conn] = deque()
@@ -252,9 +252,10 @@ class HttpPool:
         return status, raw
 
     async def request_full(self, method: str, path: str, body: Optional[bytes] = None,
-                           content_type: str = "application/json") -> Tuple[int, bytes, Optional[int]]:
+                           content_type: str = "application/json",
+                           accept: str = "application/json") -> Tuple[int, bytes, Optional[int]]:
         """``(status, body, Retry-After seconds or None)``."""
-        head = f"{method} {self.base_path}{path} HTTP/1.1\r\n{self._fixed}"
+        head = f"{method} {self.base_path}{path} HTTP/1.1\r\n{self._fixed}Accept: {accept}\r\n"
         if body is not None:
             head += f"Content-Type: {content_type}\r\nContent-Length: {len(body)}\r\n\r\n"
             data = head.encode("latin-1") + body

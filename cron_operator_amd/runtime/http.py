@@ -20,7 +20,7 @@ from ..api import errors
 from ..api.meta import GroupVersion, GroupVersionResource
 from ..utils import jsonutil
 from . import metrics
-from .client import DISCARD, PATCH_CONTENT_TYPES, Transport, WatchStream
+from .client import ACCEPT, DISCARD, PATCH_CONTENT_TYPES, Transport, WatchStream
 from .fasthttp import ConnectionFailed, HttpPool, encode_query
 from .kubeconfig import RestConfig
 
@@ -130,7 +130,8 @@ class HttpTransport(Transport):
             attempt = 0
             while True:
                 try:
-                    status, raw, retry_after = await self._fast_pool().request_full(method, target, data, ctype)
+                    status, raw, retry_after = await self._fast_pool().request_full(
+                        method, target, data, ctype, params.get(ACCEPT) or "application/json")
                 except (ConnectionFailed, OSError, asyncio.TimeoutError) as e:
                     raise errors.ApiError(503, "ServiceUnavailable", f"connection error: {e}") from None
                 if retry_after is None or not (status == 429 or status >= 500) or attempt >= self.max_retries:
@@ -149,7 +150,7 @@ class HttpTransport(Transport):
                 return None
             return jsonutil.loads(raw) if raw else None
         url = self.config.host + path
-        headers = {"Accept": "application/json"}
+        headers = {"Accept": params.get(ACCEPT) or "application/json"}
         data = None
         if body is not None:
             data = jsonutil.dumpb(body)
