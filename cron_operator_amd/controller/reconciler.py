@@ -302,7 +302,7 @@ class CronReconciler(Reconciler):
         patch = jsonutil.create_merge_patch({"status": old_status}, {"status": new_status} if new_status else {})
         if not patch and self.opts.skip_noop_patch:
             self.stats["noop_patches_skipped"] += 1
-            metrics.STATUS_PATCHES.labels("skipped").inc()
+            metrics.child(metrics.STATUS_PATCHES, "skipped").inc()
             return
         m = old_obj.get("metadata") or {}
         key = f"{m.get('namespace', '')}/{m.get('name', '')}"
@@ -317,7 +317,7 @@ class CronReconciler(Reconciler):
             self.own_writes.pop(key, None)
             raise
         self.stats["patches"] += 1
-        metrics.STATUS_PATCHES.labels("ok").inc()
+        metrics.child(metrics.STATUS_PATCHES, "ok").inc()
 
     def is_own_write(self, old: Optional[Dict[str, Any]], new: Dict[str, Any]) -> bool:
         """Predicate helper: is this Cron update exactly our last status write?
@@ -447,7 +447,7 @@ class CronReconciler(Reconciler):
                     await self.client.delete(gvk, m.get("namespace", ""), m.get("name", ""),
                                              propagation_policy="Background", discard_response=True)
                     self.stats["deletes"] += 1
-                    metrics.WORKLOADS_DELETED.labels(gvk.kind, "replace").inc()
+                    metrics.child(metrics.WORKLOADS_DELETED, gvk.kind, "replace").inc()
                 except errors.ApiError as e:
                     if not errors.is_not_found(e):
                         if self.opts.expectations:
@@ -475,7 +475,7 @@ class CronReconciler(Reconciler):
                 created = await self.client.create(gvk, workload, wm.get("namespace", ""))
                 sp.set(tick_to_create_ms=(self.clock.now_ns() - missed_run.unix_nano()) / 1e6)
             self.stats["creates"] += 1
-            metrics.WORKLOADS_CREATED.labels(gvk.kind).inc()
+            metrics.child(metrics.WORKLOADS_CREATED, gvk.kind).inc()
             if self.opts.expectations:
                 self.expect.expect_create(self._ckey(cron), created)
             if self.opts.fold_created_into_active:
@@ -487,7 +487,7 @@ class CronReconciler(Reconciler):
                     resource_version=cm.get("resourceVersion", "") if self.opts.active_ref_resource_version else ""))
             if self.latency_observer is not None:
                 self.latency_observer(self._ckey(cron), missed_run, created)
-            metrics.SCHEDULE_LATENCY.labels("cron").observe(
+            metrics.child(metrics.SCHEDULE_LATENCY, "cron").observe(
                 max(0.0, (self.clock.now_ns() - missed_run.unix_nano()) / 1e9))
         except errors.ApiError as e:
             if self.opts.expectations:
@@ -629,7 +629,7 @@ class CronReconciler(Reconciler):
                     await self.client.delete(wgvk, m.get("namespace", ""), m.get("name", ""),
                                              propagation_policy="Background", discard_response=True)
                     self.stats["deletes"] += 1
-                    metrics.WORKLOADS_DELETED.labels(wgvk.kind, "history").inc()
+                    metrics.child(metrics.WORKLOADS_DELETED, wgvk.kind, "history").inc()
                 except errors.ApiError as e:
                     if not errors.is_not_found(e):
                         if self.opts.expectations:

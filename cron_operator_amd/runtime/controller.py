@@ -170,7 +170,7 @@ class Controller:
 
     def _count(self, label: str) -> None:
         self.result_counts[label] = self.result_counts.get(label, 0) + 1
-        metrics.RECONCILE_TOTAL.labels(self.name, label).inc()
+        metrics.child(metrics.RECONCILE_TOTAL, self.name, label).inc()
 
     async def process_one(self, req: Request) -> None:
         q = self.queue

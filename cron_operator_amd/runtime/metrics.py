@@ -109,5 +109,18 @@ MISSED_TICKS = Counter("cron_operator_missed_ticks_total", "Scheduled ticks coll
 STATUS_PATCHES = Counter("cron_operator_status_patches_total", "Cron status writes.", ["result"], registry=REGISTRY)
 
 
+_CHILDREN: dict = {}
+
+
+def child(metric, *labels: str):
+    """``metric.labels(*labels)`` memoised: prometheus_client's ``labels()`` takes a lock and
+    builds a key tuple on every call, which showed up in the reconcile hot path."""
+    key = (id(metric), labels)
+    c = _CHILDREN.get(key)
+    if c is None:
+        c = _CHILDREN[key] = metric.labels(*labels)
+    return c
+
+
 def exposition() -> bytes:
     return generate_latest(REGISTRY)
