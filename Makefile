@@ -115,7 +115,8 @@ build-installer: manifests ## Render deploy/kustomize/default into dist/install.
 ##@ Helm
 
 .PHONY: helm-unittest
-helm-unittest: ## Chart rendering tests (charts/cron-operator/tests analog).
+helm-unittest: ## Run the chart's helm-unittest suites (charts/cron-operator/tests) + chart render tests.
+	$(PYTHON) -m cron_operator_amd.utils.helmunittest
 	$(PYTHON) -m pytest tests/test_helm_chart.py $(PYTEST_ARGS)
 
 .PHONY: helm-template

@@ -171,3 +171,39 @@ def test_engine_basics():
     assert _r("{{ and 1 0 }}{{ or 0 2 }}") == "02"
     with pytest.raises(TemplateError):
         _r('{{ required "need x" .x }}')
+
+
+# ---------------------------------------------------------------- helm-unittest suites (charts/cron-operator/tests)
+
+
+def test_helm_unittest_suites_pass():
+    """The chart's helm-unittest suites (reference tier: charts/cron-operator/tests, Makefile:158-160)."""
+    from cron_operator_amd.utils.helmunittest import run_all
+
+    passed, failed, results = run_all(CHART)
+    assert failed == 0, [(r.suite, r.name, r.failures) for r in results if not r.passed]
+    assert passed >= 25
+
+
+def test_helm_unittest_runner_detects_failures(tmp_path):
+    from cron_operator_amd.utils.helmunittest import get_path, run_suite
+
+    doc = {"spec": {"containers": [{"name": "a", "args": ["x"]}, {"name": "b"}]},
+           "metadata": {"labels": {"app.kubernetes.io/name": "n"}}}
+    assert get_path(doc, "spec.containers[?(@.name=='b')].name") == "b"
+    assert get_path(doc, 'metadata.labels["app.kubernetes.io/name"]') == "n"
+    suite = tmp_path / "bad_test.yaml"
+    suite.write_text("""
+suite: negative
+templates: [deployment.yaml]
+tests:
+  - it: wrong replicas
+    asserts:
+      - equal: {path: spec.replicas, value: 7}
+  - it: negated assertion
+    asserts:
+      - isKind: {of: Deployment}
+        not: true
+""")
+    res = run_suite(str(suite), CHART)
+    assert [r.passed for r in res] == [False, False]
