@@ -101,6 +101,11 @@ class HttpTransport(Transport):
                                   timeout=self._timeout, server_hostname=self.config.tls_server_name or None)
         return self._pool
 
+    def _tls_kw(self) -> Dict[str, Any]:
+        """kubeconfig ``tls-server-name``: verify the certificate against this name."""
+        name = self.config.tls_server_name
+        return {"server_hostname": name} if name and self.config.host.startswith("https://") else {}
+
     def _sess(self) -> aiohttp.ClientSession:
         if self._session is None or self._session.closed:
             conn = aiohttp.TCPConnector(limit=self._pool_size, ssl=self.config.ssl_context() or False,
@@ -159,7 +164,7 @@ class HttpTransport(Transport):
         timeout = aiohttp.ClientTimeout(total=self._timeout)
         try:
             async with self._sess().request(method, url, params=_clean(params), data=data, headers=headers,
-                                            timeout=timeout) as resp:
+                                            timeout=timeout, **self._tls_kw()) as resp:
                 if resp.status >= 400:
                     await self._raise(resp)
                 raw = await resp.read()
@@ -174,7 +179,7 @@ class HttpTransport(Transport):
         p["watch"] = "true"
         timeout = aiohttp.ClientTimeout(total=None, sock_connect=self._timeout)
         try:
-            resp = await self._sess().get(url, params=p, timeout=timeout)
+            resp = await self._sess().get(url, params=p, timeout=timeout, **self._tls_kw())
         except aiohttp.ClientConnectionError as e:
             raise errors.ApiError(503, "ServiceUnavailable", f"connection error: {e}") from None
         if resp.status >= 400:
@@ -188,7 +193,7 @@ class HttpTransport(Transport):
         path = f"/api/{group_version.version}" if not group_version.group else \
             f"/apis/{group_version.group}/{group_version.version}"
         try:
-            async with self._sess().get(self.config.host + path) as resp:
+            async with self._sess().get(self.config.host + path, **self._tls_kw()) as resp:
                 if resp.status >= 400:
                     await self._raise(resp)
                 doc = json.loads(await resp.read())

@@ -192,3 +192,49 @@ async def test_retry_after_429_is_honoured_by_http_transport():
     finally:
         await client.close()
         await app.stop()
+
+
+async def test_https_apiserver_with_ca_and_bearer_token(tmp_path):
+    """TLS end to end: the fake apiserver serves HTTPS, the client verifies it against the CA from the
+    kubeconfig-style RestConfig, sends a bearer token, and watches over the same TLS endpoint."""
+    import ssl
+
+    from cron_operator_amd.api.v1alpha1 import CRON_GVR, new_cron
+    from cron_operator_amd.apiserver.http import APIServerApp
+    from cron_operator_amd.runtime.client import Client
+    from cron_operator_amd.runtime.http import HttpTransport
+    from cron_operator_amd.runtime.kubeconfig import RestConfig
+    from cron_operator_amd.runtime.servers import self_signed_cert
+    from cron_operator_amd.testing.env import TestEnv
+
+    cert, key = self_signed_cert(str(tmp_path), host="localhost")
+    ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+    ctx.load_cert_chain(cert, key)
+    env = TestEnv()
+    env.server.tokens = {"tok": {"username": "admin", "groups": ["system:masters"]}}
+    app = APIServerApp(env.server)
+    port = await app.start("127.0.0.1", 0, ssl_context=ctx)
+    with open(cert, "rb") as fh:
+        ca = fh.read()
+    cfg = RestConfig(host=f"https://127.0.0.1:{port}", bearer_token="tok", ca_data=ca, tls_server_name="localhost")
+    client = Client(HttpTransport(cfg), qps=-1)
+    try:
+        obj = new_cron("tls", "default", "@daily", {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob"}).to_dict()
+        created = await client.create(CRON_GVR, obj, "default")
+        w = await client.watch(CRON_GVR, "default", resource_version=created["metadata"]["resourceVersion"])
+        await client.patch(CRON_GVR, "default", "tls", {"metadata": {"labels": {"a": "b"}}})
+        et, ev = await asyncio.wait_for(w.__anext__(), 5)
+        assert et == "MODIFIED" and ev["metadata"]["labels"] == {"a": "b"}
+        w.stop()
+        # wrong token over TLS -> 401
+        bad = Client(HttpTransport(RestConfig(host=cfg.host, bearer_token="nope", ca_data=ca,
+                                              tls_server_name="localhost")), qps=-1)
+        from cron_operator_amd.api import errors
+
+        with pytest.raises(errors.ApiError) as ei:
+            await bad.get(CRON_GVR, "default", "tls")
+        assert ei.value.code == 401
+        await bad.close()
+    finally:
+        await client.close()
+        await app.stop()
