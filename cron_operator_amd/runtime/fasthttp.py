@@ -19,7 +19,10 @@ This module is exactly that, on ``asyncio.Protocol``:
   fresh connection, as Go's ``net/http`` does; the operator's writes are
   idempotent anyway (deterministic names, merge patches).
 
-Watch streams stay on aiohttp (few, long-lived); see :mod:`.http`.
+Watch streams (:meth:`HttpPool.open_stream`) get a dedicated connection whose
+protocol de-chunks the body, splits it into lines and decodes each line as it
+arrives, so an informer receives ready-made events in batches (no per-line
+stream-reader round trips).
 """
 from __future__ import annotations
 
@@ -192,6 +195,149 @@ class _Conn(asyncio.Protocol):
         return self.fut
 
 
+class HttpStatusError(Exception):
+    """A streaming request was answered with an error status."""
+
+    def __init__(self, status: int, body: bytes):
+        super().__init__(f"HTTP {status}")
+        self.status = status
+        self.body = body
+
+
+class _StreamConn(asyncio.Protocol):
+    """One streaming response (chunked or read-to-close), split into decoded lines."""
+
+    def __init__(self, decode):
+        self.decode = decode
+        self.transport: Optional[asyncio.Transport] = None
+        self.buf = bytearray()
+        self.lines = bytearray()
+        self.items: Deque = deque()
+        self.ready = asyncio.Event()
+        self.head: Optional[asyncio.Future] = None
+        self.status = 0
+        self.chunked = False
+        self.done = False
+        self.error: Optional[BaseException] = None
+        self._err_body = bytearray()
+        self._clen = -1
+
+    def connection_made(self, transport: asyncio.BaseTransport) -> None:
+        self.transport = transport  # type: ignore[assignment]
+
+    def connection_lost(self, exc: Optional[BaseException]) -> None:
+        self.done = True
+        if self.head is not None and not self.head.done():
+            if self.status >= 400:
+                self.head.set_exception(HttpStatusError(self.status, bytes(self._err_body)))
+            else:
+                self.head.set_exception(ConnectionFailed(f"stream closed: {exc or 'by peer'}", True, False))
+        self.ready.set()
+
+    def data_received(self, data: bytes) -> None:
+        self.buf += data
+        try:
+            self._parse()
+        except Exception as e:  # noqa: BLE001 - malformed stream: end it
+            self.error = e
+            self.done = True
+            self.ready.set()
+            if self.transport is not None:
+                self.transport.close()
+
+    def _parse(self) -> None:
+        buf = self.buf
+        if self.status == 0:
+            end = buf.find(b"\r\n\r\n")
+            if end < 0:
+                return
+            lines = bytes(buf[:end]).decode("latin-1").split("\r\n")
+            del buf[:end + 4]
+            self.status = int(lines[0].split(" ", 2)[1])
+            for line in lines[1:]:
+                k, _, v = line.partition(":")
+                k = k.strip().lower()
+                if k == "transfer-encoding" and "chunked" in v.lower():
+                    self.chunked = True
+                elif k == "content-length":
+                    self._clen = int(v.strip())
+            if self.status < 400 and self.head is not None and not self.head.done():
+                self.head.set_result(self.status)
+        if self.status >= 400:  # collect the error body, then fail the open
+            self._err_body += self._dechunk() if self.chunked else bytes(buf)
+            if not self.chunked:
+                buf.clear()
+            if (self._clen >= 0 and len(self._err_body) >= self._clen) or self.done:
+                if self.head is not None and not self.head.done():
+                    self.head.set_exception(HttpStatusError(self.status, bytes(self._err_body)))
+            return
+        self.lines += self._dechunk() if self.chunked else bytes(buf)
+        if not self.chunked:
+            buf.clear()
+        got = False
+        while True:
+            nl = self.lines.find(b"\n")
+            if nl < 0:
+                break
+            line = bytes(self.lines[:nl]).strip()
+            del self.lines[:nl + 1]
+            if line:
+                self.items.append(self.decode(line))
+                got = True
+        if got:
+            self.ready.set()
+
+    def _dechunk(self) -> bytes:
+        buf = self.buf
+        out = bytearray()
+        while True:
+            nl = buf.find(b"\r\n")
+            if nl < 0:
+                break
+            size = int(bytes(buf[:nl]).split(b";", 1)[0], 16)
+            if size == 0:
+                self.done = True
+                del buf[:]
+                break
+            if len(buf) < nl + 2 + size + 2:
+                break
+            out += buf[nl + 2:nl + 2 + size]
+            del buf[:nl + 2 + size + 2]
+        return bytes(out)
+
+    def close(self) -> None:
+        self.done = True
+        self.ready.set()
+        if self.transport is not None:
+            self.transport.close()
+
+
+class Stream:
+    """Async iterator over a streaming response's decoded lines."""
+
+    def __init__(self, conn: _StreamConn):
+        self._c = conn
+
+    def __aiter__(self) -> "Stream":
+        return self
+
+    async def __anext__(self):
+        c = self._c
+        while not c.items:
+            if c.done:
+                raise StopAsyncIteration
+            c.ready.clear()
+            if c.items or c.done:
+                continue
+            await c.ready.wait()
+        if c.error is not None and not c.items:
+            raise StopAsyncIteration
+        return c.items.popleft()
+
+    def close(self) -> None:
+        self._c.close()
+
+
 def _expire(fut: asyncio.Future) -> None:
     if not fut.done():
         fut.set_exception(asyncio.TimeoutError())
@@ -291,6 +437,28 @@ class HttpPool:
             return status, raw, retry_after
         raise ConnectionFailed("unreachable", True, False)  # pragma: no cover
 
+    async def open_stream(self, path: str, decode, accept: str = "application/json") -> Stream:
+        """GET ``path`` on a dedicated connection and stream its body line by line
+        (``decode`` turns each non-empty line into an item).  Raises
+        :class:`HttpStatusError` for an error status."""
+        loop = asyncio.get_running_loop()
+        kw = {}
+        if self.ssl is not None:
+            kw["ssl"] = self.ssl
+            kw["server_hostname"] = self.server_hostname or self.host
+        _, conn = await asyncio.wait_for(
+            loop.create_connection(lambda: _StreamConn(decode), self.host, self.port, **kw), self.timeout)
+        conn.head = loop.create_future()
+        assert conn.transport is not None
+        conn.transport.write(f"GET {self.base_path}{path} HTTP/1.1\r\n{self._fixed}Accept: {accept}\r\n\r\n"
+                             .encode("latin-1"))
+        try:
+            await asyncio.wait_for(conn.head, self.timeout)
+        except BaseException:
+            conn.close()
+            raise
+        return Stream(conn)
+
     async def close(self) -> None:
         self._closed = True
         while self._idle:
@@ -307,4 +475,4 @@ def encode_query(params: Dict[str, str]) -> str:
     return "?" + urlencode(params)
 
 
-__all__: List[str] = ["HttpPool", "ConnectionFailed", "encode_query"]
+__all__: List[str] = ["HttpPool", "ConnectionFailed", "HttpStatusError", "Stream", "encode_query"]

@@ -21,7 +21,7 @@ from ..api.meta import GroupVersion, GroupVersionResource
 from ..utils import jsonutil
 from . import metrics
 from .client import ACCEPT, DISCARD, PATCH_CONTENT_TYPES, Transport, WatchStream
-from .fasthttp import ConnectionFailed, HttpPool, encode_query
+from .fasthttp import ConnectionFailed, HttpPool, HttpStatusError, Stream, encode_query
 from .kubeconfig import RestConfig
 
 
@@ -77,6 +77,30 @@ class _HttpWatch(WatchStream):
 
 _METHODS = {"get": "GET", "list": "GET", "create": "POST", "update": "PUT", "patch": "PATCH",
             "delete": "DELETE", "deletecollection": "DELETE"}
+
+
+def _decode_event(line: bytes) -> Tuple[str, Dict[str, Any]]:
+    ev = jsonutil.loads(line)
+    return ev.get("type", ""), ev.get("object") or {}
+
+
+class _FastWatch(WatchStream):
+    def __init__(self, stream: Stream):
+        self._s = stream
+
+    async def __anext__(self) -> Tuple[str, Dict[str, Any]]:
+        return await self._s.__anext__()
+
+    def stop(self) -> None:
+        self._s.close()
+
+
+def _status_error(status: int, raw: bytes) -> errors.ApiError:
+    try:
+        body: Any = jsonutil.loads(raw)
+    except ValueError:
+        body = raw.decode(errors="replace")
+    return errors.ApiError.from_status(status, body)
 
 
 class HttpTransport(Transport):
@@ -174,9 +198,18 @@ class HttpTransport(Transport):
 
     async def watch(self, gvr: GroupVersionResource, namespace: str = "",
                     params: Optional[Dict[str, Any]] = None) -> WatchStream:
-        url = self.config.host + resource_path(gvr, namespace)
         p = _clean(params)
         p["watch"] = "true"
+        if self.fast:
+            try:
+                stream = await self._fast_pool().open_stream(resource_path(gvr, namespace) + encode_query(p),
+                                                             _decode_event)
+            except HttpStatusError as e:
+                raise _status_error(e.status, e.body) from None
+            except (ConnectionFailed, OSError, asyncio.TimeoutError) as e:
+                raise errors.ApiError(503, "ServiceUnavailable", f"connection error: {e}") from None
+            return _FastWatch(stream)
+        url = self.config.host + resource_path(gvr, namespace)
         timeout = aiohttp.ClientTimeout(total=None, sock_connect=self._timeout)
         try:
             resp = await self._sess().get(url, params=p, timeout=timeout, **self._tls_kw())

@@ -238,3 +238,47 @@ async def test_https_apiserver_with_ca_and_bearer_token(tmp_path):
     finally:
         await client.close()
         await app.stop()
+
+
+async def test_stream_chunked_lines_split_across_chunks():
+    body_lines = [b'{"type":"ADDED","object":{"a":1}}', b'{"type":"MODIFIED","object":{"a":2}}']
+    payload = b"\n".join(body_lines) + b"\n"
+    # split the payload mid-line across chunks, deliver in small TCP writes
+    chunks = [payload[:10], payload[10:40], payload[40:]]
+    wire = b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n" + b"".join(
+        b"%x\r\n" % len(c) + c + b"\r\n" for c in chunks) + b"0\r\n\r\n"
+
+    async def handle(reader, writer):
+        await reader.readuntil(b"\r\n\r\n")
+        for i in range(0, len(wire), 7):
+            writer.write(wire[i:i + 7])
+            await writer.drain()
+            await asyncio.sleep(0)
+        writer.close()
+
+    srv = await asyncio.start_server(handle, "127.0.0.1", 0)
+    pool = HttpPool(f"http://127.0.0.1:{srv.sockets[0].getsockname()[1]}")
+    import json
+
+    try:
+        st = await pool.open_stream("/w?watch=true", json.loads)
+        got = [x async for x in st]
+        assert got == [{"type": "ADDED", "object": {"a": 1}}, {"type": "MODIFIED", "object": {"a": 2}}]
+    finally:
+        await pool.close()
+        srv.close()
+
+
+async def test_stream_error_status_raises():
+    from cron_operator_amd.runtime.fasthttp import HttpStatusError
+
+    body = b'{"kind":"Status","code":410,"reason":"Expired","message":"too old"}'
+    srv, port = await serve([b"HTTP/1.1 410 Gone\r\nContent-Length: %d\r\n\r\n" % len(body) + body])
+    pool = HttpPool(f"http://127.0.0.1:{port}")
+    try:
+        with pytest.raises(HttpStatusError) as ei:
+            await pool.open_stream("/w", lambda b: b)
+        assert ei.value.status == 410 and b"Expired" in ei.value.body
+    finally:
+        await pool.close()
+        srv.close()
