@@ -107,6 +107,10 @@ def build_parser() -> argparse.ArgumentParser:
                     help="'reference' reproduces every reference behaviour (live child LIST, finished=now, ...).")
     st.add_argument("--cron-engine", choices=["auto", "native", "python"], default="auto",
                     help="Cron next-fire engine implementation.")
+    st.add_argument("--shard-count", type=int, default=1, help="Split Crons across this many operator "
+                                                                "replicas (hash of namespace/name).")
+    st.add_argument("--shard-index", type=int, default=int(os.environ.get("SHARD_INDEX", "0") or 0),
+                    help="This replica's shard in [0, --shard-count) (default: $SHARD_INDEX).")
     st.add_argument("--sync-period", default="10h", help="Minimum frequency at which every watched object is "
                                                         "reconciled again (controller-runtime's cache SyncPeriod; "
                                                         "Go duration, 0 disables).")
@@ -192,6 +196,9 @@ async def run_start(a: argparse.Namespace) -> int:
     except ConfigError as e:
         log.error(e, "unable to get kubeconfig")
         return 1
+    if a.shard_count < 1 or not 0 <= a.shard_index < a.shard_count:
+        log.error(ValueError(f"--shard-index {a.shard_index} not in [0, {a.shard_count})"), "invalid sharding")
+        return 2
     cfg.qps, cfg.burst = a.qps, a.burst
     from ..utils.gotime import NANOS, parse_duration
 
@@ -208,7 +215,7 @@ async def run_start(a: argparse.Namespace) -> int:
                            metrics_cert_key=a.metrics_cert_key,
                            health_probe_bind_address=a.health_probe_bind_address, enable_http2=a.enable_http2,
                            max_concurrent_reconciles=a.max_concurrent_reconciles,
-                           sync_period=sync_period)
+                           sync_period=sync_period, shard_index=a.shard_index, shard_count=a.shard_count)
     try:
         mgr = Manager(client, mopts)
         opts = ReconcilerOptions.reference() if a.compat_mode == "reference" else ReconcilerOptions()

@@ -41,6 +41,8 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
                          opts, cron_inf)
     ctrl = Controller(CONTROLLER_NAME, rec, mgr.clock, mgr.opts.max_concurrent_reconciles, log)
     ctrl.set_log_constructor(log_constructor(log, "Cron"))
+    if mgr.opts.shard_count > 1:
+        ctrl.set_shard(mgr.opts.shard_index, mgr.opts.shard_count)
 
     preds = []
     if opts.own_write_filter:

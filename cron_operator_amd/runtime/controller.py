@@ -74,11 +74,21 @@ def _key(obj: Dict[str, Any]) -> Request:
     return Request(m.get("namespace", ""), m.get("name", ""))
 
 
+
+def shard_of(namespace: str, name: str, count: int) -> int:
+    """Stable shard of an object key: FNV-1a (32-bit) of ``namespace/name`` modulo ``count``.
+    Python's ``hash()`` is salted per process, so it cannot be used across replicas."""
+    h = 0x811C9DC5
+    for b in f"{namespace}/{name}".encode():
+        h = ((h ^ b) * 0x01000193) & 0xFFFFFFFF
+    return h % count if count > 1 else 0
+
 class Controller:
     def __init__(self, name: str, reconciler: Reconciler, clock: Clock, max_concurrent_reconciles: int = 1,
                  logger: Optional[Logger] = None, recover_panic: bool = True, queue: Optional[WorkQueue] = None):
         self.name = name
         self.reconciler = reconciler
+        self.shard: Tuple[int, int] = (0, 1)
         self.clock = clock
         self.max_concurrent = max(1, max_concurrent_reconciles)
         base = logger or get_logger()
@@ -103,9 +113,21 @@ class Controller:
         self._log_ctor = ctor
 
     # ------------------------------------------------------------------ sources
+    def set_shard(self, index: int, count: int) -> None:
+        """Only reconcile keys of shard ``index`` out of ``count`` (see :func:`shard_of`)."""
+        if count < 1 or not 0 <= index < count:
+            raise ValueError(f"invalid shard {index}/{count}")
+        self.shard = (index, count)
+
     def _handler(self, mapper: Callable[[Dict[str, Any]], List[Request]],
                  predicates: List[Predicate]) -> EventHandler:
         q = self.queue
+        if self.shard[1] > 1:  # horizontal sharding: drop keys owned by other shards
+            inner = mapper
+            index, count = self.shard
+
+            def mapper(obj: Dict[str, Any]) -> List[Request]:  # type: ignore[no-redef]
+                return [r for r in inner(obj) if shard_of(r.namespace, r.name, count) == index]
 
         def ok(event: str, old: Optional[Dict[str, Any]], new: Dict[str, Any]) -> bool:
             return all(p(event, old, new) for p in predicates)

@@ -57,6 +57,10 @@ class ManagerOptions:
     cache_sync_timeout: float = 120.0
     # controller-runtime's cache SyncPeriod: every object is re-reconciled at least this often
     sync_period: float = 10 * 3600.0
+    # horizontal sharding: this replica reconciles the Crons with shard_of(key) == shard_index; each
+    # shard elects its own leader (Lease "<leader_election_id>-shard-<index>")
+    shard_index: int = 0
+    shard_count: int = 1
 
 
 class Manager:
@@ -129,7 +133,9 @@ class Manager:
         try:
             if self.opts.leader_election:
                 ns = self.opts.leader_election_namespace or in_cluster_namespace()
-                self.elector = LeaderElector(self.client, self.opts.leader_election_id, ns,
+                lease = self.opts.leader_election_id if self.opts.shard_count <= 1 else \
+                    f"{self.opts.leader_election_id}-shard-{self.opts.shard_index}"
+                self.elector = LeaderElector(self.client, lease, ns,
                                              self.opts.leader_election_identity, self.clock,
                                              self.opts.lease_duration, self.opts.renew_deadline,
                                              self.opts.retry_period,

@@ -201,3 +201,73 @@ async def test_manager_leader_election_single_active():
     standby.stop()
     await asyncio.wait_for(t, 10)
     await env.stop()
+
+
+async def test_horizontal_sharding_splits_crons_and_leases():
+    """Two replicas with --shard-count 2: every Cron fires exactly once per tick, each shard only
+    reconciles its own Crons, and each shard elects its own leader Lease."""
+    from cron_operator_amd.api.meta import GroupVersionResource as GVR
+    from cron_operator_amd.controller.setup import setup_with_manager
+    from cron_operator_amd.runtime.controller import shard_of
+    from cron_operator_amd.runtime.manager import Manager, ManagerOptions
+
+    clock = FakeClock(1767268805 * 10**9)
+    env = TestEnv(clock=clock)
+    n = 24
+    for i in range(n):
+        await env.create_cron(new_cron(f"s{i}", NS, "*/1 * * * *", PT_TMPL))
+    owners = {0: set(), 1: set()}
+    for i in range(n):
+        owners[shard_of(NS, f"s{i}", 2)].add(f"s{i}")
+    assert owners[0] and owners[1]  # the hash spreads the keys
+
+    mgrs, ctrls, tasks = [], [], []
+    for idx in (0, 1):
+        m = Manager(env.new_client(), ManagerOptions(clock=clock, leader_election=True, leader_election_namespace=NS,
+                                                     leader_election_identity=f"r{idx}", shard_index=idx,
+                                                     shard_count=2, health_probe_bind_address="0",
+                                                     metrics_bind_address="0"))
+        ctrl, _ = await setup_with_manager(m)
+        mgrs.append(m)
+        ctrls.append(ctrl)
+        tasks.append(asyncio.get_running_loop().create_task(m.start()))
+    for m in mgrs:
+        await asyncio.wait_for(m.started.wait(), 10)
+    seen = {0: set(), 1: set()}
+    for idx, c in enumerate(ctrls):
+        orig = c.reconciler.reconcile
+
+        async def spy(req, log, _orig=orig, _idx=idx):
+            seen[_idx].add(req.name)
+            return await _orig(req, log)
+        c.reconciler.reconcile = spy
+    for _ in range(2):
+        for _ in range(60):
+            clock.advance(1)
+            await asyncio.sleep(0.001)
+        for _ in range(50):
+            await asyncio.sleep(0.002)
+    for i in range(n):
+        assert len(names(env.server, PT, f"s{i}")) == 2, f"s{i}"
+    assert seen[0] <= owners[0] and seen[1] <= owners[1]
+    leases = {o["metadata"]["name"] for o in env.server.list(GVR("coordination.k8s.io", "v1", "leases"), NS)["items"]}
+    assert {"619a52b8.kubedl.io-shard-0", "619a52b8.kubedl.io-shard-1"} <= leases
+    for m in mgrs:
+        m.stop()
+    for t in tasks:
+        try:
+            await asyncio.wait_for(t, 10)
+        except Exception:  # noqa: BLE001
+            pass
+    env.server.close_all_watches()
+
+
+def test_shard_of_is_stable_and_balanced():
+    from cron_operator_amd.runtime.controller import shard_of
+
+    assert shard_of("default", "a", 1) == 0
+    assert shard_of("default", "nightly", 4) == shard_of("default", "nightly", 4)
+    counts = [0] * 4
+    for i in range(4000):
+        counts[shard_of("ns", f"cron-{i}", 4)] += 1
+    assert min(counts) > 800
