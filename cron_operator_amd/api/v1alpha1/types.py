@@ -175,6 +175,13 @@ class CronStatus:
                                    for h in self.history],
                           last_schedule_time=self.last_schedule_time)
 
+    def snapshot(self) -> "CronStatus":
+        """A copy sharing the (never mutated) entries: the reconciler only ever replaces
+        ``active``/``history`` lists and their elements, so a list-level copy is enough to
+        compare before/after (the deep copy rebuilt every history entry per reconcile)."""
+        return CronStatus(active=list(self.active), history=list(self.history),
+                          last_schedule_time=self.last_schedule_time)
+
     def semantic_equal(self, o: "CronStatus") -> bool:
         if len(self.active) != len(o.active) or len(self.history) != len(o.history):
             return False

@@ -274,7 +274,7 @@ class CronReconciler(Reconciler):
             log.info("Skip reconciling Cron for it may have been deleted")
             return Result()
         cron = Cron.from_dict(old_obj)
-        old_status = cron.status.deepcopy()
+        old_status = cron.status.snapshot()
 
         result = Result()
         err: Optional[BaseException] = None
