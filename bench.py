@@ -10,6 +10,12 @@ finished job into history, garbage-collect the overflow, create the tick's
 PyTorchJob and update status -- against a fake Kubernetes apiserver running in
 its own process, over HTTP + watch streams.  Synthetic objects, no cluster.
 
+Each rank runs the operator as ``--shards`` (default 2) shard processes of the
+operator's horizontal sharding feature against one apiserver: the reference's Go
+controller spreads its 10 reconcile workers over all cores as goroutines, and
+sharding is how this asyncio operator uses more than one core.  ``--shards 1``
+keeps a single operator process.
+
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
 it runs under ``torch.distributed.run`` with one rank per GPU.  The operator is
 pure control plane, so ranks do not use the GPU: each
@@ -75,6 +81,9 @@ def main() -> int:
     ap.add_argument("--burst", type=int, default=50)
     ap.add_argument("--transport", choices=["http", "memory"], default="http")
     ap.add_argument("--mode", choices=["optimized", "reference"], default="optimized")
+    ap.add_argument("--shards", type=int, default=2,
+                    help="operator shards per rank (--shard-count): the reference's controller spreads its 10 "
+                         "workers over every core as goroutines; this asyncio operator uses cores by sharding")
     ap.add_argument("--out", default="", help="also write the full result JSON here")
     a = ap.parse_args()
 
@@ -83,7 +92,7 @@ def main() -> int:
 
     cfg = BenchConfig(n_crons=a.crons, steps=a.steps, warmup=a.warmup, history_limit=a.history_limit,
                       mode=a.mode, transport=a.transport, qps=a.qps, burst=a.burst, workers=a.workers,
-                      namespace=f"bench-r{rank}")
+                      namespace=f"bench-r{rank}", shards=a.shards if a.transport == "http" else 1)
     def on_step(k: int, dt: float, timed: bool) -> None:
         # bracket the K timed steps with barriers so every rank times the same window: the
         # harness starts its clock right after step `warmup` returns and stops it after the
@@ -130,6 +139,7 @@ def main() -> int:
                        "parallelism": f"shard{world}", "crons_per_rank": cfg.n_crons,
                        "history_limit": cfg.history_limit, "schedule": "* * * * *",
                        "transport": cfg.transport, "mode": cfg.mode, "workers": cfg.workers,
+                       "operator_shards": cfg.shards,
                        "qps": cfg.qps},
             "p50_schedule_to_create_ms": round(max(r["p50"] for r in allr), 2),
             "p99_schedule_to_create_ms": round(max(r["p99"] for r in allr), 2),

@@ -83,6 +83,9 @@ class BenchConfig:
     step_timeout: float = 600.0
     seed_history: bool = True  # requires history_limit >= 1
     apiserver_profile: str = ""  # write a cProfile of the apiserver process over the timed steps here
+    # operator shards (--shard-count): >1 runs one operator process per shard against the same apiserver
+    # (bench/shard_worker.py); 1 keeps the operator in this process
+    shards: int = 1
 
 
 @dataclass
@@ -272,6 +275,12 @@ async def run(cfg: BenchConfig, on_step=None) -> BenchResult:
             async with admin.post(remote.url + "/debug/fake/gc", json={}) as r:
                 await r.read()
 
+        if cfg.shards > 1:
+            if remote is None:
+                raise ValueError("shards > 1 needs transport='http'")
+            await setup_client.close()
+            return await _run_sharded(cfg, remote, admin, set_time, complete_jobs, on_step)
+
         client = Client(transport, qps=cfg.qps, burst=cfg.burst)
         opts = ReconcilerOptions.reference() if cfg.mode == "reference" else ReconcilerOptions()
         mgr = Manager(client, ManagerOptions(clock=clock, max_concurrent_reconciles=cfg.workers,
@@ -408,6 +417,119 @@ async def run(cfg: BenchConfig, on_step=None) -> BenchResult:
             await admin.close()
         if remote is not None:
             remote.stop()
+
+
+class _Shard:
+    """A shard_worker child process and its JSON-lines pipe."""
+
+    def __init__(self, proc: "asyncio.subprocess.Process"):
+        self.proc = proc
+
+    async def send(self, msg: Dict[str, Any]) -> None:
+        assert self.proc.stdin is not None
+        self.proc.stdin.write((json.dumps(msg) + "\n").encode())
+        await self.proc.stdin.drain()
+
+    async def recv(self, timeout: float) -> Dict[str, Any]:
+        assert self.proc.stdout is not None
+        line = await asyncio.wait_for(self.proc.stdout.readline(), timeout)
+        if not line:
+            err = (await self.proc.stderr.read()).decode()[-3000:] if self.proc.stderr else ""
+            raise RuntimeError(f"shard worker exited rc={self.proc.returncode}: {err}")
+        return json.loads(line)
+
+
+async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_time, complete_jobs,
+                       on_step) -> BenchResult:
+    """The step loop of :func:`run` with the operator split over ``cfg.shards`` processes."""
+    from ..cron.engine import default_engine
+    from ..utils import jsonutil
+
+    env = dict(os.environ)
+    root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    shards: List[_Shard] = []
+    try:
+        for i in range(cfg.shards):
+            p = await asyncio.create_subprocess_exec(
+                sys.executable, "-m", "cron_operator_amd.bench.shard_worker", "--url", remote.url,
+                "--namespace", cfg.namespace, "--shard-index", str(i), "--shard-count", str(cfg.shards),
+                "--start-ns", str(T0_NS + NANOS // 2), "--workers", str(cfg.workers),
+                "--history-limit", str(cfg.history_limit), "--qps", str(cfg.qps), "--burst", str(cfg.burst),
+                "--mode", cfg.mode, env=env, stdin=asyncio.subprocess.PIPE, stdout=asyncio.subprocess.PIPE,
+                stderr=asyncio.subprocess.PIPE, limit=1 << 24)
+            shards.append(_Shard(p))
+        ready = await asyncio.gather(*(s.recv(300) for s in shards))
+        assert sum(r["owned"] for r in ready) == cfg.n_crons, ready
+
+        async def phase(ns: int, name: str, tick_ns: int) -> List[Dict[str, Any]]:
+            await asyncio.gather(*(s.send({"cmd": "time", "ns": ns, "phase": name, "tick_ns": tick_ns})
+                                   for s in shards))
+            return list(await asyncio.gather(*(s.recv(cfg.step_timeout) for s in shards)))
+
+        total = cfg.warmup + cfg.steps
+        step_ms: List[float] = []
+        phase_ms: Dict[str, List[float]] = {"completion": [], "fire": []}
+        timed_lat: List[float] = []
+        base: Optional[List[Dict[str, Any]]] = None
+        last: List[Dict[str, Any]] = []
+        api0 = api1 = 0.0
+        t_start = 0.0
+        for k in range(1, total + 1):
+            tick_ns = T0_NS + k * 60 * NANOS
+            if k == cfg.warmup + 1:
+                api0 = _cpu_times(remote)[1]
+                t_start = time.perf_counter()
+            t0 = time.perf_counter()
+            if k > 1:
+                await complete_jobs(tick_ns - 30 * NANOS)
+                await set_time(tick_ns - 30 * NANOS)
+                await phase(tick_ns - 30 * NANOS, "completion", tick_ns)
+            t1 = time.perf_counter()
+            await set_time(tick_ns)
+            last = await phase(tick_ns, "fire", tick_ns)
+            t2 = time.perf_counter()
+            if k == cfg.warmup:
+                base = last
+            if k > cfg.warmup:
+                step_ms.append((t2 - t0) * 1000)
+                phase_ms["completion"].append((t1 - t0) * 1000)
+                phase_ms["fire"].append((t2 - t1) * 1000)
+                for r in last:
+                    timed_lat.extend(r["lat"])
+            if on_step is not None:
+                on_step(k, t2 - t0, k > cfg.warmup)
+        elapsed = time.perf_counter() - t_start
+        api1 = _cpu_times(remote)[1]
+        if base is None:  # warmup == 0: counters since process start
+            base = [{"reconciles": 0, "requests": 0, "by_verb": {}, "cpu": 0.0} for _ in shards]
+        reconciles = sum(r["reconciles"] - b["reconciles"] for r, b in zip(last, base))
+        requests = sum(r["requests"] - b["requests"] for r, b in zip(last, base))
+        by_verb: Dict[str, int] = {}
+        for r, b in zip(last, base):
+            for v, n in r["by_verb"].items():
+                by_verb[v] = by_verb.get(v, 0) + n - b["by_verb"].get(v, 0)
+        fires = cfg.n_crons * cfg.steps
+        return BenchResult(
+            config=asdict(cfg), steps=cfg.steps, elapsed_s=elapsed, ms_per_step=elapsed * 1000 / max(1, cfg.steps),
+            cron_reconciles_per_s=fires / elapsed, raw_reconciles_per_s=reconciles / elapsed,
+            p50_latency_ms=_pct(timed_lat, 50) * 1000, p99_latency_ms=_pct(timed_lat, 99) * 1000,
+            max_latency_ms=max(timed_lat) * 1000 if timed_lat else float("nan"),
+            api_requests_per_fire=requests / fires, api_requests_by_verb=by_verb,
+            reconciles_per_fire=reconciles / fires, step_ms=step_ms, phase_ms=phase_ms,
+            engine=default_engine().name, fastjson_native=jsonutil.NATIVE,
+            cpu_s_operator=sum(r["cpu"] - b["cpu"] for r, b in zip(last, base)), cpu_s_apiserver=api1 - api0)
+    finally:
+        for s in shards:
+            try:
+                await s.send({"cmd": "stop"})
+            except Exception:  # noqa: BLE001
+                pass
+        for s in shards:
+            try:
+                await asyncio.wait_for(s.proc.wait(), 30)
+            except Exception:  # noqa: BLE001
+                s.proc.kill()
 
 
 def run_sync(cfg: BenchConfig, on_step=None) -> BenchResult:

@@ -1,0 +1,146 @@
+"""One operator shard as a child process of the benchmark harness.
+
+The reference's controller runs its ``--max-concurrent-reconciles`` workers as
+goroutines spread over every core of the pod.  This operator is an asyncio
+process (one core); its horizontal-sharding feature (``--shard-count``) is how
+it uses more than one.  With ``BenchConfig.shards > 1`` the harness starts one
+of these workers per shard, all against the same fake apiserver, and drives them
+over a line protocol on stdin/stdout:
+
+``{"cmd": "time", "ns": <unix ns>, "phase": "completion"|"fire", "tick_ns": <ns>}``
+    set this shard's (fake) clock and reply once every Cron it owns has settled
+    for the phase: ``{"ok": true, "lat": [s, ...], "reconciles": n, "requests": n,
+    "by_verb": {...}, "cpu": s}`` (counters cumulative since start);
+``{"cmd": "stop"}``
+    shut the manager down and exit.
+
+Latency is measured inside the shard from the moment it applied the tick to each
+CREATE response, like the in-process harness does.
+"""
+from __future__ import annotations
+
+import argparse
+import asyncio
+import json
+import os
+import sys
+import time
+from typing import Any, Dict, List
+
+
+async def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--url", required=True)
+    ap.add_argument("--namespace", required=True)
+    ap.add_argument("--shard-index", type=int, required=True)
+    ap.add_argument("--shard-count", type=int, required=True)
+    ap.add_argument("--start-ns", type=int, required=True)
+    ap.add_argument("--workers", type=int, default=10)
+    ap.add_argument("--history-limit", type=int, default=10)
+    ap.add_argument("--qps", type=float, default=-1.0)
+    ap.add_argument("--burst", type=int, default=50)
+    ap.add_argument("--mode", default="optimized")
+    a = ap.parse_args()
+
+    from ..controller.reconciler import ReconcilerOptions
+    from ..controller.setup import setup_with_manager
+    from ..runtime.client import Client
+    from ..runtime.controller import shard_of
+    from ..runtime.http import HttpTransport
+    from ..runtime.kubeconfig import RestConfig
+    from ..runtime.manager import Manager, ManagerOptions
+    from ..utils.clock import FakeClock
+    from ..utils.gotime import NANOS, UTC, GoTime
+    from ..utils.logging import new_from_options, set_logger
+
+    set_logger(new_from_options(encoder="json", level="error", stream=open(os.devnull, "w")))
+    clock = FakeClock(a.start_ns)
+    client = Client(HttpTransport(RestConfig(host=a.url), pool_size=max(16, a.workers * 2)), qps=a.qps,
+                    burst=a.burst)
+    opts = ReconcilerOptions.reference() if a.mode == "reference" else ReconcilerOptions()
+    mgr = Manager(client, ManagerOptions(clock=clock, max_concurrent_reconciles=a.workers,
+                                         health_probe_bind_address="0", metrics_bind_address="0",
+                                         namespace=a.namespace, shard_index=a.shard_index,
+                                         shard_count=a.shard_count))
+    ctrl, rec = await setup_with_manager(mgr, opts)
+    task = asyncio.get_running_loop().create_task(mgr.start())
+    await asyncio.wait_for(mgr.started.wait(), 120)
+    cron_inf = rec.cron_informer
+    assert cron_inf is not None
+    await ctrl.wait_idle(timeout=120)
+
+    owned_keys = [k for k, o in cron_inf.store.items()
+                  if shard_of(o["metadata"].get("namespace", ""), o["metadata"]["name"], a.shard_count)
+                  == a.shard_index]
+
+    def owned() -> List[Dict[str, Any]]:
+        store = cron_inf.store
+        return [store[k] for k in owned_keys if k in store]
+
+    n_owned = len(owned_keys)
+    lat: List[float] = []
+    tick_wall = [0.0]
+    creates = [0]
+
+    def on_create(key, missed, created) -> None:
+        lat.append(time.perf_counter() - tick_wall[0])
+        creates[0] += 1
+
+    rec.latency_observer = on_create
+    out = sys.stdout
+    out.write(json.dumps({"ready": True, "owned": n_owned}) + "\n")
+    out.flush()
+
+    loop = asyncio.get_running_loop()
+    reader = asyncio.StreamReader()
+    await loop.connect_read_pipe(lambda: asyncio.StreamReaderProtocol(reader), sys.stdin)
+
+    async def settled(phase: str, tick_ns: int) -> None:
+        want_hist = a.history_limit
+        want_ts = GoTime(tick_ns // NANOS, 0, UTC).rfc3339()
+        while True:
+            if ctrl.queue.idle() and (phase == "completion" or creates[0] >= n_owned):
+                ok = True
+                for obj in owned():
+                    st = obj.get("status") or {}
+                    if phase == "completion":
+                        if st.get("active") or len(st.get("history") or ()) != want_hist:
+                            ok = False
+                            break
+                    elif st.get("lastScheduleTime") != want_ts or len(st.get("active") or ()) != 1 or \
+                            len(st.get("history") or ()) != want_hist:
+                        ok = False
+                        break
+                if ok and ctrl.queue.idle():
+                    return
+            await asyncio.sleep(0.002)
+
+    while True:
+        line = await reader.readline()
+        if not line:
+            break
+        msg = json.loads(line)
+        if msg.get("cmd") == "stop":
+            break
+        if msg.get("cmd") == "time":
+            lat.clear()
+            creates[0] = 0
+            tick_wall[0] = time.perf_counter()
+            clock.set(int(msg["ns"]))
+            await settled(msg.get("phase", "fire"), int(msg.get("tick_ns", msg["ns"])))
+            # counters are cumulative: the harness differences them over its timed window
+            out.write(json.dumps({"ok": True, "lat": lat, "reconciles": ctrl.reconciles,
+                                  "requests": client.requests, "by_verb": dict(client.requests_by_verb),
+                                  "cpu": time.process_time()}) + "\n")
+            out.flush()
+    mgr.stop()
+    try:
+        await asyncio.wait_for(task, 30)
+    except Exception:  # noqa: BLE001
+        pass
+    await client.close()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(asyncio.run(main()))

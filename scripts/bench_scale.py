@@ -26,6 +26,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--transport", default="http")
+    ap.add_argument("--shards", type=int, default=1, help="operator shard processes")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
 
@@ -37,7 +38,8 @@ def main() -> int:
             t0 = time.perf_counter()
             # small fleets get more ticks so percentiles rest on >= ~30 samples
             steps = max(a.steps, min(30, -(-30 // n)))
-            r = run_sync(BenchConfig(n_crons=n, steps=steps, warmup=a.warmup, mode=mode, transport=a.transport))
+            r = run_sync(BenchConfig(n_crons=n, steps=steps, warmup=a.warmup, mode=mode, transport=a.transport,
+                                     shards=a.shards if a.transport == "http" else 1))
             rows.append({"mode": mode, "n_crons": n, "steps": steps, "cron_reconciles_per_s": r.cron_reconciles_per_s,
                          "raw_reconciles_per_s": r.raw_reconciles_per_s, "p50_ms": r.p50_latency_ms,
                          "p99_ms": r.p99_latency_ms, "ms_per_step": r.ms_per_step,

@@ -24,6 +24,13 @@ echo "== bench $(date)"
 timeout -k 10 600 python bench.py --steps 5 --warmup 2 --out "$OUT/bench.json" > "$OUT/bench.log" 2>&1
 rc=$?; echo "bench rc=$rc"; tail -1 "$OUT/bench.log"; fatal $rc bench
 
+echo "== bench variants $(date)"
+for v in "--shards 1" "--mode reference --shards 1 --steps 3 --warmup 1" "--mode reference --shards 2 --steps 3 --warmup 1"; do
+  name=$(echo "$v" | tr -d ' -' )
+  timeout -k 10 600 python bench.py --steps 5 --warmup 2 $v --out "$OUT/bench_$name.json" > "$OUT/bench_$name.log" 2>&1
+  rc=$?; echo "bench $v rc=$rc"; tail -1 "$OUT/bench_$name.log" | cut -c1-330; fatal $rc "bench $v"
+done
+
 echo "== scale $(date)"
 timeout -k 10 900 python scripts/bench_scale.py --steps 3 --warmup 1 --out "$OUT/scale.json" > "$OUT/scale.log" 2>&1
 rc=$?; echo "scale rc=$rc"; tail -12 "$OUT/scale.log"; fatal $rc scale

@@ -33,6 +33,7 @@ def test_single_rank_line():
     assert KEYS <= set(d)
     assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["higher_is_better"] is True
     assert d["value"] > 0 and d["config"]["global_batch"] == 20 and d["scaling"] == "weak"
+    assert d["config"]["operator_shards"] == 2
     assert abs(d["value"] - 20 * 2 / (d["ms_per_step"] * 2 / 1000)) / d["value"] < 0.01
 
 
