@@ -46,6 +46,10 @@ def _go_type_name(v: Any) -> str:
     return "null"
 
 
+def _always_true(v: Any) -> bool:
+    return True
+
+
 class CompiledSchema:
     """One-pass prune + default + validity check, compiled from a structural schema.
 
@@ -86,10 +90,62 @@ class CompiledSchema:
         items = self._compile(items_s) if isinstance(items_s, dict) else None
         skip_meta = root
         deep = jsonutil.deepcopy
+        none_ok = nullable or root or t is None
+
+        # Specialised closures: most schema nodes are plain typed leaves or objects
+        # without pruning/defaults, and this runs on every custom-resource write.
+        simple = enum is None and not is_dt and minimum is None and maximum is None
+        if simple and not props_s and addl_s is None and items is None and not required:
+            if t is None or tcheck is None:
+                return _always_true
+            if t == "string":
+                return lambda v: type(v) is str or (v is None and none_ok) or isinstance(v, str)
+            if t == "object" and keep_unknown:
+                return lambda v: type(v) is dict or (v is None and none_ok)
+            return lambda v: (none_ok if v is None else tcheck(v))
+        if simple and t == "array" and items is not None and not props_s and addl_s is None:
+            def check_array(v: Any) -> bool:
+                if v is None:
+                    return none_ok
+                if type(v) is not list:
+                    return False
+                ok = True
+                for it in v:
+                    if not items(it):
+                        ok = False
+                return ok
+            return check_array
+        if simple and t == "object" and props_s is not None and addl is None:
+            prune_unknown = not keep_unknown and not addl_true
+
+            def check_object(v: Any) -> bool:
+                if v is None:
+                    return none_ok
+                if type(v) is not dict:
+                    return False
+                ok = True
+                if prune_unknown:
+                    extra = [k for k in v if k not in props]
+                    for k in extra:
+                        if skip_meta and k in ("apiVersion", "kind", "metadata"):
+                            continue
+                        del v[k]
+                for k, d in defaults:
+                    if k not in v:
+                        v[k] = deep(d)
+                for k in required:
+                    if k not in v:
+                        ok = False
+                for k, val in v.items():
+                    sub = props.get(k)
+                    if sub is not None and not (skip_meta and k == "metadata") and not sub(val):
+                        ok = False
+                return ok
+            return check_object
 
         def check(v: Any) -> bool:
             if v is None:
-                return nullable or root or t is None
+                return none_ok
             if tcheck is not None and not tcheck(v):
                 return False
             ok = True

@@ -321,3 +321,62 @@ def test_fault_injection():
         s.faults.check("create", "configmaps")
     assert e.value.code == 503
     s.faults.check("create", "configmaps")  # times exhausted
+
+
+# ---------------------------------------------------------------- compiled schema == slow path (property test)
+from hypothesis import given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+
+_vals = st.recursive(st.none() | st.booleans() | st.integers(-5, 5) | st.text(max_size=4)
+                     | st.sampled_from(["Allow", "Forbid", "Replace", "2026-01-01T00:00:00Z", "* * * * *"]),
+                     lambda c: st.lists(c, max_size=3) | st.dictionaries(
+                         st.sampled_from(["schedule", "suspend", "concurrencyPolicy", "historyLimit", "deadline",
+                                          "template", "workload", "active", "history", "status", "object", "kind",
+                                          "name", "uid", "created", "finished", "lastScheduleTime", "x"]), c,
+                         max_size=4), max_leaves=12)
+
+
+_PATHS = [("spec", "schedule"), ("spec", "suspend"), ("spec", "concurrencyPolicy"), ("spec", "historyLimit"),
+          ("spec", "deadline"), ("spec", "template"), ("spec", "x"), ("status", "lastScheduleTime"),
+          ("status", "active"), ("status", "history"), ("status", "x"), ("spec", "template", "workload"),
+          ("status", "history", 0, "status"), ("status", "history", 0, "object"), ("status", "history", 0, "created"),
+          ("status", "history", 0, "object", "name"), ("status", "active", 0, "uid"), ("status", "active", 0, "x")]
+
+
+@settings(max_examples=400, deadline=None)
+@given(mutations=st.lists(st.tuples(st.sampled_from(_PATHS), _vals | st.just("<delete>")), max_size=3))
+def test_compiled_schema_property_matches_prune_default_validate(mutations):
+    """Start from a valid Cron, apply up to three random field mutations, and require the compiled
+    one-pass checker to agree with prune + default + validate on validity and on the pruned object."""
+    import copy as _copy
+
+    schema = crd()["spec"]["versions"][0]["schema"]["openAPIV3Schema"]
+    obj = new_cron("c", "ns", "* * * * *", {"apiVersion": "a/b", "kind": "K"}, history_limit=3).to_dict()
+    obj["status"] = {"lastScheduleTime": "2026-01-01T00:00:00Z",
+                     "active": [{"kind": "K", "name": "a", "uid": "u1", "apiVersion": "a/b"}],
+                     "history": [{"object": {"kind": "K", "name": "n", "apiGroup": "a/b"}, "status": "Succeeded",
+                                  "uid": "u2", "created": "2026-01-01T00:00:00Z"}]}
+    for path, val in mutations:
+        cur = obj
+        for p in path[:-1]:
+            if isinstance(cur, dict) and p in cur:
+                cur = cur[p]
+            elif isinstance(cur, list) and isinstance(p, int) and p < len(cur):
+                cur = cur[p]
+            else:
+                cur = None
+                break
+        if isinstance(cur, dict):
+            if val == "<delete>":
+                cur.pop(path[-1], None)
+            else:
+                cur[path[-1]] = _copy.deepcopy(val)
+    a = _copy.deepcopy(obj)
+    b = _copy.deepcopy(obj)
+    ok_fast = sch.CompiledSchema(schema)(a)
+    sch.prune(b, schema)
+    sch.apply_defaults(b, schema)
+    ok_slow = sch.validate(b, schema) == []
+    assert ok_fast == ok_slow, (obj, sch.validate(b, schema))
+    if ok_fast:
+        assert a == b
