@@ -328,10 +328,12 @@ class APIServerApp:
         # The verb runs synchronously and its result is serialised right here, so the
         # stored object can be returned without a defensive copy.
         s.copy_responses = False
+        s.copy_inputs = False  # `body` was decoded for this request alone
         try:
             resp = self._apply(verb, gvr, ns, name, sub, body, ptype, q)
         finally:
             s.copy_responses = True
+            s.copy_inputs = True
         if s.faults.faults:  # "lost response" faults fire after the verb was applied
             s.faults.check(verb, gvr.resource, sub or None, name or None, after=True)
         return resp

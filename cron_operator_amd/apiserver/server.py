@@ -238,6 +238,9 @@ class APIServer:
         self._compiled_schemas: Dict[Tuple[str, str, str, int], Tuple[Any, Any]] = {}
         # verbs return deep copies unless a caller that serialises immediately opts out
         self.copy_responses = True
+        # verbs copy their input bodies unless the caller hands over private, never-reused
+        # objects (the HTTP front end: every body is freshly decoded for the request)
+        self.copy_inputs = True
         self._rng = random.Random(7)
         for ri in builtin_resources():
             self.register(ri)
@@ -457,7 +460,7 @@ class APIServer:
                dry_run: bool = False) -> Dict[str, Any]:
         ri = self.resource(gvr)
         self.stats.record("create", ri.resource)
-        body = jsonutil.deepcopy(obj)
+        body = jsonutil.deepcopy(obj) if self.copy_inputs else obj
         m = body.get("metadata")
         if not isinstance(m, dict):
             m = body["metadata"] = {}
@@ -586,7 +589,7 @@ class APIServer:
         self.stats.record("update", ri.resource)
         ns = namespace if ri.namespaced else ""
         old = self._get_raw(ri, ns, name)
-        body = jsonutil.deepcopy(obj)
+        body = jsonutil.deepcopy(obj) if self.copy_inputs else obj
         bm = body.get("metadata") or {}
         if bm.get("name") and bm["name"] != name:
             raise errors.bad_request("the name of the object does not match the name on the URL")
@@ -615,7 +618,13 @@ class APIServer:
                                                                    "application/merge-patch+json")
             if not isinstance(patch, dict):
                 raise errors.bad_request("merge patch must be a JSON object")
-            merged = jsonutil.apply_merge_patch(old, patch)
+            # stored objects are never mutated in place, so a status merge shares untouched subtrees
+            # (the status path copies metadata and admits only the status); a main-resource patch
+            # may be pruned/defaulted in place, so it gets a private tree
+            share = not self.copy_inputs and subresource == "status"
+            merged = jsonutil.apply_merge_patch(old, patch, share=share)
+            if share:
+                merged["metadata"] = dict(merged.get("metadata") or {})
         elif patch_type == "json":
             try:
                 merged = jsonutil.apply_json_patch(old, patch)

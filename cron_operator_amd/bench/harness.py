@@ -478,6 +478,9 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
         for k in range(1, total + 1):
             tick_ns = T0_NS + k * 60 * NANOS
             if k == cfg.warmup + 1:
+                if cfg.apiserver_profile:
+                    async with admin.post(remote.url + "/debug/fake/profile", json={"action": "start"}) as r:
+                        await r.read()
                 api0 = _cpu_times(remote)[1]
                 t_start = time.perf_counter()
             t0 = time.perf_counter()
@@ -501,6 +504,10 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
                 on_step(k, t2 - t0, k > cfg.warmup)
         elapsed = time.perf_counter() - t_start
         api1 = _cpu_times(remote)[1]
+        if cfg.apiserver_profile:
+            async with admin.post(remote.url + "/debug/fake/profile",
+                                  json={"action": "stop", "path": os.path.abspath(cfg.apiserver_profile)}) as r:
+                await r.read()
         if base is None:  # warmup == 0: counters since process start
             base = [{"reconciles": 0, "requests": 0, "by_verb": {}, "cpu": 0.0} for _ in shards]
         reconciles = sum(r["reconciles"] - b["reconciles"] for r, b in zip(last, base))

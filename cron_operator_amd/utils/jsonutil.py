@@ -72,18 +72,27 @@ def py_create_merge_patch(old: Any, new: Any) -> Any:
     return patch
 
 
-def apply_merge_patch(target: Any, patch: Any) -> Any:
-    """RFC 7386 apply; returns a new tree (inputs untouched)."""
+def apply_merge_patch(target: Any, patch: Any, share: bool = False) -> Any:
+    """RFC 7386 apply; returns a new tree (inputs untouched).
+
+    ``share=True`` (structural sharing): only the dicts on the patch's paths are
+    copied (shallowly) and every untouched subtree -- and the patch's own values --
+    is shared with the inputs.  For callers that treat both inputs as immutable,
+    e.g. the apiserver merging a freshly decoded request body into a stored object.
+    """
     if type(patch) is not dict:
-        return deepcopy(patch)
-    out = deepcopy(target) if type(target) is dict else {}
+        return patch if share else deepcopy(patch)
+    if type(target) is dict:
+        out = dict(target) if share else deepcopy(target)
+    else:
+        out = {}
     for k, v in patch.items():
         if v is None:
             out.pop(k, None)
         elif type(v) is dict:
-            out[k] = apply_merge_patch(out.get(k), v)
+            out[k] = apply_merge_patch(out.get(k), v, share)
         else:
-            out[k] = deepcopy(v)
+            out[k] = v if share else deepcopy(v)
     return out
 
 

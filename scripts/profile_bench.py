@@ -27,6 +27,8 @@ def main() -> int:
     ap.add_argument("--transport", default="http")
     ap.add_argument("--mode", default="optimized")
     ap.add_argument("--top", type=int, default=45)
+    ap.add_argument("--shards", type=int, default=1,
+                    help="operator shard processes (then only the apiserver profile is meaningful)")
     ap.add_argument("--out", required=True)
     a = ap.parse_args()
 
@@ -34,7 +36,7 @@ def main() -> int:
 
     api_prof = a.out + ".apiserver.pstats" if a.transport == "http" else ""
     cfg = BenchConfig(n_crons=a.crons, steps=a.steps, warmup=a.warmup, transport=a.transport, mode=a.mode,
-                      apiserver_profile=api_prof)
+                      apiserver_profile=api_prof, shards=a.shards)
     prof = cProfile.Profile()
     t0, c0 = time.perf_counter(), time.process_time()
 

@@ -380,3 +380,43 @@ def test_compiled_schema_property_matches_prune_default_validate(mutations):
     assert ok_fast == ok_slow, (obj, sch.validate(b, schema))
     if ok_fast:
         assert a == b
+
+
+async def test_http_writes_never_mutate_stored_objects():
+    """The HTTP front end hands request bodies over without copies and status merges share
+    untouched subtrees; previously stored objects (already sent in watch events) stay intact."""
+    import copy as _copy
+
+    from cron_operator_amd.apiserver.http import APIServerApp
+    from cron_operator_amd.runtime.client import Client
+    from cron_operator_amd.runtime.http import HttpTransport
+    from cron_operator_amd.runtime.kubeconfig import RestConfig
+
+    s = mk()
+    app = APIServerApp(s)
+    port = await app.start("127.0.0.1", 0)
+    client = Client(HttpTransport(RestConfig(host=f"http://127.0.0.1:{port}")), qps=-1)
+    try:
+        await client.create(CRON_GVR, new_cron("m", "default", "* * * * *", {"apiVersion": "a/b", "kind": "K"})
+                            .to_dict(), "default")
+        ri = s.resource(CRON_GVR)
+        v1 = s._get_raw(ri, "default", "m")
+        snap1 = _copy.deepcopy(v1)
+        await client.patch(CRON_GVR, "default", "m", {"status": {"lastScheduleTime": "2026-01-01T00:00:00Z",
+                                                                 "history": [{"object": {"kind": "K", "name": "a"},
+                                                                              "status": "Succeeded"}]}},
+                           "merge", "status")
+        v2 = s._get_raw(ri, "default", "m")
+        snap2 = _copy.deepcopy(v2)
+        await client.patch(CRON_GVR, "default", "m", {"status": {"lastScheduleTime": "2026-01-01T00:01:00Z"}},
+                           "merge", "status")
+        await client.patch(CRON_GVR, "default", "m", {"spec": {"suspend": True}, "metadata": {"labels": {"x": "y"}}})
+        v4 = s._get_raw(ri, "default", "m")
+        assert v1 == snap1 and v2 == snap2  # earlier versions untouched
+        assert v4["spec"]["suspend"] is True and v4["metadata"]["labels"] == {"x": "y"}
+        assert v4["status"]["history"] == snap2["status"]["history"]
+        assert int(v4["metadata"]["resourceVersion"]) > int(v2["metadata"]["resourceVersion"])
+        assert v4["metadata"]["generation"] == 2 and v2["metadata"].get("generation", 1) == 1
+    finally:
+        await client.close()
+        await app.stop()
