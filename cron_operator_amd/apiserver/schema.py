@@ -50,6 +50,19 @@ def _always_true(v: Any) -> bool:
     return True
 
 
+_DT_SEEN: Dict[str, bool] = {}
+
+
+def _is_date_time(v: str) -> bool:
+    """RFC 3339 check, memoised: the same few timestamps recur on every status write."""
+    r = _DT_SEEN.get(v)
+    if r is None:
+        if len(_DT_SEEN) > 100_000:
+            _DT_SEEN.clear()
+        r = _DT_SEEN[v] = _DATE_TIME.match(v) is not None
+    return r
+
+
 class CompiledSchema:
     """One-pass prune + default + validity check, compiled from a structural schema.
 
@@ -95,7 +108,10 @@ class CompiledSchema:
         # Specialised closures: most schema nodes are plain typed leaves or objects
         # without pruning/defaults, and this runs on every custom-resource write.
         simple = enum is None and not is_dt and minimum is None and maximum is None
-        if simple and not props_s and addl_s is None and items is None and not required:
+        leaf = not props_s and addl_s is None and items is None and not required
+        if leaf and is_dt and t == "string" and enum is None and minimum is None and maximum is None:
+            return lambda v: (none_ok if v is None else (type(v) is str and _is_date_time(v)))
+        if simple and leaf:
             if t is None or tcheck is None:
                 return _always_true
             if t == "string":
@@ -151,7 +167,7 @@ class CompiledSchema:
             ok = True
             if enum is not None and v not in enum:
                 ok = False
-            if is_dt and isinstance(v, str) and not _DATE_TIME.match(v):
+            if is_dt and isinstance(v, str) and not _is_date_time(v):
                 ok = False
             if minimum is not None and isinstance(v, (int, float)) and not isinstance(v, bool) and v < minimum:
                 ok = False
