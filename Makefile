@@ -136,6 +136,29 @@ helm-upgrade: ## Install/upgrade the chart into the current cluster (needs helm)
 helm-uninstall: ## Uninstall the chart.
 	helm uninstall cron-operator --namespace cron-operator
 
+##@ kind (local cluster; needs kind + kubectl + helm)
+
+KIND_CLUSTER ?= cron-operator
+KIND_K8S_VERSION ?= v1.34.0
+
+.PHONY: kind-create-cluster
+kind-create-cluster: ## Create a kind cluster for e2e runs against a real apiserver.
+	kind create cluster --name $(KIND_CLUSTER) --image kindest/node:$(KIND_K8S_VERSION)
+
+.PHONY: kind-load-image
+kind-load-image: docker-build ## Load the operator image into the kind cluster.
+	kind load docker-image $(IMG) --name $(KIND_CLUSTER)
+
+.PHONY: kind-delete-cluster
+kind-delete-cluster: ## Delete the kind cluster.
+	kind delete cluster --name $(KIND_CLUSTER)
+
+.PHONY: test-e2e-kind
+test-e2e-kind: kind-load-image helm-upgrade ## Real-cluster smoke: operator Running, a Cron fires (test/e2e analog).
+	kubectl -n cron-operator rollout status deploy/cron-operator --timeout=180s
+	kubectl apply -f examples/v1alpha1/cron/cron-pod.yaml
+	kubectl wait --for=jsonpath='{.status.lastScheduleTime}' cron/cron-pod --timeout=120s
+
 ##@ Deployment
 
 ignore-not-found ?= false
