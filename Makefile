@@ -157,7 +157,7 @@ kind-delete-cluster: ## Delete the kind cluster.
 test-e2e-kind: kind-load-image helm-upgrade ## Real-cluster smoke: operator Running, a Cron fires (test/e2e analog).
 	kubectl -n cron-operator rollout status deploy/cron-operator --timeout=180s
 	kubectl apply -f examples/v1alpha1/cron/cron-pod.yaml
-	kubectl wait --for=jsonpath='{.status.lastScheduleTime}' cron/cron-pod --timeout=120s
+	kubectl wait --for=jsonpath='{.status.lastScheduleTime}' cron/heartbeat-pod --timeout=120s
 
 ##@ Deployment
 
