@@ -143,4 +143,10 @@ async def main() -> int:
 
 
 if __name__ == "__main__":
-    sys.exit(asyncio.run(main()))
+    _prof = os.environ.get("CRON_BENCH_SHARD_PROFILE")
+    if _prof:  # cProfile of the whole worker (setup included): <prefix>.<pid>.pstats
+        import cProfile
+
+        cProfile.run("asyncio.run(main())", f"{_prof}.{os.getpid()}.pstats")
+    else:
+        sys.exit(asyncio.run(main()))

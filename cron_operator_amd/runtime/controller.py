@@ -23,6 +23,7 @@ import time
 import traceback
 import uuid
 from dataclasses import dataclass
+from functools import lru_cache
 from typing import Any, Awaitable, Callable, Dict, List, Optional, Tuple
 
 from ..api.meta import GroupVersionKind, NamespacedName, controller_ref
@@ -75,9 +76,11 @@ def _key(obj: Dict[str, Any]) -> Request:
 
 
 
+@lru_cache(maxsize=1 << 17)
 def shard_of(namespace: str, name: str, count: int) -> int:
     """Stable shard of an object key: FNV-1a (32-bit) of ``namespace/name`` modulo ``count``.
-    Python's ``hash()`` is salted per process, so it cannot be used across replicas."""
+    Python's ``hash()`` is salted per process, so it cannot be used across replicas.  Memoised:
+    every watch event of every Cron and child is routed through it."""
     h = 0x811C9DC5
     for b in f"{namespace}/{name}".encode():
         h = ((h ^ b) * 0x01000193) & 0xFFFFFFFF
