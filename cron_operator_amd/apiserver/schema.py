@@ -46,6 +46,9 @@ def _go_type_name(v: Any) -> str:
     return "null"
 
 
+_MISSING = object()
+
+
 def _always_true(v: Any) -> bool:
     return True
 
@@ -76,6 +79,31 @@ class CompiledSchema:
 
     def __init__(self, schema: Dict[str, Any], root: bool = True):
         self.fn = self._compile(schema, root)
+        # top-level view for incremental admission (see check_changed)
+        s = schema if isinstance(schema, dict) else {}
+        self.top_props = {k: self._compile(v) for k, v in (s.get("properties") or {}).items()}
+        self.top_required = tuple(s.get("required") or ())
+        self.top_simple = (bool(s.get("properties")) and s.get("type") in (None, "object")
+                           and not s.get("x-kubernetes-preserve-unknown-fields")
+                           and s.get("additionalProperties") is None and "enum" not in s
+                           and not any(isinstance(v, dict) and "default" in v
+                                       for v in (s.get("properties") or {}).values()))
+
+    def check_changed(self, obj: Any, old: Any) -> bool:
+        """Like ``self(obj)`` but skips top-level fields whose value *is* (identity) the old
+        object's: a structurally shared subtree of an admitted object is already valid."""
+        if not self.top_simple or type(obj) is not dict or type(old) is not dict:
+            return self.fn(obj)
+        props = self.top_props
+        for k in [k for k in obj if k not in props]:
+            del obj[k]
+        ok = all(k in obj for k in self.top_required)
+        for k, v in obj.items():
+            if v is old.get(k, _MISSING):
+                continue
+            if not props[k](v):
+                ok = False
+        return ok
 
     def __call__(self, obj: Any) -> bool:
         return self.fn(obj)

@@ -376,14 +376,16 @@ class APIServer:
             if errs:
                 raise errors.invalid(ri.kind, ri.group, name, errs)
 
-    def _admit_status(self, ri: ResourceInfo, obj: Dict[str, Any], name: str) -> None:
-        """Status-subresource writes only change ``status``: admit just that subtree."""
+    def _admit_status(self, ri: ResourceInfo, obj: Dict[str, Any], name: str,
+                      old_status: Any = None) -> None:
+        """Status-subresource writes only change ``status``: admit just that subtree (and of it,
+        only the fields not shared by identity with the already-admitted old status)."""
         st_schema = ((ri.schema or {}).get("properties") or {}).get("status")
         if st_schema is None:
             return
         st = obj["status"]
         fast = self._compiled(ri)[1]
-        if fast is not None and fast(st):
+        if fast is not None and (fast.check_changed(st, old_status) if old_status is not None else fast(st)):
             return
         errs = sch.validate(st, st_schema, "status")
         if errs:
@@ -555,7 +557,7 @@ class APIServer:
             else:
                 new.pop("status", None)
             if ri.schema is not None and new.get("status") is not None:
-                self._admit_status(ri, new, om["name"])
+                self._admit_status(ri, new, om["name"], old.get("status"))
             return new
         if subresource not in (None, ""):
             raise errors.ApiError(404, "NotFound", f"the server could not find the requested resource "

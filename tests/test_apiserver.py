@@ -420,3 +420,26 @@ async def test_http_writes_never_mutate_stored_objects():
     finally:
         await client.close()
         await app.stop()
+
+
+@settings(max_examples=300, deadline=None)
+@given(key=st.sampled_from(["lastScheduleTime", "active", "history", "x"]), val=_vals | st.just("<delete>"))
+def test_incremental_status_admission_matches_full(key, val):
+    """check_changed (skip fields shared by identity with the admitted old status) == full check."""
+    import copy as _copy
+
+    schema = crd()["spec"]["versions"][0]["schema"]["openAPIV3Schema"]["properties"]["status"]
+    cs = sch.CompiledSchema(schema, root=False)
+    old = {"lastScheduleTime": "2026-01-01T00:00:00Z",
+           "active": [{"kind": "K", "name": "a", "uid": "u1", "apiVersion": "a/b"}],
+           "history": [{"object": {"kind": "K", "name": "n"}, "status": "Succeeded", "uid": "u2"}]}
+    assert cs(_copy.deepcopy(old))
+    new = dict(old)  # shares every untouched field with old, like a structural-sharing merge
+    if val == "<delete>":
+        new.pop(key, None)
+    else:
+        new[key] = _copy.deepcopy(val)
+    full = _copy.deepcopy(new)
+    assert cs.check_changed(new, old) == cs(full)
+    if cs(_copy.deepcopy(new)):
+        assert new == full
