@@ -83,6 +83,7 @@ class BenchConfig:
     step_timeout: float = 600.0
     seed_history: bool = True  # requires history_limit >= 1
     apiserver_profile: str = ""  # write a cProfile of the apiserver process over the timed steps here
+    shard_profile: str = ""      # shards > 1: cProfile of each shard over the timed steps, <prefix>.<i>.pstats
     # operator shards (--shard-count): >1 runs one operator process per shard against the same apiserver
     # (bench/shard_worker.py); 1 keeps the operator in this process
     shards: int = 1
@@ -478,6 +479,9 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
         for k in range(1, total + 1):
             tick_ns = T0_NS + k * 60 * NANOS
             if k == cfg.warmup + 1:
+                if cfg.shard_profile:
+                    await asyncio.gather(*(s.send({"cmd": "profile", "action": "start"}) for s in shards))
+                    await asyncio.gather(*(s.recv(60) for s in shards))
                 if cfg.apiserver_profile:
                     async with admin.post(remote.url + "/debug/fake/profile", json={"action": "start"}) as r:
                         await r.read()
@@ -504,6 +508,11 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
                 on_step(k, t2 - t0, k > cfg.warmup)
         elapsed = time.perf_counter() - t_start
         api1 = _cpu_times(remote)[1]
+        if cfg.shard_profile:
+            await asyncio.gather(*(s.send({"cmd": "profile", "action": "stop",
+                                           "path": os.path.abspath(f"{cfg.shard_profile}.{i}.pstats")})
+                                   for i, s in enumerate(shards)))
+            await asyncio.gather(*(s.recv(60) for s in shards))
         if cfg.apiserver_profile:
             async with admin.post(remote.url + "/debug/fake/profile",
                                   json={"action": "stop", "path": os.path.abspath(cfg.apiserver_profile)}) as r:

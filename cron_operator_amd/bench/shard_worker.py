@@ -115,6 +115,7 @@ async def main() -> int:
                     return
             await asyncio.sleep(0.002)
 
+    prof = None
     while True:
         line = await reader.readline()
         if not line:
@@ -122,6 +123,19 @@ async def main() -> int:
         msg = json.loads(line)
         if msg.get("cmd") == "stop":
             break
+        if msg.get("cmd") == "profile":  # cProfile of this shard over the harness's timed steps
+            import cProfile
+
+            if msg.get("action") == "start":
+                prof = cProfile.Profile()
+                prof.enable()
+            elif prof is not None:
+                prof.disable()
+                prof.dump_stats(msg["path"])
+                prof = None
+            out.write(json.dumps({"ok": True}) + "\n")
+            out.flush()
+            continue
         if msg.get("cmd") == "time":
             lat.clear()
             creates[0] = 0

@@ -35,8 +35,9 @@ def main() -> int:
     from cron_operator_amd.bench.harness import BenchConfig, run_sync, summarize
 
     api_prof = a.out + ".apiserver.pstats" if a.transport == "http" else ""
+    shard_prof = a.out + ".shard" if a.shards > 1 else ""
     cfg = BenchConfig(n_crons=a.crons, steps=a.steps, warmup=a.warmup, transport=a.transport, mode=a.mode,
-                      apiserver_profile=api_prof, shards=a.shards)
+                      apiserver_profile=api_prof, shards=a.shards, shard_profile=shard_prof)
     prof = cProfile.Profile()
     t0, c0 = time.perf_counter(), time.process_time()
 
@@ -59,6 +60,11 @@ def main() -> int:
     st = pstats.Stats(prof, stream=buf)
     st.sort_stats("tottime").print_stats(a.top)
     st.sort_stats("cumulative").print_stats(a.top)
+    if shard_prof and os.path.exists(shard_prof + ".0.pstats"):
+        buf.write("\n\n# ===== operator shard 0 process, same timed steps =====\n")
+        sst = pstats.Stats(shard_prof + ".0.pstats", stream=buf)
+        sst.sort_stats("tottime").print_stats(a.top)
+        sst.sort_stats("cumulative").print_stats(a.top)
     if api_prof and os.path.exists(api_prof):
         buf.write("\n\n# ===== fake apiserver process, same timed steps =====\n")
         ast = pstats.Stats(api_prof, stream=buf)
