@@ -301,9 +301,10 @@ class Cron:
         return d
 
     @staticmethod
-    def from_dict(d: Dict[str, Any]) -> "Cron":
+    def from_dict(d: Dict[str, Any], status: Optional[CronStatus] = None) -> "Cron":
+        """``status``: an already parsed equivalent of ``d["status"]`` (the caller vouches for it)."""
         return Cron(metadata=jsonutil.deepcopy(d.get("metadata") or {}), spec=CronSpec.from_dict(d.get("spec")),
-                    status=CronStatus.from_dict(d.get("status")),
+                    status=status if status is not None else CronStatus.from_dict(d.get("status")),
                     api_version=d.get("apiVersion") or CRON_GVK.api_version, kind=d.get("kind") or CRON_GVK.kind)
 
     def deepcopy(self) -> "Cron":

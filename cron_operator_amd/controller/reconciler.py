@@ -58,6 +58,7 @@ from ..api.v1alpha1 import (
     ConcurrentPolicyReplace,
     Cron,
     CronHistory,
+    CronStatus,
     ObjectReference,
     TypedLocalObjectReference,
 )
@@ -245,6 +246,9 @@ class CronReconciler(Reconciler):
         self.stats = {"creates": 0, "deletes": 0, "patches": 0, "noop_patches_skipped": 0, "lists": 0}
         # child uid -> derived data for one resourceVersion (objects are immutable per resourceVersion)
         self._class_cache: Dict[str, _ChildInfo] = {}
+        # key -> (status dict we last wrote, its parsed form): the next reconcile of that Cron
+        # usually reads exactly that status back, so it skips re-parsing every history entry
+        self._parsed_status: Dict[str, Tuple[Dict[str, Any], CronStatus]] = {}
         # tick bookkeeping for latency: key -> (tick unix ns, wall perf_counter when it became due)
         self.latency_observer: Optional[Callable[[str, GoTime, Dict[str, Any]], None]] = None
 
@@ -272,8 +276,14 @@ class CronReconciler(Reconciler):
         old_obj = await self._get_cron(req)
         if old_obj is None:
             log.info("Skip reconciling Cron for it may have been deleted")
+            self._parsed_status.pop(f"{req.namespace}/{req.name}", None)
             return Result()
-        cron = Cron.from_dict(old_obj)
+        parsed = None
+        if self.opts.classification_cache:
+            memo = self._parsed_status.get(f"{req.namespace}/{req.name}")
+            if memo is not None and jsonutil.json_equal(old_obj.get("status") or {}, memo[0]):
+                parsed = memo[1].snapshot()
+        cron = Cron.from_dict(old_obj, status=parsed)
         old_status = cron.status.snapshot()
 
         result = Result()
@@ -300,12 +310,14 @@ class CronReconciler(Reconciler):
         new_status = cron.status.to_dict()
         old_status = old_obj.get("status") or {}
         patch = jsonutil.create_merge_patch({"status": old_status}, {"status": new_status} if new_status else {})
+        m = old_obj.get("metadata") or {}
+        key = f"{m.get('namespace', '')}/{m.get('name', '')}"
+        if self.opts.classification_cache:
+            self._parsed_status[key] = (new_status, cron.status.snapshot())
         if not patch and self.opts.skip_noop_patch:
             self.stats["noop_patches_skipped"] += 1
             metrics.child(metrics.STATUS_PATCHES, "skipped").inc()
             return
-        m = old_obj.get("metadata") or {}
-        key = f"{m.get('namespace', '')}/{m.get('name', '')}"
         if self.opts.own_write_filter:
             # recorded before the call: the watch event can overtake the PATCH response
             self.own_writes[key] = (m.get("generation"), new_status)

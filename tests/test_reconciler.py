@@ -169,6 +169,31 @@ async def test_b2_status_written_only_via_status_patch(mode):
     assert st["lastScheduleTime"] == rig.clock.now(UTC).utc().rfc3339()
 
 
+async def test_parsed_status_memo_reused_only_for_identical_status(monkeypatch):
+    """The status parsed on the last write is reused only while the stored status equals it."""
+    from cron_operator_amd.api.v1alpha1 import types
+
+    calls = []
+    orig = types.CronStatus.from_dict
+    monkeypatch.setattr(types.CronStatus, "from_dict", staticmethod(lambda d: calls.append(d) or orig(d)))
+    rig = Rig()
+    await rig.create(concurrency_policy="Forbid")
+    rig.set_status(lastScheduleTime=rig.clock.now(UTC).add(-2 * MINUTE).utc().rfc3339())
+    await rig.reconcile()
+    job = rig.jobs()[0]["metadata"]["name"]
+    n = len(calls)
+    await rig.reconcile()  # status unchanged since our write: no re-parse
+    assert len(calls) == n
+    assert [a["name"] for a in rig.cron()["status"]["active"]] == [job]
+    # an out-of-band edit (active cleared) must be parsed, not masked by the memo
+    obj = rig.cron()
+    obj["status"].pop("active", None)
+    rig.server.update(CRON_GVR, NS, NAME, obj, "status")
+    await rig.reconcile()
+    assert len(calls) == n + 1
+    assert [a["name"] for a in rig.cron()["status"]["active"]] == [job]  # re-derived from the child
+
+
 async def test_b2_patch_error_is_joined_and_result_cleared():
     rig = Rig()
     await rig.create()
