@@ -584,7 +584,6 @@ class CronReconciler(Reconciler):
         await self.sync_cron_history(cron, gvk, terminated, log)
 
     @staticmethod
-    @staticmethod
     def _sort(items: List[Child]) -> None:
         """``sortByCreationTimestamp`` (``cron_util.go:116-129``): stable, oldest first."""
         if all(x[2] is not None for x in items):

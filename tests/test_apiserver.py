@@ -443,3 +443,26 @@ def test_incremental_status_admission_matches_full(key, val):
     assert cs.check_changed(new, old) == cs(full)
     if cs(_copy.deepcopy(new)):
         assert new == full
+
+
+_HIST = [{"object": {"kind": "K", "name": f"n{i}", "apiGroup": "a/b"}, "status": "Succeeded", "uid": f"u{i}",
+          "created": "2026-01-01T00:00:00Z", "finished": "2026-01-01T00:01:00Z"} for i in range(6)]
+
+
+@settings(max_examples=300, deadline=None)
+@given(picks=st.lists(st.integers(0, 5) | _vals, max_size=8))
+def test_elementwise_status_admission_matches_full(picks):
+    """Array elements equal (not identical) to the old ones are skipped; the verdict and the
+    pruned result still match a full check, whatever mix of old and new elements arrives."""
+    import copy as _copy
+
+    schema = crd()["spec"]["versions"][0]["schema"]["openAPIV3Schema"]["properties"]["status"]
+    cs = sch.CompiledSchema(schema, root=False)
+    old = {"lastScheduleTime": "2026-01-01T00:00:00Z", "history": _copy.deepcopy(_HIST)}
+    assert cs(_copy.deepcopy(old))
+    hist = [_copy.deepcopy(_HIST[p]) if type(p) is int else _copy.deepcopy(p) for p in picks]
+    new = {"lastScheduleTime": "2026-01-01T00:00:00Z", "history": hist}  # equal, not identical, values
+    full = _copy.deepcopy(new)
+    assert cs.check_changed(new, old) == cs(full)
+    if cs(_copy.deepcopy(new)):
+        assert new == full
