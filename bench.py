@@ -14,7 +14,9 @@ Each rank runs the operator as ``--shards`` (default 2) shard processes of the
 operator's horizontal sharding feature against one apiserver: the reference's Go
 controller spreads its 10 reconcile workers over all cores as goroutines, and
 sharding is how this asyncio operator uses more than one core.  ``--shards 1``
-keeps a single operator process.
+keeps a single operator process.  ``--shard-routing labels`` (default) has each
+shard watch only its own Crons and children (``kubedl.io/shard`` labels, assigned
+by the shards during setup); ``hash`` has every shard watch everything.
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
 it runs under ``torch.distributed.run`` with one rank per GPU.  The operator is
@@ -85,6 +87,8 @@ def main() -> int:
     ap.add_argument("--shards", type=int, default=2,
                     help="operator shards per rank (--shard-count): the reference's controller spreads its 10 "
                          "workers over every core as goroutines; this asyncio operator uses cores by sharding")
+    ap.add_argument("--shard-routing", choices=["hash", "labels"], default="labels",
+                    help="how shards split the watch traffic (controller/sharding.py)")
     ap.add_argument("--out", default="", help="also write the full result JSON here")
     a = ap.parse_args()
 
@@ -93,7 +97,8 @@ def main() -> int:
 
     cfg = BenchConfig(n_crons=a.crons, steps=a.steps, warmup=a.warmup, history_limit=a.history_limit,
                       mode=a.mode, transport=a.transport, qps=a.qps, burst=a.burst, workers=a.workers,
-                      namespace=f"bench-r{rank}", shards=a.shards if a.transport == "http" else 1)
+                      namespace=f"bench-r{rank}", shards=a.shards if a.transport == "http" else 1,
+                      shard_routing=a.shard_routing)
     def on_step(k: int, dt: float, timed: bool) -> None:
         # bracket the K timed steps with barriers so every rank times the same window: the
         # harness starts its clock right after step `warmup` returns and stops it after the
@@ -137,10 +142,11 @@ def main() -> int:
                     "fake apiserver process per rank",
             "config": {"model": "cron-operator Cron reconciler (apps.kubedl.io/v1alpha1)",
                        "global_batch": fires // a.steps, "seq_len": None,
-                       "parallelism": f"shard{world}", "crons_per_rank": cfg.n_crons,
+                       "parallelism": f"ranks{world}x{cfg.shards}shards", "crons_per_rank": cfg.n_crons,
                        "history_limit": cfg.history_limit, "schedule": "* * * * *",
                        "transport": cfg.transport, "mode": cfg.mode, "workers": cfg.workers,
                        "operator_shards": cfg.shards,
+                       "shard_routing": cfg.shard_routing if cfg.shards > 1 else None,
                        "qps": cfg.qps},
             "p50_schedule_to_create_ms": round(max(r["p50"] for r in allr), 2),
             "p99_schedule_to_create_ms": round(max(r["p99"] for r in allr), 2),

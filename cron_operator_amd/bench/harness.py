@@ -87,6 +87,9 @@ class BenchConfig:
     # operator shards (--shard-count): >1 runs one operator process per shard against the same apiserver
     # (bench/shard_worker.py); 1 keeps the operator in this process
     shards: int = 1
+    # how shards split the watch traffic: "hash" (every shard sees every event) or "labels"
+    # (kubedl.io/shard labels + per-shard selectors, controller/sharding.py)
+    shard_routing: str = "labels"
 
 
 @dataclass
@@ -457,7 +460,8 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
                 "--namespace", cfg.namespace, "--shard-index", str(i), "--shard-count", str(cfg.shards),
                 "--start-ns", str(T0_NS + NANOS // 2), "--workers", str(cfg.workers),
                 "--history-limit", str(cfg.history_limit), "--qps", str(cfg.qps), "--burst", str(cfg.burst),
-                "--mode", cfg.mode, env=env, stdin=asyncio.subprocess.PIPE, stdout=asyncio.subprocess.PIPE,
+                "--mode", cfg.mode, "--routing", cfg.shard_routing,
+                env=env, stdin=asyncio.subprocess.PIPE, stdout=asyncio.subprocess.PIPE,
                 stderr=asyncio.subprocess.PIPE, limit=1 << 24)
             shards.append(_Shard(p))
         ready = await asyncio.gather(*(s.recv(300) for s in shards))

@@ -40,8 +40,10 @@ async def main() -> int:
     ap.add_argument("--qps", type=float, default=-1.0)
     ap.add_argument("--burst", type=int, default=50)
     ap.add_argument("--mode", default="optimized")
+    ap.add_argument("--routing", default="hash", choices=["hash", "labels"])
     a = ap.parse_args()
 
+    from ..api.v1alpha1 import CRON_GVR
     from ..controller.reconciler import ReconcilerOptions
     from ..controller.setup import setup_with_manager
     from ..runtime.client import Client
@@ -61,17 +63,23 @@ async def main() -> int:
     mgr = Manager(client, ManagerOptions(clock=clock, max_concurrent_reconciles=a.workers,
                                          health_probe_bind_address="0", metrics_bind_address="0",
                                          namespace=a.namespace, shard_index=a.shard_index,
-                                         shard_count=a.shard_count))
+                                         shard_count=a.shard_count, shard_routing=a.routing))
     ctrl, rec = await setup_with_manager(mgr, opts)
     task = asyncio.get_running_loop().create_task(mgr.start())
     await asyncio.wait_for(mgr.started.wait(), 120)
     cron_inf = rec.cron_informer
     assert cron_inf is not None
+    owned_keys = sorted(f"{a.namespace}/{o['metadata']['name']}"
+                        for o in (await client.list(CRON_GVR, a.namespace))["items"]
+                        if shard_of(a.namespace, o["metadata"]["name"], a.shard_count) == a.shard_index)
+    # label routing: wait until the assigner has labelled every owned Cron and its children
+    deadline = time.monotonic() + 300
+    while any(k not in cron_inf.store for k in owned_keys) or (
+            rec.shard_assigner is not None and rec.shard_assigner.pending()):
+        if time.monotonic() > deadline:
+            raise TimeoutError("shard assignment did not finish")
+        await asyncio.sleep(0.05)
     await ctrl.wait_idle(timeout=120)
-
-    owned_keys = [k for k, o in cron_inf.store.items()
-                  if shard_of(o["metadata"].get("namespace", ""), o["metadata"]["name"], a.shard_count)
-                  == a.shard_index]
 
     def owned() -> List[Dict[str, Any]]:
         store = cron_inf.store

@@ -111,6 +111,10 @@ def build_parser() -> argparse.ArgumentParser:
                                                                 "replicas (hash of namespace/name).")
     st.add_argument("--shard-index", type=int, default=int(os.environ.get("SHARD_INDEX", "0") or 0),
                     help="This replica's shard in [0, --shard-count) (default: $SHARD_INDEX).")
+    st.add_argument("--shard-routing", choices=["hash", "labels"], default="hash",
+                    help="hash: every shard watches all objects and drops other shards' keys; labels: shards "
+                         "label their Crons and children kubedl.io/shard=<index>-of-<count> and watch only "
+                         "their own (the apiserver splits the watch traffic).")
     st.add_argument("--sync-period", default="10h", help="Minimum frequency at which every watched object is "
                                                         "reconciled again (controller-runtime's cache SyncPeriod; "
                                                         "Go duration, 0 disables).")
@@ -215,7 +219,8 @@ async def run_start(a: argparse.Namespace) -> int:
                            metrics_cert_key=a.metrics_cert_key,
                            health_probe_bind_address=a.health_probe_bind_address, enable_http2=a.enable_http2,
                            max_concurrent_reconciles=a.max_concurrent_reconciles,
-                           sync_period=sync_period, shard_index=a.shard_index, shard_count=a.shard_count)
+                           sync_period=sync_period, shard_index=a.shard_index, shard_count=a.shard_count,
+                           shard_routing=a.shard_routing)
     try:
         mgr = Manager(client, mopts)
         opts = ReconcilerOptions.reference() if a.compat_mode == "reference" else ReconcilerOptions()

@@ -241,6 +241,10 @@ class CronReconciler(Reconciler):
         self.expect = Expectations(self.opts.expectation_ttl)
         self.child_informers: Dict[GroupVersionKind, Informer] = {}
         self.on_child_informer: Optional[Callable[[GroupVersionKind, Informer], None]] = None
+        # the child informers' selector, and labels stamped on every child (label-routed sharding)
+        self.child_selector = LABEL_CRON_NAME
+        self.child_labels: Dict[str, str] = {}
+        self.shard_assigner: Any = None  # controller.sharding.ShardAssigner with label routing
         # key -> resourceVersion of the Cron object produced by our last status write
         self.own_writes: Dict[str, Tuple[Any, Dict[str, Any]]] = {}  # key -> (generation, status we wrote)
         self.stats = {"creates": 0, "deletes": 0, "patches": 0, "noop_patches_skipped": 0, "lists": 0}
@@ -545,7 +549,7 @@ class CronReconciler(Reconciler):
             assert self.cache is not None
             from ..runtime.informer import label_index
 
-            inf = await self.cache.get_informer(gvk, label_selector=LABEL_CRON_NAME,
+            inf = await self.cache.get_informer(gvk, label_selector=self.child_selector,
                                                 indexers={CHILD_INDEX: label_index(LABEL_CRON_NAME)})
             self.child_informers[gvk] = inf
             inf.start()
@@ -698,6 +702,8 @@ class CronReconciler(Reconciler):
         if not isinstance(labels, dict):
             labels = m["labels"] = {}
         labels[LABEL_CRON_NAME] = cron.name
+        if self.child_labels:
+            labels.update(self.child_labels)
         set_controller_reference({"metadata": cron.metadata}, CRON_GVK, w)
         return w
 

@@ -17,6 +17,7 @@ by :mod:`cron_operator_amd.controller.rbac`.
 """
 from __future__ import annotations
 
+import asyncio
 from typing import Dict, Optional, Tuple
 
 from ..api import errors
@@ -27,6 +28,7 @@ from ..runtime.controller import Controller
 from ..runtime.informer import EventHandler, Informer, label_index
 from ..runtime.manager import Manager
 from ..utils.logging import get_logger, log_constructor
+from . import sharding
 from .reconciler import CHILD_INDEX, CronReconciler, ReconcilerOptions
 
 CONTROLLER_NAME = "cron"
@@ -36,13 +38,26 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
                              engine: Optional[CronEngine] = None) -> Tuple[Controller, CronReconciler]:
     opts = options or ReconcilerOptions()
     log = get_logger()
-    cron_inf = await mgr.cache.get_informer(CRON_GVK)
+    index, count = mgr.opts.shard_index, mgr.opts.shard_count
+    if mgr.opts.shard_routing not in sharding.ROUTINGS:
+        raise ValueError(f"unknown shard routing {mgr.opts.shard_routing!r}")
+    by_label = count > 1 and mgr.opts.shard_routing == "labels"
+    cron_inf = await mgr.cache.get_informer(CRON_GVK,
+                                            label_selector=sharding.shard_selector(index, count) if by_label else None)
     rec = CronReconciler(mgr.client, mgr.cache, mgr.get_event_recorder_for(CONTROLLER_NAME), mgr.clock, engine,
                          opts, cron_inf)
     ctrl = Controller(CONTROLLER_NAME, rec, mgr.clock, mgr.opts.max_concurrent_reconciles, log)
     ctrl.set_log_constructor(log_constructor(log, "Cron"))
-    if mgr.opts.shard_count > 1:
-        ctrl.set_shard(mgr.opts.shard_index, mgr.opts.shard_count)
+    assigner: Optional[sharding.ShardAssigner] = None
+    if count > 1:
+        ctrl.set_shard(index, count)  # with label routing too: a mislabelled object is never reconciled twice
+    if by_label:
+        rec.child_selector = sharding.child_selector(index, count)
+        rec.child_labels = {sharding.LABEL_SHARD: sharding.shard_label_value(index, count)}
+        assigner = sharding.ShardAssigner(mgr.client, index, count)
+        await assigner.watch(mgr.cache, CRON_GVK, child=False)
+        mgr.add(assigner.run)
+    rec.shard_assigner = assigner
 
     preds = []
     if opts.own_write_filter:
@@ -73,6 +88,8 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
                 return True
             owned_preds.append(not_expected)
         ctrl.watch_owned(inf, CRON_GVK, owned_preds)
+        if assigner is not None:
+            asyncio.get_running_loop().create_task(assigner.watch(mgr.cache, gvk, child=True))
         if opts.expectations:
             inf.add_handler(EventHandler(
                 on_add=lambda o: rec.expect.observe_add(key_of(o), (o.get("metadata") or {}).get("uid", "")),
@@ -82,11 +99,13 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
     for gvk in opts.static_owned_kinds:
         try:
             if opts.list_mode == "cache":
-                inf = await mgr.cache.get_informer(gvk, label_selector=LABEL_CRON_NAME,
+                inf = await mgr.cache.get_informer(gvk, label_selector=rec.child_selector,
                                                    indexers={CHILD_INDEX: label_index(LABEL_CRON_NAME)})
                 rec.child_informers[gvk] = inf
             else:
-                inf = await mgr.cache.get_informer(gvk)
+                inf = await mgr.cache.get_informer(gvk, label_selector=rec.child_selector if by_label else None)
+            if assigner is not None:
+                await assigner.watch(mgr.cache, gvk, child=True)
         except errors.ApiError as e:
             # the reference fails to start without these CRDs; we keep running and
             # pick the kind up lazily once a Cron uses it

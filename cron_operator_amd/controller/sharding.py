@@ -1,0 +1,147 @@
+"""Label-routed horizontal sharding (``--shard-routing=labels``).
+
+The reference runs one leader-elected replica; this operator can split
+its Crons across ``--shard-count`` replicas.  Two routings exist:
+
+``hash`` (default, :func:`cron_operator_amd.runtime.controller.shard_of`)
+    every shard's informers hold *all* Crons and children, and the event handler
+    drops the keys of other shards.  Nothing is written to user objects, but N
+    shards decode and cache N times the watch traffic.
+``labels`` (this module)
+    every Cron and child carries ``kubedl.io/shard=<index>-of-<count>`` and shard
+    *i*'s informers select on its own value, so the apiserver sends each event to
+    one shard only.  Total operator work stays O(events) as shards are added.
+
+Assignment is done by the shards themselves.  Each one also watches the objects
+whose shard label is missing or belongs to another shard count
+(``kubedl.io/shard notin (0-of-n, ..., n-1-of-n)``), which is an empty watch in
+steady state, and labels the ones whose Cron hashes (``shard_of``, FNV-1a of
+``namespace/name``) to itself.  The labelled object leaves that watch and enters
+the shard's main informers: the apiserver turns a label change into DELETED /
+ADDED per watch selector.  Children created by the reconciler carry the label
+from the start; children of a Cron that moved (after a change of shard count) are
+relabelled the same way, keyed by their ``kubedl.io/cron-name`` label.
+
+A change of ``--shard-count`` needs every shard restarted with the new count, as
+with hash routing; objects are then relabelled in the background.
+"""
+from __future__ import annotations
+
+import asyncio
+from typing import Any, Dict, List, Optional, Set, Tuple
+
+from ..api import errors
+from ..api.meta import GroupVersionKind
+from ..api.v1alpha1.groupversion import LABEL_CRON_NAME, LABEL_PREFIX_KUBEDL
+from ..runtime.client import Client
+from ..runtime.controller import shard_of
+from ..runtime.informer import Cache, EventHandler, Informer
+from ..utils.logging import Logger, get_logger
+
+LABEL_SHARD = LABEL_PREFIX_KUBEDL + "/shard"
+ROUTINGS = ("hash", "labels")
+
+
+def shard_label_value(index: int, count: int) -> str:
+    return f"{index}-of-{count}"
+
+
+def shard_selector(index: int, count: int) -> str:
+    """Selector of the Crons shard ``index`` owns."""
+    return f"{LABEL_SHARD}={shard_label_value(index, count)}"
+
+
+def child_selector(index: int, count: int) -> str:
+    """Selector of the children shard ``index`` owns."""
+    return f"{LABEL_CRON_NAME},{shard_selector(index, count)}"
+
+
+def unassigned_selector(count: int) -> str:
+    """Objects without a valid label for ``count`` shards (``notin`` also matches a missing label)."""
+    return f"{LABEL_SHARD} notin ({','.join(shard_label_value(i, count) for i in range(count))})"
+
+
+class ShardAssigner:
+    """Labels this shard's unassigned Crons and children (a leader-only runnable)."""
+
+    def __init__(self, client: Client, index: int, count: int, workers: int = 4,
+                 retry_delay: float = 1.0, logger: Optional[Logger] = None):
+        if count < 1 or not 0 <= index < count:
+            raise ValueError(f"invalid shard {index}/{count}")
+        self.client = client
+        self.index = index
+        self.count = count
+        self.value = shard_label_value(index, count)
+        self.workers = max(1, workers)
+        self.retry_delay = retry_delay
+        self.log = logger or get_logger("shard-assigner")
+        self.informers: Dict[GroupVersionKind, Informer] = {}
+        self._queue: "asyncio.Queue[Tuple[GroupVersionKind, str, str]]" = asyncio.Queue()
+        self._queued: Set[Tuple[GroupVersionKind, str, str]] = set()
+        self.labelled = 0
+        self.errors = 0
+
+    async def watch(self, cache: Cache, gvk: GroupVersionKind, child: bool) -> Informer:
+        """Watch ``gvk``'s unassigned objects (children: only those with a cron-name label)."""
+        inf = self.informers.get(gvk)
+        if inf is not None:
+            return inf
+        sel = f"{LABEL_CRON_NAME},{unassigned_selector(self.count)}" if child else unassigned_selector(self.count)
+        inf = await cache.get_informer(gvk, label_selector=sel)
+        self.informers[gvk] = inf
+        inf.add_handler(EventHandler(on_add=lambda o: self._offer(gvk, o, child),
+                                     on_update=lambda _old, o: self._offer(gvk, o, child)))
+        for o in list(inf.store.values()):
+            self._offer(gvk, o, child)
+        return inf
+
+    def owns(self, obj: Dict[str, Any], child: bool) -> bool:
+        m = obj.get("metadata") or {}
+        cron = (m.get("labels") or {}).get(LABEL_CRON_NAME, "") if child else m.get("name", "")
+        return shard_of(m.get("namespace", ""), cron, self.count) == self.index
+
+    def _offer(self, gvk: GroupVersionKind, obj: Dict[str, Any], child: bool) -> None:
+        if not self.owns(obj, child):
+            return
+        m = obj.get("metadata") or {}
+        key = (gvk, m.get("namespace", ""), m.get("name", ""))
+        if key not in self._queued:
+            self._queued.add(key)
+            self._queue.put_nowait(key)
+
+    def pending(self) -> int:
+        return len(self._queued)
+
+    async def run(self) -> None:
+        tasks: List[asyncio.Task] = [asyncio.get_running_loop().create_task(self._worker())
+                                     for _ in range(self.workers)]
+        try:
+            await asyncio.gather(*tasks)
+        finally:
+            for t in tasks:
+                t.cancel()
+
+    async def _worker(self) -> None:
+        patch = {"metadata": {"labels": {LABEL_SHARD: self.value}}}
+        while True:
+            key = await self._queue.get()
+            gvk, ns, name = key
+            try:
+                await self.client.patch(gvk, ns, name, patch, "merge", discard_response=True)
+                self.labelled += 1
+            except errors.ApiError as e:
+                if not errors.is_not_found(e):
+                    self.errors += 1
+                    self.log.error(e, "Failed to assign shard", kind=gvk.kind, namespace=ns, name=name)
+                    await asyncio.sleep(self.retry_delay)
+                    inf = self.informers.get(gvk)
+                    if inf is not None and inf.get(ns, name, copy=False) is not None:
+                        self._queue.put_nowait(key)  # still unassigned: retry
+                        continue
+            except Exception as e:  # noqa: BLE001 - transport errors: retry later
+                self.errors += 1
+                self.log.error(e, "Failed to assign shard", kind=gvk.kind, namespace=ns, name=name)
+                await asyncio.sleep(self.retry_delay)
+                self._queue.put_nowait(key)
+                continue
+            self._queued.discard(key)

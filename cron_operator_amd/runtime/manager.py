@@ -61,6 +61,9 @@ class ManagerOptions:
     # shard elects its own leader (Lease "<leader_election_id>-shard-<index>")
     shard_index: int = 0
     shard_count: int = 1
+    # "hash": every shard watches everything and drops other shards' keys; "labels": objects carry
+    # kubedl.io/shard and each shard's informers select on it (controller/sharding.py)
+    shard_routing: str = "hash"
 
 
 class Manager:

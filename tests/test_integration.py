@@ -203,9 +203,11 @@ async def test_manager_leader_election_single_active():
     await env.stop()
 
 
-async def test_horizontal_sharding_splits_crons_and_leases():
+@pytest.mark.parametrize("routing", ["hash", "labels"])
+async def test_horizontal_sharding_splits_crons_and_leases(routing):
     """Two replicas with --shard-count 2: every Cron fires exactly once per tick, each shard only
-    reconciles its own Crons, and each shard elects its own leader Lease."""
+    reconciles its own Crons, and each shard elects its own leader Lease.  With label routing
+    each shard also caches only its own Crons and children, all labelled with their shard."""
     from cron_operator_amd.api.meta import GroupVersionResource as GVR
     from cron_operator_amd.controller.setup import setup_with_manager
     from cron_operator_amd.runtime.controller import shard_of
@@ -226,7 +228,7 @@ async def test_horizontal_sharding_splits_crons_and_leases():
         m = Manager(env.new_client(), ManagerOptions(clock=clock, leader_election=True, leader_election_namespace=NS,
                                                      leader_election_identity=f"r{idx}", shard_index=idx,
                                                      shard_count=2, health_probe_bind_address="0",
-                                                     metrics_bind_address="0"))
+                                                     metrics_bind_address="0", shard_routing=routing))
         ctrl, _ = await setup_with_manager(m)
         mgrs.append(m)
         ctrls.append(ctrl)
@@ -252,6 +254,19 @@ async def test_horizontal_sharding_splits_crons_and_leases():
     assert seen[0] <= owners[0] and seen[1] <= owners[1]
     leases = {o["metadata"]["name"] for o in env.server.list(GVR("coordination.k8s.io", "v1", "leases"), NS)["items"]}
     assert {"619a52b8.kubedl.io-shard-0", "619a52b8.kubedl.io-shard-1"} <= leases
+    if routing == "labels":
+        from cron_operator_amd.controller.sharding import LABEL_SHARD
+
+        for idx, c in enumerate(ctrls):
+            rec = c.reconciler
+            assert {o["metadata"]["name"] for o in rec.cron_informer.store.values()} == owners[idx]
+            for inf in rec.child_informers.values():
+                assert {o["metadata"]["labels"][LABEL_CRON_NAME] for o in inf.store.values()} <= owners[idx]
+        for o in env.server.list(CRON_GVR, NS)["items"]:
+            assert o["metadata"]["labels"][LABEL_SHARD] == f"{shard_of(NS, o['metadata']['name'], 2)}-of-2"
+        for o in env.server.list(PT, NS)["items"]:
+            cron = o["metadata"]["labels"][LABEL_CRON_NAME]
+            assert o["metadata"]["labels"][LABEL_SHARD] == f"{shard_of(NS, cron, 2)}-of-2"
     for m in mgrs:
         m.stop()
     for t in tasks:
@@ -271,3 +286,63 @@ def test_shard_of_is_stable_and_balanced():
     for i in range(4000):
         counts[shard_of("ns", f"cron-{i}", 4)] += 1
     assert min(counts) > 800
+
+
+async def test_label_routing_reshard_relabels_crons_and_children():
+    """Label routing, 2 shards then 3: the new shards relabel every Cron and every existing child
+    (<i>-of-3) and keep firing each Cron exactly once per tick, with history intact."""
+    from cron_operator_amd.controller.setup import setup_with_manager
+    from cron_operator_amd.controller.sharding import LABEL_SHARD
+    from cron_operator_amd.runtime.controller import shard_of
+    from cron_operator_amd.runtime.manager import Manager, ManagerOptions
+
+    clock = FakeClock(1767268805 * 10**9)
+    env = TestEnv(clock=clock)
+    trainer = FakeTrainingOperator(env.new_client(), clock, mode="timed", duration=30)
+    await trainer.start()
+    n = 12
+    for i in range(n):
+        await env.create_cron(new_cron(f"r{i}", NS, "*/1 * * * *", PT_TMPL, history_limit=5))
+
+    async def run_shards(count, minutes):
+        mgrs, tasks = [], []
+        for idx in range(count):
+            m = Manager(env.new_client(), ManagerOptions(clock=clock, shard_index=idx, shard_count=count,
+                                                         shard_routing="labels", health_probe_bind_address="0",
+                                                         metrics_bind_address="0"))
+            await setup_with_manager(m)
+            mgrs.append(m)
+            tasks.append(asyncio.get_running_loop().create_task(m.start()))
+        for m in mgrs:
+            await asyncio.wait_for(m.started.wait(), 10)
+        for _ in range(50):
+            await asyncio.sleep(0.002)
+        for _ in range(minutes):
+            for _ in range(60):
+                clock.advance(1)
+                await asyncio.sleep(0.001)
+            for _ in range(50):
+                await asyncio.sleep(0.002)
+        for m in mgrs:
+            m.stop()
+        for t in tasks:
+            await asyncio.wait_for(t, 10)
+
+    await run_shards(2, 2)
+    first = {}
+    for i in range(n):
+        first[i] = names(env.server, PT, f"r{i}")
+        assert len(first[i]) == 2, f"r{i}"
+    await run_shards(3, 2)
+    for i in range(n):
+        assert len(names(env.server, PT, f"r{i}")) == 4, f"r{i}"  # one per tick, none duplicated
+        st = env.server.get(CRON_GVR, NS, f"r{i}")["status"]
+        hist = {h["object"]["name"] for h in st.get("history") or []}
+        assert set(first[i]) <= hist, f"r{i}"  # children made under 2 shards are still seen
+    for o in env.server.list(CRON_GVR, NS)["items"]:
+        assert o["metadata"]["labels"][LABEL_SHARD] == f"{shard_of(NS, o['metadata']['name'], 3)}-of-3"
+    for o in env.server.list(PT, NS)["items"]:
+        cron = o["metadata"]["labels"][LABEL_CRON_NAME]
+        assert o["metadata"]["labels"][LABEL_SHARD] == f"{shard_of(NS, cron, 3)}-of-3"
+    await trainer.stop()
+    env.server.close_all_watches()
