@@ -8,6 +8,7 @@ The reference lists children with ``client.MatchingLabels{kubedl.io/cron-name:
 from __future__ import annotations
 
 import re
+from functools import lru_cache
 from typing import Any, Callable, Dict, List, Optional, Tuple
 
 Requirement = Tuple[str, str, Tuple[str, ...]]  # (key, op, values); op in = != in notin exists !exists
@@ -167,15 +168,61 @@ def matches_fields(reqs: List[Tuple[str, str, str]], obj: Dict[str, Any]) -> boo
     return True
 
 
-def compile_selectors(label_selector: Optional[str], field_selector: Optional[str]) -> Callable[[Dict[str, Any]], bool]:
-    lreq = parse_label_selector(label_selector)
-    freq = parse_field_selector(field_selector)
-    if not lreq and not freq:
-        return lambda obj: True
+def _requirement_check(key: str, op: str, vals: Tuple[str, ...]) -> Callable[[Dict[str, str]], bool]:
+    if op == "=":
+        v = vals[0]
+        return lambda labels: labels.get(key) == v
+    if op == "!=":
+        v = vals[0]
+        return lambda labels: labels.get(key) != v
+    if op == "in":
+        vs = frozenset(vals)
+        return lambda labels: key in labels and labels[key] in vs
+    if op == "notin":
+        vs = frozenset(vals)
+        return lambda labels: labels.get(key) not in vs if key in labels else True
+    if op == "exists":
+        return lambda labels: key in labels
+    return lambda labels: key not in labels
 
-    def pred(obj: Dict[str, Any]) -> bool:
-        if lreq and not matches_labels(lreq, (obj.get("metadata") or {}).get("labels") or {}):
-            return False
-        return not freq or matches_fields(freq, obj)
 
-    return pred
+class Selector:
+    """A compiled label + field selector: ``sel(obj) -> bool``.
+
+    ``pinned`` is the first ``key=value`` label requirement, if any: every matching
+    object carries that label value, which lets the fake apiserver index watchers by it.
+    Instances are shared per selector string (:func:`compile_selectors` memoises), so
+    watchers with equal selectors can share one evaluation per event.
+    """
+
+    __slots__ = ("label_selector", "field_selector", "pinned", "_fn")
+
+    def __init__(self, label_selector: Optional[str], field_selector: Optional[str]):
+        self.label_selector = label_selector or ""
+        self.field_selector = field_selector or ""
+        lreq = parse_label_selector(label_selector)
+        freq = parse_field_selector(field_selector)
+        self.pinned: Optional[Tuple[str, str]] = next(((k, vals[0]) for k, op, vals in lreq if op == "="), None)
+        checks = tuple(_requirement_check(*r) for r in lreq)
+        if not checks and not freq:
+            self._fn: Callable[[Dict[str, Any]], bool] = lambda obj: True
+        elif len(checks) == 1 and not freq:
+            c = checks[0]
+            self._fn = lambda obj: c((obj.get("metadata") or {}).get("labels") or {})
+        else:
+            def fn(obj: Dict[str, Any]) -> bool:
+                if checks:
+                    labels = (obj.get("metadata") or {}).get("labels") or {}
+                    for c in checks:
+                        if not c(labels):
+                            return False
+                return not freq or matches_fields(freq, obj)
+            self._fn = fn
+
+    def __call__(self, obj: Dict[str, Any]) -> bool:
+        return self._fn(obj)
+
+
+@lru_cache(maxsize=4096)
+def compile_selectors(label_selector: Optional[str], field_selector: Optional[str]) -> Selector:
+    return Selector(label_selector, field_selector)

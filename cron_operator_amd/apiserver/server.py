@@ -130,6 +130,9 @@ class Watcher:
         self.info = info
         self.namespace = namespace or None
         self.pred = pred
+        self._match = getattr(pred, "_fn", pred)
+        # label routing key of the selector (Selector.pinned): lets _emit skip watchers by index
+        self.pinned: Optional[Tuple[str, str]] = getattr(pred, "pinned", None)
         self.bookmarks = bookmarks
         self.queue: "asyncio.Queue[Optional[Tuple[str, Dict[str, Any]]]]" = asyncio.Queue()
         self.closed = False
@@ -138,14 +141,21 @@ class Watcher:
     def _in_scope(self, obj: Dict[str, Any]) -> bool:
         if self.namespace is not None and (obj.get("metadata") or {}).get("namespace") != self.namespace:
             return False
-        return self.pred(obj)
+        return self._match(obj)
 
     def offer(self, etype: str, obj: Dict[str, Any], old: Optional[Dict[str, Any]]) -> None:
         if self.closed:
             return
         now_in = self._in_scope(obj)
+        self.offer_scoped(etype, obj, old, now_in,
+                          self._in_scope(old) if etype == "MODIFIED" and old is not None else False)
+
+    def offer_scoped(self, etype: str, obj: Dict[str, Any], old: Optional[Dict[str, Any]], now_in: bool,
+                     was_in: bool) -> None:
+        """:meth:`offer` with the selector already evaluated on ``obj`` and ``old``."""
+        if self.closed:
+            return
         if etype == "MODIFIED" and old is not None:
-            was_in = self._in_scope(old)
             if was_in and not now_in:
                 self._put("DELETED", obj)
             elif now_in and not was_in:
@@ -229,6 +239,8 @@ class APIServer:
         # (group, resource) -> namespace -> name -> stored object (never mutated in place)
         self._data: Dict[Tuple[str, str], Dict[str, Dict[str, Dict[str, Any]]]] = defaultdict(dict)
         self._watchers: Dict[Tuple[str, str], List[Watcher]] = defaultdict(list)
+        # per resource: (watchers to always offer, {label key: {value: watchers pinned to it}})
+        self._watch_plan: Dict[Tuple[str, str], Tuple[List[Watcher], Dict[str, Dict[str, List[Watcher]]]]] = {}
         self._log: Dict[Tuple[str, str], Deque[Tuple[int, str, Dict[str, Any], Optional[Dict[str, Any]]]]] = {}
         self._log_floor: Dict[Tuple[str, str], int] = defaultdict(int)
         self._watch_window = watch_window
@@ -331,13 +343,57 @@ class APIServer:
         if len(log) > self._watch_window:
             dropped = log.popleft()
             self._log_floor[key] = dropped[0]
-        for w in list(self._watchers.get(key, ())):
-            w.offer(etype, obj, old)
+        ws = self._watchers.get(key)
+        if not ws:
+            return
+        plan = self._watch_plan.get(key)
+        if plan is None:
+            plan = self._watch_plan[key] = self._plan(ws)
+        plain, pinned = plan
+        targets = plain
+        modified = etype == "MODIFIED" and old is not None
+        if pinned:
+            # watchers whose selector pins a label value only see objects carrying it (before or after)
+            targets = list(plain)
+            labels = (obj.get("metadata") or {}).get("labels") or {}
+            old_labels = ((old.get("metadata") or {}).get("labels") or {}) if modified else None
+            for lk, by_value in pinned.items():
+                v = labels.get(lk)
+                hit = by_value.get(v)
+                if hit:
+                    targets.extend(hit)
+                if old_labels is not None:
+                    ov = old_labels.get(lk)
+                    if ov != v:
+                        hit = by_value.get(ov)
+                        if hit:
+                            targets.extend(hit)
+        # one selector evaluation per distinct (namespace, selector) per event
+        seen: Dict[Tuple[Optional[str], Any], Tuple[bool, bool]] = {}
+        for w in targets:
+            gk = (w.namespace, w.pred)
+            r = seen.get(gk)
+            if r is None:
+                r = seen[gk] = (w._in_scope(obj), w._in_scope(old) if modified else False)  # type: ignore[arg-type]
+            w.offer_scoped(etype, obj, old, r[0], r[1])
+
+    @staticmethod
+    def _plan(ws: List[Watcher]) -> Tuple[List[Watcher], Dict[str, Dict[str, List[Watcher]]]]:
+        plain: List[Watcher] = []
+        pinned: Dict[str, Dict[str, List[Watcher]]] = {}
+        for w in ws:
+            if w.pinned is None:
+                plain.append(w)
+            else:
+                pinned.setdefault(w.pinned[0], {}).setdefault(w.pinned[1], []).append(w)
+        return plain, pinned
 
     def _remove_watcher(self, w: Watcher) -> None:
-        lst = self._watchers.get((w.info.group, w.info.resource))
+        key = (w.info.group, w.info.resource)
+        lst = self._watchers.get(key)
         if lst and w in lst:
             lst.remove(w)
+            self._watch_plan.pop(key, None)
 
     def _index_owners(self, ri: ResourceInfo, obj: Optional[Dict[str, Any]], old: Optional[Dict[str, Any]]) -> None:
         if old is not None:
@@ -809,6 +865,7 @@ class APIServer:
                 if rv > since:
                     w.offer(etype, obj, old)
         self._watchers[key].append(w)
+        self._watch_plan.pop(key, None)
         return w
 
     def send_bookmarks(self) -> None:

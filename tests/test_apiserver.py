@@ -466,3 +466,63 @@ def test_elementwise_status_admission_matches_full(picks):
     assert cs.check_changed(new, old) == cs(full)
     if cs(_copy.deepcopy(new)):
         assert new == full
+
+
+_SELS = ["", "s=0", "s=1", "s=0,k", "s notin (0,1)", "k", "!s", "s in (1,2)", "s=2,k=a", "k=a"]
+_OPS = st.lists(st.tuples(st.sampled_from(["create", "label", "unlabel", "delete"]), st.integers(0, 3),
+                          st.sampled_from(["s", "k"]), st.sampled_from(["0", "1", "2", "a"])), max_size=25)
+
+
+@settings(max_examples=150, deadline=None)
+@given(ops=_OPS, sels=st.lists(st.sampled_from(_SELS), min_size=1, max_size=6))
+def test_indexed_watch_fanout_matches_per_watcher_selectors(ops, sels):
+    """The label-pinned watcher index and the shared per-selector evaluation deliver exactly the
+    events a per-watcher selector check would (ADDED/DELETED on label transitions included)."""
+    from cron_operator_amd.api.selectors import matches_labels, parse_label_selector
+
+    s = mk()
+    ws = [s.watch(CM, "default", label_selector=sel or None) for sel in sels]
+    want = [[] for _ in sels]
+    cur = {}
+    for op, i, key, val in ops:
+        name = f"o{i}"
+        old = cur.get(name)
+        if op == "create" and old is None:
+            new = {key: val}
+            s.create(CM, "default", cm(name, dict(new)))
+        elif op in ("label", "unlabel") and old is not None:
+            new = dict(old)
+            if op == "label":
+                new[key] = val
+            else:
+                new.pop(key, None)
+            if new == old:
+                continue  # a no-op patch writes nothing and emits no event
+            s.patch(CM, "default", name, {"metadata": {"labels": {key: val if op == "label" else None}}})
+        elif op == "delete" and old is not None:
+            new = None
+            s.delete(CM, "default", name)
+        else:
+            continue
+        for j, sel in enumerate(sels):
+            reqs = parse_label_selector(sel)
+            was = old is not None and matches_labels(reqs, old)
+            now = new is not None and matches_labels(reqs, new)
+            if new is None:
+                ev = "DELETED" if was else None
+            elif old is None:
+                ev = "ADDED" if now else None
+            else:
+                ev = {(True, True): "MODIFIED", (True, False): "DELETED", (False, True): "ADDED"}.get((was, now))
+            if ev:
+                want[j].append((ev, name))
+        if new is None:
+            cur.pop(name, None)
+        else:
+            cur[name] = new
+    for j, w in enumerate(ws):
+        got = []
+        while not w.queue.empty():
+            etype, obj = w.queue.get_nowait()
+            got.append((etype, obj["metadata"]["name"]))
+        assert got == want[j], sels[j]
