@@ -10,7 +10,7 @@ finished job into history, garbage-collect the overflow, create the tick's
 PyTorchJob and update status -- against a fake Kubernetes apiserver running in
 its own process, over HTTP + watch streams.  Synthetic objects, no cluster.
 
-Each rank runs the operator as ``--shards`` (default 2) shard processes of the
+Each rank runs the operator as ``--shards`` (default 3) shard processes of the
 operator's horizontal sharding feature against one apiserver: the reference's Go
 controller spreads its 10 reconcile workers over all cores as goroutines, and
 sharding is how this asyncio operator uses more than one core.  ``--shards 1``
@@ -42,9 +42,9 @@ if ROOT not in sys.path:
 # BASELINE.md row "Reference algorithm, measured in this harness" (cron-reconciles/s @1000 Crons,
 # `--mode reference` in the same harness + fake apiserver, MI355X box).  Re-measured whenever the
 # harness/apiserver changes (the reference's live LISTs load the apiserver); the HIGHEST same-harness
-# measurement is kept so vs_baseline is conservative: r1f 79.5 (profiles/scale_mi355x_box_r1f.json;
-# other runs: 54.4-76.4, incl. the reference algorithm on 2 shards, 74.6).
-BASELINE_VALUE = 79.5
+# measurement is kept so vs_baseline is conservative: r1i 80.7 (profiles/shard_sweep_mi355x_box_r1i.json;
+# other runs: 42.8-79.5, incl. the reference algorithm on 2 shards, 69.7-74.6).
+BASELINE_VALUE = 80.72
 
 
 def _dist():
@@ -84,7 +84,7 @@ def main() -> int:
     ap.add_argument("--burst", type=int, default=50)
     ap.add_argument("--transport", choices=["http", "memory"], default="http")
     ap.add_argument("--mode", choices=["optimized", "reference"], default="optimized")
-    ap.add_argument("--shards", type=int, default=2,
+    ap.add_argument("--shards", type=int, default=3,
                     help="operator shards per rank (--shard-count): the reference's controller spreads its 10 "
                          "workers over every core as goroutines; this asyncio operator uses cores by sharding")
     ap.add_argument("--shard-routing", choices=["hash", "labels"], default="labels",

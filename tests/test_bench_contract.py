@@ -33,7 +33,7 @@ def test_single_rank_line():
     assert KEYS <= set(d)
     assert d["n_gpus"] == 1 and d["steps"] == 2 and d["warmup"] == 1 and d["higher_is_better"] is True
     assert d["value"] > 0 and d["config"]["global_batch"] == 20 and d["scaling"] == "weak"
-    assert d["config"]["operator_shards"] == 2 and d["config"]["shard_routing"] == "labels"
+    assert d["config"]["operator_shards"] == 3 and d["config"]["shard_routing"] == "labels"
     assert abs(d["value"] - 20 * 2 / (d["ms_per_step"] * 2 / 1000)) / d["value"] < 0.01
 
 
@@ -47,4 +47,4 @@ def test_two_ranks_aggregate():
                        capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json_line(r.stdout)  # rank 0 only
-    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 40 and d["config"]["parallelism"] == "ranks2x2shards"
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 40 and d["config"]["parallelism"] == "ranks2x3shards"
