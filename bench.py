@@ -89,6 +89,8 @@ def main() -> int:
                          "workers over every core as goroutines; this asyncio operator uses cores by sharding")
     ap.add_argument("--shard-routing", choices=["hash", "labels"], default="labels",
                     help="how shards split the watch traffic (controller/sharding.py)")
+    ap.add_argument("--apiserver-latency", choices=["none", "etcd"], default="none",
+                    help="server-side per-verb latency model of the fake apiserver (harness LATENCY_PROFILES)")
     ap.add_argument("--out", default="", help="also write the full result JSON here")
     a = ap.parse_args()
 
@@ -98,7 +100,7 @@ def main() -> int:
     cfg = BenchConfig(n_crons=a.crons, steps=a.steps, warmup=a.warmup, history_limit=a.history_limit,
                       mode=a.mode, transport=a.transport, qps=a.qps, burst=a.burst, workers=a.workers,
                       namespace=f"bench-r{rank}", shards=a.shards if a.transport == "http" else 1,
-                      shard_routing=a.shard_routing)
+                      shard_routing=a.shard_routing, apiserver_latency=a.apiserver_latency)
     def on_step(k: int, dt: float, timed: bool) -> None:
         # bracket the K timed steps with barriers so every rank times the same window: the
         # harness starts its clock right after step `warmup` returns and stops it after the
@@ -147,6 +149,7 @@ def main() -> int:
                        "transport": cfg.transport, "mode": cfg.mode, "workers": cfg.workers,
                        "operator_shards": cfg.shards,
                        "shard_routing": cfg.shard_routing if cfg.shards > 1 else None,
+                       "apiserver_latency": cfg.apiserver_latency,
                        "qps": cfg.qps},
             "p50_schedule_to_create_ms": round(max(r["p50"] for r in allr), 2),
             "p99_schedule_to_create_ms": round(max(r["p99"] for r in allr), 2),

@@ -55,6 +55,16 @@ PYTORCHJOBS = GroupVersionResource("kubeflow.org", "v1", "pytorchjobs")
 T0_NS = 1767268800 * NANOS
 
 
+# Server-side latency models for the fake apiserver (seconds per verb, applied after setup).
+# "etcd" is an ASSUMED model of a small kube-apiserver + etcd on SSD -- writes pay a quorum
+# fsync, reads come from the watch cache / etcd range -- not a measurement; it turns the bench
+# from CPU-bound into latency-bound, where request count per fire and worker count dominate.
+LATENCY_PROFILES: Dict[str, Dict[str, float]] = {
+    "none": {},
+    "etcd": {"create": 0.008, "update": 0.006, "patch": 0.006, "delete": 0.006, "get": 0.001, "list": 0.004},
+}
+
+
 def pytorchjob_template() -> Dict[str, Any]:
     """A 1 master + 1 worker PyTorchJob (no-op container), like the reference example."""
     def replica(n: int) -> Dict[str, Any]:
@@ -90,6 +100,8 @@ class BenchConfig:
     # how shards split the watch traffic: "hash" (every shard sees every event) or "labels"
     # (kubedl.io/shard labels + per-shard selectors, controller/sharding.py)
     shard_routing: str = "labels"
+    # per-verb server-side latency (LATENCY_PROFILES name), applied after setup; needs transport="http"
+    apiserver_latency: str = "none"
 
 
 @dataclass
@@ -277,6 +289,12 @@ async def run(cfg: BenchConfig, on_step=None) -> BenchResult:
         await set_time(T0_NS + NANOS // 2)
         if admin is not None:  # the apiserver process holds the seeded store for the whole run
             async with admin.post(remote.url + "/debug/fake/gc", json={}) as r:
+                await r.read()
+        latency = LATENCY_PROFILES[cfg.apiserver_latency]
+        if latency:
+            if admin is None:
+                raise ValueError("apiserver_latency needs transport='http'")
+            async with admin.post(remote.url + "/debug/fake/faults", json={"latency": latency}) as r:
                 await r.read()
 
         if cfg.shards > 1:

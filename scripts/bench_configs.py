@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""Deployment-shaped variants of the headline bench, both algorithms side by side.
+
+The headline (``bench.py``) runs the operator unthrottled against a fake
+apiserver that answers as fast as its CPU allows, so it is CPU-bound.  SURVEY
+section 7.4 asks for honest numbers under a QPS limiter and realistic apiserver
+latency too.  Each row here is one harness run:
+
+``unthrottled``
+    client rate limiter off, no server latency (the headline shape, one replica);
+``chart-defaults``
+    the reference chart's ``--qps 30 --burst 50`` (values.yaml), no server latency:
+    throughput is capped by requests per fire;
+``etcd-latency``
+    unthrottled, with the harness's ``etcd`` latency model on every verb (an
+    assumed model, see ``LATENCY_PROFILES``): throughput is bounded by workers x
+    round trips per fire.
+
+``optimized`` rows are this operator, ``reference`` rows the reference algorithm
+(``ReconcilerOptions.reference()``), both with 10 workers on one replica unless the
+row says otherwise.  Prints a Markdown table and writes JSON (``--out``).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+# name, mode, shards, crons, qps, burst, latency profile, steps, warmup
+ROWS = [
+    ("unthrottled", "reference", 1, 1000, -1.0, 50, "none", 3, 1),
+    ("unthrottled", "optimized", 1, 1000, -1.0, 50, "none", 5, 2),
+    ("chart-defaults", "reference", 1, 100, 30.0, 50, "none", 2, 1),
+    ("chart-defaults", "optimized", 1, 100, 30.0, 50, "none", 2, 1),
+    ("chart-defaults", "optimized", 3, 300, 30.0, 50, "none", 2, 1),
+    ("etcd-latency", "reference", 1, 1000, -1.0, 50, "etcd", 3, 1),
+    ("etcd-latency", "optimized", 1, 1000, -1.0, 50, "etcd", 5, 2),
+    ("etcd-latency", "optimized", 3, 1000, -1.0, 50, "etcd", 5, 2),
+]
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="", help="comma-separated config names to run")
+    ap.add_argument("--scale", type=float, default=1.0, help="multiply Cron counts (quick local runs)")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+
+    from cron_operator_amd.bench.harness import BenchConfig, run_sync
+
+    only = set(filter(None, a.only.split(",")))
+    rows = []
+    for name, mode, shards, n, qps, burst, lat, steps, warmup in ROWS:
+        if only and name not in only:
+            continue
+        n = max(1, int(n * a.scale))
+        t0 = time.perf_counter()
+        r = run_sync(BenchConfig(n_crons=n, steps=steps, warmup=warmup, mode=mode, qps=qps, burst=burst,
+                                 shards=shards, apiserver_latency=lat))
+        row = {"config": name, "mode": mode, "shards": shards, "n_crons": n, "qps": qps, "burst": burst,
+               "apiserver_latency": lat, "steps": steps, "cron_reconciles_per_s": r.cron_reconciles_per_s,
+               "p50_ms": r.p50_latency_ms, "p99_ms": r.p99_latency_ms, "ms_per_step": r.ms_per_step,
+               "api_requests_per_fire": r.api_requests_per_fire, "reconciles_per_fire": r.reconciles_per_fire,
+               "wall_s": round(time.perf_counter() - t0, 1)}
+        rows.append(row)
+        print(f"{name:>14} {mode:>9} x{shards} n={n:>5}: {r.cron_reconciles_per_s:9.1f} cron-reconciles/s  "
+              f"p50 {r.p50_latency_ms:8.1f} ms  {r.api_requests_per_fire:.1f} req/fire", flush=True)
+    print()
+    print("| config | algorithm | replicas | Crons | cron-reconciles/s | p50 tick→create ms | p99 ms "
+          "| API req/fire | reconciles/fire |")
+    print("|---|---|---:|---:|---:|---:|---:|---:|---:|")
+    for x in rows:
+        print(f"| {x['config']} | {x['mode']} | {x['shards']} | {x['n_crons']} | "
+              f"{x['cron_reconciles_per_s']:.1f} | {x['p50_ms']:.1f} | {x['p99_ms']:.1f} | "
+              f"{x['api_requests_per_fire']:.1f} | {x['reconciles_per_fire']:.1f} |")
+    if a.out:
+        with open(a.out, "w") as fh:
+            json.dump({"rows": rows}, fh, indent=1)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -27,3 +27,7 @@ timeout -k 10 600 python scripts/profile_bench.py --shards 4 --out "$OUT/prof/cp
     > "$OUT/prof/cprofile.log" 2>&1
 rc=$?; echo "cprofile rc=$rc"; fatal $rc cprofile
 echo "== done $(date)"
+
+echo "== deployment-shaped configs $(date)"
+timeout -k 10 900 python scripts/bench_configs.py --out "$OUT/configs.json" > "$OUT/configs.log" 2>&1
+rc=$?; echo "configs rc=$rc"; tail -11 "$OUT/configs.log"; fatal $rc configs
