@@ -14,28 +14,21 @@ dashboards and alerts carry over:
 * ``rest_client_requests_total{code,host,method}``,
   ``rest_client_request_duration_seconds``, ``rest_client_rate_limiter_duration_seconds``;
 * ``leader_election_master_status{name}``;
-* process/platform/GC collectors (the Go/process collectors' counterpart).
+* process and Python runtime collectors (the Go/process collectors' counterpart).
+
+The series live in :mod:`cron_operator_amd.runtime.promlite`, a small client
+whose per-update cost is an attribute add (the operator is one asyncio thread).
 
 Operator-specific additions (``cron_operator_*``): tick->create latency,
 workloads created/deleted, missed ticks and status patches.
 """
 from __future__ import annotations
 
-from prometheus_client import (
-    CollectorRegistry,
-    Counter,
-    Gauge,
-    Histogram,
-    GCCollector,
-    PlatformCollector,
-    ProcessCollector,
-    generate_latest,
-)
+from .promlite import Counter, Gauge, Histogram, ProcessCollector, PythonCollector, Registry
 
-REGISTRY = CollectorRegistry(auto_describe=True)
+REGISTRY = Registry()
 ProcessCollector(registry=REGISTRY)
-PlatformCollector(registry=REGISTRY)
-GCCollector(registry=REGISTRY)
+PythonCollector(registry=REGISTRY)
 
 _RECONCILE_BUCKETS = (0.005, 0.01, 0.025, 0.05, 0.1, 0.15, 0.2, 0.25, 0.3, 0.35, 0.4, 0.45, 0.5, 0.6, 0.7, 0.8,
                       0.9, 1.0, 1.25, 1.5, 1.75, 2.0, 2.5, 3.0, 3.5, 4.0, 4.5, 5, 6, 7, 8, 9, 10, 15, 20, 25, 30,
@@ -113,8 +106,8 @@ _CHILDREN: dict = {}
 
 
 def child(metric, *labels: str):
-    """``metric.labels(*labels)`` memoised: prometheus_client's ``labels()`` takes a lock and
-    builds a key tuple on every call, which showed up in the reconcile hot path."""
+    """``metric.labels(*labels)`` memoised: the reconcile hot path resolves the same few
+    label sets over and over."""
     key = (id(metric), labels)
     c = _CHILDREN.get(key)
     if c is None:
@@ -123,4 +116,4 @@ def child(metric, *labels: str):
 
 
 def exposition() -> bytes:
-    return generate_latest(REGISTRY)
+    return REGISTRY.exposition()

@@ -1,0 +1,66 @@
+"""The in-repo Prometheus client (``runtime/promlite.py``): values, histogram buckets,
+escaping, and a text exposition that a standard Prometheus parser accepts."""
+from __future__ import annotations
+
+import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
+
+from cron_operator_amd.runtime import promlite as pl
+
+
+def _parse(text: str):
+    parser = pytest.importorskip("prometheus_client.parser")
+    return {f.name: f for f in parser.text_string_to_metric_families(text)}
+
+
+@settings(max_examples=100, deadline=None)
+@given(values=st.lists(st.floats(min_value=0, max_value=100, allow_nan=False), max_size=50))
+def test_histogram_buckets_are_cumulative_le_counts(values):
+    reg = pl.Registry()
+    bounds = (0.5, 1.0, 5.0, 50.0)
+    h = pl.Histogram("h_seconds", "doc", ["a"], buckets=bounds, registry=reg)
+    hx = h.labels("x")  # a child appears in the exposition once it is created
+    for v in values:
+        hx.observe(v)
+    fam = _parse(reg.exposition().decode())["h_seconds"]
+    got = {s.labels["le"]: s.value for s in fam.samples if s.name == "h_seconds_bucket"}
+    for b in bounds:
+        assert got[pl._fmt(b)] == sum(1 for v in values if v <= b)
+    assert got["+Inf"] == len(values)
+    total = [s.value for s in fam.samples if s.name == "h_seconds_sum"]
+    assert total and abs(total[0] - sum(values)) < 1e-6
+
+
+def test_counter_gauge_and_escaping_round_trip():
+    reg = pl.Registry()
+    c = pl.Counter("reqs_total", "Requests.\nSecond line", ["code", "host"], registry=reg)
+    g = pl.Gauge("depth", "Depth", ["name"], registry=reg)
+    u = pl.Counter("plain_total", "No labels", registry=reg)
+    c.labels("200", 'we"ird\\host\n').inc()
+    c.labels(code="200", host='we"ird\\host\n').inc(2)
+    g.labels("q").inc(5)
+    g.labels("q").dec(2)
+    u.inc()
+    with pytest.raises(ValueError):
+        c.labels("200", "h").inc(-1)
+    with pytest.raises(ValueError):
+        c.labels("only-one")
+    with pytest.raises(ValueError):
+        pl.Counter("reqs_total", "dup", registry=reg)
+    fams = _parse(reg.exposition().decode())
+    (s,) = [s for s in fams["reqs"].samples if s.name == "reqs_total" and s.labels["host"] != "h"]
+    assert s.labels == {"code": "200", "host": 'we"ird\\host\n'} and s.value == 3
+    assert fams["depth"].samples[0].value == 3
+    assert fams["plain"].samples[0].value == 1
+    assert 'reqs_total{code="200",host="h"} 0' in reg.exposition().decode()  # sorted label names
+
+
+def test_operator_registry_exposes_controller_runtime_names():
+    from cron_operator_amd.runtime import metrics
+
+    metrics.child(metrics.RECONCILE_TOTAL, "cron", "success").inc()
+    fams = _parse(metrics.exposition().decode())
+    for name in ("controller_runtime_reconcile", "controller_runtime_reconcile_time_seconds", "workqueue_depth",
+                 "rest_client_requests", "process_cpu_seconds", "process_resident_memory_bytes", "python_info"):
+        assert name in fams, name
