@@ -173,6 +173,49 @@ def test_controller_running_metrics_and_cron_fires(cluster):
     assert rc == 0, proc.stdout.read()[-3000:]
 
 
+def test_label_routed_shards_as_processes(cluster):
+    """Two `start --shard-count 2 --shard-routing labels` processes: each labels and runs its own
+    Crons (kubedl.io/shard=<i>-of-2 on Crons and their jobs) and holds its own Lease."""
+    from cron_operator_amd.runtime.controller import shard_of
+
+    base = cluster["base"]
+    _api(base, "POST", "/api/v1/namespaces", {"apiVersion": "v1", "kind": "Namespace",
+                                              "metadata": {"name": "sharded"}})
+    procs = [_start_operator(cluster, "--leader-elect", "--metrics-secure=false", "--shard-count", "2",
+                             "--shard-index", str(i), "--shard-routing", "labels")[0] for i in range(2)]
+    names = [f"s{i}" for i in range(6)]
+    try:
+        tmpl = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+                "spec": {"pytorchReplicaSpecs": {"Master": {"replicas": 1}}}}
+        past = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(time.time() - 120))
+        for n in names:
+            _api(base, "POST", "/apis/apps.kubedl.io/v1alpha1/namespaces/sharded/crons",
+                 {"apiVersion": "apps.kubedl.io/v1alpha1", "kind": "Cron", "metadata": {"name": n},
+                  "spec": {"schedule": "*/1 * * * *", "concurrencyPolicy": "Forbid", "template": {"workload": tmpl}}})
+            _api(base, "PATCH", f"/apis/apps.kubedl.io/v1alpha1/namespaces/sharded/crons/{n}/status",
+                 {"status": {"lastScheduleTime": past}}, "application/merge-patch+json")
+
+        def all_fired():
+            jobs = _api(base, "GET", "/apis/kubeflow.org/v1/namespaces/sharded/pytorchjobs")["items"]
+            owners = {j["metadata"]["labels"]["kubedl.io/cron-name"] for j in jobs}
+            return jobs if owners >= set(names) else None
+
+        jobs = _wait(all_fired, 60, "every Cron fired", procs[0])
+        for j in jobs:
+            cron = j["metadata"]["labels"]["kubedl.io/cron-name"]
+            assert j["metadata"]["labels"]["kubedl.io/shard"] == f"{shard_of('sharded', cron, 2)}-of-2"
+        for n in names:
+            c = _api(base, "GET", f"/apis/apps.kubedl.io/v1alpha1/namespaces/sharded/crons/{n}")
+            assert c["metadata"]["labels"]["kubedl.io/shard"] == f"{shard_of('sharded', n, 2)}-of-2"
+        for i in range(2):
+            lease = _api(base, "GET", "/apis/coordination.k8s.io/v1/namespaces/cron-operator-system/leases/"
+                                      f"619a52b8.kubedl.io-shard-{i}")
+            assert lease["spec"]["holderIdentity"]
+    finally:
+        rcs = [_stop(p) for p in procs]
+    assert rcs == [0, 0], [p.stdout.read()[-2000:] for p in procs]
+
+
 def test_secure_metrics_require_authorized_token(cluster):
     """Binary default --metrics-secure=true: HTTPS + TokenReview/SubjectAccessReview filter (start.go:127-133)."""
     proc, probe, mport = _start_operator(cluster, "--leader-elect=false")
