@@ -105,10 +105,6 @@ def time_from_json(s: Optional[str]) -> Optional[GoTime]:
     return parse_rfc3339(s)
 
 
-def truncate_second(t: GoTime) -> GoTime:
-    """metav1.Time serialises with second precision; ``NewTime(t).Rfc3339Copy()``."""
-    return GoTime(t.sec, 0, t.loc)
-
 
 # --------------------------------------------------------------------------- metadata accessors
 
@@ -119,25 +115,6 @@ def meta(obj: Dict[str, Any]) -> Dict[str, Any]:
         m = obj["metadata"] = {}
     return m
 
-
-def name_of(obj: Dict[str, Any]) -> str:
-    return (obj.get("metadata") or {}).get("name", "")
-
-
-def namespace_of(obj: Dict[str, Any]) -> str:
-    return (obj.get("metadata") or {}).get("namespace", "")
-
-
-def uid_of(obj: Dict[str, Any]) -> str:
-    return (obj.get("metadata") or {}).get("uid", "")
-
-
-def rv_of(obj: Dict[str, Any]) -> str:
-    return (obj.get("metadata") or {}).get("resourceVersion", "")
-
-
-def labels_of(obj: Dict[str, Any]) -> Dict[str, str]:
-    return (obj.get("metadata") or {}).get("labels") or {}
 
 
 def creation_timestamp(obj: Dict[str, Any]) -> GoTime:
@@ -228,13 +205,3 @@ def _same_owner(a: Dict[str, Any], b: Dict[str, Any]) -> bool:
     return ga == gb and a.get("kind") == b.get("kind") and a.get("name") == b.get("name")
 
 
-def object_reference(obj: Dict[str, Any]) -> Dict[str, Any]:
-    """``corev1.ObjectReference`` JSON for an object (fields omitted when empty)."""
-    m = obj.get("metadata") or {}
-    ref: Dict[str, Any] = {}
-    for key, val in (("kind", obj.get("kind")), ("namespace", m.get("namespace")), ("name", m.get("name")),
-                     ("uid", m.get("uid")), ("apiVersion", obj.get("apiVersion")),
-                     ("resourceVersion", m.get("resourceVersion"))):
-        if val:
-            ref[key] = val
-    return ref

@@ -113,17 +113,6 @@ def matches_labels(reqs: List[Requirement], labels: Dict[str, str]) -> bool:
     return True
 
 
-def format_label_selector(match: Dict[str, str]) -> str:
-    return ",".join(f"{k}={v}" for k, v in sorted(match.items()))
-
-
-def equality_value(reqs: List[Requirement], key: str) -> Optional[str]:
-    """The value ``key`` is pinned to by an ``=`` requirement, if any (index lookups)."""
-    for k, op, vals in reqs:
-        if k == key and op == "=":
-            return vals[0]
-    return None
-
 
 def _field_value(obj: Dict[str, Any], path: str) -> Optional[str]:
     cur: Any = obj

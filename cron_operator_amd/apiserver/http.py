@@ -138,6 +138,7 @@ class APIServerApp:
         self._srv: Optional[asyncio.AbstractServer] = None
         self._conns: "set[_ServerConn]" = set()
         self._streams: List[Watcher] = []
+        self._bookmarks: Optional[asyncio.Task] = None
         self.requests = 0
 
     # ------------------------------------------------------------------ discovery
@@ -448,13 +449,27 @@ class APIServerApp:
         return _err(errors.ApiError(404, "NotFound", f"unknown debug endpoint {what}"))
 
     # ------------------------------------------------------------------ lifecycle
-    async def start(self, host: str = "127.0.0.1", port: int = 0, ssl_context=None) -> int:
+    async def start(self, host: str = "127.0.0.1", port: int = 0, ssl_context=None,
+                    bookmark_interval: float = 60.0) -> int:
+        """``bookmark_interval``: seconds between BOOKMARK events on watches that allow them
+        (kube-apiserver sends one about every minute, so a resumed watch starts from a fresh
+        resourceVersion instead of hitting "too old" and relisting); 0 disables."""
         loop = asyncio.get_running_loop()
         self._srv = await loop.create_server(lambda: _ServerConn(self), host, port, ssl=ssl_context, backlog=1024)
         self.port = self._srv.sockets[0].getsockname()[1]
+        if bookmark_interval > 0:
+            self._bookmarks = loop.create_task(self._bookmark_loop(bookmark_interval))
         return self.port
 
+    async def _bookmark_loop(self, interval: float) -> None:
+        while True:
+            await asyncio.sleep(interval)
+            self.server.send_bookmarks()
+
     async def stop(self) -> None:
+        if self._bookmarks is not None:
+            self._bookmarks.cancel()
+            self._bookmarks = None
         for w in list(self._streams):
             w.stop()
         if self._srv is not None:

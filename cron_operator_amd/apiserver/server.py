@@ -275,8 +275,6 @@ class APIServer:
                                   f"the server could not find the requested resource ({gvr.resource})")
         return ri
 
-    def resource_for_kind(self, group: str, version: str, kind: str) -> Optional[ResourceInfo]:
-        return self._by_kind.get((group, version, kind))
 
     def install_crd(self, crd: Dict[str, Any]) -> Dict[str, Any]:
         """Create (or replace) a CRD object and register its resources."""

@@ -243,11 +243,6 @@ async def run(cfg: BenchConfig, on_step=None) -> BenchResult:
                                   json={"namespace": cfg.namespace, "time": ts}) as r:
                 await r.read()
 
-    async def api_stats() -> Dict[str, Any]:
-        if server is not None:
-            return server.stats.snapshot()
-        async with admin.get(remote.url + "/debug/fake/stats") as r:
-            return json.loads(await r.read())
 
     try:
         # ---------------------------------------------------------------- setup (untimed)

@@ -61,9 +61,6 @@ def available() -> bool:
         return False
 
 
-def load_error() -> Optional[BaseException]:
-    return _load_error
-
 
 def _resolve_name(name: str) -> int:
     return zone_id(load_location(name))
@@ -101,12 +98,6 @@ def zone_id(loc: Location) -> int:
         return zid
     raise TypeError(f"unsupported location {loc!r}")
 
-
-def reset_local() -> None:
-    """Forget the cached Local zone (after $TZ changes)."""
-    LOCAL.reset()
-    for k in [k for k in _zone_ids if k.startswith("Local:")]:
-        del _zone_ids[k]
 
 
 def engine_path() -> str:

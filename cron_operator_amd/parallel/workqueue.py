@@ -223,8 +223,6 @@ class WorkQueue:
     def waiting(self) -> int:
         return len(self._wait_when)
 
-    def next_ready_ns(self) -> Optional[int]:
-        return min((w for w, _ in self._wait_when.values()), default=None)
 
     # ------------------------------------------------------------------ rate limiting
     def add_rate_limited(self, item: Hashable, priority: int = 0) -> None:

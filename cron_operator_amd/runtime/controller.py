@@ -267,6 +267,14 @@ class Controller:
         loop = asyncio.get_running_loop()
         for i in range(self.max_concurrent):
             self._workers.append(loop.create_task(self._worker(), name=f"{self.name}-worker-{i}"))
+        self._workers.append(loop.create_task(self._unfinished_loop(), name=f"{self.name}-metrics"))
+
+    async def _unfinished_loop(self, interval: float = 0.5) -> None:
+        """workqueue_unfinished_work_seconds / ..._longest_running_processor_seconds, refreshed
+        every 500 ms like client-go's ``updateUnfinishedWorkLoop``."""
+        while True:
+            await asyncio.sleep(interval)
+            self.queue.update_unfinished_metrics()
 
     async def stop(self) -> None:
         self.queue.shutdown()

@@ -58,20 +58,6 @@ def label_index(label: str) -> IndexFunc:
     return fn
 
 
-def controller_owner_index(owner_kind: str, owner_group: str) -> IndexFunc:
-    """Index by ``namespace/<controller owner name>`` for owners of the given kind."""
-
-    def fn(obj: Dict[str, Any]) -> List[str]:
-        m = obj.get("metadata") or {}
-        for ref in m.get("ownerReferences") or ():
-            if ref.get("controller") and ref.get("kind") == owner_kind:
-                av = ref.get("apiVersion", "")
-                if av.split("/")[0] == owner_group:
-                    return [f"{m.get('namespace', '')}/{ref.get('name', '')}"]
-        return []
-
-    return fn
-
 
 class EventHandler:
     """add/update/delete callbacks (``cache.ResourceEventHandlerFuncs``)."""

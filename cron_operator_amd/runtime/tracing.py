@@ -187,5 +187,3 @@ def span(name: str, /, **attrs: Any):
     return t.span(name, **attrs)
 
 
-def current_span() -> Optional[Span]:
-    return _current.get()

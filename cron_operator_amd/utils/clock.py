@@ -114,10 +114,6 @@ class FakeClock(Clock):
     def pending(self) -> int:
         return sum(1 for _, _, h in self._heap if not h.cancelled)
 
-    def next_deadline(self) -> Optional[int]:
-        while self._heap and self._heap[0][2].cancelled:
-            heapq.heappop(self._heap)
-        return self._heap[0][0] if self._heap else None
 
     def set(self, t_ns: int) -> int:
         """Move time to ``t_ns`` (never backwards) and fire due timers in order."""
@@ -147,5 +143,3 @@ class FakeClock(Clock):
 _default_clock: Clock = RealClock()
 
 
-def default_clock() -> Clock:
-    return _default_clock

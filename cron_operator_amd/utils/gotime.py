@@ -24,7 +24,7 @@ from __future__ import annotations
 
 import os
 import re
-from datetime import datetime, timezone
+from datetime import datetime
 from functools import lru_cache
 from typing import Optional, Tuple
 
@@ -509,31 +509,3 @@ def parse_duration(s: str) -> int:
     return -total if neg else total
 
 
-def format_duration(ns: int) -> str:
-    """A compact Go-like rendering (used in log lines and event messages)."""
-    if ns == 0:
-        return "0s"
-    neg = ns < 0
-    ns = abs(ns)
-    if ns < SECOND:
-        if ns < 1000:
-            out = f"{ns}ns"
-        elif ns < 1_000_000:
-            out = f"{ns / 1000:g}µs"
-        else:
-            out = f"{ns / 1_000_000:g}ms"
-    else:
-        h, rem = divmod(ns, HOUR)
-        m, rem = divmod(rem, MINUTE)
-        secs = rem / SECOND
-        out = ""
-        if h:
-            out += f"{h}h"
-        if h or m:
-            out += f"{m}m"
-        out += f"{secs:.9f}".rstrip("0").rstrip(".") + "s"
-    return "-" + out if neg else out
-
-
-def now_utc_datetime() -> datetime:
-    return datetime.now(timezone.utc)

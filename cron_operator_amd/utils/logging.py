@@ -232,15 +232,6 @@ def get_logger(name: str = "") -> Logger:
     return _root.with_name(name) if name else _root
 
 
-class DelegatingLogger:
-    """A module-level handle that always resolves to the current root (``ctrl.Log``)."""
-
-    def __init__(self, name: str = ""):
-        self._name = name
-
-    def __getattr__(self, item):
-        return getattr(get_logger(self._name), item)
-
 
 def new_from_options(encoder: Optional[str] = None, level: Optional[str] = None, devel: bool = False,
                      stacktrace_level: Optional[str] = None, time_encoding: Optional[str] = None,

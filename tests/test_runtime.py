@@ -188,6 +188,58 @@ async def test_http_transport_end_to_end():
         await app.stop()
 
 
+async def test_bookmarks_advance_informer_resource_version():
+    """Periodic BOOKMARKs (kube-apiserver sends ~1/min) move an idle informer's resourceVersion to
+    the server's current one, so a resumed watch does not start from a compacted version."""
+    env = TestEnv()
+    app = APIServerApp(env.server)
+    port = await app.start("127.0.0.1", 0, bookmark_interval=0.05)
+    client = Client(HttpTransport(RestConfig(host=f"http://127.0.0.1:{port}")), qps=-1)
+    try:
+        inf = Informer(client, CRON_GVR, "default")
+        inf.start()
+        await asyncio.wait_for(inf.synced.wait(), 5)
+        start_rv = inf.last_rv
+        # writes the informer does not watch (another namespace) still advance the global RV
+        env.server.create_namespace("elsewhere")
+        await client.create(CRON_GVK, new_cron("other", "elsewhere", "* * * * *",
+                                               {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob"}).to_dict())
+        target = str(env.server.current_rv())
+        for _ in range(200):
+            if inf.last_rv == target:
+                break
+            await asyncio.sleep(0.01)
+        assert int(inf.last_rv) > int(start_rv or 0) and inf.last_rv == target
+        assert inf.get("elsewhere", "other") is None  # bookmarks carry no object
+        await inf.stop()
+    finally:
+        await client.close()
+        await app.stop()
+
+
+async def test_workqueue_unfinished_work_metrics_refresh():
+    from cron_operator_amd.runtime import metrics
+    from cron_operator_amd.runtime.controller import Controller, Request
+
+    gate = asyncio.Event()
+
+    class Slow:
+        async def reconcile(self, req, log):
+            await gate.wait()
+
+    ctrl = Controller("unfinished-test", Slow(), FakeClock(0), 1)
+    ctrl.start()
+    ctrl.queue.add(Request("ns", "a"))
+    longest = metrics.WQ_LONGEST.labels("unfinished-test", "unfinished-test")
+    for _ in range(300):
+        if longest.get() > 0:
+            break
+        await asyncio.sleep(0.01)
+    assert longest.get() > 0 and metrics.WQ_UNFINISHED.labels("unfinished-test", "unfinished-test").get() > 0
+    gate.set()
+    await ctrl.stop()
+
+
 def test_resource_paths():
     assert resource_path(CRON_GVR, "ns", "n", "status") == "/apis/apps.kubedl.io/v1alpha1/namespaces/ns/crons/n/status"
     assert resource_path(GroupVersionResource("", "v1", "namespaces"), "", "x") == "/api/v1/namespaces/x"
