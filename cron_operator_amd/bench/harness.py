@@ -6,10 +6,11 @@ reconciles/sec and the p50 schedule->create latency.
 
 One **step** is one schedule tick across all Crons, in virtual time:
 
-1. (untimed, cluster side) the fake training-operator marks every job of the
-   previous tick Succeeded -- on the apiserver, not in the operator;
-2. the timer starts; the operator's clock (and the apiserver's) jumps to the
-   next minute boundary, which fires every Cron's ``RequeueAfter``;
+1. the timer starts; cluster side, the fake training-operator marks every job
+   of the previous tick Succeeded (apiserver work, not operator work, but kept
+   inside the timed region -- conservative);
+2. the operator's clock (and the apiserver's) jumps to the next minute
+   boundary, which fires every Cron's ``RequeueAfter``;
 3. the operator reconciles: moves finished jobs into ``status.history``,
    deletes the ones beyond ``historyLimit`` (GC), creates the tick's job,
    patches status, and absorbs the resulting watch events;
