@@ -239,8 +239,8 @@ class APIServer:
         # (group, resource) -> namespace -> name -> stored object (never mutated in place)
         self._data: Dict[Tuple[str, str], Dict[str, Dict[str, Dict[str, Any]]]] = defaultdict(dict)
         self._watchers: Dict[Tuple[str, str], List[Watcher]] = defaultdict(list)
-        # per resource: (watchers to always offer, {label key: {value: watchers pinned to it}})
-        self._watch_plan: Dict[Tuple[str, str], Tuple[List[Watcher], Dict[str, Dict[str, List[Watcher]]]]] = {}
+        # per resource: (selector groups to always check, {label key: {value: groups pinned to it}})
+        self._watch_plan: Dict[Tuple[str, str], Any] = {}
         self._log: Dict[Tuple[str, str], Deque[Tuple[int, str, Dict[str, Any], Optional[Dict[str, Any]]]]] = {}
         self._log_floor: Dict[Tuple[str, str], int] = defaultdict(int)
         self._watch_window = watch_window
@@ -348,42 +348,48 @@ class APIServer:
         if plan is None:
             plan = self._watch_plan[key] = self._plan(ws)
         plain, pinned = plan
-        targets = plain
+        groups = plain
         modified = etype == "MODIFIED" and old is not None
         if pinned:
             # watchers whose selector pins a label value only see objects carrying it (before or after)
-            targets = list(plain)
+            groups = list(plain)
             labels = (obj.get("metadata") or {}).get("labels") or {}
             old_labels = ((old.get("metadata") or {}).get("labels") or {}) if modified else None
             for lk, by_value in pinned.items():
                 v = labels.get(lk)
                 hit = by_value.get(v)
                 if hit:
-                    targets.extend(hit)
+                    groups.extend(hit)
                 if old_labels is not None:
                     ov = old_labels.get(lk)
                     if ov != v:
                         hit = by_value.get(ov)
                         if hit:
-                            targets.extend(hit)
-        # one selector evaluation per distinct (namespace, selector) per event
-        seen: Dict[Tuple[Optional[str], Any], Tuple[bool, bool]] = {}
-        for w in targets:
-            gk = (w.namespace, w.pred)
-            r = seen.get(gk)
-            if r is None:
-                r = seen[gk] = (w._in_scope(obj), w._in_scope(old) if modified else False)  # type: ignore[arg-type]
-            w.offer_scoped(etype, obj, old, r[0], r[1])
+                            groups.extend(hit)
+        # one selector evaluation per (namespace, selector) group per event
+        for first, members in groups:
+            now_in = first._in_scope(obj)
+            was_in = first._in_scope(old) if modified else False  # type: ignore[arg-type]
+            if now_in or was_in:
+                for w in members:
+                    w.offer_scoped(etype, obj, old, now_in, was_in)
 
     @staticmethod
-    def _plan(ws: List[Watcher]) -> Tuple[List[Watcher], Dict[str, Dict[str, List[Watcher]]]]:
-        plain: List[Watcher] = []
-        pinned: Dict[str, Dict[str, List[Watcher]]] = {}
+    def _plan(ws: List[Watcher]) -> Tuple[List[Tuple[Watcher, List[Watcher]]],
+                                         Dict[str, Dict[str, List[Tuple[Watcher, List[Watcher]]]]]]:
+        """Watchers grouped by (namespace, selector); groups with a pinned label value indexed
+        by it.  A group is ``(representative, members)``."""
+        by_sel: Dict[Tuple[Optional[str], Any], List[Watcher]] = {}
         for w in ws:
-            if w.pinned is None:
-                plain.append(w)
+            by_sel.setdefault((w.namespace, w.pred), []).append(w)
+        plain: List[Tuple[Watcher, List[Watcher]]] = []
+        pinned: Dict[str, Dict[str, List[Tuple[Watcher, List[Watcher]]]]] = {}
+        for members in by_sel.values():
+            first = members[0]
+            if first.pinned is None:
+                plain.append((first, members))
             else:
-                pinned.setdefault(w.pinned[0], {}).setdefault(w.pinned[1], []).append(w)
+                pinned.setdefault(first.pinned[0], {}).setdefault(first.pinned[1], []).append((first, members))
         return plain, pinned
 
     def _remove_watcher(self, w: Watcher) -> None:
