@@ -191,6 +191,11 @@ class Expectations:
         if d is not None and d.pop(uid, None) is not None and not d:
             del self.deleted[key]
 
+    def forget(self, key: str) -> None:
+        self.created.pop(key, None)
+        self.deleted.pop(key, None)
+        self.pending.pop(key, None)
+
     def matches_created(self, key: str, obj: Dict[str, Any]) -> bool:
         """Is ``obj`` exactly the object our CREATE returned (same uid and resourceVersion)?"""
         m = obj.get("metadata") or {}
@@ -256,6 +261,16 @@ class CronReconciler(Reconciler):
         # tick bookkeeping for latency: key -> (tick unix ns, wall perf_counter when it became due)
         self.latency_observer: Optional[Callable[[str, GoTime, Dict[str, Any]], None]] = None
 
+    def forget_cron(self, key: str) -> None:
+        """Drop the per-Cron memos of a Cron that is gone (``namespace/name``)."""
+        self._parsed_status.pop(key, None)
+        self.own_writes.pop(key, None)
+        self.expect.forget(key)
+
+    def forget_child(self, uid: str) -> None:
+        """Drop the per-child memo of a deleted child."""
+        self._class_cache.pop(uid, None)
+
     # ------------------------------------------------------------------ entry point
     async def reconcile(self, req: Request, log: Logger) -> Result:
         """``Reconcile`` (``cron_controller.go:90-239``)."""
@@ -280,7 +295,7 @@ class CronReconciler(Reconciler):
         old_obj = await self._get_cron(req)
         if old_obj is None:
             log.info("Skip reconciling Cron for it may have been deleted")
-            self._parsed_status.pop(f"{req.namespace}/{req.name}", None)
+            self.forget_cron(f"{req.namespace}/{req.name}")
             return Result()
         parsed = None
         if self.opts.classification_cache:

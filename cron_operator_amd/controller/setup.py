@@ -95,6 +95,9 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
                 on_add=lambda o: rec.expect.observe_add(key_of(o), (o.get("metadata") or {}).get("uid", "")),
                 on_update=lambda old, o: rec.expect.observe_add(key_of(o), (o.get("metadata") or {}).get("uid", "")),
                 on_delete=lambda o: rec.expect.observe_delete(key_of(o), (o.get("metadata") or {}).get("uid", ""))))
+        if opts.classification_cache:
+            inf.add_handler(EventHandler(
+                on_delete=lambda o: rec.forget_child((o.get("metadata") or {}).get("uid", ""))))
 
     for gvk in opts.static_owned_kinds:
         try:

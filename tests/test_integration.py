@@ -346,3 +346,28 @@ async def test_label_routing_reshard_relabels_crons_and_children():
         assert o["metadata"]["labels"][LABEL_SHARD] == f"{shard_of(NS, cron, 3)}-of-3"
     await trainer.stop()
     env.server.close_all_watches()
+
+
+async def test_memos_dropped_when_crons_and_children_go_away():
+    """Per-Cron memos (own writes, parsed status, expectations) and per-child memos are dropped
+    when the Cron or the child is deleted, so a churning fleet does not grow them forever."""
+    env = TestEnv()
+    await env.create_cron(new_cron("m", NS, "*/1 * * * *", PT_TMPL))
+    await env.start_manager()
+    await env.settle()
+    await env.advance(60)
+    rec = env.reconciler
+    job = names(env.server, PT, "m")[0]
+    env.server.patch(PT, NS, job, {"status": {"conditions": [{"type": "Succeeded", "status": "True"}]}},
+                     "merge", "status")
+    await env.settle()
+    uid = env.server.get(PT, NS, job)["metadata"]["uid"]
+    assert uid in rec._class_cache and f"{NS}/m" in rec.own_writes and f"{NS}/m" in rec._parsed_status
+    env.server.delete(PT, NS, job)
+    await env.settle()
+    assert uid not in rec._class_cache
+    env.server.delete(CRON_GVR, NS, "m")
+    await env.settle()
+    assert f"{NS}/m" not in rec.own_writes and f"{NS}/m" not in rec._parsed_status
+    assert f"{NS}/m" not in rec.expect.created and f"{NS}/m" not in rec.expect.deleted
+    await env.stop()
