@@ -358,16 +358,20 @@ class HttpPool:
         if self.scheme == "https" and self.ssl is None:
             self.ssl = _ssl.create_default_context()
         self.server_hostname = server_hostname
-        hosthdr = self.host if (self.port in (80, 443)) else f"{self.host}:{self.port}"
-        hdrs = {"User-Agent": "cron-operator-amd"}
-        hdrs.update({k: v for k, v in (headers or {}).items() if k.lower() != "accept"})
-        extra = "".join(f"{k}: {v}\r\n" for k, v in hdrs.items())
-        self._fixed = f"Host: {hosthdr}\r\n{extra}"
+        self._hosthdr = self.host if (self.port in (80, 443)) else f"{self.host}:{self.port}"
+        self.set_headers(headers)
         self._idle: Deque[_Conn] = deque()
         self.max_idle = max_idle
         self.timeout = timeout
         self.connects = 0
         self._closed = False
+
+    def set_headers(self, headers: Optional[Dict[str, str]]) -> None:
+        """Replace the headers sent with every request (e.g. a rotated ``Authorization``)."""
+        hdrs = {"User-Agent": "cron-operator-amd"}
+        hdrs.update({k: v for k, v in (headers or {}).items() if k.lower() != "accept"})
+        extra = "".join(f"{k}: {v}\r\n" for k, v in hdrs.items())
+        self._fixed = f"Host: {self._hosthdr}\r\n{extra}"
 
     async def _connect(self) -> _Conn:
         loop = asyncio.get_running_loop()

@@ -117,13 +117,34 @@ class HttpTransport(Transport):
         self._session: Optional[aiohttp.ClientSession] = None
         self.fast = fast
         self._pool: Optional[HttpPool] = None
+        self._token = ""  # the bearer token the pool/session headers carry
 
     def _fast_pool(self) -> HttpPool:
         if self._pool is None:
+            self._token = self.config.token()
             self._pool = HttpPool(self.config.host, ssl_context=self.config.ssl_context() or None,
                                   headers=self.config.auth_headers(), max_idle=self._pool_size,
                                   timeout=self._timeout, server_hostname=self.config.tls_server_name or None)
+        elif self.config.bearer_token_file:
+            self._rotate_token()
         return self._pool
+
+    def _rotate_token(self) -> None:
+        """Re-stamp ``Authorization`` when the token file's content changed (kubeconfig.py)."""
+        tok = self.config.token()
+        if tok == self._token:
+            return
+        self._token = tok
+        hdrs = self.config.auth_headers()
+        if self._pool is not None:
+            self._pool.set_headers(hdrs)
+        if self._session is not None and not self._session.closed:
+            self._session.headers.update(hdrs)
+
+    def _unauthorized(self) -> None:
+        """A 401: drop the cached file token so the next request re-reads it."""
+        if self.config.bearer_token_file:
+            self.config.reset_token()
 
     def _tls_kw(self) -> Dict[str, Any]:
         """kubeconfig ``tls-server-name``: verify the certificate against this name."""
@@ -131,7 +152,10 @@ class HttpTransport(Transport):
         return {"server_hostname": name} if name and self.config.host.startswith("https://") else {}
 
     def _sess(self) -> aiohttp.ClientSession:
+        if self.config.bearer_token_file and self._session is not None:
+            self._rotate_token()
         if self._session is None or self._session.closed:
+            self._token = self.config.token()
             conn = aiohttp.TCPConnector(limit=self._pool_size, ssl=self.config.ssl_context() or False,
                                         keepalive_timeout=120)
             self._session = aiohttp.ClientSession(connector=conn, headers=self.config.auth_headers(),
@@ -139,6 +163,8 @@ class HttpTransport(Transport):
         return self._session
 
     async def _raise(self, resp: aiohttp.ClientResponse) -> None:
+        if resp.status == 401:
+            self._unauthorized()
         raw = await resp.read()
         try:
             body: Any = json.loads(raw)
@@ -170,6 +196,8 @@ class HttpTransport(Transport):
                 metrics.REST_RETRIES.labels(str(status), method, self.host).inc()
                 await asyncio.sleep(max(0, retry_after))
             if status >= 400:
+                if status == 401:
+                    self._unauthorized()
                 try:
                     err_body: Any = jsonutil.loads(raw)
                 except ValueError:
@@ -205,6 +233,8 @@ class HttpTransport(Transport):
                 stream = await self._fast_pool().open_stream(resource_path(gvr, namespace) + encode_query(p),
                                                              _decode_event)
             except HttpStatusError as e:
+                if e.status == 401:
+                    self._unauthorized()
                 raise _status_error(e.status, e.body) from None
             except (ConnectionFailed, OSError, asyncio.TimeoutError) as e:
                 raise errors.ApiError(503, "ServiceUnavailable", f"connection error: {e}") from None

@@ -7,6 +7,14 @@ then ``~/.kube/config``.  Supported kubeconfig auth: bearer token / tokenFile,
 client certificate + key (file or ``*-data``), basic auth, CA bundle or
 ``insecure-skip-tls-verify``, ``tls-server-name`` and ``proxy-url``-less
 direct connections.  ``--qps``/``--burst`` are applied by the caller.
+
+Token files rotate: the in-cluster service-account token is a projected,
+kubelet-refreshed file (bound tokens expire; ``/var/run/secrets/.../token``).
+[ext client-go ``transport.NewCachedFileTokenSource``] re-reads the file once
+a minute (10 s leeway) and drops its cached token when a request comes back
+401; :meth:`RestConfig.token` and :meth:`RestConfig.reset_token` do the same,
+and the HTTP transport re-stamps its ``Authorization`` header when the token
+changes (``runtime/http.py``).
 """
 from __future__ import annotations
 
@@ -14,12 +22,15 @@ import base64
 import os
 import ssl
 import tempfile
+import time
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional
 
 import yaml
 
 SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
+TOKEN_FILE_PERIOD = 60.0   # client-go fileTokenSource: a token read from a file is good for a minute
+TOKEN_LEEWAY = 10.0        # client-go cachingTokenSource: refresh that long before expiry
 
 
 class ConfigError(RuntimeError):
@@ -45,15 +56,29 @@ class RestConfig:
     burst: int = 50
     user_agent: str = "cron-operator-amd"
     _tmp: List[str] = field(default_factory=list)
+    _file_token: str = ""
+    _file_token_refresh_at: float = 0.0   # monotonic; 0 = read on next use
 
     def token(self) -> str:
+        """The bearer token; a ``tokenFile`` is re-read at most once per ``TOKEN_FILE_PERIOD -
+        TOKEN_LEEWAY`` seconds.  A read error keeps the last good token (client-go logs and
+        serves the cached one), falling back to the inline ``token``."""
         if self.bearer_token_file:
-            try:
-                with open(self.bearer_token_file) as fh:
-                    return fh.read().strip()
-            except OSError:
-                pass
+            now = time.monotonic()
+            if now >= self._file_token_refresh_at:
+                try:
+                    with open(self.bearer_token_file) as fh:
+                        self._file_token = fh.read().strip()
+                    self._file_token_refresh_at = now + TOKEN_FILE_PERIOD - TOKEN_LEEWAY
+                except OSError:
+                    pass
+            if self._file_token:
+                return self._file_token
         return self.bearer_token
+
+    def reset_token(self) -> None:
+        """Forget the cached file token (client-go ``ResetTokenOlderThan`` after a 401)."""
+        self._file_token_refresh_at = 0.0
 
     def _materialise(self, data: bytes, suffix: str) -> str:
         fd, path = tempfile.mkstemp(prefix="cron-operator-", suffix=suffix)

@@ -265,6 +265,51 @@ async def test_http_bearer_token_required():
         await app.stop()
 
 
+@pytest.mark.parametrize("fast", [True, False])
+async def test_http_token_file_rotation(fast):
+    """A projected service-account token rotates under the running operator: the file is
+    re-read once its cache period passes, and a 401 forces the re-read right away."""
+    env = TestEnv()
+    env.server.tokens = {"tok-1": {"username": "u"}}
+    app = APIServerApp(env.server)
+    port = await app.start("127.0.0.1", 0)
+    with tempfile.TemporaryDirectory() as d:
+        path = os.path.join(d, "token")
+        with open(path, "w") as fh:
+            fh.write("tok-1\n")
+        cfg = RestConfig(host=f"http://127.0.0.1:{port}", bearer_token_file=path)
+        c = Client(HttpTransport(cfg, fast=fast), qps=-1)
+        try:
+            with pytest.raises(errors.ApiError) as e:
+                await c.get(CRON_GVR, "default", "x")
+            assert e.value.code == 404
+            # kubelet rotates the file; the apiserver stops accepting the old token
+            with open(path, "w") as fh:
+                fh.write("tok-2\n")
+            env.server.tokens = {"tok-2": {"username": "u"}}
+            with pytest.raises(errors.ApiError) as e:  # cached old token: one 401 ...
+                await c.get(CRON_GVR, "default", "x")
+            assert e.value.code == 401
+            with pytest.raises(errors.ApiError) as e:  # ... which drops the cache
+                await c.get(CRON_GVR, "default", "x")
+            assert e.value.code == 404
+            # and the periodic re-read, without a 401
+            with open(path, "w") as fh:
+                fh.write("tok-3\n")
+            env.server.tokens = {"tok-2": {"username": "u"}, "tok-3": {"username": "u"}}
+            cfg._file_token_refresh_at = 0.0  # the minute passed
+            await c.create(CM, {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "rot"}}, "default")
+            env.server.tokens = {"tok-3": {"username": "u"}}
+            assert (await c.get(CM, "default", "rot"))["metadata"]["name"] == "rot"
+            # a vanished file keeps the last good token
+            os.unlink(path)
+            cfg._file_token_refresh_at = 0.0
+            assert cfg.token() == "tok-3"
+        finally:
+            await c.close()
+            await app.stop()
+
+
 # ---------------------------------------------------------------- leader election
 
 
