@@ -22,7 +22,17 @@ option                     default here                           reference
 ``dynamic_watches``        watch whatever kind templates use      PyTorchJob + TFJob only (B22)
 ``dedupe_ran_tick``        a tick whose job already exists is     the tick runs again when the status
                            recorded, not run again                 write after its CREATE was lost
+``overlap_gc_deletes``     history-GC DELETEs run concurrently    each DELETE awaited in turn, before
+                           with the rest of the reconcile          the CREATE and the status PATCH
 =========================  =====================================  =======================================
+
+``overlap_gc_deletes``: a GC DELETE's outcome feeds nothing else in the
+reconcile -- the reference only logs its error and drops the child from
+``status.history`` either way (``cron_controller.go:324-333``) -- so the
+DELETEs are started as they are decided and awaited together with the status
+PATCH at the end.  Under apiserver latency a reconcile then costs one round
+trip less per GC'd child; the reconcile still returns only after every DELETE
+finished, so per-key serialisation is unchanged.
 
 ``dedupe_ran_tick``: the reference advances ``lastScheduleTime`` only in the
 deferred status patch after a successful CREATE (B20).  If that patch fails, or
@@ -39,6 +49,7 @@ Time comes from the injected clock (the reference calls ``time.Now()``,
 """
 from __future__ import annotations
 
+import asyncio
 import json
 import time
 from dataclasses import dataclass, field
@@ -134,6 +145,7 @@ class ReconcilerOptions:
     skip_expected_events: bool = True        # child add/delete events we caused do not requeue the Cron
     classification_cache: bool = True
     dedupe_ran_tick: bool = True
+    overlap_gc_deletes: bool = True
     workload: WorkloadPolicy = field(default_factory=WorkloadPolicy)
     static_owned_kinds: Tuple[GroupVersionKind, ...] = (
         GroupVersionKind("kubeflow.org", "v1", "PyTorchJob"),
@@ -146,7 +158,7 @@ class ReconcilerOptions:
                                  own_write_filter=False, dynamic_watches=False, expectations=False,
                                  fold_created_into_active=False, skip_expected_events=False,
                                  classification_cache=False, dedupe_ran_tick=False,
-                                 workload=WorkloadPolicy.reference())
+                                 overlap_gc_deletes=False, workload=WorkloadPolicy.reference())
 
 
 class Expectations:
@@ -307,23 +319,38 @@ class CronReconciler(Reconciler):
 
         result = Result()
         err: Optional[BaseException] = None
+        gc: Optional[List["asyncio.Future[None]"]] = [] if self.opts.overlap_gc_deletes else None
         try:
-            result = await self._sync(cron, log)
+            result = await self._sync(cron, log, gc)
         except Exception as e:  # noqa: BLE001 - joined with the patch error below
             err = e
         # B2: deferred status patch when status changed semantically (cron_controller.go:107-120)
         if not old_status.semantic_equal(cron.status):
             try:
-                await self._patch_status(old_obj, cron, log)
+                if gc:
+                    pending, gc = gc, None
+                    perr0, _ = await asyncio.gather(self._patch_status(old_obj, cron, log), self._await_gc(pending),
+                                                    return_exceptions=True)
+                    if isinstance(perr0, BaseException):
+                        raise perr0
+                else:
+                    await self._patch_status(old_obj, cron, log)
             except Exception as pe:  # noqa: BLE001
                 perr = RuntimeError(f"failed to patch Cron status: {pe}")
                 perr.__cause__ = pe
                 err = JoinedError(err, perr) if err is not None else perr
             if err is not None:
                 result = Result()
+        if gc:
+            await self._await_gc(gc)
         if err is not None:
             raise err
         return result
+
+    @staticmethod
+    async def _await_gc(gc: List["asyncio.Future[None]"]) -> None:
+        """Wait for every overlapped GC DELETE; each logs its own API error (B7)."""
+        await asyncio.gather(*gc, return_exceptions=True)
 
     async def _patch_status(self, old_obj: Dict[str, Any], cron: Cron, log: Logger) -> None:
         new_status = cron.status.to_dict()
@@ -372,7 +399,7 @@ class CronReconciler(Reconciler):
         return jsonutil.json_equal(new.get("status") or {}, status)
 
     # ------------------------------------------------------------------ the algorithm
-    async def _sync(self, cron: Cron, log: Logger) -> Result:
+    async def _sync(self, cron: Cron, log: Logger, gc: Optional[List["asyncio.Future[None]"]] = None) -> Result:
         policy = self.opts.workload
         # B3 (cron_controller.go:122-126)
         try:
@@ -418,7 +445,7 @@ class CronReconciler(Reconciler):
 
         # B6/B7/B8 (cron_controller.go:155-158)
         with tracing.span("sync_status", active=len(active), terminated=len(terminated)):
-            await self.sync_status(cron, gvk, active, terminated, log)
+            await self.sync_status(cron, gvk, active, terminated, log, gc)
 
         now = self.clock.now(LOCAL)
 
@@ -596,11 +623,12 @@ class CronReconciler(Reconciler):
 
     # ------------------------------------------------------------------ status
     async def sync_status(self, cron: Cron, gvk: GroupVersionKind, active: List[Child],
-                          terminated: List[Child], log: Logger) -> None:
+                          terminated: List[Child], log: Logger,
+                          gc: Optional[List["asyncio.Future[None]"]] = None) -> None:
         """``syncStatus`` (``cron_controller.go:268-282``)."""
         log.v(1).info("Syncing Cron status")
         self.sync_active_list(cron, gvk, active, log)
-        await self.sync_cron_history(cron, gvk, terminated, log)
+        await self.sync_cron_history(cron, gvk, terminated, log, gc)
 
     @staticmethod
     def _sort(items: List[Child]) -> None:
@@ -632,8 +660,12 @@ class CronReconciler(Reconciler):
         cron.status.active = refs
 
     async def sync_cron_history(self, cron: Cron, gvk: GroupVersionKind,
-                                terminated: List[Child], log: Logger) -> None:
-        """``syncCronHistory`` incl. history-limit GC (``cron_controller.go:306-346``)."""
+                                terminated: List[Child], log: Logger,
+                                gc: Optional[List["asyncio.Future[None]"]] = None) -> None:
+        """``syncCronHistory`` incl. history-limit GC (``cron_controller.go:306-346``).
+
+        With ``gc`` (a list) the DELETEs are started and appended there instead of
+        awaited one by one (``ReconcilerOptions.overlap_gc_deletes``)."""
         log.v(1).info("Syncing Cron history")
         self._sort(terminated)
         n = len(terminated)
@@ -655,16 +687,11 @@ class CronReconciler(Reconciler):
                 uid = m.get("uid", "")
                 if self.opts.expectations:  # before the call: the watch event may beat the response
                     self.expect.expect_delete(self._ckey(cron), uid)
-                try:
-                    await self.client.delete(wgvk, m.get("namespace", ""), m.get("name", ""),
-                                             propagation_policy="Background", discard_response=True)
-                    self.stats["deletes"] += 1
-                    metrics.child(metrics.WORKLOADS_DELETED, wgvk.kind, "history").inc()
-                except errors.ApiError as e:
-                    if not errors.is_not_found(e):
-                        if self.opts.expectations:
-                            self.expect.observe_delete(self._ckey(cron), uid)
-                        log.error(e, f"Failed to delete terminated {wgvk.kind}", **{wgvk.kind: ref})
+                op = self._gc_delete(cron, wgvk, m.get("namespace", ""), m.get("name", ""), uid, ref, log)
+                if gc is None:
+                    await op
+                else:
+                    gc.append(asyncio.ensure_future(op))
                 continue
             if not memo_ok:
                 info = None
@@ -693,6 +720,19 @@ class CronReconciler(Reconciler):
                         entry.finished = GoTime(t.sec, 0, t.loc)
             history.append(entry)
         cron.status.history = history
+
+    async def _gc_delete(self, cron: Cron, gvk: GroupVersionKind, namespace: str, name: str, uid: str,
+                         ref: ObjectRef, log: Logger) -> None:
+        """One history-limit DELETE (Background); errors are only logged (``cron_controller.go:324-333``)."""
+        try:
+            await self.client.delete(gvk, namespace, name, propagation_policy="Background", discard_response=True)
+            self.stats["deletes"] += 1
+            metrics.child(metrics.WORKLOADS_DELETED, gvk.kind, "history").inc()
+        except errors.ApiError as e:
+            if not errors.is_not_found(e):
+                if self.opts.expectations:
+                    self.expect.observe_delete(self._ckey(cron), uid)
+                log.error(e, f"Failed to delete terminated {gvk.kind}", **{gvk.kind: ref})
 
     # ------------------------------------------------------------------ workload creation
     def new_workload_from_template(self, cron: Cron, schedule_time: GoTime) -> Dict[str, Any]:

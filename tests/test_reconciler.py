@@ -282,6 +282,37 @@ async def test_b7_history_limit_gc(mode, limit, kept):
     assert [h["object"]["name"] for h in hist] == remaining
 
 
+async def test_b7_gc_deletes_overlap_the_status_patch():
+    """``overlap_gc_deletes``: under apiserver latency the GC DELETEs and the status PATCH
+    take one round trip together, not one each -- and the reconcile still returns only after
+    every DELETE finished; a failed DELETE is only logged, as in the reference."""
+    import time
+
+    async def run(opts):
+        rig = Rig(opts)
+        await rig.create(history_limit=1)
+        for i in range(4):
+            rig.clock.advance(1)
+            name = f"{NAME}-{i}"
+            rig.server.create(PT, NS, {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+                                       "metadata": {"name": name, "labels": {LABEL_CRON_NAME: NAME}}})
+            rig.finish(name)
+        rig.server.faults.add(verb="delete", resource="pytorchjobs", name=f"{NAME}-1", code=500)
+        rig.server.faults.latency.update({"delete": 0.08, "patch": 0.08})
+        t0 = time.perf_counter()
+        await rig.reconcile()
+        dt = time.perf_counter() - t0
+        rig.server.faults.clear()
+        assert sorted(j["metadata"]["name"] for j in rig.jobs()) == [f"{NAME}-1", f"{NAME}-3"]
+        assert [h["object"]["name"] for h in rig.cron()["status"]["history"]] == [f"{NAME}-3"]
+        return dt
+
+    seq = await run(ReconcilerOptions(list_mode="live", overlap_gc_deletes=False))
+    par = await run(ReconcilerOptions(list_mode="live"))
+    assert seq >= 0.3  # 3 DELETEs + 1 PATCH, one after the other
+    assert par < 0.2, (seq, par)
+
+
 async def test_b7_finished_time_now_vs_completion():
     ref = Rig(ReconcilerOptions.reference())
     opt = Rig(ReconcilerOptions(list_mode="live"))
