@@ -32,6 +32,7 @@ from urllib.parse import parse_qsl, unquote
 
 from ..api import errors
 from ..api.meta import GroupVersionResource
+from ..ops import httpcodec_native
 from ..utils import jsonutil
 from ..utils.clock import FakeClock
 from .server import APIServer, Watcher
@@ -48,6 +49,8 @@ _REASONS = {200: "OK", 201: "Created", 202: "Accepted", 204: "No Content", 400: 
             429: "Too Many Requests", 431: "Request Header Fields Too Large", 500: "Internal Server Error",
             503: "Service Unavailable", 504: "Gateway Timeout"}
 MAX_BODY = 64 * 1024 * 1024
+_codec = httpcodec_native.load()  # native request framing (ops/csrc/httpcodec.cpp), else None
+_CODEC_ERRORS = {400: b"bad request", 413: b"request body too large", 431: b"request header too large"}
 
 
 class _EncodeCache:
@@ -516,6 +519,32 @@ class _ServerConn(asyncio.Protocol):
 
     # --------------------------------------------------------------- parsing
     def _next_request(self) -> Optional[Tuple[Request, bool]]:
+        if _codec is None:
+            return self._next_request_py()
+        r = _codec.parse_request(self.buf, MAX_BODY)
+        if r is None:
+            return None
+        if r.__class__ is int:
+            if r == 100:
+                if not self._continued:
+                    self._continued = True
+                    assert self.transport is not None
+                    self.transport.write(b"HTTP/1.1 100 Continue\r\n\r\n")
+                return None
+            self._reply_raw(r, _CODEC_ERRORS.get(r, b"bad request"), "text/plain", close=True)
+            return None
+        method, target, headers, raw, consumed, keep = r
+        del self.buf[:consumed]
+        self._continued = False
+        path, _, qs = target.partition("?")
+        query: Dict[str, str] = {}
+        if qs:
+            for k, v in parse_qsl(qs, keep_blank_values=True):
+                query.setdefault(k, v)
+        return Request(method.upper(), unquote(path) if "%" in path else path, query, headers, raw), keep
+
+    def _next_request_py(self) -> Optional[Tuple[Request, bool]]:
+        """Pure-Python framing: the fallback, and the oracle of tests/test_httpcodec.py."""
         buf = self.buf
         end = buf.find(b"\r\n\r\n")
         if end < 0:

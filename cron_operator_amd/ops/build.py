@@ -27,6 +27,7 @@ CSRC = HERE / "csrc"
 EXTENSIONS: Dict[str, List[str]] = {
     "_cron_engine": ["cron_engine.cpp"],
     "_fastjson": ["fastjson.cpp"],
+    "_httpcodec": ["httpcodec.cpp"],
 }
 
 

@@ -32,6 +32,10 @@ from collections import deque
 from typing import Deque, Dict, List, Optional, Tuple
 from urllib.parse import urlsplit
 
+from ..ops import httpcodec_native
+
+_codec = httpcodec_native.load()  # native response framing (ops/csrc/httpcodec.cpp), else None
+
 
 class ConnectionFailed(Exception):
     """The connection broke; ``no_response`` + ``reused`` tell whether a retry is safe."""
@@ -94,6 +98,19 @@ class _Conn(asyncio.Protocol):
                 self.transport.close()
 
     def _parse(self) -> None:
+        if _codec is not None and self._state == 0:
+            r = _codec.parse_response(self.buf)
+            if r is None:
+                return
+            if r.__class__ is tuple:
+                self._status, self._body, consumed, self._close_after, self.retry_after = r
+                del self.buf[:consumed]
+                self._finish()
+                return
+            # -1: an interim 1xx or a read-until-close body: the incremental parser below
+        self._parse_py()
+
+    def _parse_py(self) -> None:
         buf = self.buf
         while True:
             if self._state == 0:

@@ -52,9 +52,14 @@ def test_native_components_loaded():
     from cron_operator_amd.ops import cron_native
     from cron_operator_amd.utils import jsonutil
 
+    from cron_operator_amd.apiserver import http as srvhttp
+    from cron_operator_amd.runtime import fasthttp
+
     NativeEngine()
     assert os.path.realpath(cron_native.engine_path()).startswith(os.path.realpath(ROOT))
     assert jsonutil.NATIVE
+    assert fasthttp._codec is not None and srvhttp._codec is not None
+    assert os.path.realpath(fasthttp._codec.__file__).startswith(os.path.realpath(ROOT))
 
 
 def test_train_smoke_payload_on_gpu(gpu):
