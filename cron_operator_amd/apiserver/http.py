@@ -413,14 +413,19 @@ class APIServerApp:
                                        body.get("resource", "pytorchjobs"))
             ts = body.get("time") or ""
             n = 0
-            for obj in list(s.objects(gvr, body.get("namespace"))):
-                st = obj.get("status") or {}
-                if st.get("completionTime"):
-                    continue
-                m = obj["metadata"]
-                s.patch(gvr, m["namespace"], m["name"],
-                        {"status": finished_status(obj.get("kind", ""), m["name"], ts, True)}, "merge", "status")
-                n += 1
+            # each patch body is built here and its result discarded: no defensive copies (as in _verb)
+            s.copy_responses = s.copy_inputs = False
+            try:
+                for obj in list(s.objects(gvr, body.get("namespace"))):
+                    st = obj.get("status") or {}
+                    if st.get("completionTime"):
+                        continue
+                    m = obj["metadata"]
+                    s.patch(gvr, m["namespace"], m["name"],
+                            {"status": finished_status(obj.get("kind", ""), m["name"], ts, True)}, "merge", "status")
+                    n += 1
+            finally:
+                s.copy_responses = s.copy_inputs = True
             return _json({"completed": n})
         if what == "profile" and req.method == "POST":
             # cProfile of this process between "start" and "stop" (the bench profiles its timed steps)

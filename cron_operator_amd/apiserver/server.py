@@ -133,6 +133,9 @@ class Watcher:
         self._match = getattr(pred, "_fn", pred)
         # label routing key of the selector (Selector.pinned): lets _emit skip watchers by index
         self.pinned: Optional[Tuple[str, str]] = getattr(pred, "pinned", None)
+        # the selector reads only labels (+ the namespace above): an update that keeps both
+        # cannot move the object in or out of scope
+        self.labels_only = getattr(pred, "field_selector", None) == ""
         self.bookmarks = bookmarks
         self.queue: "asyncio.Queue[Optional[Tuple[str, Dict[str, Any]]]]" = asyncio.Queue()
         self.closed = False
@@ -366,10 +369,21 @@ class APIServer:
                         hit = by_value.get(ov)
                         if hit:
                             groups.extend(hit)
+        same_scope = False
+        if modified:
+            om = old.get("metadata") or {}  # type: ignore[union-attr]
+            nm = obj.get("metadata") or {}
+            ol, nl = om.get("labels"), nm.get("labels")
+            same_scope = (ol is nl or ol == nl) and om.get("namespace") == nm.get("namespace")
         # one selector evaluation per (namespace, selector) group per event
         for first, members in groups:
             now_in = first._in_scope(obj)
-            was_in = first._in_scope(old) if modified else False  # type: ignore[arg-type]
+            if not modified:
+                was_in = False
+            elif same_scope and first.labels_only:
+                was_in = now_in
+            else:
+                was_in = first._in_scope(old)  # type: ignore[arg-type]
             if now_in or was_in:
                 for w in members:
                     w.offer_scoped(etype, obj, old, now_in, was_in)
@@ -746,13 +760,15 @@ class APIServer:
     def _remove(self, ri: ResourceInfo, ns: str, name: str, old: Dict[str, Any]) -> Dict[str, Any]:
         self._bucket(ri).get(ns, {}).pop(name, None)
         rv = self._next_rv()
-        gone_obj = jsonutil.deepcopy(old)
+        # stored objects are immutable: the tombstone shares everything but its metadata
+        gone_obj = dict(old)
+        gone_obj["metadata"] = dict(old["metadata"])
         gone_obj["metadata"]["resourceVersion"] = str(rv)
         self._index_owners(ri, None, old)
         self._emit(ri, "DELETED", gone_obj, None, rv)
         if self.gc_enabled:
             self._schedule_gc(ri, old)
-        return gone_obj
+        return self._out(gone_obj)
 
     def delete_collection(self, gvr: GroupVersionResource, namespace: Optional[str],
                           label_selector: Optional[str] = None) -> int:
