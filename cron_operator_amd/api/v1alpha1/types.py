@@ -117,18 +117,25 @@ class CronHistory:
     uid: str = ""
     created: Optional[GoTime] = None
     finished: Optional[GoTime] = None
+    # to_dict(shared=True) result: entries are complete before they are first serialised and
+    # never mutated after (the reconciler reuses one entry per child version across reconciles)
+    _json: Optional[Dict[str, Any]] = field(default=None, init=False, repr=False, compare=False)
 
-    def to_dict(self) -> Dict[str, Any]:
+    def to_dict(self, shared: bool = False) -> Dict[str, Any]:
+        """JSON form; ``shared=True`` returns one cached dict per entry (read-only for callers)."""
+        if shared and self._json is not None:
+            return self._json
         d: Dict[str, Any] = {}
         if self.uid:
             d["uid"] = self.uid
         d["object"] = self.object.to_dict()
         d["status"] = self.status
-        c = time_to_json(self.created)
         if self.created is not None:
-            d["created"] = c
+            d["created"] = time_to_json(self.created)
         if self.finished is not None:
             d["finished"] = time_to_json(self.finished)
+        if shared:
+            self._json = d
         return d
 
     @staticmethod
@@ -151,12 +158,14 @@ class CronStatus:
     def is_zero(self) -> bool:
         return not self.active and not self.history and self.last_schedule_time is None
 
-    def to_dict(self) -> Dict[str, Any]:
+    def to_dict(self, shared: bool = False) -> Dict[str, Any]:
+        """JSON form; ``shared=True`` reuses each history entry's cached dict (the result is then
+        read-only: the reconciler's status write only compares and serialises it)."""
         d: Dict[str, Any] = {}
         if self.active:
             d["active"] = [a.to_dict() for a in self.active]
         if self.history:
-            d["history"] = [h.to_dict() for h in self.history]
+            d["history"] = [h.to_dict(shared) for h in self.history]
         if self.last_schedule_time is not None:
             d["lastScheduleTime"] = time_to_json(self.last_schedule_time)
         return d

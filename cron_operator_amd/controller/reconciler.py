@@ -353,7 +353,7 @@ class CronReconciler(Reconciler):
         await asyncio.gather(*gc, return_exceptions=True)
 
     async def _patch_status(self, old_obj: Dict[str, Any], cron: Cron, log: Logger) -> None:
-        new_status = cron.status.to_dict()
+        new_status = cron.status.to_dict(shared=True)
         old_status = old_obj.get("status") or {}
         patch = jsonutil.create_merge_patch({"status": old_status}, {"status": new_status} if new_status else {})
         m = old_obj.get("metadata") or {}
