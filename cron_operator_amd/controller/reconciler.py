@@ -81,6 +81,7 @@ from ..models.workload import (
     WorkloadPolicy,
     classify,
     get_default_job_name,
+    get_workload_gvk,
     new_empty_workload,
 )
 from ..runtime import metrics, tracing
@@ -403,7 +404,7 @@ class CronReconciler(Reconciler):
         policy = self.opts.workload
         # B3 (cron_controller.go:122-126)
         try:
-            gvk = GroupVersionKind.from_object(new_empty_workload(cron.spec.template.workload, policy))
+            gvk = get_workload_gvk(cron.spec.template.workload, policy)
         except WorkloadError as e:
             log.error(e, "Failed to get workload GVK")
             return Result()

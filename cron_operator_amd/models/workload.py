@@ -62,6 +62,10 @@ def _decode(workload: Any) -> Dict[str, Any]:
             raise WorkloadError(f"failed to unmarshal workload template: {e}") from None
     else:
         obj = jsonutil.deepcopy(workload)
+    return _check_decoded(obj)
+
+
+def _check_decoded(obj: Any) -> Dict[str, Any]:
     if not isinstance(obj, dict):
         raise WorkloadError("failed to unmarshal workload template: cannot unmarshal into Object: "
                            f"unexpected {type(obj).__name__}")
@@ -88,7 +92,16 @@ def new_empty_workload(workload: Any, policy: Optional[WorkloadPolicy] = None) -
 
 
 def get_workload_gvk(workload: Any, policy: Optional[WorkloadPolicy] = None) -> GroupVersionKind:
-    return GroupVersionKind.from_object(new_empty_workload(workload, policy))
+    """``getWorkloadGVK`` (``cron_util.go:58-65``): the same checks and errors as
+    :func:`new_empty_workload`, without copying a parsed (dict) template."""
+    if workload is None:
+        raise WorkloadError("workload template is missing in Cron spec")
+    obj = _check_decoded(workload) if isinstance(workload, dict) else _decode(workload)
+    gvk = GroupVersionKind.from_object(obj)
+    allow_core = policy.allow_core_group if policy is not None else False
+    if (gvk.group == "" and not allow_core) or gvk.version == "" or gvk.kind == "":
+        raise WorkloadError("workload template is missing apiVersion or kind")
+    return gvk
 
 
 def get_default_job_name(cron_name: str, schedule_time: GoTime) -> str:
