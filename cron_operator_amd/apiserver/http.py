@@ -53,19 +53,35 @@ _codec = httpcodec_native.load()  # native request framing (ops/csrc/httpcodec.c
 _CODEC_ERRORS = {400: b"bad request", 413: b"request body too large", 431: b"request header too large"}
 
 
+_VOLATILE = ("metadata",)  # rewritten by every write (resourceVersion): never worth caching
+
+
 class _EncodeCache:
     """Serialised bytes of stored objects.  A write's response and its watch events
-    carry the same (immutable) stored object, so it is encoded once."""
+    carry the same (immutable) stored object, so it is encoded once.
 
-    def __init__(self, size: int = 8192):
+    With ``shared=True`` (stored objects only: they are never mutated) the top-level
+    values of the object (but ``metadata``) are cached by identity too: a status write
+    shares the stored object's ``spec``, a tombstone everything but its metadata, so
+    only the changed parts are serialised again (``_fastjson.dumpb_shared``)."""
+
+    def __init__(self, size: int = 8192, sub_size: int = 16384):
         self._d: Dict[int, Tuple[Any, bytes]] = {}
         self._size = size
+        self._sub: Dict[int, Tuple[Any, bytes]] = {}
+        self._sub_size = sub_size
+        self._shared_enc = getattr(jsonutil, "dumpb_shared", None)
 
-    def encode(self, obj: Any) -> bytes:
+    def encode(self, obj: Any, shared: bool = False) -> bytes:
         hit = self._d.get(id(obj))
         if hit is not None and hit[0] is obj:
             return hit[1]
-        b = jsonutil.dumpb(obj)
+        if shared and self._shared_enc is not None:
+            if len(self._sub) >= self._sub_size:
+                self._sub.clear()
+            b = self._shared_enc(obj, self._sub, _VOLATILE)
+        else:
+            b = jsonutil.dumpb(obj)
         if len(self._d) >= self._size:
             self._d.clear()
         self._d[id(obj)] = (obj, b)
@@ -118,12 +134,13 @@ class WatchResponse:
 Reply = Union[Response, WatchResponse]
 
 
-def _json(data: Any, status: int = 200) -> Response:
-    return Response(status, _ENC.encode(data) if status < 300 else jsonutil.dumpb(data))
+def _json(data: Any, status: int = 200, stored: bool = False) -> Response:
+    """``stored``: ``data`` is a stored object (immutable), see :class:`_EncodeCache`."""
+    return Response(status, _ENC.encode(data, stored) if status < 300 else jsonutil.dumpb(data))
 
 
 def _event_line(etype: str, obj: Any) -> bytes:
-    return b'{"type":"' + etype.encode() + b'","object":' + _ENC.encode(obj) + b"}"
+    return b'{"type":"' + etype.encode() + b'","object":' + _ENC.encode(obj, True) + b"}"
 
 
 def _err(e: errors.ApiError) -> Response:
@@ -366,17 +383,17 @@ class APIServerApp:
             return _json(s.list(gvr, ns or None, q.get("labelSelector"), q.get("fieldSelector"),
                                 int(q.get("limit") or 0), q.get("continue"), copy=False))
         if verb == "get":
-            return _json(s.get(gvr, ns, name))
+            return _json(s.get(gvr, ns, name), stored=True)
         if verb == "create":
-            return _json(s.create(gvr, ns, body, dry_run=q.get("dryRun") == "All"), 201)
+            return _json(s.create(gvr, ns, body, dry_run=q.get("dryRun") == "All"), 201, stored=True)
         if verb == "update":
-            return _json(s.update(gvr, ns, name, body, sub or None))
+            return _json(s.update(gvr, ns, name, body, sub or None), stored=True)
         if verb == "patch":
-            return _json(s.patch(gvr, ns, name, body, ptype, sub or None))
+            return _json(s.patch(gvr, ns, name, body, ptype, sub or None), stored=True)
         if verb == "delete":
             opts = body or {}
             policy = opts.get("propagationPolicy") or q.get("propagationPolicy")
-            return _json(s.delete(gvr, ns, name, policy, opts.get("preconditions")))
+            return _json(s.delete(gvr, ns, name, policy, opts.get("preconditions")), stored=True)
         n = s.delete_collection(gvr, ns or None, q.get("labelSelector"))
         return _json({"kind": "Status", "apiVersion": "v1", "status": "Success", "details": {"deleted": n}})
 

@@ -15,6 +15,11 @@
 //   dumpb(tree) -> bytes             compact UTF-8 JSON, byte-identical to
 //                                    json.dumps(tree, separators=(",", ":"), ensure_ascii=False).encode()
 //   dumps(tree) -> str               the same as str
+//   dumpb_shared(tree, cache, volatile_keys=()) -> bytes
+//                                    dumpb for trees that are never mutated (the fake
+//                                    apiserver's stored objects): the top-level container
+//                                    values, except under volatile_keys, are cached by
+//                                    identity in `cache` and reused
 //
 // loads: every API response and watch event the operator receives is decoded,
 // and in the 1000-Cron bench that was the largest single item of operator CPU
@@ -597,6 +602,10 @@ PyObject* py_loads(PyObject*, PyObject* arg) {
 
 struct Encoder {
   std::string out;
+  // dumpb_shared: id(subtree) -> (subtree, bytes) for the top-level values of immutable trees,
+  // except those under a key in `volatile_keys` (they change on every write: never reused)
+  PyObject* shared = nullptr;
+  PyObject* volatile_keys = nullptr;
 
   bool str(PyObject* u) {
     Py_ssize_t n;
@@ -692,6 +701,46 @@ struct Encoder {
     if (PyUnicode_Check(o)) return str(o);
     if (PyLong_Check(o)) return integer(o);
     if (PyFloat_Check(o)) return flt(PyFloat_AS_DOUBLE(o));
+    return container(o, depth);
+  }
+
+  // A subtree shared by identity with one encoded before (a status write keeps the stored
+  // object's spec, a tombstone everything but its metadata) is copied from its bytes.
+  bool cached(PyObject* o, int depth) {
+    PyObject* id = PyLong_FromVoidPtr(o);
+    if (!id) return false;
+    PyObject* hit = PyDict_GetItemWithError(shared, id);  // borrowed
+    if (hit != nullptr && PyTuple_GET_ITEM(hit, 0) == o) {
+      PyObject* b = PyTuple_GET_ITEM(hit, 1);
+      out.append(PyBytes_AS_STRING(b), static_cast<size_t>(PyBytes_GET_SIZE(b)));
+      Py_DECREF(id);
+      return true;
+    }
+    if (PyErr_Occurred()) {
+      Py_DECREF(id);
+      return false;
+    }
+    const size_t start = out.size();
+    if (!container(o, depth)) {
+      Py_DECREF(id);
+      return false;
+    }
+    const size_t n = out.size() - start;
+    int rc = 0;
+    if (n >= kSharedMin) {
+      PyObject* b = PyBytes_FromStringAndSize(out.data() + start, static_cast<Py_ssize_t>(n));
+      PyObject* t = b ? PyTuple_Pack(2, o, b) : nullptr;  // holds o: its id stays unique while cached
+      rc = t ? PyDict_SetItem(shared, id, t) : -1;
+      Py_XDECREF(b);
+      Py_XDECREF(t);
+    }
+    Py_DECREF(id);
+    return rc == 0;
+  }
+
+  static constexpr size_t kSharedMin = 64;
+
+  bool container(PyObject* o, int depth) {
     if (PyDict_Check(o)) {
       out.push_back('{');
       Py_ssize_t pos = 0;
@@ -702,6 +751,12 @@ struct Encoder {
         first = false;
         if (!key(k)) return false;
         out.push_back(':');
+        if (depth == 0 && shared != nullptr && (PyDict_CheckExact(v) || PyList_CheckExact(v))) {
+          const int vol = volatile_keys != nullptr ? PySequence_Contains(volatile_keys, k) : 0;
+          if (vol < 0) return false;
+          if (!(vol ? value(v, depth + 1) : cached(v, depth + 1))) return false;
+          continue;
+        }
         if (!value(v, depth + 1)) return false;
       }
       out.push_back('}');
@@ -728,6 +783,19 @@ PyObject* py_dumpb(PyObject*, PyObject* o) {
   Encoder e;
   e.out.reserve(1024);
   if (!e.value(o, 0)) return nullptr;
+  return PyBytes_FromStringAndSize(e.out.data(), static_cast<Py_ssize_t>(e.out.size()));
+}
+
+PyObject* py_dumpb_shared(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if ((nargs != 2 && nargs != 3) || !PyDict_CheckExact(args[1])) {
+    PyErr_SetString(PyExc_TypeError, "dumpb_shared(tree, cache: dict, volatile_keys=())");
+    return nullptr;
+  }
+  Encoder e;
+  e.shared = args[1];
+  e.volatile_keys = nargs == 3 ? args[2] : nullptr;
+  e.out.reserve(1024);
+  if (!e.value(args[0], 0)) return nullptr;
   return PyBytes_FromStringAndSize(e.out.data(), static_cast<Py_ssize_t>(e.out.size()));
 }
 
@@ -772,6 +840,8 @@ PyMethodDef methods[] = {
     {"loads", py_loads, METH_O, "decode JSON (bytes, bytearray or str)"},
     {"dumpb", py_dumpb, METH_O, "compact JSON as UTF-8 bytes"},
     {"dumps", py_dumps, METH_O, "compact JSON as str"},
+    {"dumpb_shared", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(py_dumpb_shared)),
+     METH_FASTCALL, "dumpb of an immutable tree, reusing the bytes of subtrees cached by identity"},
     {"clear_key_cache", py_clear_key_cache, METH_NOARGS, "drop the interned-key cache"},
     {nullptr, nullptr, 0, nullptr}};
 

@@ -16,7 +16,7 @@ documents), which the reference uses for its deferred status write
 from __future__ import annotations
 
 import json
-from typing import Any
+from typing import Any, Dict
 
 _SCALARS = (str, int, float, bool, type(None))
 
@@ -181,6 +181,13 @@ loads = json.loads
 
 # --------------------------------------------------------------------------- native dispatch
 
+def dumpb_shared(obj: Any, cache: Dict[int, Any], volatile_keys: Any = ()) -> bytes:
+    """``dumpb`` of a tree that is never mutated, reusing the bytes of its top-level
+    containers (except under ``volatile_keys``) cached by identity in ``cache`` (native);
+    the Python twin ignores the cache."""
+    return dumpb(obj)
+
+
 deepcopy = py_deepcopy
 json_equal = py_json_equal
 create_merge_patch = py_create_merge_patch
@@ -188,7 +195,7 @@ NATIVE = False
 
 
 def _try_native() -> None:
-    global deepcopy, json_equal, create_merge_patch, loads, dumps, dumpb, NATIVE
+    global deepcopy, json_equal, create_merge_patch, loads, dumps, dumpb, dumpb_shared, NATIVE
     import os
 
     if os.environ.get("CRON_OPERATOR_FASTJSON", "auto").lower() == "python":
@@ -207,6 +214,7 @@ def _try_native() -> None:
     loads = mod.loads
     dumps = mod.dumps
     dumpb = mod.dumpb
+    dumpb_shared = mod.dumpb_shared
     NATIVE = True
 
 

@@ -83,6 +83,37 @@ def test_encoder_matches_json(v):
     assert m.dumpb(v) == _ref_dumps(v).encode()
 
 
+@settings(max_examples=300, deadline=None)
+@given(st.dictionaries(st.text(max_size=8), json_values, max_size=5),
+       st.dictionaries(st.text(max_size=8), json_values, max_size=5))
+def test_dumpb_shared_matches_dumpb(a, b):
+    """Subtrees shared by identity between successive (immutable) objects reuse their bytes;
+    the output is always dumpb's."""
+    cache = {}
+    objs = [a, b, dict(a, **{k: v for k, v in b.items() if k not in a}), {"x": a, "y": [b, a]}, dict(a)]
+    for _ in range(2):
+        for o in objs:
+            assert m.dumpb_shared(o, cache) == m.dumpb(o)
+    for k, (obj, raw) in cache.items():
+        assert id(obj) == k and raw == m.dumpb(obj) and len(raw) >= 64
+    vol = {}
+    for o in objs:
+        assert m.dumpb_shared(o, vol, ("x",)) == m.dumpb(o)
+    assert all(obj is not objs[3]["x"] for obj, _ in vol.values())
+
+
+def test_dumpb_shared_reuses_spec_bytes():
+    spec = {"template": {"workload": {"kind": "PyTorchJob", "spec": {"replicas": list(range(40))}}}}
+    cache = {}
+    old = {"apiVersion": "v1", "spec": spec, "status": {"n": 1}}
+    m.dumpb_shared(old, cache)
+    assert id(spec) in cache
+    new = dict(old, status={"n": 2})  # a status write shares spec by identity
+    assert m.dumpb_shared(new, cache) == m.dumpb(new)
+    with pytest.raises(TypeError):
+        m.dumpb_shared(new, [])
+
+
 @pytest.mark.parametrize("v", [float("inf"), float("-inf"), -0.0, 1e-7, 2 ** 80, -(2 ** 70), "\x00\x1f\u2028\"\\",
                                (1, [2, (3,)]), {1: "a", 2.5: "b", None: "c", False: "d"}, 123456789.123])
 def test_encoder_edge_cases(v):
