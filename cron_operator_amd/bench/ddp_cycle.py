@@ -1,0 +1,160 @@
+"""BASELINE.json config 5: "Cron -> PyTorchJob 8-worker DDP template targeting one
+8xMI355X ROCm node, suspend/resume cycle".
+
+The Cron is ``examples/mi355x/cron-pytorch-ddp-mi355x.yaml`` itself, read from
+the repo, with three environment-sized substitutions: the schedule becomes
+``*/1 * * * *`` (the scenario runs on a virtual clock), ``torchrun`` gets one
+worker per available device (``--nproc-per-node``; 8 on a full MI355X node, 1 on
+the single-GPU box, 2 CPU ranks over gloo in the CPU tier) and a loopback
+rendezvous, and the model is shrunk so one job takes seconds.  Everything else
+-- Forbid, historyLimit, the RCCL env, the DDP payload and its bucket size -- is
+the example's.
+
+Cycle (reference semantics: ``cron_controller.go:169-173`` suspend returns
+without requeue; on resume the missed ticks collapse into the most recent one,
+``:408-436``; Forbid delays while a job is active, ``:204-207``):
+
+1. tick -> the PyTorchJob is created, the fake training-operator (real mode) runs
+   the replica's ``torchrun`` command, DDP trains over RCCL (or gloo), the job
+   becomes ``Succeeded`` and moves to ``status.history``;
+2. ``spec.suspend=true`` -> three more ticks pass with no job;
+3. ``spec.suspend=false`` -> exactly one job, named for the latest tick, runs
+   and succeeds.
+"""
+from __future__ import annotations
+
+import asyncio
+import os
+import socket
+import sys
+import time
+from typing import Any, Dict, List
+
+import yaml
+
+from ..api.meta import GroupVersionResource
+from ..api.v1alpha1 import CRON_GVR
+
+PYTORCHJOBS = GroupVersionResource("kubeflow.org", "v1", "pytorchjobs")
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+EXAMPLE = os.path.join(ROOT, "examples", "mi355x", "cron-pytorch-ddp-mi355x.yaml")
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def ddp_cron(nproc: int, cpu: bool, steps: int = 5, hidden: int = 256) -> Dict[str, Any]:
+    """The example Cron, sized for this environment (see the module docstring)."""
+    with open(EXAMPLE) as fh:
+        cron = yaml.safe_load(fh)
+    cron["metadata"]["namespace"] = "default"
+    cron["spec"]["schedule"] = "*/1 * * * *"
+    master = cron["spec"]["template"]["workload"]["spec"]["pytorchReplicaSpecs"]["Master"]
+    ctr = master["template"]["spec"]["containers"][0]
+    assert ctr["command"][0] == "torchrun" and "--nproc-per-node" in ctr["command"], ctr["command"]
+    ctr["command"] = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node",
+                      str(nproc), "--master-addr", "127.0.0.1", "--master-port", str(_free_port())]
+    args: List[str] = list(ctr["args"])
+    for flag, val in (("--steps", steps), ("--hidden", hidden), ("--layers", 2), ("--batch", 8)):
+        args[args.index(flag) + 1] = str(val)
+    if cpu:
+        args.append("--cpu")
+    ctr["args"] = args
+    return cron
+
+
+async def run_ddp_cycle(nproc: int = 1, cpu: bool = False, timeout: float = 600.0) -> Dict[str, Any]:
+    from ..testing.env import TestEnv
+    from ..trainingop.operator import FakeTrainingOperator
+
+    env = TestEnv()
+    pp = os.environ.get("PYTHONPATH", "")
+    extra = {"PYTHONPATH": ROOT + (os.pathsep + pp if pp else "")}
+    if cpu:
+        extra["CUDA_VISIBLE_DEVICES"] = ""
+        extra["HIP_VISIBLE_DEVICES"] = ""
+    trainer = FakeTrainingOperator(env.new_client(), env.clock, mode="real", workdir=ROOT, timeout=timeout, env=extra)
+    cron = ddp_cron(nproc, cpu)
+    name = cron["metadata"]["name"]
+    t0 = time.perf_counter()
+
+    def jobs() -> List[str]:
+        return sorted(j["metadata"]["name"] for j in env.server.list(PYTORCHJOBS, "default")["items"])
+
+    def status() -> Dict[str, Any]:
+        return env.server.get(CRON_GVR, "default", name).get("status") or {}
+
+    async def finish_running() -> None:
+        await trainer.wait_all(timeout)
+        await env.settle()
+
+    try:
+        await env.client.create(CRON_GVR, cron, "default")
+        await trainer.start()
+        await env.start_manager()
+        await env.settle()
+        # 1. a tick runs the DDP job to completion
+        await env.advance(60)
+        first = jobs()
+        if len(first) != 1:
+            raise AssertionError(f"expected one PyTorchJob after the first tick, found {first}")
+        await finish_running()
+        # 2. suspended: ticks pass, nothing is created
+        obj = env.server.get(CRON_GVR, "default", name)
+        obj["spec"]["suspend"] = True
+        env.server.update(CRON_GVR, "default", name, obj)
+        await env.settle()
+        for _ in range(3):
+            await env.advance(60)
+        suspended = jobs()
+        if suspended != first:
+            raise AssertionError(f"a suspended Cron created jobs: {suspended}")
+        # 3. resumed: the missed ticks collapse into one run, named for the latest tick
+        obj = env.server.get(CRON_GVR, "default", name)
+        obj["spec"]["suspend"] = False
+        env.server.update(CRON_GVR, "default", name, obj)
+        await env.settle()
+        resumed = jobs()
+        new = [j for j in resumed if j not in first]
+        if len(new) != 1:
+            raise AssertionError(f"resume should run exactly one job, found {new}")
+        await finish_running()
+        st = status()
+        hist = [(h["object"]["name"], h["status"]) for h in st.get("history") or []]
+        results = {k.split("/", 1)[1]: v for k, v in trainer.results.items()}
+        out = {"jobs": resumed, "history": hist, "active": len(st.get("active") or []),
+               "exit_codes": {j: results.get(j, (False, [], 0))[1] for j in resumed},
+               "payload_s": {j: round(results.get(j, (False, [], 0.0))[2], 2) for j in resumed},
+               "nproc": nproc, "device": "cpu" if cpu else "gpu", "total_s": round(time.perf_counter() - t0, 2)}
+        if hist != [(first[0], "Succeeded"), (new[0], "Succeeded")] or out["active"]:
+            raise AssertionError(f"suspend/resume cycle did not end with two succeeded runs: {out}")
+        return out
+    finally:
+        await trainer.stop()
+        await env.stop()
+
+
+def main() -> int:
+    import argparse
+
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--nproc", type=int, default=0, help="DDP workers (default: visible GPUs, or 2 on CPU)")
+    ap.add_argument("--cpu", action="store_true")
+    a = ap.parse_args()
+    nproc = a.nproc
+    if nproc <= 0:
+        if a.cpu:
+            nproc = 2
+        else:
+            import torch
+
+            nproc = max(1, torch.cuda.device_count())
+    print(asyncio.run(run_ddp_cycle(nproc, a.cpu)), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

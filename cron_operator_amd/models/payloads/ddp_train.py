@@ -75,7 +75,7 @@ def main(argv=None) -> int:
     in_sync = bool(torch.allclose(flat, ref))
     if rank == 0:
         print("DDP_OK " if in_sync else "DDP_FAIL ", json.dumps({
-            "world": world, "backend": dist.get_backend(), "device": str(dev), "loss": float(loss),
+            "world": world, "backend": dist.get_backend(), "device": str(dev), "loss": float(loss.detach()),
             "steps_per_s": a.steps / dt, "samples_per_s": a.steps * a.batch * world / dt}), flush=True)
     dist.destroy_process_group()
     return 0 if in_sync else 1

@@ -93,6 +93,20 @@ def test_ddp_payload_rccl_single_rank(gpu):
     assert "DDP_OK" in out.stdout and '"backend": "nccl"' in out.stdout
 
 
+def test_ddp_cron_suspend_resume_cycle_on_gpu(gpu):
+    """BASELINE config 5 on the box: the examples/mi355x DDP Cron (torchrun, RCCL) through a
+    suspend/resume cycle (cron_operator_amd/bench/ddp_cycle.py)."""
+    import asyncio
+
+    import torch
+
+    from cron_operator_amd.bench.ddp_cycle import run_ddp_cycle
+
+    res = asyncio.run(run_ddp_cycle(max(1, torch.cuda.device_count()), cpu=False))
+    assert [s for _, s in res["history"]] == ["Succeeded", "Succeeded"]
+    assert all(codes == [0] for codes in res["exit_codes"].values())
+
+
 def test_headline_bench_short_run():
     out = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--crons", "300"],
                          capture_output=True, text=True, timeout=900, env=_env(), cwd=ROOT)

@@ -102,6 +102,18 @@ async def test_suspend_resume_collapses_missed_runs(mode):
     await env.stop()
 
 
+@pytest.mark.timeout(300)
+async def test_mi355x_ddp_example_suspend_resume_cycle_cpu():
+    """BASELINE config 5 with the real example Cron (examples/mi355x): its torchrun DDP job
+    runs for real (2 gloo ranks on CPU here, RCCL on the GPU box -- tests/test_gpu.py), then
+    a suspend/resume cycle collapses the missed ticks into one more run."""
+    from cron_operator_amd.bench.ddp_cycle import run_ddp_cycle
+
+    res = await run_ddp_cycle(2, cpu=True, timeout=240)
+    assert [s for _, s in res["history"]] == ["Succeeded", "Succeeded"] and res["active"] == 0
+    assert all(codes == [0] for codes in res["exit_codes"].values())
+
+
 async def test_pod_template_busybox_config():
     # BASELINE config 1: a Cron spawning a no-op busybox Pod (core group; optimized mode only)
     env = TestEnv()
