@@ -1,7 +1,7 @@
 # Operator image.  Reference: Dockerfile:1-28 (static Go binary on debian-12-slim,
 # USER 65534).  Here: stage 1 compiles the native C++ components (cron engine,
-# JSON-tree ops) against the image's CPython; stage 2 carries only the package,
-# its three runtime deps and the built .so files.  No GPU stack: the operator is
+# JSON-tree ops, HTTP framing) against the image's CPython; stage 2 carries only
+# the package, its two runtime deps and the built .so files.  No GPU stack: the operator is
 # control plane; the MI355X workloads it schedules use their own ROCm images.
 ARG PYTHON_IMAGE=python:3.10-slim-bookworm
 
@@ -11,7 +11,7 @@ WORKDIR /workspace
 COPY pyproject.toml README.md ./
 COPY cron_operator_amd ./cron_operator_amd
 RUN python -m cron_operator_amd.ops.build --force \
- && pip install --no-cache-dir --prefix=/install aiohttp prometheus_client PyYAML \
+ && pip install --no-cache-dir --prefix=/install aiohttp PyYAML \
  && find cron_operator_amd -name '__pycache__' -prune -exec rm -rf {} +
 
 FROM ${PYTHON_IMAGE}

@@ -83,7 +83,7 @@ def test_encoder_matches_json(v):
     assert m.dumpb(v) == _ref_dumps(v).encode()
 
 
-@settings(max_examples=300, deadline=None)
+@settings(max_examples=120, deadline=None)
 @given(st.dictionaries(st.text(max_size=8), json_values, max_size=5),
        st.dictionaries(st.text(max_size=8), json_values, max_size=5))
 def test_dumpb_shared_matches_dumpb(a, b):
