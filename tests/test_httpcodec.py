@@ -191,7 +191,8 @@ def test_response_read_until_close_falls_back():
 
 
 @settings(max_examples=150, deadline=None)
-@given(st.integers(200, 599), st.binary(max_size=80), st.booleans(), st.booleans(),
+@given(st.integers(200, 599).filter(lambda s: s not in (204, 304)),  # no body allowed: framing differs
+       st.binary(max_size=80), st.booleans(), st.booleans(),
        st.sampled_from(["", "close", "keep-alive"]), st.integers(1, 30))
 def test_response_property_matches_python(status, body, chunked, http10, conn, split):
     import pytest as _pytest
