@@ -22,6 +22,17 @@ from cron_operator_amd.utils.logging import new_from_options, set_logger  # noqa
 set_logger(new_from_options(encoder="console", level="error", stream=open(os.devnull, "w")))
 
 
+# Property tests draw the same examples on every run (a CI run must not turn red on a
+# fresh random draw); HYPOTHESIS_RANDOM=1 explores new examples when hunting for bugs.
+try:
+    from hypothesis import settings as _hyp_settings
+
+    _hyp_settings.register_profile("repo", derandomize=os.environ.get("HYPOTHESIS_RANDOM") != "1")
+    _hyp_settings.load_profile("repo")
+except ImportError:  # pragma: no cover - hypothesis is a test dependency
+    pass
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an AMD GPU (MI355X) visible to PyTorch")
     config.addinivalue_line("markers", "slow: long-running test")
