@@ -45,6 +45,10 @@ vet: ## Byte-compile every module and import the package (the `go vet` analog).
 lint: vet ## Static checks: unused imports/names, line length, whitespace (stdlib only).
 	$(PYTHON) scripts/lint.py
 
+.PHONY: sanitize
+sanitize: ## ASan + UBSan build of the C++ extensions, fuzzed and property-driven (host code only).
+	$(PYTHON) scripts/sanitize.py
+
 .PHONY: test
 test: build ## CPU test tiers: unit, envtest-analog, manager integration, e2e processes, chart/manifests.
 	$(PYTHON) -m pytest tests/ -m "not gpu" $(PYTEST_ARGS)

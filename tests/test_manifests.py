@@ -117,3 +117,18 @@ def test_mi355x_example_requests_gpus_and_rccl_payload():
     ctr = master["template"]["spec"]["containers"][0]
     assert ctr["resources"]["limits"]["amd.com/gpu"] == 8
     assert "cron_operator_amd.models.payloads.ddp_train" in ctr["args"]
+
+
+def test_native_extensions_clean_under_asan_ubsan():
+    """scripts/sanitize.py: the C++ extensions built with ASan + UBSan survive fuzzed HTTP
+    framing, random JSON trees and random cron specs (a short run; `make sanitize` runs more)."""
+    import shutil
+    import subprocess
+    import sys
+
+    if shutil.which("g++") is None:
+        pytest.skip("no g++")
+    env = dict(os.environ, SANITIZE_ITERS="4000")
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "sanitize.py")], capture_output=True,
+                         text=True, timeout=600, env=env)
+    assert out.returncode == 0 and "sanitize ok" in out.stdout, out.stdout[-2000:] + out.stderr[-4000:]
