@@ -126,6 +126,8 @@ class BenchResult:
     # CPU seconds burnt in the timed region by the operator process and the apiserver process
     cpu_s_operator: float = 0.0
     cpu_s_apiserver: float = 0.0
+    # peak RSS of each operator shard process (sharded runs; the in-process run shares the harness)
+    operator_maxrss_mib: List[float] = field(default_factory=list)
 
     def to_dict(self) -> Dict[str, Any]:
         return asdict(self)
@@ -552,7 +554,8 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
             api_requests_per_fire=requests / fires, api_requests_by_verb=by_verb,
             reconciles_per_fire=reconciles / fires, step_ms=step_ms, phase_ms=phase_ms,
             engine=default_engine().name, fastjson_native=jsonutil.NATIVE,
-            cpu_s_operator=sum(r["cpu"] - b["cpu"] for r, b in zip(last, base)), cpu_s_apiserver=api1 - api0)
+            cpu_s_operator=sum(r["cpu"] - b["cpu"] for r, b in zip(last, base)), cpu_s_apiserver=api1 - api0,
+            operator_maxrss_mib=[round(r.get("maxrss_mib", 0.0), 1) for r in last])
     finally:
         for s in shards:
             try:

@@ -10,7 +10,7 @@ over a line protocol on stdin/stdout:
 ``{"cmd": "time", "ns": <unix ns>, "phase": "completion"|"fire", "tick_ns": <ns>}``
     set this shard's (fake) clock and reply once every Cron it owns has settled
     for the phase: ``{"ok": true, "lat": [s, ...], "reconciles": n, "requests": n,
-    "by_verb": {...}, "cpu": s}`` (counters cumulative since start);
+    "by_verb": {...}, "cpu": s, "maxrss_mib": peak RSS}`` (counters cumulative since start);
 ``{"cmd": "stop"}``
     shut the manager down and exit.
 
@@ -23,6 +23,7 @@ import argparse
 import asyncio
 import json
 import os
+import resource
 import sys
 import time
 from typing import Any, Dict, List
@@ -153,7 +154,8 @@ async def main() -> int:
             # counters are cumulative: the harness differences them over its timed window
             out.write(json.dumps({"ok": True, "lat": lat, "reconciles": ctrl.reconciles,
                                   "requests": client.requests, "by_verb": dict(client.requests_by_verb),
-                                  "cpu": time.process_time()}) + "\n")
+                                  "cpu": time.process_time(),
+                                  "maxrss_mib": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024}) + "\n")
             out.flush()
     mgr.stop()
     try:

@@ -24,6 +24,8 @@ option                     default here                           reference
                            recorded, not run again                 write after its CREATE was lost
 ``overlap_gc_deletes``     history-GC DELETEs run concurrently    each DELETE awaited in turn, before
                            with the rest of the reconcile          the CREATE and the status PATCH
+``slim_child_cache``       cached children keep metadata, kind    typed informers cache whole objects
+                           and status (``spec`` is never read)     (``Owns(&PyTorchJob{})``)
 =========================  =====================================  =======================================
 
 ``overlap_gc_deletes``: a GC DELETE's outcome feeds nothing else in the
@@ -124,6 +126,17 @@ class _ChildInfo:
 Child = Tuple[Dict[str, Any], Classification, Optional[_ChildInfo]]
 
 
+def slim_child(obj: Dict[str, Any]) -> Dict[str, Any]:
+    """Informer transform for children: a reconcile reads their metadata, kind and status
+    (classification, history, GC, Replace) and never their ``spec`` -- the bulk of a
+    PyTorchJob/TFJob -- so the cache keeps everything else (``ReconcilerOptions.slim_child_cache``)."""
+    obj.pop("spec", None)
+    m = obj.get("metadata")
+    if type(m) is dict and "managedFields" in m:
+        del m["managedFields"]
+    return obj
+
+
 class JoinedError(Exception):
     """``errors.Join`` of a reconcile error and a status-patch error."""
 
@@ -147,6 +160,7 @@ class ReconcilerOptions:
     classification_cache: bool = True
     dedupe_ran_tick: bool = True
     overlap_gc_deletes: bool = True
+    slim_child_cache: bool = True
     workload: WorkloadPolicy = field(default_factory=WorkloadPolicy)
     static_owned_kinds: Tuple[GroupVersionKind, ...] = (
         GroupVersionKind("kubeflow.org", "v1", "PyTorchJob"),
@@ -159,7 +173,8 @@ class ReconcilerOptions:
                                  own_write_filter=False, dynamic_watches=False, expectations=False,
                                  fold_created_into_active=False, skip_expected_events=False,
                                  classification_cache=False, dedupe_ran_tick=False,
-                                 overlap_gc_deletes=False, workload=WorkloadPolicy.reference())
+                                 overlap_gc_deletes=False, slim_child_cache=False,
+                                 workload=WorkloadPolicy.reference())
 
 
 class Expectations:
@@ -593,7 +608,8 @@ class CronReconciler(Reconciler):
             from ..runtime.informer import label_index
 
             inf = await self.cache.get_informer(gvk, label_selector=self.child_selector,
-                                                indexers={CHILD_INDEX: label_index(LABEL_CRON_NAME)})
+                                                indexers={CHILD_INDEX: label_index(LABEL_CRON_NAME)},
+                                                transform=slim_child if self.opts.slim_child_cache else None)
             self.child_informers[gvk] = inf
             inf.start()
             if self.on_child_informer is not None:

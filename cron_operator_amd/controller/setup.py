@@ -29,7 +29,7 @@ from ..runtime.informer import EventHandler, Informer, label_index
 from ..runtime.manager import Manager
 from ..utils.logging import get_logger, log_constructor
 from . import sharding
-from .reconciler import CHILD_INDEX, CronReconciler, ReconcilerOptions
+from .reconciler import CHILD_INDEX, CronReconciler, ReconcilerOptions, slim_child
 
 CONTROLLER_NAME = "cron"
 
@@ -103,7 +103,8 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
         try:
             if opts.list_mode == "cache":
                 inf = await mgr.cache.get_informer(gvk, label_selector=rec.child_selector,
-                                                   indexers={CHILD_INDEX: label_index(LABEL_CRON_NAME)})
+                                                   indexers={CHILD_INDEX: label_index(LABEL_CRON_NAME)},
+                                                   transform=slim_child if opts.slim_child_cache else None)
                 rec.child_informers[gvk] = inf
             else:
                 inf = await mgr.cache.get_informer(gvk, label_selector=rec.child_selector if by_label else None)

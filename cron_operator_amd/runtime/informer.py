@@ -70,12 +70,32 @@ class EventHandler:
         self.on_delete = on_delete
 
 
+Transform = Callable[[Dict[str, Any]], Dict[str, Any]]
+
+
+def strip_managed_fields(obj: Dict[str, Any]) -> Dict[str, Any]:
+    """``cache.TransformStripManagedFields``: server-side-apply bookkeeping no controller reads."""
+    m = obj.get("metadata")
+    if type(m) is dict and "managedFields" in m:
+        del m["managedFields"]
+    return obj
+
+
 class Informer:
+    """A reflector + indexed store (``cache.SharedIndexInformer``).
+
+    ``transform`` (client-go ``SetTransform``) rewrites every object before it is
+    stored or handed to handlers -- e.g. dropping fields no consumer reads to keep
+    a large cache small.  Objects reaching it were decoded for this informer alone,
+    so it may modify them in place.
+    """
+
     def __init__(self, client: Client, target: Any, namespace: str = "", label_selector: Optional[str] = None,
                  field_selector: Optional[str] = None, indexers: Optional[Dict[str, IndexFunc]] = None,
                  page_size: int = 500, name: str = "", resync_period: float = 0.0,
-                 clock: Optional[Clock] = None):
+                 clock: Optional[Clock] = None, transform: Optional[Transform] = None):
         self.client = client
+        self.transform = transform
         self.resync_period = resync_period
         self.clock = clock
         self._resync_timer: Optional[TimerHandle] = None
@@ -154,6 +174,8 @@ class Informer:
 
     # ------------------------------------------------------------------ store mutation + dispatch
     def _apply(self, etype: str, obj: Dict[str, Any]) -> None:
+        if self.transform is not None:
+            obj = self.transform(obj)
         key = obj_key(obj)
         old = self.store.get(key)
         self.events += 1
@@ -207,7 +229,7 @@ class Informer:
             if old is not None and (old.get("metadata") or {}).get("resourceVersion") == \
                     (obj.get("metadata") or {}).get("resourceVersion"):
                 continue
-            self._apply("ADDED" if old is None else "MODIFIED", obj)
+            self._apply("ADDED" if old is None else "MODIFIED", obj)  # _apply transforms
         for key in [k for k in self.store if k not in seen]:
             self._apply("DELETED", self.store[key])
 
@@ -304,14 +326,17 @@ class Cache:
         return target
 
     async def get_informer(self, target: Any, label_selector: Optional[str] = None,
-                           indexers: Optional[Dict[str, IndexFunc]] = None) -> Informer:
+                           indexers: Optional[Dict[str, IndexFunc]] = None,
+                           transform: Optional[Transform] = None) -> Informer:
+        """The shared informer for ``(target, namespace, selector)``.  ``transform`` applies
+        when this call creates it (like ``cache.Options.ByObject[...].Transform``)."""
         gvr = await self._resolve(target)
         key = (gvr, self.namespace, label_selector)
         inf = self._informers.get(key)
         if inf is None:
             inf = Informer(self.client, gvr, self.namespace, label_selector, indexers=indexers,
                            name=f"{gvr.resource}.{gvr.group}" if gvr.group else gvr.resource,
-                           resync_period=self.resync_period, clock=self.clock)
+                           resync_period=self.resync_period, clock=self.clock, transform=transform)
             self._informers[key] = inf
             if self._started:
                 inf.start()

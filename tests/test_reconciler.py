@@ -533,3 +533,29 @@ async def test_noop_reconcile_sends_no_patch_optimized_but_does_in_reference():
         await rig.reconcile()
         patched = rig.server.stats.by_verb.get("patch", 0) > before
         assert patched == expect_patch
+
+
+async def test_child_cache_is_slimmed_in_optimized_mode_only():
+    """``slim_child_cache``: cached children drop ``spec`` and ``managedFields`` (never read by a
+    reconcile); the reference's typed informers cache whole objects."""
+    from cron_operator_amd.testing.env import TestEnv as _Env
+
+    for opts, slim in ((ReconcilerOptions(), True), (ReconcilerOptions.reference(), False)):
+        env = _Env()
+        await env.create_cron(new_cron(NAME, NS, "*/1 * * * *", PT_TMPL))
+        env.server.create(PT, NS, {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+                                   "metadata": {"name": "j", "labels": {LABEL_CRON_NAME: NAME},
+                                                "managedFields": [{"manager": "kubectl"}]},
+                                   "spec": {"pytorchReplicaSpecs": {"Master": {"replicas": 1}}}})
+        await env.start_manager(opts)
+        await env.settle()
+        from cron_operator_amd.api.meta import GroupVersionKind
+
+        inf = env.reconciler.child_informers.get(GroupVersionKind("kubeflow.org", "v1", "PyTorchJob"))
+        if inf is None:  # reference mode: the static Owns() informer
+            inf = next(i for i in env.manager.cache.informers() if i.name.startswith("pytorchjobs"))
+        cached = inf.get(NS, "j", copy=False)
+        assert ("spec" not in cached) is slim and ("managedFields" not in cached["metadata"]) is slim
+        st = env.server.get(CRON_GVR, NS, NAME).get("status") or {}
+        assert [a["name"] for a in st.get("active") or []] == ["j"]
+        await env.stop()
