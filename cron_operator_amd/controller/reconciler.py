@@ -25,7 +25,8 @@ option                     default here                           reference
 ``overlap_gc_deletes``     history-GC DELETEs run concurrently    each DELETE awaited in turn, before
                            with the rest of the reconcile          the CREATE and the status PATCH
 ``slim_child_cache``       cached children keep metadata, kind    typed informers cache whole objects
-                           and status (``spec`` is never read)     (``Owns(&PyTorchJob{})``)
+                           and status (``spec`` is never read);    (``Owns(&PyTorchJob{})``)
+                           cached Crons drop ``managedFields``
 =========================  =====================================  =======================================
 
 ``overlap_gc_deletes``: a GC DELETE's outcome feeds nothing else in the

@@ -25,7 +25,7 @@ from ..api.meta import GroupVersionKind
 from ..api.v1alpha1 import CRON_GVK, LABEL_CRON_NAME
 from ..cron.engine import CronEngine
 from ..runtime.controller import Controller
-from ..runtime.informer import EventHandler, Informer, label_index
+from ..runtime.informer import EventHandler, Informer, label_index, strip_managed_fields
 from ..runtime.manager import Manager
 from ..utils.logging import get_logger, log_constructor
 from . import sharding
@@ -43,7 +43,8 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
         raise ValueError(f"unknown shard routing {mgr.opts.shard_routing!r}")
     by_label = count > 1 and mgr.opts.shard_routing == "labels"
     cron_inf = await mgr.cache.get_informer(CRON_GVK,
-                                            label_selector=sharding.shard_selector(index, count) if by_label else None)
+                                            label_selector=sharding.shard_selector(index, count) if by_label else None,
+                                            transform=strip_managed_fields if opts.slim_child_cache else None)
     rec = CronReconciler(mgr.client, mgr.cache, mgr.get_event_recorder_for(CONTROLLER_NAME), mgr.clock, engine,
                          opts, cron_inf)
     ctrl = Controller(CONTROLLER_NAME, rec, mgr.clock, mgr.opts.max_concurrent_reconciles, log)
