@@ -92,6 +92,10 @@ bench: build ## Headline benchmark (1000 Crons, `* * * * *`, historyLimit=10) ->
 bench-reference: build ## Same benchmark with the reference algorithm (BASELINE.md denominator).
 	$(PYTHON) bench.py --mode reference --steps 3 --warmup 1
 
+.PHONY: bench-baseline-configs
+bench-baseline-configs: build ## All five BASELINE.json configs in both modes, with their invariants checked.
+	$(PYTHON) scripts/baseline_configs.py --out baseline_configs.json
+
 .PHONY: bench-scale
 bench-scale: build ## Scaling curve over 1/10/100/1000 Crons (BASELINE.json configs).
 	$(PYTHON) scripts/bench_scale.py
