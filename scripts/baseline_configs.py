@@ -192,7 +192,8 @@ def config4(mode: str) -> Dict[str, Any]:
     return {"mode": mode, "fires": fires, "cron_reconciles_per_s": round(res.cron_reconciles_per_s, 1),
             "api_requests_per_fire": round(res.api_requests_per_fire, 2),
             "reconciles_per_fire": round(res.reconciles_per_fire, 2),
-            "p50_tick_to_create_ms": round(res.p50_latency_ms, 2), "p99_tick_to_create_ms": round(res.p99_latency_ms, 2),
+            "p50_tick_to_create_ms": round(res.p50_latency_ms, 2),
+            "p99_tick_to_create_ms": round(res.p99_latency_ms, 2),
             "operator_shards": cfg.shards, "checks": {"every_cron_fired_every_tick": True}, "ok": True}
 
 
