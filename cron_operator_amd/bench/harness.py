@@ -37,11 +37,13 @@ live LIST per reconcile, ``finished=now``, no event filtering).
 from __future__ import annotations
 
 import asyncio
+import collections
 import json
 import os
 import statistics
 import subprocess
 import sys
+import threading
 import time
 from dataclasses import asdict, dataclass, field
 from typing import Any, Dict, List, Optional
@@ -161,7 +163,15 @@ class _RemoteServer:
             rest = self.proc.stdout.read() if self.proc.poll() is not None else ""
             raise RuntimeError(f"fake apiserver failed to start: {line}{rest}")
         self.url = line.split()[1].strip()
+        # keep draining the pipe: a child blocked on a full stdout pipe would stall the bench
+        self.tail: "collections.deque[str]" = collections.deque(maxlen=50)
+        threading.Thread(target=self._drain, daemon=True, name="apiserver-stdout").start()
         return self.url
+
+    def _drain(self) -> None:
+        assert self.proc is not None and self.proc.stdout is not None
+        for ln in self.proc.stdout:
+            self.tail.append(ln)
 
     def stop(self) -> None:
         if self.proc is not None and self.proc.poll() is None:
