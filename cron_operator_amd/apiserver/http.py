@@ -518,7 +518,7 @@ class _ServerConn(asyncio.Protocol):
         self.busy = False               # a reply (watch / delayed) is pending; later requests wait
         self.closed = False
         self._continued = False         # "100 Continue" already sent for the pending request
-        self._watch_task: Optional[asyncio.Task] = None
+        self._watch: Optional["_WatchStream"] = None
 
     def connection_made(self, transport: asyncio.BaseTransport) -> None:
         self.transport = transport  # type: ignore[assignment]
@@ -527,8 +527,8 @@ class _ServerConn(asyncio.Protocol):
     def connection_lost(self, exc: Optional[BaseException]) -> None:
         self.closed = True
         self.app._conns.discard(self)
-        if self._watch_task is not None:
-            self._watch_task.cancel()
+        if self._watch is not None:
+            self._watch.end()
 
     def close(self) -> None:
         if self.transport is not None and not self.closed:
@@ -643,7 +643,7 @@ class _ServerConn(asyncio.Protocol):
                 continue
             self.busy = True
             if isinstance(reply, WatchResponse):
-                self._watch_task = asyncio.ensure_future(self._stream(reply, keep))
+                self._start_watch(reply, keep)
             else:
                 reply.add_done_callback(lambda f, keep=keep: self._delayed_done(f, keep))
 
@@ -657,7 +657,7 @@ class _ServerConn(asyncio.Protocol):
             reply = _err(errors.ApiError(500, "InternalError", str(e)))
         if isinstance(reply, WatchResponse):
             self.busy = True
-            self._watch_task = asyncio.ensure_future(self._stream(reply, keep))
+            self._start_watch(reply, keep)
             return
         self._reply(reply, keep)
         self._drain()
@@ -678,49 +678,103 @@ class _ServerConn(asyncio.Protocol):
             self.transport.close()
             self.closed = True
 
-    async def _stream(self, wr: WatchResponse, keep: bool) -> None:
-        w = wr.watcher
-        app = self.app
-        app._streams.append(w)
-        t = self.transport
-        assert t is not None
-        t.write(b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nTransfer-Encoding: chunked\r\n\r\n")
-        deadline = time.monotonic() + wr.timeout
-        try:
-            while not self.closed:
-                remaining = deadline - time.monotonic()
-                if remaining <= 0:
-                    break
-                try:
-                    ev = await asyncio.wait_for(w.queue.get(), remaining)
-                except asyncio.TimeoutError:
-                    break
-                if ev is None:
-                    break
-                buf = [_event_line(ev[0], ev[1])]
-                # coalesce whatever is already queued into one chunk
-                while not w.queue.empty() and len(buf) < 512:
-                    nxt = w.queue.get_nowait()
-                    if nxt is None:
-                        w.closed = True
-                        break
-                    buf.append(_event_line(nxt[0], nxt[1]))
-                chunk = b"\n".join(buf) + b"\n"
-                t.write(b"%x\r\n" % len(chunk) + chunk + b"\r\n")
-                if w.closed:
-                    break
-        except asyncio.CancelledError:
-            pass
-        finally:
-            w.stop()
-            if w in app._streams:
-                app._streams.remove(w)
-        if not self.closed:
-            t.write(b"0\r\n\r\n")
-            if not keep:
-                t.close()
-                self.closed = True
-                return
-            self.busy = False
-            self._watch_task = None
-            self._drain()
+    def _start_watch(self, wr: WatchResponse, keep: bool) -> None:
+        ws = _WatchStream(self, wr, keep)
+        if not ws.ended:  # a watcher stopped before it started has already finished the reply
+            self._watch = ws
+
+    def _after_watch(self) -> None:
+        """The watch response ended on a kept-alive connection: serve what queued up."""
+        if self.closed:
+            return
+        self.busy = False
+        self._drain()
+
+
+_WATCH_HEAD = b"HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nTransfer-Encoding: chunked\r\n\r\n"
+
+
+class _WatchStream:
+    """One watch response, fed synchronously by its :class:`Watcher` (``Watcher.sink``).
+
+    Each event is encoded when it happens; everything that arrives within one turn of
+    the event loop goes out as one chunk (``call_soon`` flush).  Compared with a
+    consumer coroutine per stream this saves a queue hand-off, a task wake-up and a
+    ``wait_for`` timer per batch.  ``timeoutSeconds`` is one ``call_later``.
+    """
+
+    __slots__ = ("conn", "watcher", "keep", "lines", "loop", "flush_h", "timer", "ended")
+
+    def __init__(self, conn: "_ServerConn", wr: WatchResponse, keep: bool):
+        self.conn = conn
+        self.watcher = w = wr.watcher
+        self.keep = keep
+        self.lines: List[bytes] = []
+        self.loop = asyncio.get_running_loop()
+        self.flush_h: Optional[asyncio.Handle] = None
+        self.ended = False
+        conn.app._streams.append(w)
+        assert conn.transport is not None
+        conn.transport.write(_WATCH_HEAD)
+        # events queued before the sink attached: the initial state or the resumed backlog
+        stopped = False
+        while not w.queue.empty():
+            ev = w.queue.get_nowait()
+            if ev is None:
+                stopped = True
+                break
+            self.lines.append(_event_line(ev[0], ev[1]))
+        w.sink = self.on_event
+        self.timer = self.loop.call_later(wr.timeout, self.end)
+        if stopped or w.closed:
+            self.end()
+        elif self.lines:
+            self.flush_h = self.loop.call_soon(self.flush)
+
+    def on_event(self, ev: Optional[Tuple[str, Dict[str, Any]]]) -> None:
+        if self.ended:
+            return
+        if ev is None:
+            self.end()
+            return
+        self.lines.append(_event_line(ev[0], ev[1]))
+        if self.flush_h is None:
+            self.flush_h = self.loop.call_soon(self.flush)
+
+    def flush(self) -> None:
+        self.flush_h = None
+        if not self.lines:
+            return
+        conn = self.conn
+        if conn.closed or conn.transport is None:
+            self.lines.clear()
+            return
+        chunk = b"\n".join(self.lines) + b"\n"
+        self.lines.clear()
+        conn.transport.write(b"%x\r\n" % len(chunk) + chunk + b"\r\n")
+
+    def end(self) -> None:
+        if self.ended:
+            return
+        self.ended = True
+        self.timer.cancel()
+        if self.flush_h is not None:
+            self.flush_h.cancel()
+        self.flush()  # what is pending goes out before the terminating chunk
+        w = self.watcher
+        w.sink = None
+        w.stop()
+        streams = self.conn.app._streams
+        if w in streams:
+            streams.remove(w)
+        conn = self.conn
+        conn._watch = None
+        if conn.closed or conn.transport is None:
+            return
+        conn.transport.write(b"0\r\n\r\n")
+        if not self.keep:
+            conn.transport.close()
+            conn.closed = True
+            return
+        # not from inside whatever stopped the watcher (a handler, a timer): next turn
+        self.loop.call_soon(conn._after_watch)

@@ -138,6 +138,9 @@ class Watcher:
         self.labels_only = getattr(pred, "field_selector", None) == ""
         self.bookmarks = bookmarks
         self.queue: "asyncio.Queue[Optional[Tuple[str, Dict[str, Any]]]]" = asyncio.Queue()
+        # set by a consumer that takes events synchronously (the HTTP front end): events go
+        # straight to it instead of through the queue; ``None`` ends the stream
+        self.sink: Optional[Callable[[Optional[Tuple[str, Dict[str, Any]]]], None]] = None
         self.closed = False
         self.sent = 0
 
@@ -171,18 +174,29 @@ class Watcher:
 
     def _put(self, etype: str, obj: Dict[str, Any]) -> None:
         self.sent += 1
-        self.queue.put_nowait((etype, jsonutil.deepcopy(obj) if self.copy_events else obj))
+        ev = (etype, jsonutil.deepcopy(obj) if self.copy_events else obj)
+        if self.sink is not None:
+            self.sink(ev)
+        else:
+            self.queue.put_nowait(ev)
 
     def bookmark(self, rv: int) -> None:
         if self.bookmarks and not self.closed:
-            self.queue.put_nowait(("BOOKMARK", {"kind": self.info.kind, "apiVersion": self.info.api_version,
-                                                "metadata": {"resourceVersion": str(rv)}}))
+            ev = ("BOOKMARK", {"kind": self.info.kind, "apiVersion": self.info.api_version,
+                               "metadata": {"resourceVersion": str(rv)}})
+            if self.sink is not None:
+                self.sink(ev)
+            else:
+                self.queue.put_nowait(ev)
 
     def stop(self) -> None:
         if not self.closed:
             self.closed = True
             self.server._remove_watcher(self)
-            self.queue.put_nowait(None)
+            if self.sink is not None:
+                self.sink(None)
+            else:
+                self.queue.put_nowait(None)
 
     def __aiter__(self):
         return self

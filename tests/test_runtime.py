@@ -3,6 +3,7 @@ leader election, event recorder, probe + metrics servers, kubeconfig."""
 from __future__ import annotations
 
 import asyncio
+import json
 import os
 import tempfile
 
@@ -506,3 +507,45 @@ async def test_resync_disabled_with_zero_period():
     await env.advance(100 * 3600)
     assert env.controller.reconciles == before
     await env.stop()
+
+
+async def test_http_watch_stream_timeout_keepalive_and_disconnect():
+    """The HTTP front end's watch responses: events written as chunks, timeoutSeconds ends the
+    response with the terminating chunk and the kept-alive connection serves the next request;
+    a client that disconnects mid-watch leaves no watcher behind."""
+    env = TestEnv()
+    app = APIServerApp(env.server)
+    port = await app.start("127.0.0.1", 0)
+    try:
+        reader, writer = await asyncio.open_connection("127.0.0.1", port)
+        writer.write(b"GET /api/v1/namespaces/default/configmaps?watch=true&timeoutSeconds=1 HTTP/1.1\r\n"
+                     b"Host: x\r\n\r\n")
+        await writer.drain()
+        head = await asyncio.wait_for(reader.readuntil(b"\r\n\r\n"), 5)
+        assert head.startswith(b"HTTP/1.1 200") and b"chunked" in head
+        env.server.create(CM, "default", {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "a"}})
+        env.server.create(CM, "default", {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "b"}})
+        size = int((await asyncio.wait_for(reader.readuntil(b"\r\n"), 5)).strip(), 16)
+        chunk = await reader.readexactly(size + 2)
+        lines = [json.loads(ln) for ln in chunk[:-2].splitlines()]
+        assert [(e["type"], e["object"]["metadata"]["name"]) for e in lines] == [("ADDED", "a"), ("ADDED", "b")]
+        assert await asyncio.wait_for(reader.readuntil(b"0\r\n\r\n"), 5)  # timeoutSeconds ended the response
+        writer.write(b"GET /api/v1/namespaces/default/configmaps/a HTTP/1.1\r\nHost: x\r\n\r\n")
+        await writer.drain()
+        assert (await asyncio.wait_for(reader.readuntil(b"\r\n\r\n"), 5)).startswith(b"HTTP/1.1 200")
+        writer.close()
+        # a watch whose client goes away
+        reader, writer = await asyncio.open_connection("127.0.0.1", port)
+        writer.write(b"GET /api/v1/namespaces/default/configmaps?watch=true HTTP/1.1\r\nHost: x\r\n\r\n")
+        await writer.drain()
+        await asyncio.wait_for(reader.readuntil(b"\r\n\r\n"), 5)
+        key = ("", "configmaps")
+        assert len(env.server._watchers[key]) == 1
+        writer.close()
+        for _ in range(100):
+            await asyncio.sleep(0.01)
+            if not env.server._watchers[key]:
+                break
+        assert not env.server._watchers[key] and not app._streams
+    finally:
+        await app.stop()
