@@ -48,7 +48,7 @@ class ConnectionFailed(Exception):
 
 class _Conn(asyncio.Protocol):
     __slots__ = ("transport", "buf", "fut", "alive", "used", "_state", "_status", "_clen", "_chunked",
-                 "_close_after", "_body", "_got_any", "retry_after")
+                 "_close_after", "_body", "_got_any", "retry_after", "ssl_gen")
 
     def __init__(self) -> None:
         self.transport: Optional[asyncio.Transport] = None
@@ -56,6 +56,7 @@ class _Conn(asyncio.Protocol):
         self.fut: Optional[asyncio.Future] = None
         self.alive = True
         self.used = 0
+        self.ssl_gen = 0         # HttpPool TLS-context generation this connection was made with
         self._reset()
 
     def _reset(self) -> None:
@@ -382,6 +383,7 @@ class HttpPool:
         self.timeout = timeout
         self.connects = 0
         self._closed = False
+        self._ssl_gen = 0
 
     def set_headers(self, headers: Optional[Dict[str, str]]) -> None:
         """Replace the headers sent with every request (e.g. a rotated ``Authorization``)."""
@@ -390,13 +392,25 @@ class HttpPool:
         extra = "".join(f"{k}: {v}\r\n" for k, v in hdrs.items())
         self._fixed = f"Host: {self._hosthdr}\r\n{extra}"
 
+    def set_ssl(self, ctx: _ssl.SSLContext) -> None:
+        """New connections handshake with ``ctx`` (a rotated client certificate); idle
+        connections made with the old one are closed, busy ones when they are given back."""
+        self.ssl = ctx
+        self._ssl_gen += 1
+        while self._idle:
+            c = self._idle.pop()
+            if c.transport is not None:
+                c.transport.close()
+
     async def _connect(self) -> _Conn:
         loop = asyncio.get_running_loop()
         kw = {}
         if self.ssl is not None:
             kw["ssl"] = self.ssl
             kw["server_hostname"] = self.server_hostname or self.host
+        gen = self._ssl_gen
         _, proto = await asyncio.wait_for(loop.create_connection(_Conn, self.host, self.port, **kw), self.timeout)
+        proto.ssl_gen = gen
         self.connects += 1
         return proto  # type: ignore[return-value]
 
@@ -408,7 +422,8 @@ class HttpPool:
         return None
 
     def _give_back(self, c: _Conn) -> None:
-        if c.alive and not self._closed and len(self._idle) < self.max_idle and c.fut is None:
+        if c.alive and not self._closed and len(self._idle) < self.max_idle and c.fut is None \
+                and c.ssl_gen == self._ssl_gen:
             self._idle.append(c)
         elif c.transport is not None:
             c.transport.close()

@@ -118,32 +118,41 @@ class HttpTransport(Transport):
         self.fast = fast
         self._pool: Optional[HttpPool] = None
         self._token = ""  # the bearer token the pool/session headers carry
+        self._cert_generation = 0  # the exec-plugin client certificate the pool's TLS context holds
 
     def _fast_pool(self) -> HttpPool:
         if self._pool is None:
             self._token = self.config.token()
             self._pool = HttpPool(self.config.host, ssl_context=self.config.ssl_context() or None,
-                                  headers=self.config.auth_headers(), max_idle=self._pool_size,
+                                  headers=self.config.auth_headers(self._token), max_idle=self._pool_size,
                                   timeout=self._timeout, server_hostname=self.config.tls_server_name or None)
-        elif self.config.bearer_token_file:
+            self._cert_generation = self.config.cert_generation
+        elif self.config.rotating:
             self._rotate_token()
         return self._pool
 
     def _rotate_token(self) -> None:
-        """Re-stamp ``Authorization`` when the token file's content changed (kubeconfig.py)."""
+        """Re-stamp ``Authorization`` when the token file's content or the exec plugin's token
+        changed, and switch new connections to a rotated exec client certificate (client-go
+        closes the old connections then; here idle ones are dropped, busy ones finish)."""
         tok = self.config.token()
+        if self.config.cert_generation != self._cert_generation and self._pool is not None:
+            self._cert_generation = self.config.cert_generation
+            ctx = self.config.ssl_context()
+            if ctx is not None:
+                self._pool.set_ssl(ctx)
         if tok == self._token:
             return
         self._token = tok
-        hdrs = self.config.auth_headers()
+        hdrs = self.config.auth_headers(tok)
         if self._pool is not None:
             self._pool.set_headers(hdrs)
         if self._session is not None and not self._session.closed:
             self._session.headers.update(hdrs)
 
     def _unauthorized(self) -> None:
-        """A 401: drop the cached file token so the next request re-reads it."""
-        if self.config.bearer_token_file:
+        """A 401: drop the cached file token / exec credential so the next request refreshes it."""
+        if self.config.rotating:
             self.config.reset_token()
 
     def _tls_kw(self) -> Dict[str, Any]:
@@ -152,13 +161,13 @@ class HttpTransport(Transport):
         return {"server_hostname": name} if name and self.config.host.startswith("https://") else {}
 
     def _sess(self) -> aiohttp.ClientSession:
-        if self.config.bearer_token_file and self._session is not None:
+        if self.config.rotating and self._session is not None:
             self._rotate_token()
         if self._session is None or self._session.closed:
             self._token = self.config.token()
             conn = aiohttp.TCPConnector(limit=self._pool_size, ssl=self.config.ssl_context() or False,
                                         keepalive_timeout=120)
-            self._session = aiohttp.ClientSession(connector=conn, headers=self.config.auth_headers(),
+            self._session = aiohttp.ClientSession(connector=conn, headers=self.config.auth_headers(self._token),
                                                   read_bufsize=1 << 20, json_serialize=jsonutil.dumps)
         return self._session
 

@@ -4,7 +4,7 @@ Order [ext controller-runtime ``config.GetConfig``]: ``--kubeconfig`` flag,
 ``$KUBECONFIG``, in-cluster service account
 (``KUBERNETES_SERVICE_HOST``/``_PORT`` + ``/var/run/secrets/kubernetes.io/serviceaccount``),
 then ``~/.kube/config``.  Supported kubeconfig auth: bearer token / tokenFile,
-client certificate + key (file or ``*-data``), basic auth, CA bundle or
+client certificate + key (file or ``*-data``), exec credential plugins, basic auth, CA bundle or
 ``insecure-skip-tls-verify``, ``tls-server-name`` and ``proxy-url``-less
 direct connections.  ``--qps``/``--burst`` are applied by the caller.
 
@@ -15,26 +15,154 @@ a minute (10 s leeway) and drops its cached token when a request comes back
 401; :meth:`RestConfig.token` and :meth:`RestConfig.reset_token` do the same,
 and the HTTP transport re-stamps its ``Authorization`` header when the token
 changes (``runtime/http.py``).
+
+``users[].user.exec`` credential plugins (``kubelogin``, ``aws eks get-token``,
+``gke-gcloud-auth-plugin``, ...) follow [ext client-go
+``plugin/pkg/client/auth/exec``]: the command runs with the kubeconfig's
+``args``/``env`` plus ``KUBERNETES_EXEC_INFO`` (an ``ExecCredential`` request,
+with the cluster when ``provideClusterInfo``), and its stdout must be an
+``ExecCredential`` of the same ``apiVersion`` carrying a ``token`` and/or a
+``clientCertificateData``/``clientKeyData`` pair.  The credential is cached
+until its ``expirationTimestamp`` (forever without one) and fetched again after
+a 401.  Plugins run non-interactively: ``interactiveMode: Always`` is refused.
 """
 from __future__ import annotations
 
 import base64
+import json
 import os
 import ssl
+import subprocess
 import tempfile
 import time
 from dataclasses import dataclass, field
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, List, Optional, Tuple
 
 import yaml
 
 SA_DIR = "/var/run/secrets/kubernetes.io/serviceaccount"
 TOKEN_FILE_PERIOD = 60.0   # client-go fileTokenSource: a token read from a file is good for a minute
 TOKEN_LEEWAY = 10.0        # client-go cachingTokenSource: refresh that long before expiry
+EXEC_API_VERSIONS = ("client.authentication.k8s.io/v1", "client.authentication.k8s.io/v1beta1")
+EXEC_TIMEOUT = 60.0        # seconds a credential plugin may run
 
 
 class ConfigError(RuntimeError):
     pass
+
+
+@dataclass
+class ExecCredentials:
+    token: str = ""
+    cert_data: bytes = b""
+    key_data: bytes = b""
+    expires_at: Optional[float] = None   # wall-clock seconds; None = until a 401
+
+
+@dataclass
+class ExecProvider:
+    """A kubeconfig ``user.exec`` stanza (``ExecConfig``)."""
+    command: str
+    api_version: str
+    args: List[str] = field(default_factory=list)
+    env: List[Dict[str, str]] = field(default_factory=list)
+    interactive_mode: str = "IfAvailable"
+    provide_cluster_info: bool = False
+    install_hint: str = ""
+    cluster: Dict[str, Any] = field(default_factory=dict)   # the kubeconfig cluster, for provideClusterInfo
+
+    @staticmethod
+    def from_kubeconfig(ex: Dict[str, Any], cluster: Dict[str, Any]) -> "ExecProvider":
+        cmd = ex.get("command") or ""
+        if not cmd:
+            raise ConfigError("exec plugin: command must be specified")
+        api_version = ex.get("apiVersion") or ""
+        if api_version not in EXEC_API_VERSIONS:
+            raise ConfigError(f"exec plugin: invalid apiVersion {api_version!r}")
+        mode = ex.get("interactiveMode") or ""
+        if not mode:
+            if api_version.endswith("/v1"):
+                raise ConfigError("exec plugin: interactiveMode must be specified for "
+                                  f"{api_version} to use exec authentication plugin")
+            mode = "IfAvailable"
+        if mode not in ("Never", "IfAvailable", "Always"):
+            raise ConfigError(f"exec plugin: invalid interactiveMode {mode!r}")
+        if mode == "Always":
+            raise ConfigError("exec plugin cannot support interactive mode: the operator has no terminal")
+        env = ex.get("env") or []
+        for e in env:
+            if not isinstance(e, dict) or "name" not in e:
+                raise ConfigError("exec plugin: env entries need a name")
+        return ExecProvider(command=cmd, api_version=api_version, args=[str(a) for a in ex.get("args") or []],
+                            env=env, interactive_mode=mode,
+                            provide_cluster_info=bool(ex.get("provideClusterInfo", False)),
+                            install_hint=ex.get("installHint") or "", cluster=dict(cluster))
+
+    def _exec_info(self) -> str:
+        spec: Dict[str, Any] = {"interactive": False}
+        if self.provide_cluster_info:
+            c = self.cluster
+            info: Dict[str, Any] = {"server": c.get("server", "")}
+            for k in ("tls-server-name", "insecure-skip-tls-verify", "certificate-authority-data", "proxy-url",
+                      "disable-compression"):
+                if c.get(k):
+                    info[k] = c[k]
+            ext = next((e.get("extension") for e in c.get("extensions") or []
+                        if e.get("name") == "client.authentication.k8s.io/exec"), None)
+            if ext is not None:
+                info["config"] = ext
+            spec["cluster"] = info
+        return json.dumps({"apiVersion": self.api_version, "kind": "ExecCredential", "spec": spec})
+
+    def run(self) -> ExecCredentials:
+        env = dict(os.environ)
+        for e in self.env:
+            env[e["name"]] = str(e.get("value", ""))
+        env["KUBERNETES_EXEC_INFO"] = self._exec_info()
+        try:
+            p = subprocess.run([self.command, *self.args], env=env, stdin=subprocess.DEVNULL,
+                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=EXEC_TIMEOUT, check=False)
+        except FileNotFoundError:
+            hint = f"\n\n{self.install_hint}" if self.install_hint else ""
+            raise ConfigError(f"exec: executable {self.command} not found{hint}") from None
+        except (OSError, subprocess.TimeoutExpired) as e:
+            raise ConfigError(f"exec: executable {self.command} failed: {e}") from None
+        if p.returncode != 0:
+            err = p.stderr.decode(errors="replace").strip()
+            raise ConfigError(f"exec: executable {self.command} failed with exit code {p.returncode}"
+                              + (f": {err}" if err else ""))
+        return self.parse(p.stdout)
+
+    def parse(self, out: bytes) -> ExecCredentials:
+        try:
+            doc = json.loads(out)
+        except ValueError as e:
+            raise ConfigError(f"exec: decoding stdout: {e}") from None
+        if not isinstance(doc, dict) or doc.get("kind") != "ExecCredential":
+            raise ConfigError("exec: stdout is not an ExecCredential")
+        if doc.get("apiVersion") != self.api_version:
+            raise ConfigError(f"exec plugin is configured to use API version {self.api_version}, "
+                              f"plugin returned version {doc.get('apiVersion')}")
+        st = doc.get("status")
+        if not isinstance(st, dict):
+            raise ConfigError("exec plugin didn't return a status field")
+        token = st.get("token") or ""
+        cert, key = st.get("clientCertificateData") or "", st.get("clientKeyData") or ""
+        if not token and not (cert and key):
+            raise ConfigError("exec plugin didn't return a token or cert/key pair")
+        if bool(cert) != bool(key):
+            raise ConfigError("exec plugin returned only certificate or key, not both")
+        exp = None
+        if st.get("expirationTimestamp"):
+            from ..api.meta import time_from_json
+            try:
+                t = time_from_json(str(st["expirationTimestamp"]))
+            except ValueError:
+                t = None
+            if t is None:
+                raise ConfigError(f"exec: bad expirationTimestamp {st['expirationTimestamp']!r}")
+            exp = t.unix_nano() / 1e9
+        return ExecCredentials(token=token, cert_data=cert.encode(), key_data=key.encode(), expires_at=exp)
 
 
 @dataclass
@@ -55,14 +183,43 @@ class RestConfig:
     qps: float = 30.0
     burst: int = 50
     user_agent: str = "cron-operator-amd"
-    _tmp: List[str] = field(default_factory=list)
+    exec_provider: Optional[ExecProvider] = None
     _file_token: str = ""
     _file_token_refresh_at: float = 0.0   # monotonic; 0 = read on next use
+    _exec_creds: Optional[ExecCredentials] = None
+    cert_generation: int = 0              # bumped when an exec plugin hands out a new client certificate
+
+    @property
+    def rotating(self) -> bool:
+        """Credentials can change while the process runs (token file or exec plugin)."""
+        return bool(self.bearer_token_file) or self.exec_provider is not None
+
+    def _exec(self) -> ExecCredentials:
+        """The plugin's cached credential, re-run once expired (client-go ``credsExpired``)."""
+        c = self._exec_creds
+        if c is None or (c.expires_at is not None and time.time() >= c.expires_at):
+            new = self.exec_provider.run()  # type: ignore[union-attr]
+            if c is None or (new.cert_data, new.key_data) != (c.cert_data, c.key_data):
+                self.cert_generation += 1
+            self._exec_creds = c = new
+        return c
+
+    def client_cert(self) -> Tuple[bytes, bytes]:
+        """PEM client certificate and key from an exec plugin, or empty."""
+        if self.exec_provider is None:
+            return b"", b""
+        c = self._exec()
+        return c.cert_data, c.key_data
 
     def token(self) -> str:
         """The bearer token; a ``tokenFile`` is re-read at most once per ``TOKEN_FILE_PERIOD -
         TOKEN_LEEWAY`` seconds.  A read error keeps the last good token (client-go logs and
-        serves the cached one), falling back to the inline ``token``."""
+        serves the cached one), falling back to the inline ``token``.  An exec plugin's token
+        takes precedence over both (client-go wraps the transport with the exec authenticator)."""
+        if self.exec_provider is not None:
+            tok = self._exec().token
+            if tok:
+                return tok
         if self.bearer_token_file:
             now = time.monotonic()
             if now >= self._file_token_refresh_at:
@@ -77,14 +234,19 @@ class RestConfig:
         return self.bearer_token
 
     def reset_token(self) -> None:
-        """Forget the cached file token (client-go ``ResetTokenOlderThan`` after a 401)."""
+        """Forget the cached file token (client-go ``ResetTokenOlderThan`` after a 401) and an
+        exec plugin's credential (the exec authenticator refreshes on 401)."""
         self._file_token_refresh_at = 0.0
+        if self._exec_creds is not None:
+            self._exec_creds.expires_at = 0.0
 
-    def _materialise(self, data: bytes, suffix: str) -> str:
+    @staticmethod
+    def _materialise(data: bytes, suffix: str) -> str:
+        """Write PEM bytes to a private (0600) temp file for ``load_cert_chain``; the caller
+        unlinks it as soon as the chain is loaded."""
         fd, path = tempfile.mkstemp(prefix="cron-operator-", suffix=suffix)
         with os.fdopen(fd, "wb") as fh:
             fh.write(data)
-        self._tmp.append(path)
         return path
 
     def ssl_context(self) -> Optional[ssl.SSLContext]:
@@ -98,16 +260,36 @@ class RestConfig:
             ctx.load_verify_locations(cadata=self.ca_data.decode())
         elif self.ca_file:
             ctx.load_verify_locations(cafile=self.ca_file)
-        cert = self.cert_file or (self._materialise(self.cert_data, ".crt") if self.cert_data else "")
-        key = self.key_file or (self._materialise(self.key_data, ".key") if self.key_data else "")
-        if cert:
-            ctx.load_cert_chain(cert, key or None)
+        cert_data, key_data = self.client_cert()
+        cert, key = "", ""
+        if not cert_data:
+            cert, key = self.cert_file, self.key_file
+            cert_data = b"" if cert else self.cert_data
+            key_data = b"" if key else self.key_data
+        tmp: List[str] = []
+        try:
+            if cert_data:
+                cert = self._materialise(cert_data, ".crt")
+                tmp.append(cert)
+            if key_data:
+                key = self._materialise(key_data, ".key")
+                tmp.append(key)
+            if cert:
+                ctx.load_cert_chain(cert, key or None)
+        finally:
+            for path in tmp:  # key material does not outlive the load
+                try:
+                    os.unlink(path)
+                except OSError:
+                    pass
         ctx.set_alpn_protocols(["http/1.1"])
         return ctx
 
-    def auth_headers(self) -> Dict[str, str]:
+    def auth_headers(self, token: Optional[str] = None) -> Dict[str, str]:
+        """Headers for every request; ``token`` saves a second :meth:`token` call when the caller
+        just fetched it."""
         h = {"User-Agent": self.user_agent}
-        tok = self.token()
+        tok = self.token() if token is None else token
         if tok:
             h["Authorization"] = f"Bearer {tok}"
         elif self.username:
@@ -143,8 +325,10 @@ def load_kubeconfig(path: str, context: Optional[str] = None) -> RestConfig:
     if cl is None:
         raise ConfigError(f"cluster {ctx.get('cluster')!r} not found in {path}")
     us = users.get(ctx.get("user", ""), {})
-    if "exec" in us or "auth-provider" in us:
-        raise ConfigError("exec/auth-provider credential plugins are not supported; use a token or client cert")
+    if "auth-provider" in us:
+        raise ConfigError("auth-provider plugins are not supported (removed from client-go for gcp/azure); "
+                          "use an exec credential plugin, a token or a client certificate")
+    exec_provider = ExecProvider.from_kubeconfig(us["exec"], cl) if us.get("exec") else None
     return RestConfig(
         host=cl.get("server", "").rstrip("/"),
         ca_file=_resolve(cl.get("certificate-authority", ""), path),
@@ -159,6 +343,7 @@ def load_kubeconfig(path: str, context: Optional[str] = None) -> RestConfig:
         key_file=_resolve(us.get("client-key", ""), path),
         cert_data=_b64(us.get("client-certificate-data")),
         key_data=_b64(us.get("client-key-data")),
+        exec_provider=exec_provider,
     )
 
 
