@@ -508,6 +508,19 @@ class APIServerApp:
             self._srv = None
 
 
+def _origin_form(target: str) -> str:
+    """RFC 9112 3.2.2: a server accepts the absolute form (``http://host:port/path?q``) that
+    clients use through a proxy; routing only needs the path and query."""
+    scheme, sep, rest = target.partition("://")
+    if not sep or scheme.lower() not in ("http", "https"):
+        return target
+    slash = rest.find("/")
+    q = rest.find("?")
+    if slash < 0 or (0 <= q < slash):
+        return "/" + (rest[q:] if q >= 0 else "")
+    return rest[slash:]
+
+
 class _ServerConn(asyncio.Protocol):
     """One client connection: parse requests, dispatch in order, write replies."""
 
@@ -558,6 +571,8 @@ class _ServerConn(asyncio.Protocol):
         method, target, headers, raw, consumed, keep = r
         del self.buf[:consumed]
         self._continued = False
+        if target[:1] != "/":
+            target = _origin_form(target)
         path, _, qs = target.partition("?")
         query: Dict[str, str] = {}
         if qs:
@@ -619,6 +634,8 @@ class _ServerConn(asyncio.Protocol):
             pos += clen
         del buf[:pos]
         self._continued = False
+        if target[:1] != "/":
+            target = _origin_form(target)
         path, _, qs = target.partition("?")
         query: Dict[str, str] = {}
         if qs:

@@ -8,7 +8,8 @@ fixed header set, ``Content-Length`` or ``chunked`` responses, keep-alive.
 This module is exactly that, on ``asyncio.Protocol``:
 
 * a pool of persistent connections per host (TLS via the kubeconfig's
-  ``ssl.SSLContext``; plain TCP for ``http://``);
+  ``ssl.SSLContext``; plain TCP for ``http://``), optionally through an http
+  proxy (absolute-form requests, or a ``CONNECT`` tunnel under TLS);
 * request bytes built once per call (method, path, fixed auth headers,
   ``Content-Length``);
 * an incremental response parser (status line, headers, ``Content-Length`` /
@@ -27,10 +28,11 @@ stream-reader round trips).
 from __future__ import annotations
 
 import asyncio
+import base64
 import ssl as _ssl
 from collections import deque
 from typing import Deque, Dict, List, Optional, Tuple
-from urllib.parse import urlsplit
+from urllib.parse import unquote, urlsplit
 
 from ..ops import httpcodec_native
 
@@ -361,12 +363,34 @@ def _expire(fut: asyncio.Future) -> None:
         fut.set_exception(asyncio.TimeoutError())
 
 
+class _Tunnel(asyncio.Protocol):
+    """Reads a proxy's answer to ``CONNECT``; ``done`` resolves to its status code."""
+
+    def __init__(self) -> None:
+        self.done: asyncio.Future = asyncio.get_running_loop().create_future()
+        self.buf = bytearray()
+
+    def data_received(self, data: bytes) -> None:
+        self.buf += data
+        end = self.buf.find(b"\r\n\r\n")
+        if end >= 0 and not self.done.done():
+            line = bytes(self.buf[:self.buf.find(b"\r\n")]).split(b" ", 2)
+            try:
+                self.done.set_result(int(line[1]))
+            except (IndexError, ValueError):
+                self.done.set_exception(ConnectionFailed("bad proxy response", True, False))
+
+    def connection_lost(self, exc: Optional[BaseException]) -> None:
+        if not self.done.done():
+            self.done.set_exception(ConnectionFailed(f"proxy closed the connection: {exc}", True, False))
+
+
 class HttpPool:
     """Keep-alive connection pool to one ``scheme://host:port``."""
 
     def __init__(self, base_url: str, ssl_context: Optional[_ssl.SSLContext] = None,
                  headers: Optional[Dict[str, str]] = None, max_idle: int = 64, timeout: float = 60.0,
-                 server_hostname: Optional[str] = None):
+                 server_hostname: Optional[str] = None, proxy: str = ""):
         u = urlsplit(base_url)
         self.scheme = u.scheme or "http"
         self.host = u.hostname or "127.0.0.1"
@@ -377,6 +401,19 @@ class HttpPool:
             self.ssl = _ssl.create_default_context()
         self.server_hostname = server_hostname
         self._hosthdr = self.host if (self.port in (80, 443)) else f"{self.host}:{self.port}"
+        self._proxy: Optional[Tuple[str, int]] = None
+        self._proxy_auth = ""
+        self._target = self.base_path  # request-target prefix: absolute form through an http proxy
+        if proxy:
+            pu = urlsplit(proxy if "://" in proxy else "http://" + proxy)
+            if pu.scheme != "http":
+                raise ValueError(f"proxy {proxy!r}: only http:// proxies are supported")
+            self._proxy = (pu.hostname or "127.0.0.1", pu.port or 80)
+            if pu.username is not None:
+                cred = f"{unquote(pu.username)}:{unquote(pu.password or '')}".encode()
+                self._proxy_auth = f"Proxy-Authorization: Basic {base64.b64encode(cred).decode()}\r\n"
+            if self.scheme == "http":
+                self._target = f"http://{self._hosthdr}{self.base_path}"
         self.set_headers(headers)
         self._idle: Deque[_Conn] = deque()
         self.max_idle = max_idle
@@ -390,6 +427,8 @@ class HttpPool:
         hdrs = {"User-Agent": "cron-operator-amd"}
         hdrs.update({k: v for k, v in (headers or {}).items() if k.lower() != "accept"})
         extra = "".join(f"{k}: {v}\r\n" for k, v in hdrs.items())
+        if self._proxy is not None and self.scheme == "http":
+            extra += self._proxy_auth  # plain requests go to the proxy itself
         self._fixed = f"Host: {self._hosthdr}\r\n{extra}"
 
     def set_ssl(self, ctx: _ssl.SSLContext) -> None:
@@ -402,17 +441,42 @@ class HttpPool:
             if c.transport is not None:
                 c.transport.close()
 
-    async def _connect(self) -> _Conn:
+    async def _open(self, factory):
+        """A connected protocol from ``factory``: direct, to an http proxy (plain servers), or
+        through a ``CONNECT`` tunnel to the server with TLS on top (https servers)."""
         loop = asyncio.get_running_loop()
-        kw = {}
-        if self.ssl is not None:
-            kw["ssl"] = self.ssl
-            kw["server_hostname"] = self.server_hostname or self.host
+        if self._proxy is None or self.ssl is None:
+            kw = {}
+            if self.ssl is not None:
+                kw["ssl"] = self.ssl
+                kw["server_hostname"] = self.server_hostname or self.host
+            host, port = self._proxy or (self.host, self.port)
+            _, proto = await asyncio.wait_for(loop.create_connection(factory, host, port, **kw), self.timeout)
+            return proto
+        transport, tun = await asyncio.wait_for(loop.create_connection(_Tunnel, *self._proxy), self.timeout)
+        authority = f"{self.host}:{self.port}" if ":" not in self.host else f"[{self.host}]:{self.port}"
+        transport.write(f"CONNECT {authority} HTTP/1.1\r\nHost: {authority}\r\n{self._proxy_auth}\r\n"
+                        .encode("latin-1"))
+        try:
+            status = await asyncio.wait_for(tun.done, self.timeout)
+            if status != 200:
+                raise ConnectionFailed(f"proxy CONNECT {authority}: HTTP {status}", True, False)
+            proto = factory()
+            tls = await asyncio.wait_for(loop.start_tls(transport, proto, self.ssl,
+                                                        server_hostname=self.server_hostname or self.host),
+                                         self.timeout)
+        except BaseException:
+            transport.close()
+            raise
+        proto.connection_made(tls)
+        return proto
+
+    async def _connect(self) -> _Conn:
         gen = self._ssl_gen
-        _, proto = await asyncio.wait_for(loop.create_connection(_Conn, self.host, self.port, **kw), self.timeout)
+        proto = await self._open(_Conn)
         proto.ssl_gen = gen
         self.connects += 1
-        return proto  # type: ignore[return-value]
+        return proto
 
     def _take_idle(self) -> Optional[_Conn]:
         while self._idle:
@@ -437,7 +501,7 @@ class HttpPool:
                            content_type: str = "application/json",
                            accept: str = "application/json") -> Tuple[int, bytes, Optional[int]]:
         """``(status, body, Retry-After seconds or None)``."""
-        head = f"{method} {self.base_path}{path} HTTP/1.1\r\n{self._fixed}Accept: {accept}\r\n"
+        head = f"{method} {self._target}{path} HTTP/1.1\r\n{self._fixed}Accept: {accept}\r\n"
         if body is not None:
             head += f"Content-Type: {content_type}\r\nContent-Length: {len(body)}\r\n\r\n"
             data = head.encode("latin-1") + body
@@ -477,16 +541,10 @@ class HttpPool:
         """GET ``path`` on a dedicated connection and stream its body line by line
         (``decode`` turns each non-empty line into an item).  Raises
         :class:`HttpStatusError` for an error status."""
-        loop = asyncio.get_running_loop()
-        kw = {}
-        if self.ssl is not None:
-            kw["ssl"] = self.ssl
-            kw["server_hostname"] = self.server_hostname or self.host
-        _, conn = await asyncio.wait_for(
-            loop.create_connection(lambda: _StreamConn(decode), self.host, self.port, **kw), self.timeout)
-        conn.head = loop.create_future()
+        conn = await self._open(lambda: _StreamConn(decode))
+        conn.head = asyncio.get_running_loop().create_future()
         assert conn.transport is not None
-        conn.transport.write(f"GET {self.base_path}{path} HTTP/1.1\r\n{self._fixed}Accept: {accept}\r\n\r\n"
+        conn.transport.write(f"GET {self._target}{path} HTTP/1.1\r\n{self._fixed}Accept: {accept}\r\n\r\n"
                              .encode("latin-1"))
         try:
             await asyncio.wait_for(conn.head, self.timeout)

@@ -119,13 +119,15 @@ class HttpTransport(Transport):
         self._pool: Optional[HttpPool] = None
         self._token = ""  # the bearer token the pool/session headers carry
         self._cert_generation = 0  # the exec-plugin client certificate the pool's TLS context holds
+        self._proxy: Optional[str] = None  # resolved on first use (aiohttp path)
 
     def _fast_pool(self) -> HttpPool:
         if self._pool is None:
             self._token = self.config.token()
             self._pool = HttpPool(self.config.host, ssl_context=self.config.ssl_context() or None,
                                   headers=self.config.auth_headers(self._token), max_idle=self._pool_size,
-                                  timeout=self._timeout, server_hostname=self.config.tls_server_name or None)
+                                  timeout=self._timeout, server_hostname=self.config.tls_server_name or None,
+                                  proxy=self.config.proxy())
             self._cert_generation = self.config.cert_generation
         elif self.config.rotating:
             self._rotate_token()
@@ -156,9 +158,17 @@ class HttpTransport(Transport):
             self.config.reset_token()
 
     def _tls_kw(self) -> Dict[str, Any]:
-        """kubeconfig ``tls-server-name``: verify the certificate against this name."""
+        """Per-request aiohttp options: kubeconfig ``tls-server-name`` (verify the certificate
+        against this name) and the proxy (kubeconfig ``proxy-url`` or the environment)."""
+        kw: Dict[str, Any] = {}
         name = self.config.tls_server_name
-        return {"server_hostname": name} if name and self.config.host.startswith("https://") else {}
+        if name and self.config.host.startswith("https://"):
+            kw["server_hostname"] = name
+        if self._proxy is None:
+            self._proxy = self.config.proxy()
+        if self._proxy:
+            kw["proxy"] = self._proxy if "://" in self._proxy else "http://" + self._proxy
+        return kw
 
     def _sess(self) -> aiohttp.ClientSession:
         if self.config.rotating and self._session is not None:

@@ -5,8 +5,13 @@ Order [ext controller-runtime ``config.GetConfig``]: ``--kubeconfig`` flag,
 (``KUBERNETES_SERVICE_HOST``/``_PORT`` + ``/var/run/secrets/kubernetes.io/serviceaccount``),
 then ``~/.kube/config``.  Supported kubeconfig auth: bearer token / tokenFile,
 client certificate + key (file or ``*-data``), exec credential plugins, basic auth, CA bundle or
-``insecure-skip-tls-verify``, ``tls-server-name`` and ``proxy-url``-less
-direct connections.  ``--qps``/``--burst`` are applied by the caller.
+``insecure-skip-tls-verify``, ``tls-server-name``.  ``--qps``/``--burst`` are applied by the caller.
+
+Proxies follow client-go: the kubeconfig's ``proxy-url`` for every request, else
+``HTTPS_PROXY``/``HTTP_PROXY`` minus ``NO_PROXY`` (Go ``http.ProxyFromEnvironment``;
+loopback servers are never proxied).  Only ``http://`` proxies are supported: plain
+requests in absolute form, ``https`` servers through a ``CONNECT`` tunnel
+(``runtime/fasthttp.py``), with ``user:password@`` sent as ``Proxy-Authorization``.
 
 Token files rotate: the in-cluster service-account token is a projected,
 kubelet-refreshed file (bound tokens expire; ``/var/run/secrets/.../token``).
@@ -29,6 +34,7 @@ a 401.  Plugins run non-interactively: ``interactiveMode: Always`` is refused.
 from __future__ import annotations
 
 import base64
+import ipaddress
 import json
 import os
 import ssl
@@ -37,6 +43,7 @@ import tempfile
 import time
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Tuple
+from urllib.parse import urlsplit
 
 import yaml
 
@@ -180,6 +187,7 @@ class RestConfig:
     key_data: bytes = b""
     insecure: bool = False
     tls_server_name: str = ""
+    proxy_url: str = ""                   # kubeconfig ``proxy-url``: every request, no NO_PROXY
     qps: float = 30.0
     burst: int = 50
     user_agent: str = "cron-operator-amd"
@@ -285,6 +293,10 @@ class RestConfig:
         ctx.set_alpn_protocols(["http/1.1"])
         return ctx
 
+    def proxy(self) -> str:
+        """The proxy for this server: kubeconfig ``proxy-url``, else the environment."""
+        return self.proxy_url or proxy_from_environment(self.host)
+
     def auth_headers(self, token: Optional[str] = None) -> Dict[str, str]:
         """Headers for every request; ``token`` saves a second :meth:`token` call when the caller
         just fetched it."""
@@ -335,6 +347,7 @@ def load_kubeconfig(path: str, context: Optional[str] = None) -> RestConfig:
         ca_data=_b64(cl.get("certificate-authority-data")),
         insecure=bool(cl.get("insecure-skip-tls-verify", False)),
         tls_server_name=cl.get("tls-server-name", ""),
+        proxy_url=_check_proxy(cl.get("proxy-url", "")),
         bearer_token=us.get("token", ""),
         bearer_token_file=_resolve(us.get("tokenFile", ""), path),
         username=us.get("username", ""),
@@ -345,6 +358,86 @@ def load_kubeconfig(path: str, context: Optional[str] = None) -> RestConfig:
         key_data=_b64(us.get("client-key-data")),
         exec_provider=exec_provider,
     )
+
+
+def _check_proxy(url: str) -> str:
+    if url and urlsplit(url if "://" in url else "http://" + url).scheme != "http":
+        raise ConfigError(f"proxy {url!r}: only http:// proxies are supported (CONNECT tunnels for https "
+                          "servers)")
+    return url
+
+
+def _no_proxy_match(host: str, port: int, entries: str) -> bool:
+    """Go ``httpproxy.Config``'s NO_PROXY rules: ``*``; an IP or CIDR; a domain name matching
+    itself and its subdomains, or with a leading ``.`` (or ``*.``) its subdomains only; IPs and
+    names optionally with ``:port``."""
+    host = host.strip("[]").lower()
+    try:
+        ip = ipaddress.ip_address(host)
+    except ValueError:
+        ip = None
+    for raw in entries.split(","):
+        e = raw.strip().lower()
+        if not e:
+            continue
+        if e == "*":
+            return True
+        if "/" in e:
+            try:
+                if ip is not None and ip in ipaddress.ip_network(e, strict=False):
+                    return True
+            except ValueError:
+                pass
+            continue
+        e_port = 0
+        h = e
+        if e.startswith("["):
+            h, _, rest = e[1:].partition("]")
+            e_port = int(rest[1:]) if rest.startswith(":") and rest[1:].isdigit() else 0
+        elif e.count(":") == 1:
+            h, _, ps = e.partition(":")
+            e_port = int(ps) if ps.isdigit() else 0
+        if e_port and e_port != port:
+            continue
+        if ip is not None:
+            try:
+                if ipaddress.ip_address(h) == ip:
+                    return True
+            except ValueError:
+                pass
+            continue
+        if h.startswith("*."):
+            h = h[1:]
+        if h.startswith("."):  # subdomains only
+            if host.endswith(h):
+                return True
+        elif host == h or host.endswith("." + h):
+            return True
+    return False
+
+
+def proxy_from_environment(server: str) -> str:
+    """``http.ProxyFromEnvironment`` for ``server``: ``HTTPS_PROXY``/``HTTP_PROXY`` by the
+    server's scheme (upper case first, then lower case), minus ``NO_PROXY`` matches; loopback
+    servers never go through a proxy."""
+    u = urlsplit(server)
+    host = (u.hostname or "").lower()
+    if host == "localhost" or host.endswith(".localhost"):
+        return ""
+    try:
+        if ipaddress.ip_address(host).is_loopback:
+            return ""
+    except ValueError:
+        pass
+    names = ("HTTPS_PROXY", "https_proxy") if u.scheme == "https" else ("HTTP_PROXY", "http_proxy")
+    proxy = next((os.environ[n] for n in names if os.environ.get(n)), "")
+    if not proxy:
+        return ""
+    no_proxy = os.environ.get("NO_PROXY") or os.environ.get("no_proxy") or ""
+    port = u.port or (443 if u.scheme == "https" else 80)
+    if no_proxy and _no_proxy_match(host, port, no_proxy):
+        return ""
+    return _check_proxy(proxy)
 
 
 def in_cluster_config() -> Optional[RestConfig]:
