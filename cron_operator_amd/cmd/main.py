@@ -111,6 +111,10 @@ def build_parser() -> argparse.ArgumentParser:
                                                                 "replicas (hash of namespace/name).")
     st.add_argument("--shard-index", type=int, default=int(os.environ.get("SHARD_INDEX", "0") or 0),
                     help="This replica's shard in [0, --shard-count) (default: $SHARD_INDEX).")
+    st.add_argument("--shard-processes", type=int, default=1,
+                    help="Run this many operator processes in this pod, one shard each (the pod's share of "
+                         "--shard-count is split further), under a supervisor that serves the merged metrics "
+                         "and the probes. Uses that many cores, like the reference's goroutine workers.")
     st.add_argument("--shard-routing", choices=["hash", "labels"], default="hash",
                     help="hash: every shard watches all objects and drops other shards' keys; labels: shards "
                          "label their Crons and children kubedl.io/shard=<index>-of-<count> and watch only "
@@ -249,6 +253,42 @@ async def run_start(a: argparse.Namespace) -> int:
     finally:
         await client.close()
     return 0
+
+
+async def run_supervisor(a: argparse.Namespace, argv: List[str]) -> int:
+    """``start --shard-processes N`` (runtime/supervisor.py)."""
+    from ..runtime.client import Client
+    from ..runtime.http import HttpTransport
+    from ..runtime.kubeconfig import ConfigError, get_config
+    from ..runtime.servers import MetricsServer, parse_bind_address
+    from ..runtime.supervisor import Supervisor
+    from ..utils.logging import get_logger
+
+    log = get_logger("setup")
+    if a.shard_count < 1 or not 0 <= a.shard_index < a.shard_count:
+        log.error(ValueError(f"--shard-index {a.shard_index} not in [0, {a.shard_count})"), "invalid sharding")
+        return 2
+    client = None
+    metrics = None
+    if parse_bind_address(a.metrics_bind_address) is not None:
+        if a.metrics_secure:  # TokenReview / SubjectAccessReview need the API
+            try:
+                cfg = get_config(a.kubeconfig)
+            except ConfigError as e:
+                log.error(e, "unable to get kubeconfig")
+                return 1
+            client = Client(HttpTransport(cfg), qps=a.qps, burst=a.burst)
+        metrics = MetricsServer(a.metrics_bind_address, secure=a.metrics_secure, cert_dir=a.metrics_cert_path,
+                                cert_name=a.metrics_cert_name, key_name=a.metrics_cert_key, client=client,
+                                enable_http2=a.enable_http2)
+    sup = Supervisor(argv, a.shard_processes, a.shard_count, a.shard_index, metrics, a.health_probe_bind_address)
+    log.info("starting shard processes", processes=a.shard_processes,
+             shards=[c.index for c in sup.children], shardCount=a.shard_count * a.shard_processes)
+    try:
+        return await sup.run()
+    finally:
+        if client is not None:
+            await client.close()
 
 
 async def run_fake_apiserver(a: argparse.Namespace) -> int:
@@ -425,6 +465,11 @@ def main(argv: Optional[List[str]] = None) -> int:
             return 2
         if a.cron_engine != "auto":
             os.environ["CRON_OPERATOR_ENGINE"] = a.cron_engine
+        if a.shard_processes > 1:
+            return asyncio.run(run_supervisor(a, list(sys.argv[1:] if argv is None else argv)))
+        if a.shard_processes < 1:
+            print("invalid argument: --shard-processes must be >= 1", file=sys.stderr)
+            return 2
         return asyncio.run(run_start(a))
     parser.print_help()
     return 2

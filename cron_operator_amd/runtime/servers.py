@@ -155,6 +155,8 @@ class MetricsServer:
         self._tmp: Optional[tempfile.TemporaryDirectory] = None
         self.port: Optional[int] = None
         self.extra_handlers: Dict[str, Callable[[web.Request], Awaitable[web.Response]]] = {}
+        # replaces the /metrics handler (the shard-process supervisor serves merged expositions)
+        self.handler: Optional[Callable[[web.Request], Awaitable[web.Response]]] = None
         self.log = get_logger("controller-runtime.metrics")
 
     async def _authorize(self, req: web.Request) -> Optional[web.Response]:
@@ -194,7 +196,7 @@ class MetricsServer:
             body = metrics.exposition()
             return web.Response(body=body, headers={"Content-Type": "text/plain; version=0.0.4; charset=utf-8"})
 
-        app.router.add_get("/metrics", handle)
+        app.router.add_get("/metrics", self.handler or handle)
         for path, h in self.extra_handlers.items():
             app.router.add_get(path, h)
         return app

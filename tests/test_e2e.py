@@ -255,3 +255,63 @@ def test_cli_help_version_crd():
     r = subprocess.run([sys.executable, "-m", "cron_operator_amd", "crd"], env=env, capture_output=True, text=True,
                        timeout=120)
     assert r.returncode == 0 and "crons.apps.kubedl.io" in r.stdout
+
+
+def test_shard_processes_in_one_pod(cluster):
+    """`start --shard-processes 2`: one supervisor, two shard processes with their own Leases;
+    the supervisor's /metrics merges theirs (labelled by shard), its probes cover both, a
+    crashed shard process is restarted, and SIGTERM stops everything cleanly."""
+    import psutil
+
+    from cron_operator_amd.runtime.controller import shard_of
+
+    base = cluster["base"]
+    _api(base, "POST", "/api/v1/namespaces", {"apiVersion": "v1", "kind": "Namespace",
+                                              "metadata": {"name": "procs"}})
+    proc, probe, mport = _start_operator(cluster, "--leader-elect", "--metrics-secure=false",
+                                         "--shard-processes", "2", "--shard-routing", "labels")
+    names = [f"p{i}" for i in range(6)]
+    try:
+        _wait(lambda: _get(f"http://127.0.0.1:{probe}/readyz")[0] == 200, 60, "readyz", proc)
+        assert _get(f"http://127.0.0.1:{probe}/healthz")[0] == 200
+        tmpl = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+                "spec": {"pytorchReplicaSpecs": {"Master": {"replicas": 1}}}}
+        past = time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime(time.time() - 120))
+        for n in names:
+            _api(base, "POST", "/apis/apps.kubedl.io/v1alpha1/namespaces/procs/crons",
+                 {"apiVersion": "apps.kubedl.io/v1alpha1", "kind": "Cron", "metadata": {"name": n},
+                  "spec": {"schedule": "*/1 * * * *", "concurrencyPolicy": "Forbid", "template": {"workload": tmpl}}})
+            _api(base, "PATCH", f"/apis/apps.kubedl.io/v1alpha1/namespaces/procs/crons/{n}/status",
+                 {"status": {"lastScheduleTime": past}}, "application/merge-patch+json")
+
+        def all_fired():
+            jobs = _api(base, "GET", "/apis/kubeflow.org/v1/namespaces/procs/pytorchjobs")["items"]
+            return jobs if {j["metadata"]["labels"]["kubedl.io/cron-name"] for j in jobs} >= set(names) else None
+
+        for j in _wait(all_fired, 60, "every Cron fired", proc):
+            cron = j["metadata"]["labels"]["kubedl.io/cron-name"]
+            assert j["metadata"]["labels"]["kubedl.io/shard"] == f"{shard_of('procs', cron, 2)}-of-2"
+        for i in range(2):
+            lease = _api(base, "GET", "/apis/coordination.k8s.io/v1/namespaces/cron-operator-system/leases/"
+                                      f"619a52b8.kubedl.io-shard-{i}")
+            assert lease["spec"]["holderIdentity"]
+
+        status, body = _get(f"http://127.0.0.1:{mport}/metrics")
+        assert status == 200
+        for i in range(2):
+            assert f'controller_runtime_reconcile_total{{shard="{i}",controller="cron",result="requeue_after"}}' \
+                in body
+        assert body.count("# TYPE controller_runtime_reconcile_total counter") == 1
+
+        # a shard process dies: health reports it, the supervisor restarts it
+        kids = psutil.Process(proc.pid).children()
+        assert len(kids) == 2
+        kids[0].kill()
+        _wait(lambda: len([k for k in psutil.Process(proc.pid).children() if k.pid != kids[0].pid]) == 2,
+              30, "shard process restarted", proc)
+        _wait(lambda: _get(f"http://127.0.0.1:{probe}/readyz")[0] == 200, 60, "readyz after restart", proc)
+        kids = psutil.Process(proc.pid).children()
+    finally:
+        rc = _stop(proc)
+    assert rc == 0, proc.stdout.read()[-3000:]
+    assert not any(psutil.pid_exists(k.pid) and k.status() != psutil.STATUS_ZOMBIE for k in kids)

@@ -51,9 +51,17 @@ def test_replicas_and_pull_policy():
     ({"burst": 200}, "--burst=200"),
     ({"compatMode": "reference"}, "--compat-mode=reference"),
     ({"extraArgs": ["--namespace=team-a"]}, "--namespace=team-a"),
+    ({"sharding": {"processes": 4, "routing": "labels"}}, "--shard-processes=4"),
+    ({"sharding": {"processes": 4, "routing": "labels"}}, "--shard-routing=labels"),
+    ({"sharding": {"count": 2, "index": 1}}, "--shard-index=1"),
 ])
 def test_args(values, arg):
     assert arg in container(values)["args"]
+
+
+def test_sharding_args_absent_by_default():
+    args = container()["args"]
+    assert not [a for a in args if a.startswith("--shard")]
 
 
 def test_args_are_parsed_by_the_cli():

@@ -64,3 +64,21 @@ def test_operator_registry_exposes_controller_runtime_names():
     for name in ("controller_runtime_reconcile", "controller_runtime_reconcile_time_seconds", "workqueue_depth",
                  "rest_client_requests", "process_cpu_seconds", "process_resident_memory_bytes", "python_info"):
         assert name in fams, name
+
+
+def test_supervisor_merges_shard_expositions():
+    """runtime/supervisor.py: one HELP/TYPE per family, every sample labelled by shard,
+    histogram series kept under their family; the result parses."""
+    from cron_operator_amd.runtime.supervisor import merge_expositions
+
+    a = ("# HELP x_total Things.\n# TYPE x_total counter\nx_total{kind=\"a\"} 1.0\n"
+         "# HELP h_seconds Lat.\n# TYPE h_seconds histogram\nh_seconds_bucket{le=\"+Inf\"} 2.0\n"
+         "h_seconds_sum 0.5\nh_seconds_count 2.0\n# HELP g Plain.\n# TYPE g gauge\ng 3.0\n")
+    b = a.replace("1.0", "4.0")
+    out = merge_expositions([("0", a), ("1", b)])
+    assert out.count("# TYPE x_total counter") == 1
+    assert 'x_total{shard="0",kind="a"} 1.0' in out and 'x_total{shard="1",kind="a"} 4.0' in out
+    assert 'g{shard="1"} 3.0' in out and 'h_seconds_sum{shard="0"} 0.5' in out
+    fams = _parse(out)
+    assert {s.labels["shard"] for s in fams["x"].samples} == {"0", "1"}
+    assert len(fams["h_seconds"].samples) == 6
