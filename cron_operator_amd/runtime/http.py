@@ -120,6 +120,7 @@ class HttpTransport(Transport):
         self._token = ""  # the bearer token the pool/session headers carry
         self._cert_generation = 0  # the exec-plugin client certificate the pool's TLS context holds
         self._proxy: Optional[str] = None  # resolved on first use (aiohttp path)
+        self._exec_lock: Optional[asyncio.Lock] = None
 
     def _fast_pool(self) -> HttpPool:
         if self._pool is None:
@@ -151,6 +152,14 @@ class HttpTransport(Transport):
             self._pool.set_headers(hdrs)
         if self._session is not None and not self._session.closed:
             self._session.headers.update(hdrs)
+
+    async def _fresh_exec(self) -> None:
+        """Run a stale exec credential plugin off the event loop, once for all waiting requests."""
+        if self._exec_lock is None:
+            self._exec_lock = asyncio.Lock()
+        async with self._exec_lock:
+            if self.config.exec_stale():
+                await asyncio.get_running_loop().run_in_executor(None, self.config.refresh_exec)
 
     def _unauthorized(self) -> None:
         """A 401: drop the cached file token / exec credential so the next request refreshes it."""
@@ -193,6 +202,8 @@ class HttpTransport(Transport):
 
     async def request(self, verb: str, gvr: GroupVersionResource, namespace: str = "", name: str = "",
                       subresource: str = "", body: Any = None, params: Optional[Dict[str, Any]] = None) -> Any:
+        if self.config.exec_provider is not None and self.config.exec_stale():
+            await self._fresh_exec()
         params = params or {}
         method = _METHODS[verb]
         path = resource_path(gvr, namespace, name if verb not in ("list", "create", "deletecollection") else "",
@@ -245,6 +256,8 @@ class HttpTransport(Transport):
 
     async def watch(self, gvr: GroupVersionResource, namespace: str = "",
                     params: Optional[Dict[str, Any]] = None) -> WatchStream:
+        if self.config.exec_provider is not None and self.config.exec_stale():
+            await self._fresh_exec()
         p = _clean(params)
         p["watch"] = "true"
         if self.fast:
@@ -272,6 +285,8 @@ class HttpTransport(Transport):
         return _HttpWatch(resp)
 
     async def discover(self, group_version: GroupVersion) -> List[Dict[str, Any]]:
+        if self.config.exec_provider is not None and self.config.exec_stale():
+            await self._fresh_exec()
         path = f"/api/{group_version.version}" if not group_version.group else \
             f"/apis/{group_version.group}/{group_version.version}"
         try:

@@ -202,15 +202,28 @@ class RestConfig:
         """Credentials can change while the process runs (token file or exec plugin)."""
         return bool(self.bearer_token_file) or self.exec_provider is not None
 
+    def exec_stale(self) -> bool:
+        """An exec plugin is configured and its credential is missing or expired."""
+        if self.exec_provider is None:
+            return False
+        c = self._exec_creds
+        return c is None or (c.expires_at is not None and time.time() >= c.expires_at)
+
+    def refresh_exec(self) -> None:
+        """Run the plugin now if its credential is stale (blocking: the HTTP transport calls
+        this in a worker thread so the event loop keeps serving leases and watches)."""
+        if self.exec_stale():
+            old = self._exec_creds
+            new = self.exec_provider.run()  # type: ignore[union-attr]
+            if old is None or (new.cert_data, new.key_data) != (old.cert_data, old.key_data):
+                self.cert_generation += 1
+            self._exec_creds = new
+
     def _exec(self) -> ExecCredentials:
         """The plugin's cached credential, re-run once expired (client-go ``credsExpired``)."""
-        c = self._exec_creds
-        if c is None or (c.expires_at is not None and time.time() >= c.expires_at):
-            new = self.exec_provider.run()  # type: ignore[union-attr]
-            if c is None or (new.cert_data, new.key_data) != (c.cert_data, c.key_data):
-                self.cert_generation += 1
-            self._exec_creds = c = new
-        return c
+        self.refresh_exec()
+        assert self._exec_creds is not None
+        return self._exec_creds
 
     def client_cert(self) -> Tuple[bytes, bytes]:
         """PEM client certificate and key from an exec plugin, or empty."""
