@@ -57,6 +57,17 @@ def _add_bool(p: argparse.ArgumentParser, name: str, default: bool, help_: str) 
     p.add_argument(name, nargs="?", const=True, default=default, type=_bool, metavar="true|false", help=help_)
 
 
+def _processes(v: str) -> int:
+    if v == "auto":
+        from ..runtime.supervisor import available_cpus
+
+        return available_cpus()
+    try:
+        return int(v)
+    except ValueError:
+        raise argparse.ArgumentTypeError(f"invalid --shard-processes {v!r} (an integer or 'auto')") from None
+
+
 def build_parser() -> argparse.ArgumentParser:
     root = argparse.ArgumentParser(prog="cron-operator", description="Cron operator for scheduled ML training jobs "
                                                                      "(apps.kubedl.io/v1alpha1 Cron).")
@@ -111,10 +122,11 @@ def build_parser() -> argparse.ArgumentParser:
                                                                 "replicas (hash of namespace/name).")
     st.add_argument("--shard-index", type=int, default=int(os.environ.get("SHARD_INDEX", "0") or 0),
                     help="This replica's shard in [0, --shard-count) (default: $SHARD_INDEX).")
-    st.add_argument("--shard-processes", type=int, default=1,
+    st.add_argument("--shard-processes", type=_processes, default=1,
                     help="Run this many operator processes in this pod, one shard each (the pod's share of "
                          "--shard-count is split further), under a supervisor that serves the merged metrics "
-                         "and the probes. Uses that many cores, like the reference's goroutine workers.")
+                         "and the probes. Uses that many cores, like the reference's goroutine workers. "
+                         "'auto': the CPUs the container may use (cgroup quota, else affinity).")
     st.add_argument("--shard-routing", choices=["hash", "labels"], default="hash",
                     help="hash: every shard watches all objects and drops other shards' keys; labels: shards "
                          "label their Crons and children kubedl.io/shard=<index>-of-<count> and watch only "

@@ -21,6 +21,8 @@ process becomes a supervisor:
 from __future__ import annotations
 
 import asyncio
+import math
+import os
 import signal
 import socket
 import sys
@@ -40,6 +42,34 @@ def _free_port() -> int:
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+def available_cpus(cgroup_root: str = "/sys/fs/cgroup") -> int:
+    """CPUs this container may use: the cgroup CPU quota rounded up (v2 ``cpu.max``, v1
+    ``cpu.cfs_quota_us``/``cpu.cfs_period_us``), else the scheduler affinity mask; at least 1."""
+    quota = None
+    try:
+        with open(os.path.join(cgroup_root, "cpu.max")) as fh:
+            q, period = (fh.read().split() + ["100000"])[:2]  # "max 100000" or "<quota> <period>"
+        if q != "max":
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        try:
+            with open(os.path.join(cgroup_root, "cpu", "cpu.cfs_quota_us")) as fh:
+                q1 = int(fh.read())
+            with open(os.path.join(cgroup_root, "cpu", "cpu.cfs_period_us")) as fh:
+                p1 = int(fh.read())
+            if q1 > 0 and p1 > 0:
+                quota = q1 / p1
+        except (OSError, ValueError):
+            pass
+    try:
+        cpus = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        cpus = os.cpu_count() or 1
+    if quota is not None:
+        cpus = min(cpus, math.ceil(quota))
+    return max(1, cpus)
 
 
 def merge_expositions(parts: List[Tuple[str, str]]) -> str:

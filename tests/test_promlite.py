@@ -82,3 +82,30 @@ def test_supervisor_merges_shard_expositions():
     fams = _parse(out)
     assert {s.labels["shard"] for s in fams["x"].samples} == {"0", "1"}
     assert len(fams["h_seconds"].samples) == 6
+
+
+def test_available_cpus_reads_cgroup_quotas(tmp_path):
+    """`--shard-processes auto`: the container's CPU quota, rounded up, capped by affinity."""
+    import os
+
+    from cron_operator_amd.cmd.main import build_parser
+    from cron_operator_amd.runtime.supervisor import available_cpus
+
+    affinity = len(os.sched_getaffinity(0))
+    v2 = tmp_path / "v2"
+    v2.mkdir()
+    (v2 / "cpu.max").write_text("150000 100000\n")
+    assert available_cpus(str(v2)) == min(2, affinity)
+    (v2 / "cpu.max").write_text("max 100000\n")
+    assert available_cpus(str(v2)) == affinity
+    v1 = tmp_path / "v1"
+    (v1 / "cpu").mkdir(parents=True)
+    (v1 / "cpu" / "cpu.cfs_quota_us").write_text("100000\n")
+    (v1 / "cpu" / "cpu.cfs_period_us").write_text("100000\n")
+    assert available_cpus(str(v1)) == 1
+    (v1 / "cpu" / "cpu.cfs_quota_us").write_text("-1\n")
+    assert available_cpus(str(v1)) == affinity
+    assert available_cpus(str(tmp_path / "none")) == affinity
+    a = build_parser().parse_args(["start", "--shard-processes", "auto"])
+    assert a.shard_processes >= 1
+    assert build_parser().parse_args(["start", "--shard-processes", "3"]).shard_processes == 3
