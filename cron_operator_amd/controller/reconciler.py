@@ -162,6 +162,10 @@ class ReconcilerOptions:
     dedupe_ran_tick: bool = True
     overlap_gc_deletes: bool = True
     slim_child_cache: bool = True
+    # cache mode: how long a reconcile waits for a new child informer's first LIST before
+    # it falls back to a live LIST; a LIST that *fails* (403, 404, 5xx) is returned as the
+    # reconcile's error at once, like the reference's live LIST (cron_controller.go:129-133)
+    child_sync_timeout: float = 5.0
     workload: WorkloadPolicy = field(default_factory=WorkloadPolicy)
     static_owned_kinds: Tuple[GroupVersionKind, ...] = (
         GroupVersionKind("kubeflow.org", "v1", "PyTorchJob"),
@@ -615,8 +619,19 @@ class CronReconciler(Reconciler):
             inf.start()
             if self.on_child_informer is not None:
                 self.on_child_informer(gvk, inf)
+        return inf
+
+    async def _synced_child_informer(self, gvk: GroupVersionKind) -> Optional[Informer]:
+        """The synced child informer of ``gvk``; ``None`` when its first LIST is still running
+        after ``child_sync_timeout`` (the caller then LISTs live).  A failed LIST raises: the
+        worker is freed and the Cron retried with backoff instead of waiting on an informer
+        that cannot sync (e.g. a kind the operator may not list)."""
+        inf = await self.child_informer(gvk)
         if not inf.synced.is_set():
-            await inf.synced.wait()
+            try:
+                await inf.wait_synced(self.opts.child_sync_timeout)
+            except asyncio.TimeoutError:
+                return None
             gctune.freeze()  # a newly synced child cache: long-lived, keep it out of GC scans
         return inf
 
@@ -625,7 +640,10 @@ class CronReconciler(Reconciler):
         the Cron's namespace labelled ``kubedl.io/cron-name=<name>``."""
         log.v(1).info(f"Listing {gvk.kind}")
         self.stats["lists"] += 1
-        if self.opts.list_mode == "live" or self.cache is None:
+        inf = None
+        if self.opts.list_mode != "live" and self.cache is not None:
+            inf = await self._synced_child_informer(gvk)
+        if inf is None:
             lst = await self.client.list(gvk, cron.namespace, label_selector=f"{LABEL_CRON_NAME}={cron.name}")
             items = lst.get("items") or []
             for it in items:
@@ -633,7 +651,6 @@ class CronReconciler(Reconciler):
                 it.setdefault("apiVersion", gvk.api_version)
                 it.setdefault("kind", gvk.kind)
             return items
-        inf = await self.child_informer(gvk)
         children = inf.by_index(CHILD_INDEX, f"{cron.namespace}/{cron.name}", copy=False)
         if self.opts.expectations:
             children = self.expect.adjust(self._ckey(cron), children)

@@ -1,8 +1,9 @@
 """Python-facing wrapper of the native cron engine (``csrc/cron_engine.cpp``).
 
 Zones: the extension knows nothing about the filesystem.  This module hands it
-TZif blobs from the ``tzdata`` wheel (there is no ``/usr/share/zoneinfo`` in the
-image) and maps :class:`~cron_operator_amd.utils.gotime.Location` objects to
+TZif blobs found the way Go's ``time.LoadLocation`` finds them
+(:func:`~cron_operator_amd.utils.gotime.tzif_bytes`: ``$ZONEINFO``, the system
+zoneinfo directories, then the ``tzdata`` wheel) and maps :class:`~cron_operator_amd.utils.gotime.Location` objects to
 native zone ids.  ``Local`` is resolved the same way Go resolves ``time.Local``
 ($TZ, else /etc/localtime, else UTC).
 """
@@ -13,7 +14,7 @@ import os
 import threading
 from typing import Dict, Optional
 
-from ..utils.gotime import LOCAL, UTC, FixedZone, Location, ZoneLocation, load_location
+from ..utils.gotime import LOCAL, UTC, FixedZone, Location, ZoneLocation, load_location, tzif_bytes
 from . import build as _build
 
 _lock = threading.Lock()
@@ -23,14 +24,7 @@ _load_error: Optional[BaseException] = None
 
 
 def _tzif_bytes(name: str) -> bytes:
-    if name.startswith("/"):
-        with open(name, "rb") as fh:
-            return fh.read()
-    from importlib import resources
-
-    parts = name.split("/")
-    node = resources.files("tzdata").joinpath("zoneinfo", *parts)
-    return node.read_bytes()
+    return tzif_bytes(name)
 
 
 def load(build_if_missing: bool = True):

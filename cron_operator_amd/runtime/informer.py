@@ -112,6 +112,12 @@ class Informer:
         self.indices: Dict[str, Dict[str, Set[str]]] = {n: {} for n in self.indexers}
         self.handlers: List[EventHandler] = []
         self.synced = asyncio.Event()
+        # the outcome of the most recent LIST: ``list_error`` is its error (None after a
+        # success) and ``_attempted`` is set after every attempt, so a reader waiting for
+        # the first sync learns of a failing LIST instead of waiting without bound
+        self.list_error: Optional[BaseException] = None
+        self.list_failures = 0
+        self._attempted = asyncio.Event()
         self.last_rv = ""
         self._task: Optional[asyncio.Task] = None
         self._watch = None
@@ -235,14 +241,48 @@ class Informer:
 
     # ------------------------------------------------------------------ reflector
     async def _list(self) -> None:
-        lst = await self.client.list_all(self.target, self.namespace, self.label_selector, self.page_size) \
-            if not self.field_selector else \
-            await self.client.list(self.target, self.namespace, self.label_selector, self.field_selector)
+        try:
+            lst = await self.client.list_all(self.target, self.namespace, self.label_selector, self.page_size) \
+                if not self.field_selector else \
+                await self.client.list(self.target, self.namespace, self.label_selector, self.field_selector)
+        except asyncio.CancelledError:
+            raise
+        except Exception as e:
+            self.list_error = e
+            self.list_failures += 1
+            self._attempted.set()
+            raise
+        self.list_error = None
+        self.list_failures = 0
+        self._attempted.set()
         self.relists += 1
         self._replace(lst.get("items") or [])
         self.last_rv = (lst.get("metadata") or {}).get("resourceVersion", "")
         if not self.synced.is_set():
             self.synced.set()
+
+    async def wait_synced(self, timeout: Optional[float] = None) -> None:
+        """Wait for the first successful LIST.  Raises the LIST's error as soon as an attempt
+        fails (403 Forbidden, 404, 5xx, a transport error) -- client-go's reflector only logs
+        it and retries, but a caller that needs the data now (a reconcile) must not hold its
+        worker while the informer backs off -- and :class:`asyncio.TimeoutError` after
+        ``timeout`` seconds without an outcome."""
+        loop = asyncio.get_running_loop()
+        deadline = None if timeout is None else loop.time() + timeout
+        while not self.synced.is_set():
+            if self.list_error is not None:
+                raise self.list_error
+            self._attempted.clear()
+            if deadline is None:
+                await self._attempted.wait()
+                continue
+            left = deadline - loop.time()
+            if left <= 0:
+                raise asyncio.TimeoutError(f"informer {self.name} has not synced after {timeout}s")
+            try:
+                await asyncio.wait_for(self._attempted.wait(), left)
+            except asyncio.TimeoutError:
+                raise asyncio.TimeoutError(f"informer {self.name} has not synced after {timeout}s") from None
 
     async def run(self) -> None:
         backoff = 0.1
@@ -271,7 +311,7 @@ class Informer:
                     need_list = True
                     self.log.v(1).info("watch expired, relisting")
                     continue
-                self.log.error(e, "watch failed")
+                self.log.error(e, "failed to list" if need_list else "watch failed")
                 if e.code == 404:
                     need_list = True
                 await asyncio.sleep(backoff * (1 + random.random()))

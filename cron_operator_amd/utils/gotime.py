@@ -17,8 +17,9 @@ differs from Python ``datetime`` in the details that matter for cron parity:
 ``GoTime`` reproduces exactly these rules on top of an integer
 ``(unix_seconds, nanoseconds, location)`` triple, with the proleptic-Gregorian
 day arithmetic done in integers (no ``datetime`` on the hot path).  Time-zone
-offsets come from the IANA database through :mod:`zoneinfo` (the ``tzdata``
-wheel here; there is no ``/usr/share/zoneinfo`` in the image).
+offsets come from the IANA database, looked up in Go's order (:func:`tzif_bytes`):
+``$ZONEINFO``, the system zoneinfo directories, then the ``tzdata`` wheel (Go's
+embedded ``time/tzdata``).
 """
 from __future__ import annotations
 
@@ -26,7 +27,7 @@ import os
 import re
 from datetime import datetime
 from functools import lru_cache
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
 NANOS = 1_000_000_000
 SECOND = NANOS
@@ -139,6 +140,69 @@ class ZoneLocation(Location):
 UTC = FixedZone("UTC", 0)
 
 
+def _zone_dirs() -> List[str]:
+    """System zoneinfo directories: :data:`zoneinfo.TZPATH` (``PYTHONTZPATH`` when set,
+    else Go's list, ``/usr/share/zoneinfo`` first)."""
+    try:
+        import zoneinfo
+
+        return [d for d in zoneinfo.TZPATH if d]
+    except ImportError:  # pragma: no cover - py<3.9
+        return ["/usr/share/zoneinfo", "/usr/lib/zoneinfo", "/usr/share/lib/zoneinfo", "/etc/zoneinfo"]
+
+
+def tzif_bytes(name: str) -> bytes:
+    """The TZif data of IANA zone ``name`` (or of an absolute file path).
+
+    Search order of Go's ``time.LoadLocation``: ``$ZONEINFO`` (a directory or a
+    zip of the zoneinfo tree), the system zoneinfo directories, then the ``tzdata``
+    wheel -- the counterpart of Go's embedded ``time/tzdata``.  Both cron engines read
+    zones through here, so an image with only the OS ``tzdata`` package (no wheel)
+    and one with only the wheel resolve the same names."""
+    if name.startswith("/"):
+        with open(name, "rb") as fh:
+            return fh.read()
+    if not name or name.startswith(".") or ".." in name.split("/") or "\\" in name:
+        raise ValueError(f"unknown time zone {name}")
+    zi = os.environ.get("ZONEINFO")
+    if zi:
+        try:
+            if zi.endswith(".zip"):
+                import zipfile
+
+                with zipfile.ZipFile(zi) as zf:
+                    return zf.read(name)
+            with open(os.path.join(zi, name), "rb") as fh:
+                return fh.read()
+        except (OSError, KeyError):
+            pass
+    for d in _zone_dirs():
+        try:
+            with open(os.path.join(d, name), "rb") as fh:
+                data = fh.read()
+        except OSError:
+            continue
+        if data[:4] == b"TZif":
+            return data
+    try:
+        from importlib import resources
+
+        node = resources.files("tzdata").joinpath("zoneinfo", *name.split("/"))
+        data = node.read_bytes()
+        if data[:4] == b"TZif":
+            return data
+    except (ImportError, OSError, TypeError, AttributeError):
+        pass
+    raise ValueError(f"unknown time zone {name}")
+
+
+def _zoneinfo_from(name: str):
+    import io
+    from zoneinfo import ZoneInfo
+
+    return ZoneInfo.from_file(io.BytesIO(tzif_bytes(name)), key=name)
+
+
 @lru_cache(maxsize=256)
 def load_location(name: str) -> Location:
     """Go ``time.LoadLocation``: "" and "UTC" are UTC, "Local" is :data:`LOCAL`."""
@@ -149,9 +213,7 @@ def load_location(name: str) -> Location:
     if name.startswith("/") or ".." in name or "\\" in name:
         raise ValueError(f"unknown time zone {name}")
     try:
-        from zoneinfo import ZoneInfo
-
-        tz = ZoneInfo(name)
+        tz = _zoneinfo_from(name)
     except Exception:
         raise ValueError(f"unknown time zone {name}") from None
     return ZoneLocation(name, tz)
@@ -165,12 +227,7 @@ def _resolve_local() -> Location:
             return FixedZone("Local", 0)
         name = tzenv[1:] if tzenv.startswith(":") else tzenv
         try:
-            from zoneinfo import ZoneInfo
-
-            if name.startswith("/"):
-                with open(name, "rb") as fh:
-                    return ZoneLocation("Local", ZoneInfo.from_file(fh), key=name)
-            return ZoneLocation("Local", ZoneInfo(name), key=name)
+            return ZoneLocation("Local", _zoneinfo_from(name), key=name)
         except Exception:
             return FixedZone("Local", 0)
     try:

@@ -231,3 +231,90 @@ def test_every_rounds_to_second():
     assert iso(e.next(s, t)) == "2026-01-01T12:01:30Z"
     assert e.next(s, t).nsec == 0
     assert e.parse("@every 1h").impl.delay == HOUR
+
+
+# ---------------------------------------------------------------- zone lookup without the tzdata wheel
+
+_NO_WHEEL_PROBE = r'''
+import json, os, sys
+sys.modules["tzdata"] = None  # hide the wheel: zones must come from the system directory
+import yaml
+from cron_operator_amd.cron.engine import NativeEngine, PythonEngine
+from cron_operator_amd.utils.gotime import LOCAL, UTC, GoTime, parse_rfc3339
+spec = yaml.safe_load(open(sys.argv[1]))["spec"]["schedule"]
+specs = [spec, "CRON_TZ=America/New_York 0 9 * * mon-fri", "TZ=Europe/Berlin 30 1 * * *",
+         "CRON_TZ=Australia/Lord_Howe */30 * * * *", "0 2 * * *"]
+out = {}
+for s in specs:
+    row = []
+    for eng in (PythonEngine(), NativeEngine()):
+        sched = eng.parse(s)
+        t = parse_rfc3339("2026-03-07T00:00:00Z")
+        ts = []
+        for _ in range(40):
+            t = eng.next(sched, t)
+            ts.append((t.sec, t.nsec))
+        if s == "0 2 * * *":  # Local: $TZ of this process
+            ts.append(eng.next(sched, GoTime(1772841600, 0, LOCAL)).sec)
+        row.append(ts)
+    out[s] = row
+print(json.dumps(out))
+'''
+
+
+@pytest.mark.parametrize("local_tz", ["Asia/Shanghai", "America/Los_Angeles"])
+def test_zones_resolve_from_system_dir_without_tzdata_wheel(tmp_path, local_tz):
+    """The image may ship only the OS zoneinfo tree (no ``tzdata`` wheel): both engines must
+    resolve ``CRON_TZ=``/``TZ=`` specs and a named ``$TZ`` from ``PYTHONTZPATH`` and agree,
+    including the flagship example's schedule (robfig ``CRON_TZ=``, SURVEY 3.3)."""
+    import json
+    import os
+    import shutil
+    import subprocess
+    import sys
+    from importlib import resources
+
+    src = resources.files("tzdata").joinpath("zoneinfo")
+    zdir = tmp_path / "zoneinfo"
+    shutil.copytree(str(src), zdir, ignore=shutil.ignore_patterns("__init__.py", "__pycache__"))
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    example = os.path.join(root, "examples/mi355x/cron-pytorch-ddp-mi355x.yaml")
+    env = dict(os.environ, PYTHONTZPATH=str(zdir), TZ=local_tz, PYTHONPATH=root)
+    r = subprocess.run([sys.executable, "-c", _NO_WHEEL_PROBE, example], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert "CRON_TZ=Asia/Shanghai 30 2 * * *" in out
+    for spec, (py, nat) in out.items():
+        assert py == nat, spec
+    # 02:30 Asia/Shanghai is 18:30 UTC the day before
+    first = out["CRON_TZ=Asia/Shanghai 30 2 * * *"][0][0][0]
+    assert GoTime(first, 0, UTC).rfc3339() == "2026-03-07T18:30:00Z"
+
+
+def test_zone_lookup_fails_cleanly_without_any_source(tmp_path):
+    """No wheel and no zoneinfo directory: both engines reject the zone the same way."""
+    import os
+    import subprocess
+    import sys
+
+    probe = r'''
+import sys
+sys.modules["tzdata"] = None
+from cron_operator_amd.cron.engine import NativeEngine, PythonEngine, ScheduleError
+for eng in (PythonEngine(), NativeEngine()):
+    try:
+        eng.parse("CRON_TZ=Asia/Shanghai 30 2 * * *")
+    except ScheduleError as e:
+        print("ERR", type(eng).__name__, e)
+    else:
+        print("OK", type(eng).__name__)
+'''
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONTZPATH=str(tmp_path / "empty"), PYTHONPATH=root)
+    env.pop("ZONEINFO", None)
+    r = subprocess.run([sys.executable, "-c", probe], env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = r.stdout.strip().splitlines()
+    assert len(lines) == 2 and all(x.startswith("ERR") for x in lines), lines
+    assert all("unknown time zone Asia/Shanghai" in x for x in lines), lines
