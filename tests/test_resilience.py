@@ -129,3 +129,80 @@ async def test_slow_child_sync_falls_back_to_live_list():
     assert len(jobs(env, MPI, "mpi")) == 1
     gate.set()
     await env.stop()
+
+
+# ---------------------------------------------------------------- leader election (client-go semantics)
+
+
+async def test_follower_clock_skew_cannot_steal_a_renewed_lease():
+    """A follower whose clock runs 30 s ahead never takes a lease the leader keeps renewing
+    (expiry is judged from *local* observation time, client-go ``observedTime``); once the
+    leader stops, the follower takes over after one lease duration of its own time."""
+    from cron_operator_amd.parallel.leaderelection import LEASES, LeaderElector
+    from cron_operator_amd.utils.clock import FakeClock
+
+    t0 = 1_800_000_000 * 10**9
+    ca, cb = FakeClock(t0), FakeClock(t0 + 30 * 10**9)
+    env = TestEnv(clock=ca)
+    a = LeaderElector(env.new_client(), "619a52b8.kubedl.io", NS, "a", ca, 15, 10, 2)
+    b = LeaderElector(env.new_client(), "619a52b8.kubedl.io", NS, "b", cb, 15, 10, 2)
+    assert await a.try_acquire_or_renew()
+    for _ in range(30):  # a minute of renewals every retryPeriod
+        ca.advance(2)
+        cb.advance(2)
+        assert await a.try_acquire_or_renew()
+        assert not await b.try_acquire_or_renew(), "skewed follower stole a live lease"
+    assert env.server.get(LEASES, NS, "619a52b8.kubedl.io")["spec"]["holderIdentity"] == "a"
+    # the leader dies; the follower keeps polling
+    took = None
+    for step in range(1, 15):
+        ca.advance(2)
+        cb.advance(2)
+        if await b.try_acquire_or_renew():
+            took = 2 * step
+            break
+    assert took is not None and 15 <= took <= 18, took
+    spec = env.server.get(LEASES, NS, "619a52b8.kubedl.io")["spec"]
+    assert spec["holderIdentity"] == "b" and spec["leaseTransitions"] == 1
+
+
+async def test_leader_steps_down_within_renew_deadline_when_lease_updates_hang():
+    """Lease PUTs hang (an apiserver that stopped answering): the leader must stop its
+    controllers within ``renewDeadline`` of the renewal that hangs -- not after the
+    transport's 60 s timeout -- so it never reconciles past its lease."""
+    from cron_operator_amd.parallel.leaderelection import LEASES
+    from cron_operator_amd.runtime.manager import LeaderElectionLost
+
+    env = TestEnv()
+    await env.create_cron(new_cron("pt", NS, "*/1 * * * *", PT_TMPL))
+    await env.start_manager(leader_election=True, leader_election_namespace=NS, leader_election_identity="me",
+                            lease_duration=15, renew_deadline=10, retry_period=2)
+    await env.settle()
+    assert env.manager.elector is not None and env.manager.elector.is_leader
+    for _ in range(10):  # healthy renewals
+        await env.advance(1)
+    renew_time = env.server.get(LEASES, NS, "619a52b8.kubedl.io")["spec"]["renewTime"]
+    hang = asyncio.Event()
+    orig_update = env.client.update
+
+    async def hung_update(target, obj, *a, **kw):
+        if target == LEASES:
+            await hang.wait()
+        return await orig_update(target, obj, *a, **kw)
+
+    env.client.update = hung_update  # type: ignore[assignment]
+    stopped_after = None
+    for sec in range(1, 30):
+        env.clock.advance(1)
+        for _ in range(20):
+            await asyncio.sleep(0)
+        if env._mgr_task.done():
+            stopped_after = sec
+            break
+    assert stopped_after is not None, "leader kept running with hung lease renewals"
+    # next renewal starts within retryPeriod (2 s), its window closes renewDeadline (10 s) later
+    assert stopped_after <= 2 + 10, stopped_after
+    assert isinstance(env._mgr_task.exception(), LeaderElectionLost)
+    assert not env.controller.started
+    assert env.server.get(LEASES, NS, "619a52b8.kubedl.io")["spec"]["renewTime"] == renew_time
+    hang.set()

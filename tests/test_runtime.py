@@ -325,7 +325,13 @@ async def test_leader_election_single_leader_and_failover():
     assert lease["spec"]["holderIdentity"] == "a" and lease["spec"]["leaseTransitions"] == 0
     clock.advance(10)
     assert await a.try_acquire_or_renew()  # renew
-    clock.advance(16)  # a stops renewing; lease expires
+    clock.advance(16)  # a stops renewing
+    # b last saw the record before a's renewal: it sees it change now, and its local
+    # expiry clock restarts (client-go observedTime), so the lease is still a's
+    assert not await b.try_acquire_or_renew()
+    clock.advance(14)
+    assert not await b.try_acquire_or_renew()
+    clock.advance(2)  # 16 s of local time without a change: expired
     assert await b.try_acquire_or_renew()
     lease = env.server.get(LEASES, "default", "619a52b8.kubedl.io")
     assert lease["spec"]["holderIdentity"] == "b" and lease["spec"]["leaseTransitions"] == 1
