@@ -775,6 +775,12 @@ class _WatchStream:
             return
         self.ended = True
         self.timer.cancel()
+        if self.watcher.stalled:  # a dead connection: nothing more reaches the client, not even the end
+            self.watcher.sink = None
+            self.watcher.stop()
+            if self.watcher in self.conn.app._streams:
+                self.conn.app._streams.remove(self.watcher)
+            return
         if self.flush_h is not None:
             self.flush_h.cancel()
         self.flush()  # what is pending goes out before the terminating chunk

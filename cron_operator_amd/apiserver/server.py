@@ -142,6 +142,9 @@ class Watcher:
         # straight to it instead of through the queue; ``None`` ends the stream
         self.sink: Optional[Callable[[Optional[Tuple[str, Dict[str, Any]]]], None]] = None
         self.closed = False
+        # a stalled stream stays open but delivers nothing more -- no events, no bookmarks,
+        # no end -- like a connection whose peer vanished without a FIN (fault injection)
+        self.stalled = False
         self.sent = 0
 
     def _in_scope(self, obj: Dict[str, Any]) -> bool:
@@ -173,6 +176,8 @@ class Watcher:
             self._put(etype, obj)
 
     def _put(self, etype: str, obj: Dict[str, Any]) -> None:
+        if self.stalled:
+            return
         self.sent += 1
         ev = (etype, jsonutil.deepcopy(obj) if self.copy_events else obj)
         if self.sink is not None:
@@ -181,7 +186,7 @@ class Watcher:
             self.queue.put_nowait(ev)
 
     def bookmark(self, rv: int) -> None:
-        if self.bookmarks and not self.closed:
+        if self.bookmarks and not self.closed and not self.stalled:
             ev = ("BOOKMARK", {"kind": self.info.kind, "apiVersion": self.info.api_version,
                                "metadata": {"resourceVersion": str(rv)}})
             if self.sink is not None:
@@ -906,6 +911,18 @@ class APIServer:
         for lst in self._watchers.values():
             for w in lst:
                 w.bookmark(self._rv)
+
+    def stall_watches(self, resource: Optional[str] = None) -> int:
+        """Silently stall the open watches (of one plural resource, or all): they deliver
+        nothing more and are never ended by the server.  Returns how many were stalled."""
+        n = 0
+        for (_, res), lst in self._watchers.items():
+            if resource is None or res == resource:
+                for w in lst:
+                    if not w.stalled:
+                        w.stalled = True
+                        n += 1
+        return n
 
     def close_all_watches(self) -> None:
         for lst in list(self._watchers.values()):

@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import asyncio
 import base64
+import socket as _socket
 import ssl as _ssl
 from collections import deque
 from typing import Deque, Dict, List, Optional, Tuple
@@ -358,6 +359,29 @@ class Stream:
         self._c.close()
 
 
+# TCP keepalive on every connection (Go's net.Dialer probes after 30 s idle): a peer that
+# vanished without a FIN -- node loss, a dropped NAT entry -- is detected in about a minute
+# instead of never on a long-lived watch connection
+KEEPALIVE_IDLE = 30
+KEEPALIVE_INTERVAL = 10
+KEEPALIVE_COUNT = 3
+
+
+def enable_keepalive(transport: Optional[asyncio.BaseTransport]) -> bool:
+    sock = transport.get_extra_info("socket") if transport is not None else None
+    if sock is None:
+        return False
+    try:
+        sock.setsockopt(_socket.SOL_SOCKET, _socket.SO_KEEPALIVE, 1)
+        for opt, val in (("TCP_KEEPIDLE", KEEPALIVE_IDLE), ("TCP_KEEPINTVL", KEEPALIVE_INTERVAL),
+                         ("TCP_KEEPCNT", KEEPALIVE_COUNT)):
+            if hasattr(_socket, opt):
+                sock.setsockopt(_socket.IPPROTO_TCP, getattr(_socket, opt), val)
+    except OSError:
+        return False
+    return True
+
+
 def _expire(fut: asyncio.Future) -> None:
     if not fut.done():
         fut.set_exception(asyncio.TimeoutError())
@@ -451,9 +475,11 @@ class HttpPool:
                 kw["ssl"] = self.ssl
                 kw["server_hostname"] = self.server_hostname or self.host
             host, port = self._proxy or (self.host, self.port)
-            _, proto = await asyncio.wait_for(loop.create_connection(factory, host, port, **kw), self.timeout)
+            tr, proto = await asyncio.wait_for(loop.create_connection(factory, host, port, **kw), self.timeout)
+            enable_keepalive(tr)
             return proto
         transport, tun = await asyncio.wait_for(loop.create_connection(_Tunnel, *self._proxy), self.timeout)
+        enable_keepalive(transport)
         authority = f"{self.host}:{self.port}" if ":" not in self.host else f"[{self.host}]:{self.port}"
         transport.write(f"CONNECT {authority} HTTP/1.1\r\nHost: {authority}\r\n{self._proxy_auth}\r\n"
                         .encode("latin-1"))

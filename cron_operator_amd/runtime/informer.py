@@ -13,6 +13,13 @@ the list's resourceVersion; a closed watch resumes from the last seen version;
 410 Expired triggers a relist whose diff is replayed as add/update/delete
 events.  Objects in the store are read-only snapshots.
 
+Watch liveness: every WATCH carries a random ``timeoutSeconds`` in [300, 600)
+as client-go's reflector sends, and a watchdog drops a stream that delivered
+nothing -- no event, no BOOKMARK -- for ``watch_idle_timeout`` seconds (a
+half-open connection after a silent network drop); the reflector then resumes
+from the last resourceVersion, relisting on 410.  The HTTP transport also enables
+TCP keepalive on its connections.
+
 Periodic resync (controller-runtime's ``SyncPeriod``, default 10 h with up to
 10% jitter): every object in the store is re-delivered to the handlers as an
 update whose old and new object are the same, so every Cron is reconciled at
@@ -35,6 +42,13 @@ from .client import Client
 IndexFunc = Callable[[Dict[str, Any]], List[str]]
 
 NAMESPACE_INDEX = "namespace"
+
+# client-go reflector: each WATCH carries timeoutSeconds in [5 min, 10 min)
+MIN_WATCH_TIMEOUT = 300.0
+# no event and no BOOKMARK for this long (apiservers send a bookmark about once a
+# minute to watches that allow them): the connection is presumed dead
+WATCH_IDLE_TIMEOUT = 150.0
+WATCH_TIMEOUT_GRACE = 30
 
 
 def obj_key(obj: Dict[str, Any]) -> str:
@@ -93,8 +107,19 @@ class Informer:
     def __init__(self, client: Client, target: Any, namespace: str = "", label_selector: Optional[str] = None,
                  field_selector: Optional[str] = None, indexers: Optional[Dict[str, IndexFunc]] = None,
                  page_size: int = 500, name: str = "", resync_period: float = 0.0,
-                 clock: Optional[Clock] = None, transform: Optional[Transform] = None):
+                 clock: Optional[Clock] = None, transform: Optional[Transform] = None,
+                 min_watch_timeout: float = MIN_WATCH_TIMEOUT, watch_idle_timeout: float = WATCH_IDLE_TIMEOUT):
         self.client = client
+        # watch liveness: every WATCH asks the server to end it after a random
+        # [min, 2*min) seconds (client-go reflector), and a watch silent for
+        # ``watch_idle_timeout`` seconds -- no event and no bookmark -- is dropped and
+        # re-established from the last resourceVersion (a half-open connection)
+        self.min_watch_timeout = min_watch_timeout
+        self.watch_idle_timeout = watch_idle_timeout
+        self.idle_timeouts = 0
+        self._last_item = 0.0
+        self._idle_limit = 0.0
+        self._watchdog: Optional[asyncio.TimerHandle] = None
         self.transform = transform
         self.resync_period = resync_period
         self.clock = clock
@@ -292,17 +317,26 @@ class Informer:
                 if need_list:
                     await self._list()
                     need_list = False
+                timeout_s = int(self.min_watch_timeout * (1.0 + random.random())) \
+                    if self.min_watch_timeout > 0 else None
                 self._watch = await self.client.watch(self.target, self.namespace, self.last_rv,
-                                                      self.label_selector, self.field_selector)
-                async for etype, obj in self._watch:
-                    if etype == "ERROR":
-                        st = errors.ApiError.from_status(int(obj.get("code") or 500), obj)
-                        raise st
-                    rv = (obj.get("metadata") or {}).get("resourceVersion")
-                    if etype != "BOOKMARK":
-                        self._apply(etype, obj)
-                    if rv:
-                        self.last_rv = rv
+                                                      self.label_selector, self.field_selector,
+                                                      timeout_seconds=timeout_s)
+                self._arm_watchdog(timeout_s)
+                loop = asyncio.get_running_loop()
+                try:
+                    async for etype, obj in self._watch:
+                        self._last_item = loop.time()
+                        if etype == "ERROR":
+                            st = errors.ApiError.from_status(int(obj.get("code") or 500), obj)
+                            raise st
+                        rv = (obj.get("metadata") or {}).get("resourceVersion")
+                        if etype != "BOOKMARK":
+                            self._apply(etype, obj)
+                        if rv:
+                            self.last_rv = rv
+                finally:
+                    self._disarm_watchdog()
                 backoff = 0.1
             except asyncio.CancelledError:
                 raise
@@ -324,6 +358,41 @@ class Informer:
                 await asyncio.sleep(backoff * (1 + random.random()))
                 backoff = min(backoff * 2, 30.0)
 
+    # ------------------------------------------------------------------ watch liveness
+    def _arm_watchdog(self, timeout_s: Optional[int]) -> None:
+        idle = self.watch_idle_timeout
+        if timeout_s:
+            # the server should have ended the watch by then: a grace period past it is dead
+            idle = min(idle, timeout_s + WATCH_TIMEOUT_GRACE) if idle > 0 else timeout_s + WATCH_TIMEOUT_GRACE
+        if idle <= 0:
+            return
+        loop = asyncio.get_running_loop()
+        self._idle_limit = idle
+        self._last_item = loop.time()
+        self._watchdog = loop.call_later(idle, self._check_idle)
+
+    def _disarm_watchdog(self) -> None:
+        if self._watchdog is not None:
+            self._watchdog.cancel()
+            self._watchdog = None
+
+    def _check_idle(self) -> None:
+        self._watchdog = None
+        w = self._watch
+        if w is None or self._stopped:
+            return
+        loop = asyncio.get_running_loop()
+        quiet = loop.time() - self._last_item
+        if quiet < self._idle_limit:
+            self._watchdog = loop.call_later(self._idle_limit - quiet, self._check_idle)
+            return
+        self.idle_timeouts += 1
+        self.log.info("watch silent, re-establishing it", seconds=round(quiet, 1))
+        try:
+            w.stop()
+        except Exception:  # noqa: BLE001 - the stream is being dropped anyway
+            pass
+
     def start(self) -> asyncio.Task:
         if self._task is None:
             self._task = asyncio.get_running_loop().create_task(self.run(), name=f"informer:{self.name}")
@@ -332,6 +401,7 @@ class Informer:
 
     async def stop(self) -> None:
         self._stopped = True
+        self._disarm_watchdog()
         if self._resync_timer is not None:
             self._resync_timer.cancel()
             self._resync_timer = None
@@ -352,8 +422,11 @@ class Cache:
     """Shared informers keyed by (resource, namespace, selector) -- ``cache.Cache``."""
 
     def __init__(self, client: Client, namespace: str = "", resync_period: float = 0.0,
-                 clock: Optional[Clock] = None):
+                 clock: Optional[Clock] = None, min_watch_timeout: float = MIN_WATCH_TIMEOUT,
+                 watch_idle_timeout: float = WATCH_IDLE_TIMEOUT):
         self.client = client
+        self.min_watch_timeout = min_watch_timeout
+        self.watch_idle_timeout = watch_idle_timeout
         self.namespace = namespace
         self.resync_period = resync_period
         self.clock = clock
@@ -376,7 +449,8 @@ class Cache:
         if inf is None:
             inf = Informer(self.client, gvr, self.namespace, label_selector, indexers=indexers,
                            name=f"{gvr.resource}.{gvr.group}" if gvr.group else gvr.resource,
-                           resync_period=self.resync_period, clock=self.clock, transform=transform)
+                           resync_period=self.resync_period, clock=self.clock, transform=transform,
+                           min_watch_timeout=self.min_watch_timeout, watch_idle_timeout=self.watch_idle_timeout)
             self._informers[key] = inf
             if self._started:
                 inf.start()

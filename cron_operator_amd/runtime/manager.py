@@ -24,7 +24,7 @@ from ..utils.logging import get_logger
 from .client import Client
 from .controller import Controller
 from .events import Broadcaster, Recorder
-from .informer import Cache
+from .informer import WATCH_IDLE_TIMEOUT, Cache
 from .servers import Check, MetricsServer, ProbeServer, ping
 
 DEFAULT_LEADER_ELECTION_ID = "619a52b8.kubedl.io"
@@ -64,6 +64,9 @@ class ManagerOptions:
     # "hash": every shard watches everything and drops other shards' keys; "labels": objects carry
     # kubedl.io/shard and each shard's informers select on it (controller/sharding.py)
     shard_routing: str = "hash"
+    # informer watch liveness (runtime/informer.py): seconds without an event or bookmark
+    # before a watch is presumed dead and re-established
+    watch_idle_timeout: float = WATCH_IDLE_TIMEOUT
 
 
 class Manager:
@@ -71,7 +74,8 @@ class Manager:
         self.client = client
         self.opts = options or ManagerOptions()
         self.clock = self.opts.clock
-        self.cache = Cache(client, self.opts.namespace, self.opts.sync_period, self.clock)
+        self.cache = Cache(client, self.opts.namespace, self.opts.sync_period, self.clock,
+                           watch_idle_timeout=self.opts.watch_idle_timeout)
         self.broadcaster = Broadcaster(client, self.clock)
         self.controllers: List[Controller] = []
         self.runnables: List[Callable[[], Awaitable[None]]] = []

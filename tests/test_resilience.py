@@ -206,3 +206,97 @@ async def test_leader_steps_down_within_renew_deadline_when_lease_updates_hang()
     assert not env.controller.started
     assert env.server.get(LEASES, NS, "619a52b8.kubedl.io")["spec"]["renewTime"] == renew_time
     hang.set()
+
+
+# ---------------------------------------------------------------- watch liveness
+
+
+async def test_silently_stalled_child_watch_is_reestablished_and_cron_converges():
+    """The apiserver stops writing to the PyTorchJob watch without closing it (a half-open
+    connection).  A Forbid Cron's running job then finishes: the operator cannot see it
+    until the idle watchdog drops the silent stream and resumes the watch -- after which
+    the job's completion arrives and the next tick fires."""
+    from cron_operator_amd.trainingop.operator import finished_status
+    from cron_operator_amd.utils.gotime import NANOS, UTC, GoTime
+
+    env = TestEnv()
+    await env.create_cron(new_cron("pt", NS, "*/1 * * * *", PT_TMPL, concurrency_policy="Forbid"))
+    await env.start_manager(watch_idle_timeout=0.3)
+    await env.settle()
+    for _ in range(60):
+        await env.advance(1)
+    assert len(jobs(env, PT, "pt")) == 1
+    inf = next(i for g, i in env.reconciler.child_informers.items() if g.kind == "PyTorchJob")
+    assert env.server.stall_watches("pytorchjobs") >= 1
+    job = jobs(env, PT, "pt")[0]
+    ts = GoTime(env.clock.now_ns() // NANOS, 0, UTC).rfc3339()
+    env.server.patch(PT, NS, job, {"status": finished_status("PyTorchJob", job, ts, True)}, "merge", "status")
+    for _ in range(60):  # next tick: the operator still believes the job runs (Forbid)
+        await env.advance(1)
+    assert len(jobs(env, PT, "pt")) == 1
+    # real time passes: the watchdog notices the silence and the watch resumes
+    for _ in range(100):
+        await asyncio.sleep(0.05)
+        if inf.idle_timeouts:
+            break
+    assert inf.idle_timeouts >= 1
+    await env.settle()
+    for _ in range(60):
+        await env.advance(1)
+    assert len(jobs(env, PT, "pt")) == 2, "Cron did not converge after the watch was re-established"
+    st = env.server.get(CRON_GVR, NS, "pt")["status"]
+    assert [h["object"]["name"] for h in st.get("history") or []] == [job]
+    await env.stop()
+
+
+async def test_http_watch_carries_timeout_and_survives_a_silent_connection():
+    """Over real HTTP: the informer's WATCH asks for ``timeoutSeconds`` in [300, 600), and a
+    stream the server stops writing to (no FIN, no terminating chunk) is replaced; an
+    object created meanwhile reaches the cache.  Connections have TCP keepalive on."""
+    import socket
+
+    from cron_operator_amd.apiserver.http import APIServerApp
+    from cron_operator_amd.runtime.client import Client
+    from cron_operator_amd.runtime.http import HttpTransport
+    from cron_operator_amd.runtime.informer import Informer
+    from cron_operator_amd.runtime.kubeconfig import RestConfig
+
+    CM = GroupVersionResource("", "v1", "configmaps")
+    env = TestEnv()
+    app = APIServerApp(env.server)
+    port = await app.start("127.0.0.1", 0)
+    client = Client(HttpTransport(RestConfig(host=f"http://127.0.0.1:{port}")), qps=-1)
+    seen_params = []
+    orig_watch = client.transport.watch
+
+    async def spy_watch(gvr, namespace="", params=None):
+        seen_params.append(dict(params or {}))
+        return await orig_watch(gvr, namespace, params)
+
+    client.transport.watch = spy_watch  # type: ignore[assignment]
+    inf = Informer(client, CM, NS, watch_idle_timeout=0.4)
+    try:
+        inf.start()
+        await asyncio.wait_for(inf.synced.wait(), 10)
+        for _ in range(50):
+            await asyncio.sleep(0.01)
+            if seen_params:
+                break
+        assert seen_params and 300 <= int(seen_params[0]["timeoutSeconds"]) < 600
+        stream = inf._watch._s._c  # the dedicated watch connection
+        sock = stream.transport.get_extra_info("socket")
+        assert sock.getsockopt(socket.SOL_SOCKET, socket.SO_KEEPALIVE) == 1
+        assert env.server.stall_watches("configmaps") == 1
+        env.server.create(CM, NS, {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "late"}})
+        await asyncio.sleep(0.1)
+        assert inf.get(NS, "late") is None  # the stalled stream delivered nothing
+        for _ in range(200):
+            await asyncio.sleep(0.02)
+            if inf.get(NS, "late") is not None:
+                break
+        assert inf.get(NS, "late") is not None
+        assert inf.idle_timeouts >= 1 and len(seen_params) >= 2
+    finally:
+        await inf.stop()
+        await client.close()
+        await app.stop()
