@@ -19,11 +19,18 @@ shard watch only its own Crons and children (``kubedl.io/shard`` labels, assigne
 by the shards during setup); ``hash`` has every shard watch everything.
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
-it runs under ``torch.distributed.run`` with one rank per GPU.  The operator is
+it runs under ``torch.distributed.run`` with one rank per GPU (without a launcher,
+``--gpus N`` spawns the N rank processes itself).  The operator is
 pure control plane, so ranks do not use the GPU: each
 rank is one operator shard (its own apiserver process and 1000 Crons, weak
 scaling) and rank 0 reports the whole-job aggregate.  Ranks synchronise with
 gloo barriers; there is no device work to ``torch.cuda.synchronize()``.
+
+``vs_baseline``: the reference publishes no numbers, so the denominator
+is the reference *algorithm* (``--mode reference``: live LIST per reconcile, status
+churn, no event filtering) run by this same invocation on the same Crons, after the
+timed run.  ``operator_cpu_ms_per_fire`` and ``apiserver_busy_frac`` show how much of
+the headline is the operator and how much the fake apiserver fixture.
 
 Prints ONE JSON line on rank 0.
 """
@@ -40,11 +47,34 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 # BASELINE.md row "Reference algorithm, measured in this harness" (cron-reconciles/s @1000 Crons,
-# `--mode reference` in the same harness + fake apiserver, MI355X box).  Re-measured whenever the
-# harness/apiserver changes (the reference's live LISTs load the apiserver); the HIGHEST same-harness
-# measurement is kept so vs_baseline is conservative: r1i 80.7 (profiles/shard_sweep_mi355x_box_r1i.json;
-# other runs: 42.8-79.5, incl. the reference algorithm on 2 shards, 69.7-74.6).
-BASELINE_VALUE = 80.72
+# `--mode reference`, MI355X box, r1i: profiles/shard_sweep_mi355x_box_r1i.json).  Only used with
+# `--baseline recorded`; by default the denominator is measured in the same invocation (below).
+RECORDED_BASELINE_VALUE = 80.72
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawn_ranks(n: int) -> int:
+    """``--gpus N`` without a launcher: start N rank processes of this script (gloo rendezvous on
+    127.0.0.1) and exit with the worst exit code.  Nothing here touches the GPU, so child
+    processes are started, never exec'd.  Only rank 0 prints the JSON line."""
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    return bad[0] if bad else 0
 
 
 def _dist():
@@ -91,10 +121,24 @@ def main() -> int:
                     help="how shards split the watch traffic (controller/sharding.py)")
     ap.add_argument("--apiserver-latency", choices=["none", "etcd"], default="none",
                     help="server-side per-verb latency model of the fake apiserver (harness LATENCY_PROFILES)")
+    ap.add_argument("--baseline", choices=["measure", "recorded", "none"], default="measure",
+                    help="vs_baseline denominator: 'measure' runs the reference algorithm (--mode reference, "
+                         "one operator process, same Crons) in this same invocation after the timed run; "
+                         "'recorded' divides by the BASELINE.md figure")
+    ap.add_argument("--baseline-steps", type=int, default=2)
+    ap.add_argument("--baseline-warmup", type=int, default=1)
     ap.add_argument("--out", default="", help="also write the full result JSON here")
     a = ap.parse_args()
 
+    if a.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return _spawn_ranks(a.gpus)
     dist, rank, world = _dist()
+    if world != a.gpus:
+        print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}; refusing to report n_gpus={a.gpus}",
+              file=sys.stderr)
+        return 2
     from cron_operator_amd.bench.harness import BenchConfig, run_sync
 
     cfg = BenchConfig(n_crons=a.crons, steps=a.steps, warmup=a.warmup, history_limit=a.history_limit,
@@ -118,7 +162,21 @@ def main() -> int:
 
     mine = {"elapsed_s": res.elapsed_s, "fires": cfg.n_crons * cfg.steps,
             "reconciles": res.raw_reconciles_per_s * res.elapsed_s, "p50": res.p50_latency_ms,
-            "p99": res.p99_latency_ms, "req_per_fire": res.api_requests_per_fire}
+            "p99": res.p99_latency_ms, "req_per_fire": res.api_requests_per_fire,
+            "cpu_op": res.cpu_s_operator, "cpu_api": res.cpu_s_apiserver}
+
+    # the denominator: the reference algorithm on the same Crons, same box, same invocation
+    # (untimed for the headline; one operator process, as the reference is one controller)
+    if a.baseline == "measure":
+        bcfg = BenchConfig(n_crons=a.crons, steps=a.baseline_steps, warmup=a.baseline_warmup,
+                           history_limit=a.history_limit, mode="reference", transport=a.transport, qps=a.qps,
+                           burst=a.burst, workers=a.workers, namespace=f"bench-ref-r{rank}", shards=1)
+        _barrier(dist)
+        bres = run_sync(bcfg)
+        _barrier(dist)
+        mine["ref_elapsed_s"] = bres.elapsed_s
+        mine["ref_fires"] = bcfg.n_crons * bcfg.steps
+        mine["ref_p50"] = bres.p50_latency_ms
     if dist is not None:
         allr = [None] * world
         dist.all_gather_object(allr, mine)
@@ -128,6 +186,14 @@ def main() -> int:
         t_max = max(r["elapsed_s"] for r in allr)  # timed region: max over ranks
         fires = sum(r["fires"] for r in allr)
         value = fires / t_max
+        if a.baseline == "measure":
+            base_value = sum(r["ref_fires"] for r in allr) / max(r["ref_elapsed_s"] for r in allr)
+            base_src = (f"measured: reference algorithm (--mode reference, 1 process/rank), {a.baseline_steps} "
+                        f"timed ticks, this invocation")
+        elif a.baseline == "recorded":
+            base_value, base_src = RECORDED_BASELINE_VALUE * world, "recorded: BASELINE.md r1i x ranks"
+        else:
+            base_value, base_src = None, "none"
         out = {
             "metric": "reconciles/sec + p50 schedule→create latency @1000 Cron CRs",
             "value": round(value, 2),
@@ -138,7 +204,7 @@ def main() -> int:
             "ms_per_step": round(t_max * 1000 / a.steps, 2),
             "higher_is_better": True,
             "scaling": "weak",
-            "vs_baseline": round(value / BASELINE_VALUE, 3) if BASELINE_VALUE else None,
+            "vs_baseline": round(value / base_value, 3) if base_value else None,
             "dtype": "n/a (control plane; no tensor compute)",
             "data": "synthetic: 1000 random-free Cron CRs (* * * * *, historyLimit=10) + PyTorchJob children on a "
                     "fake apiserver process per rank",
@@ -155,6 +221,14 @@ def main() -> int:
             "p99_schedule_to_create_ms": round(max(r["p99"] for r in allr), 2),
             "raw_reconciles_per_s": round(sum(r["reconciles"] for r in allr) / t_max, 2),
             "api_requests_per_fire": round(sum(r["req_per_fire"] for r in allr) / len(allr), 3),
+            # operator-side cost (all shard processes), the number to track rather than the
+            # fake apiserver's speed; and how busy that fixture was (CPU s / wall s, max rank)
+            "operator_cpu_ms_per_fire": round(sum(r["cpu_op"] for r in allr) * 1000 / fires, 4),
+            "apiserver_busy_frac": round(max(r["cpu_api"] / r["elapsed_s"] for r in allr), 3),
+            "baseline_value": round(base_value, 2) if base_value else None,
+            "baseline_source": base_src,
+            "baseline_p50_schedule_to_create_ms": round(max(r["ref_p50"] for r in allr), 2)
+            if a.baseline == "measure" else None,
             "cron_engine": res.engine,
             "wall_s": round(wall, 2),
         }

@@ -1,4 +1,6 @@
-"""bench.py driver contract: one JSON line with the required keys, 1 rank and 2 ranks (gloo)."""
+"""bench.py driver contract: one JSON line with the required keys, 1 rank and 2 ranks (gloo),
+launched by torch.distributed.run or spawned by bench.py itself; operator-cost keys; a
+vs_baseline denominator measured in the same invocation."""
 from __future__ import annotations
 
 import json
@@ -35,6 +37,44 @@ def test_single_rank_line():
     assert d["value"] > 0 and d["config"]["global_batch"] == 20 and d["scaling"] == "weak"
     assert d["config"]["operator_shards"] == 3 and d["config"]["shard_routing"] == "labels"
     assert abs(d["value"] - 20 * 2 / (d["ms_per_step"] * 2 / 1000)) / d["value"] < 0.01
+    # operator cost, separated from the fake apiserver fixture
+    assert d["operator_cpu_ms_per_fire"] > 0
+    assert 0 < d["apiserver_busy_frac"] < 2
+    # the denominator is the reference algorithm measured by this same invocation
+    assert d["baseline_source"].startswith("measured")
+    assert d["baseline_value"] > 0 and d["baseline_p50_schedule_to_create_ms"] > 0
+    assert abs(d["vs_baseline"] - d["value"] / d["baseline_value"]) < 0.01 * d["vs_baseline"] + 0.002
+
+
+def test_recorded_baseline_option():
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "1", "--warmup", "1", "--crons", "10", "--shards", "1",
+                        "--baseline", "recorded"], cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _json_line(r.stdout)
+    assert d["baseline_value"] == 80.72 and d["baseline_source"].startswith("recorded")
+
+
+def test_gpus_without_launcher_spawns_ranks():
+    """``--gpus 2`` with no WORLD_SIZE: bench.py starts both ranks itself; one line, 2 ranks' work."""
+    env = _env()
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "2", "--warmup", "1", "--crons", "20",
+                        "--baseline", "none"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 40 and d["config"]["parallelism"] == "ranks2x3shards"
+    assert d["vs_baseline"] is None
+
+
+def test_gpus_mismatching_world_size_is_refused():
+    env = _env()
+    env["WORLD_SIZE"] = "1"
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0", "--crons", "5"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert "refusing" in r.stderr
 
 
 def test_two_ranks_aggregate():
