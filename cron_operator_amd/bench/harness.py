@@ -183,6 +183,65 @@ class _RemoteServer:
                 self.proc.wait()
 
 
+class SettleTracker:
+    """The owned Crons whose status has not reached the current phase's target yet.
+
+    An informer handler re-evaluates one Cron per event (O(1)), so waiting for a
+    step to settle is a counter check instead of a scan of every Cron on each poll --
+    a scan that ran inside the operator's process and event loop every 2 ms and made
+    the harness itself cost O(N) per poll."""
+
+    def __init__(self, informer, keys: Optional[List[str]] = None):
+        from ..runtime.informer import EventHandler
+
+        self.inf = informer
+        self.keys = set(keys) if keys is not None else None
+        self.pred = None
+        self.pending: set = set()
+        informer.add_handler(EventHandler(on_add=self._on, on_update=lambda old, new: self._on(new)))
+
+    def _on(self, obj: Dict[str, Any]) -> None:
+        if self.pred is None:
+            return
+        from ..runtime.informer import obj_key
+
+        k = obj_key(obj)
+        if self.keys is not None and k not in self.keys:
+            return
+        if self.pred(obj):
+            self.pending.discard(k)
+        else:
+            self.pending.add(k)
+
+    def begin(self, pred) -> None:
+        self.pred = pred
+        self.pending = {k for k, o in self.inf.store.items()
+                        if (self.keys is None or k in self.keys) and not pred(o)}
+        if self.keys is not None:
+            self.pending |= {k for k in self.keys if k not in self.inf.store}
+
+
+def fired_pred(tick_ns: int, want_hist: int):
+    """Status of a Cron that ran tick ``tick_ns``: one active job, ``want_hist`` in history."""
+    from ..utils.gotime import UTC, GoTime
+
+    want_ts = GoTime(tick_ns // NANOS, 0, UTC).rfc3339()
+
+    def pred(obj: Dict[str, Any]) -> bool:
+        st = obj.get("status") or {}
+        return st.get("lastScheduleTime") == want_ts and len(st.get("active") or ()) == 1 and \
+            len(st.get("history") or ()) == want_hist
+    return pred
+
+
+def completed_pred(want_hist: int):
+    """Status of a Cron whose job finished: nothing active, ``want_hist`` in history (GC done)."""
+    def pred(obj: Dict[str, Any]) -> bool:
+        st = obj.get("status") or {}
+        return not st.get("active") and len(st.get("history") or ()) == want_hist
+    return pred
+
+
 def _cpu_times(remote: Optional["_RemoteServer"]) -> "tuple[float, float]":
     """(operator process CPU s, apiserver process CPU s) -- the apiserver shares our process in memory mode."""
     me = time.process_time()
@@ -332,43 +391,29 @@ async def run(cfg: BenchConfig, on_step=None) -> BenchResult:
 
         rec.latency_observer = on_create
 
+        tracker = SettleTracker(cron_inf)
+
         async def wait_settled(tick_ns: int, k: int, deadline: float) -> None:
             """Every Cron reflects tick k and the queue is idle."""
-            from ..utils.gotime import UTC, GoTime
-
-            want_ts = GoTime(tick_ns // NANOS, 0, UTC).rfc3339()
             want_hist = cfg.history_limit if cfg.seed_history else min(k - 1, cfg.history_limit)
+            tracker.begin(fired_pred(tick_ns, want_hist))
             while True:
                 if time.monotonic() > deadline:
                     raise TimeoutError(f"step {k} did not settle (creates={creates_this_tick[0]})")
-                if creates_this_tick[0] >= cfg.n_crons and ctrl.queue.idle():
-                    ok = True
-                    for obj in cron_inf.store.values():
-                        st = obj.get("status") or {}
-                        if st.get("lastScheduleTime") != want_ts or len(st.get("active") or ()) != 1 or \
-                                len(st.get("history") or ()) != want_hist:
-                            ok = False
-                            break
-                    if ok and ctrl.queue.idle():
-                        return
+                if creates_this_tick[0] >= cfg.n_crons and not tracker.pending and ctrl.queue.idle():
+                    return
                 await asyncio.sleep(0.002)
 
         want_hist = cfg.history_limit
 
         async def wait_completed(deadline: float) -> None:
             """Every Cron moved its finished job into history (and GC'd the overflow)."""
+            tracker.begin(completed_pred(want_hist))
             while True:
                 if time.monotonic() > deadline:
                     raise TimeoutError("completion phase did not settle")
-                if ctrl.queue.idle():
-                    ok = True
-                    for obj in cron_inf.store.values():
-                        st = obj.get("status") or {}
-                        if st.get("active") or len(st.get("history") or ()) != want_hist:
-                            ok = False
-                            break
-                    if ok and ctrl.queue.idle():
-                        return
+                if not tracker.pending and ctrl.queue.idle():
+                    return
                 await asyncio.sleep(0.002)
 
         await ctrl.wait_idle(timeout=120)

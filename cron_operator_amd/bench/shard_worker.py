@@ -26,7 +26,7 @@ import os
 import resource
 import sys
 import time
-from typing import Any, Dict, List
+from typing import List
 
 
 async def main() -> int:
@@ -53,7 +53,6 @@ async def main() -> int:
     from ..runtime.kubeconfig import RestConfig
     from ..runtime.manager import Manager, ManagerOptions
     from ..utils.clock import FakeClock
-    from ..utils.gotime import NANOS, UTC, GoTime
     from ..utils.logging import new_from_options, set_logger
 
     set_logger(new_from_options(encoder="json", level="error", stream=open(os.devnull, "w")))
@@ -82,10 +81,9 @@ async def main() -> int:
         await asyncio.sleep(0.05)
     await ctrl.wait_idle(timeout=120)
 
-    def owned() -> List[Dict[str, Any]]:
-        store = cron_inf.store
-        return [store[k] for k in owned_keys if k in store]
+    from .harness import SettleTracker, completed_pred, fired_pred
 
+    tracker = SettleTracker(cron_inf, owned_keys)
     n_owned = len(owned_keys)
     lat: List[float] = []
     tick_wall = [0.0]
@@ -105,23 +103,11 @@ async def main() -> int:
     await loop.connect_read_pipe(lambda: asyncio.StreamReaderProtocol(reader), sys.stdin)
 
     async def settled(phase: str, tick_ns: int) -> None:
-        want_hist = a.history_limit
-        want_ts = GoTime(tick_ns // NANOS, 0, UTC).rfc3339()
+        tracker.begin(completed_pred(a.history_limit) if phase == "completion"
+                      else fired_pred(tick_ns, a.history_limit))
         while True:
-            if ctrl.queue.idle() and (phase == "completion" or creates[0] >= n_owned):
-                ok = True
-                for obj in owned():
-                    st = obj.get("status") or {}
-                    if phase == "completion":
-                        if st.get("active") or len(st.get("history") or ()) != want_hist:
-                            ok = False
-                            break
-                    elif st.get("lastScheduleTime") != want_ts or len(st.get("active") or ()) != 1 or \
-                            len(st.get("history") or ()) != want_hist:
-                        ok = False
-                        break
-                if ok and ctrl.queue.idle():
-                    return
+            if (phase == "completion" or creates[0] >= n_owned) and not tracker.pending and ctrl.queue.idle():
+                return
             await asyncio.sleep(0.002)
 
     prof = None
