@@ -20,11 +20,21 @@ timeout -k 10 600 python -u -m pytest tests/ -m gpu -x -v --timeout 300 --timeou
     > "$OUT/gpu_tests.log" 2>&1
 rc=$?; echo "tests rc=$rc"; tail -3 "$OUT/gpu_tests.log"; fatal $rc tests
 
-for v in "" "--shards 1" "--shards 4"; do
+# the driver's invocation (reference baseline measured in the same run), then shard variants
+timeout -k 10 900 python bench.py --gpus 1 --steps 20 --warmup 5 --out "$OUT/bench_driver.json" \
+    > "$OUT/bench_driver.log" 2>&1
+rc=$?; echo "bench driver-shape rc=$rc"; tail -1 "$OUT/bench_driver.log" | cut -c1-400; fatal $rc "bench driver"
+for v in "--shards 1" "--shards 4"; do
   name=$(echo "default$v" | tr -d ' -' )
-  timeout -k 10 600 python bench.py --steps 5 --warmup 2 $v --out "$OUT/bench_$name.json" > "$OUT/bench_$name.log" 2>&1
+  timeout -k 10 600 python bench.py --steps 5 --warmup 2 --baseline none $v --out "$OUT/bench_$name.json" \
+      > "$OUT/bench_$name.log" 2>&1
   rc=$?; echo "bench $v rc=$rc"; tail -1 "$OUT/bench_$name.log" | cut -c1-200; fatal $rc "bench $v"
 done
+
+echo "== per-process scaling 100 vs 1000 $(date)"
+timeout -k 10 600 python scripts/bench_scale.py --sizes 100,1000 --modes optimized --steps 5 --warmup 2 \
+    --out "$OUT/scale_1proc.json" > "$OUT/scale_1proc.log" 2>&1
+rc=$?; echo "scale rc=$rc"; tail -6 "$OUT/scale_1proc.log"; fatal $rc scale
 
 echo "== smoke $(date)"
 timeout -k 10 600 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1

@@ -108,8 +108,10 @@ def test_ddp_cron_suspend_resume_cycle_on_gpu(gpu):
 
 
 def test_headline_bench_short_run():
-    out = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--crons", "300"],
+    out = subprocess.run([sys.executable, "bench.py", "--steps", "2", "--warmup", "1", "--crons", "300",
+                          "--baseline-steps", "1"],
                          capture_output=True, text=True, timeout=900, env=_env(), cwd=ROOT)
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
     res = json.loads(out.stdout.strip().splitlines()[-1])
     assert res["value"] > 0 and res["cron_engine"] == "native"
+    assert res["baseline_source"].startswith("measured") and res["vs_baseline"] > 1
