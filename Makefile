@@ -120,6 +120,10 @@ docker-buildx: ## Multi-arch build and push.
 build-installer: manifests ## Render deploy/kustomize/default into dist/install.yaml.
 	$(PYTHON) -m cron_operator_amd kustomize deploy/kustomize/default -o dist/install.yaml
 
+.PHONY: build-installer-certs
+build-installer-certs: manifests ## Render deploy/kustomize/default with cert-manager metrics TLS, ServiceMonitor and network policy into dist/install-certs.yaml.
+	$(PYTHON) -m cron_operator_amd kustomize --enable-optional deploy/kustomize/default -o dist/install-certs.yaml
+
 ##@ Helm
 
 .PHONY: helm-unittest

@@ -166,6 +166,9 @@ def build_parser() -> argparse.ArgumentParser:
     kz = sub.add_parser("kustomize", help="Render a kustomization directory (kustomize build)")
     kz.add_argument("dir", nargs="?", default="deploy/kustomize/default")
     kz.add_argument("-o", "--output", default="", help="Write here instead of stdout (e.g. dist/install.yaml).")
+    kz.add_argument("--enable-optional", action="store_true",
+                    help="Render with every commented-out optional section enabled (cert-manager metrics "
+                         "certificate, ServiceMonitor with TLS verification, network policy)")
     hm = sub.add_parser("helm-template", help="Render the Helm chart (helm template)")
     hm.add_argument("chart", nargs="?", default="charts/cron-operator")
     hm.add_argument("--release", default="cron-operator")
@@ -455,9 +458,15 @@ def main(argv: Optional[List[str]] = None) -> int:
     if a.command == "get":
         return asyncio.run(run_get(a))
     if a.command == "kustomize":
-        from ..utils.kustomize import build_yaml
+        from ..utils.kustomize import build_yaml, enable_optional
 
-        out = build_yaml(a.dir)
+        if a.enable_optional:
+            import tempfile
+
+            with tempfile.TemporaryDirectory() as tmp:
+                out = build_yaml(enable_optional(a.dir, os.path.join(tmp, "tree")))
+        else:
+            out = build_yaml(a.dir)
         if a.output:
             os.makedirs(os.path.dirname(a.output) or ".", exist_ok=True)
             with open(a.output, "w") as fh:

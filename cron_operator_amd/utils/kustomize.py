@@ -12,13 +12,23 @@ module implements the subset of its transformers the ``deploy/kustomize`` tree
   subjects of (Cluster)RoleBindings;
 * ``namePrefix`` / ``nameSuffix`` -- on every object except CRDs, with the
   name references kustomize fixes up (roleRef, ServiceAccount subjects,
-  ``serviceAccountName``, Service/ServiceMonitor/NetworkPolicy don't need it);
+  ``serviceAccountName``, Service/ServiceMonitor/NetworkPolicy don't need it)
+  plus the ``nameReference`` entries of ``configurations`` files (for CRD
+  fields such as a Certificate's ``spec.issuerRef.name``);
 * ``labels`` (with ``includeSelectors``) and legacy ``commonLabels``;
 * ``images`` -- ``newName`` / ``newTag`` / ``digest`` by image name;
 * ``patches`` -- JSON 6902 op lists or strategic-merge documents, inline
   (``patch``) or from a file (``path``), selected by ``target``
   (group/version/kind/name/namespace/labelSelector) or by the patch's own
-  kind+name.
+  kind+name;
+* ``replacements`` -- copy a field of one object (``source``: selected by
+  group/version/kind/name/namespace, matching the name before or after
+  ``namePrefix``) into fields of others (``targets``: ``fieldPaths`` with
+  ``[key=value]`` list selectors and ``[dotted.key]`` map keys, ``options``
+  ``delimiter``/``index``/``create``), run last as kustomize does.
+
+:func:`enable_optional` un-comments the optional sections of a kustomization
+(the reference's ``[CERTMANAGER]``-style toggles) into a copy of the tree.
 
 Output uses kustomize's default ``legacy`` sort: Namespaces, CRDs,
 ServiceAccounts and RBAC before workloads, webhooks last (stable within a
@@ -272,7 +282,35 @@ def _set_labels(objs: List[Dict[str, Any]], labels: Dict[str, str], selectors: b
             spec.setdefault("selector", {}).update(labels)
 
 
-def _rename(objs: List[Dict[str, Any]], prefix: str, suffix: str, namespace: Optional[str]) -> None:
+def _load_name_refs(directory: str, files: List[str]) -> List[Dict[str, Any]]:
+    """``configurations:`` files -> their ``nameReference`` entries (how kustomize learns that a
+    CRD field, e.g. a cert-manager Certificate's ``spec.issuerRef.name``, names another object)."""
+    refs: List[Dict[str, Any]] = []
+    for f in files:
+        for doc in _load_docs(os.path.join(directory, f)):
+            refs.extend(doc.get("nameReference") or [])
+    return refs
+
+
+def _fix_name_refs(objs: List[Dict[str, Any]], renamed: Dict[tuple, str], refs: List[Dict[str, Any]]) -> None:
+    for ref in refs:
+        kind = ref.get("kind")
+        for fs in ref.get("fieldSpecs") or []:
+            for o in objs:
+                if fs.get("kind") is not None and fs["kind"] != o.get("kind"):
+                    continue
+                if fs.get("group") is not None and fs["group"] != _gvk(o)[0]:
+                    continue
+                node: Any = o
+                toks = [t for t in str(fs.get("path", "")).split("/") if t]
+                for t in toks[:-1]:
+                    node = node.get(t) if isinstance(node, dict) else None
+                if isinstance(node, dict) and toks and (kind, node.get(toks[-1])) in renamed:
+                    node[toks[-1]] = renamed[(kind, node[toks[-1]])]
+
+
+def _rename(objs: List[Dict[str, Any]], prefix: str, suffix: str, namespace: Optional[str],
+            name_refs: Optional[List[Dict[str, Any]]] = None) -> None:
     renamed: Dict[tuple, str] = {}
     for o in objs:
         kind = o.get("kind", "")
@@ -304,6 +342,192 @@ def _rename(objs: List[Dict[str, Any]], prefix: str, suffix: str, namespace: Opt
             conv = ((o.get("spec") or {}).get("conversion") or {}).get("webhook", {}).get("clientConfig", {})
             if conv.get("service"):
                 conv["service"]["namespace"] = namespace
+    if name_refs:
+        _fix_name_refs(objs, renamed, name_refs)
+
+
+# ------------------------------------------------------------------ replacements
+def _field_tokens(path: str) -> List[str]:
+    """``spec.endpoints.0.tlsConfig.serverName`` / ``.metadata.annotations.[a.b/c]`` /
+    ``spec.containers.[name=manager].args`` -> tokens (brackets keep their dots)."""
+    toks: List[str] = []
+    i, cur, n = 0, "", len(path)
+    while i < n:
+        c = path[i]
+        if c == "[":
+            j = path.index("]", i)
+            toks.append(path[i:j + 1])
+            i = j + 1
+            continue
+        if c == ".":
+            if cur:
+                toks.append(cur)
+            cur = ""
+        else:
+            cur += c
+        i += 1
+    if cur:
+        toks.append(cur)
+    return toks
+
+
+def _step(node: Any, tok: str, create: bool, last: bool) -> Any:
+    """One path step; with ``create`` missing maps (or the final key) are made."""
+    if tok.startswith("[") and tok.endswith("]"):
+        inner = tok[1:-1]
+        if "=" in inner and isinstance(node, list):
+            k, v = inner.split("=", 1)
+            for it in node:
+                if isinstance(it, dict) and str(it.get(k)) == v:
+                    return it
+            if not create:
+                raise KeyError(tok)
+            it = {k: v}
+            node.append(it)
+            return it
+        tok = inner
+    if isinstance(node, list):
+        idx = int(tok)
+        if idx < len(node):
+            return node[idx]
+        raise KeyError(tok)
+    if not isinstance(node, dict):
+        raise KeyError(tok)
+    if tok not in node:
+        if not create:
+            raise KeyError(tok)
+        if not last:
+            node[tok] = {}
+    return node.get(tok)
+
+
+def _get_field(obj: Dict[str, Any], path: str) -> Any:
+    node: Any = obj
+    for t in _field_tokens(path):
+        node = _step(node, t, False, False)
+    return node
+
+
+def _set_field(obj: Dict[str, Any], path: str, value: Any, opts: Dict[str, Any]) -> bool:
+    toks = _field_tokens(path)
+    create = bool(opts.get("create"))
+    node: Any = obj
+    try:
+        for t in toks[:-1]:
+            node = _step(node, t, create, False)
+    except KeyError:
+        return False
+    last = toks[-1]
+    if last.startswith("[") and "=" not in last:
+        last = last[1:-1]
+    if isinstance(node, list):
+        idx = int(last)
+        if idx >= len(node):
+            return False
+        cur, setter = node[idx], (lambda v: node.__setitem__(idx, v))
+    elif isinstance(node, dict):
+        if last not in node and not create:
+            return False
+        cur, setter = node.get(last), (lambda v: node.__setitem__(last, v))
+    else:
+        return False
+    if "delimiter" in opts:
+        d = str(opts["delimiter"])
+        parts = str(cur).split(d) if cur not in (None, "") else []
+        at = int(opts.get("index", 0))
+        if at < 0:
+            parts.insert(0, str(value))
+        elif at >= len(parts):
+            parts.append(str(value))
+        else:
+            parts[at] = str(value)
+        setter(d.join(parts))
+    else:
+        setter(copy.deepcopy(value))
+    return True
+
+
+def _select(objs: List[Dict[str, Any]], sel: Dict[str, Any], orig: Dict[int, str]) -> List[Dict[str, Any]]:
+    out = []
+    for o in objs:
+        group, version, kind = _gvk(o)
+        md = o.get("metadata") or {}
+        if sel.get("kind") is not None and sel["kind"] != kind:
+            continue
+        if sel.get("group") is not None and sel["group"] != group:
+            continue
+        if sel.get("version") is not None and sel["version"] != version:
+            continue
+        if sel.get("namespace") is not None and sel["namespace"] != md.get("namespace", ""):
+            continue
+        if sel.get("name") is not None and sel["name"] not in (md.get("name"), orig.get(id(o))):
+            continue
+        out.append(o)
+    return out
+
+
+def _replacements(objs: List[Dict[str, Any]], reps: List[Dict[str, Any]], orig: Dict[int, str],
+                  where: str) -> None:
+    for rep in reps:
+        src = rep.get("source") or {}
+        found = _select(objs, src, orig)
+        if len(found) != 1:
+            raise KustomizeError(f"{where}: replacement source {src} matched {len(found)} objects")
+        try:
+            value = _get_field(found[0], src.get("fieldPath") or "metadata.name")
+        except KeyError:
+            raise KustomizeError(f"{where}: source fieldPath {src.get('fieldPath')} not found") from None
+        sopts = src.get("options") or {}
+        if "delimiter" in sopts:
+            parts = str(value).split(str(sopts["delimiter"]))
+            value = parts[int(sopts.get("index", 0))]
+        for tgt in rep.get("targets") or []:
+            hits = _select(objs, tgt.get("select") or {}, orig)
+            for rej in tgt.get("reject") or []:
+                bad = {id(o) for o in _select(objs, rej, orig)}
+                hits = [o for o in hits if id(o) not in bad]
+            for o in hits:
+                for fp in tgt.get("fieldPaths") or ["metadata.name"]:
+                    if not _set_field(o, fp, value, tgt.get("options") or {}):
+                        raise KustomizeError(f"{where}: target field {fp} missing in "
+                                             f"{o.get('kind')}/{(o.get('metadata') or {}).get('name')}")
+
+
+def enable_optional(directory: str, dest: str) -> str:
+    """Copy the kustomize tree holding ``directory`` to ``dest`` with every optional section
+    of its kustomization files un-commented, and return the copied ``directory``.
+
+    A toggle is a comment whose text is YAML at its own indentation -- ``#  - ../x``,
+    ``#patches:``, ``#    target:`` -- i.e. ``#`` followed by a key at column 0 or by two or
+    more spaces; prose comments are ``# `` plus one space and stay comments."""
+    import shutil
+
+    root = os.path.dirname(os.path.abspath(directory))
+    shutil.copytree(root, dest, dirs_exist_ok=True)
+    toggle = re.compile(r"^#(?:[A-Za-z_][\w-]*:| {2,}\S)")
+    for dirpath, _, files in os.walk(dest):
+        for f in files:
+            if f not in ("kustomization.yaml", "kustomization.yml", "Kustomization"):
+                continue
+            p = os.path.join(dirpath, f)
+            with open(p) as fh:
+                lines = fh.read().splitlines()
+            with open(p, "w") as fh:
+                fh.write("\n".join(ln[1:] if toggle.match(ln) else ln for ln in lines) + "\n")
+    return os.path.join(dest, os.path.basename(os.path.abspath(directory)))
+
+
+def _collect_name_refs(directory: str) -> List[Dict[str, Any]]:
+    """``configurations`` of this kustomization and of every kustomization it includes
+    (kustomize merges them, so a base's configuration applies to the overlay's prefix)."""
+    with open(_kfile(directory)) as fh:
+        k = yaml.safe_load(fh) or {}
+    refs = _load_name_refs(directory, k.get("configurations") or [])
+    for r in k.get("resources") or []:
+        p = os.path.normpath(os.path.join(directory, r))
+        if os.path.isdir(p):
+            refs.extend(_collect_name_refs(p))
+    return refs
 
 
 def build(directory: str) -> List[Dict[str, Any]]:
@@ -356,7 +580,11 @@ def build(directory: str) -> List[Dict[str, Any]]:
         _set_labels(objs, k["commonLabels"], True)
     for ent in k.get("labels") or []:
         _set_labels(objs, ent.get("pairs") or {}, bool(ent.get("includeSelectors")))
-    _rename(objs, k.get("namePrefix", ""), k.get("nameSuffix", ""), k.get("namespace"))
+    orig = {id(o): (o.get("metadata") or {}).get("name", "") for o in objs}
+    _rename(objs, k.get("namePrefix", ""), k.get("nameSuffix", ""), k.get("namespace"),
+            _collect_name_refs(directory))
+    if k.get("replacements"):
+        _replacements(objs, k["replacements"], orig, kpath)
     return objs
 
 

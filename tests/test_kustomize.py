@@ -175,3 +175,89 @@ def test_patch_target_must_match(tmp_path):
         "resources": [], "patches": [{"patch": "[]", "target": {"kind": "Deployment"}}]}))
     with pytest.raises(KustomizeError):
         build(str(tmp_path))
+
+
+# ---------------------------------------------------------------- optional TLS pieces
+
+
+def test_default_keeps_optional_sections_off():
+    kinds = {o["kind"] for o in build(DEFAULT)}
+    assert not kinds & {"Certificate", "Issuer", "ServiceMonitor", "NetworkPolicy"}
+    dep = by_kind(build(DEFAULT), "Deployment")[0]["spec"]["template"]["spec"]
+    assert dep["volumes"] == [] and dep["containers"][0]["volumeMounts"] == []
+
+
+def test_cert_manager_metrics_and_servicemonitor_tls(tmp_path):
+    """The reference's [METRICS-WITH-CERTS] + [PROMETHEUS] TLS variant
+    (config/default/cert_metrics_manager_patch.yaml, config/prometheus/monitor_tls_patch.yaml):
+    the Deployment mounts the cert-manager Secret and serves it; the ServiceMonitor verifies it
+    against the prefixed Service's DNS name; the Certificate covers those names and points at
+    the prefixed Issuer."""
+    from cron_operator_amd.utils.kustomize import enable_optional
+
+    objs = build_sorted(enable_optional(DEFAULT, str(tmp_path / "tree")))
+    svc = [o for o in by_kind(objs, "Service") if "metrics" in o["metadata"]["name"]][0]
+    host = f"{svc['metadata']['name']}.cron-operator-system.svc"
+    assert host == "cron-operator-controller-manager-metrics.cron-operator-system.svc"
+    cert = by_kind(objs, "Certificate")[0]
+    assert cert["spec"]["dnsNames"] == [host, host + ".cluster.local"]
+    assert cert["spec"]["secretName"] == "metrics-server-cert"
+    issuer = by_kind(objs, "Issuer")[0]
+    assert cert["spec"]["issuerRef"] == {"kind": "Issuer", "name": issuer["metadata"]["name"]}
+    assert issuer["metadata"]["namespace"] == cert["metadata"]["namespace"] == "cron-operator-system"
+    pod = by_kind(objs, "Deployment")[0]["spec"]["template"]["spec"]
+    c = pod["containers"][0]
+    assert "--metrics-cert-path=/tmp/k8s-metrics-server/metrics-certs" in c["args"]
+    assert "--metrics-bind-address=:8443" in c["args"]
+    assert c["volumeMounts"] == [{"name": "metrics-certs", "mountPath": "/tmp/k8s-metrics-server/metrics-certs",
+                                  "readOnly": True}]
+    vol = pod["volumes"][0]
+    assert vol["secret"]["secretName"] == "metrics-server-cert"
+    assert sorted(i["key"] for i in vol["secret"]["items"]) == ["ca.crt", "tls.crt", "tls.key"]
+    mon = by_kind(objs, "ServiceMonitor")[0]
+    tls = mon["spec"]["endpoints"][0]["tlsConfig"]
+    assert tls["serverName"] == host and tls["insecureSkipVerify"] is False
+    assert tls["ca"]["secret"] == {"name": "metrics-server-cert", "key": "ca.crt"}
+    assert tls["keySecret"] == {"name": "metrics-server-cert", "key": "tls.key"}
+    assert by_kind(objs, "NetworkPolicy")
+
+
+def test_cli_enable_optional_renders_certs(tmp_path):
+    out = tmp_path / "install-certs.yaml"
+    assert cli(["kustomize", "--enable-optional", DEFAULT, "-o", str(out)]) == 0
+    kinds = [d["kind"] for d in yaml.safe_load_all(out.read_text())]
+    assert "Certificate" in kinds and "ServiceMonitor" in kinds
+
+
+def test_replacements_semantics(tmp_path):
+    (tmp_path / "kustomization.yaml").write_text(yaml.safe_dump({
+        "namePrefix": "p-",
+        "resources": ["objs.yaml"],
+        "replacements": [
+            {"source": {"kind": "Service", "name": "svc", "fieldPath": "metadata.name"},
+             "targets": [{"select": {"kind": "ConfigMap"},
+                          "fieldPaths": ["data.host", "data.[a.b/c]"],
+                          "options": {"delimiter": ".", "index": 0, "create": True}},
+                         {"select": {"kind": "Deployment"},
+                          "fieldPaths": ["spec.template.spec.containers.[name=app].env.[name=SVC].value"]}]},
+            {"source": {"kind": "ConfigMap", "name": "cm", "fieldPath": "data.host",
+                        "options": {"delimiter": ".", "index": 1}},
+             "targets": [{"select": {"kind": "Deployment"}, "fieldPaths": ["metadata.annotations.zone"],
+                          "options": {"create": True}}]},
+        ]}))
+    (tmp_path / "objs.yaml").write_text(yaml.safe_dump_all([
+        {"apiVersion": "v1", "kind": "Service", "metadata": {"name": "svc"}},
+        {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "cm"}, "data": {"host": "X.zone1.svc"}},
+        {"apiVersion": "apps/v1", "kind": "Deployment", "metadata": {"name": "d"},
+         "spec": {"template": {"spec": {"containers": [{"name": "app", "env": [{"name": "SVC", "value": ""}]}]}}}},
+    ]))
+    objs = {o["kind"]: o for o in build(str(tmp_path))}
+    assert objs["ConfigMap"]["data"] == {"host": "p-svc.zone1.svc", "a.b/c": "p-svc"}
+    assert objs["Deployment"]["spec"]["template"]["spec"]["containers"][0]["env"][0]["value"] == "p-svc"
+    assert objs["Deployment"]["metadata"]["annotations"] == {"zone": "zone1"}
+    # a source that matches nothing is an error, as in kustomize
+    k = yaml.safe_load((tmp_path / "kustomization.yaml").read_text())
+    k["replacements"][0]["source"]["name"] = "nope"
+    (tmp_path / "kustomization.yaml").write_text(yaml.safe_dump(k))
+    with pytest.raises(KustomizeError):
+        build(str(tmp_path))
