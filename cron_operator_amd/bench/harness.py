@@ -130,6 +130,8 @@ class BenchResult:
     cpu_s_apiserver: float = 0.0
     # peak RSS of each operator shard process (sharded runs; the in-process run shares the harness)
     operator_maxrss_mib: List[float] = field(default_factory=list)
+    # cyclic-GC collections per generation and pause time in the operator process(es), timed region
+    operator_gc: Dict[str, Any] = field(default_factory=dict)
 
     def to_dict(self) -> Dict[str, Any]:
         return asdict(self)
@@ -262,7 +264,7 @@ async def run(cfg: BenchConfig, on_step=None) -> BenchResult:
     from ..cron.engine import default_engine
     from ..runtime.client import Client, InMemoryTransport
     from ..runtime.manager import Manager, ManagerOptions
-    from ..utils import jsonutil
+    from ..utils import gctune, jsonutil
     from ..utils.clock import FakeClock
     from ..utils.logging import new_from_options, set_logger
 
@@ -433,6 +435,7 @@ async def run(cfg: BenchConfig, on_step=None) -> BenchResult:
                     async with admin.post(remote.url + "/debug/fake/profile", json={"action": "start"}) as r:
                         await r.read()
                 cpu0 = _cpu_times(remote)
+                gcs = gctune.GcStats().start()
                 rec0 = ctrl.reconciles
                 req0 = client.requests
                 reqv0 = dict(client.requests_by_verb)
@@ -462,6 +465,7 @@ async def run(cfg: BenchConfig, on_step=None) -> BenchResult:
                 on_step(k, dt, k > cfg.warmup)
         elapsed = time.perf_counter() - t_start
         cpu1 = _cpu_times(remote)
+        gc_stats = gcs.stop().to_dict() if cfg.warmup < total else {}
         if cfg.apiserver_profile and admin is not None:
             async with admin.post(remote.url + "/debug/fake/profile",
                                   json={"action": "stop", "path": os.path.abspath(cfg.apiserver_profile)}) as r:
@@ -479,7 +483,7 @@ async def run(cfg: BenchConfig, on_step=None) -> BenchResult:
             api_requests_per_fire=requests / fires, api_requests_by_verb=by_verb,
             reconciles_per_fire=reconciles / fires, step_ms=step_ms, phase_ms=phase_ms,
             engine=default_engine().name, fastjson_native=jsonutil.NATIVE,
-            cpu_s_operator=cpu1[0] - cpu0[0], cpu_s_apiserver=cpu1[1] - cpu0[1])
+            cpu_s_operator=cpu1[0] - cpu0[0], cpu_s_apiserver=cpu1[1] - cpu0[1], operator_gc=gc_stats)
         mgr.stop()
         try:
             await asyncio.wait_for(mgr_task, 30)
@@ -610,7 +614,12 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
             reconciles_per_fire=reconciles / fires, step_ms=step_ms, phase_ms=phase_ms,
             engine=default_engine().name, fastjson_native=jsonutil.NATIVE,
             cpu_s_operator=sum(r["cpu"] - b["cpu"] for r, b in zip(last, base)), cpu_s_apiserver=api1 - api0,
-            operator_maxrss_mib=[round(r.get("maxrss_mib", 0.0), 1) for r in last])
+            operator_maxrss_mib=[round(r.get("maxrss_mib", 0.0), 1) for r in last],
+            operator_gc={"collections": [sum(r.get("gc_collections", [0, 0, 0])[g] - b.get("gc_collections",
+                                                                                            [0, 0, 0])[g]
+                                             for r, b in zip(last, base)) for g in range(3)],
+                         "ms": round(sum(r.get("gc_s", 0.0) - b.get("gc_s", 0.0) for r, b in zip(last, base))
+                                     * 1000, 2)})
     finally:
         for s in shards:
             try:

@@ -94,6 +94,9 @@ async def main() -> int:
         creates[0] += 1
 
     rec.latency_observer = on_create
+    from ..utils.gctune import GcStats
+
+    gcs = GcStats().start()
     out = sys.stdout
     out.write(json.dumps({"ready": True, "owned": n_owned}) + "\n")
     out.flush()
@@ -140,7 +143,8 @@ async def main() -> int:
             # counters are cumulative: the harness differences them over its timed window
             out.write(json.dumps({"ok": True, "lat": lat, "reconciles": ctrl.reconciles,
                                   "requests": client.requests, "by_verb": dict(client.requests_by_verb),
-                                  "cpu": time.process_time(),
+                                  "cpu": time.process_time(), "gc_s": gcs.seconds,
+                                  "gc_collections": list(gcs.collections),
                                   "maxrss_mib": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024}) + "\n")
             out.flush()
     mgr.stop()

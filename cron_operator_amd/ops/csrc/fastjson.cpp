@@ -33,6 +33,14 @@
 // errors (ValueError), \uXXXX escapes combine surrogate pairs and keep lone
 // surrogates, numbers with a fraction/exponent become float (correctly
 // rounded, via PyOS_string_to_double), the rest int (arbitrary precision).
+//
+// GC: a JSON tree cannot contain a reference cycle, so the dicts and lists that
+// loads() and deepcopy() build are removed from the cyclic collector's lists
+// (PyObject_GC_UnTrack) -- reference counting alone frees them.  The operator
+// caches ~12k such trees in the 1000-Cron bench; every young-generation pass
+// used to walk all of the recently replaced ones (~47 ms per pass, measured).
+// set_gc_untrack(False) restores normal tracking.  An untracked dict that later
+// receives a container value is re-tracked by CPython itself.
 
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
@@ -44,6 +52,14 @@
 #include <vector>
 
 namespace {
+
+bool g_untrack = true;
+
+// A finished JSON container: exempt it from cyclic GC (see the header comment).
+inline PyObject* acyclic(PyObject* c) {
+  if (c != nullptr && g_untrack && PyObject_GC_IsTracked(c)) PyObject_GC_UnTrack(c);
+  return c;
+}
 
 PyObject* deepcopy_impl(PyObject* x, int depth);
 
@@ -78,7 +94,7 @@ PyObject* deepcopy_impl(PyObject* x, int depth) {
         return nullptr;
       }
     }
-    return out;
+    return acyclic(out);
   }
   if (PyList_CheckExact(x)) {
     const Py_ssize_t n = PyList_GET_SIZE(x);
@@ -99,7 +115,7 @@ PyObject* deepcopy_impl(PyObject* x, int depth) {
       }
       PyList_SET_ITEM(out, i, cv);
     }
-    return out;
+    return acyclic(out);
   }
   Py_INCREF(x);
   return x;
@@ -479,7 +495,7 @@ struct Decoder {
         PyObject* d = PyDict_New();
         if (!d) return nullptr;
         ws();
-        if (p < end && *p == '}') { ++p; return d; }
+        if (p < end && *p == '}') { ++p; return acyclic(d); }
         while (true) {
           ws();
           if (p >= end || *p != '"') { Py_DECREF(d); return fail("Expecting property name enclosed in double quotes"); }
@@ -497,7 +513,7 @@ struct Decoder {
           if (rc < 0) { Py_DECREF(d); return nullptr; }
           ws();
           if (p < end && *p == ',') { ++p; continue; }
-          if (p < end && *p == '}') { ++p; return d; }
+          if (p < end && *p == '}') { ++p; return acyclic(d); }
           Py_DECREF(d);
           return fail("Expecting ',' delimiter");
         }
@@ -506,7 +522,7 @@ struct Decoder {
         ++p;
         std::vector<PyObject*> items;
         ws();
-        if (p < end && *p == ']') { ++p; return PyList_New(0); }
+        if (p < end && *p == ']') { ++p; return acyclic(PyList_New(0)); }
         while (true) {
           PyObject* v = value(depth + 1);
           if (!v) {
@@ -526,7 +542,7 @@ struct Decoder {
           return nullptr;
         }
         for (size_t i = 0; i < items.size(); ++i) PyList_SET_ITEM(l, static_cast<Py_ssize_t>(i), items[i]);
-        return l;
+        return acyclic(l);
       }
       case '"':
         ++p;
@@ -831,6 +847,15 @@ PyObject* py_merge_patch(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
   return merge_patch_impl(args[0], args[1], 0);
 }
 
+PyObject* py_set_gc_untrack(PyObject*, PyObject* arg) {
+  const int on = PyObject_IsTrue(arg);
+  if (on < 0) return nullptr;
+  PyObject* prev = g_untrack ? Py_True : Py_False;
+  g_untrack = on != 0;
+  Py_INCREF(prev);
+  return prev;
+}
+
 PyMethodDef methods[] = {
     {"deepcopy", py_deepcopy, METH_O, "copy a JSON tree"},
     {"json_equal", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(py_json_equal)), METH_FASTCALL,
@@ -843,6 +868,8 @@ PyMethodDef methods[] = {
     {"dumpb_shared", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(py_dumpb_shared)),
      METH_FASTCALL, "dumpb of an immutable tree, reusing the bytes of subtrees cached by identity"},
     {"clear_key_cache", py_clear_key_cache, METH_NOARGS, "drop the interned-key cache"},
+    {"set_gc_untrack", py_set_gc_untrack, METH_O,
+     "set_gc_untrack(bool) -> previous: exempt decoded/copied containers from cyclic GC"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef moddef = {PyModuleDef_HEAD_INIT, "_fastjson", "Native JSON-tree helpers", -1, methods,

@@ -37,3 +37,39 @@ def freeze() -> None:
     if _ENABLED:
         gc.collect()
         gc.freeze()
+
+
+class GcStats:
+    """Collections per generation and time spent in the cyclic GC while installed
+    (``gc.callbacks``), to tell GC pauses apart from real work in a benchmark."""
+
+    def __init__(self) -> None:
+        import time
+
+        self._now = time.perf_counter
+        self.collections = [0, 0, 0]
+        self.seconds = 0.0
+        self._t0 = 0.0
+        self._on = False
+
+    def _cb(self, phase: str, info) -> None:
+        if phase == "start":
+            self._t0 = self._now()
+        else:
+            self.seconds += self._now() - self._t0
+            self.collections[info.get("generation", 0)] += 1
+
+    def start(self) -> "GcStats":
+        if not self._on:
+            gc.callbacks.append(self._cb)
+            self._on = True
+        return self
+
+    def stop(self) -> "GcStats":
+        if self._on:
+            gc.callbacks.remove(self._cb)
+            self._on = False
+        return self
+
+    def to_dict(self):
+        return {"collections": list(self.collections), "ms": round(self.seconds * 1000, 2)}

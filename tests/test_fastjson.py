@@ -136,3 +136,40 @@ def test_encoder_nan_and_errors():
         cur = nxt
     with pytest.raises(ValueError):
         m.dumpb(deep)
+
+
+def test_decoded_and_copied_trees_are_exempt_from_cyclic_gc():
+    """JSON trees are acyclic: the native decoder and deepcopy untrack their containers so
+    young-generation GC passes do not walk the informer caches; refcounting still frees
+    them, and CPython re-tracks a dict that later receives a container."""
+    import gc
+    import weakref
+
+    from cron_operator_amd.ops import _fastjson as fj
+
+    doc = fj.loads(b'{"metadata":{"labels":{"a":"b"},"ownerReferences":[{"uid":"1"}]},"items":[[],{}]}')
+    nodes = [doc, doc["metadata"], doc["metadata"]["ownerReferences"], doc["metadata"]["ownerReferences"][0],
+             doc["items"], doc["items"][0], doc["items"][1]]
+    assert not any(gc.is_tracked(n) for n in nodes)
+    cp = fj.deepcopy(doc)
+    assert cp == doc and not gc.is_tracked(cp) and not gc.is_tracked(cp["metadata"]["ownerReferences"])
+
+    class Probe:  # a tracked object referenced from an untracked tree stays alive while the tree is
+        pass
+
+    p = Probe()
+    ref = weakref.ref(p)
+    doc["items"].append(p)
+    del p
+    gc.collect()
+    assert ref() is not None
+    del doc, nodes
+    gc.collect()
+    assert ref() is None  # freed by refcounting once the tree goes
+    cp["metadata"]["new"] = {"x": []}
+    assert gc.is_tracked(cp["metadata"])
+    prev = fj.set_gc_untrack(False)
+    try:
+        assert prev is True and gc.is_tracked(fj.loads(b'{"a":[1]}')["a"])
+    finally:
+        fj.set_gc_untrack(prev)
