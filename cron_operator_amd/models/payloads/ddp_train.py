@@ -73,9 +73,18 @@ def main(argv=None) -> int:
     ref = flat.clone()
     dist.broadcast(ref, 0)
     in_sync = bool(torch.allclose(flat, ref))
+    # which physical device each rank trained on (PCI bus id on GPUs): ranks must not share one
+    if use_gpu:
+        props = torch.cuda.get_device_properties(dev)
+        ident = f"{props.pci_domain_id:04x}:{props.pci_bus_id:02x}:{props.pci_device_id:02x}"
+    else:
+        ident = f"cpu:{rank}"
+    devices = [None] * world
+    dist.all_gather_object(devices, ident)
     if rank == 0:
         print("DDP_OK " if in_sync else "DDP_FAIL ", json.dumps({
-            "world": world, "backend": dist.get_backend(), "device": str(dev), "loss": float(loss.detach()),
+            "world": world, "backend": dist.get_backend(), "device": str(dev), "devices": devices,
+            "visible_devices": torch.cuda.device_count() if use_gpu else 0, "loss": float(loss.detach()),
             "steps_per_s": a.steps / dt, "samples_per_s": a.steps * a.batch * world / dt}), flush=True)
     dist.destroy_process_group()
     return 0 if in_sync else 1

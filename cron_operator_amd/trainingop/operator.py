@@ -86,6 +86,7 @@ class FakeTrainingOperator:
         self._tasks: List[asyncio.Task] = []
         self._handled: set = set()
         self.results: Dict[str, Tuple[bool, List[int], float]] = {}
+        self.outputs: Dict[str, str] = {}  # real mode: "ns/name" -> the first replica's (rank 0's) output
         self.log = get_logger("training-operator")
 
     # ------------------------------------------------------------------ status writes
@@ -199,7 +200,7 @@ class FakeTrainingOperator:
                                                               stdout=asyncio.subprocess.PIPE,
                                                               stderr=asyncio.subprocess.STDOUT))
         codes: List[int] = []
-        for p in procs:
+        for i, p in enumerate(procs):
             try:
                 out, _ = await asyncio.wait_for(p.communicate(), self.timeout)
             except asyncio.TimeoutError:
@@ -207,6 +208,8 @@ class FakeTrainingOperator:
                 out, _ = await p.communicate()
             codes.append(p.returncode if p.returncode is not None else -9)
             text = (out or b"").decode(errors="replace")
+            if i == 0:
+                self.outputs[f"{ns}/{name}"] = text[-20000:]
             if text:
                 self.log.info("replica output", job=f"{ns}/{name}", output=text[-4000:])
         ok = bool(codes) and all(c == 0 for c in codes)

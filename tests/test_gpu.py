@@ -102,9 +102,32 @@ def test_ddp_cron_suspend_resume_cycle_on_gpu(gpu):
 
     from cron_operator_amd.bench.ddp_cycle import run_ddp_cycle
 
-    res = asyncio.run(run_ddp_cycle(max(1, torch.cuda.device_count()), cpu=False))
+    n = torch.cuda.device_count()
+    res = asyncio.run(run_ddp_cycle(max(1, n), cpu=False))
     assert [s for _, s in res["history"]] == ["Succeeded", "Succeeded"]
     assert all(codes == [0] for codes in res["exit_codes"].values())
+    for rep in res["ddp"].values():
+        # one rank per visible GPU, each on its own device (PCI address), over RCCL
+        assert rep["world"] == n and rep["backend"] == "nccl", rep
+        assert len(set(rep["devices"])) == rep["world"], rep
+
+
+def test_ddp_8_replica_cron_cycle_on_gpu(gpu):
+    """The Master + Worker example (one process per replica, ranks from the PyTorchJob env):
+    Workers = visible GPUs - 1, so world == device_count (8 on a full node, 1 here), each
+    rank on a distinct GPU."""
+    import asyncio
+
+    import torch
+
+    from cron_operator_amd.bench.ddp_cycle import run_ddp_cycle
+
+    n = torch.cuda.device_count()
+    res = asyncio.run(run_ddp_cycle(max(1, n), cpu=False, topology="replicas"))
+    assert [s for _, s in res["history"]] == ["Succeeded", "Succeeded"]
+    for job, rep in res["ddp"].items():
+        assert rep["world"] == n and rep["backend"] == "nccl", (job, rep)
+        assert len(set(rep["devices"])) == n, rep
 
 
 def test_headline_bench_short_run():

@@ -112,6 +112,24 @@ async def test_mi355x_ddp_example_suspend_resume_cycle_cpu():
     res = await run_ddp_cycle(2, cpu=True, timeout=240)
     assert [s for _, s in res["history"]] == ["Succeeded", "Succeeded"] and res["active"] == 0
     assert all(codes == [0] for codes in res["exit_codes"].values())
+    assert all(r["world"] == 2 for r in res["ddp"].values())
+
+
+@pytest.mark.timeout(400)
+async def test_mi355x_ddp_8_replica_cron_suspend_resume_cycle_cpu():
+    """BASELINE config 5 as written: the Master + 7 Worker example PyTorchJob
+    (examples/mi355x/cron-pytorch-ddp-8worker-mi355x.yaml, the reference examples' replica
+    topology).  The fake training-operator starts 8 replica processes with the PyTorchJob
+    env (WORLD_SIZE=8, RANK 0..7); they train with DDP over gloo here, in sync, each on its
+    own rank, through a suspend/resume cycle."""
+    from cron_operator_amd.bench.ddp_cycle import run_ddp_cycle
+
+    res = await run_ddp_cycle(8, cpu=True, timeout=300, topology="replicas")
+    assert [s for _, s in res["history"]] == ["Succeeded", "Succeeded"] and res["active"] == 0
+    assert all(codes == [0] * 8 for codes in res["exit_codes"].values()), res["exit_codes"]
+    for job, rep in res["ddp"].items():
+        assert rep["world"] == 8 and rep["backend"] == "gloo", (job, rep)
+        assert rep["devices"] == [f"cpu:{r}" for r in range(8)], rep
 
 
 async def test_pod_template_busybox_config():

@@ -119,6 +119,33 @@ def test_mi355x_example_requests_gpus_and_rccl_payload():
     assert "cron_operator_amd.models.payloads.ddp_train" in ctr["args"]
 
 
+def test_mi355x_8_replica_example_is_master_plus_7_workers():
+    """BASELINE config 5's "8-worker DDP template" in the reference's replica topology: 1 Master
+    + 7 Workers, one GPU each, all pods pinned to one node, valid against the Cron CRD."""
+    from cron_operator_amd.api.v1alpha1.crd import crd
+    from cron_operator_amd.apiserver.server import APIServer
+    from cron_operator_amd.api.v1alpha1 import CRON_GVR
+    from cron_operator_amd.utils.clock import FakeClock
+
+    with open(os.path.join(ROOT, "examples/mi355x/cron-pytorch-ddp-8worker-mi355x.yaml")) as fh:
+        c = yaml.safe_load(fh)
+    specs = c["spec"]["template"]["workload"]["spec"]["pytorchReplicaSpecs"]
+    assert specs["Master"]["replicas"] == 1 and specs["Worker"]["replicas"] == 7
+    for rs in specs.values():
+        pod = rs["template"]["spec"]
+        ctr = pod["containers"][0]
+        assert ctr["resources"]["limits"]["amd.com/gpu"] == 1
+        assert ctr["command"][-1] == "cron_operator_amd.models.payloads.ddp_train"
+        aff = pod["affinity"]["podAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"][0]
+        assert aff["topologyKey"] == "kubernetes.io/hostname"
+        assert aff["labelSelector"]["matchLabels"].items() <= rs["template"]["metadata"]["labels"].items()
+    assert c["spec"]["concurrencyPolicy"] == "Forbid"
+    srv = APIServer(FakeClock(0))
+    srv.install_crd(crd())
+    c["metadata"]["namespace"] = "default"
+    assert srv.create(CRON_GVR, "default", c)["spec"]["schedule"] == "CRON_TZ=Asia/Shanghai 30 2 * * *"
+
+
 def test_native_extensions_clean_under_asan_ubsan():
     """scripts/sanitize.py: the C++ extensions built with ASan + UBSan survive fuzzed HTTP
     framing, random JSON trees and random cron specs (a short run; `make sanitize` runs more)."""
