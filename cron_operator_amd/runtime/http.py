@@ -119,7 +119,9 @@ class HttpTransport(Transport):
         self._pool: Optional[HttpPool] = None
         self._token = ""  # the bearer token the pool/session headers carry
         self._cert_generation = 0  # the exec-plugin client certificate the pool's TLS context holds
-        self._proxy: Optional[str] = None  # resolved on first use (aiohttp path)
+        # resolved once, at construction: a bad proxy fails (or is reported) at startup,
+        # not on every request
+        self._proxy: Optional[str] = config.proxy()
         self._exec_lock: Optional[asyncio.Lock] = None
 
     def _fast_pool(self) -> HttpPool:
@@ -128,7 +130,7 @@ class HttpTransport(Transport):
             self._pool = HttpPool(self.config.host, ssl_context=self.config.ssl_context() or None,
                                   headers=self.config.auth_headers(self._token), max_idle=self._pool_size,
                                   timeout=self._timeout, server_hostname=self.config.tls_server_name or None,
-                                  proxy=self.config.proxy())
+                                  proxy=self._proxy or "")
             self._cert_generation = self.config.cert_generation
         elif self.config.rotating:
             self._rotate_token()
@@ -173,8 +175,6 @@ class HttpTransport(Transport):
         name = self.config.tls_server_name
         if name and self.config.host.startswith("https://"):
             kw["server_hostname"] = name
-        if self._proxy is None:
-            self._proxy = self.config.proxy()
         if self._proxy:
             kw["proxy"] = self._proxy if "://" in self._proxy else "http://" + self._proxy
         return kw
@@ -214,6 +214,8 @@ class HttpTransport(Transport):
             target = path + encode_query(_clean(params))
             attempt = 0
             while True:
+                if attempt and self.config.exec_provider is not None and self.config.exec_stale():
+                    await self._fresh_exec()  # expired while waiting out Retry-After: refresh off the loop
                 try:
                     status, raw, retry_after = await self._fast_pool().request_full(
                         method, target, data, ctype, params.get(ACCEPT) or "application/json")

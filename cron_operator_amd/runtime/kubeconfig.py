@@ -220,8 +220,12 @@ class RestConfig:
             self._exec_creds = new
 
     def _exec(self) -> ExecCredentials:
-        """The plugin's cached credential, re-run once expired (client-go ``credsExpired``)."""
-        self.refresh_exec()
+        """The plugin's cached credential -- even when it has expired: refreshing runs the
+        plugin (a subprocess, up to 60 s), which the HTTP transport does off the event loop
+        before each request attempt (``HttpTransport._fresh_exec``).  Only the very first
+        use, with nothing cached yet, runs the plugin here."""
+        if self._exec_creds is None:
+            self.refresh_exec()
         assert self._exec_creds is not None
         return self._exec_creds
 
@@ -307,8 +311,19 @@ class RestConfig:
         return ctx
 
     def proxy(self) -> str:
-        """The proxy for this server: kubeconfig ``proxy-url``, else the environment."""
-        return self.proxy_url or proxy_from_environment(self.host)
+        """The proxy for this server: kubeconfig ``proxy-url`` (validated when the kubeconfig is
+        loaded), else the environment.  An environment proxy of a scheme this client cannot
+        speak (``https://``, ``socks5://``) is skipped with a warning -- the connection goes
+        direct -- rather than failing every request."""
+        if self.proxy_url:
+            return self.proxy_url
+        try:
+            return proxy_from_environment(self.host)
+        except ConfigError as e:
+            from ..utils.logging import get_logger
+
+            get_logger("kubeconfig").info("ignoring the environment proxy; connecting directly", reason=str(e))
+            return ""
 
     def auth_headers(self, token: Optional[str] = None) -> Dict[str, str]:
         """Headers for every request; ``token`` saves a second :meth:`token` call when the caller

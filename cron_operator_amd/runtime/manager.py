@@ -135,6 +135,9 @@ class Manager:
         """Run until :meth:`stop` (or leadership loss, which raises)."""
         await self.probes.start()
         await self.metrics_server.start()
+        from .supervisor import report_ports
+
+        report_ports(self.metrics_server.port, self.probes.port)
         self.broadcaster.start()
         lost = False
         try:

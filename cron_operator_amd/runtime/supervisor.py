@@ -9,7 +9,8 @@ process becomes a supervisor:
 * it starts ``N`` children, ``start ... --shard-count C*N --shard-index I*N+i``
   (``C``/``I`` are the pod-level ``--shard-count``/``--shard-index``, so pods of
   processes compose), each with its own shard Lease, informers and workers;
-* children serve plain metrics and probes on loopback ports; the supervisor serves
+* children serve plain metrics and probes on loopback ports they bind themselves
+  (port 0, reported back over a pipe on every start); the supervisor serves
   the configured ``--metrics-bind-address`` (with the same TokenReview /
   SubjectAccessReview filter when secure) as the merge of the children's
   expositions, every series labelled ``shard="<index>"``;
@@ -24,7 +25,6 @@ import asyncio
 import math
 import os
 import signal
-import socket
 import sys
 import time
 from typing import Dict, List, Optional, Tuple
@@ -36,12 +36,6 @@ from ..utils.logging import get_logger
 from .servers import MetricsServer, ProbeServer
 
 RESTART_BACKOFF = (1.0, 30.0)
-
-
-def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
 
 
 def available_cpus(cgroup_root: str = "/sys/fs/cgroup") -> int:
@@ -118,20 +112,68 @@ def merge_expositions(parts: List[Tuple[str, str]]) -> str:
     return "\n".join(out) + "\n"
 
 
+REPORT_FD_ENV = "CRON_OPERATOR_REPORT_FD"
+
+
+def report_ports(metrics_port: Optional[int], probe_port: Optional[int]) -> None:
+    """In a supervised child: tell the supervisor which loopback ports the servers bound
+    (one JSON line on the inherited pipe named by ``$CRON_OPERATOR_REPORT_FD``)."""
+    fd = os.environ.pop(REPORT_FD_ENV, None)
+    if not fd:
+        return
+    import json
+
+    try:
+        with os.fdopen(int(fd), "w") as fh:
+            fh.write(json.dumps({"metrics": metrics_port, "probes": probe_port}) + "\n")
+    except (OSError, ValueError):
+        pass
+
+
 class _Child:
+    """One shard process.  Its metrics and probe servers bind loopback port 0 -- the kernel
+    picks a free port at bind time, on every (re)start -- and the child reports the ports
+    back over a pipe, so nothing can take a port between choosing and binding it."""
+
     def __init__(self, index: int, argv: List[str]):
         self.index = index
         self.argv = argv
-        self.metrics_port = _free_port()
-        self.probe_port = _free_port()
+        self.metrics_port: Optional[int] = None
+        self.probe_port: Optional[int] = None
         self.proc: Optional[asyncio.subprocess.Process] = None
         self.restarts = 0
 
     async def spawn(self) -> None:
-        self.proc = await asyncio.create_subprocess_exec(
-            sys.executable, "-m", "cron_operator_amd", *self.argv,
-            f"--metrics-bind-address=127.0.0.1:{self.metrics_port}", "--metrics-secure=false",
-            f"--health-probe-bind-address=127.0.0.1:{self.probe_port}")
+        self.metrics_port = self.probe_port = None
+        r, w = os.pipe()
+        try:
+            env = dict(os.environ, **{REPORT_FD_ENV: str(w)})
+            self.proc = await asyncio.create_subprocess_exec(
+                sys.executable, "-m", "cron_operator_amd", *self.argv,
+                "--metrics-bind-address=127.0.0.1:0", "--metrics-secure=false",
+                "--health-probe-bind-address=127.0.0.1:0", env=env, pass_fds=(w,))
+        except BaseException:
+            os.close(r)
+            raise
+        finally:
+            os.close(w)
+        asyncio.ensure_future(self._read_ports(r, self.proc))
+
+    async def _read_ports(self, r: int, proc: asyncio.subprocess.Process) -> None:
+        import json
+
+        def read() -> bytes:
+            with os.fdopen(r, "rb") as fh:
+                return fh.readline()
+
+        line = await asyncio.get_running_loop().run_in_executor(None, read)
+        if self.proc is not proc or not line:
+            return
+        try:
+            ports = json.loads(line)
+        except ValueError:
+            return
+        self.metrics_port, self.probe_port = ports.get("metrics"), ports.get("probes")
 
     @property
     def running(self) -> bool:
@@ -172,7 +214,7 @@ class Supervisor:
         while not self._stopping.is_set():
             for c in self.children:
                 ok = False
-                if c.running:
+                if c.running and c.probe_port:
                     try:
                         async with self._sess().get(f"http://127.0.0.1:{c.probe_port}/readyz") as r:
                             ok = r.status == 200
@@ -186,7 +228,7 @@ class Supervisor:
 
     async def scrape(self) -> str:
         async def one(c: _Child) -> Tuple[str, str]:
-            if not c.running:
+            if not c.running or not c.metrics_port:
                 return str(c.index), ""
             try:
                 async with self._sess().get(f"http://127.0.0.1:{c.metrics_port}/metrics") as r:

@@ -176,7 +176,7 @@ def test_exec_plugin_client_certificate_loaded_and_rotated():
         assert cfg.token() == ""  # certificate-only credential
         # the same certificate again does not bump the generation; a new one does
         cfg._exec_creds.expires_at = 0.0
-        cfg.client_cert()
+        cfg.refresh_exec()
         assert cfg.cert_generation == 1
         d2 = os.path.join(d, "two")
         os.mkdir(d2)
@@ -185,7 +185,9 @@ def test_exec_plugin_client_certificate_loaded_and_rotated():
             with open(src) as i, open(os.path.join(d, dst), "w") as o:
                 o.write(i.read())
         cfg._exec_creds.expires_at = 0.0
-        cfg.client_cert()
+        cfg.client_cert()  # reads the cache: never runs the plugin on the caller's thread
+        assert cfg.cert_generation == 1
+        cfg.refresh_exec()  # what HttpTransport does in a worker thread before a request
         assert cfg.cert_generation == 2
 
         pool = HttpPool("https://127.0.0.1:1", ssl_context=ctx)
@@ -249,3 +251,51 @@ def test_auth_provider_still_rejected():
             yaml.safe_dump(doc, fh)
         with pytest.raises(ConfigError, match="auth-provider"):
             load_kubeconfig(p)
+
+
+async def test_credential_expiring_during_retry_after_is_refreshed_off_the_loop():
+    """A 429 with Retry-After, and the exec credential expires while the request waits it out:
+    the retry refreshes the credential in a worker thread (never on the event-loop thread)
+    and goes out with the new token."""
+    import threading
+
+    env = TestEnv()
+    env.server.tokens = {"tok-1": {"username": "u"}, "tok-2": {"username": "u"}}
+    app = APIServerApp(env.server)
+    port = await app.start("127.0.0.1", 0)
+    with tempfile.TemporaryDirectory() as d:
+        with open(os.path.join(d, "token"), "w") as fh:
+            fh.write("tok-1")
+        cfg = load_kubeconfig(_kubeconfig(d, f"http://127.0.0.1:{port}"))
+        threads = []
+        orig_run = cfg.exec_provider.run
+
+        def run():
+            threads.append(threading.current_thread())
+            return orig_run()
+
+        cfg.exec_provider.run = run
+        c = Client(HttpTransport(cfg), qps=-1)
+        try:
+            with pytest.raises(errors.ApiError):
+                await c.get(CM, "default", "x")  # first credential (tok-1)
+            assert _runs(d) == 1
+            env.server.faults.add(verb="get", resource="configmaps", code=429, reason="TooManyRequests",
+                                  times=1, retry_after=1)
+            with open(os.path.join(d, "token"), "w") as fh:
+                fh.write("tok-2")
+            loop = asyncio.get_running_loop()
+
+            def rotate():  # during the Retry-After wait: tok-1 is revoked and its credential expires
+                env.server.tokens = {"tok-2": {"username": "u"}}
+                cfg._exec_creds.expires_at = 0.0
+
+            loop.call_later(0.3, rotate)
+            with pytest.raises(errors.ApiError) as e:
+                await c.get(CM, "default", "x")
+            assert e.value.code == 404  # retried with tok-2 (a stale tok-1 would be 401)
+            assert _runs(d) == 2
+            assert all(t is not threading.main_thread() for t in threads[1:]), threads
+        finally:
+            await c.close()
+            await app.stop()

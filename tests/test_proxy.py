@@ -197,6 +197,14 @@ def test_proxy_from_environment(monkeypatch):
     monkeypatch.setenv("HTTPS_PROXY", "socks5://s:1080")
     with pytest.raises(ConfigError, match="only http://"):
         proxy_from_environment("https://api.other.org")
+    # a client built in such an environment connects directly (warned once, at construction)
+    # instead of failing every request
+    from cron_operator_amd.runtime.http import HttpTransport
+
+    cfg = RestConfig(host="https://api.other.org")
+    assert cfg.proxy() == ""
+    t = HttpTransport(cfg)
+    assert t._proxy == "" and t._fast_pool()._proxy is None
 
 
 def test_kubeconfig_proxy_url():
