@@ -58,7 +58,7 @@ def all_bits(r: Bounds) -> int:
     return _bits(r[0], r[1], 1) | STAR_BIT
 
 
-_INT32_MAX = 2**63 - 1  # strconv.Atoi on 64-bit Go
+_GO_INT_MAX = 2**63 - 1  # strconv.Atoi on 64-bit Go
 
 
 def _atoi(expr: str) -> int:
@@ -68,7 +68,7 @@ def _atoi(expr: str) -> int:
     if body == "" or not all("0" <= c <= "9" for c in body):
         raise CronParseError(f'failed to parse int from {expr}: strconv.Atoi: parsing "{expr}": invalid syntax')
     v = int(s)
-    if v > _INT32_MAX or v < -_INT32_MAX - 1:
+    if v > _GO_INT_MAX or v < -_GO_INT_MAX - 1:
         raise CronParseError(f'failed to parse int from {expr}: strconv.Atoi: parsing "{expr}": value out of range')
     return v
 

@@ -3,7 +3,8 @@
 Behavioural contract: ``robfig/cron/v3`` ``ParseStandard`` + ``Schedule.Next`` as
 used by the reference at ``internal/controller/cron_controller.go:392,405,409,436``
 (upstream library is [ext], not vendored; semantics re-derived and pinned by the
-golden tables in ``tests/test_cron_golden.py``):
+hand-derived vectors and the native-vs-Python differential tests in
+``tests/test_cron_engine.py``):
 
 * a :class:`SpecSchedule` is six 64-bit field masks (second is fixed to ``0`` by
   the standard 5-field parser) with bit 63 (:data:`STAR_BIT`) recording that the
