@@ -112,15 +112,35 @@ class _ChildInfo:
     version instead of on every reconcile of its Cron (the 10 history children of a
     Cron were re-parsed ~2x per tick otherwise)."""
 
-    __slots__ = ("rv", "cls", "sort_key", "gvk", "active_ref", "history_entry")
+    __slots__ = ("rv", "cls", "sort_key", "gvk", "active_ref", "history_entry", "obj", "name", "uid", "err")
 
-    def __init__(self, rv: str, cls: Classification, sort_key: Any, gvk: GroupVersionKind):
+    def __init__(self, rv: str, cls: Optional[Classification], sort_key: Any, gvk: GroupVersionKind):
         self.rv = rv
         self.cls = cls
         self.sort_key = sort_key
         self.gvk = gvk
         self.active_ref: Optional[ObjectReference] = None
         self.history_entry: Optional[CronHistory] = None
+        self.obj: Optional[Dict[str, Any]] = None
+        self.name = ""
+        self.uid = ""
+        self.err: Optional[Exception] = None  # a status that cannot be decoded (kf.ConversionError)
+
+
+def child_info(w: Dict[str, Any], gvk: GroupVersionKind, policy: WorkloadPolicy) -> _ChildInfo:
+    """Everything a reconcile needs from child ``w`` (a cached object of the template's kind)."""
+    m = w.get("metadata") or {}
+    try:
+        cls: Optional[Classification] = classify(w, gvk, policy)
+        err = None
+    except kf.ConversionError as e:
+        cls, err = None, e
+    info = _ChildInfo(m.get("resourceVersion", ""), cls, creation_timestamp(w).key(), GroupVersionKind.from_object(w))
+    info.obj = w
+    info.name = m.get("name", "")
+    info.uid = m.get("uid", "")
+    info.err = err
+    return info
 
 
 # (child object, its classification, its memo record when the classification cache is on)
@@ -291,6 +311,9 @@ class CronReconciler(Reconciler):
         # key -> (status dict we last wrote, its parsed form): the next reconcile of that Cron
         # usually reads exactly that status back, so it skips re-parsing every history entry
         self._parsed_status: Dict[str, Tuple[Dict[str, Any], CronStatus]] = {}
+        # key -> (resourceVersion, status dict) of the Cron version is_own_write() proved to hold
+        # exactly that status: the next reconcile then trusts its memo without comparing again
+        self._own_rv: Dict[str, Tuple[str, Dict[str, Any]]] = {}
         # tick bookkeeping for latency: key -> (tick unix ns, wall perf_counter when it became due)
         self.latency_observer: Optional[Callable[[str, GoTime, Dict[str, Any]], None]] = None
 
@@ -298,6 +321,7 @@ class CronReconciler(Reconciler):
         """Drop the per-Cron memos of a Cron that is gone (``namespace/name``)."""
         self._parsed_status.pop(key, None)
         self.own_writes.pop(key, None)
+        self._own_rv.pop(key, None)
         self.expect.forget(key)
 
     def forget_child(self, uid: str) -> None:
@@ -332,9 +356,14 @@ class CronReconciler(Reconciler):
             return Result()
         parsed = None
         if self.opts.classification_cache:
-            memo = self._parsed_status.get(f"{req.namespace}/{req.name}")
-            if memo is not None and jsonutil.json_equal(old_obj.get("status") or {}, memo[0]):
-                parsed = memo[1].snapshot()
+            key = f"{req.namespace}/{req.name}"
+            memo = self._parsed_status.get(key)
+            if memo is not None:
+                ov = self._own_rv.get(key)
+                if (ov is not None and ov[1] is memo[0]
+                        and ov[0] == (old_obj.get("metadata") or {}).get("resourceVersion")) \
+                        or jsonutil.json_equal(old_obj.get("status") or {}, memo[0]):
+                    parsed = memo[1].snapshot()
         cron = Cron.from_dict(old_obj, status=parsed)
         old_status = cron.status.snapshot()
 
@@ -409,7 +438,8 @@ class CronReconciler(Reconciler):
         if old is new:  # periodic resync: always reconcile
             return False
         m = new.get("metadata") or {}
-        hit = self.own_writes.get(f"{m.get('namespace', '')}/{m.get('name', '')}")
+        key = f"{m.get('namespace', '')}/{m.get('name', '')}"
+        hit = self.own_writes.get(key)
         if hit is None:
             return False
         gen, status = hit
@@ -417,7 +447,10 @@ class CronReconciler(Reconciler):
             return False
         if old is not None and (old.get("metadata") or {}).get("deletionTimestamp") != m.get("deletionTimestamp"):
             return False
-        return jsonutil.json_equal(new.get("status") or {}, status)
+        if not jsonutil.json_equal(new.get("status") or {}, status):
+            return False
+        self._own_rv[key] = (m.get("resourceVersion", ""), status)
+        return True
 
     # ------------------------------------------------------------------ the algorithm
     async def _sync(self, cron: Cron, log: Logger, gc: Optional[List["asyncio.Future[None]"]] = None) -> Result:
@@ -430,10 +463,17 @@ class CronReconciler(Reconciler):
             return Result()
 
         # B4 (cron_controller.go:129-133)
+        infos: Optional[List[_ChildInfo]] = None
+        workloads: List[Dict[str, Any]] = []
         try:
             with tracing.span("list_children", kind=gvk.kind, mode=self.opts.list_mode) as sp:
-                workloads = await self.list_workloads(cron, gvk, log)
-                sp.set(count=len(workloads))
+                if self.opts.classification_cache and self.opts.list_mode != "live" and self.cache is not None:
+                    infos = await self.list_child_infos(cron, gvk, log)
+                if infos is None:
+                    workloads = await self.list_workloads(cron, gvk, log, force_live=self.cache is not None
+                                                          and self.opts.list_mode != "live"
+                                                          and self.opts.classification_cache)
+                sp.set(count=len(workloads) if infos is None else len(infos))
         except Exception as e:
             log.error(e, f"Failed to list {gvk.kind}")
             raise
@@ -441,6 +481,13 @@ class CronReconciler(Reconciler):
         # B5 (cron_controller.go:136-152)
         active: List[Child] = []
         terminated: List[Child] = []
+        if infos is not None:
+            # children classified once per version, at informer-event time (Informer.derive)
+            for info in infos:
+                if info.err is not None:
+                    log.error(info.err, f"Failed to get {gvk.kind} status")
+                    continue
+                (terminated if info.cls.finished else active).append((info.obj, info.cls, info))  # type: ignore
         cache = self._class_cache if self.opts.classification_cache else None
         for w in workloads:
             try:
@@ -593,12 +640,11 @@ class CronReconciler(Reconciler):
                                                                         missed_run))
         except ScheduleError:
             return False
-        for w, _, _ in active:
-            if (w.get("metadata") or {}).get("name") == ran_name:
-                return True
-        for w, _, _ in terminated:
-            if (w.get("metadata") or {}).get("name") == ran_name:
-                return True
+        for lst in (active, terminated):
+            for w, _, info in lst:
+                if (info.name if info is not None and info.obj is w else
+                        (w.get("metadata") or {}).get("name")) == ran_name:
+                    return True
         return False
 
     # ------------------------------------------------------------------ children
@@ -635,13 +681,46 @@ class CronReconciler(Reconciler):
             gctune.freeze()  # a newly synced child cache: long-lived, keep it out of GC scans
         return inf
 
-    async def list_workloads(self, cron: Cron, gvk: GroupVersionKind, log: Logger) -> List[Dict[str, Any]]:
+    async def list_child_infos(self, cron: Cron, gvk: GroupVersionKind, log: Logger) -> Optional[List[_ChildInfo]]:
+        """Cache mode: the Cron's children as :class:`_ChildInfo` memos kept by the child
+        informer (``Informer.derive``), adjusted by expectations; ``None`` when the informer
+        has not synced within ``child_sync_timeout`` (the caller LISTs live)."""
+        log.v(1).info(f"Listing {gvk.kind}")
+        inf = await self._synced_child_informer(gvk)
+        if inf is None:
+            return None
+        self.stats["lists"] += 1
+        if inf.derive is None:
+            policy = self.opts.workload
+            inf.set_derive(lambda o, g=gvk: child_info(o, g, policy))
+        key = f"{cron.namespace}/{cron.name}"
+        infos = inf.derived_by_index(CHILD_INDEX, key)
+        if self.opts.expectations and (key in self.expect.created or key in self.expect.deleted):
+            objs = [i.obj for i in infos]
+            adj = self.expect.adjust(key, objs)  # type: ignore[arg-type]
+            if adj is not objs:
+                by_id = {id(i.obj): i for i in infos}
+                infos = [by_id.get(id(o)) or self._extra_info(o, gvk) for o in adj]
+        return infos
+
+    def _extra_info(self, w: Dict[str, Any], gvk: GroupVersionKind) -> _ChildInfo:
+        """The memo of a child the informer has not delivered yet (our CREATE's response)."""
+        m = w.get("metadata") or {}
+        uid, rv = m.get("uid", ""), m.get("resourceVersion", "")
+        info = self._class_cache.get(uid)
+        if info is None or info.rv != rv or info.obj is not w:
+            info = child_info(w, gvk, self.opts.workload)
+            self._class_cache[uid] = info
+        return info
+
+    async def list_workloads(self, cron: Cron, gvk: GroupVersionKind, log: Logger,
+                             force_live: bool = False) -> List[Dict[str, Any]]:
         """``listWorkloads`` (``cron_controller.go:241-266``): children of the template GVK in
         the Cron's namespace labelled ``kubedl.io/cron-name=<name>``."""
         log.v(1).info(f"Listing {gvk.kind}")
         self.stats["lists"] += 1
         inf = None
-        if self.opts.list_mode != "live" and self.cache is not None:
+        if self.opts.list_mode != "live" and self.cache is not None and not force_live:
             inf = await self._synced_child_informer(gvk)
         if inf is None:
             lst = await self.client.list(gvk, cron.namespace, label_selector=f"{LABEL_CRON_NAME}={cron.name}")

@@ -121,6 +121,11 @@ class Informer:
         self._idle_limit = 0.0
         self._watchdog: Optional[asyncio.TimerHandle] = None
         self.transform = transform
+        # ``derive`` (set with :meth:`set_derive`): a per-object memo computed once per stored
+        # object version -- readers that only need facts derived from an object (a child's
+        # classification) take them from ``derived`` instead of re-reading the object
+        self.derive: Optional[Callable[[Dict[str, Any]], Any]] = None
+        self.derived: Dict[str, Any] = {}
         self.resync_period = resync_period
         self.clock = clock
         self._resync_timer: Optional[TimerHandle] = None
@@ -191,6 +196,17 @@ class Informer:
             objs = list(self.store.values())
         return [jsonutil.deepcopy(o) for o in objs] if copy else objs
 
+    def set_derive(self, fn: Callable[[Dict[str, Any]], Any]) -> None:
+        """Install the per-object memo function and compute it for what is stored already."""
+        self.derive = fn
+        self.derived = {k: fn(o) for k, o in self.store.items()}
+
+    def derived_by_index(self, index: str, value: str) -> List[Any]:
+        """``derive(obj)`` of every object under ``value`` of ``index``."""
+        keys = self.indices.get(index, {}).get(value, ())
+        d = self.derived
+        return [d[k] for k in keys]
+
     def by_index(self, index: str, value: str, copy: bool = True) -> List[Dict[str, Any]]:
         keys = self.indices.get(index, {}).get(value, ())
         objs = [self.store[k] for k in keys]
@@ -214,12 +230,16 @@ class Informer:
             if old is None:
                 return
             del self.store[key]
+            if self.derive is not None:
+                self.derived.pop(key, None)
             self._index(key, None, old)
             for h in self.handlers:
                 if h.on_delete:
                     h.on_delete(obj)
             return
         self.store[key] = obj
+        if self.derive is not None:
+            self.derived[key] = self.derive(obj)
         self._index(key, obj, old)
         if old is None:
             for h in self.handlers:

@@ -392,10 +392,13 @@ async def test_memos_dropped_when_crons_and_children_go_away():
                      "merge", "status")
     await env.settle()
     uid = env.server.get(PT, NS, job)["metadata"]["uid"]
-    assert uid in rec._class_cache and f"{NS}/m" in rec.own_writes and f"{NS}/m" in rec._parsed_status
+    # per-child memos live beside the cached object in the child informer (Informer.derive)
+    inf = next(i for g, i in rec.child_informers.items() if g.kind == "PyTorchJob")
+    assert inf.derived[f"{NS}/{job}"].uid == uid
+    assert f"{NS}/m" in rec.own_writes and f"{NS}/m" in rec._parsed_status
     env.server.delete(PT, NS, job)
     await env.settle()
-    assert uid not in rec._class_cache
+    assert f"{NS}/{job}" not in inf.derived and uid not in rec._class_cache
     env.server.delete(CRON_GVR, NS, "m")
     await env.settle()
     assert f"{NS}/m" not in rec.own_writes and f"{NS}/m" not in rec._parsed_status
