@@ -8,14 +8,15 @@ plain JSON trees (``dict``); these helpers read and write their metadata.
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, List, NamedTuple, Optional, Tuple
 
 from ..utils.gotime import GoTime, format_rfc3339_utc, parse_rfc3339
 
 
-@dataclass(frozen=True)
-class GroupVersion:
+class GroupVersion(NamedTuple):
+    """``schema.GroupVersion``.  This and the GVK/GVR types are named tuples: they key the
+    REST mapper, the informer cache and the path memo, so hashing runs in C."""
+
     group: str
     version: str
 
@@ -41,8 +42,7 @@ class GroupVersion:
         return GroupVersionResource(self.group, self.version, resource)
 
 
-@dataclass(frozen=True)
-class GroupVersionKind:
+class GroupVersionKind(NamedTuple):
     group: str
     version: str
     kind: str
@@ -59,16 +59,27 @@ class GroupVersionKind:
 
     @staticmethod
     def from_object(obj: Dict[str, Any]) -> "GroupVersionKind":
-        """``Unstructured.GroupVersionKind()``: an unparsable apiVersion yields empty."""
+        """``Unstructured.GroupVersionKind()``: an unparsable apiVersion yields empty.
+        Memoised per (apiVersion, kind): a handful of kinds recur on every event."""
+        av = obj.get("apiVersion") or ""
+        kind = obj.get("kind") or ""
+        hit = _GVK_MEMO.get((av, kind))
+        if hit is not None:
+            return hit
         try:
-            gv = GroupVersion.parse(obj.get("apiVersion") or "")
+            gv = GroupVersion.parse(av)
+            hit = GroupVersionKind(gv.group, gv.version, kind)
         except ValueError:
-            return GroupVersionKind("", "", "")
-        return GroupVersionKind(gv.group, gv.version, obj.get("kind") or "")
+            hit = GroupVersionKind("", "", "")
+        if len(_GVK_MEMO) < 4096:
+            _GVK_MEMO[(av, kind)] = hit
+        return hit
 
 
-@dataclass(frozen=True)
-class GroupVersionResource:
+_GVK_MEMO: Dict[Tuple[str, str], GroupVersionKind] = {}
+
+
+class GroupVersionResource(NamedTuple):
     group: str
     version: str
     resource: str
@@ -81,8 +92,10 @@ class GroupVersionResource:
         return f"{self.api_version}/{self.resource}"
 
 
-@dataclass(frozen=True)
-class NamespacedName:
+class NamespacedName(NamedTuple):
+    """``types.NamespacedName`` -- the work-queue key.  A named tuple so that hashing and
+    equality (every queue, dirty-set and rate-limiter lookup) run in C."""
+
     namespace: str
     name: str
 

@@ -333,7 +333,57 @@ class CronReconciler(Reconciler):
         """``Reconcile`` (``cron_controller.go:90-239``)."""
         log.info("Start reconciling Cron")
         try:
-            return await self._reconcile(req, log)
+            # B1: cache read; NotFound -> no-op (cron_controller.go:95-104)
+            inf = self.cron_informer
+            old_obj = inf.get(req.namespace, req.name, copy=False) if inf is not None else \
+                await self._get_cron(req)
+            if old_obj is None:
+                log.info("Skip reconciling Cron for it may have been deleted")
+                self.forget_cron(f"{req.namespace}/{req.name}")
+                return Result()
+            parsed = None
+            if self.opts.classification_cache:
+                key = f"{req.namespace}/{req.name}"
+                memo = self._parsed_status.get(key)
+                if memo is not None:
+                    ov = self._own_rv.get(key)
+                    if (ov is not None and ov[1] is memo[0]
+                            and ov[0] == (old_obj.get("metadata") or {}).get("resourceVersion")) \
+                            or jsonutil.json_equal(old_obj.get("status") or {}, memo[0]):
+                        parsed = memo[1].snapshot()
+            cron = Cron.from_dict(old_obj, status=parsed)
+            old_status = cron.status.snapshot()
+
+            result = Result()
+            err: Optional[BaseException] = None
+            gc: Optional[List["asyncio.Future[None]"]] = [] if self.opts.overlap_gc_deletes else None
+            try:
+                result = await self._sync(cron, log, gc)
+            except Exception as e:  # noqa: BLE001 - joined with the patch error below
+                err = e
+            # B2: deferred status patch when status changed semantically (cron_controller.go:107-120)
+            if not old_status.semantic_equal(cron.status):
+                try:
+                    if gc:
+                        # the DELETE tasks are already running: the PATCH overlaps them
+                        pending, gc = gc, None
+                        try:
+                            await self._patch_status(old_obj, cron, log)
+                        finally:
+                            await self._await_gc(pending)
+                    else:
+                        await self._patch_status(old_obj, cron, log)
+                except Exception as pe:  # noqa: BLE001
+                    perr = RuntimeError(f"failed to patch Cron status: {pe}")
+                    perr.__cause__ = pe
+                    err = JoinedError(err, perr) if err is not None else perr
+                if err is not None:
+                    result = Result()
+            if gc:
+                await self._await_gc(gc)
+            if err is not None:
+                raise err
+            return result
         finally:
             log.info("Finish reconciling Cron")
 
@@ -347,60 +397,17 @@ class CronReconciler(Reconciler):
                 return None
             raise
 
-    async def _reconcile(self, req: Request, log: Logger) -> Result:
-        # B1: cache read; NotFound -> no-op (cron_controller.go:95-104)
-        old_obj = await self._get_cron(req)
-        if old_obj is None:
-            log.info("Skip reconciling Cron for it may have been deleted")
-            self.forget_cron(f"{req.namespace}/{req.name}")
-            return Result()
-        parsed = None
-        if self.opts.classification_cache:
-            key = f"{req.namespace}/{req.name}"
-            memo = self._parsed_status.get(key)
-            if memo is not None:
-                ov = self._own_rv.get(key)
-                if (ov is not None and ov[1] is memo[0]
-                        and ov[0] == (old_obj.get("metadata") or {}).get("resourceVersion")) \
-                        or jsonutil.json_equal(old_obj.get("status") or {}, memo[0]):
-                    parsed = memo[1].snapshot()
-        cron = Cron.from_dict(old_obj, status=parsed)
-        old_status = cron.status.snapshot()
-
-        result = Result()
-        err: Optional[BaseException] = None
-        gc: Optional[List["asyncio.Future[None]"]] = [] if self.opts.overlap_gc_deletes else None
-        try:
-            result = await self._sync(cron, log, gc)
-        except Exception as e:  # noqa: BLE001 - joined with the patch error below
-            err = e
-        # B2: deferred status patch when status changed semantically (cron_controller.go:107-120)
-        if not old_status.semantic_equal(cron.status):
-            try:
-                if gc:
-                    pending, gc = gc, None
-                    perr0, _ = await asyncio.gather(self._patch_status(old_obj, cron, log), self._await_gc(pending),
-                                                    return_exceptions=True)
-                    if isinstance(perr0, BaseException):
-                        raise perr0
-                else:
-                    await self._patch_status(old_obj, cron, log)
-            except Exception as pe:  # noqa: BLE001
-                perr = RuntimeError(f"failed to patch Cron status: {pe}")
-                perr.__cause__ = pe
-                err = JoinedError(err, perr) if err is not None else perr
-            if err is not None:
-                result = Result()
-        if gc:
-            await self._await_gc(gc)
-        if err is not None:
-            raise err
-        return result
-
     @staticmethod
     async def _await_gc(gc: List["asyncio.Future[None]"]) -> None:
-        """Wait for every overlapped GC DELETE; each logs its own API error (B7)."""
-        await asyncio.gather(*gc, return_exceptions=True)
+        """Wait for every overlapped GC DELETE; each logs its own API error (B7), anything
+        else it raised is dropped like ``gather(return_exceptions=True)`` would."""
+        for f in gc:
+            try:
+                await f
+            except asyncio.CancelledError:
+                raise
+            except Exception:  # noqa: BLE001
+                pass
 
     async def _patch_status(self, old_obj: Dict[str, Any], cron: Cron, log: Logger) -> None:
         new_status = cron.status.to_dict(shared=True)

@@ -243,6 +243,13 @@ class Client:
         self._m_rl: Dict[str, Any] = {}
 
     # -- plumbing
+    def _gvr_now(self, target: GVRorGVK) -> Optional[GroupVersionResource]:
+        """The resource of ``target`` without a discovery round trip (None: not known yet)."""
+        if target.__class__ is GroupVersionResource:
+            return target  # type: ignore[return-value]
+        hit = self.mapper._gvk.get(target)  # type: ignore[arg-type]
+        return hit[0] if hit is not None else None
+
     async def _gvr(self, target: GVRorGVK) -> GroupVersionResource:
         if isinstance(target, GroupVersionResource):
             return target
@@ -261,13 +268,14 @@ class Client:
 
     async def _do(self, verb: str, gvr: GroupVersionResource, namespace: str = "", name: str = "",
                   subresource: str = "", body: Any = None, params: Optional[Dict[str, Any]] = None) -> Any:
-        await self._throttle(verb)
+        if self.limiter is not None:
+            await self._throttle(verb)
         self.requests += 1
         self.requests_by_verb[verb] = self.requests_by_verb.get(verb, 0) + 1
         t0 = time.perf_counter()
         code = "200"
         sp = tracing.span("http." + verb, resource=gvr.resource + ("/" + subresource if subresource else ""),
-                          namespace=namespace, name=name)
+                          namespace=namespace, name=name) if tracing.get_tracer().enabled else tracing.NOOP
         try:
             with sp:
                 return await self.transport.request(verb, gvr, namespace, name, subresource, body, params)
@@ -292,7 +300,8 @@ class Client:
 
     # -- verbs
     async def get(self, target: GVRorGVK, namespace: str, name: str) -> Dict[str, Any]:
-        return await self._do("get", await self._gvr(target), namespace, name)
+        gvr = self._gvr_now(target) or await self._gvr(target)
+        return await self._do("get", gvr, namespace, name)
 
     async def list(self, target: GVRorGVK, namespace: str = "", label_selector: Optional[str] = None,
                    field_selector: Optional[str] = None, limit: int = 0,
@@ -306,7 +315,8 @@ class Client:
             params["limit"] = limit
         if continue_:
             params["continue"] = continue_
-        return await self._do("list", await self._gvr(target), namespace, params=params)
+        gvr = self._gvr_now(target) or await self._gvr(target)
+        return await self._do("list", gvr, namespace, params=params)
 
     async def table(self, target: GVRorGVK, namespace: str = "", name: str = "",
                     label_selector: Optional[str] = None) -> Dict[str, Any]:
@@ -314,7 +324,8 @@ class Client:
         params: Dict[str, Any] = {ACCEPT: TABLE_ACCEPT}
         if label_selector:
             params["labelSelector"] = label_selector
-        return await self._do("get" if name else "list", await self._gvr(target), namespace, name, params=params)
+        gvr = self._gvr_now(target) or await self._gvr(target)
+        return await self._do("get" if name else "list", gvr, namespace, name, params=params)
 
     async def list_all(self, target: GVRorGVK, namespace: str = "", label_selector: Optional[str] = None,
                        page_size: int = 500) -> Dict[str, Any]:
@@ -338,12 +349,14 @@ class Client:
     async def create(self, target: GVRorGVK, obj: Dict[str, Any], namespace: Optional[str] = None,
                      dry_run: bool = False) -> Dict[str, Any]:
         ns = namespace if namespace is not None else (obj.get("metadata") or {}).get("namespace", "")
-        return await self._do("create", await self._gvr(target), ns, body=obj,
+        gvr = self._gvr_now(target) or await self._gvr(target)
+        return await self._do("create", gvr, ns, body=obj,
                               params={"dryRun": "All"} if dry_run else None)
 
     async def update(self, target: GVRorGVK, obj: Dict[str, Any], subresource: str = "") -> Dict[str, Any]:
         m = obj.get("metadata") or {}
-        return await self._do("update", await self._gvr(target), m.get("namespace", ""), m.get("name", ""),
+        gvr = self._gvr_now(target) or await self._gvr(target)
+        return await self._do("update", gvr, m.get("namespace", ""), m.get("name", ""),
                               subresource, body=obj)
 
     async def patch(self, target: GVRorGVK, namespace: str, name: str, patch: Any, patch_type: str = MERGE,
@@ -353,7 +366,8 @@ class Client:
         params: Dict[str, Any] = {"patchType": patch_type}
         if discard_response:
             params[DISCARD] = True
-        return await self._do("patch", await self._gvr(target), namespace, name, subresource, body=patch,
+        gvr = self._gvr_now(target) or await self._gvr(target)
+        return await self._do("patch", gvr, namespace, name, subresource, body=patch,
                               params=params)
 
     async def delete(self, target: GVRorGVK, namespace: str, name: str, propagation_policy: Optional[str] = None,
@@ -363,17 +377,20 @@ class Client:
             opts["propagationPolicy"] = propagation_policy
         if preconditions:
             opts["preconditions"] = preconditions
-        return await self._do("delete", await self._gvr(target), namespace, name, body=opts or None,
+        gvr = self._gvr_now(target) or await self._gvr(target)
+        return await self._do("delete", gvr, namespace, name, body=opts or None,
                               params={DISCARD: True} if discard_response else None)
 
     async def delete_all_of(self, target: GVRorGVK, namespace: str = "", label_selector: Optional[str] = None) -> Any:
         params = {"labelSelector": label_selector} if label_selector else {}
-        return await self._do("deletecollection", await self._gvr(target), namespace, params=params)
+        gvr = self._gvr_now(target) or await self._gvr(target)
+        return await self._do("deletecollection", gvr, namespace, params=params)
 
     async def watch(self, target: GVRorGVK, namespace: str = "", resource_version: str = "",
                     label_selector: Optional[str] = None, field_selector: Optional[str] = None,
                     allow_bookmarks: bool = True, timeout_seconds: Optional[int] = None) -> WatchStream:
-        gvr = await self._gvr(target)
+        gvr = self._gvr_now(target) or await self._gvr(target)
+        gvr = gvr
         await self._throttle("watch")
         self.requests += 1
         self.requests_by_verb["watch"] = self.requests_by_verb.get("watch", 0) + 1

@@ -132,8 +132,15 @@ class Controller:
             def mapper(obj: Dict[str, Any]) -> List[Request]:  # type: ignore[no-redef]
                 return [r for r in inner(obj) if shard_of(r.namespace, r.name, count) == index]
 
-        def ok(event: str, old: Optional[Dict[str, Any]], new: Dict[str, Any]) -> bool:
-            return all(p(event, old, new) for p in predicates)
+        ok: Predicate
+        if len(predicates) == 1:
+            ok = predicates[0]  # the common case: no generator per event
+        else:
+            def ok(event: str, old: Optional[Dict[str, Any]], new: Dict[str, Any]) -> bool:
+                for p in predicates:
+                    if not p(event, old, new):
+                        return False
+                return True
 
         def on_add(obj: Dict[str, Any]) -> None:
             if ok("create", None, obj):

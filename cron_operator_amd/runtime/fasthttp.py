@@ -51,7 +51,7 @@ class ConnectionFailed(Exception):
 
 class _Conn(asyncio.Protocol):
     __slots__ = ("transport", "buf", "fut", "alive", "used", "_state", "_status", "_clen", "_chunked",
-                 "_close_after", "_body", "_got_any", "retry_after", "ssl_gen")
+                 "_close_after", "_body", "_got_any", "retry_after", "ssl_gen", "deadline")
 
     def __init__(self) -> None:
         self.transport: Optional[asyncio.Transport] = None
@@ -60,6 +60,7 @@ class _Conn(asyncio.Protocol):
         self.alive = True
         self.used = 0
         self.ssl_gen = 0         # HttpPool TLS-context generation this connection was made with
+        self.deadline = 0.0      # loop time by which the in-flight response must have arrived
         self._reset()
 
     def _reset(self) -> None:
@@ -387,6 +388,12 @@ def _expire(fut: asyncio.Future) -> None:
         fut.set_exception(asyncio.TimeoutError())
 
 
+# request deadlines are checked by one sweep timer per pool instead of a timer per request
+# (a TimerHandle, a heap push and a cancel on every call); the sweep runs at most this often,
+# and at least four times per timeout
+SWEEP_INTERVAL = 1.0
+
+
 class _Tunnel(asyncio.Protocol):
     """Reads a proxy's answer to ``CONNECT``; ``done`` resolves to its status code."""
 
@@ -445,6 +452,9 @@ class HttpPool:
         self.connects = 0
         self._closed = False
         self._ssl_gen = 0
+        self._busy: set = set()   # connections with a request in flight (deadline sweep)
+        self._sweeper: Optional[asyncio.TimerHandle] = None
+        self._sweep_every = min(SWEEP_INTERVAL, max(0.01, timeout / 4))
 
     def set_headers(self, headers: Optional[Dict[str, str]]) -> None:
         """Replace the headers sent with every request (e.g. a rotated ``Authorization``)."""
@@ -534,12 +544,16 @@ class HttpPool:
         else:
             data = (head + ("Content-Length: 0\r\n\r\n" if method in ("POST", "PUT", "PATCH") else "\r\n")
                     ).encode("latin-1")
+        loop = asyncio.get_running_loop()
         for attempt in (0, 1):
             conn = self._take_idle() if attempt == 0 else None
             if conn is None:
                 conn = await self._connect()
             fut = conn.send(data)
-            timer = asyncio.get_running_loop().call_later(self.timeout, _expire, fut)
+            conn.deadline = loop.time() + self.timeout
+            self._busy.add(conn)
+            if self._sweeper is None:
+                self._sweeper = loop.call_later(self._sweep_every, self._sweep)
             try:
                 status, raw, retry_after = await fut
             except ConnectionFailed as e:
@@ -558,10 +572,23 @@ class HttpPool:
                     conn.transport.close()
                 raise
             finally:
-                timer.cancel()
+                self._busy.discard(conn)
             self._give_back(conn)
             return status, raw, retry_after
         raise ConnectionFailed("unreachable", True, False)  # pragma: no cover
+
+    def _sweep(self) -> None:
+        """Fail every in-flight request past its deadline; re-arm while any is in flight."""
+        self._sweeper = None
+        if not self._busy:
+            return
+        loop = asyncio.get_running_loop()
+        now = loop.time()
+        for c in [c for c in self._busy if c.deadline <= now]:
+            if c.fut is not None:
+                _expire(c.fut)
+        if self._busy:
+            self._sweeper = loop.call_later(self._sweep_every, self._sweep)
 
     async def open_stream(self, path: str, decode, accept: str = "application/json") -> Stream:
         """GET ``path`` on a dedicated connection and stream its body line by line
@@ -581,6 +608,9 @@ class HttpPool:
 
     async def close(self) -> None:
         self._closed = True
+        if self._sweeper is not None:
+            self._sweeper.cancel()
+            self._sweeper = None
         while self._idle:
             c = self._idle.pop()
             if c.transport is not None:

@@ -25,7 +25,22 @@ from .fasthttp import ConnectionFailed, HttpPool, HttpStatusError, Stream, encod
 from .kubeconfig import RestConfig
 
 
+_PATHS: Dict[Tuple[GroupVersionResource, str, str, str], str] = {}
+
+
 def resource_path(gvr: GroupVersionResource, namespace: str = "", name: str = "", sub: str = "") -> str:
+    """The REST path of a resource (collection when ``name`` is empty).  Memoised: a Cron's
+    status path and its children's paths repeat on every reconcile."""
+    key = (gvr, namespace, name, sub)
+    p = _PATHS.get(key)
+    if p is None:
+        if len(_PATHS) >= 1 << 16:
+            _PATHS.clear()
+        p = _PATHS[key] = _resource_path(gvr, namespace, name, sub)
+    return p
+
+
+def _resource_path(gvr: GroupVersionResource, namespace: str, name: str, sub: str) -> str:
     base = f"/api/{gvr.version}" if not gvr.group else f"/apis/{gvr.group}/{gvr.version}"
     if namespace:
         base += f"/namespaces/{quote(namespace, safe='')}"
@@ -38,8 +53,10 @@ def resource_path(gvr: GroupVersionResource, namespace: str = "", name: str = ""
 
 
 def _clean(params: Optional[Dict[str, Any]]) -> Dict[str, str]:
-    out = {}
-    for k, v in (params or {}).items():
+    out: Dict[str, str] = {}
+    if not params:
+        return out
+    for k, v in params.items():
         if k == "patchType" or k.startswith("_") or v is None or v == "":
             continue
         out[k] = str(v)

@@ -170,6 +170,20 @@ class Informer:
     def _index(self, key: str, obj: Optional[Dict[str, Any]], old: Optional[Dict[str, Any]]) -> None:
         for name, fn in self.indexers.items():
             idx = self.indices[name]
+            if old is not None and obj is not None:
+                ov = fn(old)
+                nv = fn(obj)
+                if ov == nv:
+                    continue  # an update that keeps its index values: the key is filed already
+                for v in ov:
+                    s = idx.get(v)
+                    if s is not None:
+                        s.discard(key)
+                        if not s:
+                            del idx[v]
+                for v in nv:
+                    idx.setdefault(v, set()).add(key)
+                continue
             if old is not None:
                 for v in fn(old):
                     s = idx.get(v)

@@ -57,6 +57,7 @@ def main() -> int:
     buf.write(f"# operator-process cProfile of the {a.steps} timed steps ({a.mode}/{a.transport}, {a.crons} Crons, "
               f"{a.warmup} warmup steps excluded; profiler overhead inflates absolute times)\n")
     buf.write(f"# {summarize(res)}\n# wall {wall:.2f} s, operator CPU {cpu:.2f} s\n\n")
+    prof.dump_stats(a.out + ".operator.pstats")
     st = pstats.Stats(prof, stream=buf)
     st.sort_stats("tottime").print_stats(a.top)
     st.sort_stats("cumulative").print_stats(a.top)
