@@ -475,7 +475,13 @@ class CronReconciler(Reconciler):
         try:
             with tracing.span("list_children", kind=gvk.kind, mode=self.opts.list_mode) as sp:
                 if self.opts.classification_cache and self.opts.list_mode != "live" and self.cache is not None:
-                    infos = await self.list_child_infos(cron, gvk, log)
+                    inf = self.child_informers.get(gvk)
+                    if inf is not None and inf.derive is not None and inf.synced.is_set():
+                        if log.enabled():
+                            log.v(1).info(f"Listing {gvk.kind}")
+                        infos = self._child_infos(inf, cron, gvk)  # the steady state: no await
+                    else:
+                        infos = await self.list_child_infos(cron, gvk, log)
                 if infos is None:
                     workloads = await self.list_workloads(cron, gvk, log, force_live=self.cache is not None
                                                           and self.opts.list_mode != "live"
@@ -516,11 +522,19 @@ class CronReconciler(Reconciler):
                 log.error(e, f"Failed to get {gvk.kind} status")
                 continue
             (terminated if c.finished else active).append((w, c, info))
-        log.info(f"{gvk.kind} count", active=len(active), terminated=len(terminated))
+        chatty = log.enabled()  # info logging on: skip building messages nobody writes otherwise
+        if chatty:
+            log.info(f"{gvk.kind} count", active=len(active), terminated=len(terminated))
 
         # B6/B7/B8 (cron_controller.go:155-158)
         with tracing.span("sync_status", active=len(active), terminated=len(terminated)):
-            await self.sync_status(cron, gvk, active, terminated, log, gc)
+            if gc is not None:  # DELETEs are only started: nothing to await here
+                if chatty:
+                    log.v(1).info("Syncing Cron status")
+                self.sync_active_list(cron, gvk, active, log)
+                self._sync_history(cron, terminated, log, gc)
+            else:
+                await self.sync_status(cron, gvk, active, terminated, log, gc)
 
         now = self.clock.now(LOCAL)
 
@@ -599,7 +613,8 @@ class CronReconciler(Reconciler):
         # B19 (cron_controller.go:227-236)
         wm = workload["metadata"]
         ref = ObjectRef(wm.get("namespace", ""), wm.get("name", ""))
-        log.info(f"Creating {gvk.kind}", **{gvk.kind: ref})
+        if chatty:
+            log.info(f"Creating {gvk.kind}", **{gvk.kind: ref})
         if self.opts.expectations:
             self.expect.expect_pending(self._ckey(cron), wm.get("name", ""))
         try:
@@ -696,10 +711,14 @@ class CronReconciler(Reconciler):
         inf = await self._synced_child_informer(gvk)
         if inf is None:
             return None
-        self.stats["lists"] += 1
         if inf.derive is None:
             policy = self.opts.workload
             inf.set_derive(lambda o, g=gvk: child_info(o, g, policy))
+        return self._child_infos(inf, cron, gvk)
+
+    def _child_infos(self, inf: Informer, cron: Cron, gvk: GroupVersionKind) -> List[_ChildInfo]:
+        """The Cron's children from the synced informer's memos, adjusted by expectations."""
+        self.stats["lists"] += 1
         key = f"{cron.namespace}/{cron.name}"
         infos = inf.derived_by_index(CHILD_INDEX, key)
         if self.opts.expectations and (key in self.expect.created or key in self.expect.deleted):
@@ -762,7 +781,8 @@ class CronReconciler(Reconciler):
     def sync_active_list(self, cron: Cron, gvk: GroupVersionKind, active: List[Child],
                          log: Logger) -> None:
         """``syncActiveList`` (``cron_controller.go:284-304``)."""
-        log.v(1).info("Syncing active list")
+        if log.enabled():
+            log.v(1).info("Syncing active list")
         self._sort(active)
         refs = []
         with_rv = self.opts.active_ref_resource_version
@@ -787,7 +807,17 @@ class CronReconciler(Reconciler):
 
         With ``gc`` (a list) the DELETEs are started and appended there instead of
         awaited one by one (``ReconcilerOptions.overlap_gc_deletes``)."""
-        log.v(1).info("Syncing Cron history")
+        for op in self._sync_history(cron, terminated, log, gc):
+            await op
+
+    def _sync_history(self, cron: Cron, terminated: List[Child], log: Logger,
+                      gc: Optional[List["asyncio.Future[None]"]]) -> List[Any]:
+        """The body of :meth:`sync_cron_history`.  GC DELETEs go to ``gc`` as started tasks,
+        or (``gc`` is None) are returned as coroutines for the caller to await in order."""
+        chatty = log.enabled()
+        if chatty:
+            log.v(1).info("Syncing Cron history")
+        ops: List[Any] = []
         self._sort(terminated)
         n = len(terminated)
         limit = cron.spec.history_limit if cron.spec.history_limit is not None else MAX_INT
@@ -804,13 +834,14 @@ class CronReconciler(Reconciler):
             wgvk = GroupVersionKind.from_object(w)
             ref = ObjectRef(m.get("namespace", ""), m.get("name", ""))
             if i < n - limit:
-                log.info(f"Deleting terminated {wgvk.kind}", **{wgvk.kind: ref})
+                if chatty:
+                    log.info(f"Deleting terminated {wgvk.kind}", **{wgvk.kind: ref})
                 uid = m.get("uid", "")
                 if self.opts.expectations:  # before the call: the watch event may beat the response
                     self.expect.expect_delete(self._ckey(cron), uid)
                 op = self._gc_delete(cron, wgvk, m.get("namespace", ""), m.get("name", ""), uid, ref, log)
                 if gc is None:
-                    await op
+                    ops.append(op)
                 else:
                     gc.append(asyncio.ensure_future(op))
                 continue
@@ -841,6 +872,7 @@ class CronReconciler(Reconciler):
                         entry.finished = GoTime(t.sec, 0, t.loc)
             history.append(entry)
         cron.status.history = history
+        return ops
 
     async def _gc_delete(self, cron: Cron, gvk: GroupVersionKind, namespace: str, name: str, uid: str,
                          ref: ObjectRef, log: Logger) -> None:
