@@ -441,8 +441,25 @@ def _helm_template(a: argparse.Namespace) -> int:
     return 0
 
 
+SUBCOMMANDS = ("start", "fake-apiserver", "get", "crd", "kustomize", "helm-template", "version")
+
+
+def cobra_order(argv: List[str]) -> List[str]:
+    """Accept a subcommand's flags before its name, as cobra does: it strips leading flags to
+    find the subcommand, which then parses every remaining flag.  The reference's kustomize
+    tree relies on it -- its metrics patch inserts ``--metrics-bind-address=:8443`` at
+    ``args[0]``, ahead of ``start`` (``config/default/manager_metrics_patch.yaml``)."""
+    if not argv or not argv[0].startswith("-") or argv[0] in ("-h", "--help"):
+        return list(argv)
+    for i, tok in enumerate(argv):
+        if tok in SUBCOMMANDS:
+            return [tok] + list(argv[:i]) + list(argv[i + 1:])
+    return list(argv)
+
+
 def main(argv: Optional[List[str]] = None) -> int:
     parser = build_parser()
+    argv = cobra_order(sys.argv[1:] if argv is None else argv)
     a = parser.parse_args(argv)
     if a.command is None:
         parser.print_help()
@@ -487,7 +504,7 @@ def main(argv: Optional[List[str]] = None) -> int:
         if a.cron_engine != "auto":
             os.environ["CRON_OPERATOR_ENGINE"] = a.cron_engine
         if a.shard_processes > 1:
-            return asyncio.run(run_supervisor(a, list(sys.argv[1:] if argv is None else argv)))
+            return asyncio.run(run_supervisor(a, list(argv)))
         if a.shard_processes < 1:
             print("invalid argument: --shard-processes must be >= 1", file=sys.stderr)
             return 2

@@ -35,7 +35,13 @@ from ..utils.gotime import GoTime, UTC
 from ..utils.logging import get_logger
 
 JOB_GVRS = [GroupVersionResource("kubeflow.org", "v1", r) for r in
-            ("pytorchjobs", "tfjobs", "xgboostjobs", "paddlejobs", "jaxjobs", "mpijobs")]
+            ("pytorchjobs", "tfjobs", "xgboostjobs", "paddlejobs", "jaxjobs", "mpijobs")] + \
+    [GroupVersionResource("kubeflow.org", "v1alpha1", "mpijobs")]  # the reference's MPI example (cron-mpi.yaml)
+
+
+def _mpi_v1alpha1(gvr: GroupVersionResource) -> bool:
+    """MPIJob v1alpha1: no conditions, the launcher's phase in ``status.launcherStatus``."""
+    return gvr.version == "v1alpha1" and gvr.resource == "mpijobs"
 
 # replica-type order used to pick the "master" process in real mode
 _MASTER_TYPES = ("Master", "Chief", "Launcher", "Worker", "PS", "Evaluator")
@@ -99,8 +105,9 @@ class FakeTrainingOperator:
 
     async def mark_running(self, gvr: GroupVersionResource, obj: Dict[str, Any]) -> None:
         m = obj["metadata"]
-        await self._write_status(gvr, m["namespace"], m["name"],
-                                 running_status(obj.get("kind", ""), m["name"], _now_str(self.clock)))
+        st = {"launcherStatus": "Active"} if _mpi_v1alpha1(gvr) else \
+            running_status(obj.get("kind", ""), m["name"], _now_str(self.clock))
+        await self._write_status(gvr, m["namespace"], m["name"], st)
 
     async def complete(self, gvr: GroupVersionResource, ns: str, name: str, succeeded: bool = True) -> None:
         kind = gvr.resource
@@ -110,7 +117,7 @@ class FakeTrainingOperator:
             start = (obj.get("status") or {}).get("startTime")
         except errors.ApiError:
             start = None
-        if gvr.version == "v1alpha1" and gvr.resource == "mpijobs":
+        if _mpi_v1alpha1(gvr):
             st = {"launcherStatus": "Succeeded" if succeeded else "Failed", "completionTime": _now_str(self.clock)}
         else:
             st = finished_status(kind, name, _now_str(self.clock), succeeded, start)

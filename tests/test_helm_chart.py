@@ -107,7 +107,7 @@ def test_tolerations_concat():
 
 def test_host_timezone_mount():
     s = spec({"useHostTimezone": True})
-    assert s["volumes"] == [{"name": "host-localtime", "hostPath": {"path": "/etc/localtime"}}]
+    assert s["volumes"] == [{"name": "volume-localtime", "hostPath": {"path": "/etc/localtime"}}]
     assert s["containers"][0]["volumeMounts"][0]["mountPath"] == "/etc/localtime"
     assert "volumes" not in spec({})
 
@@ -135,11 +135,12 @@ def test_service():
 
 
 def test_rbac_rules_match_generator_and_group_is_correct():
-    docs = render_chart(CHART)["rbac.yaml"]
-    role = [d for d in docs if d["kind"] == "ClusterRole"][0]
+    out = render_chart(CHART)
+    role = out["cluster_role.yaml"][0]
+    assert role["kind"] == "ClusterRole"
     assert role["rules"] == RULES
     assert any("apps.kubedl.io" in r["apiGroups"] and "crons" in r["resources"] for r in role["rules"])
-    binding = [d for d in docs if d["kind"] == "ClusterRoleBinding"][0]
+    binding = out["cluster_role_binding.yaml"][0]
     assert binding["roleRef"] == {"apiGroup": "rbac.authorization.k8s.io", "kind": "ClusterRole",
                                   "name": "cron-operator"}
     assert binding["subjects"] == [{"kind": "ServiceAccount", "name": "cron-operator", "namespace": "cron-operator"}]
@@ -147,8 +148,8 @@ def test_rbac_rules_match_generator_and_group_is_correct():
 
 def test_extra_workload_rules():
     docs = render_chart(CHART, {"rbac": {"extraWorkloadRules": [{"apiGroups": ["ray.io"],
-                                                                 "resources": ["rayjobs"]}]}})["rbac.yaml"]
-    role = [d for d in docs if d["kind"] == "ClusterRole"][0]
+                                                                 "resources": ["rayjobs"]}]}})["cluster_role.yaml"]
+    role = docs[0]
     assert role["rules"][-1]["apiGroups"] == ["ray.io"]
 
 
@@ -215,3 +216,27 @@ tests:
 """)
     res = run_suite(str(suite), CHART)
     assert [r.passed for r in res] == [False, False]
+
+
+REF_CHART_TESTS = "/root/reference/charts/cron-operator/tests"
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_CHART_TESTS), reason="reference checkout not mounted")
+def test_reference_helm_unittest_suites_pass_against_this_chart(tmp_path):
+    """Parity pin: the reference's OWN helm-unittest suites (``charts/cron-operator/tests/*_test.yaml``,
+    run by its ``make helm-unittest``) assert against this chart, unmodified.  The template files carry
+    the reference's names (``cluster_role.yaml``, ``cluster_role_binding.yaml``,
+    ``service_account.yaml``) so every suite resolves its templates."""
+    import shutil
+
+    from cron_operator_amd.utils.helmunittest import run_all
+
+    chart = tmp_path / "chart"
+    shutil.copytree(CHART, chart, ignore=shutil.ignore_patterns("tests"))
+    (chart / "tests").mkdir()
+    for name in sorted(os.listdir(REF_CHART_TESTS)):
+        if name.endswith("_test.yaml"):
+            shutil.copy(os.path.join(REF_CHART_TESTS, name), chart / "tests" / name)
+    passed, failed, results = run_all(str(chart))
+    assert failed == 0, [(r.suite, r.name, r.failures) for r in results if not r.passed]
+    assert passed >= 20

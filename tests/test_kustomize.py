@@ -261,3 +261,32 @@ def test_replacements_semantics(tmp_path):
     (tmp_path / "kustomization.yaml").write_text(yaml.safe_dump(k))
     with pytest.raises(KustomizeError):
         build(str(tmp_path))
+
+
+REF_CONFIG = "/root/reference/config/default"
+
+
+@pytest.mark.skipif(not os.path.isdir(REF_CONFIG), reason="reference checkout not mounted")
+def test_reference_config_tree_builds_with_this_renderer():
+    """Parity pin for the kustomize subset: the reference's own ``config/default`` tree
+    (``make build-installer``, Makefile) renders with ``utils/kustomize.py``: the
+    ``cron-operator-`` name prefix and ``cron-operator-system`` namespace land on every object,
+    the metrics JSON6902 patch inserts ``--metrics-bind-address=:8443`` at ``args[0]``
+    (``config/default/manager_metrics_patch.yaml``), and this CLI parses the resulting args."""
+    from cron_operator_amd.cmd.main import build_parser, cobra_order
+
+    objs = build_sorted(REF_CONFIG)
+    kinds = sorted(o["kind"] for o in objs)
+    assert kinds.count("ClusterRole") == 6 and kinds.count("Deployment") == 1 \
+        and kinds.count("CustomResourceDefinition") == 1
+    for o in objs:
+        m = o["metadata"]
+        if o["kind"] not in ("Namespace", "CustomResourceDefinition"):
+            assert m["name"].startswith("cron-operator-"), m["name"]
+        if o["kind"] in ("Deployment", "Service", "ServiceAccount", "Role", "RoleBinding"):
+            assert m["namespace"] == "cron-operator-system", (o["kind"], m)
+    (dep,) = by_kind(objs, "Deployment")
+    args = dep["spec"]["template"]["spec"]["containers"][0]["args"]
+    assert args[0] == "--metrics-bind-address=:8443" and "start" in args and "--leader-elect" in args
+    ns = build_parser().parse_args(cobra_order(args))
+    assert ns.metrics_bind_address == ":8443" and ns.leader_elect

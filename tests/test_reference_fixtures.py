@@ -1,0 +1,92 @@
+"""Parity pins against fixtures the reference itself ships (skipped when it is not mounted).
+
+The reference's envtest suite (``internal/controller/suite_test.go:53-124``) installs the
+Cron CRD from ``charts/cron-operator/crds`` and the Kubeflow CRDs from ``test/crds``.
+Here the fake apiserver is given exactly those files (not this repo's CRD generator or
+its slim training-operator schemas), and the reference's own example Crons
+(``examples/v1alpha1/cron/cron-{pytorch,tf,mpi}.yaml``) run through several schedule
+ticks in both reconciler modes.  Every object the operator writes -- the workloads built
+from the templates, the Cron status patches -- is admitted by the reference's structural
+schemas, and the fake training-operator's finished-status writes are too.
+"""
+from __future__ import annotations
+
+import os
+
+import pytest
+import yaml
+
+from cron_operator_amd.api.meta import GroupVersionResource
+from cron_operator_amd.api.v1alpha1 import CRON_GVR, LABEL_CRON_NAME
+from cron_operator_amd.controller.reconciler import ReconcilerOptions
+from cron_operator_amd.testing.env import TestEnv
+from cron_operator_amd.trainingop.operator import FakeTrainingOperator
+
+REF = "/root/reference"
+pytestmark = pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "test", "crds")),
+                                reason="reference checkout not mounted")
+
+EXAMPLES = {
+    "cron-pytorch.yaml": GroupVersionResource("kubeflow.org", "v1", "pytorchjobs"),
+    "cron-tf.yaml": GroupVersionResource("kubeflow.org", "v1", "tfjobs"),
+    "cron-mpi.yaml": GroupVersionResource("kubeflow.org", "v1alpha1", "mpijobs"),
+}
+MODES = {"optimized": ReconcilerOptions(), "reference": ReconcilerOptions.reference()}
+NS = "default"
+
+
+def _load(path: str):
+    with open(path) as fh:
+        return [d for d in yaml.safe_load_all(fh) if d]
+
+
+def _reference_env() -> TestEnv:
+    env = TestEnv(install_kubeflow=False)
+    # the reference's CRDs replace this repo's: the Cron CRD as the chart ships it ...
+    for d in _load(os.path.join(REF, "charts", "cron-operator", "crds", "apps.kubedl.io_crons.yaml")):
+        env.server.install_crd(d)
+    # ... and the Kubeflow CRDs its envtest installs
+    for name in sorted(os.listdir(os.path.join(REF, "test", "crds"))):
+        for d in _load(os.path.join(REF, "test", "crds", name)):
+            env.server.install_crd(d)
+    return env
+
+
+@pytest.mark.parametrize("mode", MODES)
+async def test_reference_examples_run_against_reference_crds(mode):
+    env = _reference_env()
+    trainer = FakeTrainingOperator(env.new_client(), env.clock, mode="timed", duration=20)
+    await trainer.start()
+    crons = {}
+    for fname in EXAMPLES:
+        (cron,) = _load(os.path.join(REF, "examples", "v1alpha1", "cron", fname))
+        cron["metadata"]["namespace"] = NS
+        await env.client.create(CRON_GVR, cron, NS)
+        crons[fname] = cron["metadata"]["name"]
+    await env.start_manager(MODES[mode])
+    await env.settle()
+    for _ in range(8):  # four one-minute ticks; every job finishes 20 s after it starts
+        await env.advance(30)
+    for fname, gvr in EXAMPLES.items():
+        name = crons[fname]
+        items = env.server.list(gvr, NS, label_selector=f"{LABEL_CRON_NAME}={name}")["items"]
+        assert items, f"{fname}: no {gvr.resource} created"
+        for w in items:
+            # the template's labels/annotations are carried over, the owner is the Cron
+            assert w["metadata"]["labels"]["key1"] == "value1"
+            assert w["metadata"]["annotations"]["key2"] == "value2"
+            ref = w["metadata"]["ownerReferences"][0]
+            assert (ref["kind"], ref["name"], ref["controller"]) == ("Cron", name, True)
+        st = env.server.get(CRON_GVR, NS, name)["status"]
+        assert st.get("lastScheduleTime"), fname
+        hist = st.get("history") or []
+        if fname == "cron-mpi.yaml" and mode == "reference":
+            # MPIJob v1alpha1 reports only status.launcherStatus, no conditions: the reference's
+            # condition-based isWorkloadFinished never sees it finish, so
+            # under Forbid its first job stays active and nothing else runs
+            assert hist == [] and len(items) == 1 and len(st.get("active") or []) == 1
+            continue
+        assert hist and all(h["status"] == "Succeeded" for h in hist), (fname, hist)
+        assert len(hist) <= 3  # the examples' historyLimit
+    await trainer.stop()
+    await env.stop()
