@@ -70,7 +70,7 @@ def _jsonable(v: Any) -> Any:
         return str(v)
     if isinstance(v, (str, int, float, bool)) or v is None:
         return v
-    if isinstance(v, (list, tuple)):
+    if isinstance(v, (list, tuple)) and not hasattr(v, "_fields"):  # named tuples (GVK, keys) log as str()
         return [_jsonable(x) for x in v]
     if isinstance(v, dict):
         return {str(k): _jsonable(x) for k, x in v.items()}
@@ -157,7 +157,8 @@ class Sink:
             pass
 
 
-def _caller(depth: int = 3) -> str:
+def _caller(depth: int = 2) -> str:
+    """``file:line`` of the log call (frame 0 is this function, 1 is Logger.info/error)."""
     f = sys._getframe(depth)
     fn = f.f_code.co_filename
     parts = fn.replace("\\", "/").split("/")

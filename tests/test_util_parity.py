@@ -8,6 +8,7 @@ for the API types (``api/v1alpha1/cron_types.go``).
 from __future__ import annotations
 
 import io
+import sys
 import json
 
 import pytest
@@ -228,3 +229,15 @@ def test_cron_from_dict_roundtrip():
     d = c.to_dict()
     c2 = Cron.from_dict(d)
     assert c2.to_dict() == d and c2.gvk() == CRON_GVK
+
+
+def test_log_caller_is_the_log_call_site():
+    """zap's ``caller`` field names the line of the log call itself (AddCaller)."""
+    from cron_operator_amd.utils.logging import new_from_options
+
+    buf = io.StringIO()
+    log = new_from_options(encoder="json", level="info", stream=buf)
+    line = sys._getframe().f_lineno + 1
+    log.info("here")
+    rec = json.loads(buf.getvalue().strip().splitlines()[-1])
+    assert rec["caller"] == f"tests/test_util_parity.py:{line}"
