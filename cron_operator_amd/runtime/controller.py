@@ -97,6 +97,7 @@ class Controller:
         base = logger or get_logger()
         self.log = base.with_values(controller=name)
         self._log_ctor = log_constructor(base, "Cron") if name == "cron" else None
+        self._loggers: Dict[Request, Logger] = {}
         self.recover_panic = recover_panic
         self.queue = queue or WorkQueue(name, clock, controller=name)
         self._sources: List[Tuple[Informer, EventHandler]] = []
@@ -107,13 +108,15 @@ class Controller:
         self.started = False
         self.result_counts: Dict[str, int] = {}
         self.on_result: Optional[Callable[[Request, Optional[Result], Optional[BaseException]], None]] = None
-        self._m_active = metrics.ACTIVE_WORKERS.labels(name)
+        self._m_active = metrics.ACTIVE_WORKERS.labels(name)  # a gauge child: ``.value`` is its sample
+        self._m_total: Dict[str, Any] = {}
         self._m_time = metrics.RECONCILE_TIME.labels(name)
         metrics.MAX_CONCURRENT.labels(name).set(self.max_concurrent)
         self.for_kind: Optional[GroupVersionKind] = None
 
     def set_log_constructor(self, ctor: Callable[[Optional[Request]], Logger]) -> None:
         self._log_ctor = ctor
+        self._loggers.clear()
 
     # ------------------------------------------------------------------ sources
     def set_shard(self, index: int, count: int) -> None:
@@ -194,30 +197,43 @@ class Controller:
 
     # ------------------------------------------------------------------ workers
     def _logger_for(self, req: Request) -> Logger:
-        base = self._log_ctor(req) if self._log_ctor else self.log.with_values(
-            **{"namespace": req.namespace, "name": req.name})
+        base = self._loggers.get(req)
+        if base is None:
+            base = self._log_ctor(req) if self._log_ctor else self.log.with_values(
+                **{"namespace": req.namespace, "name": req.name})
+            if len(self._loggers) >= 1 << 16:
+                self._loggers.clear()
+            self._loggers[req] = base  # loggers are immutable: one per key is reused
         if base.sink.level > 0:  # info disabled: skip the per-request ID
             return base
         return base.with_values(reconcileID=str(uuid.uuid4()))
 
     def _count(self, label: str) -> None:
         self.result_counts[label] = self.result_counts.get(label, 0) + 1
-        metrics.child(metrics.RECONCILE_TOTAL, self.name, label).inc()
+        c = self._m_total.get(label)
+        if c is None:
+            c = self._m_total[label] = metrics.RECONCILE_TOTAL.labels(self.name, label)
+        c.inc()
 
     async def process_one(self, req: Request) -> None:
         q = self.queue
         log = self._logger_for(req)
         self.active += 1
-        self._m_active.set(self.active)
+        self._m_active.value = float(self.active)
         t0 = time.perf_counter()
         result: Optional[Result] = None
         err: Optional[BaseException] = None
         try:
-            with tracing.span("reconcile", controller=self.name, namespace=req.namespace, name=req.name) as sp:
+            if tracing.get_tracer().enabled:
+                with tracing.span("reconcile", controller=self.name, namespace=req.namespace, name=req.name) as sp:
+                    result = await self.reconciler.reconcile(req, log)
+                    if result is None:
+                        result = Result()
+                    sp.set(requeue_after_ms=result.after_ns() / 1e6)
+            else:
                 result = await self.reconciler.reconcile(req, log)
                 if result is None:
                     result = Result()
-                sp.set(requeue_after_ms=result.after_ns() / 1e6)
         except asyncio.CancelledError:
             raise
         except Exception as e:  # noqa: BLE001 - recover like RecoverPanic
@@ -226,7 +242,7 @@ class Controller:
                 raise
         finally:
             self.active -= 1
-            self._m_active.set(self.active)
+            self._m_active.value = float(self.active)
             self._m_time.observe(time.perf_counter() - t0)
         self.reconciles += 1
         if err is not None:

@@ -105,8 +105,8 @@ class _FastWatch(WatchStream):
     def __init__(self, stream: Stream):
         self._s = stream
 
-    async def __anext__(self) -> Tuple[str, Dict[str, Any]]:
-        return await self._s.__anext__()
+    def __anext__(self):  # the stream's own awaitable: no extra coroutine frame per event
+        return self._s.__anext__()
 
     def stop(self) -> None:
         self._s.close()
