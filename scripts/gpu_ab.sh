@@ -1,0 +1,28 @@
+#!/bin/bash
+# One gpurun call: paired A/B of operator CPU per fire on the box.  ab_base/ holds an older
+# tree (git archive <rev> | tar -x -C ab_base; git-ignored, shipped with the snapshot);
+# both trees build their extensions and run the 1-process 1000-Cron bench alternately.
+#   TAG=r2g ROUNDS=4 bash scripts/gpu_ab.sh
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${TAG:-ab}
+ROUNDS=${ROUNDS:-4}
+OUT=$PWD/gpurun_out/$TAG
+mkdir -p "$OUT"
+for d in ab_base .; do
+  (cd "$d" && timeout -k 10 300 python -m cron_operator_amd.ops.build > "$OUT/build_$(basename "$(realpath "$d")").log" 2>&1) || exit $?
+done
+for i in $(seq "$ROUNDS"); do
+  for d in ab_base .; do
+    name=$([ "$d" = "." ] && echo head || echo base)
+    (cd "$d" && PYTHONPATH=$PWD timeout -k 10 300 python bench.py --shards 1 --steps 10 --warmup 3 --baseline none \
+        > "$OUT/${name}_$i.log" 2>&1)
+    rc=$?; [ $rc -eq 0 ] || { echo "$name round $i rc=$rc"; exit $rc; }
+    python - "$OUT/${name}_$i.log" "$name" "$i" <<'PY'
+import json, sys
+d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
+print(sys.argv[2], sys.argv[3], d["value"], d["operator_cpu_ms_per_fire"], d["p50_schedule_to_create_ms"], flush=True)
+PY
+  done
+done
