@@ -356,6 +356,28 @@ class Stream:
             raise StopAsyncIteration
         return c.items.popleft()
 
+    def take_ready(self) -> list:
+        """Every item decoded so far, without waiting (an informer applies a whole batch per
+        wake-up instead of one coroutine round trip per event)."""
+        items = self._c.items
+        if not items:
+            return []
+        out = list(items)
+        items.clear()
+        return out
+
+    async def wait_ready(self) -> bool:
+        """Wait until items are ready (True) or the stream ended (False)."""
+        c = self._c
+        while not c.items:
+            if c.done:
+                return False
+            c.ready.clear()
+            if c.items or c.done:
+                continue
+            await c.ready.wait()
+        return True
+
     def close(self) -> None:
         self._c.close()
 

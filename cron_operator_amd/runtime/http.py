@@ -108,6 +108,12 @@ class _FastWatch(WatchStream):
     def __anext__(self):  # the stream's own awaitable: no extra coroutine frame per event
         return self._s.__anext__()
 
+    def take_ready(self) -> List[Tuple[str, Dict[str, Any]]]:
+        return self._s.take_ready()
+
+    def wait_ready(self):
+        return self._s.wait_ready()
+
     def stop(self) -> None:
         self._s.close()
 

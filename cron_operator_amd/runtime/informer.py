@@ -358,17 +358,24 @@ class Informer:
                                                       timeout_seconds=timeout_s)
                 self._arm_watchdog(timeout_s)
                 loop = asyncio.get_running_loop()
+                w = self._watch
                 try:
-                    async for etype, obj in self._watch:
-                        self._last_item = loop.time()
-                        if etype == "ERROR":
-                            st = errors.ApiError.from_status(int(obj.get("code") or 500), obj)
-                            raise st
-                        rv = (obj.get("metadata") or {}).get("resourceVersion")
-                        if etype != "BOOKMARK":
-                            self._apply(etype, obj)
-                        if rv:
-                            self.last_rv = rv
+                    take = getattr(w, "take_ready", None)
+                    if take is not None:
+                        # batched: every event that arrived is applied per wake-up
+                        while True:
+                            batch = take()
+                            if not batch:
+                                if not await w.wait_ready():
+                                    break
+                                continue
+                            self._last_item = loop.time()
+                            for etype, obj in batch:
+                                self._on_item(etype, obj)
+                    else:
+                        async for etype, obj in w:
+                            self._last_item = loop.time()
+                            self._on_item(etype, obj)
                 finally:
                     self._disarm_watchdog()
                 backoff = 0.1
@@ -391,6 +398,16 @@ class Informer:
                 need_list = need_list or not self.last_rv
                 await asyncio.sleep(backoff * (1 + random.random()))
                 backoff = min(backoff * 2, 30.0)
+
+    def _on_item(self, etype: str, obj: Dict[str, Any]) -> None:
+        """One watch event: apply it (BOOKMARKs only move the resume point); ERROR raises."""
+        if etype == "ERROR":
+            raise errors.ApiError.from_status(int(obj.get("code") or 500), obj)
+        rv = (obj.get("metadata") or {}).get("resourceVersion")
+        if etype != "BOOKMARK":
+            self._apply(etype, obj)
+        if rv:
+            self.last_rv = rv
 
     # ------------------------------------------------------------------ watch liveness
     def _arm_watchdog(self, timeout_s: Optional[int]) -> None:
