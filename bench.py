@@ -177,6 +177,7 @@ def main() -> int:
         mine["ref_elapsed_s"] = bres.elapsed_s
         mine["ref_fires"] = bcfg.n_crons * bcfg.steps
         mine["ref_p50"] = bres.p50_latency_ms
+        mine["ref_req_per_fire"] = bres.api_requests_per_fire
     if dist is not None:
         allr = [None] * world
         dist.all_gather_object(allr, mine)
@@ -228,6 +229,10 @@ def main() -> int:
             "baseline_value": round(base_value, 2) if base_value else None,
             "baseline_source": base_src,
             "baseline_p50_schedule_to_create_ms": round(max(r["ref_p50"] for r in allr), 2)
+            if a.baseline == "measure" else None,
+            # the fixture-independent comparison: API requests per fire of each algorithm (under a
+            # client QPS limit, throughput is QPS / requests per fire)
+            "baseline_api_requests_per_fire": round(sum(r["ref_req_per_fire"] for r in allr) / len(allr), 3)
             if a.baseline == "measure" else None,
             "cron_engine": res.engine,
             "wall_s": round(wall, 2),

@@ -43,6 +43,7 @@ def test_single_rank_line():
     # the denominator is the reference algorithm measured by this same invocation
     assert d["baseline_source"].startswith("measured")
     assert d["baseline_value"] > 0 and d["baseline_p50_schedule_to_create_ms"] > 0
+    assert d["baseline_api_requests_per_fire"] > d["api_requests_per_fire"]
     assert abs(d["vs_baseline"] - d["value"] / d["baseline_value"]) < 0.01 * d["vs_baseline"] + 0.002
 
 
