@@ -207,8 +207,8 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": round(value / base_value, 3) if base_value else None,
             "dtype": "n/a (control plane; no tensor compute)",
-            "data": "synthetic: 1000 random-free Cron CRs (* * * * *, historyLimit=10) + PyTorchJob children on a "
-                    "fake apiserver process per rank",
+            "data": f"synthetic: {cfg.n_crons} random-free Cron CRs per rank (* * * * *, "
+                    f"historyLimit={cfg.history_limit}) + PyTorchJob children on a fake apiserver process per rank",
             "config": {"model": "cron-operator Cron reconciler (apps.kubedl.io/v1alpha1)",
                        "global_batch": fires // a.steps, "seq_len": None,
                        "parallelism": f"ranks{world}x{cfg.shards}shards", "crons_per_rank": cfg.n_crons,
