@@ -315,3 +315,17 @@ def test_shard_processes_in_one_pod(cluster):
         rc = _stop(proc)
     assert rc == 0, proc.stdout.read()[-3000:]
     assert not any(psutil.pid_exists(k.pid) and k.status() != psutil.STATUS_ZOMBIE for k in kids)
+
+
+def test_cli_accepts_subcommand_flags_before_the_subcommand():
+    """cobra parses a subcommand's flags wherever they appear; the reference's kustomize
+    metrics patch puts ``--metrics-bind-address=:8443`` ahead of ``start``."""
+    from cron_operator_amd.cmd.main import build_parser, cobra_order
+
+    argv = ["--metrics-bind-address=:8443", "start", "--leader-elect", "--health-probe-bind-address=:8081"]
+    assert cobra_order(argv) == ["start", "--metrics-bind-address=:8443", "--leader-elect",
+                                 "--health-probe-bind-address=:8081"]
+    ns = build_parser().parse_args(cobra_order(argv))
+    assert (ns.command, ns.metrics_bind_address, ns.leader_elect) == ("start", ":8443", True)
+    for unchanged in (["start", "--qps", "5"], ["--help"], [], ["version"]):
+        assert cobra_order(unchanged) == unchanged
