@@ -228,6 +228,25 @@ inline uint64_t fnv1a(const char* p, size_t n) {
   return h;
 }
 
+// Short ASCII *values* recur across objects and watch events: apiVersion/kind, condition
+// types, statuses and reasons, namespaces, label values, the tick's timestamps, and an
+// object's own name/uid in each of its versions.  A direct-mapped cache hands back the
+// existing str, so decoded trees share those strings with the trees already cached: an
+// informer holding 11k jobs keeps one "kubeflow.org/v1" instead of 11k.  Strings are
+// immutable, so the sharing is invisible.  Second-chance replacement: a slot hit since it
+// was last probed survives one miss, so one-off strings (resourceVersions, fresh uids) do
+// not evict the recurring ones.
+constexpr size_t kValSlots = 16384;  // power of two
+constexpr size_t kMaxValLen = 48;
+
+struct ValSlot {
+  uint64_t hash;
+  PyObject* str;  // strong ref; nullptr = empty
+  uint32_t len;
+  bool hot;
+};
+ValSlot g_vals[kValSlots];
+
 void clear_keys() {
   for (auto& s : g_keys) {
     Py_CLEAR(s.str);
@@ -235,6 +254,12 @@ void clear_keys() {
     s.len = 0;
   }
   g_keys_used = 0;
+  for (auto& s : g_vals) {
+    Py_CLEAR(s.str);
+    s.hash = 0;
+    s.len = 0;
+    s.hot = false;
+  }
 }
 
 // ASCII key without escapes -> cached str (new reference)
@@ -264,6 +289,30 @@ PyObject* cached_key(const char* p, size_t n) {
   PyObject* str = PyUnicode_New(static_cast<Py_ssize_t>(n), 127);
   if (!str) return nullptr;
   std::memcpy(PyUnicode_DATA(str), p, n);
+  return str;
+}
+
+// ASCII value without escapes -> shared str (new reference)
+PyObject* cached_value(const char* p, size_t n) {
+  const uint64_t h = fnv1a(p, n);
+  ValSlot& s = g_vals[h & (kValSlots - 1)];
+  if (s.str != nullptr && s.hash == h && s.len == n && std::memcmp(PyUnicode_DATA(s.str), p, n) == 0) {
+    s.hot = true;
+    Py_INCREF(s.str);
+    return s.str;
+  }
+  PyObject* str = PyUnicode_New(static_cast<Py_ssize_t>(n), 127);
+  if (!str) return nullptr;
+  std::memcpy(PyUnicode_DATA(str), p, n);
+  if (s.str != nullptr && s.hot) {
+    s.hot = false;  // second chance: keep the recurring string, do not cache this one
+    return str;
+  }
+  Py_INCREF(str);
+  Py_XSETREF(s.str, str);
+  s.hash = h;
+  s.len = static_cast<uint32_t>(n);
+  s.hot = false;
   return str;
 }
 
@@ -344,6 +393,7 @@ struct Decoder {
       ++p;  // closing quote
       if (ascii) {
         if (key && n <= kMaxKeyLen) return cached_key(s, n);
+        if (!key && n <= kMaxValLen) return cached_value(s, n);
         PyObject* str = PyUnicode_New(static_cast<Py_ssize_t>(n), 127);
         if (!str) return nullptr;
         std::memcpy(PyUnicode_DATA(str), s, n);

@@ -72,6 +72,24 @@ def test_keys_are_shared_and_cache_clear():
     assert m.loads('{"metadata":1}') == {"metadata": 1}
 
 
+def test_recurring_short_values_are_shared():
+    """Short ASCII values recur across cached objects (apiVersion, kind, condition types,
+    namespaces, timestamps): decoded trees share one str per value.  Longer, escaped and
+    non-ASCII values still decode to equal (fresh) strings."""
+    doc = ('{"apiVersion":"kubeflow.org/v1","kind":"PyTorchJob","status":"Succeeded",'
+           '"long":"%s","esc":"a\\"b","uni":"caf\u00e9","n":""}' % ("x" * 80))
+    a, b = m.loads(doc), m.loads(doc.encode())
+    assert a == b == json.loads(doc)
+    for k in ("apiVersion", "kind", "status", "n"):
+        assert a[k] is b[k], k
+    # many one-off values (slot collisions, replacement) never change what decodes
+    for i in range(50_000):
+        assert m.loads('{"v":"uid-%d"}' % i)["v"] == "uid-%d" % i
+    assert m.loads('{"v":"kubeflow.org/v1"}')["v"] == "kubeflow.org/v1"
+    m.clear_key_cache()
+    assert m.loads(doc) == json.loads(doc)
+
+
 def _ref_dumps(v):
     return json.dumps(v, separators=(",", ":"), ensure_ascii=False)
 
