@@ -77,8 +77,49 @@ def _observed(env: TestEnv, crons: List[str]) -> Dict[str, Tuple[Any, ...]]:
     return out
 
 
-async def _scenario(mode: str, specs, steps) -> List[Dict[str, Tuple[Any, ...]]]:
-    env = TestEnv()
+class _HttpEnv(TestEnv):
+    """The same fake apiserver, but the manager talks to it over HTTP: the keep-alive client
+    pool, the streamed watch decoding and batched event application are all in the loop."""
+
+    async def serve(self) -> None:
+        from cron_operator_amd.apiserver.http import APIServerApp
+        from cron_operator_amd.runtime.client import Client
+        from cron_operator_amd.runtime.http import HttpTransport
+        from cron_operator_amd.runtime.kubeconfig import RestConfig
+
+        self.app = APIServerApp(self.server)
+        port = await self.app.start("127.0.0.1", 0, bookmark_interval=0)
+        self.client = Client(HttpTransport(RestConfig(host=f"http://127.0.0.1:{port}")), qps=-1)
+
+    def _applied(self) -> int:
+        assert self.manager is not None
+        infs = list(self.manager.cache.informers())
+        if self.reconciler is not None:
+            infs += [i for i in self.reconciler.child_informers.values() if i not in infs]
+        return sum(i.events for i in infs)
+
+    async def settle(self, timeout: float = 30.0) -> None:
+        # events travel through sockets: idle means no informer applied anything for a while
+        loop = asyncio.get_running_loop()
+        deadline = loop.time() + timeout
+        while loop.time() < deadline:
+            await TestEnv.settle(self, timeout)
+            before = self._applied()
+            await asyncio.sleep(0.01)
+            if self._applied() == before and self.controller is not None and self.controller.queue.idle():
+                return
+        raise TimeoutError("HTTP env did not settle")
+
+    async def stop(self) -> None:
+        await TestEnv.stop(self)
+        await self.client.close()
+        await self.app.stop()
+
+
+async def _scenario(mode: str, specs, steps, http: bool = False) -> List[Dict[str, Tuple[Any, ...]]]:
+    env: TestEnv = _HttpEnv() if http else TestEnv()
+    if http:
+        await env.serve()  # type: ignore[attr-defined]
     names = [f"c{i}" for i in range(len(specs))]
     for name, (sched, policy, limit) in zip(names, specs):
         await env.create_cron(new_cron(name, NS, sched, PT_TMPL, concurrency_policy=policy, history_limit=limit))
@@ -122,3 +163,13 @@ def test_optimized_mode_matches_reference_algorithm(specs, steps):
     opt = asyncio.run(_scenario("optimized", specs, steps))
     for i, (r, o) in enumerate(zip(ref, opt)):
         assert o == r, f"step {i}: optimized {o} != reference {r}"
+
+
+@settings(max_examples=15, deadline=None, suppress_health_check=[HealthCheck.too_slow])
+@given(cron_specs, st.lists(step, min_size=3, max_size=8))
+def test_optimized_mode_over_http_matches_reference_algorithm(specs, steps):
+    """The same, with the optimized operator talking HTTP + watch streams to the apiserver."""
+    ref = asyncio.run(_scenario("reference", specs, steps))
+    opt = asyncio.run(_scenario("optimized", specs, steps, http=True))
+    for i, (r, o) in enumerate(zip(ref, opt)):
+        assert o == r, f"step {i}: optimized/http {o} != reference {r}"
