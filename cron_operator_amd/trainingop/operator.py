@@ -47,6 +47,17 @@ def _mpi_v1alpha1(gvr: GroupVersionResource) -> bool:
 _MASTER_TYPES = ("Master", "Chief", "Launcher", "Worker", "PS", "Evaluator")
 
 
+def _free_port() -> int:
+    """A loopback port free at this moment (the rendezvous port of one job's replicas).  The
+    real training-operator uses a fixed port in each pod's own network namespace; here every
+    replica shares the host, so concurrent jobs must not collide."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
 def _now_str(clock: Clock) -> str:
     return GoTime(clock.now_ns() // 1_000_000_000, 0, UTC).rfc3339()
 
@@ -184,7 +195,7 @@ class FakeTrainingOperator:
             await self.complete(gvr, ns, name, False)
             return
         world = len(procs_spec)
-        port = 29500 + (abs(hash(name)) % 2000)
+        port = _free_port()  # one host for every replica: a port nothing else holds right now
         procs = []
         t0 = self.clock.monotonic()
         for rank, (rtype, idx, c) in enumerate(procs_spec):
