@@ -90,3 +90,34 @@ async def test_reference_examples_run_against_reference_crds(mode):
         assert len(hist) <= 3  # the examples' historyLimit
     await trainer.stop()
     await env.stop()
+
+
+async def test_mi355x_examples_are_valid_kubeflow_jobs_under_reference_crds():
+    """This repo's MI355X example Crons (``examples/mi355x``: the smoke job, the torchrun DDP
+    job and the Master + 7 Worker DDP job, with ``amd.com/gpu`` limits and RCCL env) produce
+    PyTorchJobs the reference's ``kubeflow.org_pytorchjobs.yaml`` schema admits, on their own
+    schedules (two of them ``CRON_TZ=Asia/Shanghai 30 2 * * *``)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = _reference_env()
+    trainer = FakeTrainingOperator(env.new_client(), env.clock, mode="timed", duration=60)
+    await trainer.start()
+    pt = EXAMPLES["cron-pytorch.yaml"]
+    crons = []
+    for fname in sorted(os.listdir(os.path.join(root, "examples", "mi355x"))):
+        for cron in _load(os.path.join(root, "examples", "mi355x", fname)):
+            if cron.get("kind") != "Cron":
+                continue
+            cron["metadata"]["namespace"] = NS
+            await env.client.create(CRON_GVR, cron, NS)
+            crons.append(cron["metadata"]["name"])
+    await env.start_manager(ReconcilerOptions())
+    await env.settle()
+    for _ in range(16):  # 8 hours: 02:30 Asia/Shanghai is 18:30 UTC, the env starts at 12:00 UTC
+        await env.advance(1800)
+    for name in crons:
+        items = env.server.list(pt, NS, label_selector=f"{LABEL_CRON_NAME}={name}")["items"]
+        assert items, f"{name}: no PyTorchJob admitted"
+        st = env.server.get(CRON_GVR, NS, name)["status"]
+        assert any(h["status"] == "Succeeded" for h in st.get("history") or []), (name, st)
+    await trainer.stop()
+    await env.stop()
