@@ -121,6 +121,7 @@ class Informer:
         self._idle_limit = 0.0
         self._watchdog: Optional[asyncio.TimerHandle] = None
         self.transform = transform
+        self._pretransformed = False  # _replace() of a LIST whose pages were transformed already
         # ``derive`` (set with :meth:`set_derive`): a per-object memo computed once per stored
         # object version -- readers that only need facts derived from an object (a child's
         # classification) take them from ``derived`` instead of re-reading the object
@@ -235,7 +236,7 @@ class Informer:
 
     # ------------------------------------------------------------------ store mutation + dispatch
     def _apply(self, etype: str, obj: Dict[str, Any]) -> None:
-        if self.transform is not None:
+        if self.transform is not None and not self._pretransformed:
             obj = self.transform(obj)
         key = obj_key(obj)
         old = self.store.get(key)
@@ -299,10 +300,34 @@ class Informer:
             self._apply("DELETED", self.store[key])
 
     # ------------------------------------------------------------------ reflector
+    async def _list_pages(self) -> Dict[str, Any]:
+        """Paged LIST (client-go pager) whose items are transformed page by page, as each page
+        arrives: a large initial LIST then never holds every untrimmed object at once (the
+        process's peak memory, which it keeps as RSS, would be set by that moment)."""
+        out: Optional[Dict[str, Any]] = None
+        cont: Optional[str] = None
+        tf = self.transform
+        while True:
+            page = await self.client.list(self.target, self.namespace, self.label_selector,
+                                          limit=self.page_size, continue_=cont)
+            if tf is not None:
+                page["items"] = [tf(o) for o in page.get("items") or []]
+                self._pretransformed = True
+            if out is None:
+                out = page
+            else:
+                out["items"].extend(page.get("items") or [])
+                out["metadata"]["resourceVersion"] = (page.get("metadata") or {}).get("resourceVersion")
+            cont = (page.get("metadata") or {}).get("continue")
+            if not cont:
+                break
+        assert out is not None
+        (out.get("metadata") or {}).pop("continue", None)
+        return out
+
     async def _list(self) -> None:
         try:
-            lst = await self.client.list_all(self.target, self.namespace, self.label_selector, self.page_size) \
-                if not self.field_selector else \
+            lst = await self._list_pages() if not self.field_selector else \
                 await self.client.list(self.target, self.namespace, self.label_selector, self.field_selector)
         except asyncio.CancelledError:
             raise
@@ -315,7 +340,10 @@ class Informer:
         self.list_failures = 0
         self._attempted.set()
         self.relists += 1
-        self._replace(lst.get("items") or [])
+        try:
+            self._replace(lst.get("items") or [])
+        finally:
+            self._pretransformed = False
         self.last_rv = (lst.get("metadata") or {}).get("resourceVersion", "")
         if not self.synced.is_set():
             self.synced.set()
