@@ -33,6 +33,25 @@ TF_TMPL = {"apiVersion": "kubeflow.org/v1", "kind": "TFJob",
 MODES = {"optimized": ReconcilerOptions(), "reference": ReconcilerOptions.reference()}
 
 
+async def _quiesce(env, ctrls, timeout: float = 15.0) -> None:
+    """Wait until every controller's queue is idle, its shard assigner has nothing pending and
+    no watch event is in flight, for a stretch of consecutive polls (a fixed sleep is too
+    short on a loaded CI host)."""
+    loop = asyncio.get_running_loop()
+    end = loop.time() + timeout
+    stable = 0
+    while loop.time() < end:
+        await asyncio.sleep(0.002)
+        if env._watches_drained() and all(c.queue.idle() for c in ctrls) and all(
+                c.reconciler.shard_assigner is None or not c.reconciler.shard_assigner.pending() for c in ctrls):
+            stable += 1
+            if stable >= 25:
+                return
+        else:
+            stable = 0
+    raise TimeoutError("controllers did not go idle")
+
+
 def names(server, gvr, cron):
     items = server.list(gvr, NS, label_selector=f"{LABEL_CRON_NAME}={cron}")["items"]
     return sorted(o["metadata"]["name"] for o in items)
@@ -277,8 +296,7 @@ async def test_horizontal_sharding_splits_crons_and_leases(routing):
         for _ in range(60):
             clock.advance(1)
             await asyncio.sleep(0.001)
-        for _ in range(50):
-            await asyncio.sleep(0.002)
+        await _quiesce(env, ctrls)
     for i in range(n):
         assert len(names(env.server, PT, f"s{i}")) == 2, f"s{i}"
     assert seen[0] <= owners[0] and seen[1] <= owners[1]
@@ -335,24 +353,22 @@ async def test_label_routing_reshard_relabels_crons_and_children():
         await env.create_cron(new_cron(f"r{i}", NS, "*/1 * * * *", PT_TMPL, history_limit=5))
 
     async def run_shards(count, minutes):
-        mgrs, tasks = [], []
+        mgrs, tasks, ctrls = [], [], []
         for idx in range(count):
             m = Manager(env.new_client(), ManagerOptions(clock=clock, shard_index=idx, shard_count=count,
                                                          shard_routing="labels", health_probe_bind_address="0",
                                                          metrics_bind_address="0"))
-            await setup_with_manager(m)
+            ctrls.append((await setup_with_manager(m))[0])
             mgrs.append(m)
             tasks.append(asyncio.get_running_loop().create_task(m.start()))
         for m in mgrs:
             await asyncio.wait_for(m.started.wait(), 10)
-        for _ in range(50):
-            await asyncio.sleep(0.002)
+        await _quiesce(env, ctrls)
         for _ in range(minutes):
             for _ in range(60):
                 clock.advance(1)
                 await asyncio.sleep(0.001)
-            for _ in range(50):
-                await asyncio.sleep(0.002)
+            await _quiesce(env, ctrls)
         for m in mgrs:
             m.stop()
         for t in tasks:

@@ -278,9 +278,9 @@ async def test_http_watch_carries_timeout_and_survives_a_silent_connection():
     try:
         inf.start()
         await asyncio.wait_for(inf.synced.wait(), 10)
-        for _ in range(50):
+        for _ in range(500):  # the WATCH was requested and its stream is established
             await asyncio.sleep(0.01)
-            if seen_params:
+            if seen_params and inf._watch is not None:
                 break
         assert seen_params and 300 <= int(seen_params[0]["timeoutSeconds"]) < 600
         stream = inf._watch._s._c  # the dedicated watch connection
