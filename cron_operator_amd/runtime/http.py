@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import asyncio
 import json
+import re
 from typing import Any, Dict, List, Optional, Tuple
 from urllib.parse import quote
 
@@ -25,31 +26,33 @@ from .fasthttp import ConnectionFailed, HttpPool, HttpStatusError, Stream, encod
 from .kubeconfig import RestConfig
 
 
-_PATHS: Dict[Tuple[GroupVersionResource, str, str, str], str] = {}
+_PREFIXES: Dict[Tuple[GroupVersionResource, str], str] = {}
+# characters quote(..., safe="") leaves alone: a Kubernetes name (DNS-1123) never needs quoting
+_UNRESERVED = re.compile(r"[A-Za-z0-9._~-]+").fullmatch
 
 
 def resource_path(gvr: GroupVersionResource, namespace: str = "", name: str = "", sub: str = "") -> str:
-    """The REST path of a resource (collection when ``name`` is empty).  Memoised: a Cron's
-    status path and its children's paths repeat on every reconcile."""
-    key = (gvr, namespace, name, sub)
-    p = _PATHS.get(key)
-    if p is None:
-        if len(_PATHS) >= 1 << 16:
-            _PATHS.clear()
-        p = _PATHS[key] = _resource_path(gvr, namespace, name, sub)
-    return p
+    """The REST path of a resource (collection when ``name`` is empty).  The collection
+    prefix is memoised per (resource, namespace); names are only quoted when they need it
+    (a per-name memo would grow with every job ever deleted)."""
+    key = (gvr, namespace)
+    base = _PREFIXES.get(key)
+    if base is None:
+        if len(_PREFIXES) >= 4096:
+            _PREFIXES.clear()
+        base = _PREFIXES[key] = _collection_path(gvr, namespace)
+    if name:
+        base += "/" + (name if _UNRESERVED(name) else quote(name, safe=""))
+    if sub:
+        base += "/" + sub
+    return base
 
 
-def _resource_path(gvr: GroupVersionResource, namespace: str, name: str, sub: str) -> str:
+def _collection_path(gvr: GroupVersionResource, namespace: str) -> str:
     base = f"/api/{gvr.version}" if not gvr.group else f"/apis/{gvr.group}/{gvr.version}"
     if namespace:
         base += f"/namespaces/{quote(namespace, safe='')}"
-    base += f"/{gvr.resource}"
-    if name:
-        base += f"/{quote(name, safe='')}"
-    if sub:
-        base += f"/{sub}"
-    return base
+    return base + f"/{gvr.resource}"
 
 
 def _clean(params: Optional[Dict[str, Any]]) -> Dict[str, str]:
