@@ -625,7 +625,11 @@ class CronReconciler(Reconciler):
             self.stats["creates"] += 1
             metrics.child(metrics.WORKLOADS_CREATED, gvk.kind).inc()
             if self.opts.expectations:
-                self.expect.expect_create(self._ckey(cron), created)
+                if self._observed_already(gvk, created):
+                    # the watch event overtook the CREATE response: nothing left to expect
+                    self.expect.drop_pending(self._ckey(cron), wm.get("name", ""))
+                else:
+                    self.expect.expect_create(self._ckey(cron), created)
             if self.opts.fold_created_into_active:
                 cm = created.get("metadata") or {}
                 cgvk = GroupVersionKind.from_object(created)
@@ -648,6 +652,15 @@ class CronReconciler(Reconciler):
         # B20 (cron_controller.go:237)
         cron.status.last_schedule_time = now
         return scheduled
+
+    def _observed_already(self, gvk: GroupVersionKind, created: Dict[str, Any]) -> bool:
+        """Does the child informer already hold the object our CREATE returned (same uid)?"""
+        inf = self.child_informers.get(gvk)
+        if inf is None:
+            return False
+        m = created.get("metadata") or {}
+        cached = inf.get(m.get("namespace", ""), m.get("name", ""), copy=False)
+        return cached is not None and (cached.get("metadata") or {}).get("uid") == m.get("uid")
 
     def _tick_already_ran(self, cron: Cron, missed_run: GoTime, active: List[Child],
                           terminated: List[Child]) -> bool:
