@@ -82,20 +82,30 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
         if opts.expectations and opts.skip_expected_events:
             # events that only confirm what the reconciler already folded into status
             def not_expected(event: str, old, new) -> bool:
+                ex = rec.expect
                 if event == "create":
-                    return not rec.expect.matches_created(key_of(new), new)
+                    return not (ex.pending or ex.created) or not ex.matches_created(key_of(new), new)
                 if event == "delete":
-                    return not rec.expect.matches_deleted(key_of(new), new)
+                    return not ex.deleted or not ex.matches_deleted(key_of(new), new)
                 return True
             owned_preds.append(not_expected)
         ctrl.watch_owned(inf, CRON_GVK, owned_preds)
         if assigner is not None:
             asyncio.get_running_loop().create_task(assigner.watch(mgr.cache, gvk, child=True))
         if opts.expectations:
-            inf.add_handler(EventHandler(
-                on_add=lambda o: rec.expect.observe_add(key_of(o), (o.get("metadata") or {}).get("uid", "")),
-                on_update=lambda old, o: rec.expect.observe_add(key_of(o), (o.get("metadata") or {}).get("uid", "")),
-                on_delete=lambda o: rec.expect.observe_delete(key_of(o), (o.get("metadata") or {}).get("uid", ""))))
+            exp = rec.expect
+
+            # most events find no expectation at all: skip building the key then
+            def observe_add(o) -> None:
+                if exp.created:
+                    exp.observe_add(key_of(o), (o.get("metadata") or {}).get("uid", ""))
+
+            def observe_delete(o) -> None:
+                if exp.created or exp.deleted:
+                    exp.observe_delete(key_of(o), (o.get("metadata") or {}).get("uid", ""))
+
+            inf.add_handler(EventHandler(on_add=observe_add, on_update=lambda old, o: observe_add(o),
+                                         on_delete=observe_delete))
         if opts.classification_cache:
             inf.add_handler(EventHandler(
                 on_delete=lambda o: rec.forget_child((o.get("metadata") or {}).get("uid", ""))))
