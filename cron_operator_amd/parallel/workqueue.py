@@ -90,17 +90,20 @@ class WorkQueue:
     def add(self, item: Hashable, priority: int = 0) -> None:
         if self._shutdown:
             return
-        self.adds += 1
-        self._m_adds.inc()
         cur = self._queued.get(item)
         if cur is not None:
             if -cur[0] < priority:  # raise priority: push a fresher entry, old one goes stale
                 self._push(item, priority)
-            return
+            return  # already dirty: client-go neither queues nor counts it again
         if item in self._processing:
             prev = self._dirty.get(item)
+            if prev is None:
+                self.adds += 1
+                self._m_adds.inc()
             self._dirty[item] = priority if prev is None else max(prev, priority)
             return
+        self.adds += 1
+        self._m_adds.inc()
         self._push(item, priority)
 
     async def get(self) -> Hashable:

@@ -152,11 +152,14 @@ class Controller:
 
         def on_update(old: Dict[str, Any], new: Dict[str, Any]) -> None:
             if ok("update", old, new):
-                for r in mapper(new):
+                reqs = mapper(new)
+                for r in reqs:
                     q.add(r, PRIORITY_EVENT)
                 # an owner change moves the child: also wake the previous owner
-                for r in mapper(old):
-                    q.add(r, PRIORITY_EVENT)
+                prev = mapper(old)
+                if prev != reqs:
+                    for r in prev:
+                        q.add(r, PRIORITY_EVENT)
 
         def on_delete(obj: Dict[str, Any]) -> None:
             if ok("delete", None, obj):

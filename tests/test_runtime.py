@@ -555,3 +555,26 @@ async def test_http_watch_stream_timeout_keepalive_and_disconnect():
         assert not env.server._watchers[key] and not app._streams
     finally:
         await app.stop()
+
+
+def test_workqueue_counts_adds_like_client_go():
+    """client-go's workqueue counts an Add only when the item was not dirty already: a key
+    queued twice, or re-added twice while processing, is one add."""
+    from cron_operator_amd.parallel.workqueue import WorkQueue
+    from cron_operator_amd.runtime.controller import Request
+    from cron_operator_amd.utils.clock import FakeClock
+
+    async def run():
+        q = WorkQueue("t", FakeClock(0))
+        a = Request("ns", "a")
+        q.add(a)
+        q.add(a)
+        assert q.adds == 1 and len(q) == 1
+        assert await q.get() == a
+        q.add(a)
+        q.add(a)  # dirty while processing: once
+        assert q.adds == 2
+        q.done(a)
+        assert len(q) == 1 and q.adds == 2
+
+    asyncio.run(run())
