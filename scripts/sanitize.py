@@ -98,6 +98,15 @@ def drive(scratch: str, iters: int) -> None:
             fj.loads(_mutate(rng, raw))
         except (ValueError, RecursionError):
             pass
+    # the shared-value cache: strings handed out, dropped, evicted and handed out again
+    vals = [f"v{i}" for i in range(40000)] + ["kubeflow.org/v1", "PyTorchJob", "Succeeded"] * 100
+    for rnd in range(3):
+        rng.shuffle(vals)
+        docs = [fj.loads(('{"a":"%s","b":["%s"]}' % (v, v)).encode()) for v in vals]
+        assert all(d["a"] == d["b"][0] == v for d, v in zip(docs, vals))
+        del docs
+        if rnd == 1:
+            fj.clear_key_cache()
     fields = ["*", "*/5", "1-10/3", "MON-FRI", "JAN,MAR", "?", "61", "-1", "@every 90s", "@daily", "0 0 30 2 *",
               "CRON_TZ=Asia/Shanghai", "TZ=Bad/Zone", "1-", "/5", "L", ""]
     for _ in range(iters // 4):
