@@ -15,11 +15,12 @@
 """
 from __future__ import annotations
 
+import asyncio
 import os
 import ssl
 import subprocess
 import tempfile
-from typing import Awaitable, Callable, Dict, Optional, Tuple
+from typing import Any, Awaitable, Callable, Dict, Optional, Tuple
 
 from aiohttp import web
 
@@ -141,10 +142,22 @@ def self_signed_cert(directory: str, host: str = "localhost") -> Tuple[str, str]
     return crt, key
 
 
+# certwatcher's polling interval (it also reacts to fsnotify events; polling alone is
+# enough for a certificate that cert-manager renews well before expiry)
+CERT_POLL_INTERVAL = 10.0
+
+
 class MetricsServer:
     def __init__(self, bind: str, secure: bool = True, cert_dir: str = "", cert_name: str = "tls.crt",
-                 key_name: str = "tls.key", client=None, enable_http2: bool = False):
+                 key_name: str = "tls.key", client=None, enable_http2: bool = False,
+                 cert_poll_interval: float = CERT_POLL_INTERVAL):
         self.bind = bind
+        # a certificate from --metrics-cert-path is watched and reloaded when its files change
+        # (controller-runtime's certwatcher), so a cert-manager rotation needs no restart
+        self.cert_poll_interval = cert_poll_interval
+        self._ctx: Optional[ssl.SSLContext] = None
+        self._cert_watch: Optional[asyncio.Task] = None
+        self.cert_reloads = 0
         self.secure = secure
         self.cert_dir = cert_dir
         self.cert_name = cert_name
@@ -214,7 +227,41 @@ class MetricsServer:
         ctx.load_cert_chain(crt, key)
         # HTTP/2 is off unless --enable-http2 (start.go:83-98); aiohttp speaks HTTP/1.1 only
         ctx.set_alpn_protocols(["http/1.1"])
+        self._ctx = ctx
         return ctx
+
+    @staticmethod
+    def _stamp(*paths: str) -> Tuple[Any, ...]:
+        """What identifies a certificate's current content: the files' identity, size and
+        mtime after symlinks (a Secret volume swaps its ``..data`` link on update)."""
+        out = []
+        for p in paths:
+            try:
+                st = os.stat(p)
+                out.append((st.st_ino, st.st_size, st.st_mtime_ns))
+            except OSError:
+                out.append(None)
+        return tuple(out)
+
+    async def _watch_certs(self, crt: str, key: str) -> None:
+        """certwatcher: poll the certificate and key; load a changed pair into the live
+        SSLContext (new handshakes use it).  A pair that does not load -- e.g. caught mid
+        rotation -- keeps the previous certificate and is retried on the next poll."""
+        last = self._stamp(crt, key)
+        while True:
+            await asyncio.sleep(self.cert_poll_interval)
+            cur = self._stamp(crt, key)
+            if cur == last or self._ctx is None:
+                continue
+            try:
+                self._ctx.load_cert_chain(crt, key)
+            except (OSError, ssl.SSLError) as e:
+                self.log.error(e, "error loading the rotated certificate, keeping the current one",
+                               certPath=crt, keyPath=key)
+                continue
+            last = cur
+            self.cert_reloads += 1
+            self.log.info("Updated current TLS certificate", certPath=crt, keyPath=key)
 
     async def start(self) -> None:
         addr = parse_bind_address(self.bind)
@@ -227,9 +274,15 @@ class MetricsServer:
         site = web.TCPSite(self._runner, addr[0], addr[1], ssl_context=self._ssl())
         await site.start()
         self.port = _bound_port(site)
+        if self.secure and self.cert_dir and self.cert_poll_interval > 0:
+            self._cert_watch = asyncio.get_running_loop().create_task(self._watch_certs(
+                os.path.join(self.cert_dir, self.cert_name), os.path.join(self.cert_dir, self.key_name)))
         self.log.info("Serving metrics server", bindAddress=self.bind, secure=self.secure)
 
     async def stop(self) -> None:
+        if self._cert_watch is not None:
+            self._cert_watch.cancel()
+            self._cert_watch = None
         if self._runner is not None:
             await self._runner.cleanup()
             self._runner = None

@@ -578,3 +578,52 @@ def test_workqueue_counts_adds_like_client_go():
         assert len(q) == 1 and q.adds == 2
 
     asyncio.run(run())
+
+
+async def test_metrics_server_reloads_a_rotated_certificate(tmp_path):
+    """``--metrics-cert-path``: like controller-runtime's certwatcher, a certificate rotated
+    on disk (cert-manager renewing the Secret) is served to new connections without a restart;
+    a half-written pair keeps the previous certificate."""
+    import hashlib
+    import ssl
+
+    from cron_operator_amd.runtime.servers import self_signed_cert
+
+    def fingerprint(port):
+        ctx = ssl.create_default_context()
+        ctx.check_hostname = False
+        ctx.verify_mode = ssl.CERT_NONE
+
+        async def grab():
+            _, w = await asyncio.open_connection("127.0.0.1", port, ssl=ctx)
+            der = w.get_extra_info("ssl_object").getpeercert(binary_form=True)
+            w.close()
+            return hashlib.sha256(der).hexdigest()
+        return grab()
+
+    certs = tmp_path / "certs"
+    certs.mkdir()
+    crt, key = self_signed_cert(str(certs), host="first")
+    env = TestEnv()
+    sm = MetricsServer("127.0.0.1:0", secure=True, cert_dir=str(certs), client=env.new_client(),
+                       cert_poll_interval=0.05)
+    await sm.start()
+    try:
+        first = await fingerprint(sm.port)
+        with open(crt, "w") as fh:  # caught mid-rotation: an unreadable certificate is not loaded
+            fh.write("not a certificate")
+        await asyncio.sleep(0.3)
+        assert await fingerprint(sm.port) == first and sm.cert_reloads == 0
+        other = tmp_path / "other"
+        other.mkdir()
+        ncrt, nkey = self_signed_cert(str(other), host="second")
+        os.replace(nkey, key)
+        os.replace(ncrt, crt)
+        for _ in range(100):
+            await asyncio.sleep(0.05)
+            if sm.cert_reloads:
+                break
+        assert sm.cert_reloads == 1
+        assert await fingerprint(sm.port) != first
+    finally:
+        await sm.stop()
