@@ -14,6 +14,8 @@ dashboards and alerts carry over:
 * ``rest_client_requests_total{code,host,method}``,
   ``rest_client_request_duration_seconds``, ``rest_client_rate_limiter_duration_seconds``;
 * ``leader_election_master_status{name}``;
+* ``certwatcher_read_certificate_total`` / ``..._errors_total`` (a ``--metrics-cert-path``
+  certificate is reloaded when rotated);
 * process and Python runtime collectors (the Go/process collectors' counterpart).
 
 The series live in :mod:`cron_operator_amd.runtime.promlite`, a small client
@@ -117,3 +119,7 @@ def child(metric, *labels: str):
 
 def exposition() -> bytes:
     return REGISTRY.exposition()
+
+CERT_READS = Counter("certwatcher_read_certificate_total", "Total number of certificate reads", registry=REGISTRY)
+CERT_READ_ERRORS = Counter("certwatcher_read_certificate_errors_total", "Total number of certificate read errors",
+                           registry=REGISTRY)

@@ -224,6 +224,8 @@ class MetricsServer:
             self._tmp = tempfile.TemporaryDirectory(prefix="cron-operator-metrics-")
             crt, key = self_signed_cert(self._tmp.name)
         ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+        if self.cert_dir:
+            metrics.CERT_READS.inc()
         ctx.load_cert_chain(crt, key)
         # HTTP/2 is off unless --enable-http2 (start.go:83-98); aiohttp speaks HTTP/1.1 only
         ctx.set_alpn_protocols(["http/1.1"])
@@ -253,9 +255,11 @@ class MetricsServer:
             cur = self._stamp(crt, key)
             if cur == last or self._ctx is None:
                 continue
+            metrics.CERT_READS.inc()
             try:
                 self._ctx.load_cert_chain(crt, key)
             except (OSError, ssl.SSLError) as e:
+                metrics.CERT_READ_ERRORS.inc()
                 self.log.error(e, "error loading the rotated certificate, keeping the current one",
                                certPath=crt, keyPath=key)
                 continue

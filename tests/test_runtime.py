@@ -625,5 +625,8 @@ async def test_metrics_server_reloads_a_rotated_certificate(tmp_path):
                 break
         assert sm.cert_reloads == 1
         assert await fingerprint(sm.port) != first
+        from cron_operator_amd.runtime import metrics as m
+
+        assert m.CERT_READ_ERRORS._only().get() >= 1 and m.CERT_READS._only().get() >= 3
     finally:
         await sm.stop()
