@@ -251,9 +251,19 @@ async def run_start(a: argparse.Namespace) -> int:
     mgr.add_healthz_check("healthz")
     mgr.add_readyz_check("readyz")
     loop = asyncio.get_running_loop()
+    signals = [0]
+
+    def on_signal() -> None:
+        # ctrl.SetupSignalHandler: the first SIGTERM/SIGINT stops the manager gracefully,
+        # a second one exits at once with status 1
+        signals[0] += 1
+        if signals[0] > 1:
+            os._exit(1)
+        mgr.stop()
+
     for sig in (signal.SIGINT, signal.SIGTERM):
         try:
-            loop.add_signal_handler(sig, mgr.stop)
+            loop.add_signal_handler(sig, on_signal)
         except (NotImplementedError, RuntimeError):
             pass
     log.info("starting manager")
