@@ -405,7 +405,8 @@ class CronReconciler(Reconciler):
             try:
                 await f
             except asyncio.CancelledError:
-                raise
+                if not f.cancelled():  # this reconcile itself is being cancelled
+                    raise
             except Exception:  # noqa: BLE001
                 pass
 
