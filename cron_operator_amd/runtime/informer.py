@@ -312,7 +312,6 @@ class Informer:
                                           limit=self.page_size, continue_=cont)
             if tf is not None:
                 page["items"] = [tf(o) for o in page.get("items") or []]
-                self._pretransformed = True
             if out is None:
                 out = page
             else:
@@ -340,6 +339,8 @@ class Informer:
         self.list_failures = 0
         self._attempted.set()
         self.relists += 1
+        # the paged LIST transformed its items already (a field-selector LIST did not)
+        self._pretransformed = self.transform is not None and not self.field_selector
         try:
             self._replace(lst.get("items") or [])
         finally:
