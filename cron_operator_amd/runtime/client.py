@@ -390,7 +390,6 @@ class Client:
                     label_selector: Optional[str] = None, field_selector: Optional[str] = None,
                     allow_bookmarks: bool = True, timeout_seconds: Optional[int] = None) -> WatchStream:
         gvr = self._gvr_now(target) or await self._gvr(target)
-        gvr = gvr
         await self._throttle("watch")
         self.requests += 1
         self.requests_by_verb["watch"] = self.requests_by_verb.get("watch", 0) + 1
