@@ -47,11 +47,14 @@ def main() -> int:
                          "reconciles_per_fire": r.reconciles_per_fire, "wall_s": time.perf_counter() - t0,
                          "operator_cpu_ms_per_fire": r.cpu_s_operator * 1000 / (n * steps),
                          "apiserver_cpu_ms_per_fire": r.cpu_s_apiserver * 1000 / (n * steps),
-                         "operator_gc": r.operator_gc, "phase_ms": r.phase_ms})
+                         "operator_gc": r.operator_gc, "phase_ms": r.phase_ms,
+                         # peak RSS of each operator shard process (sharded runs only)
+                         "operator_maxrss_mib": r.operator_maxrss_mib})
             print(f"{mode:>9} n={n:>5}: {r.cron_reconciles_per_s:9.1f} cron-reconciles/s  "
                   f"p50 {r.p50_latency_ms:8.1f} ms  p99 {r.p99_latency_ms:8.1f} ms  "
                   f"{r.api_requests_per_fire:.1f} req/fire  operator {r.cpu_s_operator * 1000 / (n * steps):.3f} "
-                  f"ms CPU/fire, apiserver {r.cpu_s_apiserver * 1000 / (n * steps):.3f}, GC {r.operator_gc}",
+                  f"ms CPU/fire, apiserver {r.cpu_s_apiserver * 1000 / (n * steps):.3f}, GC {r.operator_gc}"
+                  + (f", shard peak RSS {r.operator_maxrss_mib} MiB" if r.operator_maxrss_mib else ""),
                   flush=True)
     print()
     print("| mode | Crons | cron-reconciles/s | p50 tick→create ms | p99 ms | ms/tick | API req/fire "
