@@ -69,9 +69,18 @@ async def main() -> int:
     await asyncio.wait_for(mgr.started.wait(), 120)
     cron_inf = rec.cron_informer
     assert cron_inf is not None
-    owned_keys = sorted(f"{a.namespace}/{o['metadata']['name']}"
-                        for o in (await client.list(CRON_GVR, a.namespace))["items"]
-                        if shard_of(a.namespace, o["metadata"]["name"], a.shard_count) == a.shard_index)
+    # the Crons this shard owns, paged (only names are kept: a whole-fleet LIST held at once
+    # would set this process's peak memory)
+    owned_keys: List[str] = []
+    cont = None
+    while True:
+        page = await client.list(CRON_GVR, a.namespace, limit=500, continue_=cont)
+        owned_keys += [f"{a.namespace}/{o['metadata']['name']}" for o in page.get("items") or []
+                       if shard_of(a.namespace, o["metadata"]["name"], a.shard_count) == a.shard_index]
+        cont = (page.get("metadata") or {}).get("continue")
+        if not cont:
+            break
+    owned_keys.sort()
     # label routing: wait until the assigner has labelled every owned Cron and its children
     deadline = time.monotonic() + 300
     while any(k not in cron_inf.store for k in owned_keys) or (

@@ -61,6 +61,19 @@ def unassigned_selector(count: int) -> str:
     return f"{LABEL_SHARD} notin ({','.join(shard_label_value(i, count) for i in range(count))})"
 
 
+_KEPT_METADATA = ("name", "namespace", "uid", "resourceVersion", "labels")
+
+
+def metadata_only(obj: Dict[str, Any]) -> Dict[str, Any]:
+    """Informer transform for the unassigned watches: assignment reads only names and labels.
+    Before the first assignment (a fresh install, or a new shard count) those watches hold
+    the whole fleet, so every shard process would otherwise cache every Cron and job in
+    full once -- and keep that peak as its resident size."""
+    m = obj.get("metadata") or {}
+    return {"apiVersion": obj.get("apiVersion"), "kind": obj.get("kind"),
+            "metadata": {k: m[k] for k in _KEPT_METADATA if k in m}}
+
+
 class ShardAssigner:
     """Labels this shard's unassigned Crons and children (a leader-only runnable)."""
 
@@ -87,7 +100,7 @@ class ShardAssigner:
         if inf is not None:
             return inf
         sel = f"{LABEL_CRON_NAME},{unassigned_selector(self.count)}" if child else unassigned_selector(self.count)
-        inf = await cache.get_informer(gvk, label_selector=sel)
+        inf = await cache.get_informer(gvk, label_selector=sel, transform=metadata_only)
         self.informers[gvk] = inf
         inf.add_handler(EventHandler(on_add=lambda o: self._offer(gvk, o, child),
                                      on_update=lambda _old, o: self._offer(gvk, o, child)))
