@@ -16,7 +16,7 @@ done
 for i in $(seq "$ROUNDS"); do
   for d in ab_base .; do
     name=$([ "$d" = "." ] && echo head || echo base)
-    (cd "$d" && PYTHONPATH=$PWD timeout -k 10 300 python bench.py --shards 1 --steps 10 --warmup 3 --baseline none \
+    (cd "$d" && PYTHONPATH=$PWD timeout -k 10 300 python bench.py --shards ${SHARDS:-1} --steps 10 --warmup 3 --baseline none \
         > "$OUT/${name}_$i.log" 2>&1)
     rc=$?; [ $rc -eq 0 ] || { echo "$name round $i rc=$rc"; exit $rc; }
     python - "$OUT/${name}_$i.log" "$name" "$i" <<'PY'
