@@ -420,3 +420,31 @@ async def test_memos_dropped_when_crons_and_children_go_away():
     assert f"{NS}/m" not in rec.own_writes and f"{NS}/m" not in rec._parsed_status
     assert f"{NS}/m" not in rec.expect.created and f"{NS}/m" not in rec.expect.deleted
     await env.stop()
+
+
+async def test_shard_assignment_watches_cache_metadata_only():
+    """Before assignment the "unassigned" watch sees the whole fleet: it keeps names, labels,
+    uid and resourceVersion only, so a shard's memory follows its own share."""
+    from cron_operator_amd.controller.sharding import ShardAssigner
+
+    env = TestEnv()
+    for i in range(6):
+        await env.create_cron(new_cron(f"u{i}", NS, "*/1 * * * *", PT_TMPL, history_limit=3))
+    env.server.create(PT, NS, {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+                               "metadata": {"name": "u0-1", "labels": {LABEL_CRON_NAME: "u0"}},
+                               "spec": {"pytorchReplicaSpecs": {"Master": {"replicas": 1}}}})
+    from cron_operator_amd.api.meta import GroupVersionKind
+    from cron_operator_amd.runtime.informer import Cache
+
+    cache = Cache(env.new_client(), NS)
+    asg = ShardAssigner(env.new_client(), 0, 2)
+    crons = await asg.watch(cache, GroupVersionKind("apps.kubedl.io", "v1alpha1", "Cron"), child=False)
+    jobs = await asg.watch(cache, GroupVersionKind("kubeflow.org", "v1", "PyTorchJob"), child=True)
+    cache.start()
+    assert await cache.wait_for_sync(10)
+    assert len(crons.store) == 6 and len(jobs.store) == 1
+    for o in list(crons.store.values()) + list(jobs.store.values()):
+        assert set(o) == {"apiVersion", "kind", "metadata"}
+        assert set(o["metadata"]) <= {"name", "namespace", "uid", "resourceVersion", "labels"}
+    assert asg.pending() > 0  # and the shard's own objects are queued for labelling
+    await cache.stop()

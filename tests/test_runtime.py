@@ -630,3 +630,32 @@ async def test_metrics_server_reloads_a_rotated_certificate(tmp_path):
         assert m.CERT_READ_ERRORS._only().get() >= 1 and m.CERT_READS._only().get() >= 3
     finally:
         await sm.stop()
+
+
+async def test_informer_transforms_list_pages_once():
+    """A paged initial LIST is transformed page by page as it arrives, and each object exactly
+    once (``_replace`` does not transform again); watch events are transformed as before."""
+    env = TestEnv()
+    s = env.server
+    for i in range(23):
+        s.create(CM, "default", {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": f"c{i}"},
+                                 "data": {"big": "x" * 100}})
+    seen = []
+
+    def slim(o):
+        seen.append(o["metadata"]["name"])
+        o.pop("data", None)
+        return o
+
+    inf = Informer(env.new_client(), CM, "default", page_size=5, transform=slim)
+    inf.start()
+    await asyncio.wait_for(inf.synced.wait(), 5)
+    assert sorted(seen) == sorted(f"c{i}" for i in range(23)) and len(seen) == 23
+    assert all("data" not in o for o in inf.store.values())
+    s.create(CM, "default", {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "late"}, "data": {"a": "b"}})
+    for _ in range(200):
+        await asyncio.sleep(0.001)
+        if inf.get("default", "late", copy=False) is not None:
+            break
+    assert "data" not in inf.get("default", "late", copy=False) and seen.count("late") == 1
+    await inf.stop()
