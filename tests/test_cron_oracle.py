@@ -60,6 +60,8 @@ def oracle_field(expr: str, lo: int, hi: int, names) -> Tuple[Set[int], bool]:
 
 
 def oracle_next(spec: str, t: dt.datetime) -> Optional[dt.datetime]:
+    """``t`` carries the schedule's zone; the search runs on its wall clock (exact for zones
+    without DST transitions)."""
     fields = spec.split()
     (mins, _), (hours, _), (doms, dom_star), (months, _), (dows, dow_star) = (
         oracle_field(f, lo, hi, names) for f, (lo, hi, names) in zip(fields, BOUNDS))
@@ -76,7 +78,7 @@ def oracle_next(spec: str, t: dt.datetime) -> Optional[dt.datetime]:
                 for m in sorted(mins):
                     if first and h == start.hour and m < start.minute:
                         continue
-                    return dt.datetime(day.year, day.month, day.day, h, m, tzinfo=dt.timezone.utc)
+                    return dt.datetime(day.year, day.month, day.day, h, m, tzinfo=t.tzinfo)
         day += dt.timedelta(days=1)
     return None
 
@@ -129,3 +131,22 @@ def test_oracle_agrees_on_the_classic_cases(spec):
         got = eng.next(eng.parse(spec), GoTime(start, 0, UTC))
         assert (None if got.is_zero() else got.sec) == (None if want is None else int(want.timestamp())), \
             (eng.name, spec)
+
+
+# zones without DST transitions in the tested years: the oracle's wall-clock search is exact
+FIXED_ZONES = ["Etc/GMT-5", "Etc/GMT+7", "Asia/Kolkata", "Asia/Tokyo", "Asia/Shanghai"]
+
+
+@settings(max_examples=200, deadline=None)
+@given(spec=specs, zone=st.sampled_from(FIXED_ZONES),
+       start=st.integers(min_value=1_767_225_600, max_value=1_924_992_000))
+def test_cron_tz_schedules_match_the_oracle(spec, zone, start):
+    """``CRON_TZ=<zone> <spec>``: the schedule runs on the zone's wall clock."""
+    from zoneinfo import ZoneInfo
+
+    t = dt.datetime.fromtimestamp(start, ZoneInfo(zone))
+    want = oracle_next(spec, t)
+    for eng in ENGINES:
+        got = eng.next(eng.parse(f"CRON_TZ={zone} {spec}"), GoTime(start, 0, UTC))
+        assert (None if got.is_zero() else got.sec) == (None if want is None else int(want.timestamp())), \
+            (eng.name, zone, spec, t)
