@@ -10,7 +10,8 @@ finished job into history, garbage-collect the overflow, create the tick's
 PyTorchJob and update status -- against a fake Kubernetes apiserver running in
 its own process, over HTTP + watch streams.  Synthetic objects, no cluster.
 
-Each rank runs the operator as ``--shards`` (default 3) shard processes of the
+Each rank runs the operator as ``--shards`` (default 3; fewer when the CPUs available
+to the job cannot give each rank a core per shard plus one for its apiserver) shard processes of the
 operator's horizontal sharding feature against one apiserver: the reference's Go
 controller spreads its 10 reconcile workers over all cores as goroutines, and
 sharding is how this asyncio operator uses more than one core.  ``--shards 1``
@@ -114,9 +115,11 @@ def main() -> int:
     ap.add_argument("--burst", type=int, default=50)
     ap.add_argument("--transport", choices=["http", "memory"], default="http")
     ap.add_argument("--mode", choices=["optimized", "reference"], default="optimized")
-    ap.add_argument("--shards", type=int, default=3,
+    ap.add_argument("--shards", type=int, default=0,
                     help="operator shards per rank (--shard-count): the reference's controller spreads its 10 "
-                         "workers over every core as goroutines; this asyncio operator uses cores by sharding")
+                         "workers over every core as goroutines; this asyncio operator uses cores by sharding. "
+                         "0 (default): 3, or fewer when the CPUs available to the job cannot give every rank "
+                         "one core per shard plus one for its apiserver")
     ap.add_argument("--shard-routing", choices=["hash", "labels"], default="labels",
                     help="how shards split the watch traffic (controller/sharding.py)")
     ap.add_argument("--apiserver-latency", choices=["none", "etcd"], default="none",
@@ -140,6 +143,12 @@ def main() -> int:
               file=sys.stderr)
         return 2
     from cron_operator_amd.bench.harness import BenchConfig, run_sync
+
+    if a.shards <= 0:
+        from cron_operator_amd.runtime.supervisor import available_cpus
+
+        # 3 shards saturate one fake apiserver process; never oversubscribe the CPUs the ranks share
+        a.shards = max(1, min(3, available_cpus() // world - 1))
 
     cfg = BenchConfig(n_crons=a.crons, steps=a.steps, warmup=a.warmup, history_limit=a.history_limit,
                       mode=a.mode, transport=a.transport, qps=a.qps, burst=a.burst, workers=a.workers,
