@@ -43,8 +43,9 @@ async def main() -> None:
                 stop.set()
             await asyncio.sleep(1)
 
-    loop.create_task(watchdog())
+    dog = loop.create_task(watchdog())
     await stop.wait()
+    dog.cancel()
     await app.stop()
 
 

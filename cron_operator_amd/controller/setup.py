@@ -17,7 +17,6 @@ by :mod:`cron_operator_amd.controller.rbac`.
 """
 from __future__ import annotations
 
-import asyncio
 from typing import Dict, Optional, Tuple
 
 from ..api import errors
@@ -91,7 +90,7 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
             owned_preds.append(not_expected)
         ctrl.watch_owned(inf, CRON_GVK, owned_preds)
         if assigner is not None:
-            asyncio.get_running_loop().create_task(assigner.watch(mgr.cache, gvk, child=True))
+            assigner.watch_soon(mgr.cache, gvk, child=True)
         if opts.expectations:
             exp = rec.expect
 

@@ -93,6 +93,15 @@ class ShardAssigner:
         self._queued: Set[Tuple[GroupVersionKind, str, str]] = set()
         self.labelled = 0
         self.errors = 0
+        self._bg: Set[asyncio.Task] = set()
+
+    def watch_soon(self, cache: Cache, gvk: GroupVersionKind, child: bool) -> asyncio.Task:
+        """:meth:`watch` as a task the assigner holds on to (the loop keeps only weak
+        references to tasks, so an unheld one can be collected before it finishes)."""
+        task = asyncio.get_running_loop().create_task(self.watch(cache, gvk, child))
+        self._bg.add(task)
+        task.add_done_callback(self._bg.discard)
+        return task
 
     async def watch(self, cache: Cache, gvk: GroupVersionKind, child: bool) -> Informer:
         """Watch ``gvk``'s unassigned objects (children: only those with a cron-name label)."""

@@ -142,6 +142,7 @@ class _Child:
         self.probe_port: Optional[int] = None
         self.proc: Optional[asyncio.subprocess.Process] = None
         self.restarts = 0
+        self._reader: Optional[asyncio.Future] = None  # held: the loop only weakly references tasks
 
     async def spawn(self) -> None:
         self.metrics_port = self.probe_port = None
@@ -157,7 +158,7 @@ class _Child:
             raise
         finally:
             os.close(w)
-        asyncio.ensure_future(self._read_ports(r, self.proc))
+        self._reader = asyncio.ensure_future(self._read_ports(r, self.proc))
 
     async def _read_ports(self, r: int, proc: asyncio.subprocess.Process) -> None:
         import json
