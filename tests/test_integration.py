@@ -448,3 +448,26 @@ async def test_shard_assignment_watches_cache_metadata_only():
         assert set(o["metadata"]) <= {"name", "namespace", "uid", "resourceVersion", "labels"}
     assert asg.pending() > 0  # and the shard's own objects are queued for labelling
     await cache.stop()
+
+
+async def test_shard_assigner_holds_background_watch_tasks():
+    """``watch_soon`` (used for child kinds discovered at run time) keeps its task alive until
+    it finishes: the event loop only holds tasks weakly."""
+    import gc
+
+    from cron_operator_amd.api.meta import GroupVersionKind
+    from cron_operator_amd.controller.sharding import ShardAssigner
+    from cron_operator_amd.runtime.informer import Cache
+
+    env = TestEnv()
+    cache = Cache(env.new_client(), NS)
+    asg = ShardAssigner(env.new_client(), 0, 2)
+    gvk = GroupVersionKind("kubeflow.org", "v1", "PyTorchJob")
+    asg.watch_soon(cache, gvk, child=True)  # result deliberately dropped
+    assert len(asg._bg) == 1
+    gc.collect()
+    task = next(iter(asg._bg))
+    inf = await task
+    await asyncio.sleep(0)
+    assert not asg._bg and asg.informers[gvk] is inf
+    await cache.stop()
