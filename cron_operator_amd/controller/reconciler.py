@@ -53,8 +53,8 @@ Time comes from the injected clock (the reference calls ``time.Now()``,
 from __future__ import annotations
 
 import asyncio
+import functools
 import json
-import time
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional, Tuple
 
@@ -92,9 +92,9 @@ from ..runtime.client import Client
 from ..runtime.controller import Reconciler, Request, Result
 from ..runtime.events import Normal, Warning, EventRecorder
 from ..runtime.informer import Cache, Informer
-from ..utils import gctune, jsonutil
+from ..utils import aio, gctune, jsonutil
 from ..utils.clock import Clock, RealClock
-from ..utils.gotime import LOCAL, GoTime
+from ..utils.gotime import LOCAL, NANOS, GoTime
 from ..utils.logging import Logger, ObjectRef
 
 CHILD_INDEX = "cron-name"
@@ -128,14 +128,23 @@ class _ChildInfo:
 
 
 def child_info(w: Dict[str, Any], gvk: GroupVersionKind, policy: WorkloadPolicy) -> _ChildInfo:
-    """Everything a reconcile needs from child ``w`` (a cached object of the template's kind)."""
-    m = w.get("metadata") or {}
+    """Everything a reconcile needs from child ``w`` (a cached object of the template's kind).
+
+    Runs inside the child informer's event handling (``Informer.derive``), so it never
+    raises: an object it cannot read becomes a per-child error (``info.err``) that only
+    its own Cron's reconcile reports, instead of stalling the informer on that event."""
+    m = w.get("metadata")
+    if type(m) is not dict:
+        m = {}
+    err: Optional[Exception] = None
+    cls: Optional[Classification] = None
+    sort_key: Any = (0, 0)
     try:
-        cls: Optional[Classification] = classify(w, gvk, policy)
-        err = None
-    except kf.ConversionError as e:
-        cls, err = None, e
-    info = _ChildInfo(m.get("resourceVersion", ""), cls, creation_timestamp(w).key(), GroupVersionKind.from_object(w))
+        cls = classify(w, gvk, policy)
+        sort_key = creation_timestamp(w).key()
+    except Exception as e:  # noqa: BLE001 - kf.ConversionError, or a malformed object
+        err = e
+    info = _ChildInfo(m.get("resourceVersion", ""), cls, sort_key, GroupVersionKind.from_object(w))
     info.obj = w
     info.name = m.get("name", "")
     info.uid = m.get("uid", "")
@@ -175,7 +184,7 @@ class ReconcilerOptions:
     dynamic_watches: bool = True
     active_ref_resource_version: bool = True
     expectations: bool = True
-    expectation_ttl: float = 300.0           # seconds (wall)
+    expectation_ttl: float = 300.0           # seconds on the injected clock
     fold_created_into_active: bool = True    # add the just-created child to status.active right away
     skip_expected_events: bool = True        # child add/delete events we caused do not requeue the Cron
     classification_cache: bool = True
@@ -206,17 +215,23 @@ class Expectations:
     """Children we created/deleted that the informer has not observed yet.
 
     Keyed by ``namespace/cron``.  Entries are dropped when the informer catches
-    up (``observe_*``) or after ``ttl`` seconds.
+    up (``observe_*``) or after ``ttl`` seconds on the injected clock (like
+    client-go's ``ControllerExpectations``, whose TTL runs on ``clock.Clock``), so a
+    watch event that never arrives is outlived in virtual time as well.
     """
 
-    def __init__(self, ttl: float):
+    def __init__(self, ttl: float, clock: Optional[Clock] = None):
         self.ttl = ttl
-        self.created: Dict[str, Dict[str, Tuple[float, Dict[str, Any]]]] = {}
-        self.deleted: Dict[str, Dict[str, float]] = {}
-        self.pending: Dict[str, Dict[str, float]] = {}  # key -> {name: expiry} for in-flight CREATEs
+        self.clock = clock or RealClock()
+        self.created: Dict[str, Dict[str, Tuple[int, Dict[str, Any]]]] = {}  # key -> {uid: (expiry ns, obj)}
+        self.deleted: Dict[str, Dict[str, int]] = {}
+        self.pending: Dict[str, Dict[str, int]] = {}  # key -> {name: expiry} for in-flight CREATEs
+
+    def _deadline(self) -> int:
+        return self.clock.now_ns() + int(self.ttl * NANOS)
 
     def expect_pending(self, key: str, name: str) -> None:
-        self.pending.setdefault(key, {})[name] = time.monotonic() + self.ttl
+        self.pending.setdefault(key, {})[name] = self._deadline()
 
     def drop_pending(self, key: str, name: str) -> None:
         d = self.pending.get(key)
@@ -227,11 +242,11 @@ class Expectations:
         self.drop_pending(key, (obj.get("metadata") or {}).get("name", ""))
         uid = (obj.get("metadata") or {}).get("uid", "")
         if uid:
-            self.created.setdefault(key, {})[uid] = (time.monotonic() + self.ttl, obj)
+            self.created.setdefault(key, {})[uid] = (self._deadline(), obj)
 
     def expect_delete(self, key: str, uid: str) -> None:
         if uid:
-            self.deleted.setdefault(key, {})[uid] = time.monotonic() + self.ttl
+            self.deleted.setdefault(key, {})[uid] = self._deadline()
 
     def observe_add(self, key: str, uid: str) -> None:
         d = self.created.get(key)
@@ -270,7 +285,7 @@ class Expectations:
         dl = self.deleted.get(key)
         if not cr and not dl:
             return children
-        now = time.monotonic()
+        now = self.clock.now_ns()
         if dl:
             for uid in [u for u, exp in dl.items() if exp < now]:
                 del dl[uid]
@@ -296,7 +311,7 @@ class CronReconciler(Reconciler):
         self.engine = engine or default_engine()
         self.opts = options or ReconcilerOptions()
         self.cron_informer = cron_informer
-        self.expect = Expectations(self.opts.expectation_ttl)
+        self.expect = Expectations(self.opts.expectation_ttl, self.clock)
         self.child_informers: Dict[GroupVersionKind, Informer] = {}
         self.on_child_informer: Optional[Callable[[GroupVersionKind, Informer], None]] = None
         # the child informers' selector, and labels stamped on every child (label-routed sharding)
@@ -358,29 +373,28 @@ class CronReconciler(Reconciler):
             err: Optional[BaseException] = None
             gc: Optional[List["asyncio.Future[None]"]] = [] if self.opts.overlap_gc_deletes else None
             try:
-                result = await self._sync(cron, log, gc)
-            except Exception as e:  # noqa: BLE001 - joined with the patch error below
-                err = e
-            # B2: deferred status patch when status changed semantically (cron_controller.go:107-120)
-            if not old_status.semantic_equal(cron.status):
                 try:
-                    if gc:
-                        # the DELETE tasks are already running: the PATCH overlaps them
-                        pending, gc = gc, None
-                        try:
-                            await self._patch_status(old_obj, cron, log)
-                        finally:
-                            await self._await_gc(pending)
-                    else:
-                        await self._patch_status(old_obj, cron, log)
-                except Exception as pe:  # noqa: BLE001
-                    perr = RuntimeError(f"failed to patch Cron status: {pe}")
-                    perr.__cause__ = pe
-                    err = JoinedError(err, perr) if err is not None else perr
-                if err is not None:
-                    result = Result()
-            if gc:
-                await self._await_gc(gc)
+                    result = await self._sync(cron, log, gc)
+                except Exception as e:  # noqa: BLE001 - joined with the patch error below
+                    err = e
+                # B2: deferred status patch when status changed semantically (cron_controller.go:107-120)
+                if not old_status.semantic_equal(cron.status):
+                    try:
+                        await self._patch_status(old_obj, cron, log)  # overlaps the running GC DELETEs
+                    except Exception as pe:  # noqa: BLE001
+                        perr = RuntimeError(f"failed to patch Cron status: {pe}")
+                        perr.__cause__ = pe
+                        err = JoinedError(err, perr) if err is not None else perr
+                    if err is not None:
+                        result = Result()
+                if gc:
+                    await self._await_gc(gc)
+            except asyncio.CancelledError:
+                # the reconcile itself is cancelled (shutdown, leader loss): stop its DELETEs
+                # too instead of waiting up to a request timeout for each
+                if gc:
+                    aio.cancel_all(gc)
+                raise
             if err is not None:
                 raise err
             return result
@@ -400,15 +414,10 @@ class CronReconciler(Reconciler):
     @staticmethod
     async def _await_gc(gc: List["asyncio.Future[None]"]) -> None:
         """Wait for every overlapped GC DELETE; each logs its own API error (B7), anything
-        else it raised is dropped like ``gather(return_exceptions=True)`` would."""
-        for f in gc:
-            try:
-                await f
-            except asyncio.CancelledError:
-                if not f.cancelled():  # this reconcile itself is being cancelled
-                    raise
-            except Exception:  # noqa: BLE001
-                pass
+        else it raised is dropped like ``gather(return_exceptions=True)`` would.  A
+        cancellation of the reconcile propagates (``asyncio.wait`` neither cancels the
+        DELETEs nor mistakes their outcome for the caller's)."""
+        await aio.wait_all(gc)
 
     async def _patch_status(self, old_obj: Dict[str, Any], cron: Cron, log: Logger) -> None:
         new_status = cron.status.to_dict(shared=True)
@@ -642,13 +651,15 @@ class CronReconciler(Reconciler):
                 self.latency_observer(self._ckey(cron), missed_run, created)
             metrics.child(metrics.SCHEDULE_LATENCY, "cron").observe(
                 max(0.0, (self.clock.now_ns() - missed_run.unix_nano()) / 1e9))
-        except errors.ApiError as e:
+        except BaseException as e:  # API or transport error, or cancellation: nothing is in flight
             if self.opts.expectations:
                 self.expect.drop_pending(self._ckey(cron), wm.get("name", ""))
-            if errors.is_already_exists(e):
+            if isinstance(e, errors.ApiError) and errors.is_already_exists(e):
                 log.info(f"{gvk.kind} already exists", **{gvk.kind: ref})
             else:
-                self.recorder.eventf(cron.to_dict(), Warning, "FailedCreate", "Error creating %s: %s", gvk.kind, e)
+                if isinstance(e, Exception):
+                    self.recorder.eventf(cron.to_dict(), Warning, "FailedCreate", "Error creating %s: %s",
+                                         gvk.kind, e)
                 raise
         # B20 (cron_controller.go:237)
         cron.status.last_schedule_time = now
@@ -822,12 +833,12 @@ class CronReconciler(Reconciler):
         With ``gc`` (a list) the DELETEs are started and appended there instead of
         awaited one by one (``ReconcilerOptions.overlap_gc_deletes``)."""
         for op in self._sync_history(cron, terminated, log, gc):
-            await op
+            await op()
 
     def _sync_history(self, cron: Cron, terminated: List[Child], log: Logger,
                       gc: Optional[List["asyncio.Future[None]"]]) -> List[Any]:
         """The body of :meth:`sync_cron_history`.  GC DELETEs go to ``gc`` as started tasks,
-        or (``gc`` is None) are returned as coroutines for the caller to await in order."""
+        or (``gc`` is None) are returned as coroutine functions for the caller to await in order."""
         chatty = log.enabled()
         if chatty:
             log.v(1).info("Syncing Cron history")
@@ -851,13 +862,13 @@ class CronReconciler(Reconciler):
                 if chatty:
                     log.info(f"Deleting terminated {wgvk.kind}", **{wgvk.kind: ref})
                 uid = m.get("uid", "")
-                if self.opts.expectations:  # before the call: the watch event may beat the response
-                    self.expect.expect_delete(self._ckey(cron), uid)
-                op = self._gc_delete(cron, wgvk, m.get("namespace", ""), m.get("name", ""), uid, ref, log)
+                args = (cron, wgvk, m.get("namespace", ""), m.get("name", ""), uid, ref, log)
                 if gc is None:
-                    ops.append(op)
+                    # the coroutine is created only when it is awaited: nothing is left un-awaited
+                    # if an earlier DELETE ends the reconcile
+                    ops.append(functools.partial(self._gc_delete, *args))
                 else:
-                    gc.append(asyncio.ensure_future(op))
+                    gc.append(asyncio.ensure_future(self._gc_delete(*args)))
                 continue
             if not memo_ok:
                 info = None
@@ -891,12 +902,19 @@ class CronReconciler(Reconciler):
     async def _gc_delete(self, cron: Cron, gvk: GroupVersionKind, namespace: str, name: str, uid: str,
                          ref: ObjectRef, log: Logger) -> None:
         """One history-limit DELETE (Background); errors are only logged (``cron_controller.go:324-333``)."""
+        if self.opts.expectations:  # before the call: the watch event may beat the response
+            self.expect.expect_delete(self._ckey(cron), uid)
         try:
             await self.client.delete(gvk, namespace, name, propagation_policy="Background", discard_response=True)
             self.stats["deletes"] += 1
             metrics.child(metrics.WORKLOADS_DELETED, gvk.kind, "history").inc()
-        except errors.ApiError as e:
-            if not errors.is_not_found(e):
+        except asyncio.CancelledError:
+            # the DELETE may or may not have reached the apiserver: let the informer decide
+            if self.opts.expectations:
+                self.expect.observe_delete(self._ckey(cron), uid)
+            raise
+        except Exception as e:  # noqa: BLE001 - any Delete error is only logged (:324-333)
+            if not (isinstance(e, errors.ApiError) and errors.is_not_found(e)):
                 if self.opts.expectations:
                     self.expect.observe_delete(self._ckey(cron), uid)
                 log.error(e, f"Failed to delete terminated {gvk.kind}", **{gvk.kind: ref})

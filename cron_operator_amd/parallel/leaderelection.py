@@ -27,7 +27,7 @@ from typing import Any, Awaitable, Callable, Dict, Optional
 from ..api import errors
 from ..api.meta import GroupVersionResource
 from ..runtime import metrics
-from ..utils import jsonutil
+from ..utils import aio, jsonutil
 from ..utils.clock import Clock, RealClock
 from ..utils.gotime import NANOS, UTC, GoTime, parse_rfc3339
 from ..utils.logging import get_logger
@@ -202,11 +202,7 @@ class LeaderElector:
             timer.cancel()
         if task.done():
             return bool(task.result()) if not task.cancelled() and task.exception() is None else False
-        task.cancel()
-        try:
-            await task
-        except (asyncio.CancelledError, Exception):
-            pass
+        await aio.cancel_and_wait(task)
         return False
 
     def _jitter(self, d: float) -> float:
@@ -283,7 +279,8 @@ class LeaderElector:
                     raise started.exception()  # type: ignore[misc]
                 await renew
             finally:
-                renew.cancel()
+                # wait for an in-flight renewal PUT to end before release() writes the lease
+                await aio.cancel_and_wait(renew)
             on_stopped()
         except asyncio.CancelledError:
             if self.release_on_cancel:
@@ -291,8 +288,4 @@ class LeaderElector:
             raise
         finally:
             if started is not None and not started.done():
-                started.cancel()
-                try:
-                    await started
-                except (asyncio.CancelledError, Exception):
-                    pass
+                await aio.cancel_and_wait(started)

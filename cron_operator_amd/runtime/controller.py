@@ -28,6 +28,7 @@ from typing import Any, Awaitable, Callable, Dict, List, Optional, Tuple
 
 from ..api.meta import GroupVersionKind, NamespacedName, controller_ref
 from ..parallel.workqueue import ShutDown, WorkQueue
+from ..utils import aio
 from ..utils.clock import Clock
 from ..utils.logging import Logger, get_logger, log_constructor
 from . import metrics, tracing
@@ -304,14 +305,8 @@ class Controller:
 
     async def stop(self) -> None:
         self.queue.shutdown()
-        for t in self._workers:
-            t.cancel()
-        for t in self._workers:
-            try:
-                await t
-            except (asyncio.CancelledError, Exception):
-                pass
-        self._workers.clear()
+        workers, self._workers = self._workers, []
+        await aio.cancel_and_wait(*workers)
         self.started = False
 
     async def wait_idle(self, settle: float = 0.0, timeout: float = 60.0) -> bool:

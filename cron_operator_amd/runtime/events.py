@@ -21,6 +21,7 @@ from typing import Any, Dict, List, Optional, Tuple
 
 from ..api import errors
 from ..api.meta import GroupVersionResource
+from ..utils import aio
 from ..utils.clock import Clock, RealClock
 from ..utils.gotime import GoTime, UTC
 from ..utils.logging import get_logger
@@ -100,12 +101,8 @@ class Broadcaster:
         if drain:
             await self.flush(timeout=2.0)
         if self._task is not None:
-            self._task.cancel()
-            try:
-                await self._task
-            except (asyncio.CancelledError, Exception):
-                pass
-            self._task = None
+            task, self._task = self._task, None
+            await aio.cancel_and_wait(task)
 
     async def flush(self, timeout: float = 5.0) -> None:
         deadline = time.monotonic() + timeout

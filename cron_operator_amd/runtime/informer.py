@@ -33,7 +33,7 @@ from typing import Any, Callable, Dict, Iterable, List, Optional, Set, Tuple
 
 from ..api import errors
 from ..api.meta import GroupVersionKind, GroupVersionResource
-from ..utils import jsonutil
+from ..utils import aio, jsonutil
 from ..utils.clock import Clock, TimerHandle
 from ..utils.gotime import NANOS
 from ..utils.logging import get_logger
@@ -491,11 +491,7 @@ class Informer:
             except Exception:
                 pass
         if self._task is not None:
-            self._task.cancel()
-            try:
-                await self._task
-            except (asyncio.CancelledError, Exception):
-                pass
+            await aio.cancel_and_wait(self._task)
 
 
 class Cache:

@@ -18,7 +18,7 @@ from dataclasses import dataclass, field
 from typing import Awaitable, Callable, List, Optional
 
 from ..parallel.leaderelection import LeaderElector, in_cluster_namespace
-from ..utils import gctune
+from ..utils import aio, gctune
 from ..utils.clock import Clock, RealClock
 from ..utils.logging import get_logger
 from .client import Client
@@ -160,11 +160,7 @@ class Manager:
                         raise exc
                     lost = True
                 else:
-                    le_task.cancel()
-                    try:
-                        await le_task
-                    except (asyncio.CancelledError, Exception):
-                        pass
+                    await aio.cancel_and_wait(le_task)
                 stop_task.cancel()
             else:
                 await self._start_leading()
@@ -181,14 +177,8 @@ class Manager:
     async def shutdown(self) -> None:
         for c in self.controllers:
             await c.stop()
-        for t in self._tasks:
-            t.cancel()
-        for t in self._tasks:
-            try:
-                await t
-            except (asyncio.CancelledError, Exception):
-                pass
-        self._tasks.clear()
+        tasks, self._tasks = self._tasks, []
+        await aio.cancel_and_wait(*tasks)
         await self.cache.stop()
         await self.broadcaster.stop()
         await self.metrics_server.stop()

@@ -30,6 +30,7 @@ from ..api import errors
 from ..api.meta import GroupVersionResource
 from ..runtime.client import Client
 from ..runtime.informer import EventHandler, Informer
+from ..utils import aio
 from ..utils.clock import Clock, RealClock
 from ..utils.gotime import GoTime, UTC
 from ..utils.logging import get_logger
@@ -241,11 +242,4 @@ class FakeTrainingOperator:
     async def stop(self) -> None:
         for inf in self.informers:
             await inf.stop()
-        for t in self._tasks:
-            if not t.done():
-                t.cancel()
-        for t in self._tasks:
-            try:
-                await t
-            except (asyncio.CancelledError, Exception):
-                pass
+        await aio.cancel_and_wait(*self._tasks)

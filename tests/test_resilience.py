@@ -194,7 +194,9 @@ async def test_leader_steps_down_within_renew_deadline_when_lease_updates_hang()
     stopped_after = None
     for sec in range(1, 30):
         env.clock.advance(1)
-        for _ in range(20):
+        # shutdown (workers, informers, broadcaster) waits for every cancelled task to end:
+        # give it enough loop turns within one virtual second
+        for _ in range(200):
             await asyncio.sleep(0)
         if env._mgr_task.done():
             stopped_after = sec
