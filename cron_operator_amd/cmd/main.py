@@ -127,10 +127,11 @@ def build_parser() -> argparse.ArgumentParser:
                          "--shard-count is split further), under a supervisor that serves the merged metrics "
                          "and the probes. Uses that many cores, like the reference's goroutine workers. "
                          "'auto': the CPUs the container may use (cgroup quota, else affinity).")
-    st.add_argument("--shard-routing", choices=["hash", "labels"], default="hash",
-                    help="hash: every shard watches all objects and drops other shards' keys; labels: shards "
-                         "label their Crons and children kubedl.io/shard=<index>-of-<count> and watch only "
-                         "their own (the apiserver splits the watch traffic).")
+    st.add_argument("--shard-routing", choices=["hash", "labels"], default="labels",
+                    help="Only when sharded. labels (default): shards label their Crons and children "
+                         "kubedl.io/shard=<index>-of-<count> and watch only their own (the apiserver splits "
+                         "the watch traffic; the configuration the benchmarks measure); hash: every shard "
+                         "watches all objects and drops other shards' keys (no labels written).")
     st.add_argument("--sync-period", default="10h", help="Minimum frequency at which every watched object is "
                                                         "reconciled again (controller-runtime's cache SyncPeriod; "
                                                         "Go duration, 0 disables).")

@@ -63,7 +63,7 @@ class ManagerOptions:
     shard_count: int = 1
     # "hash": every shard watches everything and drops other shards' keys; "labels": objects carry
     # kubedl.io/shard and each shard's informers select on it (controller/sharding.py)
-    shard_routing: str = "hash"
+    shard_routing: str = "labels"  # only used when shard_count > 1
     # informer watch liveness (runtime/informer.py): seconds without an event or bookmark
     # before a watch is presumed dead and re-established
     watch_idle_timeout: float = WATCH_IDLE_TIMEOUT

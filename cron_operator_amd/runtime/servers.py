@@ -245,10 +245,33 @@ class MetricsServer:
                 out.append(None)
         return tuple(out)
 
+    def _reload_pair(self, crt: str, key: str) -> None:
+        """Load a rotated pair into the live SSLContext only once it is known to load.
+
+        ``SSLContext.load_cert_chain`` installs the certificate *before* it checks the key,
+        so loading a new certificate with a stale or mismatched key straight into the live
+        context would leave it unusable (every handshake then fails).  The pair is therefore
+        snapshotted into private files (so it cannot change between the checks), loaded into
+        a scratch context first, and only then into the live one."""
+        with open(crt, "rb") as fh:
+            crt_pem = fh.read()
+        with open(key, "rb") as fh:
+            key_pem = fh.read()
+        with tempfile.TemporaryDirectory(prefix="cron-operator-cert-") as d:
+            scrt, skey = os.path.join(d, "tls.crt"), os.path.join(d, "tls.key")
+            for path, data in ((scrt, crt_pem), (skey, key_pem)):
+                fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_EXCL, 0o600)
+                with os.fdopen(fd, "wb") as fh:
+                    fh.write(data)
+            ssl.create_default_context(ssl.Purpose.CLIENT_AUTH).load_cert_chain(scrt, skey)
+            assert self._ctx is not None
+            self._ctx.load_cert_chain(scrt, skey)
+
     async def _watch_certs(self, crt: str, key: str) -> None:
         """certwatcher: poll the certificate and key; load a changed pair into the live
-        SSLContext (new handshakes use it).  A pair that does not load -- e.g. caught mid
-        rotation -- keeps the previous certificate and is retried on the next poll."""
+        SSLContext (new handshakes use it).  A pair that does not load -- caught mid
+        rotation, or a new certificate next to the old key -- keeps the previous certificate
+        serving and is retried on the next poll."""
         last = self._stamp(crt, key)
         while True:
             await asyncio.sleep(self.cert_poll_interval)
@@ -257,7 +280,7 @@ class MetricsServer:
                 continue
             metrics.CERT_READS.inc()
             try:
-                self._ctx.load_cert_chain(crt, key)
+                self._reload_pair(crt, key)
             except (OSError, ssl.SSLError) as e:
                 metrics.CERT_READ_ERRORS.inc()
                 self.log.error(e, "error loading the rotated certificate, keeping the current one",

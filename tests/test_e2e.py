@@ -258,7 +258,8 @@ def test_cli_help_version_crd():
 
 
 def test_shard_processes_in_one_pod(cluster):
-    """`start --shard-processes 2`: one supervisor, two shard processes with their own Leases;
+    """`start --shard-processes 3` with the default routing (labels): one supervisor, three shard
+    processes with their own Leases, each labelling and watching only its own Crons;
     the supervisor's /metrics merges theirs (labelled by shard), its probes cover both, a
     crashed shard process is restarted, and SIGTERM stops everything cleanly."""
     import psutil
@@ -269,7 +270,7 @@ def test_shard_processes_in_one_pod(cluster):
     _api(base, "POST", "/api/v1/namespaces", {"apiVersion": "v1", "kind": "Namespace",
                                               "metadata": {"name": "procs"}})
     proc, probe, mport = _start_operator(cluster, "--leader-elect", "--metrics-secure=false",
-                                         "--shard-processes", "2", "--shard-routing", "labels")
+                                         "--shard-processes", "3")
     names = [f"p{i}" for i in range(6)]
     try:
         _wait(lambda: _get(f"http://127.0.0.1:{probe}/readyz")[0] == 200, 60, "readyz", proc)
@@ -290,24 +291,24 @@ def test_shard_processes_in_one_pod(cluster):
 
         for j in _wait(all_fired, 60, "every Cron fired", proc):
             cron = j["metadata"]["labels"]["kubedl.io/cron-name"]
-            assert j["metadata"]["labels"]["kubedl.io/shard"] == f"{shard_of('procs', cron, 2)}-of-2"
-        for i in range(2):
+            assert j["metadata"]["labels"]["kubedl.io/shard"] == f"{shard_of('procs', cron, 3)}-of-3"
+        for i in range(3):
             lease = _api(base, "GET", "/apis/coordination.k8s.io/v1/namespaces/cron-operator-system/leases/"
                                       f"619a52b8.kubedl.io-shard-{i}")
             assert lease["spec"]["holderIdentity"]
 
         status, body = _get(f"http://127.0.0.1:{mport}/metrics")
         assert status == 200
-        for i in range(2):
+        for i in range(3):
             assert f'controller_runtime_reconcile_total{{shard="{i}",controller="cron",result="requeue_after"}}' \
                 in body
         assert body.count("# TYPE controller_runtime_reconcile_total counter") == 1
 
         # a shard process dies: health reports it, the supervisor restarts it
         kids = psutil.Process(proc.pid).children()
-        assert len(kids) == 2
+        assert len(kids) == 3
         kids[0].kill()
-        _wait(lambda: len([k for k in psutil.Process(proc.pid).children() if k.pid != kids[0].pid]) == 2,
+        _wait(lambda: len([k for k in psutil.Process(proc.pid).children() if k.pid != kids[0].pid]) == 3,
               30, "shard process restarted", proc)
         _wait(lambda: _get(f"http://127.0.0.1:{probe}/readyz")[0] == 200, 60, "readyz after restart", proc)
         kids = psutil.Process(proc.pid).children()

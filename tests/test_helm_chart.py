@@ -52,7 +52,8 @@ def test_replicas_and_pull_policy():
     ({"compatMode": "reference"}, "--compat-mode=reference"),
     ({"extraArgs": ["--namespace=team-a"]}, "--namespace=team-a"),
     ({"sharding": {"processes": 4, "routing": "labels"}}, "--shard-processes=4"),
-    ({"sharding": {"processes": 4, "routing": "labels"}}, "--shard-routing=labels"),
+    ({"sharding": {"processes": 4}}, "--shard-routing=labels"),
+    ({"sharding": {"count": 2, "routing": "hash"}}, "--shard-routing=hash"),
     ({"sharding": {"count": 2, "index": 1}}, "--shard-index=1"),
 ])
 def test_args(values, arg):

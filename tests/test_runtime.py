@@ -632,6 +632,52 @@ async def test_metrics_server_reloads_a_rotated_certificate(tmp_path):
         await sm.stop()
 
 
+async def test_metrics_cert_rotation_with_mismatched_key_keeps_serving(tmp_path):
+    """A new certificate lands before its key (a rotation seen half way, or a bad Secret):
+    the pair does not match, so the watcher must keep serving the previous certificate --
+    the live context is never half-loaded -- and pick up the new pair once the key follows."""
+    import hashlib
+    import ssl
+
+    from cron_operator_amd.runtime.servers import self_signed_cert
+
+    async def fingerprint(port):
+        ctx = ssl.create_default_context()
+        ctx.check_hostname = False
+        ctx.verify_mode = ssl.CERT_NONE
+        _, w = await asyncio.open_connection("127.0.0.1", port, ssl=ctx)
+        der = w.get_extra_info("ssl_object").getpeercert(binary_form=True)
+        w.close()
+        return hashlib.sha256(der).hexdigest()
+
+    certs = tmp_path / "certs"
+    certs.mkdir()
+    crt, key = self_signed_cert(str(certs), host="first")
+    env = TestEnv()
+    sm = MetricsServer("127.0.0.1:0", secure=True, cert_dir=str(certs), client=env.new_client(),
+                       cert_poll_interval=0.05)
+    await sm.start()
+    try:
+        first = await fingerprint(sm.port)
+        other = tmp_path / "other"
+        other.mkdir()
+        ncrt, nkey = self_signed_cert(str(other), host="second")
+        os.replace(ncrt, crt)  # valid certificate, old key: KEY_VALUES_MISMATCH
+        await asyncio.sleep(0.4)
+        assert sm.cert_reloads == 0
+        for _ in range(3):  # still serving, with the previous certificate
+            assert await fingerprint(sm.port) == first
+        os.replace(nkey, key)
+        for _ in range(100):
+            await asyncio.sleep(0.05)
+            if sm.cert_reloads:
+                break
+        assert sm.cert_reloads == 1
+        assert await fingerprint(sm.port) != first
+    finally:
+        await sm.stop()
+
+
 async def test_informer_transforms_list_pages_once():
     """A paged initial LIST is transformed page by page as it arrives, and each object exactly
     once (``_replace`` does not transform again); watch events are transformed as before."""
