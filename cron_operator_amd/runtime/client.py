@@ -23,6 +23,7 @@ from typing import Any, Dict, List, Optional, Tuple, Union
 from ..api import errors
 from ..api.meta import GroupVersion, GroupVersionKind, GroupVersionResource
 from ..utils import jsonutil
+from ..utils.gotime import format_duration
 from . import metrics, tracing
 from .ratelimit import TokenBucket, make_client_limiter
 
@@ -40,6 +41,50 @@ PATCH_CONTENT_TYPES = {
 
 
 # request-parameter keys (never sent as query parameters):
+# client-go rest.Request throttling thresholds [ext] (rest/request.go longThrottleLatency,
+# extraLongThrottleLatency)
+LONG_THROTTLE_LATENCY = 0.050
+EXTRA_LONG_THROTTLE_LATENCY = 1.0
+
+
+class ThrottledLogger:
+    """client-go's ``globalThrottledLogger`` [ext]: the first *enabled* setting decides --
+    with V(2) on, at most one line per second at V(2); otherwise at most one Info line per
+    10 s -- so a starved client reports it without flooding the log."""
+
+    SETTINGS = ((2, 1.0), (0, 10.0))  # (verbosity, min interval s)
+
+    def __init__(self, settings: Tuple[Tuple[int, float], ...] = SETTINGS, clock=time.monotonic):
+        self.settings = settings
+        self.clock = clock
+        self._last: Dict[int, float] = {}
+        self.lines = 0
+
+    def info(self, log: Any, msg: str) -> bool:
+        for level, interval in self.settings:
+            lg = log.v(level)
+            if not lg.enabled():
+                continue
+            now = self.clock()
+            last = self._last.get(level)
+            if last is not None and now - last < interval:
+                return False
+            self._last[level] = now
+            self.lines += 1
+            lg.info(msg)
+            return True
+        return False
+
+
+THROTTLED_LOGGER = ThrottledLogger()
+
+
+def _throttle_log():
+    from ..utils.logging import get_logger
+
+    return get_logger("rest")
+
+
 DISCARD = "_discardResponse"   # the caller ignores the response body
 ACCEPT = "_accept"             # Accept header override (server-side printing)
 TABLE_ACCEPT = "application/json;as=Table;v=v1;g=meta.k8s.io,application/json"
@@ -236,6 +281,8 @@ class Client:
         self.limiter = limiter if limiter is not None else make_client_limiter(qps, burst)
         self.mapper = mapper or RESTMapper(transport)
         self.host = getattr(transport, "host", "in-memory")
+        cfg = getattr(transport, "config", None)
+        self.url_base = getattr(cfg, "host", "") if cfg is not None else ""
         self.requests = 0
         self.requests_by_verb: Dict[str, int] = {}
         self._m_req: Dict[Tuple[str, str], Any] = {}
@@ -255,13 +302,36 @@ class Client:
             return target
         return (await self.mapper.resource_for(target))[0]
 
-    async def _throttle(self, verb: str) -> None:
+    async def _throttle(self, verb: str, gvr: GroupVersionResource, namespace: str, name: str,
+                        subresource: str) -> None:
         if self.limiter is not None:
             d = await self.limiter.wait()
             m = self._m_rl.get(verb)
             if m is None:
                 m = self._m_rl[verb] = metrics.REST_RATE_LIMIT.labels(verb, self.host)
             m.observe(d)
+            if d > LONG_THROTTLE_LATENCY:
+                self._log_throttle(d, verb, gvr, namespace, name, subresource)
+
+    def _log_throttle(self, d: float, verb: str, gvr: GroupVersionResource, namespace: str, name: str,
+                      subresource: str) -> None:
+        """client-go ``tryThrottleWithInfo`` [ext]: a wait on the QPS bucket above 50 ms is
+        logged at V(3); above 1 s through the process-wide throttled logger, so a starved
+        operator says so -- the reference sets ``--qps``/``--burst`` on this rest config
+        (``/root/reference/cmd/operator/start.go:152-154,218-219``)."""
+        log = _throttle_log()
+        v3 = log.v(3).enabled()
+        if not v3 and d <= EXTRA_LONG_THROTTLE_LATENCY:
+            return
+        from .http import resource_path
+
+        msg = (f"Waited for {format_duration(int(d * 1e9))} due to client-side throttling, not priority and "
+               f"fairness, request: {self._METHOD.get(verb, verb.upper())}:{self.url_base}"
+               f"{resource_path(gvr, namespace, name, subresource)}")
+        if v3:
+            log.v(3).info(msg)
+        if d > EXTRA_LONG_THROTTLE_LATENCY:
+            THROTTLED_LOGGER.info(log, msg)
 
     _METHOD = {"get": "GET", "list": "GET", "watch": "GET", "create": "POST", "update": "PUT", "patch": "PATCH",
                "delete": "DELETE", "deletecollection": "DELETE"}
@@ -269,7 +339,7 @@ class Client:
     async def _do(self, verb: str, gvr: GroupVersionResource, namespace: str = "", name: str = "",
                   subresource: str = "", body: Any = None, params: Optional[Dict[str, Any]] = None) -> Any:
         if self.limiter is not None:
-            await self._throttle(verb)
+            await self._throttle(verb, gvr, namespace, name, subresource)
         self.requests += 1
         self.requests_by_verb[verb] = self.requests_by_verb.get(verb, 0) + 1
         t0 = time.perf_counter()

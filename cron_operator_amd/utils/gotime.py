@@ -566,3 +566,32 @@ def parse_duration(s: str) -> int:
     return -total if neg else total
 
 
+
+def _frac(v: int, unit: int) -> str:
+    whole, rest = divmod(v, unit)
+    if not rest:
+        return str(whole)
+    digits = len(str(unit)) - 1
+    return f"{whole}.{rest:0{digits}d}".rstrip("0")
+
+
+def format_duration(ns: int) -> str:
+    """Go ``time.Duration.String()``: ``1.5s``, ``2m3.25s``, ``1h0m0s``, ``250ms``, ``0s``."""
+    if ns == 0:
+        return "0s"
+    sign = "-" if ns < 0 else ""
+    u = abs(ns)
+    if u < SECOND:
+        if u < 1_000:
+            return f"{sign}{u}ns"
+        if u < 1_000_000:
+            return f"{sign}{_frac(u, 1_000)}µs"
+        return f"{sign}{_frac(u, 1_000_000)}ms"
+    h, rem = divmod(u, HOUR)
+    m, rem = divmod(rem, MINUTE)
+    out = sign
+    if h:
+        out += f"{h}h"
+    if h or m:
+        out += f"{m}m"
+    return out + _frac(rem, SECOND) + "s"
