@@ -460,7 +460,7 @@ class Client:
                     label_selector: Optional[str] = None, field_selector: Optional[str] = None,
                     allow_bookmarks: bool = True, timeout_seconds: Optional[int] = None) -> WatchStream:
         gvr = self._gvr_now(target) or await self._gvr(target)
-        await self._throttle("watch")
+        await self._throttle("watch", gvr, namespace, "", "")
         self.requests += 1
         self.requests_by_verb["watch"] = self.requests_by_verb.get("watch", 0) + 1
         params: Dict[str, Any] = {"watch": "true", "resourceVersion": resource_version,
