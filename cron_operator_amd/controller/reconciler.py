@@ -27,6 +27,9 @@ option                     default here                           reference
 ``slim_child_cache``       cached children keep metadata, kind    typed informers cache whole objects
                            and status (``spec`` is never read);    (``Owns(&PyTorchJob{})``)
                            cached Crons drop ``managedFields``
+``wire_codecs``            watch events decoded by plan: child     every event decoded whole
+                           ``spec`` skipped, Cron ``spec`` and
+                           status history entries reused by bytes
 =========================  =====================================  =======================================
 
 ``overlap_gc_deletes``: a GC DELETE's outcome feeds nothing else in the
@@ -36,6 +39,14 @@ DELETEs are started as they are decided and awaited together with the status
 PATCH at the end.  Under apiserver latency a reconcile then costs one round
 trip less per GC'd child; the reconcile still returns only after every DELETE
 finished, so per-key serialisation is unchanged.
+
+``wire_codecs`` (:class:`WireCodecs`): the Cron's status write is encoded through
+a memo that remembers the bytes of every history entry it writes, and the Cron
+informer decodes its watch events through the same memo -- so the echo of our own
+write arrives holding the reconciler's own (read-only) entry dicts.  The own-write
+check and the next merge patch then compare those entries by identity, and the
+bulk of each Cron event (its spec and history) is never rebuilt.  Byte-identical
+spans are reused only, so the decoded objects are exactly what a plain decode gives.
 
 ``dedupe_ran_tick``: the reference advances ``lastScheduleTime`` only in the
 deferred status patch after a successful CREATE (B20).  If that patch fails, or
@@ -55,6 +66,7 @@ from __future__ import annotations
 import asyncio
 import functools
 import json
+import operator
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional, Tuple
 
@@ -98,6 +110,7 @@ from ..utils.gotime import LOCAL, NANOS, GoTime
 from ..utils.logging import Logger, ObjectRef
 
 CHILD_INDEX = "cron-name"
+_SORT_KEY = operator.attrgetter("sort_key")  # _ChildInfo -> creation-time sort key
 MAX_INT = 2**63 - 1
 
 
@@ -191,6 +204,7 @@ class ReconcilerOptions:
     dedupe_ran_tick: bool = True
     overlap_gc_deletes: bool = True
     slim_child_cache: bool = True
+    wire_codecs: bool = True
     # cache mode: how long a reconcile waits for a new child informer's first LIST before
     # it falls back to a live LIST; a LIST that *fails* (403, 404, 5xx) is returned as the
     # reconcile's error at once, like the reference's live LIST (cron_controller.go:129-133)
@@ -207,8 +221,29 @@ class ReconcilerOptions:
                                  own_write_filter=False, dynamic_watches=False, expectations=False,
                                  fold_created_into_active=False, skip_expected_events=False,
                                  classification_cache=False, dedupe_ran_tick=False,
-                                 overlap_gc_deletes=False, slim_child_cache=False,
+                                 overlap_gc_deletes=False, slim_child_cache=False, wire_codecs=False,
                                  workload=WorkloadPolicy.reference())
+
+
+class WireCodecs:
+    """Plan-driven JSON codecs for the objects this controller exchanges (``_fastjson.Codec``;
+    the Python twin ignores memo paths).  One memo is shared: the status-write encoder
+    remembers each history entry it writes, the Cron event decoder hands those objects
+    back when the watch echoes the same bytes.  ``slim`` also skips what the caches drop
+    anyway: a child's ``spec`` and every ``managedFields``."""
+
+    def __init__(self, slim: bool = True, memo_slots: int = 1 << 16):
+        self.memo = jsonutil.Memo(memo_slots)
+        mf = ("metadata", "managedFields")
+        child_skip = [("spec",), mf] if slim else []
+        child_memo = [("metadata", "labels"), ("metadata", "ownerReferences")]
+        self.cron_event = jsonutil.Codec(skip=[("object",) + mf] if slim else [],
+                                         memo_paths=[("object", "spec"), ("object", "status", "history", "*")],
+                                         memo=self.memo)
+        self.child_event = jsonutil.Codec(skip=[("object",) + p for p in child_skip],
+                                          memo_paths=[("object",) + p for p in child_memo], memo=self.memo)
+        self.child_object = jsonutil.Codec(skip=child_skip, memo_paths=child_memo, memo=self.memo)
+        self.status_patch = jsonutil.Codec(memo_paths=[("status", "history", "*")], memo=self.memo)
 
 
 class Expectations:
@@ -303,7 +338,8 @@ class Expectations:
 class CronReconciler(Reconciler):
     def __init__(self, client: Client, cache: Optional[Cache], recorder: EventRecorder,
                  clock: Optional[Clock] = None, engine: Optional[CronEngine] = None,
-                 options: Optional[ReconcilerOptions] = None, cron_informer: Optional[Informer] = None):
+                 options: Optional[ReconcilerOptions] = None, cron_informer: Optional[Informer] = None,
+                 codecs: Optional[WireCodecs] = None):
         self.client = client
         self.cache = cache
         self.recorder = recorder
@@ -311,6 +347,9 @@ class CronReconciler(Reconciler):
         self.engine = engine or default_engine()
         self.opts = options or ReconcilerOptions()
         self.cron_informer = cron_informer
+        # setup_with_manager passes the instance its Cron informer decodes with (one shared memo)
+        self.codecs: Optional[WireCodecs] = codecs if codecs is not None or not self.opts.wire_codecs else \
+            WireCodecs(self.opts.slim_child_cache)
         self.expect = Expectations(self.opts.expectation_ttl, self.clock)
         self.child_informers: Dict[GroupVersionKind, Informer] = {}
         self.on_child_informer: Optional[Callable[[GroupVersionKind, Informer], None]] = None
@@ -422,7 +461,10 @@ class CronReconciler(Reconciler):
     async def _patch_status(self, old_obj: Dict[str, Any], cron: Cron, log: Logger) -> None:
         new_status = cron.status.to_dict(shared=True)
         old_status = old_obj.get("status") or {}
-        patch = jsonutil.create_merge_patch({"status": old_status}, {"status": new_status} if new_status else {})
+        codecs = self.codecs
+        # share: the patch is only serialised, so it may hold new_status's (read-only) entries
+        patch = jsonutil.create_merge_patch({"status": old_status}, {"status": new_status} if new_status else {},
+                                            codecs is not None)
         m = old_obj.get("metadata") or {}
         key = f"{m.get('namespace', '')}/{m.get('name', '')}"
         if self.opts.classification_cache:
@@ -434,9 +476,11 @@ class CronReconciler(Reconciler):
         if self.opts.own_write_filter:
             # recorded before the call: the watch event can overtake the PATCH response
             self.own_writes[key] = (m.get("generation"), new_status)
+        body: Any = codecs.status_patch.dumpb(patch) if codecs is not None else patch
         try:
-            with tracing.span("patch_status", bytes=len(jsonutil.dumps(patch)) if tracing.get_tracer().enabled else 0):
-                await self.client.patch(CRON_GVR, m.get("namespace", ""), m.get("name", ""), patch, "merge",
+            with tracing.span("patch_status", bytes=len(body) if body.__class__ is bytes else
+                              len(jsonutil.dumps(patch)) if tracing.get_tracer().enabled else 0):
+                await self.client.patch(CRON_GVR, m.get("namespace", ""), m.get("name", ""), body, "merge",
                                         "status", discard_response=True)
         except Exception:
             self.own_writes.pop(key, None)
@@ -505,12 +549,18 @@ class CronReconciler(Reconciler):
         active: List[Child] = []
         terminated: List[Child] = []
         if infos is not None:
-            # children classified once per version, at informer-event time (Informer.derive)
+            # children classified once per version, at informer-event time (Informer.derive);
+            # sorted here once (C-level key) so both partitions come out ordered (B6/B7)
+            if len(infos) > 1:
+                infos.sort(key=_SORT_KEY)
+            presorted = True
             for info in infos:
                 if info.err is not None:
                     log.error(info.err, f"Failed to get {gvk.kind} status")
                     continue
                 (terminated if info.cls.finished else active).append((info.obj, info.cls, info))  # type: ignore
+        else:
+            presorted = False
         cache = self._class_cache if self.opts.classification_cache else None
         for w in workloads:
             try:
@@ -541,8 +591,8 @@ class CronReconciler(Reconciler):
             if gc is not None:  # DELETEs are only started: nothing to await here
                 if chatty:
                     log.v(1).info("Syncing Cron status")
-                self.sync_active_list(cron, gvk, active, log)
-                self._sync_history(cron, terminated, log, gc)
+                self.sync_active_list(cron, gvk, active, log, presorted)
+                self._sync_history(cron, terminated, log, gc, presorted)
             else:
                 await self.sync_status(cron, gvk, active, terminated, log, gc)
 
@@ -630,7 +680,8 @@ class CronReconciler(Reconciler):
         try:
             with tracing.span("create_workload", kind=gvk.kind, name=wm.get("name", ""),
                               tick=missed_run.rfc3339()) as sp:
-                created = await self.client.create(gvk, workload, wm.get("namespace", ""))
+                created = await self.client.create(gvk, workload, wm.get("namespace", ""),
+                                                   decoder=self.codecs.child_object if self.codecs else None)
                 sp.set(tick_to_create_ms=(self.clock.now_ns() - missed_run.unix_nano()) / 1e6)
             self.stats["creates"] += 1
             metrics.child(metrics.WORKLOADS_CREATED, gvk.kind).inc()
@@ -707,7 +758,8 @@ class CronReconciler(Reconciler):
 
             inf = await self.cache.get_informer(gvk, label_selector=self.child_selector,
                                                 indexers={CHILD_INDEX: label_index(LABEL_CRON_NAME)},
-                                                transform=slim_child if self.opts.slim_child_cache else None)
+                                                transform=slim_child if self.opts.slim_child_cache else None,
+                                                decoder=self.codecs.child_event if self.codecs else None)
             self.child_informers[gvk] = inf
             inf.start()
             if self.on_child_informer is not None:
@@ -804,11 +856,12 @@ class CronReconciler(Reconciler):
             items.sort(key=lambda x: creation_timestamp(x[0]).key())
 
     def sync_active_list(self, cron: Cron, gvk: GroupVersionKind, active: List[Child],
-                         log: Logger) -> None:
+                         log: Logger, presorted: bool = False) -> None:
         """``syncActiveList`` (``cron_controller.go:284-304``)."""
         if log.enabled():
             log.v(1).info("Syncing active list")
-        self._sort(active)
+        if not presorted:
+            self._sort(active)
         refs = []
         with_rv = self.opts.active_ref_resource_version
         for w, _, info in active:
@@ -836,14 +889,15 @@ class CronReconciler(Reconciler):
             await op()
 
     def _sync_history(self, cron: Cron, terminated: List[Child], log: Logger,
-                      gc: Optional[List["asyncio.Future[None]"]]) -> List[Any]:
+                      gc: Optional[List["asyncio.Future[None]"]], presorted: bool = False) -> List[Any]:
         """The body of :meth:`sync_cron_history`.  GC DELETEs go to ``gc`` as started tasks,
         or (``gc`` is None) are returned as coroutine functions for the caller to await in order."""
         chatty = log.enabled()
         if chatty:
             log.v(1).info("Syncing Cron history")
         ops: List[Any] = []
-        self._sort(terminated)
+        if not presorted:
+            self._sort(terminated)
         n = len(terminated)
         limit = cron.spec.history_limit if cron.spec.history_limit is not None else MAX_INT
         previous: Optional[Dict[str, CronHistory]] = None

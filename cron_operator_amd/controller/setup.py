@@ -28,7 +28,7 @@ from ..runtime.informer import EventHandler, Informer, label_index, strip_manage
 from ..runtime.manager import Manager
 from ..utils.logging import get_logger, log_constructor
 from . import sharding
-from .reconciler import CHILD_INDEX, CronReconciler, ReconcilerOptions, slim_child
+from .reconciler import CHILD_INDEX, CronReconciler, ReconcilerOptions, WireCodecs, slim_child
 
 CONTROLLER_NAME = "cron"
 
@@ -41,11 +41,13 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
     if mgr.opts.shard_routing not in sharding.ROUTINGS:
         raise ValueError(f"unknown shard routing {mgr.opts.shard_routing!r}")
     by_label = count > 1 and mgr.opts.shard_routing == "labels"
+    codecs = WireCodecs(opts.slim_child_cache) if opts.wire_codecs else None
     cron_inf = await mgr.cache.get_informer(CRON_GVK,
                                             label_selector=sharding.shard_selector(index, count) if by_label else None,
-                                            transform=strip_managed_fields if opts.slim_child_cache else None)
+                                            transform=strip_managed_fields if opts.slim_child_cache else None,
+                                            decoder=codecs.cron_event if codecs is not None else None)
     rec = CronReconciler(mgr.client, mgr.cache, mgr.get_event_recorder_for(CONTROLLER_NAME), mgr.clock, engine,
-                         opts, cron_inf)
+                         opts, cron_inf, codecs)
     ctrl = Controller(CONTROLLER_NAME, rec, mgr.clock, mgr.opts.max_concurrent_reconciles, log)
     ctrl.set_log_constructor(log_constructor(log, "Cron"))
     assigner: Optional[sharding.ShardAssigner] = None
@@ -114,7 +116,8 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
             if opts.list_mode == "cache":
                 inf = await mgr.cache.get_informer(gvk, label_selector=rec.child_selector,
                                                    indexers={CHILD_INDEX: label_index(LABEL_CRON_NAME)},
-                                                   transform=slim_child if opts.slim_child_cache else None)
+                                                   transform=slim_child if opts.slim_child_cache else None,
+                                                   decoder=codecs.child_event if codecs is not None else None)
                 rec.child_informers[gvk] = inf
             else:
                 inf = await mgr.cache.get_informer(gvk, label_selector=rec.child_selector if by_label else None)

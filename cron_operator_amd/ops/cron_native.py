@@ -60,11 +60,37 @@ def _resolve_name(name: str) -> int:
     return zone_id(load_location(name))
 
 
+# the last resolution of Local: (its current implementation object, zone id).  LOCAL.reset()
+# (tests changing $TZ) makes impl() return a new object, which misses this cache.
+_local_hit: Optional[tuple] = None
+# other Locations are immutable: their id is resolved once (the reconciler asks on every
+# schedule computation -- several times per Cron fire)
+_by_loc: Dict[Location, int] = {}
+
+
 def zone_id(loc: Location) -> int:
     """Native zone id for a Location (registering it on first use)."""
-    mod = load()
+    global _local_hit
     if loc is UTC:
         return 0
+    if loc is LOCAL:
+        impl = LOCAL.impl()
+        hit = _local_hit
+        if hit is not None and hit[0] is impl:
+            return hit[1]
+        zid = _zone_id_slow(loc)
+        _local_hit = (impl, zid)
+        return zid
+    zid = _by_loc.get(loc)
+    if zid is None:
+        if len(_by_loc) >= 4096:  # e.g. a FixedZone per parsed "+08:00" timestamp
+            _by_loc.clear()
+        zid = _by_loc[loc] = _zone_id_slow(loc)
+    return zid
+
+
+def _zone_id_slow(loc: Location) -> int:
+    mod = load()
     if loc is LOCAL:
         impl = LOCAL.impl()
         key = "Local:" + (impl.key if isinstance(impl, ZoneLocation) else f"fixed{impl.fixed}")

@@ -44,6 +44,7 @@
 
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
+#include <structmember.h>
 
 #include <cstdint>
 #include <cstdio>
@@ -158,8 +159,18 @@ int equal_impl(PyObject* a, PyObject* b, int depth) {
   return PyObject_RichCompareBool(a, b, Py_EQ);
 }
 
-PyObject* merge_patch_impl(PyObject* old, PyObject* nw, int depth) {
-  if (!PyDict_CheckExact(old) || !PyDict_CheckExact(nw)) return deepcopy_impl(nw, depth);
+// share: the patch references `nw`'s subtrees instead of copying them (a patch that is
+// only serialised and dropped; `nw` must not change while the patch lives)
+inline PyObject* patch_value(PyObject* v, int depth, bool share) {
+  if (share) {
+    Py_INCREF(v);
+    return v;
+  }
+  return deepcopy_impl(v, depth);
+}
+
+PyObject* merge_patch_impl(PyObject* old, PyObject* nw, int depth, bool share = false) {
+  if (!PyDict_CheckExact(old) || !PyDict_CheckExact(nw)) return patch_value(nw, depth, share);
   PyObject* patch = PyDict_New();
   if (!patch) return nullptr;
   Py_ssize_t pos = 0;
@@ -169,10 +180,10 @@ PyObject* merge_patch_impl(PyObject* old, PyObject* nw, int depth) {
     PyObject* entry = nullptr;
     if (!ov) {
       if (PyErr_Occurred()) goto fail;
-      entry = deepcopy_impl(v, depth + 1);
+      entry = patch_value(v, depth + 1, share);
       if (!entry) goto fail;
     } else if (PyDict_CheckExact(ov) && PyDict_CheckExact(v)) {
-      PyObject* sub = merge_patch_impl(ov, v, depth + 1);
+      PyObject* sub = merge_patch_impl(ov, v, depth + 1, share);
       if (!sub) goto fail;
       if (PyDict_GET_SIZE(sub) == 0) {
         Py_DECREF(sub);
@@ -183,7 +194,7 @@ PyObject* merge_patch_impl(PyObject* old, PyObject* nw, int depth) {
       const int eq = equal_impl(ov, v, depth + 1);
       if (eq < 0) goto fail;
       if (eq == 1) continue;
-      entry = deepcopy_impl(v, depth + 1);
+      entry = patch_value(v, depth + 1, share);
       if (!entry) goto fail;
     }
     if (PyDict_SetItem(patch, k, entry) < 0) {
@@ -316,11 +327,161 @@ PyObject* cached_value(const char* p, size_t n) {
   return str;
 }
 
+// ------------------------------------------------------------------------ decode/encode plans
+//
+// A Plan names JSON paths -- object keys, "*" for any list element -- where the codec
+// acts instead of building or writing the value plainly:
+//
+//   skip   the decoder scans past the value and leaves its key out.  A child informer
+//          never reads a PyTorchJob's `spec` (the bulk of the object); skipping it at
+//          decode time saves building it only for the informer to drop it.
+//   memo   the decoder scans the value's bytes and, when the Memo holds an object that
+//          was decoded from -- or encoded to -- exactly those bytes, returns that object
+//          instead of building a new one; otherwise it builds and remembers it.  The
+//          encoder remembers the bytes of each value it writes at a memo path.
+//
+// Memo values are shared between trees, so they must never be mutated -- the informer
+// cache and the reconciler's status entries are read-only by contract already.  Byte
+// equality of the scanned span implies JSON equality, so a hit is exact; a span that
+// does not match just costs the scan.  A Cron's status write therefore comes back on
+// the watch with the reconciler's own history-entry dicts (same objects), which makes
+// the own-write check and the next merge patch compare them by identity.
+
+enum Action : uint8_t { kActNone = 0, kActSkip = 1, kActMemo = 2 };
+
+struct PlanNode {
+  std::vector<std::pair<std::string, int>> kids;
+  int any = -1;  // child for list elements ("*")
+  Action act = kActNone;
+};
+
+struct Plan {
+  std::vector<PlanNode> nodes;  // nodes[0]: the root
+
+  int child(int node, const char* k, size_t n) const {
+    if (node < 0) return -1;
+    for (const auto& kv : nodes[static_cast<size_t>(node)].kids)
+      if (kv.first.size() == n && std::memcmp(kv.first.data(), k, n) == 0) return kv.second;
+    return -1;
+  }
+  int element(int node) const { return node < 0 ? -1 : nodes[static_cast<size_t>(node)].any; }
+  Action act(int node) const { return node < 0 ? kActNone : nodes[static_cast<size_t>(node)].act; }
+
+  // path: a sequence of str; returns false (with a Python error) on bad input
+  bool add(PyObject* path, Action a) {
+    PyObject* seq = PySequence_Fast(path, "a plan path must be a sequence of str");
+    if (!seq) return false;
+    int node = 0;
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+    if (n == 0) {
+      Py_DECREF(seq);
+      PyErr_SetString(PyExc_ValueError, "empty plan path");
+      return false;
+    }
+    for (Py_ssize_t i = 0; i < n; ++i) {
+      PyObject* e = PySequence_Fast_GET_ITEM(seq, i);
+      Py_ssize_t len;
+      const char* k = PyUnicode_Check(e) ? PyUnicode_AsUTF8AndSize(e, &len) : nullptr;
+      if (!k) {
+        Py_DECREF(seq);
+        if (!PyErr_Occurred()) PyErr_SetString(PyExc_TypeError, "plan path elements must be str");
+        return false;
+      }
+      int next;
+      if (len == 1 && k[0] == '*') {
+        next = nodes[static_cast<size_t>(node)].any;
+        if (next < 0) {
+          next = static_cast<int>(nodes.size());
+          nodes.emplace_back();
+          nodes[static_cast<size_t>(node)].any = next;
+        }
+      } else {
+        next = child(node, k, static_cast<size_t>(len));
+        if (next < 0) {
+          next = static_cast<int>(nodes.size());
+          nodes.emplace_back();
+          nodes[static_cast<size_t>(node)].kids.emplace_back(std::string(k, static_cast<size_t>(len)), next);
+        }
+      }
+      node = next;
+    }
+    Py_DECREF(seq);
+    nodes[static_cast<size_t>(node)].act = a;
+    return true;
+  }
+};
+
+inline uint64_t span_hash(const char* p, size_t n) {
+  // 8 bytes per step (multiply / xor-shift mixing); the tail byte by byte
+  uint64_t h = 0x9E3779B97F4A7C15ULL ^ (n * 0xff51afd7ed558ccdULL);
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t w;
+    std::memcpy(&w, p + i, 8);
+    h ^= w * 0xc4ceb9fe1a85ec53ULL;
+    h = (h << 27) | (h >> 37);
+    h *= 0x9E3779B97F4A7C15ULL;
+  }
+  for (; i < n; ++i) {
+    h ^= static_cast<unsigned char>(p[i]);
+    h *= 1099511628211ULL;
+  }
+  h ^= h >> 33;
+  return h;
+}
+
+struct MemoSlot {
+  uint64_t hash = 0;
+  std::string bytes;
+  PyObject* obj = nullptr;  // strong ref
+};
+
+struct MemoTable {
+  std::vector<MemoSlot> slots;
+  size_t mask = 0;
+  uint64_t hits = 0, misses = 0, stores = 0;
+
+  explicit MemoTable(size_t n) {
+    size_t cap = 64;
+    while (cap < n) cap <<= 1;
+    slots.resize(cap);
+    mask = cap - 1;
+  }
+  ~MemoTable() { clear(); }
+  void clear() {
+    for (auto& sl : slots) {
+      Py_CLEAR(sl.obj);
+      sl.bytes.clear();
+      sl.bytes.shrink_to_fit();
+      sl.hash = 0;
+    }
+  }
+  PyObject* find(const char* p, size_t n, uint64_t h) {  // borrowed
+    MemoSlot& sl = slots[h & mask];
+    if (sl.obj != nullptr && sl.hash == h && sl.bytes.size() == n && std::memcmp(sl.bytes.data(), p, n) == 0) {
+      ++hits;
+      return sl.obj;
+    }
+    ++misses;
+    return nullptr;
+  }
+  void store(const char* p, size_t n, uint64_t h, PyObject* o) {
+    MemoSlot& sl = slots[h & mask];
+    Py_INCREF(o);
+    Py_XSETREF(sl.obj, o);
+    sl.hash = h;
+    sl.bytes.assign(p, n);
+    ++stores;
+  }
+};
+
 struct Decoder {
   const char* begin;
   const char* p;
   const char* end;
   std::vector<Py_UCS4> ubuf;
+  const Plan* plan = nullptr;
+  MemoTable* memo = nullptr;
 
   PyObject* fail(const char* msg) {
     if (!PyErr_Occurred()) {
@@ -532,11 +693,102 @@ struct Decoder {
     return PyLong_FromString(z, nullptr, 10);
   }
 
-  PyObject* value(int depth) {
+  // scan past one string (p just past its opening quote); no validation
+  bool skip_string() {
+    while (p < end) {
+      const char c = *p;
+      if (c == '\\') {
+        if (end - p < 2) break;
+        p += 2;
+        continue;
+      }
+      ++p;
+      if (c == '"') return true;
+    }
+    fail("Unterminated string");
+    return false;
+  }
+
+  // scan past one value (p at its first byte, whitespace skipped); structure only
+  bool skip_value() {
+    if (p >= end) {
+      fail("Expecting value");
+      return false;
+    }
+    const char c0 = *p;
+    if (c0 == '"') {
+      ++p;
+      return skip_string();
+    }
+    if (c0 == '{' || c0 == '[') {
+      int d = 0;
+      while (p < end) {
+        const char c = *p;
+        if (c == '"') {
+          ++p;
+          if (!skip_string()) return false;
+          continue;
+        }
+        ++p;
+        if (c == '{' || c == '[') {
+          if (++d > kMaxDepth) {
+            PyErr_SetString(PyExc_RecursionError, "JSON nested too deeply");
+            return false;
+          }
+        } else if (c == '}' || c == ']') {
+          if (--d == 0) return true;
+        }
+      }
+      fail("Unterminated container");
+      return false;
+    }
+    const char* s = p;
+    while (p < end && *p != ',' && *p != '}' && *p != ']' && *p != ' ' && *p != '\n' && *p != '\r' &&
+           *p != '\t')
+      ++p;
+    if (p == s) {
+      fail("Expecting value");
+      return false;
+    }
+    return true;
+  }
+
+  // a value at a memo path: reuse the object remembered for exactly these bytes
+  PyObject* memo_value(int depth) {
+    ws();
+    const char* s = p;
+    if (!skip_value()) return nullptr;
+    const size_t n = static_cast<size_t>(p - s);
+    const uint64_t h = span_hash(s, n);
+    PyObject* hit = memo->find(s, n, h);
+    if (hit != nullptr) {
+      Py_INCREF(hit);
+      return hit;
+    }
+    const char* after = p;
+    p = s;
+    PyObject* v = value(depth, -1);
+    if (!v) return nullptr;
+    if (p != after) {  // cannot happen for well-formed input: keep the parse, do not remember it
+      return v;
+    }
+    memo->store(s, n, h, v);
+    return v;
+  }
+
+  static inline bool key_bytes(PyObject* k, const char** d, size_t* n) {
+    if (!PyUnicode_IS_COMPACT_ASCII(k)) return false;
+    *d = static_cast<const char*>(PyUnicode_DATA(k));
+    *n = static_cast<size_t>(PyUnicode_GET_LENGTH(k));
+    return true;
+  }
+
+  PyObject* value(int depth, int node = -1) {
     if (depth > kMaxDepth) {
       PyErr_SetString(PyExc_RecursionError, "JSON nested too deeply");
       return nullptr;
     }
+    if (node >= 0 && memo != nullptr && plan->act(node) == kActMemo) return memo_value(depth);
     ws();
     if (p >= end) return fail("Expecting value");
     switch (*p) {
@@ -555,7 +807,23 @@ struct Decoder {
           ws();
           if (p >= end || *p != ':') { Py_DECREF(k); Py_DECREF(d); return fail("Expecting ':' delimiter"); }
           ++p;
-          PyObject* v = value(depth + 1);
+          int kid = -1;
+          if (node >= 0) {
+            const char* kd;
+            size_t kn;
+            if (key_bytes(k, &kd, &kn)) kid = plan->child(node, kd, kn);
+            if (kid >= 0 && plan->act(kid) == kActSkip) {
+              Py_DECREF(k);
+              ws();
+              if (!skip_value()) { Py_DECREF(d); return nullptr; }
+              ws();
+              if (p < end && *p == ',') { ++p; continue; }
+              if (p < end && *p == '}') { ++p; return acyclic(d); }
+              Py_DECREF(d);
+              return fail("Expecting ',' delimiter");
+            }
+          }
+          PyObject* v = value(depth + 1, kid);
           if (!v) { Py_DECREF(k); Py_DECREF(d); return nullptr; }
           const int rc = PyDict_SetItem(d, k, v);
           Py_DECREF(k);
@@ -573,8 +841,9 @@ struct Decoder {
         std::vector<PyObject*> items;
         ws();
         if (p < end && *p == ']') { ++p; return acyclic(PyList_New(0)); }
+        const int elem = node >= 0 ? plan->element(node) : -1;
         while (true) {
-          PyObject* v = value(depth + 1);
+          PyObject* v = value(depth + 1, elem);
           if (!v) {
             for (PyObject* o : items) Py_DECREF(o);
             return nullptr;
@@ -672,6 +941,13 @@ struct Encoder {
   // except those under a key in `volatile_keys` (they change on every write: never reused)
   PyObject* shared = nullptr;
   PyObject* volatile_keys = nullptr;
+  // Codec.dumpb: values written at memo paths are remembered (bytes -> object) afterwards
+  const Plan* plan = nullptr;
+  struct Rec {
+    size_t start, end;
+    PyObject* obj;  // borrowed: alive for the whole encode (the caller holds the tree)
+  };
+  std::vector<Rec> recs;
 
   bool str(PyObject* u) {
     Py_ssize_t n;
@@ -756,10 +1032,16 @@ struct Encoder {
     return false;
   }
 
-  bool value(PyObject* o, int depth) {
+  bool value(PyObject* o, int depth, int node = -1) {
     if (depth > kMaxDepth) {
       PyErr_SetString(PyExc_ValueError, "Circular reference detected");
       return false;
+    }
+    if (node >= 0 && plan->act(node) == kActMemo) {
+      const size_t start = out.size();
+      if (!value(o, depth, -1)) return false;
+      recs.push_back(Rec{start, out.size(), o});
+      return true;
     }
     if (o == Py_None) { out.append("null"); return true; }
     if (o == Py_True) { out.append("true"); return true; }
@@ -767,7 +1049,7 @@ struct Encoder {
     if (PyUnicode_Check(o)) return str(o);
     if (PyLong_Check(o)) return integer(o);
     if (PyFloat_Check(o)) return flt(PyFloat_AS_DOUBLE(o));
-    return container(o, depth);
+    return container(o, depth, node);
   }
 
   // A subtree shared by identity with one encoded before (a status write keeps the stored
@@ -806,7 +1088,7 @@ struct Encoder {
 
   static constexpr size_t kSharedMin = 64;
 
-  bool container(PyObject* o, int depth) {
+  bool container(PyObject* o, int depth, int node = -1) {
     if (PyDict_Check(o)) {
       out.push_back('{');
       Py_ssize_t pos = 0;
@@ -823,7 +1105,11 @@ struct Encoder {
           if (!(vol ? value(v, depth + 1) : cached(v, depth + 1))) return false;
           continue;
         }
-        if (!value(v, depth + 1)) return false;
+        int kid = -1;
+        if (node >= 0 && PyUnicode_IS_COMPACT_ASCII(k))
+          kid = plan->child(node, static_cast<const char*>(PyUnicode_DATA(k)),
+                            static_cast<size_t>(PyUnicode_GET_LENGTH(k)));
+        if (!value(v, depth + 1, kid)) return false;
       }
       out.push_back('}');
       return true;
@@ -832,10 +1118,11 @@ struct Encoder {
       PyObject* seq = o;
       const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
       PyObject** items = PySequence_Fast_ITEMS(seq);
+      const int elem = node >= 0 ? plan->element(node) : -1;
       out.push_back('[');
       for (Py_ssize_t i = 0; i < n; ++i) {
         if (i) out.push_back(',');
-        if (!value(items[i], depth + 1)) return false;
+        if (!value(items[i], depth + 1, elem)) return false;
       }
       out.push_back(']');
       return true;
@@ -890,11 +1177,13 @@ PyObject* py_json_equal(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
 }
 
 PyObject* py_merge_patch(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
-  if (nargs != 2) {
-    PyErr_SetString(PyExc_TypeError, "create_merge_patch(old, new)");
+  if (nargs != 2 && nargs != 3) {
+    PyErr_SetString(PyExc_TypeError, "create_merge_patch(old, new, share=False)");
     return nullptr;
   }
-  return merge_patch_impl(args[0], args[1], 0);
+  int share = 0;
+  if (nargs == 3 && (share = PyObject_IsTrue(args[2])) < 0) return nullptr;
+  return merge_patch_impl(args[0], args[1], 0, share != 0);
 }
 
 PyObject* py_set_gc_untrack(PyObject*, PyObject* arg) {
@@ -904,6 +1193,237 @@ PyObject* py_set_gc_untrack(PyObject*, PyObject* arg) {
   g_untrack = on != 0;
   Py_INCREF(prev);
   return prev;
+}
+
+// ---------------------------------------------------------------------------- Memo / Codec types
+
+struct MemoObject {
+  PyObject_HEAD
+  MemoTable* table;
+};
+
+void memo_dealloc(PyObject* self) {
+  delete reinterpret_cast<MemoObject*>(self)->table;
+  Py_TYPE(self)->tp_free(self);
+}
+
+PyObject* memo_new(PyTypeObject* type, PyObject* args, PyObject* kwds) {
+  static const char* kw[] = {"slots", nullptr};
+  Py_ssize_t n = 1 << 16;
+  if (!PyArg_ParseTupleAndKeywords(args, kwds, "|n", const_cast<char**>(kw), &n)) return nullptr;
+  if (n < 1 || n > (1 << 24)) {
+    PyErr_SetString(PyExc_ValueError, "slots must be in [1, 2**24]");
+    return nullptr;
+  }
+  PyObject* self = type->tp_alloc(type, 0);
+  if (!self) return nullptr;
+  reinterpret_cast<MemoObject*>(self)->table = new MemoTable(static_cast<size_t>(n));
+  return self;
+}
+
+PyObject* memo_stats(PyObject* self, PyObject*) {
+  MemoTable* t = reinterpret_cast<MemoObject*>(self)->table;
+  size_t used = 0;
+  for (const auto& sl : t->slots) used += sl.obj != nullptr;
+  return Py_BuildValue("{s:K,s:K,s:K,s:n,s:n}", "hits", static_cast<unsigned long long>(t->hits), "misses",
+                       static_cast<unsigned long long>(t->misses), "stores",
+                       static_cast<unsigned long long>(t->stores), "used", static_cast<Py_ssize_t>(used),
+                       "slots", static_cast<Py_ssize_t>(t->slots.size()));
+}
+
+PyObject* memo_clear(PyObject* self, PyObject*) {
+  reinterpret_cast<MemoObject*>(self)->table->clear();
+  Py_RETURN_NONE;
+}
+
+PyMethodDef memo_methods[] = {
+    {"stats", memo_stats, METH_NOARGS, "hits, misses, stores, used and total slots"},
+    {"clear", memo_clear, METH_NOARGS, "drop every remembered object"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyTypeObject MemoType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+struct CodecObject {
+  PyObject_HEAD
+  Plan* plan;
+  PyObject* memo;  // MemoObject or nullptr
+  vectorcallfunc vectorcall;
+};
+
+void codec_dealloc(PyObject* self) {
+  CodecObject* c = reinterpret_cast<CodecObject*>(self);
+  delete c->plan;
+  Py_XDECREF(c->memo);
+  Py_TYPE(self)->tp_free(self);
+}
+
+inline MemoTable* codec_memo(CodecObject* c) {
+  return c->memo != nullptr ? reinterpret_cast<MemoObject*>(c->memo)->table : nullptr;
+}
+
+bool buffer_of(PyObject* arg, const char** data, Py_ssize_t* n) {
+  if (PyBytes_Check(arg)) {
+    *data = PyBytes_AS_STRING(arg);
+    *n = PyBytes_GET_SIZE(arg);
+    return true;
+  }
+  if (PyByteArray_Check(arg)) {
+    *data = PyByteArray_AS_STRING(arg);
+    *n = PyByteArray_GET_SIZE(arg);
+    return true;
+  }
+  if (PyUnicode_Check(arg)) {
+    *data = PyUnicode_AsUTF8AndSize(arg, n);
+    return *data != nullptr;
+  }
+  PyErr_Format(PyExc_TypeError, "the JSON object must be str, bytes or bytearray, not %s", Py_TYPE(arg)->tp_name);
+  return false;
+}
+
+PyObject* codec_decode(CodecObject* c, PyObject* arg) {
+  const char* data;
+  Py_ssize_t n;
+  if (!buffer_of(arg, &data, &n)) return nullptr;
+  Decoder d{data, data, data + n, {}};
+  d.plan = c->plan;
+  d.memo = codec_memo(c);
+  PyObject* v = d.value(0, 0);
+  if (!v) return nullptr;
+  d.ws();
+  if (d.p != d.end) {
+    Py_DECREF(v);
+    return d.fail("Extra data");
+  }
+  return v;
+}
+
+PyObject* codec_new(PyTypeObject* type, PyObject* args, PyObject* kwds) {
+  static const char* kw[] = {"skip", "memo_paths", "memo", nullptr};
+  PyObject* skip = nullptr;
+  PyObject* memo_paths = nullptr;
+  PyObject* memo = nullptr;
+  if (!PyArg_ParseTupleAndKeywords(args, kwds, "|OOO", const_cast<char**>(kw), &skip, &memo_paths, &memo))
+    return nullptr;
+  if (memo == Py_None) memo = nullptr;
+  if (memo != nullptr && !PyObject_TypeCheck(memo, &MemoType)) {
+    PyErr_SetString(PyExc_TypeError, "memo must be a Memo");
+    return nullptr;
+  }
+  auto plan = new Plan();
+  plan->nodes.emplace_back();
+  auto add_all = [&](PyObject* paths, Action a) -> bool {
+    if (paths == nullptr || paths == Py_None) return true;
+    PyObject* seq = PySequence_Fast(paths, "paths must be a sequence of paths");
+    if (!seq) return false;
+    for (Py_ssize_t i = 0; i < PySequence_Fast_GET_SIZE(seq); ++i) {
+      if (!plan->add(PySequence_Fast_GET_ITEM(seq, i), a)) {
+        Py_DECREF(seq);
+        return false;
+      }
+    }
+    Py_DECREF(seq);
+    return true;
+  };
+  if (!add_all(skip, kActSkip) || !add_all(memo_paths, kActMemo)) {
+    delete plan;
+    return nullptr;
+  }
+  PyObject* self = type->tp_alloc(type, 0);
+  if (!self) {
+    delete plan;
+    return nullptr;
+  }
+  CodecObject* c = reinterpret_cast<CodecObject*>(self);
+  c->plan = plan;
+  Py_XINCREF(memo);
+  c->memo = memo;
+  c->vectorcall = nullptr;  // set by the type's init below
+  return self;
+}
+
+// codec(line) -> (type, object): one watch event ({"type": ..., "object": {...}})
+PyObject* codec_vectorcall(PyObject* self, PyObject* const* args, size_t nargsf, PyObject* kwnames) {
+  if (PyVectorcall_NARGS(nargsf) != 1 || (kwnames && PyTuple_GET_SIZE(kwnames))) {
+    PyErr_SetString(PyExc_TypeError, "codec(line) takes exactly one argument");
+    return nullptr;
+  }
+  PyObject* ev = codec_decode(reinterpret_cast<CodecObject*>(self), args[0]);
+  if (!ev) return nullptr;
+  PyObject* type = nullptr;
+  PyObject* obj = nullptr;
+  if (PyDict_CheckExact(ev)) {
+    type = PyDict_GetItemString(ev, "type");   // borrowed
+    obj = PyDict_GetItemString(ev, "object");  // borrowed
+  }
+  PyObject* t = (type != nullptr && PyObject_IsTrue(type) == 1) ? type : nullptr;
+  PyObject* o = (obj != nullptr && PyObject_IsTrue(obj) == 1) ? obj : nullptr;
+  PyObject* out = PyTuple_New(2);
+  if (!out) {
+    Py_DECREF(ev);
+    return nullptr;
+  }
+  if (t) {
+    Py_INCREF(t);
+  } else {
+    t = PyUnicode_FromStringAndSize("", 0);
+  }
+  if (o) {
+    Py_INCREF(o);
+  } else {
+    o = PyDict_New();
+  }
+  PyTuple_SET_ITEM(out, 0, t);
+  PyTuple_SET_ITEM(out, 1, o);
+  Py_DECREF(ev);
+  if (!t || !o) {
+    Py_DECREF(out);
+    return nullptr;
+  }
+  return out;
+}
+
+PyObject* codec_call(PyObject* self, PyObject* args, PyObject* kwds) {
+  if (kwds && PyDict_GET_SIZE(kwds)) {
+    PyErr_SetString(PyExc_TypeError, "codec(line) takes no keyword arguments");
+    return nullptr;
+  }
+  return codec_vectorcall(self, &PyTuple_GET_ITEM(args, 0), static_cast<size_t>(PyTuple_GET_SIZE(args)), nullptr);
+}
+
+PyObject* codec_loads(PyObject* self, PyObject* arg) { return codec_decode(reinterpret_cast<CodecObject*>(self), arg); }
+
+PyObject* codec_dumpb(PyObject* self, PyObject* o) {
+  CodecObject* c = reinterpret_cast<CodecObject*>(self);
+  Encoder e;
+  e.plan = c->plan;
+  e.out.reserve(1024);
+  if (!e.value(o, 0, 0)) return nullptr;
+  MemoTable* m = codec_memo(c);
+  if (m != nullptr) {
+    for (const auto& r : e.recs) {
+      const char* p = e.out.data() + r.start;
+      const size_t n = r.end - r.start;
+      m->store(p, n, span_hash(p, n), r.obj);
+    }
+  }
+  return PyBytes_FromStringAndSize(e.out.data(), static_cast<Py_ssize_t>(e.out.size()));
+}
+
+PyMethodDef codec_methods[] = {
+    {"loads", codec_loads, METH_O, "decode a JSON document with this codec's plan"},
+    {"dumpb", codec_dumpb, METH_O, "encode compactly; remember the values written at memo paths"},
+    {nullptr, nullptr, 0, nullptr}};
+
+PyMemberDef codec_members[] = {
+    {"memo", T_OBJECT, offsetof(CodecObject, memo), READONLY, "the shared Memo (or None)"},
+    {nullptr, 0, 0, 0, nullptr}};
+
+PyTypeObject CodecType = {PyVarObject_HEAD_INIT(nullptr, 0)};
+
+PyObject* codec_new_vc(PyTypeObject* type, PyObject* args, PyObject* kwds) {
+  PyObject* self = codec_new(type, args, kwds);
+  if (self) reinterpret_cast<CodecObject*>(self)->vectorcall = codec_vectorcall;
+  return self;
 }
 
 PyMethodDef methods[] = {
@@ -927,4 +1447,35 @@ PyModuleDef moddef = {PyModuleDef_HEAD_INIT, "_fastjson", "Native JSON-tree help
 
 }  // namespace
 
-PyMODINIT_FUNC PyInit__fastjson(void) { return PyModule_Create(&moddef); }
+PyMODINIT_FUNC PyInit__fastjson(void) {
+  MemoType.tp_name = "_fastjson.Memo";
+  MemoType.tp_basicsize = sizeof(MemoObject);
+  MemoType.tp_flags = Py_TPFLAGS_DEFAULT;
+  MemoType.tp_doc = "Memo(slots=65536): bytes -> decoded object table shared by Codecs";
+  MemoType.tp_new = memo_new;
+  MemoType.tp_dealloc = memo_dealloc;
+  MemoType.tp_methods = memo_methods;
+  CodecType.tp_name = "_fastjson.Codec";
+  CodecType.tp_basicsize = sizeof(CodecObject);
+  CodecType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_VECTORCALL;
+  CodecType.tp_doc =
+      "Codec(skip=(), memo_paths=(), memo=None): JSON decode/encode with skipped and memoised paths; "
+      "calling it decodes one watch event line into (type, object)";
+  CodecType.tp_new = codec_new_vc;
+  CodecType.tp_dealloc = codec_dealloc;
+  CodecType.tp_methods = codec_methods;
+  CodecType.tp_members = codec_members;
+  CodecType.tp_call = codec_call;
+  CodecType.tp_vectorcall_offset = offsetof(CodecObject, vectorcall);
+  if (PyType_Ready(&MemoType) < 0 || PyType_Ready(&CodecType) < 0) return nullptr;
+  PyObject* m = PyModule_Create(&moddef);
+  if (!m) return nullptr;
+  Py_INCREF(&MemoType);
+  Py_INCREF(&CodecType);
+  if (PyModule_AddObject(m, "Memo", reinterpret_cast<PyObject*>(&MemoType)) < 0 ||
+      PyModule_AddObject(m, "Codec", reinterpret_cast<PyObject*>(&CodecType)) < 0) {
+    Py_DECREF(m);
+    return nullptr;
+  }
+  return m;
+}

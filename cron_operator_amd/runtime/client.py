@@ -86,6 +86,7 @@ def _throttle_log():
 
 
 DISCARD = "_discardResponse"   # the caller ignores the response body
+DECODE = "_decode"             # a jsonutil.Codec for the response body (e.g. one that skips spec)
 ACCEPT = "_accept"             # Accept header override (server-side printing)
 TABLE_ACCEPT = "application/json;as=Table;v=v1;g=meta.k8s.io,application/json"
 
@@ -98,7 +99,9 @@ class Transport:
         raise NotImplementedError
 
     async def watch(self, gvr: GroupVersionResource, namespace: str = "",
-                    params: Optional[Dict[str, Any]] = None) -> "WatchStream":
+                    params: Optional[Dict[str, Any]] = None, decoder: Any = None) -> "WatchStream":
+        """``decoder``: turns one event line into ``(type, object)`` (a ``jsonutil.Codec``);
+        transports that do not decode bytes ignore it."""
         raise NotImplementedError
 
     async def discover(self, group_version: GroupVersion) -> List[Dict[str, Any]]:
@@ -168,6 +171,8 @@ class InMemoryTransport(Transport):
                 else:
                     objs = s.list(gvr, namespace or None, params.get("labelSelector"))["items"]
                 return to_table(printer_columns_of(s.resource(gvr)), objs, s.clock.now_ns())
+        if body.__class__ is bytes:  # pre-encoded by the caller (Codec.dumpb)
+            body = jsonutil.loads(body)
         out = self._apply(verb, gvr, namespace, name, subresource, body, params)
         faults = self.server.faults
         if faults.faults:
@@ -196,7 +201,7 @@ class InMemoryTransport(Transport):
         raise ValueError(f"unknown verb {verb}")
 
     async def watch(self, gvr: GroupVersionResource, namespace: str = "",
-                    params: Optional[Dict[str, Any]] = None) -> WatchStream:
+                    params: Optional[Dict[str, Any]] = None, decoder: Any = None) -> WatchStream:
         params = params or {}
         await self._gate("watch", gvr.resource, "", "")
         w = self.server.watch(gvr, namespace or None, str(params.get("resourceVersion") or ""),
@@ -417,11 +422,17 @@ class Client:
         return out
 
     async def create(self, target: GVRorGVK, obj: Dict[str, Any], namespace: Optional[str] = None,
-                     dry_run: bool = False) -> Dict[str, Any]:
+                     dry_run: bool = False, decoder: Any = None) -> Dict[str, Any]:
+        """``decoder``: a ``jsonutil.Codec`` for the returned object, e.g. one that skips the
+        ``spec`` the caller never reads (HTTP transports; others return the whole object)."""
         ns = namespace if namespace is not None else (obj.get("metadata") or {}).get("namespace", "")
         gvr = self._gvr_now(target) or await self._gvr(target)
-        return await self._do("create", gvr, ns, body=obj,
-                              params={"dryRun": "All"} if dry_run else None)
+        params: Optional[Dict[str, Any]] = None
+        if dry_run or decoder is not None:
+            params = {"dryRun": "All"} if dry_run else {}
+            if decoder is not None:
+                params[DECODE] = decoder
+        return await self._do("create", gvr, ns, body=obj, params=params)
 
     async def update(self, target: GVRorGVK, obj: Dict[str, Any], subresource: str = "") -> Dict[str, Any]:
         m = obj.get("metadata") or {}
@@ -432,7 +443,8 @@ class Client:
     async def patch(self, target: GVRorGVK, namespace: str, name: str, patch: Any, patch_type: str = MERGE,
                     subresource: str = "", discard_response: bool = False) -> Dict[str, Any]:
         """``discard_response``: the caller does not read the result, so an HTTP transport
-        need not decode the returned object (it is still received, and errors still raise)."""
+        need not decode the returned object (it is still received, and errors still raise).
+        ``patch`` may be bytes already encoded by the caller (``Codec.dumpb``)."""
         params: Dict[str, Any] = {"patchType": patch_type}
         if discard_response:
             params[DISCARD] = True
@@ -458,7 +470,8 @@ class Client:
 
     async def watch(self, target: GVRorGVK, namespace: str = "", resource_version: str = "",
                     label_selector: Optional[str] = None, field_selector: Optional[str] = None,
-                    allow_bookmarks: bool = True, timeout_seconds: Optional[int] = None) -> WatchStream:
+                    allow_bookmarks: bool = True, timeout_seconds: Optional[int] = None,
+                    decoder: Any = None) -> WatchStream:
         gvr = self._gvr_now(target) or await self._gvr(target)
         await self._throttle("watch", gvr, namespace, "", "")
         self.requests += 1
@@ -472,7 +485,8 @@ class Client:
         if timeout_seconds:
             params["timeoutSeconds"] = timeout_seconds
         try:
-            w = await self.transport.watch(gvr, namespace, params)
+            w = await self.transport.watch(gvr, namespace, params, decoder) if decoder is not None \
+                else await self.transport.watch(gvr, namespace, params)
         except errors.ApiError as e:
             metrics.REST_REQUESTS.labels(str(e.code), self.host, "GET").inc()
             raise

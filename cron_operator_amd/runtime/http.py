@@ -21,7 +21,7 @@ from ..api import errors
 from ..api.meta import GroupVersion, GroupVersionResource
 from ..utils import jsonutil
 from . import metrics
-from .client import ACCEPT, DISCARD, PATCH_CONTENT_TYPES, Transport, WatchStream
+from .client import ACCEPT, DECODE, DISCARD, PATCH_CONTENT_TYPES, Transport, WatchStream
 from .fasthttp import ConnectionFailed, HttpPool, HttpStatusError, Stream, encode_query
 from .kubeconfig import RestConfig
 
@@ -67,9 +67,10 @@ def _clean(params: Optional[Dict[str, Any]]) -> Dict[str, str]:
 
 
 class _HttpWatch(WatchStream):
-    def __init__(self, resp: aiohttp.ClientResponse):
+    def __init__(self, resp: aiohttp.ClientResponse, decoder: Any = None):
         self._resp = resp
         self._done = False
+        self._decode = decoder or _decode_event
 
     async def __anext__(self) -> Tuple[str, Dict[str, Any]]:
         if self._done:
@@ -86,8 +87,7 @@ class _HttpWatch(WatchStream):
             line = line.strip()
             if not line:
                 continue
-            ev = jsonutil.loads(line)
-            return ev.get("type", ""), ev.get("object") or {}
+            return self._decode(line)
 
     def stop(self) -> None:
         if not self._done:
@@ -235,7 +235,7 @@ class HttpTransport(Transport):
         path = resource_path(gvr, namespace, name if verb not in ("list", "create", "deletecollection") else "",
                              subresource)
         if self.fast:
-            data = jsonutil.dumpb(body) if body is not None else None
+            data = (body if body.__class__ is bytes else jsonutil.dumpb(body)) if body is not None else None
             ctype = PATCH_CONTENT_TYPES[params.get("patchType", "merge")] if verb == "patch" else "application/json"
             target = path + encode_query(_clean(params))
             attempt = 0
@@ -263,12 +263,15 @@ class HttpTransport(Transport):
                 raise errors.ApiError.from_status(status, err_body)
             if params.get(DISCARD):
                 return None
-            return jsonutil.loads(raw) if raw else None
+            if not raw:
+                return None
+            dec = params.get(DECODE)
+            return dec.loads(raw) if dec is not None else jsonutil.loads(raw)
         url = self.config.host + path
         headers = {"Accept": params.get(ACCEPT) or "application/json"}
         data = None
         if body is not None:
-            data = jsonutil.dumpb(body)
+            data = body if body.__class__ is bytes else jsonutil.dumpb(body)
             headers["Content-Type"] = PATCH_CONTENT_TYPES[params.get("patchType", "merge")] if verb == "patch" \
                 else "application/json"
         timeout = aiohttp.ClientTimeout(total=self._timeout)
@@ -283,7 +286,7 @@ class HttpTransport(Transport):
         return jsonutil.loads(raw) if raw else None
 
     async def watch(self, gvr: GroupVersionResource, namespace: str = "",
-                    params: Optional[Dict[str, Any]] = None) -> WatchStream:
+                    params: Optional[Dict[str, Any]] = None, decoder: Any = None) -> WatchStream:
         if self.config.exec_provider is not None and self.config.exec_stale():
             await self._fresh_exec()
         p = _clean(params)
@@ -291,7 +294,7 @@ class HttpTransport(Transport):
         if self.fast:
             try:
                 stream = await self._fast_pool().open_stream(resource_path(gvr, namespace) + encode_query(p),
-                                                             _decode_event)
+                                                             decoder or _decode_event)
             except HttpStatusError as e:
                 if e.status == 401:
                     self._unauthorized()
@@ -310,7 +313,7 @@ class HttpTransport(Transport):
                 await self._raise(resp)
             finally:
                 resp.release()
-        return _HttpWatch(resp)
+        return _HttpWatch(resp, decoder)
 
     async def discover(self, group_version: GroupVersion) -> List[Dict[str, Any]]:
         if self.config.exec_provider is not None and self.config.exec_stale():

@@ -108,8 +108,13 @@ class Informer:
                  field_selector: Optional[str] = None, indexers: Optional[Dict[str, IndexFunc]] = None,
                  page_size: int = 500, name: str = "", resync_period: float = 0.0,
                  clock: Optional[Clock] = None, transform: Optional[Transform] = None,
-                 min_watch_timeout: float = MIN_WATCH_TIMEOUT, watch_idle_timeout: float = WATCH_IDLE_TIMEOUT):
+                 min_watch_timeout: float = MIN_WATCH_TIMEOUT, watch_idle_timeout: float = WATCH_IDLE_TIMEOUT,
+                 decoder: Any = None):
         self.client = client
+        # watch-event decoder for byte transports (a jsonutil.Codec): it may skip subtrees no
+        # consumer reads and reuse memoised ones; None decodes plainly
+        self.decoder = decoder
+        self._watch_kw: Dict[str, Any] = {"decoder": decoder} if decoder is not None else {}
         # watch liveness: every WATCH asks the server to end it after a random
         # [min, 2*min) seconds (client-go reflector), and a watch silent for
         # ``watch_idle_timeout`` seconds -- no event and no bookmark -- is dropped and
@@ -384,7 +389,7 @@ class Informer:
                     if self.min_watch_timeout > 0 else None
                 self._watch = await self.client.watch(self.target, self.namespace, self.last_rv,
                                                       self.label_selector, self.field_selector,
-                                                      timeout_seconds=timeout_s)
+                                                      timeout_seconds=timeout_s, **self._watch_kw)
                 self._arm_watchdog(timeout_s)
                 loop = asyncio.get_running_loop()
                 w = self._watch
@@ -516,9 +521,9 @@ class Cache:
 
     async def get_informer(self, target: Any, label_selector: Optional[str] = None,
                            indexers: Optional[Dict[str, IndexFunc]] = None,
-                           transform: Optional[Transform] = None) -> Informer:
-        """The shared informer for ``(target, namespace, selector)``.  ``transform`` applies
-        when this call creates it (like ``cache.Options.ByObject[...].Transform``)."""
+                           transform: Optional[Transform] = None, decoder: Any = None) -> Informer:
+        """The shared informer for ``(target, namespace, selector)``.  ``transform`` and
+        ``decoder`` apply when this call creates it (like ``cache.Options.ByObject[...].Transform``)."""
         gvr = await self._resolve(target)
         key = (gvr, self.namespace, label_selector)
         inf = self._informers.get(key)
@@ -526,7 +531,8 @@ class Cache:
             inf = Informer(self.client, gvr, self.namespace, label_selector, indexers=indexers,
                            name=f"{gvr.resource}.{gvr.group}" if gvr.group else gvr.resource,
                            resync_period=self.resync_period, clock=self.clock, transform=transform,
-                           min_watch_timeout=self.min_watch_timeout, watch_idle_timeout=self.watch_idle_timeout)
+                           min_watch_timeout=self.min_watch_timeout, watch_idle_timeout=self.watch_idle_timeout,
+                           decoder=decoder)
             self._informers[key] = inf
             if self._started:
                 inf.start()

@@ -19,6 +19,7 @@ cancellation reaches every goroutine below it (``cmd/operator/start.go:205-209``
 from __future__ import annotations
 
 import asyncio
+import functools
 from typing import Iterable, Optional
 
 
@@ -30,12 +31,33 @@ def consume(tasks: Iterable[Optional["asyncio.Future"]]) -> None:
             t.exception()
 
 
+def _wake(waiter: "asyncio.Future", _t: "asyncio.Future") -> None:
+    if not waiter.done():
+        waiter.set_result(None)
+
+
+async def wait_one(t: "asyncio.Future") -> None:
+    """Wait until ``t`` has finished, whatever its outcome (``asyncio.wait`` for one task,
+    minus its sets and counters: this runs once per reconcile that GCs a child).  The caller
+    awaits a private future, so cancelling the caller cancels only that future."""
+    if t.done():
+        return
+    waiter = t.get_loop().create_future()
+    cb = functools.partial(_wake, waiter)
+    t.add_done_callback(cb)
+    try:
+        await waiter
+    finally:
+        t.remove_done_callback(cb)
+
+
 async def wait_all(tasks: Iterable[Optional["asyncio.Future"]]) -> None:
     """Wait until every task has finished, whatever its outcome.  If the caller is
     cancelled meanwhile, ``CancelledError`` propagates and the tasks keep running."""
     live = [t for t in tasks if t is not None]
-    if live:
-        await asyncio.wait(live)
+    for t in live:
+        if not t.done():
+            await wait_one(t)
     consume(live)
 
 

@@ -50,22 +50,25 @@ def py_json_equal(a: Any, b: Any) -> bool:
     return a == b
 
 
-def py_create_merge_patch(old: Any, new: Any) -> Any:
-    """Minimal RFC 7386 patch turning ``old`` into ``new`` (objects only recurse)."""
+def py_create_merge_patch(old: Any, new: Any, share: bool = False) -> Any:
+    """Minimal RFC 7386 patch turning ``old`` into ``new`` (objects only recurse).
+    ``share=True``: the patch references ``new``'s subtrees instead of copies (for a patch
+    that is only serialised; ``new`` must not change while it lives)."""
+    cp = (lambda x: x) if share else py_deepcopy
     if type(old) is not dict or type(new) is not dict:
-        return py_deepcopy(new)
+        return cp(new)
     patch = {}
     for k, v in new.items():
         if k not in old:
-            patch[k] = py_deepcopy(v)
+            patch[k] = cp(v)
         else:
             ov = old[k]
             if type(ov) is dict and type(v) is dict:
-                sub = py_create_merge_patch(ov, v)
+                sub = py_create_merge_patch(ov, v, share)
                 if sub:
                     patch[k] = sub
             elif not py_json_equal(ov, v):
-                patch[k] = py_deepcopy(v)
+                patch[k] = cp(v)
     for k in old:
         if k not in new:
             patch[k] = None
@@ -188,14 +191,70 @@ def dumpb_shared(obj: Any, cache: Dict[int, Any], volatile_keys: Any = ()) -> by
     return dumpb(obj)
 
 
+class PyMemo:
+    """Python twin of the native ``Memo`` (no reuse: every value is built afresh)."""
+
+    def __init__(self, slots: int = 1 << 16):
+        self.slots = slots
+
+    def stats(self) -> Dict[str, int]:
+        return {"hits": 0, "misses": 0, "stores": 0, "used": 0, "slots": self.slots}
+
+    def clear(self) -> None:
+        pass
+
+
+def _drop(v: Any, path: Any) -> None:
+    if not path:
+        return
+    head, rest = path[0], path[1:]
+    if head == "*":
+        if type(v) is list:
+            for x in v:
+                _drop(x, rest)
+        return
+    if type(v) is not dict:
+        return
+    if not rest:
+        v.pop(head, None)
+    elif head in v:
+        _drop(v[head], rest)
+
+
+class PyCodec:
+    """Python twin of the native ``Codec(skip, memo_paths, memo)``: ``loads`` decodes and
+    removes the skipped paths ("*" = any list element); memo paths change nothing but
+    speed, so they are ignored here.  Calling it decodes one watch event line into
+    ``(type, object)``."""
+
+    def __init__(self, skip: Any = (), memo_paths: Any = (), memo: Any = None):
+        self.skip = [tuple(p) for p in skip or ()]
+        self.memo = memo
+
+    def loads(self, data: Any) -> Any:
+        v = loads(data)
+        for path in self.skip:
+            _drop(v, path)
+        return v
+
+    def __call__(self, line: Any) -> Any:
+        ev = self.loads(line)
+        return ev.get("type", "") or "", ev.get("object") or {}
+
+    def dumpb(self, tree: Any) -> bytes:
+        return dumpb(tree)
+
+
 deepcopy = py_deepcopy
 json_equal = py_json_equal
 create_merge_patch = py_create_merge_patch
+Codec: Any = PyCodec
+Memo: Any = PyMemo
 NATIVE = False
 
 
 def _try_native() -> None:
-    global deepcopy, json_equal, create_merge_patch, loads, dumps, dumpb, dumpb_shared, NATIVE
+    global deepcopy, json_equal, create_merge_patch, loads, dumps, dumpb, dumpb_shared, Codec, Memo, NATIVE
     import os
 
     if os.environ.get("CRON_OPERATOR_FASTJSON", "auto").lower() == "python":
@@ -215,6 +274,8 @@ def _try_native() -> None:
     dumps = mod.dumps
     dumpb = mod.dumpb
     dumpb_shared = mod.dumpb_shared
+    Codec = mod.Codec
+    Memo = mod.Memo
     NATIVE = True
 
 

@@ -33,6 +33,7 @@ class Sampler:
         self.samples = 0
         self.cpu_s = 0.0
         self._signal = signal
+        self.line_counts: "collections.Counter[str]" = collections.Counter()
 
     def _on(self, signum, frame) -> None:
         self.samples += 1
@@ -43,6 +44,7 @@ class Sampler:
             key = f"{co.co_filename.replace(ROOT + '/', '')}:{co.co_firstlineno}({co.co_name})"
             if first:
                 self.self_counts[key] += 1
+                self.line_counts[f"{key} line {frame.f_lineno}"] += 1
                 first = False
             if key not in seen:
                 seen.add(key)
@@ -66,6 +68,9 @@ class Sampler:
                f"{self.interval * 1e3:.1f} ms); a C function's time is charged to its Python caller\n",
                "\n## by self samples\n"]
         for k, c in self.self_counts.most_common(top):
+            out.append(f"{100.0 * c / n:6.2f}%  {k}\n")
+        out.append("\n## by self samples, per source line (the line executing when sampled)\n")
+        for k, c in self.line_counts.most_common(top):
             out.append(f"{100.0 * c / n:6.2f}%  {k}\n")
         out.append("\n## by inclusive samples\n")
         for k, c in self.incl_counts.most_common(top):

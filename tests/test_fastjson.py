@@ -191,3 +191,85 @@ def test_decoded_and_copied_trees_are_exempt_from_cyclic_gc():
         assert prev is True and gc.is_tracked(fj.loads(b'{"a":[1]}')["a"])
     finally:
         fj.set_gc_untrack(prev)
+
+
+# ------------------------------------------------------------------ plan codecs (skip / memo paths)
+
+from cron_operator_amd.utils import jsonutil  # noqa: E402
+
+doc_trees = st.dictionaries(st.sampled_from(["spec", "status", "metadata", "x", "items"]),
+                            json_values, max_size=5)
+
+
+@settings(max_examples=300, deadline=None)
+@given(doc_trees, st.lists(st.lists(st.sampled_from(["spec", "status", "metadata", "x", "items", "*"]),
+                                    min_size=1, max_size=3), max_size=3))
+def test_codec_skip_matches_python_twin(doc, skips):
+    """Decoding with skipped paths == json.loads followed by deleting those paths (the twin)."""
+    raw = json.dumps(doc)
+    native = m.Codec(skip=skips)
+    twin = jsonutil.PyCodec(skip=skips)
+    assert repr(native.loads(raw)) == repr(twin.loads(raw))
+    event = json.dumps({"type": "MODIFIED", "object": doc})
+    prefixed = [["object"] + p for p in skips]
+    assert repr(m.Codec(skip=prefixed)(event)) == repr(jsonutil.PyCodec(skip=prefixed)(event))
+
+
+@settings(max_examples=200, deadline=None)
+@given(doc_trees, doc_trees)
+def test_codec_memo_is_exact(a, b):
+    """Memoised paths give the same value as a plain decode -- only identity differs."""
+    memo = m.Memo(64)
+    c = m.Codec(memo_paths=[("spec",), ("status", "*"), ("items", "*")], memo=memo)
+    for doc in (a, b, a, b):
+        raw = json.dumps(doc)
+        assert repr(c.loads(raw)) == repr(json.loads(raw))
+
+
+def test_codec_memo_reuses_objects_across_documents_and_from_the_encoder():
+    memo = m.Memo()
+    enc = m.Codec(memo_paths=[("status", "history", "*")], memo=memo)
+    dec = m.Codec(memo_paths=[("object", "spec"), ("object", "status", "history", "*")], memo=memo)
+    entries = [{"uid": f"u{i}", "object": {"apiGroup": "kubeflow.org/v1", "kind": "PyTorchJob", "name": f"j{i}"},
+                "status": "Succeeded", "created": "2026-01-01T12:00:00Z"} for i in range(3)]
+    patch = {"status": {"history": entries}}
+    body = enc.dumpb(patch)
+    assert body == json.dumps(patch, separators=(",", ":"), ensure_ascii=False).encode()
+    obj = {"metadata": {"name": "c", "resourceVersion": "7"}, "spec": {"schedule": "* * * * *"},
+           "status": {"history": entries, "lastScheduleTime": "2026-01-01T12:01:00Z"}}
+    t, o = dec(json.dumps({"type": "MODIFIED", "object": obj}, separators=(",", ":")).encode())
+    assert t == "MODIFIED" and o == obj
+    assert all(x is y for x, y in zip(o["status"]["history"], entries))  # the encoder's own dicts
+    _, o2 = dec(json.dumps({"type": "MODIFIED", "object": obj}, separators=(",", ":")).encode())
+    assert o2["spec"] is o["spec"] and o2["metadata"] is not o["metadata"]
+    st_ = memo.stats()
+    assert st_["hits"] >= 7 and st_["stores"] >= 4
+    memo.clear()
+    assert memo.stats()["used"] == 0
+
+
+def test_codec_event_shape_and_errors():
+    c = m.Codec(skip=[("object", "spec")])
+    assert c(b'{"type":"ADDED","object":{"spec":{"big":[1,2,3]},"metadata":{"name":"a"}}}') == \
+        ("ADDED", {"metadata": {"name": "a"}})
+    assert c(b'{"type":"BOOKMARK"}') == ("BOOKMARK", {})
+    assert c(b'{"object":{"x":1}}') == ("", {"x": 1})
+    for bad in (b'{"type":"A","object":{"spec":{"a":[1,2}}', b'{"type":"A","object":{"spec":"open}}', b'{',
+                b'{"type":"A","object":{"spec":{"a":1}}}x', b'{"type":"A","object":{"spec":]}}'):
+        with pytest.raises(ValueError):
+            c(bad)
+    with pytest.raises(TypeError):
+        m.Codec(skip=[("a", 1)])
+    with pytest.raises(ValueError):
+        m.Codec(skip=[()])
+    with pytest.raises(TypeError):
+        m.Codec(memo_paths=[("a",)], memo=object())
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.dictionaries(st.text(max_size=6), json_values, max_size=5),
+       st.dictionaries(st.text(max_size=6), json_values, max_size=5))
+def test_merge_patch_share_equals_copy(old, new):
+    shared = m.create_merge_patch(old, new, True)
+    assert shared == m.create_merge_patch(old, new) == jsonutil.py_create_merge_patch(old, new)
+    assert jsonutil.py_create_merge_patch(old, new, True) == shared

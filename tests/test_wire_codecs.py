@@ -1,0 +1,106 @@
+"""Plan-driven watch decoding over real HTTP (``ReconcilerOptions.wire_codecs``).
+
+The operator talks to the apiserver as the reference does -- REST + watch streams
+(``/root/reference/internal/controller/cron_controller.go:70-77`` watches Crons and owned
+jobs; ``:107-120`` writes status with a merge patch).  Here the Cron informer decodes its
+watch through the same memo the status write was encoded with, so the echo of our own
+write carries the reconciler's own history-entry objects, and the child informers never
+build the job ``spec`` they drop anyway.
+"""
+from __future__ import annotations
+
+import asyncio
+
+from cron_operator_amd.api.meta import GroupVersionResource
+from cron_operator_amd.api.v1alpha1 import CRON_GVR, LABEL_CRON_NAME, new_cron
+from cron_operator_amd.controller.reconciler import ReconcilerOptions
+from cron_operator_amd.controller.setup import setup_with_manager
+from cron_operator_amd.runtime.manager import Manager, ManagerOptions
+from cron_operator_amd.testing.env import TestEnv
+from cron_operator_amd.trainingop.operator import finished_status
+from cron_operator_amd.utils import jsonutil
+from cron_operator_amd.utils.gotime import NANOS, UTC, GoTime
+
+PT = GroupVersionResource("kubeflow.org", "v1", "pytorchjobs")
+NS = "default"
+PT_TMPL = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+           "spec": {"pytorchReplicaSpecs": {"Master": {"replicas": 1, "template": {"spec": {"containers": [
+               {"name": "pytorch", "image": "rocm/pytorch:latest"}]}}}}}}
+
+
+async def _until(pred, what: str, timeout: float = 10.0) -> None:
+    loop = asyncio.get_running_loop()
+    end = loop.time() + timeout
+    while loop.time() < end:
+        if pred():
+            return
+        await asyncio.sleep(0.01)
+    raise AssertionError(f"timed out waiting for {what}")
+
+
+async def _run(opts: ReconcilerOptions):
+    from cron_operator_amd.apiserver.http import APIServerApp
+    from cron_operator_amd.runtime.client import Client
+    from cron_operator_amd.runtime.http import HttpTransport
+    from cron_operator_amd.runtime.kubeconfig import RestConfig
+
+    env = TestEnv()
+    app = APIServerApp(env.server)
+    port = await app.start("127.0.0.1", 0)
+    client = Client(HttpTransport(RestConfig(host=f"http://127.0.0.1:{port}")), qps=-1)
+    mgr = Manager(client, ManagerOptions(clock=env.clock, health_probe_bind_address="0", metrics_bind_address="0"))
+    ctrl, rec = await setup_with_manager(mgr, opts)
+    task = asyncio.get_running_loop().create_task(mgr.start())
+    try:
+        await asyncio.wait_for(mgr.started.wait(), 20)
+        await env.create_cron(new_cron("c", NS, "*/1 * * * *", PT_TMPL, history_limit=2))
+        seen: set = set()
+        for tick in range(1, 5):
+            env.clock.advance(60)
+
+            def new_jobs():
+                return {o["metadata"]["name"] for o in env.server.list(PT, NS)["items"]} - seen
+
+            await _until(lambda: new_jobs(), f"job of tick {tick}")
+            job = sorted(new_jobs())[-1]
+            seen.add(job)
+            ts = GoTime(env.clock.now_ns() // NANOS, 0, UTC).rfc3339()
+            env.server.patch(PT, NS, job, {"status": finished_status("PyTorchJob", job, ts, True)}, "merge",
+                             "status")
+            want = min(tick, 2)
+            await _until(lambda: len((rec.cron_informer.get(NS, "c", copy=False) or {}).get("status", {})
+                                     .get("history") or []) == want and ctrl.queue.idle(), f"history after {tick}")
+        cached = rec.cron_informer.get(NS, "c", copy=False)
+        stored = env.server.get(CRON_GVR, NS, "c")
+        child_inf = next(iter(rec.child_informers.values()))
+        children = child_inf.list(NS, copy=False)
+        return rec, cached, stored, children
+    finally:
+        mgr.stop()
+        await asyncio.wait({task}, timeout=10)
+        await client.close()
+        await app.stop()
+
+
+async def test_cron_events_carry_the_reconcilers_own_history_entries():
+    rec, cached, stored, children = await _run(ReconcilerOptions())
+    assert jsonutil.json_equal(cached["status"], stored["status"])  # exactly what a plain decode gives
+    key = f"{NS}/c"
+    parsed = rec._parsed_status[key][1]
+    hist = cached["status"]["history"]
+    assert len(hist) == 2
+    if jsonutil.NATIVE:
+        # the echo of our status write holds the very dicts the write encoded
+        assert all(h is e._json for h, e in zip(hist, parsed.history)), "history entries were rebuilt"
+        st = rec.codecs.memo.stats()
+        assert st["hits"] > 0 and st["stores"] > 0
+    # children: spec never built, everything the reconciler reads is there
+    assert children and all("spec" not in c and c["metadata"]["labels"][LABEL_CRON_NAME] == "c" for c in children)
+
+
+async def test_reference_mode_decodes_plainly():
+    rec, cached, stored, children = await _run(ReconcilerOptions(list_mode="cache", wire_codecs=False,
+                                                                 slim_child_cache=False))
+    assert rec.codecs is None
+    assert jsonutil.json_equal(cached["status"], stored["status"])
+    assert children and all("spec" in c for c in children)
