@@ -27,6 +27,11 @@ rank is one operator shard (its own apiserver process and 1000 Crons, weak
 scaling) and rank 0 reports the whole-job aggregate.  Ranks synchronise with
 gloo barriers; there is no device work to ``torch.cuda.synchronize()``.
 
+``single_process_*``: the chart ships ONE operator process (``sharding.count: 1``,
+``processes: 1``).  That deployment is operator-bound (its apiserver is about half
+busy), so it is the number that measures the product; it runs in the same invocation
+on the same Crons, after the timed run (``--single-process none`` skips it).
+
 ``vs_baseline``: the reference publishes no numbers, so the denominator
 is the reference *algorithm* (``--mode reference``: live LIST per reconcile, status
 churn, no event filtering) run by this same invocation on the same Crons, after the
@@ -128,6 +133,13 @@ def main() -> int:
                     help="vs_baseline denominator: 'measure' runs the reference algorithm (--mode reference, "
                          "one operator process, same Crons) in this same invocation after the timed run; "
                          "'recorded' divides by the BASELINE.md figure")
+    ap.add_argument("--single-process", choices=["measure", "none"], default="measure",
+                    help="also run the shipped default -- ONE operator process (the chart's sharding.count=1, "
+                         "processes=1) -- on the same 1000 Crons in this invocation, outside the headline's timed "
+                         "region, and report it as single_process_*: operator-bound, so it measures the product "
+                         "rather than the fake apiserver")
+    ap.add_argument("--single-steps", type=int, default=10)
+    ap.add_argument("--single-warmup", type=int, default=3)
     ap.add_argument("--baseline-steps", type=int, default=2)
     ap.add_argument("--baseline-warmup", type=int, default=1)
     ap.add_argument("--out", default="", help="also write the full result JSON here")
@@ -173,6 +185,25 @@ def main() -> int:
             "reconciles": res.raw_reconciles_per_s * res.elapsed_s, "p50": res.p50_latency_ms,
             "p99": res.p99_latency_ms, "req_per_fire": res.api_requests_per_fire,
             "cpu_op": res.cpu_s_operator, "cpu_api": res.cpu_s_apiserver}
+
+    # the shipped default: one operator process (untimed for the headline, like the baseline)
+    if a.single_process == "measure" and a.transport == "http":
+        if cfg.shards == 1:
+            sres, scfg = res, cfg
+        else:
+            scfg = BenchConfig(n_crons=a.crons, steps=a.single_steps, warmup=a.single_warmup,
+                               history_limit=a.history_limit, mode=a.mode, transport=a.transport, qps=a.qps,
+                               burst=a.burst, workers=a.workers, namespace=f"bench-1p-r{rank}", shards=1,
+                               apiserver_latency=a.apiserver_latency)
+            _barrier(dist)
+            sres = run_sync(scfg)
+            _barrier(dist)
+        mine["sp_elapsed_s"] = sres.elapsed_s
+        mine["sp_fires"] = scfg.n_crons * scfg.steps
+        mine["sp_p50"] = sres.p50_latency_ms
+        mine["sp_p99"] = sres.p99_latency_ms
+        mine["sp_cpu_op"] = sres.cpu_s_operator
+        mine["sp_cpu_api"] = sres.cpu_s_apiserver
 
     # the denominator: the reference algorithm on the same Crons, same box, same invocation
     # (untimed for the headline; one operator process, as the reference is one controller)
@@ -246,6 +277,18 @@ def main() -> int:
             "cron_engine": res.engine,
             "wall_s": round(wall, 2),
         }
+        if "sp_fires" in allr[0]:
+            sp_fires = sum(r["sp_fires"] for r in allr)
+            out.update({
+                # the chart's default deployment: one operator process per rank, same Crons
+                "single_process_value": round(sp_fires / max(r["sp_elapsed_s"] for r in allr), 2),
+                "single_process_p50_ms": round(max(r["sp_p50"] for r in allr), 2),
+                "single_process_p99_ms": round(max(r["sp_p99"] for r in allr), 2),
+                "single_process_operator_cpu_ms_per_fire": round(sum(r["sp_cpu_op"] for r in allr) * 1000
+                                                                 / sp_fires, 4),
+                "single_process_apiserver_busy_frac": round(max(r["sp_cpu_api"] / r["sp_elapsed_s"]
+                                                                for r in allr), 3),
+            })
         print(json.dumps(out), flush=True)
         if a.out:
             with open(a.out, "w") as fh:

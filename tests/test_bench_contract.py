@@ -45,6 +45,10 @@ def test_single_rank_line():
     assert d["baseline_value"] > 0 and d["baseline_p50_schedule_to_create_ms"] > 0
     assert d["baseline_api_requests_per_fire"] > d["api_requests_per_fire"]
     assert abs(d["vs_baseline"] - d["value"] / d["baseline_value"]) < 0.01 * d["vs_baseline"] + 0.002
+    # the shipped default (one operator process), measured in the same invocation
+    assert d["single_process_value"] > 0 and d["single_process_p50_ms"] > 0
+    assert d["single_process_p99_ms"] >= d["single_process_p50_ms"]
+    assert d["single_process_operator_cpu_ms_per_fire"] > 0 and 0 < d["single_process_apiserver_busy_frac"] < 2
 
 
 def test_recorded_baseline_option():
