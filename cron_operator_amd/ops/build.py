@@ -28,6 +28,17 @@ EXTENSIONS: Dict[str, List[str]] = {
     "_cron_engine": ["cron_engine.cpp"],
     "_fastjson": ["fastjson.cpp"],
     "_httpcodec": ["httpcodec.cpp"],
+    "_netconn": ["netconn.cpp"],
+}
+# headers each extension includes (a change rebuilds it)
+HEADERS: Dict[str, List[str]] = {
+    "_httpcodec": ["httpframe.h"],
+    "_netconn": ["httpframe.h"],
+}
+# extra linker inputs: _netconn speaks TLS through the system OpenSSL (the libssl CPython's own
+# ssl module is linked against, so SSL_CTX objects built by ssl.SSLContext are shared)
+LIBS: Dict[str, List[str]] = {
+    "_netconn": ["-lssl", "-lcrypto"],
 }
 
 
@@ -48,7 +59,8 @@ def needs_build(name: str) -> bool:
     if not out.exists():
         return True
     mtime = out.stat().st_mtime
-    return any((CSRC / s).stat().st_mtime > mtime for s in EXTENSIONS[name] if (CSRC / s).exists())
+    deps = EXTENSIONS[name] + HEADERS.get(name, [])
+    return any((CSRC / s).stat().st_mtime > mtime for s in deps if (CSRC / s).exists())
 
 
 def build_extension(name: str, force: bool = False, verbose: bool = False) -> Path:
@@ -64,7 +76,7 @@ def build_extension(name: str, force: bool = False, verbose: bool = False) -> Pa
     cmd = [
         _compiler(), "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden",
         "-Wall", "-Wno-missing-field-initializers", "-Wno-cast-function-type",
-        f"-I{inc}", *map(str, srcs), "-o", str(tmp),
+        f"-I{inc}", *map(str, srcs), "-o", str(tmp), *LIBS.get(name, []),
     ]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

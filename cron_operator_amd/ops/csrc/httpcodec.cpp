@@ -36,45 +36,13 @@
 #include <cstdint>
 #include <cstring>
 
+#include "httpframe.h"
+
 namespace {
 
+using namespace httpframe;
+
 constexpr Py_ssize_t kMaxHead = 1 << 20;
-
-// str.strip() of a latin-1 decoded string: ASCII whitespace, \x1c-\x1f, \x85, \xa0
-inline bool is_space(unsigned char c) {
-  return c == ' ' || (c >= '\t' && c <= '\r') || (c >= 0x1c && c <= 0x1f) || c == 0x85 || c == 0xa0;
-}
-
-inline void strip(const unsigned char*& b, const unsigned char*& e) {
-  while (b < e && is_space(*b)) ++b;
-  while (e > b && is_space(e[-1])) --e;
-}
-
-inline unsigned char lower(unsigned char c) { return (c >= 'A' && c <= 'Z') ? c + 32 : c; }
-
-bool ieq(const unsigned char* b, const unsigned char* e, const char* lit) {
-  const size_t n = std::strlen(lit);
-  if (static_cast<size_t>(e - b) != n) return false;
-  for (size_t i = 0; i < n; ++i)
-    if (lower(b[i]) != static_cast<unsigned char>(lit[i])) return false;
-  return true;
-}
-
-bool icontains(const unsigned char* b, const unsigned char* e, const char* lit) {
-  const size_t n = std::strlen(lit);
-  for (const unsigned char* p = b; p + n <= e; ++p) {
-    size_t i = 0;
-    while (i < n && lower(p[i]) == static_cast<unsigned char>(lit[i])) ++i;
-    if (i == n) return true;
-  }
-  return false;
-}
-
-const unsigned char* find(const unsigned char* b, const unsigned char* e, const char* lit, size_t n) {
-  if (e - b < static_cast<Py_ssize_t>(n)) return nullptr;
-  const void* r = memmem(b, static_cast<size_t>(e - b), lit, n);
-  return static_cast<const unsigned char*>(r);
-}
 
 PyObject* latin1(const unsigned char* b, const unsigned char* e) {
   return PyUnicode_DecodeLatin1(reinterpret_cast<const char*>(b), e - b, nullptr);
@@ -100,37 +68,6 @@ PyObject* lower_key(const unsigned char* b, const unsigned char* e) {
   Py_UCS1* d = PyUnicode_1BYTE_DATA(s);
   for (const unsigned char* p = b; p < e; ++p) *d++ = lower(*p);
   return s;
-}
-
-// Decimal integer with optional surrounding whitespace (int(v) for the values we accept)
-bool parse_dec(const unsigned char* b, const unsigned char* e, long long* out) {
-  strip(b, e);
-  if (b == e) return false;
-  long long v = 0;
-  for (const unsigned char* p = b; p < e; ++p) {
-    if (*p < '0' || *p > '9') return false;
-    if (v > (1LL << 52)) return false;
-    v = v * 10 + (*p - '0');
-  }
-  *out = v;
-  return true;
-}
-
-bool parse_hex(const unsigned char* b, const unsigned char* e, long long* out) {
-  strip(b, e);
-  if (b == e) return false;
-  long long v = 0;
-  for (const unsigned char* p = b; p < e; ++p) {
-    int d;
-    if (*p >= '0' && *p <= '9') d = *p - '0';
-    else if (*p >= 'a' && *p <= 'f') d = *p - 'a' + 10;
-    else if (*p >= 'A' && *p <= 'F') d = *p - 'A' + 10;
-    else return false;
-    if (v > (1LL << 48)) return false;
-    v = v * 16 + d;
-  }
-  *out = v;
-  return true;
 }
 
 struct Buf {
@@ -305,38 +242,12 @@ PyObject* parse_response(PyObject*, PyObject* args) {
   const unsigned char* e = buf.end();
   const unsigned char* hend = find(b, e, "\r\n\r\n", 4);
   if (!hend) Py_RETURN_NONE;
-  const unsigned char* l_end = find(b, hend + 2, "\r\n", 2);
-  const unsigned char* sp1 = static_cast<const unsigned char*>(memchr(b, ' ', static_cast<size_t>(l_end - b)));
-  if (!sp1) return PyLong_FromLong(-1);
-  const unsigned char* sp2 =
-      static_cast<const unsigned char*>(memchr(sp1 + 1, ' ', static_cast<size_t>(l_end - sp1 - 1)));
-  long long status;
-  if (!parse_dec(sp1 + 1, sp2 ? sp2 : l_end, &status)) return PyLong_FromLong(-1);
+  ResponseHead h;
+  if (!parse_response_head(b, hend, &h)) return PyLong_FromLong(-1);
+  const long long status = h.status;
   if (status >= 100 && status < 200) return PyLong_FromLong(-1);  // interim: incremental parser
-  bool close = (sp1 - b) == 8 && std::memcmp(b, "HTTP/1.0", 8) == 0;
-  long long clen = -1, retry_after = -1;
-  bool chunked = false;
-  const unsigned char* p = l_end + 2;
-  while (p < hend + 2) {
-    const unsigned char* nl = find(p, hend + 2, "\r\n", 2);
-    const unsigned char* colon = static_cast<const unsigned char*>(memchr(p, ':', static_cast<size_t>(nl - p)));
-    const unsigned char *kb = p, *ke = colon ? colon : nl;
-    const unsigned char *vb = colon ? colon + 1 : nl, *ve = nl;
-    strip(kb, ke);
-    strip(vb, ve);
-    if (ieq(kb, ke, "content-length")) {
-      if (!parse_dec(vb, ve, &clen)) return PyLong_FromLong(-1);
-    } else if (ieq(kb, ke, "transfer-encoding")) {
-      chunked = icontains(vb, ve, "chunked");
-    } else if (ieq(kb, ke, "connection")) {
-      if (ieq(vb, ve, "close")) close = true;
-      else if (ieq(vb, ve, "keep-alive")) close = false;
-    } else if (ieq(kb, ke, "retry-after")) {
-      long long ra;
-      retry_after = parse_dec(vb, ve, &ra) ? ra : -1;
-    }
-    p = nl + 2;
-  }
+  const bool close = h.close, chunked = h.chunked;
+  const long long clen = h.content_length, retry_after = h.retry_after;
   const unsigned char* body_b = hend + 4;
   PyObject* body = nullptr;
   Py_ssize_t consumed;

@@ -1,0 +1,1263 @@
+// Native HTTP/1.1 client connection for the asyncio event loop (CPython extension `_netconn`).
+//
+// Every API call the operator makes is one HTTP/1.1 exchange with the apiserver and every
+// cache update arrives on a watch stream (reference: client-go REST + watch over net/http,
+// used by controller-runtime's client and informers -- /root/reference/cmd/operator/start.go
+// builds that rest config).  Profiling one operator process at 1000 Crons put
+// the Python side of that plumbing -- asyncio's selector transport, the protocol callbacks,
+// response framing and de-chunking, TLS through asyncio's pure-Python SSL protocol -- at a
+// tenth of the process's CPU.  `Conn` does the same work in one object that the loop calls
+// directly:
+//
+//   * the socket (already connected by the caller, handed over as a file descriptor) is
+//     registered with the loop once (`loop.add_reader(fd, conn._on_readable)`); a readiness
+//     callback receives, frames and completes the in-flight response in C++;
+//   * TLS is OpenSSL on the socket itself (non-blocking `SSL_connect`/`SSL_read`/`SSL_write`),
+//     configured by the caller's `ssl.SSLContext` -- the `SSL_CTX` Python built from the
+//     kubeconfig (CA, client certificate, verify mode, ALPN) is used as is, and hostname
+//     checks and SNI follow what `SSLContext.wrap_socket(server_hostname=...)` does;
+//   * request mode: `send(data) -> Future[(status, body, retry_after)]`, Content-Length,
+//     chunked and read-until-close bodies, interim 1xx responses skipped, keep-alive;
+//   * stream mode (`open_stream(data, decode) -> Future[status]`): the body of a watch is
+//     de-chunked and split into lines; each non-empty line is decoded by `decode` (a native
+//     `_fastjson.Codec` in the operator) and queued; `take()` hands over the whole batch and
+//     `wait()` returns a future that completes when items arrive or the stream ends.
+//
+// Failure semantics are those of the Python protocols in runtime/fasthttp.py (`_Conn`,
+// `_StreamConn`), which stay the fallback (proxies, or no native build) and the oracle of
+// tests/test_netconn.py: a connection lost before the response raises
+// `ConnectionFailed(msg, no_response, reused)` so the pool can retry a stale keep-alive
+// connection once; an error status on a stream raises `HttpStatusError(status, body)`.
+//
+// Everything runs on the loop's thread under the GIL; nothing here blocks.
+
+#define PY_SSIZE_T_CLEAN
+#include <Python.h>
+#include <structmember.h>
+
+#include <arpa/inet.h>
+#include <errno.h>
+#include <openssl/err.h>
+#include <openssl/ssl.h>
+#include <openssl/x509v3.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <cstring>
+#include <string>
+
+#include "httpframe.h"
+
+namespace {
+
+using namespace httpframe;
+
+constexpr size_t kMaxHead = 1 << 20;
+constexpr size_t kReadChunk = 256 * 1024;
+constexpr size_t kMaxReadPerWake = 4 << 20;  // bound one callback's work on a busy stream
+
+// exception classes installed by configure(): ConnectionFailed(msg, no_response, reused),
+// HttpStatusError(status, body), ssl.SSLError(msg)
+PyObject* g_conn_failed = nullptr;
+PyObject* g_status_error = nullptr;
+PyObject* g_ssl_error = nullptr;
+
+PyObject *s_create_future, *s_set_result, *s_set_exception, *s_done, *s_add_reader, *s_remove_reader,
+    *s_add_writer, *s_remove_writer, *s_on_readable, *s_on_writable, *s_options, *s_verify_mode;
+
+// one receive buffer for every connection: all callbacks run on the loop's thread under the GIL
+char g_rbuf[kReadChunk];
+
+enum Mode { kRequest = 0, kStream = 1 };
+enum Handshake { kHsNone = 0, kHsRunning = 1 };
+enum IoResult : long { kWantRead = -1, kWantWrite = -2, kIoError = -3 };
+
+// parser states (request mode): head, Content-Length body, chunked body, body until close
+enum RespState { kHead = 0, kLength = 1, kChunked = 2, kUntilClose = 3 };
+
+struct Core {
+  std::string rbuf;  // received, not yet consumed: rbuf[rpos:]
+  size_t rpos = 0;
+  std::string wbuf;  // request bytes not written yet: wbuf[wpos:]
+  size_t wpos = 0;
+  // request mode: the response being parsed
+  int state = kHead;
+  long long status = 0, clen = -1, retry_after = -1;
+  bool close_after = false;
+  std::string body;
+  // stream mode
+  long long sstatus = 0, sclen = -1;
+  bool schunked = false;
+  std::string lines;
+  std::string err_body;
+};
+
+struct ConnObject {
+  PyObject_HEAD
+  Core* core;
+  PyObject* loop;
+  PyObject* ssl_ctx;   // the Python ssl.SSLContext (keeps its SSL_CTX alive)
+  SSL* ssl;
+  int fd;
+  int mode;
+  int hs;
+  PyObject* hs_fut;    // TLS handshake
+  PyObject* fut;       // request mode: the response; stream mode: the head (status)
+  PyObject* decode;    // stream mode: bytes line -> item
+  PyObject* items;     // stream mode: decoded items not taken yet (list)
+  PyObject* waiter;    // stream mode: wait() future
+  PyObject* stream_error;
+  PyObject* weakrefs;
+  long used;           // requests sent on this connection
+  long ssl_gen;        // pool bookkeeping (TLS context generation)
+  double deadline;     // pool bookkeeping (loop time the in-flight response is due by)
+  bool alive;
+  bool got_any;        // a byte of the in-flight response arrived
+  bool reader_on;
+  bool writer_on;
+  bool stream_done;
+};
+
+// ----------------------------------------------------------------------------- helpers
+
+// fut.set_result(value) unless fut is done (cancelled, or failed by a deadline sweep); steals nothing
+void resolve(PyObject* fut, PyObject* value) {
+  if (!fut) return;
+  PyObject* d = PyObject_CallMethodNoArgs(fut, s_done);
+  if (!d) {
+    PyErr_Clear();
+    return;
+  }
+  const bool done = d == Py_True;
+  Py_DECREF(d);
+  if (done) return;
+  PyObject* r = PyObject_CallMethodOneArg(fut, s_set_result, value);
+  if (!r) PyErr_Clear();
+  Py_XDECREF(r);
+}
+
+void reject(PyObject* fut, PyObject* exc) {
+  if (!fut || !exc) {
+    PyErr_Clear();
+    return;
+  }
+  PyObject* d = PyObject_CallMethodNoArgs(fut, s_done);
+  if (!d) {
+    PyErr_Clear();
+    return;
+  }
+  const bool done = d == Py_True;
+  Py_DECREF(d);
+  if (done) return;
+  PyObject* r = PyObject_CallMethodOneArg(fut, s_set_exception, exc);
+  if (!r) PyErr_Clear();
+  Py_XDECREF(r);
+}
+
+PyObject* conn_failed(const std::string& msg, bool no_response, bool reused) {
+  return PyObject_CallFunction(g_conn_failed, "s#OO", msg.data(), static_cast<Py_ssize_t>(msg.size()),
+                               no_response ? Py_True : Py_False, reused ? Py_True : Py_False);
+}
+
+PyObject* status_error(long long status, const std::string& body) {
+  return PyObject_CallFunction(g_status_error, "Ly#", status, body.data(), static_cast<Py_ssize_t>(body.size()));
+}
+
+PyObject* ssl_error(const std::string& msg) {
+  return PyObject_CallFunction(g_ssl_error, "s#", msg.data(), static_cast<Py_ssize_t>(msg.size()));
+}
+
+std::string ssl_error_string(SSL* ssl, int err) {
+  std::string msg;
+  char buf[256];
+  unsigned long e;
+  while ((e = ERR_get_error()) != 0) {
+    ERR_error_string_n(e, buf, sizeof buf);
+    if (!msg.empty()) msg += "; ";
+    msg += buf;
+  }
+  if (ssl) {
+    const long vr = SSL_get_verify_result(ssl);
+    if (vr != X509_V_OK) {
+      msg += msg.empty() ? "" : " ";
+      msg += "(certificate verify failed: ";
+      msg += X509_verify_cert_error_string(vr);
+      msg += ")";
+    }
+  }
+  if (msg.empty()) {
+    if (err == SSL_ERROR_SYSCALL) msg = errno ? std::strerror(errno) : "unexpected EOF in TLS";
+    else msg = "TLS error " + std::to_string(err);
+  }
+  return msg;
+}
+
+void set_reader(ConnObject* s, bool on) {
+  if (s->fd < 0 || !s->loop || s->reader_on == on) return;
+  PyObject* r;
+  PyObject* fd = PyLong_FromLong(s->fd);
+  if (!fd) {
+    PyErr_Clear();
+    return;
+  }
+  if (on) {
+    PyObject* cb = PyObject_GetAttr(reinterpret_cast<PyObject*>(s), s_on_readable);
+    r = cb ? PyObject_CallMethodObjArgs(s->loop, s_add_reader, fd, cb, nullptr) : nullptr;
+    Py_XDECREF(cb);
+  } else {
+    r = PyObject_CallMethodObjArgs(s->loop, s_remove_reader, fd, nullptr);
+  }
+  Py_DECREF(fd);
+  if (r) s->reader_on = on;
+  else PyErr_Clear();  // a closed loop: nothing is registered any more
+  Py_XDECREF(r);
+}
+
+void set_writer(ConnObject* s, bool on) {
+  if (s->fd < 0 || !s->loop || s->writer_on == on) return;
+  PyObject* r;
+  PyObject* fd = PyLong_FromLong(s->fd);
+  if (!fd) {
+    PyErr_Clear();
+    return;
+  }
+  if (on) {
+    PyObject* cb = PyObject_GetAttr(reinterpret_cast<PyObject*>(s), s_on_writable);
+    r = cb ? PyObject_CallMethodObjArgs(s->loop, s_add_writer, fd, cb, nullptr) : nullptr;
+    Py_XDECREF(cb);
+  } else {
+    r = PyObject_CallMethodObjArgs(s->loop, s_remove_writer, fd, nullptr);
+  }
+  Py_DECREF(fd);
+  if (r) s->writer_on = on;
+  else PyErr_Clear();
+  Py_XDECREF(r);
+}
+
+// Unregister and close the socket (and the TLS session).  Futures are left to the caller.
+void close_io(ConnObject* s) {
+  s->alive = false;
+  if (s->fd < 0) return;
+  set_reader(s, false);
+  set_writer(s, false);
+  if (s->ssl) {
+    SSL_free(s->ssl);
+    s->ssl = nullptr;
+  }
+  ::close(s->fd);
+  s->fd = -1;
+}
+
+// >0 bytes, 0 EOF, kWantRead, kWantWrite, kIoError (*err set)
+long io_read(ConnObject* s, char* buf, size_t n, std::string* err) {
+  if (!s->ssl) {
+    for (;;) {
+      const ssize_t r = ::recv(s->fd, buf, n, 0);
+      if (r >= 0) return static_cast<long>(r);
+      if (errno == EINTR) continue;
+      if (errno == EAGAIN || errno == EWOULDBLOCK) return kWantRead;
+      *err = std::strerror(errno);
+      return kIoError;
+    }
+  }
+  ERR_clear_error();
+  errno = 0;
+  const int r = SSL_read(s->ssl, buf, static_cast<int>(n));
+  if (r > 0) return r;
+  const int e = SSL_get_error(s->ssl, r);
+  switch (e) {
+    case SSL_ERROR_WANT_READ: return kWantRead;
+    case SSL_ERROR_WANT_WRITE: return kWantWrite;
+    case SSL_ERROR_ZERO_RETURN: return 0;
+    case SSL_ERROR_SYSCALL:
+      if (ERR_peek_error() == 0 && errno == 0) return 0;  // EOF without close_notify
+      if (errno == EAGAIN || errno == EWOULDBLOCK) return kWantRead;
+      [[fallthrough]];
+    default:
+      *err = ssl_error_string(s->ssl, e);
+      return kIoError;
+  }
+}
+
+long io_write(ConnObject* s, const char* buf, size_t n, std::string* err) {
+  if (!s->ssl) {
+    for (;;) {
+      const ssize_t r = ::send(s->fd, buf, n, MSG_NOSIGNAL);
+      if (r >= 0) return static_cast<long>(r);
+      if (errno == EINTR) continue;
+      if (errno == EAGAIN || errno == EWOULDBLOCK) return kWantWrite;
+      *err = std::strerror(errno);
+      return kIoError;
+    }
+  }
+  ERR_clear_error();
+  errno = 0;
+  const int r = SSL_write(s->ssl, buf, static_cast<int>(n));
+  if (r > 0) return r;
+  const int e = SSL_get_error(s->ssl, r);
+  switch (e) {
+    case SSL_ERROR_WANT_READ: return kWantRead;
+    case SSL_ERROR_WANT_WRITE: return kWantWrite;
+    case SSL_ERROR_SYSCALL:
+      if (errno == EAGAIN || errno == EWOULDBLOCK) return kWantWrite;
+      [[fallthrough]];
+    default:
+      *err = ssl_error_string(s->ssl, e);
+      return kIoError;
+  }
+}
+
+// ----------------------------------------------------------------------------- connection loss
+
+// The connection broke or the peer closed it (`connection_lost` of the Python protocols).
+void lost(ConnObject* s, const std::string& why);
+
+// ----------------------------------------------------------------------------- request mode
+
+void reset_response(Core& c) {
+  c.state = kHead;
+  c.status = 0;
+  c.clen = -1;
+  c.retry_after = -1;
+  c.close_after = false;
+  c.body.clear();
+}
+
+// Complete the in-flight response with the parsed status and body [b, b + n).
+void finish_response(ConnObject* s, const char* b, size_t n) {
+  Core& c = *s->core;
+  PyObject* body = PyBytes_FromStringAndSize(b, static_cast<Py_ssize_t>(n));
+  PyObject* ra;
+  if (c.status >= 400 && c.retry_after >= 0) ra = PyLong_FromLongLong(c.retry_after);
+  else {
+    Py_INCREF(Py_None);
+    ra = Py_None;
+  }
+  PyObject* result = (body && ra) ? Py_BuildValue("(LNN)", c.status, body, ra) : nullptr;
+  if (!result) {
+    Py_XDECREF(body);
+    Py_XDECREF(ra);
+    PyErr_Clear();
+  }
+  const bool close_after = c.close_after;
+  reset_response(c);
+  if (close_after) close_io(s);
+  PyObject* fut = s->fut;
+  s->fut = nullptr;
+  if (result) resolve(fut, result);
+  else {
+    PyObject* exc = conn_failed("out of memory decoding the response", false, false);
+    reject(fut, exc);
+    Py_XDECREF(exc);
+  }
+  Py_XDECREF(result);
+  Py_XDECREF(fut);
+}
+
+// Advance the response parser over rbuf[rpos:].  1: a response completed (and was delivered),
+// 0: more bytes needed, -1: malformed (the caller drops the connection).
+int parse_response(ConnObject* s) {
+  Core& c = *s->core;
+  for (;;) {
+    const unsigned char* b = reinterpret_cast<const unsigned char*>(c.rbuf.data()) + c.rpos;
+    const unsigned char* e = reinterpret_cast<const unsigned char*>(c.rbuf.data()) + c.rbuf.size();
+    if (c.state == kHead) {
+      const unsigned char* hend = find(b, e, "\r\n\r\n", 4);
+      if (!hend) return static_cast<size_t>(e - b) > kMaxHead ? -1 : 0;
+      ResponseHead h;
+      if (!parse_response_head(b, hend, &h)) return -1;
+      c.rpos += static_cast<size_t>(hend + 4 - b);
+      c.status = h.status;
+      c.close_after = h.close;
+      c.retry_after = h.retry_after;
+      if (h.status >= 100 && h.status < 200) continue;  // interim response: the next head follows
+      if (h.status == 204 || h.status == 304) {
+        finish_response(s, "", 0);
+        return 1;
+      }
+      if (h.chunked) {
+        c.state = kChunked;
+        c.body.clear();
+      } else if (h.content_length >= 0) {
+        c.state = kLength;
+        c.clen = h.content_length;
+      } else {
+        c.state = kUntilClose;
+        c.close_after = true;
+      }
+      continue;
+    }
+    if (c.state == kLength) {
+      if (e - b < c.clen) return 0;
+      const size_t n = static_cast<size_t>(c.clen);
+      const size_t at = c.rpos;
+      c.rpos += n;
+      // deliver straight from the receive buffer: finishing may close the socket, never the buffer
+      finish_response(s, c.rbuf.data() + at, n);
+      if (c.rpos == c.rbuf.size()) {
+        c.rbuf.clear();  // keeps its capacity for the next response
+        c.rpos = 0;
+      }
+      return 1;
+    }
+    if (c.state == kChunked) {
+      for (;;) {
+        b = reinterpret_cast<const unsigned char*>(c.rbuf.data()) + c.rpos;
+        const unsigned char* nl = find(b, e, "\r\n", 2);
+        if (!nl) return 0;
+        long long size;
+        if (!chunk_size(b, nl, &size)) return -1;
+        if (size == 0) {
+          // trailers end with an empty line; the search starts at this line's CRLF
+          const unsigned char* tend = find(nl, e, "\r\n\r\n", 4);
+          if (!tend) return 0;
+          c.rpos += static_cast<size_t>(tend + 4 - b);
+          std::string body;
+          body.swap(c.body);
+          c.rbuf.erase(0, c.rpos);
+          c.rpos = 0;
+          finish_response(s, body.data(), body.size());
+          return 1;
+        }
+        if (e - (nl + 2) < size + 2) return 0;
+        c.body.append(reinterpret_cast<const char*>(nl + 2), static_cast<size_t>(size));
+        c.rpos += static_cast<size_t>(nl + 2 + size + 2 - b);
+      }
+    }
+    // kUntilClose: everything is body; the response completes at EOF
+    c.body.append(reinterpret_cast<const char*>(b), static_cast<size_t>(e - b));
+    c.rbuf.clear();
+    c.rpos = 0;
+    return 0;
+  }
+}
+
+// ----------------------------------------------------------------------------- stream mode
+
+void wake(ConnObject* s) {
+  if (s->waiter) {
+    PyObject* w = s->waiter;
+    s->waiter = nullptr;
+    resolve(w, Py_None);
+    Py_DECREF(w);
+  }
+}
+
+// The body bytes received so far, de-chunked when chunked, appended to *out.
+void stream_body(ConnObject* s, std::string* out) {
+  Core& c = *s->core;
+  if (!c.schunked) {
+    out->append(c.rbuf, c.rpos, std::string::npos);
+    c.rbuf.clear();
+    c.rpos = 0;
+    return;
+  }
+  for (;;) {
+    const unsigned char* b = reinterpret_cast<const unsigned char*>(c.rbuf.data()) + c.rpos;
+    const unsigned char* e = reinterpret_cast<const unsigned char*>(c.rbuf.data()) + c.rbuf.size();
+    const unsigned char* nl = find(b, e, "\r\n", 2);
+    if (!nl) break;
+    long long size;
+    if (!chunk_size(b, nl, &size)) {
+      s->stream_done = true;  // malformed framing: end the stream
+      c.rbuf.clear();
+      c.rpos = 0;
+      break;
+    }
+    if (size == 0) {
+      s->stream_done = true;
+      c.rbuf.clear();
+      c.rpos = 0;
+      break;
+    }
+    if (e - (nl + 2) < size + 2) break;
+    out->append(reinterpret_cast<const char*>(nl + 2), static_cast<size_t>(size));
+    c.rpos += static_cast<size_t>(nl + 2 + size + 2 - b);
+  }
+  if (c.rpos > 0 && c.rpos == c.rbuf.size()) {
+    c.rbuf.clear();
+    c.rpos = 0;
+  } else if (c.rpos > (1 << 16)) {
+    c.rbuf.erase(0, c.rpos);
+    c.rpos = 0;
+  }
+}
+
+void fail_stream_head(ConnObject* s, PyObject* exc) {
+  PyObject* h = s->fut;
+  s->fut = nullptr;
+  reject(h, exc);
+  Py_XDECREF(h);
+}
+
+// Decode complete lines into items.  false: the decoder raised (the stream ends with that error).
+bool stream_lines(ConnObject* s) {
+  Core& c = *s->core;
+  bool got = false;
+  size_t pos = 0;
+  for (;;) {
+    const size_t nl = c.lines.find('\n', pos);
+    if (nl == std::string::npos) break;
+    size_t b = pos, e = nl;
+    pos = nl + 1;
+    while (b < e && is_bytes_space(static_cast<unsigned char>(c.lines[b]))) ++b;
+    while (e > b && is_bytes_space(static_cast<unsigned char>(c.lines[e - 1]))) --e;
+    if (b == e) continue;
+    PyObject* line = PyBytes_FromStringAndSize(c.lines.data() + b, static_cast<Py_ssize_t>(e - b));
+    PyObject* item = line ? PyObject_CallOneArg(s->decode, line) : nullptr;
+    Py_XDECREF(line);
+    if (!item || PyList_Append(s->items, item) < 0) {
+      Py_XDECREF(item);
+      PyObject *type, *value, *tb;
+      PyErr_Fetch(&type, &value, &tb);
+      PyErr_NormalizeException(&type, &value, &tb);
+      Py_XDECREF(type);
+      Py_XDECREF(tb);
+      Py_XSETREF(s->stream_error, value);
+      c.lines.erase(0, pos);
+      if (got) wake(s);
+      return false;
+    }
+    Py_DECREF(item);
+    got = true;
+  }
+  c.lines.erase(0, pos);
+  if (got) wake(s);
+  return true;
+}
+
+// 0: keep going, -1: the stream ended (malformed head or decode error; the caller closes)
+int parse_stream(ConnObject* s) {
+  Core& c = *s->core;
+  if (c.sstatus == 0) {
+    const unsigned char* b = reinterpret_cast<const unsigned char*>(c.rbuf.data()) + c.rpos;
+    const unsigned char* e = reinterpret_cast<const unsigned char*>(c.rbuf.data()) + c.rbuf.size();
+    const unsigned char* hend = find(b, e, "\r\n\r\n", 4);
+    if (!hend) {
+      if (static_cast<size_t>(e - b) <= kMaxHead) return 0;
+      PyObject* exc = conn_failed("stream response head too large", false, false);
+      fail_stream_head(s, exc);
+      Py_XDECREF(exc);
+      return -1;
+    }
+    ResponseHead h;
+    if (!parse_response_head(b, hend, &h) || h.status <= 0) {
+      PyObject* exc = conn_failed("bad HTTP response head on a stream", false, false);
+      fail_stream_head(s, exc);
+      Py_XDECREF(exc);
+      return -1;
+    }
+    c.rpos += static_cast<size_t>(hend + 4 - b);
+    c.sstatus = h.status;
+    c.schunked = h.chunked;
+    c.sclen = h.content_length;
+    if (h.status < 400) {
+      PyObject* st = PyLong_FromLongLong(h.status);
+      PyObject* f = s->fut;
+      s->fut = nullptr;
+      if (st) resolve(f, st);
+      else PyErr_Clear();
+      Py_XDECREF(st);
+      Py_XDECREF(f);
+    }
+  }
+  if (c.sstatus >= 400) {  // collect the error body, then fail the open
+    stream_body(s, &c.err_body);
+    if ((c.sclen >= 0 && static_cast<long long>(c.err_body.size()) >= c.sclen) || s->stream_done) {
+      PyObject* exc = status_error(c.sstatus, c.err_body);
+      fail_stream_head(s, exc);
+      Py_XDECREF(exc);
+    }
+    return 0;
+  }
+  stream_body(s, &c.lines);
+  if (!stream_lines(s)) {
+    s->stream_done = true;
+    return -1;
+  }
+  if (s->stream_done) wake(s);
+  return 0;
+}
+
+// ----------------------------------------------------------------------------- loss / reads / writes
+
+void lost(ConnObject* s, const std::string& why) {
+  Core& c = *s->core;
+  if (s->mode == kStream) {
+    s->stream_done = true;
+    if (s->fut) {  // the head never completed
+      PyObject* exc = c.sstatus >= 400 ? status_error(c.sstatus, c.err_body)
+                                       : conn_failed("stream closed: " + why, true, false);
+      fail_stream_head(s, exc);
+      Py_XDECREF(exc);
+    }
+    close_io(s);
+    wake(s);
+    return;
+  }
+  if (s->fut && c.state == kUntilClose) {  // a read-until-close body ends here
+    std::string body;
+    body.swap(c.body);
+    c.close_after = true;
+    finish_response(s, body.data(), body.size());
+    close_io(s);
+    return;
+  }
+  close_io(s);
+  if (s->fut) {
+    PyObject* f = s->fut;
+    s->fut = nullptr;
+    PyObject* exc = conn_failed("connection lost: " + why, !s->got_any, s->used > 1);
+    reject(f, exc);
+    Py_XDECREF(exc);
+    Py_DECREF(f);
+  }
+}
+
+// Write what is buffered.  false: the connection broke (already handled).
+bool flush(ConnObject* s) {
+  Core& c = *s->core;
+  std::string err;
+  while (c.wpos < c.wbuf.size()) {
+    const long n = io_write(s, c.wbuf.data() + c.wpos, c.wbuf.size() - c.wpos, &err);
+    if (n > 0) {
+      c.wpos += static_cast<size_t>(n);
+      continue;
+    }
+    if (n == kWantWrite) {
+      set_writer(s, true);
+      return true;
+    }
+    if (n == kWantRead) {  // TLS needs the peer first: the reader retries the write
+      set_writer(s, false);
+      return true;
+    }
+    lost(s, err);
+    return false;
+  }
+  c.wbuf.clear();
+  c.wpos = 0;
+  set_writer(s, false);
+  return true;
+}
+
+void handshake_step(ConnObject* s) {
+  ERR_clear_error();
+  errno = 0;
+  const int r = SSL_connect(s->ssl);
+  if (r == 1) {
+    s->hs = kHsNone;
+    set_writer(s, false);
+    PyObject* f = s->hs_fut;
+    s->hs_fut = nullptr;
+    resolve(f, Py_None);
+    Py_XDECREF(f);
+    return;
+  }
+  const int e = SSL_get_error(s->ssl, r);
+  if (e == SSL_ERROR_WANT_READ) {
+    set_writer(s, false);
+    return;
+  }
+  if (e == SSL_ERROR_WANT_WRITE) {
+    set_writer(s, true);
+    return;
+  }
+  const std::string msg = ssl_error_string(s->ssl, e);
+  s->hs = kHsNone;
+  close_io(s);
+  PyObject* f = s->hs_fut;
+  s->hs_fut = nullptr;
+  PyObject* exc = ssl_error("TLS handshake failed: " + msg);
+  reject(f, exc);
+  Py_XDECREF(exc);
+  Py_XDECREF(f);
+}
+
+void read_ready(ConnObject* s) {
+  Core& c = *s->core;
+  std::string err;
+  size_t total = 0;
+  bool eof = false, failed = false;
+  for (;;) {
+    const long n = io_read(s, g_rbuf, sizeof g_rbuf, &err);
+    if (n > 0) {
+      s->got_any = true;
+      if (c.rpos == c.rbuf.size()) {
+        c.rbuf.clear();
+        c.rpos = 0;
+      }
+      c.rbuf.append(g_rbuf, static_cast<size_t>(n));
+      total += static_cast<size_t>(n);
+      // plain sockets: a short read drained the socket (the loop is level-triggered, so more
+      // data wakes us again); TLS: read until OpenSSL needs the socket, it may hold records
+      if (!s->ssl && static_cast<size_t>(n) < sizeof g_rbuf) break;
+      if (total >= kMaxReadPerWake) break;
+      continue;
+    }
+    if (n == 0) eof = true;
+    else if (n == kWantWrite) set_writer(s, true);  // TLS renegotiation needs to write first
+    else if (n == kIoError) failed = true;
+    break;
+  }
+  if (total) {
+    int r;
+    if (s->mode == kStream) r = parse_stream(s);
+    else {
+      r = 1;
+      while (r == 1 && s->fd >= 0) r = parse_response(s);  // stray bytes after a response stay buffered
+      if (r == -1) {
+        s->alive = false;
+        close_io(s);
+        if (s->fut) {
+          PyObject* f = s->fut;
+          s->fut = nullptr;
+          PyObject* exc = conn_failed("bad HTTP response", false, false);
+          reject(f, exc);
+          Py_XDECREF(exc);
+          Py_DECREF(f);
+        }
+        return;
+      }
+    }
+    if (r == -1) {  // stream ended by a decode error or bad head
+      close_io(s);
+      wake(s);
+      return;
+    }
+  }
+  if (s->fd < 0) return;
+  if (eof) lost(s, "closed by peer");
+  else if (failed) lost(s, err);
+}
+
+// ----------------------------------------------------------------------------- the type
+
+SSL_CTX* ssl_ctx_of(PyObject* ctx) {
+  // ssl.SSLContext subclasses _ssl._SSLContext, whose C struct starts with the SSL_CTX pointer
+  // right after the object header; the match with the Python-visible options and verify mode
+  // guards the layout assumption.
+  bool is_ctx = false;
+  for (PyTypeObject* t = Py_TYPE(ctx); t; t = t->tp_base)
+    if (std::strcmp(t->tp_name, "_ssl._SSLContext") == 0) {
+      is_ctx = true;
+      break;
+    }
+  if (!is_ctx) {
+    PyErr_SetString(PyExc_TypeError, "ssl_context must be an ssl.SSLContext");
+    return nullptr;
+  }
+  SSL_CTX* sc = *reinterpret_cast<SSL_CTX**>(reinterpret_cast<char*>(ctx) + sizeof(PyObject));
+  if (!sc) {
+    PyErr_SetString(PyExc_TypeError, "SSLContext has no SSL_CTX");
+    return nullptr;
+  }
+  PyObject* opt = PyObject_GetAttr(ctx, s_options);
+  PyObject* vm = opt ? PyObject_GetAttr(ctx, s_verify_mode) : nullptr;
+  if (!vm) {
+    Py_XDECREF(opt);
+    return nullptr;
+  }
+  const unsigned long long py_opt = PyLong_AsUnsignedLongLong(opt);
+  const long py_vm = PyLong_AsLong(vm);
+  Py_DECREF(opt);
+  Py_DECREF(vm);
+  if (PyErr_Occurred()) return nullptr;
+  const int mode = SSL_CTX_get_verify_mode(sc);
+  const int want = py_vm == 0 ? SSL_VERIFY_NONE
+                   : py_vm == 1 ? SSL_VERIFY_PEER
+                                : (SSL_VERIFY_PEER | SSL_VERIFY_FAIL_IF_NO_PEER_CERT);
+  if (static_cast<unsigned long long>(SSL_CTX_get_options(sc)) != py_opt || mode != want) {
+    PyErr_SetString(PyExc_TypeError, "unrecognised SSLContext layout");
+    return nullptr;
+  }
+  return sc;
+}
+
+int conn_init(ConnObject* self, PyObject* args, PyObject* kw) {
+  static const char* kwlist[] = {"loop", "fd", "ssl_context", "server_hostname", "check_hostname",
+                                 "hostname_checks_common_name", nullptr};
+  PyObject *loop, *ctx = Py_None;
+  int fd, check_hostname = 0, checks_cn = 1;
+  const char* host = nullptr;
+  if (!PyArg_ParseTupleAndKeywords(args, kw, "Oi|Ozpp", const_cast<char**>(kwlist), &loop, &fd, &ctx, &host,
+                                   &check_hostname, &checks_cn))
+    return -1;
+  if (self->core) {
+    PyErr_SetString(PyExc_RuntimeError, "Conn is already initialised");
+    return -1;
+  }
+  if (!g_conn_failed) {
+    PyErr_SetString(PyExc_RuntimeError, "_netconn.configure() was not called");
+    return -1;
+  }
+  SSL* ssl = nullptr;
+  if (ctx != Py_None) {
+    SSL_CTX* sc = ssl_ctx_of(ctx);
+    if (!sc) return -1;
+    ssl = SSL_new(sc);
+    if (!ssl || SSL_set_fd(ssl, fd) != 1) {
+      if (ssl) SSL_free(ssl);
+      PyErr_SetString(PyExc_RuntimeError, "SSL_new failed");
+      return -1;
+    }
+    SSL_set_connect_state(ssl);
+    SSL_set_mode(ssl, SSL_MODE_ENABLE_PARTIAL_WRITE | SSL_MODE_ACCEPT_MOVING_WRITE_BUFFER);
+    SSL_set_options(ssl, SSL_OP_IGNORE_UNEXPECTED_EOF);
+    if (host && *host) {
+      unsigned char tmp[16];
+      const bool ip = inet_pton(AF_INET, host, tmp) == 1 || inet_pton(AF_INET6, host, tmp) == 1;
+      if (!ip) SSL_set_tlsext_host_name(ssl, host);  // SNI is for names only (RFC 6066)
+      if (check_hostname) {
+        X509_VERIFY_PARAM* p = SSL_get0_param(ssl);
+        X509_VERIFY_PARAM_set_hostflags(
+            p, X509_CHECK_FLAG_NO_PARTIAL_WILDCARDS | (checks_cn ? 0 : X509_CHECK_FLAG_NEVER_CHECK_SUBJECT));
+        const int ok = ip ? X509_VERIFY_PARAM_set1_ip_asc(p, host) : X509_VERIFY_PARAM_set1_host(p, host, 0);
+        if (ok != 1) {
+          SSL_free(ssl);
+          PyErr_Format(PyExc_ValueError, "invalid server hostname %s", host);
+          return -1;
+        }
+      }
+    } else if (check_hostname) {
+      SSL_free(ssl);
+      PyErr_SetString(PyExc_ValueError, "check_hostname requires server_hostname");
+      return -1;
+    }
+  }
+  self->core = new Core();
+  Py_INCREF(loop);
+  self->loop = loop;
+  if (ssl) {
+    Py_INCREF(ctx);
+    self->ssl_ctx = ctx;
+  }
+  self->ssl = ssl;
+  self->fd = fd;
+  self->alive = true;
+  set_reader(self, true);
+  if (!self->reader_on) {
+    PyErr_SetString(PyExc_RuntimeError, "loop.add_reader failed");
+    close_io(self);
+    return -1;
+  }
+  return 0;
+}
+
+PyObject* conn_new(PyTypeObject* type, PyObject*, PyObject*) {
+  ConnObject* self = reinterpret_cast<ConnObject*>(type->tp_alloc(type, 0));
+  if (!self) return nullptr;
+  self->fd = -1;
+  return reinterpret_cast<PyObject*>(self);
+}
+
+int conn_traverse(ConnObject* self, visitproc visit, void* arg) {
+  Py_VISIT(self->loop);
+  Py_VISIT(self->ssl_ctx);
+  Py_VISIT(self->hs_fut);
+  Py_VISIT(self->fut);
+  Py_VISIT(self->decode);
+  Py_VISIT(self->items);
+  Py_VISIT(self->waiter);
+  Py_VISIT(self->stream_error);
+  return 0;
+}
+
+int conn_clear(ConnObject* self) {
+  Py_CLEAR(self->hs_fut);
+  Py_CLEAR(self->fut);
+  Py_CLEAR(self->decode);
+  Py_CLEAR(self->items);
+  Py_CLEAR(self->waiter);
+  Py_CLEAR(self->stream_error);
+  Py_CLEAR(self->ssl_ctx);
+  Py_CLEAR(self->loop);
+  return 0;
+}
+
+void conn_dealloc(ConnObject* self) {
+  PyObject_GC_UnTrack(self);
+  if (self->weakrefs) PyObject_ClearWeakRefs(reinterpret_cast<PyObject*>(self));
+  // the loop no longer holds our callbacks (they hold a reference to us): just release
+  if (self->ssl) SSL_free(self->ssl);
+  if (self->fd >= 0) ::close(self->fd);
+  conn_clear(self);
+  delete self->core;
+  Py_TYPE(self)->tp_free(reinterpret_cast<PyObject*>(self));
+}
+
+bool check_ready(ConnObject* self) {
+  if (!self->core) {
+    PyErr_SetString(PyExc_RuntimeError, "Conn is not initialised");
+    return false;
+  }
+  return true;
+}
+
+PyObject* new_future(ConnObject* self) {
+  if (!self->loop) {
+    PyErr_SetString(PyExc_RuntimeError, "Conn has no event loop");
+    return nullptr;
+  }
+  return PyObject_CallMethodNoArgs(self->loop, s_create_future);
+}
+
+PyObject* failed_future(ConnObject* self, PyObject* exc) {
+  PyObject* f = new_future(self);
+  if (f && exc) {
+    PyObject* r = PyObject_CallMethodOneArg(f, s_set_exception, exc);
+    Py_XDECREF(r);
+    if (!r) Py_CLEAR(f);
+  }
+  Py_XDECREF(exc);
+  return f;
+}
+
+// handshake() -> Future[None]: the TLS handshake (a plain connection returns a done future)
+PyObject* conn_handshake(ConnObject* self, PyObject*) {
+  if (!check_ready(self)) return nullptr;
+  if (!self->ssl) {
+    PyObject* f = new_future(self);
+    if (f) resolve(f, Py_None);
+    return f;
+  }
+  if (self->fd < 0) return failed_future(self, ssl_error("TLS handshake on a closed connection"));
+  if (self->hs_fut) {
+    Py_INCREF(self->hs_fut);
+    return self->hs_fut;
+  }
+  PyObject* f = new_future(self);
+  if (!f) return nullptr;
+  Py_INCREF(f);
+  self->hs_fut = f;
+  self->hs = kHsRunning;
+  Py_INCREF(self);
+  handshake_step(self);
+  Py_DECREF(self);
+  return f;
+}
+
+// Queue ``data`` and write what the socket takes now.
+bool start_write(ConnObject* self, PyObject* data) {
+  Py_buffer view;
+  if (PyObject_GetBuffer(data, &view, PyBUF_SIMPLE) < 0) return false;
+  Core& c = *self->core;
+  c.wbuf.append(static_cast<const char*>(view.buf), static_cast<size_t>(view.len));
+  PyBuffer_Release(&view);
+  if (!self->writer_on) flush(self);
+  return true;
+}
+
+// send(data) -> Future[(status, body, retry_after)]
+PyObject* conn_send(ConnObject* self, PyObject* data) {
+  if (!check_ready(self)) return nullptr;
+  if (self->mode != kRequest) {
+    PyErr_SetString(PyExc_RuntimeError, "send() on a stream connection");
+    return nullptr;
+  }
+  if (self->fd < 0 || !self->alive)
+    return failed_future(self, conn_failed("connection is closed", true, self->used > 0));
+  if (self->fut) {
+    PyErr_SetString(PyExc_RuntimeError, "a request is already in flight on this connection");
+    return nullptr;
+  }
+  PyObject* f = new_future(self);
+  if (!f) return nullptr;
+  Py_INCREF(f);
+  self->fut = f;
+  self->used += 1;
+  self->got_any = false;
+  Py_INCREF(self);
+  const bool ok = start_write(self, data);
+  Py_DECREF(self);
+  if (!ok) {
+    Py_CLEAR(self->fut);
+    Py_DECREF(f);
+    return nullptr;
+  }
+  return f;
+}
+
+// open_stream(data, decode) -> Future[int status]
+PyObject* conn_open_stream(ConnObject* self, PyObject* args) {
+  PyObject *data, *decode;
+  if (!PyArg_ParseTuple(args, "OO", &data, &decode)) return nullptr;
+  if (!check_ready(self)) return nullptr;
+  if (self->mode != kRequest || self->used) {
+    PyErr_SetString(PyExc_RuntimeError, "open_stream() needs a fresh connection");
+    return nullptr;
+  }
+  if (self->fd < 0 || !self->alive)
+    return failed_future(self, conn_failed("stream closed: connection is closed", true, false));
+  PyObject* items = PyList_New(0);
+  PyObject* f = items ? new_future(self) : nullptr;
+  if (!f) {
+    Py_XDECREF(items);
+    return nullptr;
+  }
+  self->mode = kStream;
+  self->items = items;
+  Py_INCREF(decode);
+  self->decode = decode;
+  Py_INCREF(f);
+  self->fut = f;
+  self->used = 1;
+  Py_INCREF(self);
+  const bool ok = start_write(self, data);
+  Py_DECREF(self);
+  if (!ok) {
+    Py_CLEAR(self->fut);
+    Py_DECREF(f);
+    return nullptr;
+  }
+  return f;
+}
+
+PyObject* conn_on_readable(ConnObject* self, PyObject*) {
+  if (!self->core || self->fd < 0) Py_RETURN_NONE;
+  Py_INCREF(self);  // completing futures may drop the last outside reference
+  if (self->hs == kHsRunning) handshake_step(self);
+  else {
+    if (self->core->wpos < self->core->wbuf.size() && !self->writer_on) flush(self);
+    if (self->fd >= 0) read_ready(self);
+  }
+  Py_DECREF(self);
+  Py_RETURN_NONE;
+}
+
+PyObject* conn_on_writable(ConnObject* self, PyObject*) {
+  if (!self->core || self->fd < 0) Py_RETURN_NONE;
+  Py_INCREF(self);
+  if (self->hs == kHsRunning) handshake_step(self);
+  else flush(self);
+  Py_DECREF(self);
+  Py_RETURN_NONE;
+}
+
+// close(): unregister and close the socket; a pending response or stream head fails like a
+// connection the peer closed
+PyObject* conn_close(ConnObject* self, PyObject*) {
+  if (!self->core) Py_RETURN_NONE;
+  Py_INCREF(self);
+  if (self->fd >= 0) lost(self, "closed");
+  else {
+    self->alive = false;
+    if (self->mode == kStream) {
+      self->stream_done = true;
+      wake(self);
+    }
+  }
+  if (self->hs_fut) {
+    PyObject* f = self->hs_fut;
+    self->hs_fut = nullptr;
+    PyObject* exc = ssl_error("connection closed during the TLS handshake");
+    reject(f, exc);
+    Py_XDECREF(exc);
+    Py_DECREF(f);
+  }
+  Py_DECREF(self);
+  Py_RETURN_NONE;
+}
+
+PyObject* conn_closing(ConnObject* self, PyObject*) { return PyBool_FromLong(self->fd < 0 || !self->alive); }
+
+// take() -> list: every decoded item not taken yet
+PyObject* conn_take(ConnObject* self, PyObject*) {
+  if (!self->items || PyList_GET_SIZE(self->items) == 0) return PyList_New(0);
+  PyObject* fresh = PyList_New(0);
+  if (!fresh) return nullptr;
+  PyObject* out = self->items;
+  self->items = fresh;
+  return out;
+}
+
+// take_one() -> item | None
+PyObject* conn_take_one(ConnObject* self, PyObject*) {
+  if (!self->items || PyList_GET_SIZE(self->items) == 0) Py_RETURN_NONE;
+  PyObject* item = PyList_GET_ITEM(self->items, 0);
+  Py_INCREF(item);
+  if (PySequence_DelItem(self->items, 0) < 0) {
+    Py_DECREF(item);
+    return nullptr;
+  }
+  return item;
+}
+
+// wait() -> Future | None: None when items are ready or the stream has ended
+PyObject* conn_wait(ConnObject* self, PyObject*) {
+  if (!check_ready(self)) return nullptr;
+  if ((self->items && PyList_GET_SIZE(self->items) > 0) || self->stream_done || self->fd < 0) Py_RETURN_NONE;
+  if (self->waiter) {  // a waiter cancelled with its awaiting task is replaced
+    PyObject* d = PyObject_CallMethodNoArgs(self->waiter, s_done);
+    if (!d) return nullptr;
+    const bool done = d == Py_True;
+    Py_DECREF(d);
+    if (done) Py_CLEAR(self->waiter);
+  }
+  if (!self->waiter) {
+    self->waiter = new_future(self);
+    if (!self->waiter) return nullptr;
+  }
+  Py_INCREF(self->waiter);
+  return self->waiter;
+}
+
+PyObject* get_alive(ConnObject* self, void*) { return PyBool_FromLong(self->alive && self->fd >= 0); }
+
+int set_alive(ConnObject* self, PyObject* v, void*) {
+  if (!v) {
+    PyErr_SetString(PyExc_AttributeError, "cannot delete alive");
+    return -1;
+  }
+  const int t = PyObject_IsTrue(v);
+  if (t < 0) return -1;
+  self->alive = t && self->fd >= 0;
+  return 0;
+}
+
+PyObject* get_fut(ConnObject* self, void*) {
+  PyObject* f = self->fut ? self->fut : Py_None;
+  Py_INCREF(f);
+  return f;
+}
+
+PyObject* get_done(ConnObject* self, void*) { return PyBool_FromLong(self->stream_done || self->fd < 0); }
+
+PyObject* get_error(ConnObject* self, void*) {
+  PyObject* e = self->stream_error ? self->stream_error : Py_None;
+  Py_INCREF(e);
+  return e;
+}
+
+PyObject* get_pending(ConnObject* self, void*) {
+  return PyLong_FromSsize_t(self->items ? PyList_GET_SIZE(self->items) : 0);
+}
+
+PyObject* get_tls(ConnObject* self, void*) { return PyBool_FromLong(self->ssl != nullptr); }
+
+PyObject* get_tls_version(ConnObject* self, void*) {
+  if (!self->ssl) Py_RETURN_NONE;
+  return PyUnicode_FromString(SSL_get_version(self->ssl));
+}
+
+PyObject* get_alpn(ConnObject* self, void*) {
+  if (!self->ssl) Py_RETURN_NONE;
+  const unsigned char* p = nullptr;
+  unsigned int n = 0;
+  SSL_get0_alpn_selected(self->ssl, &p, &n);
+  if (!p || !n) Py_RETURN_NONE;
+  return PyUnicode_FromStringAndSize(reinterpret_cast<const char*>(p), n);
+}
+
+PyMethodDef kConnMethods[] = {
+    {"handshake", reinterpret_cast<PyCFunction>(conn_handshake), METH_NOARGS,
+     "handshake() -> Future[None]: run the TLS handshake (plain connections: a done future)"},
+    {"send", reinterpret_cast<PyCFunction>(conn_send), METH_O,
+     "send(data) -> Future[(status, body, retry_after)]: one request/response exchange"},
+    {"open_stream", reinterpret_cast<PyCFunction>(conn_open_stream), METH_VARARGS,
+     "open_stream(data, decode) -> Future[status]: turn the connection into a line stream"},
+    {"take", reinterpret_cast<PyCFunction>(conn_take), METH_NOARGS, "take() -> list of decoded items"},
+    {"take_one", reinterpret_cast<PyCFunction>(conn_take_one), METH_NOARGS, "take_one() -> item or None"},
+    {"wait", reinterpret_cast<PyCFunction>(conn_wait), METH_NOARGS,
+     "wait() -> Future or None (None: items ready or the stream ended)"},
+    {"close", reinterpret_cast<PyCFunction>(conn_close), METH_NOARGS, "close the connection"},
+    {"closing", reinterpret_cast<PyCFunction>(conn_closing), METH_NOARGS, "closed or marked dead"},
+    {"_on_readable", reinterpret_cast<PyCFunction>(conn_on_readable), METH_NOARGS, "loop reader callback"},
+    {"_on_writable", reinterpret_cast<PyCFunction>(conn_on_writable), METH_NOARGS, "loop writer callback"},
+    {nullptr, nullptr, 0, nullptr},
+};
+
+PyGetSetDef kConnGetSet[] = {
+    {"alive", reinterpret_cast<getter>(get_alive), reinterpret_cast<setter>(set_alive),
+     "usable for another request", nullptr},
+    {"fut", reinterpret_cast<getter>(get_fut), nullptr, "the in-flight response future, or None", nullptr},
+    {"done", reinterpret_cast<getter>(get_done), nullptr, "stream mode: the stream has ended", nullptr},
+    {"error", reinterpret_cast<getter>(get_error), nullptr, "stream mode: what ended the stream", nullptr},
+    {"pending", reinterpret_cast<getter>(get_pending), nullptr, "stream mode: items not taken yet", nullptr},
+    {"tls", reinterpret_cast<getter>(get_tls), nullptr, "TLS connection", nullptr},
+    {"tls_version", reinterpret_cast<getter>(get_tls_version), nullptr, "negotiated TLS version", nullptr},
+    {"alpn", reinterpret_cast<getter>(get_alpn), nullptr, "negotiated ALPN protocol", nullptr},
+    {nullptr, nullptr, nullptr, nullptr, nullptr},
+};
+
+PyMemberDef kConnMembers[] = {
+    {"used", T_LONG, offsetof(ConnObject, used), READONLY, "requests sent"},
+    {"fd", T_INT, offsetof(ConnObject, fd), READONLY, "socket file descriptor (-1 once closed)"},
+    {"ssl_gen", T_LONG, offsetof(ConnObject, ssl_gen), 0, "pool bookkeeping: TLS context generation"},
+    {"deadline", T_DOUBLE, offsetof(ConnObject, deadline), 0, "pool bookkeeping: response due (loop time)"},
+    {nullptr, 0, 0, 0, nullptr},
+};
+
+PyTypeObject ConnType = {
+    PyVarObject_HEAD_INIT(nullptr, 0)
+    "_netconn.Conn",                       /* tp_name */
+    sizeof(ConnObject),                    /* tp_basicsize */
+};
+
+// configure(ConnectionFailed, HttpStatusError, SSLError)
+PyObject* configure(PyObject*, PyObject* args) {
+  PyObject *cf, *se, *sslerr;
+  if (!PyArg_ParseTuple(args, "OOO", &cf, &se, &sslerr)) return nullptr;
+  Py_INCREF(cf);
+  Py_INCREF(se);
+  Py_INCREF(sslerr);
+  Py_XSETREF(g_conn_failed, cf);
+  Py_XSETREF(g_status_error, se);
+  Py_XSETREF(g_ssl_error, sslerr);
+  Py_RETURN_NONE;
+}
+
+// ssl_context_supported(ctx) -> bool: can Conn use this ssl.SSLContext natively?
+PyObject* ssl_context_supported(PyObject*, PyObject* ctx) {
+  if (ssl_ctx_of(ctx)) Py_RETURN_TRUE;
+  PyErr_Clear();
+  Py_RETURN_FALSE;
+}
+
+PyMethodDef kMethods[] = {
+    {"configure", configure, METH_VARARGS, "configure(ConnectionFailed, HttpStatusError, SSLError)"},
+    {"ssl_context_supported", ssl_context_supported, METH_O,
+     "ssl_context_supported(ctx) -> bool: the SSLContext's SSL_CTX can be used natively"},
+    {nullptr, nullptr, 0, nullptr},
+};
+
+PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_netconn", "Native HTTP/1.1 client connection for asyncio.", -1,
+                       kMethods, nullptr, nullptr, nullptr, nullptr};
+
+bool intern(PyObject** slot, const char* s) {
+  *slot = PyUnicode_InternFromString(s);
+  return *slot != nullptr;
+}
+
+}  // namespace
+
+PyMODINIT_FUNC PyInit__netconn(void) {
+  if (!intern(&s_create_future, "create_future") || !intern(&s_set_result, "set_result") ||
+      !intern(&s_set_exception, "set_exception") || !intern(&s_done, "done") ||
+      !intern(&s_add_reader, "add_reader") || !intern(&s_remove_reader, "remove_reader") ||
+      !intern(&s_add_writer, "add_writer") || !intern(&s_remove_writer, "remove_writer") ||
+      !intern(&s_on_readable, "_on_readable") || !intern(&s_on_writable, "_on_writable") ||
+      !intern(&s_options, "options") || !intern(&s_verify_mode, "verify_mode"))
+    return nullptr;
+  ConnType.tp_dealloc = reinterpret_cast<destructor>(conn_dealloc);
+  ConnType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_BASETYPE | Py_TPFLAGS_HAVE_GC;
+  ConnType.tp_doc = "One HTTP/1.1 client connection driven by an asyncio loop.";
+  ConnType.tp_traverse = reinterpret_cast<traverseproc>(conn_traverse);
+  ConnType.tp_clear = reinterpret_cast<inquiry>(conn_clear);
+  ConnType.tp_weaklistoffset = offsetof(ConnObject, weakrefs);
+  ConnType.tp_methods = kConnMethods;
+  ConnType.tp_members = kConnMembers;
+  ConnType.tp_getset = kConnGetSet;
+  ConnType.tp_init = reinterpret_cast<initproc>(conn_init);
+  ConnType.tp_new = conn_new;
+  if (PyType_Ready(&ConnType) < 0) return nullptr;
+  PyObject* m = PyModule_Create(&kModule);
+  if (!m) return nullptr;
+  Py_INCREF(&ConnType);
+  if (PyModule_AddObject(m, "Conn", reinterpret_cast<PyObject*>(&ConnType)) < 0) {
+    Py_DECREF(&ConnType);
+    Py_DECREF(m);
+    return nullptr;
+  }
+  return m;
+}

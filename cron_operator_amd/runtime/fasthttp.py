@@ -24,6 +24,14 @@ Watch streams (:meth:`HttpPool.open_stream`) get a dedicated connection whose
 protocol de-chunks the body, splits it into lines and decodes each line as it
 arrives, so an informer receives ready-made events in batches (no per-line
 stream-reader round trips).
+
+With the ``_netconn`` extension (``ops/csrc/netconn.cpp``) the connections
+themselves are native: the pool dials the socket and hands it over, and the
+loop calls the native connection straight from its selector -- receive,
+framing, de-chunking, line splitting and TLS (OpenSSL, configured by the same
+``ssl.SSLContext``) run in C++.  The asyncio protocols below remain for http
+proxies, for builds without the extension (``CRON_OPERATOR_NATIVE_HTTP=python``),
+and as the behavioural oracle of the native path's tests.
 """
 from __future__ import annotations
 
@@ -216,6 +224,13 @@ class _Conn(asyncio.Protocol):
         self.transport.write(data)
         return self.fut
 
+    def close(self) -> None:
+        if self.transport is not None:
+            self.transport.close()
+
+    def closing(self) -> bool:
+        return self.transport is None or self.transport.is_closing()
+
 
 class HttpStatusError(Exception):
     """A streaming request was answered with an error status."""
@@ -382,6 +397,39 @@ class Stream:
         self._c.close()
 
 
+class NativeStream(Stream):
+    """:class:`Stream` over a native connection in stream mode (``_netconn.Conn``)."""
+
+    def __init__(self, conn) -> None:  # noqa: D107 - no _StreamConn here
+        self._n = conn
+
+    async def __anext__(self):
+        n = self._n
+        while not n.pending:
+            if n.done:
+                raise StopAsyncIteration
+            w = n.wait()
+            if w is not None:
+                await w
+        return n.take_one()
+
+    def take_ready(self) -> list:
+        return self._n.take()
+
+    async def wait_ready(self) -> bool:
+        n = self._n
+        while not n.pending:
+            if n.done:
+                return False
+            w = n.wait()
+            if w is not None:
+                await w
+        return True
+
+    def close(self) -> None:
+        self._n.close()
+
+
 # TCP keepalive on every connection (Go's net.Dialer probes after 30 s idle): a peer that
 # vanished without a FIN -- node loss, a dropped NAT entry -- is detected in about a minute
 # instead of never on a long-lived watch connection
@@ -394,6 +442,10 @@ def enable_keepalive(transport: Optional[asyncio.BaseTransport]) -> bool:
     sock = transport.get_extra_info("socket") if transport is not None else None
     if sock is None:
         return False
+    return keepalive_socket(sock)
+
+
+def keepalive_socket(sock) -> bool:
     try:
         sock.setsockopt(_socket.SOL_SOCKET, _socket.SO_KEEPALIVE, 1)
         for opt, val in (("TCP_KEEPIDLE", KEEPALIVE_IDLE), ("TCP_KEEPINTVL", KEEPALIVE_INTERVAL),
@@ -409,6 +461,10 @@ def _expire(fut: asyncio.Future) -> None:
     if not fut.done():
         fut.set_exception(asyncio.TimeoutError())
 
+
+# default of HttpPool(native=None): None picks the native connections whenever they can serve
+# the pool; False keeps the asyncio protocols (tests run the pool both ways)
+DEFAULT_NATIVE: Optional[bool] = None
 
 # request deadlines are checked by one sweep timer per pool instead of a timer per request
 # (a TimerHandle, a heap push and a cancel on every call); the sweep runs at most this often,
@@ -443,7 +499,9 @@ class HttpPool:
 
     def __init__(self, base_url: str, ssl_context: Optional[_ssl.SSLContext] = None,
                  headers: Optional[Dict[str, str]] = None, max_idle: int = 64, timeout: float = 60.0,
-                 server_hostname: Optional[str] = None, proxy: str = ""):
+                 server_hostname: Optional[str] = None, proxy: str = "", native: Optional[bool] = None):
+        """``native``: use ``_netconn`` connections (None: whenever the extension is built, no
+        proxy is configured and it can drive the TLS context; True: required)."""
         u = urlsplit(base_url)
         self.scheme = u.scheme or "http"
         self.host = u.hostname or "127.0.0.1"
@@ -477,6 +535,22 @@ class HttpPool:
         self._busy: set = set()   # connections with a request in flight (deadline sweep)
         self._sweeper: Optional[asyncio.TimerHandle] = None
         self._sweep_every = min(SWEEP_INTERVAL, max(0.01, timeout / 4))
+        self._want_native = native if native is not None else DEFAULT_NATIVE
+        self.native = False
+        self._pick_native()
+
+    def _pick_native(self) -> None:
+        from ..ops import netconn_native
+
+        want = self._want_native
+        mod = netconn_native.load() if want is not False else None
+        ok = mod is not None and self._proxy is None and \
+            (self.ssl is None or mod.ssl_context_supported(self.ssl))
+        if want and not ok:
+            raise RuntimeError("native HTTP connections unavailable for this pool "
+                               f"(extension {'missing' if mod is None else 'loaded'}, proxy={bool(self._proxy)})")
+        self._netconn = mod if ok else None
+        self.native = ok
 
     def set_headers(self, headers: Optional[Dict[str, str]]) -> None:
         """Replace the headers sent with every request (e.g. a rotated ``Authorization``)."""
@@ -492,10 +566,9 @@ class HttpPool:
         connections made with the old one are closed, busy ones when they are given back."""
         self.ssl = ctx
         self._ssl_gen += 1
+        self._pick_native()
         while self._idle:
-            c = self._idle.pop()
-            if c.transport is not None:
-                c.transport.close()
+            self._idle.pop().close()
 
     async def _open(self, factory):
         """A connected protocol from ``factory``: direct, to an http proxy (plain servers), or
@@ -531,15 +604,67 @@ class HttpPool:
 
     async def _connect(self) -> _Conn:
         gen = self._ssl_gen
-        proto = await self._open(_Conn)
+        if self._netconn is not None:
+            proto = await asyncio.wait_for(self._open_native(), self.timeout)
+        else:
+            proto = await self._open(_Conn)
         proto.ssl_gen = gen
         self.connects += 1
         return proto
 
+    async def _dial(self) -> _socket.socket:
+        """A connected non-blocking TCP socket to the server (addresses tried in order, like
+        Go's dialer without a fallback delay); TCP_NODELAY and keepalive probes on."""
+        loop = asyncio.get_running_loop()
+        infos = await loop.getaddrinfo(self.host, self.port, type=_socket.SOCK_STREAM)
+        err: Optional[BaseException] = None
+        for family, type_, proto, _, addr in infos:
+            sock = _socket.socket(family, type_, proto)
+            try:
+                sock.setblocking(False)
+                await loop.sock_connect(sock, addr)
+            except OSError as e:
+                sock.close()
+                err = e
+                continue
+            except BaseException:
+                sock.close()
+                raise
+            try:
+                sock.setsockopt(_socket.IPPROTO_TCP, _socket.TCP_NODELAY, 1)
+            except OSError:
+                pass
+            keepalive_socket(sock)
+            return sock
+        raise err if err is not None else OSError(f"no address for {self.host}:{self.port}")
+
+    async def _open_native(self):
+        """A native connection (``_netconn.Conn``), TLS handshake done."""
+        loop = asyncio.get_running_loop()
+        sock = await self._dial()
+        ctx = self.ssl
+        try:
+            if ctx is None:
+                conn = self._netconn.Conn(loop, sock.fileno())
+            else:
+                conn = self._netconn.Conn(loop, sock.fileno(), ctx, self.server_hostname or self.host,
+                                          ctx.check_hostname, ctx.hostname_checks_common_name)
+        except BaseException:
+            sock.close()
+            raise
+        sock.detach()  # the connection owns the descriptor now
+        if ctx is not None:
+            try:
+                await conn.handshake()
+            except BaseException:
+                conn.close()
+                raise
+        return conn
+
     def _take_idle(self) -> Optional[_Conn]:
         while self._idle:
             c = self._idle.pop()
-            if c.alive and c.transport is not None and not c.transport.is_closing():
+            if c.alive and not c.closing():
                 return c
         return None
 
@@ -547,8 +672,8 @@ class HttpPool:
         if c.alive and not self._closed and len(self._idle) < self.max_idle and c.fut is None \
                 and c.ssl_gen == self._ssl_gen:
             self._idle.append(c)
-        elif c.transport is not None:
-            c.transport.close()
+        else:
+            c.close()
 
     async def request(self, method: str, path: str, body: Optional[bytes] = None,
                       content_type: str = "application/json") -> Tuple[int, bytes]:
@@ -580,18 +705,13 @@ class HttpPool:
                 status, raw, retry_after = await fut
             except ConnectionFailed as e:
                 conn.alive = False
+                conn.close()
                 if attempt == 0 and e.no_response and e.reused:
                     continue  # stale keep-alive connection: retry once on a fresh one
                 raise
-            except asyncio.TimeoutError:
+            except BaseException:  # deadline (TimeoutError), cancellation, anything else
                 conn.alive = False
-                if conn.transport is not None:
-                    conn.transport.close()
-                raise
-            except BaseException:
-                conn.alive = False
-                if conn.transport is not None:
-                    conn.transport.close()
+                conn.close()
                 raise
             finally:
                 self._busy.discard(conn)
@@ -616,6 +736,16 @@ class HttpPool:
         """GET ``path`` on a dedicated connection and stream its body line by line
         (``decode`` turns each non-empty line into an item).  Raises
         :class:`HttpStatusError` for an error status."""
+        if self._netconn is not None:
+            nc = await asyncio.wait_for(self._open_native(), self.timeout)
+            try:
+                head = nc.open_stream(f"GET {self._target}{path} HTTP/1.1\r\n{self._fixed}Accept: {accept}\r\n\r\n"
+                                      .encode("latin-1"), decode)
+                await asyncio.wait_for(head, self.timeout)
+            except BaseException:
+                nc.close()
+                raise
+            return NativeStream(nc)
         conn = await self._open(lambda: _StreamConn(decode))
         conn.head = asyncio.get_running_loop().create_future()
         assert conn.transport is not None
@@ -634,9 +764,7 @@ class HttpPool:
             self._sweeper.cancel()
             self._sweeper = None
         while self._idle:
-            c = self._idle.pop()
-            if c.transport is not None:
-                c.transport.close()
+            self._idle.pop().close()
 
 
 def encode_query(params: Dict[str, str]) -> str:
@@ -647,4 +775,4 @@ def encode_query(params: Dict[str, str]) -> str:
     return "?" + urlencode(params)
 
 
-__all__: List[str] = ["HttpPool", "ConnectionFailed", "HttpStatusError", "Stream", "encode_query"]
+__all__: List[str] = ["HttpPool", "ConnectionFailed", "HttpStatusError", "Stream", "NativeStream", "encode_query"]

@@ -1,23 +1,31 @@
 #!/bin/bash
-# One gpurun call: paired A/B of operator CPU per fire on the box.  ab_base/ holds an older
-# tree (git archive <rev> | tar -x -C ab_base; git-ignored, shipped with the snapshot);
-# both trees build their extensions and run the 1-process 1000-Cron bench alternately.
-#   TAG=r2g ROUNDS=4 bash scripts/gpu_ab.sh
+# One gpurun call: paired A/B of the 1-process 1000-Cron bench on the box.  ab_base/ holds an
+# older tree (git archive <rev> | tar -x -C ab_base; git-ignored, shipped with the snapshot).
+# ARMS lists the arms run in turn each round: "base", "head", or "head:VAR=value" (head with an
+# environment override, e.g. head:CRON_OPERATOR_NATIVE_HTTP=python).
+#   TAG=r3b ROUNDS=4 ARMS="base head:CRON_OPERATOR_NATIVE_HTTP=python head" bash scripts/gpu_ab.sh
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 TAG=${TAG:-ab}
 ROUNDS=${ROUNDS:-4}
+ARMS=${ARMS:-base head}
 OUT=$PWD/gpurun_out/$TAG
 mkdir -p "$OUT"
 for d in ab_base .; do
+  [ "$d" = ab_base ] && [[ " $ARMS " != *" base "* ]] && continue
   (cd "$d" && timeout -k 10 300 python -m cron_operator_amd.ops.build > "$OUT/build_$(basename "$(realpath "$d")").log" 2>&1) || exit $?
 done
 for i in $(seq "$ROUNDS"); do
-  for d in ab_base .; do
-    name=$([ "$d" = "." ] && echo head || echo base)
-    (cd "$d" && PYTHONPATH=$PWD timeout -k 10 300 python bench.py --shards ${SHARDS:-1} --steps 10 --warmup 3 --baseline none \
-        > "$OUT/${name}_$i.log" 2>&1)
+  for arm in $ARMS; do
+    d=.; envs=()
+    case "$arm" in
+      base) d=ab_base ;;
+      head:*) envs=("${arm#head:}") ;;
+    esac
+    name=$(echo "$arm" | tr ':=' '__')
+    (cd "$d" && env "${envs[@]}" PYTHONPATH=$PWD timeout -k 10 300 python bench.py --shards ${SHARDS:-1} --steps 10 \
+        --warmup 3 --baseline none > "$OUT/${name}_$i.log" 2>&1)
     rc=$?; [ $rc -eq 0 ] || { echo "$name round $i rc=$rc"; exit $rc; }
     python - "$OUT/${name}_$i.log" "$name" "$i" <<'PY'
 import json, sys

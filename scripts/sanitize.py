@@ -1,12 +1,14 @@
 #!/usr/bin/env python3
 """Host sanitizer run of the native extensions (ASan + UBSan).
 
-Builds ``_cron_engine``, ``_fastjson`` and ``_httpcodec`` from ``ops/csrc`` with
+Builds ``_cron_engine``, ``_fastjson``, ``_httpcodec`` and ``_netconn`` from ``ops/csrc`` with
 ``-fsanitize=address,undefined`` into a scratch directory, re-executes itself with
 the sanitizer runtimes preloaded (CPython itself is not instrumented), and drives
 every entry point with mutated and generated inputs:
 
 * ``_httpcodec``: byte-level mutations of valid requests/responses (fuzz);
+* ``_netconn``: mutated responses and watch streams delivered over a socketpair in random
+  splits to native connections on a live event loop, closed by either side at random;
 * ``_fastjson``: random JSON trees through loads/dumpb/dumpb_shared/deepcopy/
   json_equal/create_merge_patch, plus malformed documents;
 * ``_cron_engine``: random and malformed cron specs through parse/next/missed.
@@ -25,7 +27,9 @@ import tempfile
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "cron_operator_amd", "ops", "csrc")
-EXTS = {"_cron_engine": "cron_engine.cpp", "_fastjson": "fastjson.cpp", "_httpcodec": "httpcodec.cpp"}
+EXTS = {"_cron_engine": "cron_engine.cpp", "_fastjson": "fastjson.cpp", "_httpcodec": "httpcodec.cpp",
+        "_netconn": "netconn.cpp"}
+LIBS = {"_netconn": ["-lssl", "-lcrypto"]}
 
 
 def build(out_dir: str) -> None:
@@ -34,7 +38,7 @@ def build(out_dir: str) -> None:
     for name, src in EXTS.items():
         cmd = ["g++", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
                "-fno-sanitize-recover=undefined", "-std=c++17", "-shared", "-fPIC", f"-I{inc}",
-               os.path.join(CSRC, src), "-o", os.path.join(out_dir, name + suffix)]
+               os.path.join(CSRC, src), "-o", os.path.join(out_dir, name + suffix), *LIBS.get(name, [])]
         subprocess.run(cmd, check=True)
 
 
@@ -122,7 +126,75 @@ def drive(scratch: str, iters: int) -> None:
             h.missed(t, 0, t2, 0, 0)
             t = t2
         ce.bulk_next([h, h], [t, t + 1], [0, 5], 0)
-    print(f"sanitize ok: {iters} http, {iters // 4} json, {iters // 4} cron cases", flush=True)
+    net = drive_netconn(rng, iters // 20)
+    print(f"sanitize ok: {iters} http, {iters // 4} json, {iters // 4} cron, {net} connection cases", flush=True)
+
+
+def drive_netconn(rng: random.Random, cases: int) -> int:
+    import asyncio
+    import socket
+    import ssl
+
+    import _netconn as ncm  # noqa: E402
+
+    class ConnectionFailed(Exception):
+        def __init__(self, msg, no_response, reused):
+            super().__init__(msg)
+
+    class HttpStatusError(Exception):
+        def __init__(self, status, body):
+            super().__init__(status)
+
+    ncm.configure(ConnectionFailed, HttpStatusError, ssl.SSLError)
+    seeds = [b"HTTP/1.1 200 OK\r\nContent-Length: 5\r\n\r\nhello",
+             b"HTTP/1.1 100 Continue\r\n\r\nHTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n"
+             b"4;x\r\nWiki\r\n0\r\nT: 1\r\n\r\n",
+             b"HTTP/1.0 200 OK\r\n\r\nuntil close",
+             b"HTTP/1.1 410 Gone\r\nTransfer-Encoding: chunked\r\n\r\n5\r\n{\"a\":\r\n0\r\n\r\n",
+             b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n"
+             b"10\r\n{\"type\":\"A\"}\n{\"b\r\n3\r\n\":1\r\n2\r\n}\n\r\n0\r\n\r\n"]
+
+    def decode(line: bytes):
+        if line.startswith(b"!"):
+            raise ValueError("bad line")
+        return line
+
+    async def run() -> None:
+        loop = asyncio.get_running_loop()
+        for _ in range(cases):
+            a, b = socket.socketpair()
+            a.setblocking(False)
+            b.setblocking(False)
+            c = ncm.Conn(loop, a.detach())
+            stream = rng.random() < 0.5
+            fut = c.open_stream(b"GET /w HTTP/1.1\r\n\r\n", decode) if stream else \
+                c.send(b"GET / HTTP/1.1\r\n\r\n" * rng.randint(1, 3))
+            data = _mutate(rng, rng.choice(seeds))
+            pos = 0
+            while pos < len(data):
+                n = rng.randint(1, 48)
+                try:
+                    b.send(data[pos:pos + n])
+                except OSError:
+                    break
+                pos += n
+                await asyncio.sleep(0)
+                if stream:
+                    c.take()
+                    w = c.wait()
+                    if w is not None and rng.random() < 0.2:
+                        w.cancel()
+            if rng.random() < 0.5:
+                b.close()
+                await asyncio.sleep(0)
+                await asyncio.sleep(0)
+            c.close()
+            b.close()
+            if fut.done() and not fut.cancelled():
+                fut.exception()
+
+    asyncio.run(run())
+    return cases
 
 
 def main() -> int:

@@ -5,7 +5,22 @@ import asyncio
 
 import pytest
 
+from cron_operator_amd.runtime import fasthttp
 from cron_operator_amd.runtime.fasthttp import ConnectionFailed, HttpPool, encode_query
+
+
+@pytest.fixture(autouse=True, params=["native", "python"])
+def pool_mode(request, monkeypatch):
+    """Every test runs on the native connections (``_netconn``) and on the asyncio protocols."""
+    if request.param == "native":
+        from cron_operator_amd.ops import netconn_native
+
+        if netconn_native.load() is None:
+            pytest.skip("_netconn extension not built")
+        monkeypatch.setattr(fasthttp, "DEFAULT_NATIVE", True)
+    else:
+        monkeypatch.setattr(fasthttp, "DEFAULT_NATIVE", False)
+    return request.param
 
 
 async def serve(replies, record=None):

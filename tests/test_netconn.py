@@ -1,0 +1,344 @@
+"""The native HTTP/1.1 connection (``ops/csrc/netconn.cpp``) where it differs from the asyncio
+protocols it replaces: TLS through OpenSSL on the caller's ``ssl.SSLContext`` (verification,
+hostname checks, SNI), bodies larger than a socket buffer in both directions, and the stream
+mode's end-of-stream, decode-error and cancellation paths.  ``tests/test_fasthttp.py`` runs the
+shared behaviour (keep-alive, chunking, retries, deadlines, streams) on both implementations."""
+from __future__ import annotations
+
+import asyncio
+import json
+import ssl
+
+import pytest
+
+from cron_operator_amd.ops import netconn_native
+from cron_operator_amd.runtime.fasthttp import ConnectionFailed, HttpPool, HttpStatusError, NativeStream
+
+nc = netconn_native.load()
+pytestmark = pytest.mark.skipif(nc is None, reason="_netconn extension not built")
+
+
+async def _server(handler, ssl_context=None):
+    srv = await asyncio.start_server(handler, "127.0.0.1", 0, ssl=ssl_context)
+    return srv, srv.sockets[0].getsockname()[1]
+
+
+async def _read_request(reader):
+    head = await reader.readuntil(b"\r\n\r\n")
+    clen = 0
+    for line in head.split(b"\r\n"):
+        if line.lower().startswith(b"content-length:"):
+            clen = int(line.split(b":")[1])
+    body = await reader.readexactly(clen) if clen else b""
+    return head, body
+
+
+@pytest.fixture(scope="module")
+def certs(tmp_path_factory):
+    from cron_operator_amd.runtime.servers import self_signed_cert
+
+    d = tmp_path_factory.mktemp("certs")
+    cert, key = self_signed_cert(str(d), host="localhost")
+    (d / "other").mkdir()
+    other_cert, _ = self_signed_cert(str(d / "other"), host="localhost")
+    return cert, key, other_cert
+
+
+def _server_ctx(cert, key):
+    ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+    ctx.load_cert_chain(cert, key)
+    return ctx
+
+
+async def _echo_tls_server(cert, key):
+    async def handle(reader, writer):
+        try:
+            while True:
+                head, body = await _read_request(reader)
+                payload = json.dumps({"path": head.split(b" ")[1].decode(), "n": len(body)}).encode()
+                writer.write(b"HTTP/1.1 200 OK\r\nContent-Length: %d\r\n\r\n" % len(payload) + payload)
+                await writer.drain()
+        except (asyncio.IncompleteReadError, ConnectionResetError, ssl.SSLError):
+            writer.close()
+
+    return await _server(handle, _server_ctx(cert, key))
+
+
+def test_ssl_context_layout_is_recognised():
+    ctx = ssl.create_default_context()
+    assert nc.ssl_context_supported(ctx)
+    ctx.check_hostname = False
+    ctx.verify_mode = ssl.CERT_NONE
+    assert nc.ssl_context_supported(ctx)
+    assert not nc.ssl_context_supported(object())
+
+
+async def test_tls_verified_against_ca_with_hostname(certs):
+    cert, key, _ = certs
+    srv, port = await _echo_tls_server(cert, key)
+    ctx = ssl.create_default_context(cafile=cert)
+    pool = HttpPool(f"https://127.0.0.1:{port}", ssl_context=ctx, server_hostname="localhost", native=True)
+    try:
+        st, raw = await pool.request("POST", "/tls", b"x" * 1000)
+        assert st == 200 and json.loads(raw) == {"path": "/tls", "n": 1000}
+        st, raw = await pool.request("GET", "/again")
+        assert json.loads(raw)["path"] == "/again" and pool.connects == 1  # kept alive over TLS
+        conn = pool._idle[0]
+        assert conn.tls and conn.tls_version.startswith("TLS")
+    finally:
+        await pool.close()
+        srv.close()
+
+
+async def test_tls_rejects_wrong_hostname_and_untrusted_ca(certs):
+    cert, key, other = certs
+    srv, port = await _echo_tls_server(cert, key)
+    try:
+        # the certificate is for "localhost"
+        bad_host = HttpPool(f"https://127.0.0.1:{port}", ssl_context=ssl.create_default_context(cafile=cert),
+                            server_hostname="not-localhost", native=True)
+        with pytest.raises(ssl.SSLError, match="verify"):
+            await bad_host.request("GET", "/")
+        await bad_host.close()
+        # a CA that did not sign it
+        untrusted = HttpPool(f"https://127.0.0.1:{port}", ssl_context=ssl.create_default_context(cafile=other),
+                             server_hostname="localhost", native=True)
+        with pytest.raises(ssl.SSLError, match="verify"):
+            await untrusted.request("GET", "/")
+        await untrusted.close()
+        # insecure-skip-tls-verify: no verification at all
+        ctx = ssl.create_default_context()
+        ctx.check_hostname = False
+        ctx.verify_mode = ssl.CERT_NONE
+        insecure = HttpPool(f"https://127.0.0.1:{port}", ssl_context=ctx, native=True)
+        assert (await insecure.request("GET", "/ok"))[0] == 200
+        await insecure.close()
+    finally:
+        srv.close()
+
+
+async def test_large_bodies_both_ways():
+    """A request body far larger than the socket send buffer (the native writer waits for
+    writability) and a response body delivered in many reads, Content-Length and chunked."""
+    big = bytes(range(256)) * (16 * 1024)  # 4 MiB
+
+    async def handle(reader, writer):
+        try:
+            while True:
+                head, body = await _read_request(reader)
+                await asyncio.sleep(0.05)  # let the client's send buffer fill up
+                if b"/chunked" in head:
+                    writer.write(b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n")
+                    for i in range(0, len(big), 100_000):
+                        c = big[i:i + 100_000]
+                        writer.write(b"%x\r\n" % len(c) + c + b"\r\n")
+                        await writer.drain()
+                    writer.write(b"0\r\n\r\n")
+                else:
+                    writer.write(b"HTTP/1.1 200 OK\r\nContent-Length: %d\r\n\r\n" % len(body) + body)
+                await writer.drain()
+        except (asyncio.IncompleteReadError, ConnectionResetError):
+            writer.close()
+
+    srv, port = await _server(handle)
+    pool = HttpPool(f"http://127.0.0.1:{port}", native=True)
+    try:
+        st, raw = await pool.request("POST", "/echo", big)
+        assert st == 200 and raw == big
+        st, raw = await pool.request("GET", "/chunked")
+        assert st == 200 and raw == big
+        assert pool.connects == 1
+    finally:
+        await pool.close()
+        srv.close()
+
+
+async def test_interim_response_and_retry_after():
+    async def handle(reader, writer):
+        await _read_request(reader)
+        writer.write(b"HTTP/1.1 100 Continue\r\n\r\nHTTP/1.1 429 Too Many Requests\r\nRetry-After: 3\r\n"
+                     b"Content-Length: 2\r\n\r\n{}")
+        await writer.drain()
+        writer.close()
+
+    srv, port = await _server(handle)
+    pool = HttpPool(f"http://127.0.0.1:{port}", native=True)
+    try:
+        assert await pool.request_full("GET", "/") == (429, b"{}", 3)
+    finally:
+        await pool.close()
+        srv.close()
+
+
+async def test_malformed_response_fails_the_request():
+    async def handle(reader, writer):
+        await _read_request(reader)
+        writer.write(b"HTTP/1.1 200 OK\r\nContent-Length: nope\r\n\r\n")
+        await writer.drain()
+
+    srv, port = await _server(handle)
+    pool = HttpPool(f"http://127.0.0.1:{port}", native=True)
+    try:
+        with pytest.raises(ConnectionFailed, match="bad HTTP response"):
+            await pool.request("GET", "/")
+        assert not pool._idle
+    finally:
+        await pool.close()
+        srv.close()
+
+
+def _chunk(b: bytes) -> bytes:
+    return b"%x\r\n" % len(b) + b + b"\r\n"
+
+
+async def test_stream_terminal_chunk_ends_iteration_and_wait():
+    async def handle(reader, writer):
+        await reader.readuntil(b"\r\n\r\n")
+        writer.write(b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n")
+        writer.write(_chunk(b'{"a":1}\n{"a":2}\n'))
+        await writer.drain()
+        await asyncio.sleep(0.05)
+        writer.write(_chunk(b'{"a":3}\n') + b"0\r\n\r\n")
+        await writer.drain()
+        await asyncio.sleep(1)  # the connection stays open: the terminal chunk alone ends the stream
+
+    srv, port = await _server(handle)
+    pool = HttpPool(f"http://127.0.0.1:{port}", native=True)
+    try:
+        st = await pool.open_stream("/w", json.loads)
+        assert isinstance(st, NativeStream)
+        got = []
+        while await asyncio.wait_for(st.wait_ready(), 2):
+            got.extend(st.take_ready())
+        assert got == [{"a": 1}, {"a": 2}, {"a": 3}]
+        st.close()
+    finally:
+        await pool.close()
+        srv.close()
+
+
+async def test_stream_decode_error_ends_the_stream():
+    async def handle(reader, writer):
+        await reader.readuntil(b"\r\n\r\n")
+        writer.write(b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n" +
+                     _chunk(b'{"ok":1}\nnot json\n{"x":2}\n'))
+        await writer.drain()
+        await asyncio.sleep(1)
+
+    srv, port = await _server(handle)
+    pool = HttpPool(f"http://127.0.0.1:{port}", native=True)
+    try:
+        st = await pool.open_stream("/w", json.loads)
+        got = [x async for x in st]
+        assert got == [{"ok": 1}]
+        assert isinstance(st._n.error, ValueError) and st._n.done
+    finally:
+        await pool.close()
+        srv.close()
+
+
+async def test_stream_error_status_chunked_body():
+    body = b'{"kind":"Status","code":403,"reason":"Forbidden"}'
+
+    async def handle(reader, writer):
+        await reader.readuntil(b"\r\n\r\n")
+        writer.write(b"HTTP/1.1 403 Forbidden\r\nTransfer-Encoding: chunked\r\n\r\n" + _chunk(body[:10]) +
+                     _chunk(body[10:]) + b"0\r\n\r\n")
+        await writer.drain()
+
+    srv, port = await _server(handle)
+    pool = HttpPool(f"http://127.0.0.1:{port}", native=True)
+    try:
+        with pytest.raises(HttpStatusError) as ei:
+            await pool.open_stream("/w", json.loads)
+        assert ei.value.status == 403 and ei.value.body == body
+    finally:
+        await pool.close()
+        srv.close()
+
+
+async def test_cancelled_wait_does_not_poison_the_next_one():
+    gate = asyncio.Event()
+
+    async def handle(reader, writer):
+        await reader.readuntil(b"\r\n\r\n")
+        writer.write(b"HTTP/1.1 200 OK\r\nTransfer-Encoding: chunked\r\n\r\n")
+        await writer.drain()
+        await gate.wait()
+        writer.write(_chunk(b'{"late":true}\n'))
+        await writer.drain()
+        await asyncio.sleep(1)
+
+    srv, port = await _server(handle)
+    pool = HttpPool(f"http://127.0.0.1:{port}", native=True)
+    try:
+        st = await pool.open_stream("/w", json.loads)
+        t = asyncio.ensure_future(st.wait_ready())
+        await asyncio.sleep(0.05)
+        t.cancel()
+        with pytest.raises(asyncio.CancelledError):
+            await t
+        gate.set()
+        assert await asyncio.wait_for(st.wait_ready(), 2)
+        assert st.take_ready() == [{"late": True}]
+        st.close()
+        assert st._n.done and not await st.wait_ready()
+    finally:
+        await pool.close()
+        srv.close()
+
+
+async def test_closed_connection_fails_fast_and_close_fails_inflight():
+    async def silent(reader, writer):
+        await asyncio.sleep(2)
+
+    srv, port = await _server(silent)
+    pool = HttpPool(f"http://127.0.0.1:{port}", native=True)
+    try:
+        conn = await pool._connect()
+        fut = conn.send(b"GET / HTTP/1.1\r\nHost: x\r\n\r\n")
+        conn.close()
+        with pytest.raises(ConnectionFailed) as ei:
+            await fut
+        assert ei.value.no_response
+        with pytest.raises(ConnectionFailed):
+            await conn.send(b"GET / HTTP/1.1\r\n\r\n")
+        assert conn.closing() and conn.fd == -1
+    finally:
+        await pool.close()
+        srv.close()
+
+
+async def test_watch_and_requests_over_tls_against_fake_apiserver(certs):
+    """The operator's client over native TLS end to end: CREATE, PATCH and a WATCH stream."""
+    from cron_operator_amd.api.v1alpha1 import CRON_GVR, new_cron
+    from cron_operator_amd.apiserver.http import APIServerApp
+    from cron_operator_amd.runtime.client import Client
+    from cron_operator_amd.runtime.http import HttpTransport
+    from cron_operator_amd.runtime.kubeconfig import RestConfig
+    from cron_operator_amd.testing.env import TestEnv
+
+    cert, key, _ = certs
+    env = TestEnv()
+    app = APIServerApp(env.server)
+    port = await app.start("127.0.0.1", 0, ssl_context=_server_ctx(cert, key))
+    with open(cert, "rb") as fh:
+        ca = fh.read()
+    tr = HttpTransport(RestConfig(host=f"https://127.0.0.1:{port}", ca_data=ca, tls_server_name="localhost"))
+    client = Client(tr, qps=-1)
+    try:
+        obj = new_cron("tls", "default", "@daily", {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob"}).to_dict()
+        created = await client.create(CRON_GVR, obj, "default")
+        assert tr._fast_pool().native
+        w = await client.watch(CRON_GVR, "default", resource_version=created["metadata"]["resourceVersion"])
+        for i in range(20):
+            await client.patch(CRON_GVR, "default", "tls", {"metadata": {"labels": {"i": str(i)}}})
+        seen = []
+        while len(seen) < 20:
+            et, ev = await asyncio.wait_for(w.__anext__(), 5)
+            seen.append(ev["metadata"]["labels"]["i"])
+        assert seen == [str(i) for i in range(20)]
+        w.stop()
+    finally:
+        await client.close()
+        await app.stop()

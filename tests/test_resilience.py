@@ -285,9 +285,15 @@ async def test_http_watch_carries_timeout_and_survives_a_silent_connection():
             if seen_params and inf._watch is not None:
                 break
         assert seen_params and 300 <= int(seen_params[0]["timeoutSeconds"]) < 600
-        stream = inf._watch._s._c  # the dedicated watch connection
-        sock = stream.transport.get_extra_info("socket")
-        assert sock.getsockopt(socket.SOL_SOCKET, socket.SO_KEEPALIVE) == 1
+        st = inf._watch._s  # the dedicated watch connection: native (_netconn) or asyncio protocol
+        if hasattr(st, "_n"):
+            import os
+
+            with socket.socket(fileno=os.dup(st._n.fd)) as sock:
+                assert sock.getsockopt(socket.SOL_SOCKET, socket.SO_KEEPALIVE) == 1
+        else:
+            sock = st._c.transport.get_extra_info("socket")
+            assert sock.getsockopt(socket.SOL_SOCKET, socket.SO_KEEPALIVE) == 1
         assert env.server.stall_watches("configmaps") == 1
         env.server.create(CM, NS, {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "late"}})
         await asyncio.sleep(0.1)
