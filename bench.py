@@ -129,6 +129,9 @@ def main() -> int:
                     help="how shards split the watch traffic (controller/sharding.py)")
     ap.add_argument("--apiserver-latency", choices=["none", "etcd"], default="none",
                     help="server-side per-verb latency model of the fake apiserver (harness LATENCY_PROFILES)")
+    ap.add_argument("--tls", action="store_true",
+                    help="the fake apiserver serves HTTPS and the operator verifies it against its CA, as "
+                         "against a real cluster (every operator connection is TLS)")
     ap.add_argument("--baseline", choices=["measure", "recorded", "none"], default="measure",
                     help="vs_baseline denominator: 'measure' runs the reference algorithm (--mode reference, "
                          "one operator process, same Crons) in this same invocation after the timed run; "
@@ -165,7 +168,8 @@ def main() -> int:
     cfg = BenchConfig(n_crons=a.crons, steps=a.steps, warmup=a.warmup, history_limit=a.history_limit,
                       mode=a.mode, transport=a.transport, qps=a.qps, burst=a.burst, workers=a.workers,
                       namespace=f"bench-r{rank}", shards=a.shards if a.transport == "http" else 1,
-                      shard_routing=a.shard_routing, apiserver_latency=a.apiserver_latency)
+                      shard_routing=a.shard_routing, apiserver_latency=a.apiserver_latency, tls=a.tls)
+
     def on_step(k: int, dt: float, timed: bool) -> None:
         # bracket the K timed steps with barriers so every rank times the same window: the
         # harness starts its clock right after step `warmup` returns and stops it after the
@@ -194,7 +198,7 @@ def main() -> int:
             scfg = BenchConfig(n_crons=a.crons, steps=a.single_steps, warmup=a.single_warmup,
                                history_limit=a.history_limit, mode=a.mode, transport=a.transport, qps=a.qps,
                                burst=a.burst, workers=a.workers, namespace=f"bench-1p-r{rank}", shards=1,
-                               apiserver_latency=a.apiserver_latency)
+                               apiserver_latency=a.apiserver_latency, tls=a.tls)
             _barrier(dist)
             sres = run_sync(scfg)
             _barrier(dist)
@@ -210,7 +214,8 @@ def main() -> int:
     if a.baseline == "measure":
         bcfg = BenchConfig(n_crons=a.crons, steps=a.baseline_steps, warmup=a.baseline_warmup,
                            history_limit=a.history_limit, mode="reference", transport=a.transport, qps=a.qps,
-                           burst=a.burst, workers=a.workers, namespace=f"bench-ref-r{rank}", shards=1)
+                           burst=a.burst, workers=a.workers, namespace=f"bench-ref-r{rank}", shards=1,
+                           tls=a.tls)
         _barrier(dist)
         bres = run_sync(bcfg)
         _barrier(dist)
@@ -257,7 +262,7 @@ def main() -> int:
                        "operator_shards": cfg.shards,
                        "shard_routing": cfg.shard_routing if cfg.shards > 1 else None,
                        "apiserver_latency": cfg.apiserver_latency,
-                       "qps": cfg.qps},
+                       "tls": cfg.tls, "qps": cfg.qps},
             "p50_schedule_to_create_ms": round(max(r["p50"] for r in allr), 2),
             "p99_schedule_to_create_ms": round(max(r["p99"] for r in allr), 2),
             "raw_reconciles_per_s": round(sum(r["reconciles"] for r in allr) / t_max, 2),

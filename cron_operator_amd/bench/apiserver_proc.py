@@ -22,14 +22,26 @@ async def main() -> None:
     ap.add_argument("--start-ns", type=int, required=True)
     ap.add_argument("--port", type=int, default=0)
     ap.add_argument("--gc", action="store_true")
+    ap.add_argument("--tls-dir", default="",
+                    help="serve HTTPS with a self-signed certificate for CN=localhost written here "
+                         "(tls.crt doubles as the client's CA)")
     a = ap.parse_args()
     server = APIServer(FakeClock(a.start_ns), gc=a.gc)
     server.install_crd(crd())
     for c in kubeflow_crds():
         server.install_crd(c)
     app = APIServerApp(server)
-    port = await app.start("127.0.0.1", a.port)
-    print(f"LISTENING http://127.0.0.1:{port}", flush=True)
+    ctx = None
+    if a.tls_dir:
+        import ssl
+
+        from ..runtime.servers import self_signed_cert
+
+        cert, key = self_signed_cert(a.tls_dir, host="localhost")
+        ctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+        ctx.load_cert_chain(cert, key)
+    port = await app.start("127.0.0.1", a.port, ssl_context=ctx)
+    print(f"LISTENING {'https' if ctx else 'http'}://127.0.0.1:{port}", flush=True)
     stop = asyncio.Event()
     loop = asyncio.get_running_loop()
     for sig in (signal.SIGTERM, signal.SIGINT):

@@ -105,6 +105,9 @@ class BenchConfig:
     shard_routing: str = "labels"
     # per-verb server-side latency (LATENCY_PROFILES name), applied after setup; needs transport="http"
     apiserver_latency: str = "none"
+    # the fake apiserver serves HTTPS (self-signed CN=localhost) and every operator connection
+    # verifies it against that CA, as against a real cluster's apiserver; needs transport="http"
+    tls: bool = False
 
 
 @dataclass
@@ -148,16 +151,43 @@ def _pct(xs: List[float], p: float) -> float:
 class _RemoteServer:
     """The fake apiserver in a child process, driven over HTTP."""
 
-    def __init__(self):
+    def __init__(self, tls: bool = False):
         self.proc: Optional[subprocess.Popen] = None
         self.url = ""
+        self.tls_dir = ""
+        self.ca_file = ""
+        if tls:
+            import tempfile
+
+            self.tls_dir = tempfile.mkdtemp(prefix="bench-tls-")
+            self.ca_file = os.path.join(self.tls_dir, "tls.crt")
+
+    def rest_config(self):
+        """The operator's RestConfig for this server (CA-verified against host name localhost under TLS)."""
+        from ..runtime.kubeconfig import RestConfig
+
+        if not self.tls_dir:
+            return RestConfig(host=self.url)
+        with open(self.ca_file, "rb") as fh:
+            return RestConfig(host=self.url, ca_data=fh.read(), tls_server_name="localhost")
+
+    def ssl_context(self):
+        """The harness's own admin connection: the CA, without the host-name check (it dials the IP)."""
+        import ssl
+
+        if not self.tls_dir:
+            return None
+        ctx = ssl.create_default_context(cafile=self.ca_file)
+        ctx.check_hostname = False
+        return ctx
 
     def start(self) -> str:
         env = dict(os.environ)
         root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
         env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+        extra = ["--tls-dir", self.tls_dir] if self.tls_dir else []
         self.proc = subprocess.Popen([sys.executable, "-m", "cron_operator_amd.bench.apiserver_proc",
-                                      "--start-ns", str(T0_NS)],
+                                      "--start-ns", str(T0_NS)] + extra,
                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env, text=True)
         assert self.proc.stdout is not None
         line = self.proc.stdout.readline()
@@ -183,6 +213,10 @@ class _RemoteServer:
             except subprocess.TimeoutExpired:
                 self.proc.kill()
                 self.proc.wait()
+        if self.tls_dir:
+            import shutil
+
+            shutil.rmtree(self.tls_dir, ignore_errors=True)
 
 
 class SettleTracker:
@@ -269,6 +303,8 @@ async def run(cfg: BenchConfig, on_step=None) -> BenchResult:
     from ..utils.logging import new_from_options, set_logger
 
     set_logger(new_from_options(encoder="json", level=cfg.log_level, stream=open(os.devnull, "w")))
+    if cfg.tls and cfg.transport != "http":
+        raise ValueError("tls needs transport='http'")
     clock = FakeClock(T0_NS)
     remote: Optional[_RemoteServer] = None
     server = None
@@ -287,12 +323,12 @@ async def run(cfg: BenchConfig, on_step=None) -> BenchResult:
         import aiohttp
 
         from ..runtime.http import HttpTransport
-        from ..runtime.kubeconfig import RestConfig
 
-        remote = _RemoteServer()
-        url = remote.start()
-        transport = HttpTransport(RestConfig(host=url), pool_size=max(16, cfg.workers * 2))
-        admin = aiohttp.ClientSession()
+        remote = _RemoteServer(tls=cfg.tls)
+        remote.start()
+        transport = HttpTransport(remote.rest_config(), pool_size=max(16, cfg.workers * 2))
+        sslctx = remote.ssl_context()
+        admin = aiohttp.ClientSession(connector=aiohttp.TCPConnector(ssl=sslctx) if sslctx else None)
 
     async def set_time(ns: int) -> None:
         clock.set(ns)
@@ -536,6 +572,7 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
                 "--start-ns", str(T0_NS + NANOS // 2), "--workers", str(cfg.workers),
                 "--history-limit", str(cfg.history_limit), "--qps", str(cfg.qps), "--burst", str(cfg.burst),
                 "--mode", cfg.mode, "--routing", cfg.shard_routing,
+                *(["--ca-file", remote.ca_file] if remote.ca_file else []),
                 env=env, stdin=asyncio.subprocess.PIPE, stdout=asyncio.subprocess.PIPE,
                 stderr=asyncio.subprocess.PIPE, limit=1 << 24)
             shards.append(_Shard(p))

@@ -42,6 +42,7 @@ async def main() -> int:
     ap.add_argument("--burst", type=int, default=50)
     ap.add_argument("--mode", default="optimized")
     ap.add_argument("--routing", default="hash", choices=["hash", "labels"])
+    ap.add_argument("--ca-file", default="", help="https --url: verify the apiserver against this CA (as localhost)")
     a = ap.parse_args()
 
     from ..api.v1alpha1 import CRON_GVR
@@ -57,8 +58,11 @@ async def main() -> int:
 
     set_logger(new_from_options(encoder="json", level="error", stream=open(os.devnull, "w")))
     clock = FakeClock(a.start_ns)
-    client = Client(HttpTransport(RestConfig(host=a.url), pool_size=max(16, a.workers * 2)), qps=a.qps,
-                    burst=a.burst)
+    rc = RestConfig(host=a.url)
+    if a.ca_file:
+        with open(a.ca_file, "rb") as fh:
+            rc = RestConfig(host=a.url, ca_data=fh.read(), tls_server_name="localhost")
+    client = Client(HttpTransport(rc, pool_size=max(16, a.workers * 2)), qps=a.qps, burst=a.burst)
     opts = ReconcilerOptions.reference() if a.mode == "reference" else ReconcilerOptions()
     mgr = Manager(client, ManagerOptions(clock=clock, max_concurrent_reconciles=a.workers,
                                          health_probe_bind_address="0", metrics_bind_address="0",

@@ -59,6 +59,18 @@ def test_recorded_baseline_option():
     assert d["baseline_value"] == 80.72 and d["baseline_source"].startswith("recorded")
 
 
+def test_tls_apiserver_option():
+    """``--tls``: the fake apiserver serves HTTPS and every operator connection -- one process and
+    the shard processes -- verifies it against its CA; the run completes with the same request model."""
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "1", "--warmup", "1", "--crons", "12", "--shards", "2",
+                        "--tls", "--baseline", "none"], cwd=ROOT, env=_env(), capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _json_line(r.stdout)
+    assert d["config"]["tls"] is True and d["value"] > 0 and d["single_process_value"] > 0
+    assert d["api_requests_per_fire"] == 4.0
+
+
 def test_gpus_without_launcher_spawns_ranks():
     """``--gpus 2`` with no WORLD_SIZE: bench.py starts both ranks itself; one line, 2 ranks' work."""
     env = _env()
