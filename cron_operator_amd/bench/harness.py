@@ -108,6 +108,8 @@ class BenchConfig:
     # the fake apiserver serves HTTPS (self-signed CN=localhost) and every operator connection
     # verifies it against that CA, as against a real cluster's apiserver; needs transport="http"
     tls: bool = False
+    # the operator's apiserver connections: native (_netconn) or asyncio's transports (A/B rows)
+    native_http: bool = True
 
 
 @dataclass
@@ -293,6 +295,23 @@ def _cpu_times(remote: Optional["_RemoteServer"]) -> "tuple[float, float]":
 
 
 async def run(cfg: BenchConfig, on_step=None) -> BenchResult:
+    from ..utils.logging import new_from_options, set_logger
+
+    set_logger(new_from_options(encoder="json", level=cfg.log_level, stream=open(os.devnull, "w")))
+    if cfg.tls and cfg.transport != "http":
+        raise ValueError("tls needs transport='http'")
+    from ..runtime import fasthttp
+
+    saved_native = fasthttp.DEFAULT_NATIVE
+    if not cfg.native_http:
+        fasthttp.DEFAULT_NATIVE = False
+    try:
+        return await _run(cfg, on_step)
+    finally:
+        fasthttp.DEFAULT_NATIVE = saved_native
+
+
+async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
     from ..controller.reconciler import ReconcilerOptions
     from ..controller.setup import setup_with_manager
     from ..cron.engine import default_engine
@@ -300,11 +319,7 @@ async def run(cfg: BenchConfig, on_step=None) -> BenchResult:
     from ..runtime.manager import Manager, ManagerOptions
     from ..utils import gctune, jsonutil
     from ..utils.clock import FakeClock
-    from ..utils.logging import new_from_options, set_logger
 
-    set_logger(new_from_options(encoder="json", level=cfg.log_level, stream=open(os.devnull, "w")))
-    if cfg.tls and cfg.transport != "http":
-        raise ValueError("tls needs transport='http'")
     clock = FakeClock(T0_NS)
     remote: Optional[_RemoteServer] = None
     server = None
@@ -563,6 +578,8 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
     env = dict(os.environ)
     root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    if not cfg.native_http:
+        env["CRON_OPERATOR_NATIVE_HTTP"] = "python"
     shards: List[_Shard] = []
     try:
         for i in range(cfg.shards):

@@ -14,7 +14,13 @@ latency too.  Each row here is one harness run:
 ``etcd-latency``
     unthrottled, with the harness's ``etcd`` latency model on every verb (an
     assumed model, see ``LATENCY_PROFILES``): throughput is bounded by workers x
-    round trips per fire.
+    round trips per fire;
+``tls``
+    the apiserver serves HTTPS and the operator verifies it against its CA (every
+    real cluster), unthrottled: the ``asyncio-tls`` row is the same run on asyncio's
+    transports instead of the native connections (``_netconn``);
+``tls+etcd``
+    TLS and the ``etcd`` latency model together -- the closest shape to a cluster.
 
 ``optimized`` rows are this operator, ``reference`` rows the reference algorithm
 (``ReconcilerOptions.reference()``), both with 10 workers on one replica unless the
@@ -31,16 +37,23 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-# name, mode, shards, crons, qps, burst, latency profile, steps, warmup
+# name, mode, shards, crons, qps, burst, latency profile, steps, warmup, tls, native connections
 ROWS = [
-    ("unthrottled", "reference", 1, 1000, -1.0, 50, "none", 3, 1),
-    ("unthrottled", "optimized", 1, 1000, -1.0, 50, "none", 5, 2),
-    ("chart-defaults", "reference", 1, 100, 30.0, 50, "none", 2, 1),
-    ("chart-defaults", "optimized", 1, 100, 30.0, 50, "none", 2, 1),
-    ("chart-defaults", "optimized", 3, 300, 30.0, 50, "none", 2, 1),
-    ("etcd-latency", "reference", 1, 1000, -1.0, 50, "etcd", 3, 1),
-    ("etcd-latency", "optimized", 1, 1000, -1.0, 50, "etcd", 5, 2),
-    ("etcd-latency", "optimized", 3, 1000, -1.0, 50, "etcd", 5, 2),
+    ("unthrottled", "reference", 1, 1000, -1.0, 50, "none", 3, 1, False, True),
+    ("unthrottled", "optimized", 1, 1000, -1.0, 50, "none", 5, 2, False, True),
+    ("chart-defaults", "reference", 1, 100, 30.0, 50, "none", 2, 1, False, True),
+    ("chart-defaults", "optimized", 1, 100, 30.0, 50, "none", 2, 1, False, True),
+    ("chart-defaults", "optimized", 3, 300, 30.0, 50, "none", 2, 1, False, True),
+    ("etcd-latency", "reference", 1, 1000, -1.0, 50, "etcd", 3, 1, False, True),
+    ("etcd-latency", "optimized", 1, 1000, -1.0, 50, "etcd", 5, 2, False, True),
+    ("etcd-latency", "optimized", 3, 1000, -1.0, 50, "etcd", 5, 2, False, True),
+    ("tls", "reference", 1, 1000, -1.0, 50, "none", 3, 1, True, True),
+    ("tls", "optimized", 1, 1000, -1.0, 50, "none", 5, 2, True, True),
+    ("asyncio-tls", "optimized", 1, 1000, -1.0, 50, "none", 5, 2, True, False),
+    ("tls", "optimized", 3, 1000, -1.0, 50, "none", 5, 2, True, True),
+    ("tls+etcd", "reference", 1, 1000, -1.0, 50, "etcd", 3, 1, True, True),
+    ("tls+etcd", "optimized", 1, 1000, -1.0, 50, "etcd", 5, 2, True, True),
+    ("tls+etcd", "optimized", 3, 1000, -1.0, 50, "etcd", 5, 2, True, True),
 ]
 
 
@@ -55,29 +68,35 @@ def main() -> int:
 
     only = set(filter(None, a.only.split(",")))
     rows = []
-    for name, mode, shards, n, qps, burst, lat, steps, warmup in ROWS:
+    for name, mode, shards, n, qps, burst, lat, steps, warmup, tls, native in ROWS:
         if only and name not in only:
             continue
         n = max(1, int(n * a.scale))
         t0 = time.perf_counter()
         r = run_sync(BenchConfig(n_crons=n, steps=steps, warmup=warmup, mode=mode, qps=qps, burst=burst,
-                                 shards=shards, apiserver_latency=lat))
+                                 shards=shards, apiserver_latency=lat, tls=tls, native_http=native))
+        fires = n * steps
         row = {"config": name, "mode": mode, "shards": shards, "n_crons": n, "qps": qps, "burst": burst,
-               "apiserver_latency": lat, "steps": steps, "cron_reconciles_per_s": r.cron_reconciles_per_s,
+               "apiserver_latency": lat, "tls": tls, "native_http": native, "steps": steps,
+               "cron_reconciles_per_s": r.cron_reconciles_per_s,
                "p50_ms": r.p50_latency_ms, "p99_ms": r.p99_latency_ms, "ms_per_step": r.ms_per_step,
                "api_requests_per_fire": r.api_requests_per_fire, "reconciles_per_fire": r.reconciles_per_fire,
+               "operator_cpu_ms_per_fire": r.cpu_s_operator * 1000 / fires,
+               "apiserver_busy_frac": r.cpu_s_apiserver / r.elapsed_s,
                "wall_s": round(time.perf_counter() - t0, 1)}
         rows.append(row)
         print(f"{name:>14} {mode:>9} x{shards} n={n:>5}: {r.cron_reconciles_per_s:9.1f} cron-reconciles/s  "
-              f"p50 {r.p50_latency_ms:8.1f} ms  {r.api_requests_per_fire:.1f} req/fire", flush=True)
+              f"p50 {r.p50_latency_ms:8.1f} ms  {r.api_requests_per_fire:.1f} req/fire  "
+              f"operator {row['operator_cpu_ms_per_fire']:.3f} ms CPU/fire", flush=True)
     print()
     print("| config | algorithm | replicas | Crons | cron-reconciles/s | p50 tick→create ms | p99 ms "
-          "| API req/fire | reconciles/fire |")
-    print("|---|---|---:|---:|---:|---:|---:|---:|---:|")
+          "| API req/fire | reconciles/fire | operator CPU ms/fire | apiserver busy |")
+    print("|---|---|---:|---:|---:|---:|---:|---:|---:|---:|---:|")
     for x in rows:
         print(f"| {x['config']} | {x['mode']} | {x['shards']} | {x['n_crons']} | "
               f"{x['cron_reconciles_per_s']:.1f} | {x['p50_ms']:.1f} | {x['p99_ms']:.1f} | "
-              f"{x['api_requests_per_fire']:.1f} | {x['reconciles_per_fire']:.1f} |")
+              f"{x['api_requests_per_fire']:.1f} | {x['reconciles_per_fire']:.1f} | "
+              f"{x['operator_cpu_ms_per_fire']:.3f} | {x['apiserver_busy_frac']:.2f} |")
     if a.out:
         with open(a.out, "w") as fh:
             json.dump({"rows": rows}, fh, indent=1)
