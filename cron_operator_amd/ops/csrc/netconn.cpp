@@ -339,7 +339,9 @@ void finish_response(ConnObject* s, const char* b, size_t n) {
     Py_XDECREF(ra);
     PyErr_Clear();
   }
-  const bool close_after = c.close_after;
+  // a response that overtook the rest of its request (an early error status): the unsent
+  // bytes would precede the next request on the wire, so this connection is not reused
+  const bool close_after = c.close_after || c.wpos < c.wbuf.size();
   reset_response(c);
   if (close_after) close_io(s);
   PyObject* fut = s->fut;
@@ -692,7 +694,9 @@ void read_ready(ConnObject* s) {
       // plain sockets: a short read drained the socket (the loop is level-triggered, so more
       // data wakes us again); TLS: read until OpenSSL needs the socket, it may hold records
       if (!s->ssl && static_cast<size_t>(n) < sizeof g_rbuf) break;
-      if (total >= kMaxReadPerWake) break;
+      // past the per-wake bound, stop only if the rest is still in the kernel (the loop wakes us
+      // again); records OpenSSL already pulled off the socket would not wake anyone
+      if (total >= kMaxReadPerWake && (!s->ssl || !SSL_has_pending(s->ssl))) break;
       continue;
     }
     if (n == 0) eof = true;

@@ -342,3 +342,25 @@ async def test_watch_and_requests_over_tls_against_fake_apiserver(certs):
     finally:
         await client.close()
         await app.stop()
+
+
+async def test_early_response_to_unsent_body_retires_the_connection():
+    """A server may answer before reading the whole request (413 on a huge body).  The unsent
+    tail must never precede the next request on that connection: it is not reused."""
+    big = b"x" * (8 << 20)
+
+    async def handle(reader, writer):
+        await reader.readuntil(b"\r\n\r\n")
+        writer.write(b"HTTP/1.1 413 Request Entity Too Large\r\nContent-Length: 0\r\n\r\n")
+        await writer.drain()
+        await asyncio.sleep(1)  # never reads the body
+
+    srv, port = await _server(handle)
+    pool = HttpPool(f"http://127.0.0.1:{port}", native=True)
+    try:
+        st, raw = await asyncio.wait_for(pool.request("POST", "/big", big), 5)
+        assert st == 413 and raw == b""
+        assert not pool._idle
+    finally:
+        await pool.close()
+        srv.close()
