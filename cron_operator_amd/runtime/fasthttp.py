@@ -1,6 +1,6 @@
 """Lean HTTP/1.1 keep-alive client for the request/response verbs.
 
-Profiling the operator during the 1000-Cron bench (``profiles/operator_cprofile_r1b.txt``)
+Profiling the operator during the 1000-Cron bench (round 1)
 put aiohttp's client machinery (request/response objects, header multidicts,
 timers, stream readers) at roughly a third of the operator's CPU per API call.
 A Kubernetes client needs far less: one request in flight per connection, a
