@@ -310,9 +310,11 @@ class Cron:
         return d
 
     @staticmethod
-    def from_dict(d: Dict[str, Any], status: Optional[CronStatus] = None) -> "Cron":
-        """``status``: an already parsed equivalent of ``d["status"]`` (the caller vouches for it)."""
-        return Cron(metadata=jsonutil.deepcopy(d.get("metadata") or {}), spec=CronSpec.from_dict(d.get("spec")),
+    def from_dict(d: Dict[str, Any], status: Optional[CronStatus] = None, spec: Optional[CronSpec] = None) -> "Cron":
+        """``status`` / ``spec``: already parsed equivalents of ``d["status"]`` / ``d["spec"]`` (the
+        caller vouches for them; a shared ``spec`` is never mutated -- it is replaced)."""
+        return Cron(metadata=jsonutil.deepcopy(d.get("metadata") or {}),
+                    spec=spec if spec is not None else CronSpec.from_dict(d.get("spec")),
                     status=status if status is not None else CronStatus.from_dict(d.get("status")),
                     api_version=d.get("apiVersion") or CRON_GVK.api_version, kind=d.get("kind") or CRON_GVK.kind)
 

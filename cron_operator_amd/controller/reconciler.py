@@ -64,6 +64,7 @@ Time comes from the injected clock (the reference calls ``time.Now()``,
 from __future__ import annotations
 
 import asyncio
+import dataclasses
 import functools
 import json
 import operator
@@ -368,12 +369,16 @@ class CronReconciler(Reconciler):
         # key -> (resourceVersion, status dict) of the Cron version is_own_write() proved to hold
         # exactly that status: the next reconcile then trusts its memo without comparing again
         self._own_rv: Dict[str, Tuple[str, Dict[str, Any]]] = {}
+        # key -> (spec dict of the cached Cron, its parsed CronSpec): the Cron informer's codec hands
+        # back the same spec object while the spec bytes do not change, so it is parsed once
+        self._spec_memo: Dict[str, Tuple[Dict[str, Any], Any]] = {}
         # tick bookkeeping for latency: key -> (tick unix ns, wall perf_counter when it became due)
         self.latency_observer: Optional[Callable[[str, GoTime, Dict[str, Any]], None]] = None
 
     def forget_cron(self, key: str) -> None:
         """Drop the per-Cron memos of a Cron that is gone (``namespace/name``)."""
         self._parsed_status.pop(key, None)
+        self._spec_memo.pop(key, None)
         self.own_writes.pop(key, None)
         self._own_rv.pop(key, None)
         self.expect.forget(key)
@@ -396,6 +401,7 @@ class CronReconciler(Reconciler):
                 self.forget_cron(f"{req.namespace}/{req.name}")
                 return Result()
             parsed = None
+            spec = None
             if self.opts.classification_cache:
                 key = f"{req.namespace}/{req.name}"
                 memo = self._parsed_status.get(key)
@@ -405,7 +411,13 @@ class CronReconciler(Reconciler):
                             and ov[0] == (old_obj.get("metadata") or {}).get("resourceVersion")) \
                             or jsonutil.json_equal(old_obj.get("status") or {}, memo[0]):
                         parsed = memo[1].snapshot()
-            cron = Cron.from_dict(old_obj, status=parsed)
+                sd = old_obj.get("spec")
+                sm = self._spec_memo.get(key)
+                if sm is not None and sm[0] is sd:
+                    spec = sm[1]
+            cron = Cron.from_dict(old_obj, status=parsed, spec=spec)
+            if spec is None and self.opts.classification_cache and type(old_obj.get("spec")) is dict:
+                self._spec_memo[key] = (old_obj["spec"], cron.spec)
             old_status = cron.status.snapshot()
 
             result = Result()
@@ -990,7 +1002,8 @@ class CronReconciler(Reconciler):
             self.recorder.event(cron.to_dict(), Normal, "OverridePolicy",
                                 "metadata.name has been specified in workload template, override cron concurrency "
                                 "policy as Forbidden")
-            cron.spec.concurrency_policy = ConcurrentPolicyForbid
+            # replaced, not mutated: the parsed spec may be the memo shared across reconciles
+            cron.spec = dataclasses.replace(cron.spec, concurrency_policy=ConcurrentPolicyForbid)
         m["namespace"] = cron.namespace
         labels = m.get("labels")
         if not isinstance(labels, dict):

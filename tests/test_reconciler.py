@@ -439,6 +439,38 @@ async def test_b18_named_template_overrides_policy_in_memory():
     assert rig.cron()["spec"]["concurrencyPolicy"] == "Allow"  # never persisted
 
 
+async def test_parsed_spec_memo_follows_the_spec_object_and_is_never_mutated():
+    """With a Cron informer the parsed CronSpec is reused while the cached spec object is the
+    same (the wire codec hands back one object per spec bytes); a new spec object is parsed
+    again; the named-template override replaces the spec instead of mutating the memo."""
+    rig = Rig(ReconcilerOptions())
+    tmpl = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob", "metadata": {"name": "fixed"}}
+    await rig.create(workload=tmpl)
+    rig.set_status(lastScheduleTime=rig.clock.now(UTC).add(-2 * MINUTE).utc().rfc3339())
+
+    class Inf:
+        obj = rig.cron()
+
+        def get(self, ns, name, copy=True):
+            return self.obj
+
+    inf = Inf()
+    rig.r.cron_informer = inf
+    key = f"{NS}/{NAME}"
+    await rig.reconcile()
+    spec1 = rig.r._spec_memo[key][1]
+    assert spec1.concurrency_policy == "Allow"  # the override went to a copy
+    inf.obj = rig.cron()
+    inf.obj["spec"] = rig.r._spec_memo[key][0]  # same spec object, newer status
+    await rig.reconcile()
+    assert rig.r._spec_memo[key][1] is spec1 and spec1.concurrency_policy == "Allow"
+    inf.obj = dict(inf.obj, spec=dict(inf.obj["spec"], suspend=True))
+    await rig.reconcile()
+    assert rig.r._spec_memo[key][1] is not spec1 and rig.r._spec_memo[key][1].suspend is True
+    rig.r.forget_cron(key)
+    assert key not in rig.r._spec_memo
+
+
 @pytest.mark.parametrize("mode", MODES)
 async def test_b18_job_name_uses_next_run(mode):
     rig = Rig(MODES[mode])
