@@ -165,7 +165,9 @@ class CronStatus:
         if self.active:
             d["active"] = [a.to_dict() for a in self.active]
         if self.history:
-            d["history"] = [h.to_dict(shared) for h in self.history]
+            # shared: an entry's cached JSON (never empty) without a call per entry
+            d["history"] = [h._json or h.to_dict(True) for h in self.history] if shared else \
+                [h.to_dict() for h in self.history]
         if self.last_schedule_time is not None:
             d["lastScheduleTime"] = time_to_json(self.last_schedule_time)
         return d

@@ -947,15 +947,15 @@ class CronReconciler(Reconciler):
                     if now is None:
                         now = self.clock.now(LOCAL)
                     entry.finished = now
+                elif c.finished_at is not None:
+                    entry.finished = c.finished_at
+                    if info is not None:  # fully determined by this child version
+                        info.history_entry = entry
                 else:
-                    if previous is None:
+                    if previous is None:  # only a child without a completion time needs it
                         previous = {h.uid: h for h in cron.status.history if h.uid}
                     prev = previous.get(entry.uid)
-                    if c.finished_at is not None:
-                        entry.finished = c.finished_at
-                        if info is not None:  # fully determined by this child version
-                            info.history_entry = entry
-                    elif prev is not None and prev.finished is not None:
+                    if prev is not None and prev.finished is not None:
                         entry.finished = prev.finished
                     else:
                         # first observation: second precision so it survives the JSON round trip

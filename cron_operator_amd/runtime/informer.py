@@ -177,6 +177,8 @@ class Informer:
         for name, fn in self.indexers.items():
             idx = self.indices[name]
             if old is not None and obj is not None:
+                if fn is namespace_index:
+                    continue  # the store key carries the namespace: an update cannot move it
                 ov = fn(old)
                 nv = fn(obj)
                 if ov == nv:
