@@ -97,6 +97,74 @@ def _time(v: Any, path: str) -> Optional[GoTime]:
 
 
 def job_status_from_unstructured(status: Dict[str, Any]) -> JobStatus:
+    """The converted status; a status of well-typed JSON (what decoded objects almost always
+    are) takes the fast path, anything else the strict one, which raises the precise error."""
+    js = _fast_job_status(status)
+    return js if js is not None else _strict_job_status(status)
+
+
+_TIME_FIELDS = ("startTime", "completionTime", "lastReconcileTime")
+
+
+def _fast_time(v: Any) -> Any:
+    """A parsed time, None for absent/empty, or ``_BAD`` when the strict path must decide."""
+    if v is None or v == "":
+        return None
+    if v.__class__ is not str:
+        return _BAD
+    try:
+        return parse_rfc3339(v)
+    except ValueError:
+        return _BAD
+
+
+_BAD = object()
+
+
+def _fast_job_status(status: Dict[str, Any]) -> Optional[JobStatus]:
+    """:func:`_strict_job_status` for exactly-typed input without building error paths;
+    None when any field needs the strict path (wrong type, unparsable time, float counts)."""
+    js = JobStatus()
+    conds = status.get("conditions")
+    if conds is not None:
+        if conds.__class__ is not list:
+            return None
+        out = js.conditions
+        for c in conds:
+            if c.__class__ is not dict:
+                return None
+            t, st, r, m = c.get("type"), c.get("status"), c.get("reason"), c.get("message")
+            if (t is not None and t.__class__ is not str) or (st is not None and st.__class__ is not str) or \
+                    (r is not None and r.__class__ is not str) or (m is not None and m.__class__ is not str):
+                return None
+            lu, lt = _fast_time(c.get("lastUpdateTime")), _fast_time(c.get("lastTransitionTime"))
+            if lu is _BAD or lt is _BAD:
+                return None
+            out.append(JobCondition(t or "", st or "", r or "", m or "", lu, lt))
+    rs = status.get("replicaStatuses")
+    if rs is not None:
+        if rs.__class__ is not dict:
+            return None
+        for k, v in rs.items():
+            if v is None:
+                continue
+            if v.__class__ is not dict:
+                return None
+            a, su, f, sel, ls = v.get("active"), v.get("succeeded"), v.get("failed"), v.get("selector"), \
+                v.get("labelSelector")
+            if (a is not None and a.__class__ is not int) or (su is not None and su.__class__ is not int) or \
+                    (f is not None and f.__class__ is not int) or (sel is not None and sel.__class__ is not str) or \
+                    (ls is not None and ls.__class__ is not dict):
+                return None
+            js.replica_statuses[k] = ReplicaStatus(a or 0, su or 0, f or 0, sel or "", ls)
+    times = [_fast_time(status.get(f)) for f in _TIME_FIELDS]
+    if times[0] is _BAD or times[1] is _BAD or times[2] is _BAD:
+        return None
+    js.start_time, js.completion_time, js.last_reconcile_time = times
+    return js
+
+
+def _strict_job_status(status: Dict[str, Any]) -> JobStatus:
     js = JobStatus()
     conds = status.get("conditions")
     if conds is not None:
