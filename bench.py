@@ -58,27 +58,43 @@ if ROOT not in sys.path:
 RECORDED_BASELINE_VALUE = 80.72
 
 
-def _free_port() -> int:
-    import socket
-
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def _spawn_ranks(n: int) -> int:
-    """``--gpus N`` without a launcher: start N rank processes of this script (gloo rendezvous on
-    127.0.0.1) and exit with the worst exit code.  Nothing here touches the GPU, so child
-    processes are started, never exec'd.  Only rank 0 prints the JSON line."""
+    """``--gpus N`` without a launcher: start N rank processes of this script and exit with the
+    worst exit code.  The ranks rendezvous through a file (no port to race other jobs for); a
+    rank that fails ends the others instead of leaving them waiting at a barrier.  Nothing here
+    touches the GPU, so child processes are started, never exec'd.  Only rank 0 prints the
+    JSON line."""
     import subprocess
+    import tempfile
 
-    port = _free_port()
+    rdzv = tempfile.mktemp(prefix="bench-rdzv-")  # created by the first rank's FileStore
     procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rcs = [p.wait() for p in procs]
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                       MASTER_ADDR="127.0.0.1", BENCH_RDZV_FILE=rdzv)
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+        rcs = [None] * n
+        while any(rc is None for rc in rcs):
+            for i, p in enumerate(procs):
+                if rcs[i] is None:
+                    rcs[i] = p.poll()
+            if any(rc not in (None, 0) for rc in rcs):
+                for p in procs:
+                    if p.poll() is None:
+                        p.terminate()
+                rcs = [p.wait() if rc is None else rc for p, rc in zip(procs, rcs)]
+                break
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        try:
+            os.unlink(rdzv)
+        except OSError:
+            pass
     bad = [rc for rc in rcs if rc != 0]
     return bad[0] if bad else 0
 
@@ -87,10 +103,19 @@ def _dist():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     if ws <= 1:
         return None, 0, 1
+    from datetime import timedelta
+
     import torch.distributed as dist  # only multi-rank runs pay for importing torch
 
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    dist.init_process_group("gloo")
+    rdzv = os.environ.get("BENCH_RDZV_FILE")
+    # a rank that never arrives fails the others after this long instead of hanging them
+    timeout = timedelta(seconds=float(os.environ.get("BENCH_RDZV_TIMEOUT_S", "900")))
+    if rdzv:  # ranks spawned by _spawn_ranks
+        dist.init_process_group("gloo", init_method=f"file://{rdzv}", rank=int(os.environ["RANK"]),
+                                world_size=ws, timeout=timeout)
+    else:  # torch.distributed.run: env:// (MASTER_ADDR / MASTER_PORT)
+        dist.init_process_group("gloo", timeout=timeout)
     return dist, dist.get_rank(), dist.get_world_size()
 
 
