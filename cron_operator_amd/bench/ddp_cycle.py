@@ -33,7 +33,6 @@ from __future__ import annotations
 
 import asyncio
 import os
-import socket
 import sys
 import time
 from typing import Any, Dict, List
@@ -51,9 +50,9 @@ EXAMPLE_REPLICAS = os.path.join(ROOT, "examples", "mi355x", "cron-pytorch-ddp-8w
 
 
 def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from ..utils.ports import free_port
+
+    return free_port()
 
 
 def _shrink(ctr: Dict[str, Any], cpu: bool, steps: int, hidden: int) -> None:

@@ -52,11 +52,9 @@ def _free_port() -> int:
     """A loopback port free at this moment (the rendezvous port of one job's replicas).  The
     real training-operator uses a fixed port in each pod's own network namespace; here every
     replica shares the host, so concurrent jobs must not collide."""
-    import socket
+    from ..utils.ports import free_port
 
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    return free_port()
 
 
 def _now_str(clock: Clock) -> str:

@@ -14,7 +14,6 @@ from __future__ import annotations
 
 import json
 import os
-import socket
 import ssl
 import subprocess
 import sys
@@ -29,9 +28,9 @@ TOKEN = "e2e-admin-token"
 
 
 def _free_port() -> int:
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from cron_operator_amd.utils.ports import free_port
+
+    return free_port()
 
 
 def _env():

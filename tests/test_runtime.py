@@ -705,3 +705,16 @@ async def test_informer_transforms_list_pages_once():
             break
     assert "data" not in inf.get("default", "late", copy=False) and seen.count("late") == 1
     await inf.stop()
+
+
+def test_free_port_is_free_and_below_the_ephemeral_range():
+    import socket
+
+    from cron_operator_amd.utils.ports import _ephemeral_low, free_port
+
+    low = _ephemeral_low()
+    for _ in range(20):
+        p = free_port()
+        assert 1024 < p and (p < low or low - 15000 < 1000)
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", p))  # still free
