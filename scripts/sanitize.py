@@ -102,6 +102,16 @@ def drive(scratch: str, iters: int) -> None:
             fj.loads(_mutate(rng, raw))
         except (ValueError, RecursionError):
             pass
+    # plan-driven codecs: memo paths remembered by the encoder, reused by identity and by bytes
+    memo = fj.Memo(256)
+    codec = fj.Codec(skip=[("s",)], memo_paths=[("h", "*"), ("m",)], memo=memo)
+    for _ in range(iters // 8):
+        hist = [_tree(rng) for _ in range(rng.randint(0, 4))]
+        doc = {"h": hist, "m": _tree(rng), "s": _tree(rng), "x": "y" * rng.randint(0, 40) + "\n\"\\é"}
+        assert codec.dumpb(doc) == fj.dumpb(doc)
+        assert codec.dumpb(doc) == fj.dumpb(doc)  # second time: memo values copied by identity
+        back = codec.loads(codec.dumpb(doc))
+        assert back["h"] == hist and "s" not in back
     # the shared-value cache: strings handed out, dropped, evicted and handed out again
     vals = [f"v{i}" for i in range(40000)] + ["kubeflow.org/v1", "PyTorchJob", "Succeeded"] * 100
     for rnd in range(3):

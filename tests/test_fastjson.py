@@ -248,6 +248,27 @@ def test_codec_memo_reuses_objects_across_documents_and_from_the_encoder():
     assert memo.stats()["used"] == 0
 
 
+@settings(max_examples=200, deadline=None)
+@given(st.lists(json_values, max_size=4), json_values)
+def test_codec_encoder_reuses_remembered_bytes_by_identity(entries, other):
+    """Values at memo paths met again by identity are copied from the bytes the encoder
+    remembered -- the output stays byte-identical to a plain encode -- while values the decoder
+    remembered (a peer's encoding, maybe formatted differently) are encoded anew."""
+    memo = m.Memo(64)
+    enc = m.Codec(memo_paths=[("h", "*")], memo=memo)
+    doc = {"h": entries, "o": other}
+    plain = m.dumpb(doc)
+    assert enc.dumpb(doc) == plain
+    assert enc.dumpb(doc) == plain
+    if entries:
+        assert memo.stats()["reuses"] >= 1
+    # the decoder remembers a peer's spacing; encoding that object must not copy those bytes
+    dec = m.Codec(memo_paths=[("h", "*")], memo=memo)
+    peer = json.dumps({"h": [{"k": [1, 2]}]}, separators=(", ", ": "))
+    got = dec.loads(peer)
+    assert enc.dumpb(got) == m.dumpb(got)
+
+
 def test_codec_event_shape_and_errors():
     c = m.Codec(skip=[("object", "spec")])
     assert c(b'{"type":"ADDED","object":{"spec":{"big":[1,2,3]},"metadata":{"name":"a"}}}') == \
