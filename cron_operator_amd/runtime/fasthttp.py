@@ -29,9 +29,11 @@ With the ``_netconn`` extension (``ops/csrc/netconn.cpp``) the connections
 themselves are native: the pool dials the socket and hands it over, and the
 loop calls the native connection straight from its selector -- receive,
 framing, de-chunking, line splitting and TLS (OpenSSL, configured by the same
-``ssl.SSLContext``) run in C++.  The asyncio protocols below remain for http
-proxies, for builds without the extension (``CRON_OPERATOR_NATIVE_HTTP=python``),
-and as the behavioural oracle of the native path's tests.
+``ssl.SSLContext``) run in C++; through an http proxy the pool dials the proxy
+(a ``CONNECT`` tunnel first for TLS servers) and hands that socket over.  The
+asyncio protocols below remain for builds without the extension
+(``CRON_OPERATOR_NATIVE_HTTP=python``) and as the behavioural oracle of the native
+path's tests.
 """
 from __future__ import annotations
 
@@ -500,8 +502,8 @@ class HttpPool:
     def __init__(self, base_url: str, ssl_context: Optional[_ssl.SSLContext] = None,
                  headers: Optional[Dict[str, str]] = None, max_idle: int = 64, timeout: float = 60.0,
                  server_hostname: Optional[str] = None, proxy: str = "", native: Optional[bool] = None):
-        """``native``: use ``_netconn`` connections (None: whenever the extension is built, no
-        proxy is configured and it can drive the TLS context; True: required)."""
+        """``native``: use ``_netconn`` connections (None: whenever the extension is built and it
+        can drive the TLS context; True: required)."""
         u = urlsplit(base_url)
         self.scheme = u.scheme or "http"
         self.host = u.hostname or "127.0.0.1"
@@ -544,11 +546,10 @@ class HttpPool:
 
         want = self._want_native
         mod = netconn_native.load() if want is not False else None
-        ok = mod is not None and self._proxy is None and \
-            (self.ssl is None or mod.ssl_context_supported(self.ssl))
+        ok = mod is not None and (self.ssl is None or mod.ssl_context_supported(self.ssl))
         if want and not ok:
             raise RuntimeError("native HTTP connections unavailable for this pool "
-                               f"(extension {'missing' if mod is None else 'loaded'}, proxy={bool(self._proxy)})")
+                               f"(extension {'missing' if mod is None else 'loaded'})")
         self._netconn = mod if ok else None
         self.native = ok
 
@@ -613,10 +614,46 @@ class HttpPool:
         return proto
 
     async def _dial(self) -> _socket.socket:
-        """A connected non-blocking TCP socket to the server (addresses tried in order, like
-        Go's dialer without a fallback delay); TCP_NODELAY and keepalive probes on."""
+        """A connected non-blocking TCP socket to the server -- or, through an http proxy, to the
+        proxy (a TLS server behind it gets a ``CONNECT`` tunnel first) -- with addresses tried in
+        order like Go's dialer without a fallback delay; TCP_NODELAY and keepalive probes on."""
+        host, port = self._proxy or (self.host, self.port)
+        sock = await self._dial_addr(host, port)
+        if self._proxy is not None and self.ssl is not None:
+            try:
+                await self._connect_tunnel(sock)
+            except BaseException:
+                sock.close()
+                raise
+        return sock
+
+    async def _connect_tunnel(self, sock: _socket.socket) -> None:
+        """``CONNECT host:port`` on a fresh proxy connection; returns once the proxy answered 200
+        (the socket then carries the TLS session to the server)."""
         loop = asyncio.get_running_loop()
-        infos = await loop.getaddrinfo(self.host, self.port, type=_socket.SOCK_STREAM)
+        authority = f"{self.host}:{self.port}" if ":" not in self.host else f"[{self.host}]:{self.port}"
+        await loop.sock_sendall(sock, f"CONNECT {authority} HTTP/1.1\r\nHost: {authority}\r\n{self._proxy_auth}\r\n"
+                                .encode("latin-1"))
+        buf = b""
+        while b"\r\n\r\n" not in buf:
+            chunk = await loop.sock_recv(sock, 4096)
+            if not chunk:
+                raise ConnectionFailed("proxy closed the connection", True, False)
+            buf += chunk
+            if len(buf) > 65536:
+                raise ConnectionFailed("bad proxy response", True, False)
+        # a proxy answers CONNECT with a head only: nothing of the tunnel follows before our hello
+        line = buf.split(b"\r\n", 1)[0].split(b" ", 2)
+        try:
+            status = int(line[1])
+        except (IndexError, ValueError):
+            raise ConnectionFailed("bad proxy response", True, False) from None
+        if status != 200:
+            raise ConnectionFailed(f"proxy CONNECT {authority}: HTTP {status}", True, False)
+
+    async def _dial_addr(self, host: str, port: int) -> _socket.socket:
+        loop = asyncio.get_running_loop()
+        infos = await loop.getaddrinfo(host, port, type=_socket.SOCK_STREAM)
         err: Optional[BaseException] = None
         for family, type_, proto, _, addr in infos:
             sock = _socket.socket(family, type_, proto)
@@ -636,7 +673,7 @@ class HttpPool:
                 pass
             keepalive_socket(sock)
             return sock
-        raise err if err is not None else OSError(f"no address for {self.host}:{self.port}")
+        raise err if err is not None else OSError(f"no address for {host}:{port}")
 
     async def _open_native(self):
         """A native connection (``_netconn.Conn``), TLS handshake done."""

@@ -108,6 +108,11 @@ async def test_requests_and_watch_through_proxy(tls, fast):
                          proxy_url=f"http://op:p%40ss@127.0.0.1:{pport}")
         c = Client(HttpTransport(cfg, fast=fast), qps=-1)
         try:
+            if fast:
+                from cron_operator_amd.ops import netconn_native
+
+                # the native connections go through the proxy too (absolute form / CONNECT tunnel)
+                assert c.transport._fast_pool().native == (netconn_native.load() is not None)
             await c.create(CM, {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "a"}}, "default")
             assert (await c.get(CM, "default", "a"))["metadata"]["name"] == "a"
             with pytest.raises(errors.ApiError) as e:
