@@ -364,3 +364,44 @@ async def test_early_response_to_unsent_body_retires_the_connection():
     finally:
         await pool.close()
         srv.close()
+
+
+async def test_tls_client_certificate_is_presented(tmp_path):
+    """mTLS (a kubeconfig's client-certificate-data): the native handshake presents the
+    certificate the SSLContext holds; without it the server refuses the connection."""
+    from cron_operator_amd.runtime.servers import self_signed_cert
+
+    (tmp_path / "srv").mkdir()
+    (tmp_path / "cli").mkdir()
+    scert, skey = self_signed_cert(str(tmp_path / "srv"), host="localhost")
+    ccert, ckey = self_signed_cert(str(tmp_path / "cli"), host="operator")
+    sctx = _server_ctx(scert, skey)
+    sctx.verify_mode = ssl.CERT_REQUIRED
+    sctx.load_verify_locations(cafile=ccert)
+    peers = []
+
+    async def handle(reader, writer):
+        try:
+            peers.append(writer.get_extra_info("peercert"))
+            await _read_request(reader)
+            writer.write(b"HTTP/1.1 200 OK\r\nContent-Length: 2\r\n\r\nok")
+            await writer.drain()
+        except (asyncio.IncompleteReadError, ConnectionResetError, ssl.SSLError):
+            pass
+        writer.close()
+
+    srv, port = await _server(handle, sctx)
+    try:
+        ctx = ssl.create_default_context(cafile=scert)
+        ctx.load_cert_chain(ccert, ckey)
+        pool = HttpPool(f"https://127.0.0.1:{port}", ssl_context=ctx, server_hostname="localhost", native=True)
+        assert await pool.request("GET", "/") == (200, b"ok")
+        await pool.close()
+        assert peers and dict(x[0] for x in peers[0]["subject"])["commonName"] == "operator"
+        anon = HttpPool(f"https://127.0.0.1:{port}", ssl_context=ssl.create_default_context(cafile=scert),
+                        server_hostname="localhost", native=True)
+        with pytest.raises((ssl.SSLError, ConnectionFailed)):
+            await anon.request("GET", "/")
+        await anon.close()
+    finally:
+        srv.close()
