@@ -64,10 +64,12 @@ def _spawn_ranks(n: int) -> int:
     rank that fails ends the others instead of leaving them waiting at a barrier.  Nothing here
     touches the GPU, so child processes are started, never exec'd.  Only rank 0 prints the
     JSON line."""
+    import shutil
     import subprocess
     import tempfile
 
-    rdzv = tempfile.mktemp(prefix="bench-rdzv-")  # created by the first rank's FileStore
+    rdzv_dir = tempfile.mkdtemp(prefix="bench-rdzv-")
+    rdzv = os.path.join(rdzv_dir, "store")  # created by the first rank's FileStore
     procs = []
     try:
         for r in range(n):
@@ -91,10 +93,7 @@ def _spawn_ranks(n: int) -> int:
             if p.poll() is None:
                 p.kill()
                 p.wait()
-        try:
-            os.unlink(rdzv)
-        except OSError:
-            pass
+        shutil.rmtree(rdzv_dir, ignore_errors=True)
     bad = [rc for rc in rcs if rc != 0]
     return bad[0] if bad else 0
 
