@@ -490,8 +490,8 @@ class CronReconciler(Reconciler):
             self.own_writes[key] = (m.get("generation"), new_status)
         body: Any = codecs.status_patch.dumpb(patch) if codecs is not None else patch
         try:
-            with tracing.span("patch_status", bytes=len(body) if body.__class__ is bytes else
-                              len(jsonutil.dumps(patch)) if tracing.get_tracer().enabled else 0):
+            with (tracing.span("patch_status", bytes=len(body) if body.__class__ is bytes else
+                               len(jsonutil.dumps(patch))) if tracing.get_tracer().enabled else tracing.NOOP):
                 await self.client.patch(CRON_GVR, m.get("namespace", ""), m.get("name", ""), body, "merge",
                                         "status", discard_response=True)
         except Exception:
@@ -528,6 +528,8 @@ class CronReconciler(Reconciler):
     # ------------------------------------------------------------------ the algorithm
     async def _sync(self, cron: Cron, log: Logger, gc: Optional[List["asyncio.Future[None]"]] = None) -> Result:
         policy = self.opts.workload
+        # spans (and the attributes they would carry) only when tracing is on
+        traced = tracing.get_tracer().enabled
         # B3 (cron_controller.go:122-126)
         try:
             gvk = get_workload_gvk(cron.spec.template.workload, policy)
@@ -539,7 +541,8 @@ class CronReconciler(Reconciler):
         infos: Optional[List[_ChildInfo]] = None
         workloads: List[Dict[str, Any]] = []
         try:
-            with tracing.span("list_children", kind=gvk.kind, mode=self.opts.list_mode) as sp:
+            with (tracing.span("list_children", kind=gvk.kind, mode=self.opts.list_mode) if traced
+                  else tracing.NOOP) as sp:
                 if self.opts.classification_cache and self.opts.list_mode != "live" and self.cache is not None:
                     inf = self.child_informers.get(gvk)
                     if inf is not None and inf.derive is not None and inf.synced.is_set():
@@ -552,7 +555,8 @@ class CronReconciler(Reconciler):
                     workloads = await self.list_workloads(cron, gvk, log, force_live=self.cache is not None
                                                           and self.opts.list_mode != "live"
                                                           and self.opts.classification_cache)
-                sp.set(count=len(workloads) if infos is None else len(infos))
+                if traced:
+                    sp.set(count=len(workloads) if infos is None else len(infos))
         except Exception as e:
             log.error(e, f"Failed to list {gvk.kind}")
             raise
@@ -599,7 +603,8 @@ class CronReconciler(Reconciler):
             log.info(f"{gvk.kind} count", active=len(active), terminated=len(terminated))
 
         # B6/B7/B8 (cron_controller.go:155-158)
-        with tracing.span("sync_status", active=len(active), terminated=len(terminated)):
+        with (tracing.span("sync_status", active=len(active), terminated=len(terminated)) if traced
+              else tracing.NOOP):
             if gc is not None:  # DELETEs are only started: nothing to await here
                 if chatty:
                     log.v(1).info("Syncing Cron status")
@@ -690,11 +695,12 @@ class CronReconciler(Reconciler):
         if self.opts.expectations:
             self.expect.expect_pending(self._ckey(cron), wm.get("name", ""))
         try:
-            with tracing.span("create_workload", kind=gvk.kind, name=wm.get("name", ""),
-                              tick=missed_run.rfc3339()) as sp:
+            with (tracing.span("create_workload", kind=gvk.kind, name=wm.get("name", ""),
+                               tick=missed_run.rfc3339()) if traced else tracing.NOOP) as sp:
                 created = await self.client.create(gvk, workload, wm.get("namespace", ""),
                                                    decoder=self.codecs.child_object if self.codecs else None)
-                sp.set(tick_to_create_ms=(self.clock.now_ns() - missed_run.unix_nano()) / 1e6)
+                if traced:
+                    sp.set(tick_to_create_ms=(self.clock.now_ns() - missed_run.unix_nano()) / 1e6)
             self.stats["creates"] += 1
             metrics.child(metrics.WORKLOADS_CREATED, gvk.kind).inc()
             if self.opts.expectations:
