@@ -142,19 +142,48 @@ def _parse_time(v: Any) -> Optional[GoTime]:
     return None
 
 
+def _kubeflow_summary_py(raw: Any):
+    return None
+
+
+def _native_summary():
+    from ..utils import jsonutil
+
+    if not jsonutil.NATIVE:
+        return _kubeflow_summary_py
+    from ..ops import fastjson_native
+
+    return getattr(fastjson_native.load(), "kubeflow_summary", _kubeflow_summary_py)
+
+
+# status dict -> (finished, last condition type, #conditions, completionTime, terminal
+# lastTransitionTime) for exactly-typed statuses, else None (ops/csrc/fastjson.cpp)
+_summary = _native_summary()
+
+
 def classify(workload: Dict[str, Any], gvk: GroupVersionKind, policy: WorkloadPolicy) -> Classification:
     """Active/terminated decision for one child.  Raises ``kf.ConversionError``
     when the status does not convert (the reconciler then skips the child)."""
-    st = kf.get_job_status(workload)
-    finished = kf.is_succeeded(st) or kf.is_failed(st)
-    last = st.conditions[-1].type if st.conditions else ""
-    if finished:
-        at = st.completion_time
-        if at is None:
-            tc = kf.terminal_condition(st)
-            at = tc.last_transition_time if tc is not None else None
-        return Classification(True, last, at)
-    raw = workload.get("status") if isinstance(workload.get("status"), dict) else {}
+    raw = workload.get("status")
+    sm = _summary(raw) if raw.__class__ is dict else None
+    if sm is not None:  # a well-typed kubeflow status, read natively without building a JobStatus
+        finished, last, nconds, comp, tltt = sm
+        if finished:
+            t = comp if comp is not None else tltt
+            return Classification(True, last, parse_rfc3339(t) if t is not None else None)
+        has_conditions = nconds > 0
+    else:
+        st = kf.get_job_status(workload)
+        finished = kf.is_succeeded(st) or kf.is_failed(st)
+        last = st.conditions[-1].type if st.conditions else ""
+        if finished:
+            at = st.completion_time
+            if at is None:
+                tc = kf.terminal_condition(st)
+                at = tc.last_transition_time if tc is not None else None
+            return Classification(True, last, at)
+        has_conditions = bool(st.conditions)
+    raw = raw if isinstance(raw, dict) else {}
     if policy.builtin_status:
         if gvk.group == "batch" and gvk.kind == "Job":
             for c in reversed(raw.get("conditions") or []):
@@ -166,7 +195,7 @@ def classify(workload: Dict[str, Any], gvk: GroupVersionKind, policy: WorkloadPo
             if phase in ("Succeeded", "Failed"):
                 return Classification(True, phase, None)
             return Classification(False, phase or last, None)
-    if policy.mpi_launcher_status and gvk.kind == "MPIJob" and not st.conditions:
+    if policy.mpi_launcher_status and gvk.kind == "MPIJob" and not has_conditions:
         ls = raw.get("launcherStatus")
         if ls in (kf.JobSucceeded, kf.JobFailed):
             return Classification(True, ls, _parse_time(raw.get("completionTime")))

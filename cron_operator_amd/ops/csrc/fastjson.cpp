@@ -1281,6 +1281,116 @@ PyObject* py_merge_patch(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
   return merge_patch_impl(args[0], args[1], 0, share != 0);
 }
 
+// ---------------------------------------------------------------------- kubeflow job status
+//
+// kubeflow_summary(status) -> None | (finished, last_type, n_conditions, completion_time, terminal_ltt)
+//
+// What the reconciler's classification reads from a training-operator JobStatus
+// (models/kubeflow.py, models/workload.py classify; reference cron_util.go:73-114): whether a
+// Succeeded/Failed condition is True, the last condition's type, and the raw completionTime /
+// the terminal condition's lastTransitionTime strings.  Only exactly-typed input is taken
+// (str/None string fields, int/None counts, RFC 3339 times as time.Parse(time.RFC3339)
+// accepts them, in ASCII); anything else returns None and the Python converter -- the oracle
+// of tests/test_kubeflow_status.py -- decides, raising its precise ConversionError.
+
+// ASCII RFC 3339 with the Python parser's field ranges (a subset of what it accepts)
+bool rfc3339_ok(PyObject* v) {
+  if (!PyUnicode_IS_COMPACT_ASCII(v)) return false;
+  const char* s = static_cast<const char*>(PyUnicode_DATA(v));
+  const Py_ssize_t n = PyUnicode_GET_LENGTH(v);
+  if (n < 20) return false;
+  auto dig = [s](Py_ssize_t i) { return s[i] >= '0' && s[i] <= '9'; };
+  static const int kDigits[] = {0, 1, 2, 3, 5, 6, 8, 9, 11, 12, 14, 15, 17, 18};
+  for (int i : kDigits)
+    if (!dig(i)) return false;
+  if (s[4] != '-' || s[7] != '-' || (s[10] != 'T' && s[10] != 't') || s[13] != ':' || s[16] != ':') return false;
+  auto two = [s](int i) { return (s[i] - '0') * 10 + (s[i + 1] - '0'); };
+  const int mo = two(5), d = two(8), hh = two(11), mi = two(14), ss = two(17);
+  if (mo < 1 || mo > 12 || d < 1 || d > 31 || hh > 23 || mi > 59 || ss > 59) return false;
+  Py_ssize_t i = 19;
+  if (s[i] == '.') {
+    const Py_ssize_t b = ++i;
+    while (i < n && dig(i)) ++i;
+    if (i - b < 1 || i - b > 9) return false;
+  }
+  if (i < n && (s[i] == 'Z' || s[i] == 'z')) return i + 1 == n;
+  return n - i == 6 && (s[i] == '+' || s[i] == '-') && dig(i + 1) && dig(i + 2) && s[i + 3] == ':' &&
+         dig(i + 4) && dig(i + 5);
+}
+
+// a time field: absent/None/"" (no time) or a valid string; false -> the strict path decides
+inline bool time_ok(PyObject* v) {
+  if (v == nullptr || v == Py_None) return true;
+  if (!PyUnicode_CheckExact(v)) return false;
+  return PyUnicode_GET_LENGTH(v) == 0 || rfc3339_ok(v);
+}
+
+inline bool str_or_none(PyObject* v) { return v == nullptr || v == Py_None || PyUnicode_CheckExact(v); }
+inline bool int_or_none(PyObject* v) { return v == nullptr || v == Py_None || PyLong_CheckExact(v); }
+
+inline bool eq_ascii(PyObject* v, const char* lit) {
+  return v != nullptr && PyUnicode_CheckExact(v) && PyUnicode_IS_COMPACT_ASCII(v) &&
+         std::strcmp(static_cast<const char*>(PyUnicode_DATA(v)), lit) == 0 &&
+         static_cast<size_t>(PyUnicode_GET_LENGTH(v)) == std::strlen(lit);
+}
+
+PyObject* py_kubeflow_summary(PyObject*, PyObject* st) {
+  if (!PyDict_CheckExact(st)) Py_RETURN_NONE;
+  PyObject* conds = PyDict_GetItemString(st, "conditions");  // borrowed
+  bool finished = false;
+  PyObject* last = nullptr;
+  PyObject* tltt = nullptr;  // lastTransitionTime of the last True Succeeded/Failed condition
+  Py_ssize_t nconds = 0;
+  if (conds != nullptr && conds != Py_None) {
+    if (!PyList_CheckExact(conds)) Py_RETURN_NONE;
+    nconds = PyList_GET_SIZE(conds);
+    for (Py_ssize_t i = 0; i < nconds; ++i) {
+      PyObject* c = PyList_GET_ITEM(conds, i);
+      if (!PyDict_CheckExact(c)) Py_RETURN_NONE;
+      PyObject* type = PyDict_GetItemString(c, "type");
+      PyObject* status = PyDict_GetItemString(c, "status");
+      PyObject* ltt = PyDict_GetItemString(c, "lastTransitionTime");
+      if (!str_or_none(type) || !str_or_none(status) || !str_or_none(PyDict_GetItemString(c, "reason")) ||
+          !str_or_none(PyDict_GetItemString(c, "message")) || !time_ok(PyDict_GetItemString(c, "lastUpdateTime")) ||
+          !time_ok(ltt))
+        Py_RETURN_NONE;
+      if ((eq_ascii(type, "Succeeded") || eq_ascii(type, "Failed")) && eq_ascii(status, "True")) {
+        finished = true;
+        tltt = ltt;
+      }
+      last = type;
+    }
+  }
+  PyObject* rs = PyDict_GetItemString(st, "replicaStatuses");
+  if (rs != nullptr && rs != Py_None) {
+    if (!PyDict_CheckExact(rs)) Py_RETURN_NONE;
+    Py_ssize_t pos = 0;
+    PyObject *k, *v;
+    while (PyDict_Next(rs, &pos, &k, &v)) {
+      if (v == Py_None) continue;
+      if (!PyDict_CheckExact(v)) Py_RETURN_NONE;
+      PyObject* sel = PyDict_GetItemString(v, "labelSelector");
+      if (!int_or_none(PyDict_GetItemString(v, "active")) || !int_or_none(PyDict_GetItemString(v, "succeeded")) ||
+          !int_or_none(PyDict_GetItemString(v, "failed")) || !str_or_none(PyDict_GetItemString(v, "selector")) ||
+          !(sel == nullptr || sel == Py_None || PyDict_CheckExact(sel)))
+        Py_RETURN_NONE;
+    }
+  }
+  PyObject* comp = PyDict_GetItemString(st, "completionTime");
+  if (!time_ok(PyDict_GetItemString(st, "startTime")) || !time_ok(comp) ||
+      !time_ok(PyDict_GetItemString(st, "lastReconcileTime")))
+    Py_RETURN_NONE;
+  auto text = [](PyObject* v) -> PyObject* {  // a non-empty time string, else None
+    if (v == nullptr || v == Py_None || PyUnicode_GET_LENGTH(v) == 0) Py_RETURN_NONE;
+    Py_INCREF(v);
+    return v;
+  };
+  PyObject* last_s = (last == nullptr || last == Py_None) ? PyUnicode_FromStringAndSize("", 0) : (Py_INCREF(last), last);
+  PyObject* comp_s = text(comp);
+  PyObject* tltt_s = text(tltt);
+  return Py_BuildValue("(ONnNN)", finished ? Py_True : Py_False, last_s, nconds, comp_s, tltt_s);
+}
+
 PyObject* py_set_gc_untrack(PyObject*, PyObject* arg) {
   const int on = PyObject_IsTrue(arg);
   if (on < 0) return nullptr;
@@ -1535,6 +1645,8 @@ PyMethodDef methods[] = {
     {"dumpb_shared", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(py_dumpb_shared)),
      METH_FASTCALL, "dumpb of an immutable tree, reusing the bytes of subtrees cached by identity"},
     {"clear_key_cache", py_clear_key_cache, METH_NOARGS, "drop the interned-key cache"},
+    {"kubeflow_summary", py_kubeflow_summary, METH_O,
+     "kubeflow_summary(status) -> None | (finished, last_type, n_conditions, completion_time, terminal_ltt)"},
     {"set_gc_untrack", py_set_gc_untrack, METH_O,
      "set_gc_untrack(bool) -> previous: exempt decoded/copied containers from cyclic GC"},
     {nullptr, nullptr, 0, nullptr}};

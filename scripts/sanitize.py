@@ -112,6 +112,18 @@ def drive(scratch: str, iters: int) -> None:
         assert codec.dumpb(doc) == fj.dumpb(doc)  # second time: memo values copied by identity
         back = codec.loads(codec.dumpb(doc))
         assert back["h"] == hist and "s" not in back
+    # kubeflow job-status summaries over random (often ill-typed) statuses
+    times = ["2026-01-01T12:00:00Z", "2026-01-01T12:00:00.123+02:00", "2026-13-01T00:00:00Z", "", "x" * 30,
+             "2026-01-01T12:00:00Z\n", "٢٠٢٦-01-01T12:00:00Z"]
+    for _ in range(iters // 4):
+        conds = [{"type": rng.choice(["Succeeded", "Failed", "Running", None, 1]),
+                  "status": rng.choice(["True", "False", None, True]),
+                  "lastTransitionTime": rng.choice(times + [None, 5])} for _ in range(rng.randint(0, 3))]
+        status = {"conditions": conds if rng.random() < 0.9 else _tree(rng),
+                  "replicaStatuses": {"Master": {"succeeded": rng.choice([1, True, None, "1"])}},
+                  "completionTime": rng.choice(times + [None])}
+        fj.kubeflow_summary(status)
+        fj.kubeflow_summary(_tree(rng))
     # the shared-value cache: strings handed out, dropped, evicted and handed out again
     vals = [f"v{i}" for i in range(40000)] + ["kubeflow.org/v1", "PyTorchJob", "Succeeded"] * 100
     for rnd in range(3):

@@ -52,3 +52,56 @@ def test_fast_path_taken_for_a_typical_finished_job():
     assert fast is not None and fast == kf._strict_job_status(s)
     assert kf.is_succeeded(fast) and fast.completion_time is not None
     assert kf._fast_job_status({"replicaStatuses": {"Master": {"active": True}}}) is None  # bool: strict path
+
+
+_kinds = st.sampled_from([("kubeflow.org", "v1", "PyTorchJob"), ("kubeflow.org", "v1", "MPIJob"),
+                          ("batch", "v1", "Job"), ("", "v1", "Pod")])
+
+
+def _classify_outcome(workload, gvk):
+    from cron_operator_amd.models.workload import WorkloadPolicy, classify
+
+    try:
+        c = classify(workload, gvk, WorkloadPolicy())
+        return "ok", (c.finished, c.status, c.finished_at)
+    except kf.ConversionError as e:
+        return "err", str(e)
+
+
+@settings(max_examples=600, deadline=None)
+@given(st.one_of(_status, st.fixed_dictionaries({}, optional={"phase": st.sampled_from(["Succeeded", "Running"]),
+                                                             "launcherStatus": st.sampled_from(["Succeeded", "x"]),
+                                                             "conditions": st.lists(_cond, max_size=3)}),
+                 _scalar), _kinds)
+def test_native_status_summary_classifies_like_the_converter(status, kind):
+    """classify() with the native kubeflow summary (``_fastjson.kubeflow_summary``) equals
+    classify() on the Python converter for every status, typed or not."""
+    import pytest
+
+    from cron_operator_amd.api.meta import GroupVersionKind
+    from cron_operator_amd.models import workload as wl
+
+    if wl._summary is wl._kubeflow_summary_py:
+        pytest.skip("_fastjson not built")
+    gvk = GroupVersionKind(*kind)
+    w = {"apiVersion": gvk.api_version, "kind": gvk.kind, "metadata": {"name": "j"}, "status": status}
+    native = _classify_outcome(w, gvk)
+    saved, wl._summary = wl._summary, wl._kubeflow_summary_py
+    try:
+        python = _classify_outcome(w, gvk)
+    finally:
+        wl._summary = saved
+    assert native == python
+
+
+def test_native_summary_is_taken_for_a_typical_finished_job():
+    from cron_operator_amd.models import workload as wl
+
+    if wl._summary is wl._kubeflow_summary_py:
+        return
+    s = {"conditions": [{"type": "Created", "status": "True", "lastTransitionTime": "2026-01-01T12:00:00Z"},
+                        {"type": "Succeeded", "status": "True", "lastTransitionTime": "2026-01-01T12:01:00.5+02:00"}],
+         "replicaStatuses": {"Master": {"succeeded": 1}}, "completionTime": ""}
+    assert wl._summary(s) == (True, "Succeeded", 2, None, "2026-01-01T12:01:00.5+02:00")
+    assert wl._summary({"replicaStatuses": {"M": {"active": True}}}) is None  # bool count: strict path
+    assert wl._summary({"startTime": "2026-01-01T12:00:00Z\n"}) is None       # not ASCII-exact: strict path
