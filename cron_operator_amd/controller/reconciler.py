@@ -372,6 +372,8 @@ class CronReconciler(Reconciler):
         # key -> (spec dict of the cached Cron, its parsed CronSpec): the Cron informer's codec hands
         # back the same spec object while the spec bytes do not change, so it is parsed once
         self._spec_memo: Dict[str, Tuple[Dict[str, Any], Any]] = {}
+        # key -> (template workload dict, policy, its GVK): checked once per template object
+        self._gvk_memo: Dict[str, Tuple[Any, WorkloadPolicy, GroupVersionKind]] = {}
         # tick bookkeeping for latency: key -> (tick unix ns, wall perf_counter when it became due)
         self.latency_observer: Optional[Callable[[str, GoTime, Dict[str, Any]], None]] = None
 
@@ -379,6 +381,7 @@ class CronReconciler(Reconciler):
         """Drop the per-Cron memos of a Cron that is gone (``namespace/name``)."""
         self._parsed_status.pop(key, None)
         self._spec_memo.pop(key, None)
+        self._gvk_memo.pop(key, None)
         self.own_writes.pop(key, None)
         self._own_rv.pop(key, None)
         self.expect.forget(key)
@@ -531,11 +534,20 @@ class CronReconciler(Reconciler):
         # spans (and the attributes they would carry) only when tracing is on
         traced = tracing.get_tracer().enabled
         # B3 (cron_controller.go:122-126)
-        try:
-            gvk = get_workload_gvk(cron.spec.template.workload, policy)
-        except WorkloadError as e:
-            log.error(e, "Failed to get workload GVK")
-            return Result()
+        wl = cron.spec.template.workload
+        gm = self._gvk_memo
+        ck = f"{cron.namespace}/{cron.name}"
+        hit = gm.get(ck) if wl.__class__ is dict else None
+        if hit is not None and hit[0] is wl and hit[1] is policy:
+            gvk = hit[2]  # the same (read-only) template object as last time: same checks, same GVK
+        else:
+            try:
+                gvk = get_workload_gvk(wl, policy)
+            except WorkloadError as e:
+                log.error(e, "Failed to get workload GVK")
+                return Result()
+            if wl.__class__ is dict:
+                gm[ck] = (wl, policy, gvk)
 
         # B4 (cron_controller.go:129-133)
         infos: Optional[List[_ChildInfo]] = None
@@ -916,60 +928,63 @@ class CronReconciler(Reconciler):
         ops: List[Any] = []
         if not presorted:
             self._sort(terminated)
-        n = len(terminated)
         limit = cron.spec.history_limit if cron.spec.history_limit is not None else MAX_INT
-        previous: Optional[Dict[str, CronHistory]] = None
-        history: List[CronHistory] = []
-        now: Optional[GoTime] = None
-        memo_ok = self.opts.finished_time != "now"
-        for i, (w, c, info) in enumerate(terminated):
-            if memo_ok and i >= n - limit:
-                if info is not None and info.history_entry is not None:
-                    history.append(info.history_entry)
-                    continue
-            m = w.get("metadata") or {}
-            wgvk = GroupVersionKind.from_object(w)
-            ref = ObjectRef(m.get("namespace", ""), m.get("name", ""))
-            if i < n - limit:
+        cut = len(terminated) - limit  # the oldest `cut` children are beyond the history limit
+        if cut > 0:
+            for w, _, _ in terminated[:cut]:
+                m = w.get("metadata") or {}
+                wgvk = GroupVersionKind.from_object(w)
+                ref = ObjectRef(m.get("namespace", ""), m.get("name", ""))
                 if chatty:
                     log.info(f"Deleting terminated {wgvk.kind}", **{wgvk.kind: ref})
-                uid = m.get("uid", "")
-                args = (cron, wgvk, m.get("namespace", ""), m.get("name", ""), uid, ref, log)
+                args = (cron, wgvk, m.get("namespace", ""), m.get("name", ""), m.get("uid", ""), ref, log)
                 if gc is None:
                     # the coroutine is created only when it is awaited: nothing is left un-awaited
                     # if an earlier DELETE ends the reconcile
                     ops.append(functools.partial(self._gc_delete, *args))
                 else:
                     gc.append(asyncio.ensure_future(self._gc_delete(*args)))
-                continue
-            if not memo_ok:
-                info = None
-            entry = CronHistory(uid=m.get("uid", ""),
-                                object=TypedLocalObjectReference(api_group=wgvk.group_version().__str__(),
-                                                                 kind=wgvk.kind, name=m.get("name", "")),
-                                status=c.status, created=creation_timestamp(w))
-            if c.finished:
-                if self.opts.finished_time == "now":
-                    if now is None:
-                        now = self.clock.now(LOCAL)
-                    entry.finished = now
-                elif c.finished_at is not None:
-                    entry.finished = c.finished_at
-                    if info is not None:  # fully determined by this child version
-                        info.history_entry = entry
-                else:
-                    if previous is None:  # only a child without a completion time needs it
-                        previous = {h.uid: h for h in cron.status.history if h.uid}
-                    prev = previous.get(entry.uid)
-                    if prev is not None and prev.finished is not None:
-                        entry.finished = prev.finished
-                    else:
-                        # first observation: second precision so it survives the JSON round trip
-                        t = self.clock.now(LOCAL)
-                        entry.finished = GoTime(t.sec, 0, t.loc)
-            history.append(entry)
+            terminated = terminated[cut:]
+        if self.opts.finished_time != "now":
+            # the steady state: every kept child's entry was built for its current version
+            history: List[CronHistory] = [e if info is not None and (e := info.history_entry) is not None
+                                          else self._history_entry(cron, w, c, info, None)
+                                          for w, c, info in terminated]
+        else:
+            now = self.clock.now(LOCAL)
+            history = [self._history_entry(cron, w, c, None, now) for w, c, _ in terminated]
         cron.status.history = history
         return ops
+
+    def _history_entry(self, cron: Cron, w: Dict[str, Any], c: Classification, info: Optional[_ChildInfo],
+                       now: Optional[GoTime]) -> CronHistory:
+        """The ``status.history`` entry of terminated child ``w`` (``cron_controller.go:336-343``).
+        ``now``: ``finished_time="now"`` (the reference stamps every entry with the reconcile's
+        time).  An entry fully determined by the child's version is remembered in ``info``."""
+        m = w.get("metadata") or {}
+        wgvk = GroupVersionKind.from_object(w)
+        entry = CronHistory(uid=m.get("uid", ""),
+                            object=TypedLocalObjectReference(api_group=wgvk.group_version().__str__(),
+                                                             kind=wgvk.kind, name=m.get("name", "")),
+                            status=c.status, created=creation_timestamp(w))
+        if c.finished:
+            if now is not None:
+                entry.finished = now
+            elif c.finished_at is not None:
+                entry.finished = c.finished_at
+                if info is not None:  # fully determined by this child version
+                    info.history_entry = entry
+            else:
+                # only a child without a completion time needs the previous entries (the last
+                # entry with its uid, as a uid -> entry map of them would hold)
+                prev = next((h for h in reversed(cron.status.history) if h.uid and h.uid == entry.uid), None)
+                if prev is not None and prev.finished is not None:
+                    entry.finished = prev.finished
+                else:
+                    # first observation: second precision so it survives the JSON round trip
+                    t = self.clock.now(LOCAL)
+                    entry.finished = GoTime(t.sec, 0, t.loc)
+        return entry
 
     async def _gc_delete(self, cron: Cron, gvk: GroupVersionKind, namespace: str, name: str, uid: str,
                          ref: ObjectRef, log: Logger) -> None:

@@ -40,6 +40,10 @@ def load(build_if_missing: bool = True):
                 _build.build_extension("_cron_engine")
             mod = importlib.import_module("cron_operator_amd.ops._cron_engine")
             mod.set_zone_resolver(_resolve_name)
+            if hasattr(mod, "rfc3339_z"):
+                from ..utils import gotime
+
+                gotime.install_native(mod.rfc3339_z, mod.format_rfc3339)
             _mod = mod
         except BaseException as e:  # noqa: BLE001 - recorded for diagnostics
             _load_error = e

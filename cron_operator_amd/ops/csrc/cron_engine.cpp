@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -1211,8 +1212,82 @@ PyObject* py_parse_duration(PyObject*, PyObject* arg) {
   }
 }
 
+// ------------------------------------------------------------------ RFC 3339 timestamps
+//
+// metav1.Time is written as "YYYY-MM-DDTHH:MM:SSZ"; every child event and status write carries a
+// few new ones, so these replace the Python arithmetic of utils/gotime.py for that exact shape.
+// Anything else returns None and the Python code decides (same results, tests/test_gotime.py).
+
+inline int digits(const Py_UCS1* p, int n) {
+  int v = 0;
+  for (int i = 0; i < n; ++i) {
+    if (p[i] < '0' || p[i] > '9') return -1;
+    v = v * 10 + (p[i] - '0');
+  }
+  return v;
+}
+
+// rfc3339_z(s) -> unix seconds | None
+PyObject* py_rfc3339_z(PyObject*, PyObject* arg) {
+  if (!PyUnicode_Check(arg)) {
+    PyErr_SetString(PyExc_TypeError, "rfc3339_z expects str");
+    return nullptr;
+  }
+  if (PyUnicode_READY(arg) < 0) return nullptr;
+  if (PyUnicode_GET_LENGTH(arg) != 20 || PyUnicode_KIND(arg) != PyUnicode_1BYTE_KIND) Py_RETURN_NONE;
+  const Py_UCS1* s = PyUnicode_1BYTE_DATA(arg);
+  if (s[4] != '-' || s[7] != '-' || s[10] != 'T' || s[13] != ':' || s[16] != ':' || s[19] != 'Z') Py_RETURN_NONE;
+  const int y = digits(s, 4), mo = digits(s + 5, 2), d = digits(s + 8, 2);
+  const int hh = digits(s + 11, 2), mi = digits(s + 14, 2), ss = digits(s + 17, 2);
+  if (y < 0 || mo < 1 || mo > 12 || d < 1 || d > 31 || hh < 0 || hh > 23 || mi < 0 || mi > 59 || ss < 0 || ss > 59)
+    Py_RETURN_NONE;
+  return PyLong_FromLongLong(days_from_civil(y, mo, d) * 86400 + hh * 3600 + mi * 60 + ss);
+}
+
+// format_rfc3339(wall, nsec, offset) -> str | None: Go's RFC 3339 of the wall-clock second `wall`
+// (unix seconds + offset), fractional nanoseconds without trailing zeros when nsec != 0, and "Z"
+// or "+hh:mm" for the offset; None outside years 0..9999
+PyObject* py_format_rfc3339(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 3) {
+    PyErr_SetString(PyExc_TypeError, "format_rfc3339(wall, nsec, offset)");
+    return nullptr;
+  }
+  const long long wall = PyLong_AsLongLong(args[0]);
+  const long long nsec = PyLong_AsLongLong(args[1]);
+  const long long off = PyLong_AsLongLong(args[2]);
+  if (PyErr_Occurred()) return nullptr;
+  if (nsec < 0 || nsec >= 1000000000LL || off <= -360000 || off >= 360000) Py_RETURN_NONE;
+  const int64_t days = floordiv(wall, 86400);
+  const int64_t rem = wall - days * 86400;
+  const Civil c = civil_from_days(days);
+  if (c.y < 0 || c.y > 9999) Py_RETURN_NONE;
+  char buf[48];
+  int n = std::snprintf(buf, sizeof buf, "%04d-%02d-%02dT%02d:%02d:%02d", static_cast<int>(c.y), c.m, c.d,
+                        static_cast<int>(rem / 3600), static_cast<int>((rem / 60) % 60), static_cast<int>(rem % 60));
+  if (nsec) {
+    char frac[16];
+    std::snprintf(frac, sizeof frac, "%09lld", nsec);
+    int k = 9;
+    while (k > 0 && frac[k - 1] == '0') --k;
+    buf[n++] = '.';
+    std::memcpy(buf + n, frac, static_cast<size_t>(k));
+    n += k;
+  }
+  if (off == 0) {
+    buf[n++] = 'Z';
+  } else {
+    const long long a = off < 0 ? -off : off;
+    n += std::snprintf(buf + n, sizeof buf - static_cast<size_t>(n), "%c%02lld:%02lld", off > 0 ? '+' : '-',
+                       a / 3600, (a / 60) % 60);
+  }
+  return PyUnicode_FromStringAndSize(buf, n);
+}
+
 PyMethodDef module_methods[] = {
     {"parse", py_parse, METH_O, "parse(spec) -> Schedule"},
+    {"rfc3339_z", py_rfc3339_z, METH_O, "rfc3339_z(s) -> unix seconds of 'YYYY-MM-DDTHH:MM:SSZ', else None"},
+    {"format_rfc3339", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(py_format_rfc3339)),
+     METH_FASTCALL, "format_rfc3339(wall, nsec, offset) -> str | None"},
     {"register_zone", py_register_zone, METH_VARARGS, "register_zone(name, tzif_bytes) -> id"},
     {"register_fixed_zone", py_register_fixed, METH_VARARGS, "register_fixed_zone(name, offset) -> id"},
     {"zone_offset", py_zone_offset, METH_VARARGS, "zone_offset(id, unix) -> seconds east of UTC"},

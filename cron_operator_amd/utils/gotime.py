@@ -412,8 +412,12 @@ class GoTime:
 
     # -- formatting
     def rfc3339(self, nanos: bool = False) -> str:
-        y, m, d, hh, mm, ss = self.fields()
         off = self.offset()
+        if _native_format is not None:
+            s = _native_format(self.sec + off, self.nsec if nanos else 0, off)
+            if s is not None:
+                return s
+        y, m, d, hh, mm, ss = self.fields()
         frac = ""
         if nanos and self.nsec:
             frac = "." + f"{self.nsec:09d}".rstrip("0")
@@ -435,6 +439,21 @@ _RFC3339_RE = re.compile(
     r"^(\d{4})-(\d{2})-(\d{2})[Tt](\d{2}):(\d{2}):(\d{2})(\.\d{1,9})?([Zz]|[+-]\d{2}:\d{2})$")
 
 
+# Native twins of the hot formatting/parsing paths (``_cron_engine.rfc3339_z`` / ``format_rfc3339``),
+# installed by ops/cron_native.py when the extension loads; each returns None for anything
+# outside the shape it handles and the Python code below decides (tests/test_gotime.py).
+_native_parse_z = None
+_native_format = None
+
+
+def install_native(parse_z, fmt) -> None:
+    """Use the native timestamp helpers (``None`` restores the pure-Python paths)."""
+    global _native_parse_z, _native_format
+    _native_parse_z, _native_format = parse_z, fmt
+    _parse_cached.cache_clear()
+    _format_utc_cached.cache_clear()
+
+
 def parse_rfc3339(s: str, loc: Location = LOCAL) -> GoTime:
     """Parse like ``time.Parse(time.RFC3339, s)`` then move the result to ``loc``.
 
@@ -450,6 +469,10 @@ def parse_rfc3339(s: str, loc: Location = LOCAL) -> GoTime:
 @lru_cache(maxsize=1 << 16)
 def _parse_cached(s: str, loc: Location) -> GoTime:
     # fast path: "YYYY-MM-DDTHH:MM:SSZ" (what metav1.Time always writes)
+    if _native_parse_z is not None:
+        sec = _native_parse_z(s)
+        if sec is not None:
+            return GoTime(sec, 0, loc)
     if len(s) == 20 and s[19] == "Z" and s[10] == "T" and s[4] == "-" and s[13] == ":":
         try:
             y, mo, d = int(s[0:4]), int(s[5:7]), int(s[8:10])
@@ -488,6 +511,10 @@ def format_rfc3339_utc(t: GoTime) -> str:
 
 @lru_cache(maxsize=1 << 16)
 def _format_utc_cached(sec: int) -> str:
+    if _native_format is not None:
+        s = _native_format(sec, 0, 0)
+        if s is not None:
+            return s
     days, rem = divmod(sec, 86400)
     y, m, d = civil_from_days(days)
     return f"{y:04d}-{m:02d}-{d:02d}T{rem // 3600:02d}:{(rem // 60) % 60:02d}:{rem % 60:02d}Z"
