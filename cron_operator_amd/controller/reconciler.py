@@ -126,12 +126,14 @@ class _ChildInfo:
     version instead of on every reconcile of its Cron (the 10 history children of a
     Cron were re-parsed ~2x per tick otherwise)."""
 
-    __slots__ = ("rv", "cls", "sort_key", "gvk", "active_ref", "history_entry", "obj", "name", "uid", "err")
+    __slots__ = ("rv", "cls", "finished", "sort_key", "gvk", "active_ref", "history_entry", "obj", "name", "uid",
+                 "err")
 
-    def __init__(self, rv: str, cls: Optional[Classification], sort_key: Any, gvk: GroupVersionKind):
+    def __init__(self, rv: str, cls: Optional[Classification], sort_key: Any, gvk: Optional[GroupVersionKind]):
         self.rv = rv
         self.cls = cls
-        self.sort_key = sort_key
+        self.finished = cls is not None and cls.finished
+        self.sort_key = sort_key  # None: not computed (the caller sorts by the object's creation time)
         self.gvk = gvk
         self.active_ref: Optional[ObjectReference] = None
         self.history_entry: Optional[CronHistory] = None
@@ -166,8 +168,9 @@ def child_info(w: Dict[str, Any], gvk: GroupVersionKind, policy: WorkloadPolicy)
     return info
 
 
-# (child object, its classification, its memo record when the classification cache is on)
-Child = Tuple[Dict[str, Any], Classification, Optional[_ChildInfo]]
+# A child as the status sync sees it: its object (``obj``), classification (``cls``/``finished``)
+# and, with the classification cache, the memo record shared across reconciles
+Child = _ChildInfo
 
 
 def slim_child(obj: Dict[str, Any]) -> Dict[str, Any]:
@@ -582,18 +585,20 @@ class CronReconciler(Reconciler):
             if len(infos) > 1:
                 infos.sort(key=_SORT_KEY)
             presorted = True
-            for info in infos:
-                if info.err is not None:
-                    log.error(info.err, f"Failed to get {gvk.kind} status")
-                    continue
-                (terminated if info.cls.finished else active).append((info.obj, info.cls, info))  # type: ignore
+            # a child whose status cannot be read (info.err) is never finished
+            terminated = [i for i in infos if i.finished]
+            if len(terminated) < len(infos):
+                active = [i for i in infos if not i.finished and i.err is None]
+                for info in infos:
+                    if info.err is not None:
+                        log.error(info.err, f"Failed to get {gvk.kind} status")
         else:
             presorted = False
         cache = self._class_cache if self.opts.classification_cache else None
         for w in workloads:
+            m = w.get("metadata") or {}
             try:
                 if cache is not None:
-                    m = w.get("metadata") or {}
                     uid, rv = m.get("uid", ""), m.get("resourceVersion", "")
                     info = cache.get(uid)
                     if info is None or info.rv != rv:
@@ -602,14 +607,14 @@ class CronReconciler(Reconciler):
                         if len(cache) > 500_000:
                             cache.clear()
                         cache[uid] = info
-                    c = info.cls
                 else:
-                    info = None
-                    c = classify(w, gvk, policy)
+                    info = _ChildInfo("", classify(w, gvk, policy), None, None)
             except kf.ConversionError as e:
                 log.error(e, f"Failed to get {gvk.kind} status")
                 continue
-            (terminated if c.finished else active).append((w, c, info))
+            info.obj = w  # this reconcile's copy (a live LIST returns new objects every time)
+            info.name = m.get("name", "")
+            (terminated if info.finished else active).append(info)
         chatty = log.enabled()  # info logging on: skip building messages nobody writes otherwise
         if chatty:
             log.info(f"{gvk.kind} count", active=len(active), terminated=len(terminated))
@@ -672,8 +677,8 @@ class CronReconciler(Reconciler):
 
         # B16 (cron_controller.go:210-220)
         if cron.spec.concurrency_policy == ConcurrentPolicyReplace:
-            for w, _, _ in active:
-                m = w.get("metadata") or {}
+            for info in active:
+                m = info.obj.get("metadata") or {}  # type: ignore[union-attr]
                 ref = ObjectRef(m.get("namespace", ""), m.get("name", ""))
                 log.info(f"Deleting active {gvk.kind}", **{gvk.kind: ref})
                 uid = m.get("uid", "")
@@ -769,9 +774,8 @@ class CronReconciler(Reconciler):
         except ScheduleError:
             return False
         for lst in (active, terminated):
-            for w, _, info in lst:
-                if (info.name if info is not None and info.obj is w else
-                        (w.get("metadata") or {}).get("name")) == ran_name:
+            for info in lst:
+                if info.name == ran_name:
                     return True
         return False
 
@@ -880,10 +884,10 @@ class CronReconciler(Reconciler):
     @staticmethod
     def _sort(items: List[Child]) -> None:
         """``sortByCreationTimestamp`` (``cron_util.go:116-129``): stable, oldest first."""
-        if all(x[2] is not None for x in items):
-            items.sort(key=lambda x: x[2].sort_key)  # type: ignore[union-attr]
+        if all(x.sort_key is not None for x in items):
+            items.sort(key=_SORT_KEY)
         else:
-            items.sort(key=lambda x: creation_timestamp(x[0]).key())
+            items.sort(key=lambda x: creation_timestamp(x.obj).key())  # type: ignore[arg-type]
 
     def sync_active_list(self, cron: Cron, gvk: GroupVersionKind, active: List[Child],
                          log: Logger, presorted: bool = False) -> None:
@@ -894,17 +898,16 @@ class CronReconciler(Reconciler):
             self._sort(active)
         refs = []
         with_rv = self.opts.active_ref_resource_version
-        for w, _, info in active:
-            if info is not None and info.active_ref is not None:
-                refs.append(info.active_ref)
-                continue
-            m = w.get("metadata") or {}
-            wgvk = GroupVersionKind.from_object(w)
-            ref = ObjectReference(api_version=wgvk.api_version, kind=wgvk.kind, name=m.get("name", ""),
-                                  namespace=m.get("namespace", ""), uid=m.get("uid", ""),
-                                  resource_version=m.get("resourceVersion", "") if with_rv else "")
-            if info is not None:
-                info.active_ref = ref
+        for info in active:
+            ref = info.active_ref
+            if ref is None:
+                w = info.obj
+                m = w.get("metadata") or {}  # type: ignore[union-attr]
+                wgvk = GroupVersionKind.from_object(w)  # type: ignore[arg-type]
+                ref = info.active_ref = ObjectReference(
+                    api_version=wgvk.api_version, kind=wgvk.kind, name=m.get("name", ""),
+                    namespace=m.get("namespace", ""), uid=m.get("uid", ""),
+                    resource_version=m.get("resourceVersion", "") if with_rv else "")
             refs.append(ref)
         cron.status.active = refs
 
@@ -931,8 +934,9 @@ class CronReconciler(Reconciler):
         limit = cron.spec.history_limit if cron.spec.history_limit is not None else MAX_INT
         cut = len(terminated) - limit  # the oldest `cut` children are beyond the history limit
         if cut > 0:
-            for w, _, _ in terminated[:cut]:
-                m = w.get("metadata") or {}
+            for info in terminated[:cut]:
+                w = info.obj
+                m = w.get("metadata") or {}  # type: ignore[union-attr]
                 wgvk = GroupVersionKind.from_object(w)
                 ref = ObjectRef(m.get("namespace", ""), m.get("name", ""))
                 if chatty:
@@ -947,20 +951,20 @@ class CronReconciler(Reconciler):
             terminated = terminated[cut:]
         if self.opts.finished_time != "now":
             # the steady state: every kept child's entry was built for its current version
-            history: List[CronHistory] = [e if info is not None and (e := info.history_entry) is not None
-                                          else self._history_entry(cron, w, c, info, None)
-                                          for w, c, info in terminated]
+            history: List[CronHistory] = [info.history_entry or self._history_entry(cron, info, None)
+                                          for info in terminated]
         else:
             now = self.clock.now(LOCAL)
-            history = [self._history_entry(cron, w, c, None, now) for w, c, _ in terminated]
+            history = [self._history_entry(cron, info, now) for info in terminated]
         cron.status.history = history
         return ops
 
-    def _history_entry(self, cron: Cron, w: Dict[str, Any], c: Classification, info: Optional[_ChildInfo],
-                       now: Optional[GoTime]) -> CronHistory:
-        """The ``status.history`` entry of terminated child ``w`` (``cron_controller.go:336-343``).
+    def _history_entry(self, cron: Cron, info: _ChildInfo, now: Optional[GoTime]) -> CronHistory:
+        """The ``status.history`` entry of terminated child ``info`` (``cron_controller.go:336-343``).
         ``now``: ``finished_time="now"`` (the reference stamps every entry with the reconcile's
         time).  An entry fully determined by the child's version is remembered in ``info``."""
+        w: Dict[str, Any] = info.obj  # type: ignore[assignment]
+        c: Classification = info.cls  # type: ignore[assignment]
         m = w.get("metadata") or {}
         wgvk = GroupVersionKind.from_object(w)
         entry = CronHistory(uid=m.get("uid", ""),
@@ -972,8 +976,7 @@ class CronReconciler(Reconciler):
                 entry.finished = now
             elif c.finished_at is not None:
                 entry.finished = c.finished_at
-                if info is not None:  # fully determined by this child version
-                    info.history_entry = entry
+                info.history_entry = entry  # fully determined by this child version
             else:
                 # only a child without a completion time needs the previous entries (the last
                 # entry with its uid, as a uid -> entry map of them would hold)

@@ -21,6 +21,9 @@ def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--fires", type=int, default=200)
     ap.add_argument("--top", type=int, default=0, help="also list the functions executing the most bytecodes")
+    ap.add_argument("--bench", type=int, default=0, metavar="CRONS",
+                    help="count the whole operator process of the headline bench instead (one process, CRONS "
+                         "Crons, 3 timed steps; the fake apiserver's own process is not counted)")
     a = ap.parse_args()
     import cProfile
 
@@ -56,6 +59,33 @@ def main() -> int:
         def disable(self):
             sys.settrace(None)
             sys.setprofile(None)
+
+    if a.bench:
+        from cron_operator_amd.bench import harness
+
+        steps, warmup = 3, 2
+        win = P()
+
+        def on_step(k: int, dt: float, timed: bool) -> None:
+            if k == warmup:
+                win.enable()
+            elif k == warmup + steps:
+                win.disable()
+
+        harness.run_sync(harness.BenchConfig(n_crons=a.bench, steps=steps, warmup=warmup, history_limit=10,
+                                             transport="http", shards=1), on_step=on_step)
+        fires = a.bench * steps
+        print(f"per fire: {counts['op'] / fires:.0f} bytecodes, {counts['ccall'] / fires:.0f} C calls", flush=True)
+        for co, n in by_code.most_common(a.top):
+            fn = co.co_filename.replace(ROOT + "/", "")
+            print(f"{n / fires:8.0f}  {fn}:{co.co_firstlineno}({co.co_name})")
+        by_file: "collections.Counter[str]" = collections.Counter()
+        for co, n in by_code.items():
+            by_file[co.co_filename.replace(ROOT + "/", "")] += n
+        print("\n## by source file (share of all bytecodes)")
+        for fn, n in by_file.most_common(a.top and 25):
+            print(f"{n / fires:8.0f}  {100.0 * n / max(1, counts['op']):5.1f}%  {fn}")
+        return 0
 
     cProfile.Profile = P  # type: ignore[misc]
 
