@@ -44,7 +44,9 @@
 #include <unistd.h>
 
 #include <cstring>
+#include <ctime>
 #include <string>
+#include <vector>
 
 #include "httpframe.h"
 
@@ -108,6 +110,7 @@ struct ConnObject {
   PyObject* waiter;    // stream mode: wait() future
   PyObject* stream_error;
   PyObject* weakrefs;
+  PyObject* pool;      // the Pool whose request is in flight here (strong; set only while busy)
   long used;           // requests sent on this connection
   long ssl_gen;        // pool bookkeeping (TLS context generation)
   double deadline;     // pool bookkeeping (loop time the in-flight response is due by)
@@ -117,6 +120,29 @@ struct ConnObject {
   bool writer_on;
   bool stream_done;
 };
+
+// A keep-alive pool of request-mode connections to one server (`_netconn.Pool`): the request
+// path of runtime/fasthttp.py's HttpPool -- build the request head, take an idle connection,
+// send, and give the connection back when its response completes -- without a Python frame.
+struct PoolObject {
+  PyObject_HEAD
+  std::vector<ConnObject*>* idle;  // strong references; the most recently used at the back
+  std::vector<ConnObject*>* busy;  // strong references; each has `pool` set to this pool
+  std::string* target;             // request-target prefix (base path, or absolute form via a proxy)
+  std::string* fixed;              // header lines sent with every request (Host, auth, ...)
+  Py_ssize_t max_idle;
+  double timeout;                  // seconds a response may take (deadline sweep)
+  long ssl_gen;                    // connections of another TLS generation are not reused
+  bool closed;
+  PyObject* weakrefs;
+};
+
+PyObject* g_timeout_error = nullptr;  // asyncio.TimeoutError, for the deadline sweep
+
+// The exchange on `s` ended (response completed or connection lost): leave the pool's busy
+// list, and go back to the idle list when reusable (closed otherwise).  May drop the last
+// reference to `s`: callers hold their own.
+void pool_release(ConnObject* s);
 
 // ----------------------------------------------------------------------------- helpers
 
@@ -346,6 +372,7 @@ void finish_response(ConnObject* s, const char* b, size_t n) {
   if (close_after) close_io(s);
   PyObject* fut = s->fut;
   s->fut = nullptr;
+  pool_release(s);  // idle again before the caller resumes
   if (result) resolve(fut, result);
   else {
     PyObject* exc = conn_failed("out of memory decoding the response", false, false);
@@ -610,10 +637,12 @@ void lost(ConnObject* s, const std::string& why) {
     PyObject* f = s->fut;
     s->fut = nullptr;
     PyObject* exc = conn_failed("connection lost: " + why, !s->got_any, s->used > 1);
+    pool_release(s);
     reject(f, exc);
     Py_XDECREF(exc);
     Py_DECREF(f);
   }
+  pool_release(s);
 }
 
 // Write what is buffered.  false: the connection broke (already handled).
@@ -717,6 +746,7 @@ void read_ready(ConnObject* s) {
           PyObject* f = s->fut;
           s->fut = nullptr;
           PyObject* exc = conn_failed("bad HTTP response", false, false);
+          pool_release(s);
           reject(f, exc);
           Py_XDECREF(exc);
           Py_DECREF(f);
@@ -864,6 +894,7 @@ int conn_traverse(ConnObject* self, visitproc visit, void* arg) {
   Py_VISIT(self->items);
   Py_VISIT(self->waiter);
   Py_VISIT(self->stream_error);
+  Py_VISIT(self->pool);
   return 0;
 }
 
@@ -876,6 +907,7 @@ int conn_clear(ConnObject* self) {
   Py_CLEAR(self->stream_error);
   Py_CLEAR(self->ssl_ctx);
   Py_CLEAR(self->loop);
+  Py_CLEAR(self->pool);
   return 0;
 }
 
@@ -1059,6 +1091,7 @@ PyObject* conn_close(ConnObject* self, PyObject*) {
     Py_XDECREF(exc);
     Py_DECREF(f);
   }
+  pool_release(self);
   Py_DECREF(self);
   Py_RETURN_NONE;
 }
@@ -1198,16 +1231,376 @@ PyTypeObject ConnType = {
     sizeof(ConnObject),                    /* tp_basicsize */
 };
 
+// ----------------------------------------------------------------------------- the pool
+
+double monotonic_now() {  // asyncio's loop.time() is time.monotonic(): CLOCK_MONOTONIC
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return static_cast<double>(ts.tv_sec) + static_cast<double>(ts.tv_nsec) * 1e-9;
+}
+
+void pool_release(ConnObject* s) {
+  PoolObject* p = reinterpret_cast<PoolObject*>(s->pool);
+  if (!p) return;
+  s->pool = nullptr;  // our reference to p, released at the end
+  std::vector<ConnObject*>& busy = *p->busy;
+  bool owned = false;  // the busy list's reference to s
+  for (size_t i = 0; i < busy.size(); ++i)
+    if (busy[i] == s) {
+      busy[i] = busy.back();
+      busy.pop_back();
+      owned = true;
+      break;
+    }
+  if (owned) {
+    if (s->alive && s->fd >= 0 && !s->fut && !p->closed && s->ssl_gen == p->ssl_gen &&
+        static_cast<Py_ssize_t>(p->idle->size()) < p->max_idle) {
+      p->idle->push_back(s);  // the reference moves to the idle list
+    } else {
+      close_io(s);
+      Py_DECREF(s);
+    }
+  }
+  Py_DECREF(p);
+}
+
+// The latin-1 bytes of str `o` appended to `out` (the encoding of the Python request head).
+bool append_latin1(std::string* out, PyObject* o) {
+  if (!PyUnicode_Check(o)) {
+    PyErr_SetString(PyExc_TypeError, "expected str");
+    return false;
+  }
+  if (PyUnicode_IS_COMPACT_ASCII(o)) {
+    out->append(reinterpret_cast<const char*>(PyUnicode_DATA(o)), static_cast<size_t>(PyUnicode_GET_LENGTH(o)));
+    return true;
+  }
+  PyObject* b = PyUnicode_AsLatin1String(o);
+  if (!b) return false;
+  out->append(PyBytes_AS_STRING(b), static_cast<size_t>(PyBytes_GET_SIZE(b)));
+  Py_DECREF(b);
+  return true;
+}
+
+// The request: "<method> <target><path> HTTP/1.1", the fixed headers, Accept, and the body
+// with its Content-Type and Content-Length (POST/PUT/PATCH without a body send length 0).
+bool build_request(PoolObject* p, PyObject* const* a, std::string* out) {
+  PyObject *method = a[0], *path = a[1], *body = a[2], *ctype = a[3], *accept = a[4];
+  Py_buffer view;
+  const bool has_body = body != Py_None;
+  if (has_body && PyObject_GetBuffer(body, &view, PyBUF_SIMPLE) < 0) return false;
+  out->reserve(256 + p->fixed->size() + (has_body ? static_cast<size_t>(view.len) : 0));
+  bool ok = append_latin1(out, method);
+  if (ok) {
+    out->push_back(' ');
+    out->append(*p->target);
+    ok = append_latin1(out, path);
+  }
+  if (ok) {
+    out->append(" HTTP/1.1\r\n");
+    out->append(*p->fixed);
+    out->append("Accept: ");
+    ok = append_latin1(out, accept);
+  }
+  if (ok) {
+    out->append("\r\n");
+    if (has_body) {
+      out->append("Content-Type: ");
+      ok = append_latin1(out, ctype);
+      if (ok) {
+        out->append("\r\nContent-Length: ");
+        out->append(std::to_string(view.len));
+        out->append("\r\n\r\n");
+        out->append(static_cast<const char*>(view.buf), static_cast<size_t>(view.len));
+      }
+    } else {
+      const char* m = PyUnicode_Check(method) ? PyUnicode_AsUTF8(method) : nullptr;
+      if (!m) ok = false;
+      else if (!std::strcmp(m, "POST") || !std::strcmp(m, "PUT") || !std::strcmp(m, "PATCH"))
+        out->append("Content-Length: 0\r\n\r\n");
+      else out->append("\r\n");
+    }
+  }
+  if (has_body) PyBuffer_Release(&view);
+  return ok;
+}
+
+// Send `req` on `c` (request mode, nothing in flight) as a request of pool `p`: `c` joins the
+// busy list (taking over the caller's reference) until its response completes.
+PyObject* pool_start(PoolObject* p, ConnObject* c, const std::string& req) {
+  PyObject* f = new_future(c);
+  if (!f) {
+    Py_DECREF(c);
+    return nullptr;
+  }
+  Py_INCREF(f);
+  c->fut = f;
+  c->used += 1;
+  c->got_any = false;
+  c->deadline = monotonic_now() + p->timeout;
+  Py_INCREF(p);
+  c->pool = reinterpret_cast<PyObject*>(p);
+  p->busy->push_back(c);  // the caller's reference
+  Py_INCREF(c);           // ours, while we write (a failed write releases it from the pool)
+  c->core->wbuf.append(req);
+  if (!c->writer_on) flush(c);
+  Py_DECREF(c);
+  return f;
+}
+
+PyObject* pool_new(PyTypeObject* type, PyObject*, PyObject*) {
+  PoolObject* self = reinterpret_cast<PoolObject*>(type->tp_alloc(type, 0));
+  if (!self) return nullptr;
+  self->idle = new std::vector<ConnObject*>();
+  self->busy = new std::vector<ConnObject*>();
+  self->target = new std::string();
+  self->fixed = new std::string();
+  self->max_idle = 64;
+  self->timeout = 60.0;
+  return reinterpret_cast<PyObject*>(self);
+}
+
+// Pool(max_idle, timeout)
+int pool_init(PoolObject* self, PyObject* args, PyObject* kw) {
+  static const char* kwlist[] = {"max_idle", "timeout", nullptr};
+  Py_ssize_t max_idle = 64;
+  double timeout = 60.0;
+  if (!PyArg_ParseTupleAndKeywords(args, kw, "|nd", const_cast<char**>(kwlist), &max_idle, &timeout)) return -1;
+  self->max_idle = max_idle;
+  self->timeout = timeout;
+  return 0;
+}
+
+// Drop every connection the pool holds (idle ones are closed; busy ones are closed too, their
+// requests failing like a lost connection).
+void pool_drop_all(PoolObject* self, bool busy_too) {
+  std::vector<ConnObject*> idle;
+  idle.swap(*self->idle);
+  for (ConnObject* c : idle) {
+    close_io(c);
+    Py_DECREF(c);
+  }
+  if (!busy_too) return;
+  while (!self->busy->empty()) {
+    ConnObject* c = self->busy->back();
+    Py_INCREF(c);
+    if (c->pool) lost(c, "pool closed");  // releases c from the busy list
+    else {
+      self->busy->pop_back();  // cannot happen (busy entries point back here): keep the list finite
+      Py_DECREF(c);
+    }
+    Py_DECREF(c);
+  }
+}
+
+int pool_traverse(PoolObject* self, visitproc visit, void* arg) {
+  if (self->idle)
+    for (ConnObject* c : *self->idle) Py_VISIT(c);
+  if (self->busy)
+    for (ConnObject* c : *self->busy) Py_VISIT(c);
+  return 0;
+}
+
+int pool_clear(PoolObject* self) {
+  if (self->idle) {
+    std::vector<ConnObject*> v;
+    v.swap(*self->idle);
+    for (ConnObject* c : v) Py_DECREF(c);
+  }
+  if (self->busy) {
+    std::vector<ConnObject*> v;
+    v.swap(*self->busy);
+    for (ConnObject* c : v) Py_DECREF(c);
+  }
+  return 0;
+}
+
+void pool_dealloc(PoolObject* self) {
+  PyObject_GC_UnTrack(self);
+  if (self->weakrefs) PyObject_ClearWeakRefs(reinterpret_cast<PyObject*>(self));
+  pool_clear(self);
+  delete self->idle;
+  delete self->busy;
+  delete self->target;
+  delete self->fixed;
+  Py_TYPE(self)->tp_free(reinterpret_cast<PyObject*>(self));
+}
+
+// request(method, path, body, content_type, accept) -> Future[(status, body, retry_after)] | None
+// (None: no idle connection -- the caller connects one and uses request_on)
+PyObject* pool_request(PoolObject* self, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 5) {
+    PyErr_SetString(PyExc_TypeError, "request(method, path, body, content_type, accept)");
+    return nullptr;
+  }
+  ConnObject* c = nullptr;
+  while (!self->idle->empty()) {
+    ConnObject* t = self->idle->back();
+    self->idle->pop_back();
+    if (t->alive && t->fd >= 0 && !t->fut && t->core) {
+      c = t;
+      break;
+    }
+    close_io(t);
+    Py_DECREF(t);
+  }
+  if (!c) Py_RETURN_NONE;
+  std::string req;
+  if (!build_request(self, args, &req)) {
+    self->idle->push_back(c);  // unused: back where it was
+    return nullptr;
+  }
+  return pool_start(self, c, req);
+}
+
+// request_on(conn, method, path, body, content_type, accept) -> Future: the same on a fresh connection
+PyObject* pool_request_on(PoolObject* self, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 6 || !PyObject_TypeCheck(args[0], &ConnType)) {
+    PyErr_SetString(PyExc_TypeError, "request_on(conn, method, path, body, content_type, accept)");
+    return nullptr;
+  }
+  ConnObject* c = reinterpret_cast<ConnObject*>(args[0]);
+  if (!check_ready(c)) return nullptr;
+  if (c->mode != kRequest || c->fut || c->pool) {
+    PyErr_SetString(PyExc_RuntimeError, "request_on() needs an idle request connection");
+    return nullptr;
+  }
+  std::string req;
+  if (!build_request(self, args + 1, &req)) return nullptr;
+  if (c->fd < 0 || !c->alive) return failed_future(c, conn_failed("connection is closed", true, c->used > 0));
+  Py_INCREF(c);
+  return pool_start(self, c, req);
+}
+
+// sweep(now) -> int: fail the requests whose deadline passed (asyncio.TimeoutError, connection
+// closed); returns how many are still in flight
+PyObject* pool_sweep(PoolObject* self, PyObject* arg) {
+  const double now = PyFloat_AsDouble(arg);
+  if (now == -1.0 && PyErr_Occurred()) return nullptr;
+  std::vector<ConnObject*> late;
+  for (ConnObject* c : *self->busy)
+    if (c->deadline <= now) {
+      Py_INCREF(c);
+      late.push_back(c);
+    }
+  for (ConnObject* c : late) {
+    PyObject* f = c->fut;
+    c->fut = nullptr;
+    close_io(c);
+    pool_release(c);
+    if (f) {
+      PyObject* exc = g_timeout_error ? PyObject_CallNoArgs(g_timeout_error) : nullptr;
+      reject(f, exc);
+      Py_XDECREF(exc);
+      Py_DECREF(f);
+    }
+    Py_DECREF(c);
+  }
+  return PyLong_FromSsize_t(static_cast<Py_ssize_t>(self->busy->size()));
+}
+
+// discard(fut): the request of `fut` was abandoned (its caller was cancelled): close its connection
+PyObject* pool_discard(PoolObject* self, PyObject* fut) {
+  for (ConnObject* c : *self->busy)
+    if (c->fut == fut) {
+      Py_INCREF(c);
+      lost(c, "request abandoned");
+      Py_DECREF(c);
+      break;
+    }
+  Py_RETURN_NONE;
+}
+
+// set_fixed(target, fixed): the request-target prefix and the header lines of every request
+PyObject* pool_set_fixed(PoolObject* self, PyObject* args) {
+  PyObject *target, *fixed;
+  if (!PyArg_ParseTuple(args, "UU", &target, &fixed)) return nullptr;
+  std::string t, f;
+  if (!append_latin1(&t, target) || !append_latin1(&f, fixed)) return nullptr;
+  self->target->swap(t);
+  self->fixed->swap(f);
+  Py_RETURN_NONE;
+}
+
+// close_idle(): close the idle connections (a rotated TLS context; busy ones close when done)
+PyObject* pool_close_idle(PoolObject* self, PyObject*) {
+  pool_drop_all(self, false);
+  Py_RETURN_NONE;
+}
+
+// close(): no more reuse; idle connections close now, busy ones when their response completes
+PyObject* pool_close(PoolObject* self, PyObject*) {
+  self->closed = true;
+  pool_drop_all(self, false);
+  Py_RETURN_NONE;
+}
+
+// abort(): close every connection, failing the requests in flight
+PyObject* pool_abort(PoolObject* self, PyObject*) {
+  self->closed = true;
+  pool_drop_all(self, true);
+  Py_RETURN_NONE;
+}
+
+PyObject* pool_idle(PoolObject* self, PyObject*) {
+  PyObject* out = PyList_New(static_cast<Py_ssize_t>(self->idle->size()));
+  if (!out) return nullptr;
+  for (size_t i = 0; i < self->idle->size(); ++i) {
+    PyObject* c = reinterpret_cast<PyObject*>((*self->idle)[i]);
+    Py_INCREF(c);
+    PyList_SET_ITEM(out, static_cast<Py_ssize_t>(i), c);
+  }
+  return out;
+}
+
+PyObject* pool_get_busy(PoolObject* self, void*) { return PyLong_FromSize_t(self->busy->size()); }
+PyObject* pool_get_closed(PoolObject* self, void*) { return PyBool_FromLong(self->closed); }
+
+PyMethodDef kPoolMethods[] = {
+    {"request", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(pool_request)), METH_FASTCALL,
+     "request(method, path, body, content_type, accept) -> Future | None (no idle connection)"},
+    {"request_on", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(pool_request_on)), METH_FASTCALL,
+     "request_on(conn, method, path, body, content_type, accept) -> Future"},
+    {"sweep", reinterpret_cast<PyCFunction>(pool_sweep), METH_O, "sweep(now) -> requests still in flight"},
+    {"discard", reinterpret_cast<PyCFunction>(pool_discard), METH_O, "discard(fut): close its connection"},
+    {"set_fixed", reinterpret_cast<PyCFunction>(pool_set_fixed), METH_VARARGS, "set_fixed(target, fixed)"},
+    {"close_idle", reinterpret_cast<PyCFunction>(pool_close_idle), METH_NOARGS, "close the idle connections"},
+    {"close", reinterpret_cast<PyCFunction>(pool_close), METH_NOARGS, "stop reusing connections"},
+    {"abort", reinterpret_cast<PyCFunction>(pool_abort), METH_NOARGS, "close everything, failing requests"},
+    {"idle", reinterpret_cast<PyCFunction>(pool_idle), METH_NOARGS, "idle() -> list of idle connections"},
+    {nullptr, nullptr, 0, nullptr},
+};
+
+PyGetSetDef kPoolGetSet[] = {
+    {"busy", reinterpret_cast<getter>(pool_get_busy), nullptr, "requests in flight", nullptr},
+    {"closed", reinterpret_cast<getter>(pool_get_closed), nullptr, "close() was called", nullptr},
+    {nullptr, nullptr, nullptr, nullptr, nullptr},
+};
+
+PyMemberDef kPoolMembers[] = {
+    {"ssl_gen", T_LONG, offsetof(PoolObject, ssl_gen), 0, "TLS context generation of reusable connections"},
+    {"max_idle", T_PYSSIZET, offsetof(PoolObject, max_idle), 0, "idle connections kept"},
+    {"timeout", T_DOUBLE, offsetof(PoolObject, timeout), 0, "seconds a response may take"},
+    {nullptr, 0, 0, 0, nullptr},
+};
+
+PyTypeObject PoolType = {
+    PyVarObject_HEAD_INIT(nullptr, 0)
+    "_netconn.Pool",                       /* tp_name */
+    sizeof(PoolObject),                    /* tp_basicsize */
+};
+
 // configure(ConnectionFailed, HttpStatusError, SSLError)
 PyObject* configure(PyObject*, PyObject* args) {
-  PyObject *cf, *se, *sslerr;
-  if (!PyArg_ParseTuple(args, "OOO", &cf, &se, &sslerr)) return nullptr;
+  PyObject *cf, *se, *sslerr, *te = nullptr;
+  if (!PyArg_ParseTuple(args, "OOO|O", &cf, &se, &sslerr, &te)) return nullptr;
   Py_INCREF(cf);
   Py_INCREF(se);
   Py_INCREF(sslerr);
+  Py_XINCREF(te);
   Py_XSETREF(g_conn_failed, cf);
   Py_XSETREF(g_status_error, se);
   Py_XSETREF(g_ssl_error, sslerr);
+  Py_XSETREF(g_timeout_error, te);
   Py_RETURN_NONE;
 }
 
@@ -1219,7 +1612,8 @@ PyObject* ssl_context_supported(PyObject*, PyObject* ctx) {
 }
 
 PyMethodDef kMethods[] = {
-    {"configure", configure, METH_VARARGS, "configure(ConnectionFailed, HttpStatusError, SSLError)"},
+    {"configure", configure, METH_VARARGS,
+     "configure(ConnectionFailed, HttpStatusError, SSLError[, TimeoutError])"},
     {"ssl_context_supported", ssl_context_supported, METH_O,
      "ssl_context_supported(ctx) -> bool: the SSLContext's SSL_CTX can be used natively"},
     {nullptr, nullptr, 0, nullptr},
@@ -1255,11 +1649,29 @@ PyMODINIT_FUNC PyInit__netconn(void) {
   ConnType.tp_init = reinterpret_cast<initproc>(conn_init);
   ConnType.tp_new = conn_new;
   if (PyType_Ready(&ConnType) < 0) return nullptr;
+  PoolType.tp_dealloc = reinterpret_cast<destructor>(pool_dealloc);
+  PoolType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_GC;
+  PoolType.tp_doc = "Keep-alive pool of native connections to one server: request path in C++.";
+  PoolType.tp_traverse = reinterpret_cast<traverseproc>(pool_traverse);
+  PoolType.tp_clear = reinterpret_cast<inquiry>(pool_clear);
+  PoolType.tp_weaklistoffset = offsetof(PoolObject, weakrefs);
+  PoolType.tp_methods = kPoolMethods;
+  PoolType.tp_members = kPoolMembers;
+  PoolType.tp_getset = kPoolGetSet;
+  PoolType.tp_init = reinterpret_cast<initproc>(pool_init);
+  PoolType.tp_new = pool_new;
+  if (PyType_Ready(&PoolType) < 0) return nullptr;
   PyObject* m = PyModule_Create(&kModule);
   if (!m) return nullptr;
   Py_INCREF(&ConnType);
   if (PyModule_AddObject(m, "Conn", reinterpret_cast<PyObject*>(&ConnType)) < 0) {
     Py_DECREF(&ConnType);
+    Py_DECREF(m);
+    return nullptr;
+  }
+  Py_INCREF(&PoolType);
+  if (PyModule_AddObject(m, "Pool", reinterpret_cast<PyObject*>(&PoolType)) < 0) {
+    Py_DECREF(&PoolType);
     Py_DECREF(m);
     return nullptr;
   }

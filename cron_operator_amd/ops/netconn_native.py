@@ -35,11 +35,12 @@ def load():
                     if _build.needs_build("_netconn"):
                         _build.build_extension("_netconn")
                     m = importlib.import_module("cron_operator_amd.ops._netconn")
+                    import asyncio
                     import ssl
 
                     from ..runtime.fasthttp import ConnectionFailed, HttpStatusError
 
-                    m.configure(ConnectionFailed, HttpStatusError, ssl.SSLError)
+                    m.configure(ConnectionFailed, HttpStatusError, ssl.SSLError, asyncio.TimeoutError)
                     _mod = m
                 except Exception:  # noqa: BLE001 - the asyncio protocols remain
                     if want == "native":

@@ -290,8 +290,7 @@ class Client:
         self.url_base = getattr(cfg, "host", "") if cfg is not None else ""
         self.requests = 0
         self.requests_by_verb: Dict[str, int] = {}
-        self._m_req: Dict[Tuple[str, str], Any] = {}
-        self._m_lat: Dict[str, Any] = {}
+        self._m_verb: Dict[str, Tuple[Dict[str, Any], Any]] = {}  # verb -> ({code: counter}, latency histogram)
         self._m_rl: Dict[str, Any] = {}
 
     # -- plumbing
@@ -346,32 +345,51 @@ class Client:
         if self.limiter is not None:
             await self._throttle(verb, gvr, namespace, name, subresource)
         self.requests += 1
-        self.requests_by_verb[verb] = self.requests_by_verb.get(verb, 0) + 1
+        rbv = self.requests_by_verb
+        rbv[verb] = rbv.get(verb, 0) + 1
+        if tracing.get_tracer().enabled:
+            return await self._do_traced(verb, gvr, namespace, name, subresource, body, params)
         t0 = time.perf_counter()
         code = "200"
-        sp = tracing.span("http." + verb, resource=gvr.resource + ("/" + subresource if subresource else ""),
-                          namespace=namespace, name=name) if tracing.get_tracer().enabled else tracing.NOOP
         try:
-            with sp:
-                return await self.transport.request(verb, gvr, namespace, name, subresource, body, params)
+            return await self.transport.request(verb, gvr, namespace, name, subresource, body, params)
         except errors.ApiError as e:
             code = str(e.code)
-            sp.set(code=e.code)
             raise
         except Exception:
             code = "<error>"
             raise
         finally:
-            key = (code, verb)
-            m = self._m_req.get(key)
-            if m is None:
-                m = self._m_req[key] = metrics.REST_REQUESTS.labels(code, self.host,
-                                                                    self._METHOD.get(verb, verb.upper()))
-            m.inc()
-            lm = self._m_lat.get(verb)
-            if lm is None:
-                lm = self._m_lat[verb] = metrics.REST_LATENCY.labels(verb.upper(), self.host)
-            lm.observe(time.perf_counter() - t0)
+            self._observe(code, verb, t0)
+
+    async def _do_traced(self, verb: str, gvr: GroupVersionResource, namespace: str, name: str, subresource: str,
+                         body: Any, params: Optional[Dict[str, Any]]) -> Any:
+        t0 = time.perf_counter()
+        code = "200"
+        with tracing.span("http." + verb, resource=gvr.resource + ("/" + subresource if subresource else ""),
+                          namespace=namespace, name=name) as sp:
+            try:
+                return await self.transport.request(verb, gvr, namespace, name, subresource, body, params)
+            except errors.ApiError as e:
+                code = str(e.code)
+                sp.set(code=e.code)
+                raise
+            except Exception:
+                code = "<error>"
+                raise
+            finally:
+                self._observe(code, verb, t0)
+
+    def _observe(self, code: str, verb: str, t0: float) -> None:
+        """``rest_client_requests_total`` and ``rest_client_request_duration_seconds``."""
+        ms = self._m_verb.get(verb)
+        if ms is None:
+            ms = self._m_verb[verb] = ({}, metrics.REST_LATENCY.labels(verb.upper(), self.host))
+        m = ms[0].get(code)
+        if m is None:
+            m = ms[0][code] = metrics.REST_REQUESTS.labels(code, self.host, self._METHOD.get(verb, verb.upper()))
+        m.inc()
+        ms[1].observe(time.perf_counter() - t0)
 
     # -- verbs
     async def get(self, target: GVRorGVK, namespace: str, name: str) -> Dict[str, Any]:

@@ -42,7 +42,7 @@ import base64
 import socket as _socket
 import ssl as _ssl
 from collections import deque
-from typing import Deque, Dict, List, Optional, Tuple
+from typing import Any, Deque, Dict, List, Optional, Tuple
 from urllib.parse import unquote, urlsplit
 
 from ..ops import httpcodec_native
@@ -527,8 +527,9 @@ class HttpPool:
                 self._proxy_auth = f"Proxy-Authorization: Basic {base64.b64encode(cred).decode()}\r\n"
             if self.scheme == "http":
                 self._target = f"http://{self._hosthdr}{self.base_path}"
+        self._np = None  # the native pool (request path in C++) when the native connections serve
         self.set_headers(headers)
-        self._idle: Deque[_Conn] = deque()
+        self._pidle: Deque[_Conn] = deque()
         self.max_idle = max_idle
         self.timeout = timeout
         self.connects = 0
@@ -541,6 +542,11 @@ class HttpPool:
         self.native = False
         self._pick_native()
 
+    @property
+    def _idle(self) -> List[Any]:
+        """The idle keep-alive connections (the native pool's, or the asyncio protocols')."""
+        return self._np.idle() if self._np is not None else self._pidle  # type: ignore[return-value]
+
     def _pick_native(self) -> None:
         from ..ops import netconn_native
 
@@ -552,6 +558,14 @@ class HttpPool:
                                f"(extension {'missing' if mod is None else 'loaded'})")
         self._netconn = mod if ok else None
         self.native = ok
+        if ok and self._np is None:
+            self._np = mod.Pool(self.max_idle, self.timeout)
+            self._np.set_fixed(self._target, self._fixed)
+        if self._np is not None:
+            self._np.ssl_gen = self._ssl_gen
+            if not ok:  # the new TLS context needs the asyncio protocols: retire the native pool
+                self._np.close()
+                self._np = None
 
     def set_headers(self, headers: Optional[Dict[str, str]]) -> None:
         """Replace the headers sent with every request (e.g. a rotated ``Authorization``)."""
@@ -561,6 +575,8 @@ class HttpPool:
         if self._proxy is not None and self.scheme == "http":
             extra += self._proxy_auth  # plain requests go to the proxy itself
         self._fixed = f"Host: {self._hosthdr}\r\n{extra}"
+        if self._np is not None:
+            self._np.set_fixed(self._target, self._fixed)
 
     def set_ssl(self, ctx: _ssl.SSLContext) -> None:
         """New connections handshake with ``ctx`` (a rotated client certificate); idle
@@ -568,8 +584,10 @@ class HttpPool:
         self.ssl = ctx
         self._ssl_gen += 1
         self._pick_native()
-        while self._idle:
-            self._idle.pop().close()
+        if self._np is not None:
+            self._np.close_idle()
+        while self._pidle:
+            self._pidle.pop().close()
 
     async def _open(self, factory):
         """A connected protocol from ``factory``: direct, to an http proxy (plain servers), or
@@ -699,16 +717,16 @@ class HttpPool:
         return conn
 
     def _take_idle(self) -> Optional[_Conn]:
-        while self._idle:
-            c = self._idle.pop()
+        while self._pidle:
+            c = self._pidle.pop()
             if c.alive and not c.closing():
                 return c
         return None
 
     def _give_back(self, c: _Conn) -> None:
-        if c.alive and not self._closed and len(self._idle) < self.max_idle and c.fut is None \
+        if c.alive and not self._closed and len(self._pidle) < self.max_idle and c.fut is None \
                 and c.ssl_gen == self._ssl_gen:
-            self._idle.append(c)
+            self._pidle.append(c)
         else:
             c.close()
 
@@ -721,6 +739,30 @@ class HttpPool:
                            content_type: str = "application/json",
                            accept: str = "application/json") -> Tuple[int, bytes, Optional[int]]:
         """``(status, body, Retry-After seconds or None)``."""
+        np = self._np
+        if np is not None:
+            # native pool: head built, idle connection taken, sent, and given back when the
+            # response completes -- all in C++; Python only connects when no connection is idle
+            fut = np.request(method, path, body, content_type, accept)
+            if fut is None:
+                fut = np.request_on(await self._connect(), method, path, body, content_type, accept)
+            if self._sweeper is None:
+                self._sweeper = asyncio.get_running_loop().call_later(self._sweep_every, self._sweep)
+            try:
+                return await fut
+            except ConnectionFailed as e:
+                if not (e.no_response and e.reused):
+                    raise
+            except asyncio.CancelledError:
+                np.discard(fut)  # abandoned mid-exchange: the connection cannot be reused
+                raise
+            # a stale keep-alive connection: once more on a fresh one
+            fut = np.request_on(await self._connect(), method, path, body, content_type, accept)
+            try:
+                return await fut
+            except asyncio.CancelledError:
+                np.discard(fut)
+                raise
         head = f"{method} {self._target}{path} HTTP/1.1\r\n{self._fixed}Accept: {accept}\r\n"
         if body is not None:
             head += f"Content-Type: {content_type}\r\nContent-Length: {len(body)}\r\n\r\n"
@@ -759,14 +801,15 @@ class HttpPool:
     def _sweep(self) -> None:
         """Fail every in-flight request past its deadline; re-arm while any is in flight."""
         self._sweeper = None
-        if not self._busy:
+        np = self._np
+        if not self._busy and (np is None or not np.busy):
             return
         loop = asyncio.get_running_loop()
         now = loop.time()
         for c in [c for c in self._busy if c.deadline <= now]:
             if c.fut is not None:
                 _expire(c.fut)
-        if self._busy:
+        if self._busy or (np is not None and np.sweep(now)):
             self._sweeper = loop.call_later(self._sweep_every, self._sweep)
 
     async def open_stream(self, path: str, decode, accept: str = "application/json") -> Stream:
@@ -800,8 +843,10 @@ class HttpPool:
         if self._sweeper is not None:
             self._sweeper.cancel()
             self._sweeper = None
-        while self._idle:
-            self._idle.pop().close()
+        if self._np is not None:
+            self._np.close()
+        while self._pidle:
+            self._pidle.pop().close()
 
 
 def encode_query(params: Dict[str, str]) -> str:

@@ -95,6 +95,8 @@ class _HttpWatch(WatchStream):
             self._resp.close()
 
 
+_NO_PARAMS: Dict[str, Any] = {}  # read-only
+_COLLECTION_VERBS = frozenset(("list", "create", "deletecollection"))
 _METHODS = {"get": "GET", "list": "GET", "create": "POST", "update": "PUT", "patch": "PATCH",
             "delete": "DELETE", "deletecollection": "DELETE"}
 
@@ -228,23 +230,32 @@ class HttpTransport(Transport):
 
     async def request(self, verb: str, gvr: GroupVersionResource, namespace: str = "", name: str = "",
                       subresource: str = "", body: Any = None, params: Optional[Dict[str, Any]] = None) -> Any:
-        if self.config.exec_provider is not None and self.config.exec_stale():
+        cfg = self.config
+        if cfg.exec_provider is not None and cfg.exec_stale():
             await self._fresh_exec()
-        params = params or {}
+        params = params or _NO_PARAMS
         method = _METHODS[verb]
-        path = resource_path(gvr, namespace, name if verb not in ("list", "create", "deletecollection") else "",
-                             subresource)
+        path = resource_path(gvr, namespace, name if verb not in _COLLECTION_VERBS else "", subresource)
         if self.fast:
-            data = (body if body.__class__ is bytes else jsonutil.dumpb(body)) if body is not None else None
-            ctype = PATCH_CONTENT_TYPES[params.get("patchType", "merge")] if verb == "patch" else "application/json"
-            target = path + encode_query(_clean(params))
+            data = body if body is None or body.__class__ is bytes else jsonutil.dumpb(body)
+            if params:
+                ctype = PATCH_CONTENT_TYPES[params.get("patchType", "merge")] if verb == "patch" else \
+                    "application/json"
+                q = _clean(params)
+                target = path + encode_query(q) if q else path
+                accept = params.get(ACCEPT) or "application/json"
+            else:
+                ctype = PATCH_CONTENT_TYPES["merge"] if verb == "patch" else "application/json"
+                target, accept = path, "application/json"
+            pool = self._pool if self._pool is not None and not cfg.rotating else self._fast_pool()
             attempt = 0
             while True:
-                if attempt and self.config.exec_provider is not None and self.config.exec_stale():
-                    await self._fresh_exec()  # expired while waiting out Retry-After: refresh off the loop
+                if attempt:
+                    if cfg.exec_provider is not None and cfg.exec_stale():
+                        await self._fresh_exec()  # expired while waiting out Retry-After: refresh off the loop
+                    pool = self._fast_pool()  # a token rotated meanwhile is stamped on the retry
                 try:
-                    status, raw, retry_after = await self._fast_pool().request_full(
-                        method, target, data, ctype, params.get(ACCEPT) or "application/json")
+                    status, raw, retry_after = await pool.request_full(method, target, data, ctype, accept)
                 except (ConnectionFailed, OSError, asyncio.TimeoutError) as e:
                     raise errors.ApiError(503, "ServiceUnavailable", f"connection error: {e}") from None
                 if retry_after is None or not (status == 429 or status >= 500) or attempt >= self.max_retries:

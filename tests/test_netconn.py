@@ -405,3 +405,176 @@ async def test_tls_client_certificate_is_presented(tmp_path):
         await anon.close()
     finally:
         srv.close()
+
+
+# ----------------------------------------------------------------------------- the native pool
+
+
+async def _capture_server(responses=None, delay=0.0):
+    """A keep-alive server recording every request's exact bytes (head + body)."""
+    seen = []
+    conns = []
+
+    async def handle(reader, writer):
+        conns.append(writer)
+        try:
+            while True:
+                head, body = await _read_request(reader)
+                seen.append(head + body)
+                if delay:
+                    await asyncio.sleep(delay)
+                payload = b'{"ok":true}'
+                writer.write(b"HTTP/1.1 200 OK\r\nContent-Length: %d\r\n\r\n" % len(payload) + payload)
+                await writer.drain()
+        except (asyncio.IncompleteReadError, ConnectionResetError):
+            writer.close()
+
+    srv, port = await _server(handle)
+    return srv, port, seen, conns
+
+
+async def test_pool_request_bytes_equal_the_python_path():
+    """The request the native pool builds is byte for byte the asyncio path's: target prefix,
+    fixed headers (rotated ones too), Accept, and the body framing of every verb."""
+    srv, port, seen, _ = await _capture_server()
+    calls = [("GET", "/api/v1/namespaces/a/pods?watch=false", None, "application/json", "application/json"),
+             ("POST", "/apis/x/v1/things", b'{"a":1}', "application/json", "application/json"),
+             ("PATCH", "/apis/x/v1/things/a/status", b'{"s":2}', "application/merge-patch+json", "application/json"),
+             ("PUT", "/empty", None, "application/json", "application/json;as=Table;v=v1;g=meta.k8s.io"),
+             ("DELETE", "/apis/x/v1/things/b", None, "application/json", "application/json")]
+    try:
+        for native in (True, False):
+            pool = HttpPool(f"http://127.0.0.1:{port}/base", headers={"Authorization": "Bearer t0"}, native=native)
+            assert (pool._np is not None) == native
+            try:
+                for args in calls:
+                    assert (await pool.request_full(*args))[0] == 200
+                pool.set_headers({"Authorization": "Bearer t1"})
+                await pool.request_full(*calls[0])
+            finally:
+                await pool.close()
+        n = len(calls) + 1
+        assert len(seen) == 2 * n
+        assert seen[:n] == seen[n:]
+        assert b"Bearer t1" in seen[n - 1] and seen[0].startswith(b"GET /base/api/v1/namespaces/a/pods?watch=false ")
+        assert b"Content-Length: 0\r\n\r\n" in seen[3] and b"Content-Length" not in seen[0]
+    finally:
+        srv.close()
+
+
+async def test_pool_reuses_keeps_at_most_max_idle_and_reports_busy():
+    srv, port, seen, conns = await _capture_server(delay=0.05)
+    pool = HttpPool(f"http://127.0.0.1:{port}", max_idle=2, native=True)
+    try:
+        out = await asyncio.gather(*(pool.request("GET", f"/{i}") for i in range(4)))
+        assert all(st == 200 for st, _ in out)
+        assert pool.connects == 4 and len(pool._idle) == 2 and pool._np.busy == 0
+        await pool.request("GET", "/again")
+        assert pool.connects == 4  # reused
+        # the connections over max_idle were closed: the server saw EOF on them
+        await asyncio.sleep(0.05)
+        assert sum(w.is_closing() for w in conns) == 2
+    finally:
+        await pool.close()
+        srv.close()
+
+
+async def test_pool_deadline_sweep_fails_the_request_and_closes_it():
+    hold = asyncio.Event()
+
+    async def handle(reader, writer):
+        await _read_request(reader)
+        await hold.wait()  # never answers
+        writer.close()
+
+    srv, port = await _server(handle)
+    pool = HttpPool(f"http://127.0.0.1:{port}", timeout=0.2, native=True)
+    try:
+        t0 = asyncio.get_running_loop().time()
+        with pytest.raises(asyncio.TimeoutError):
+            await pool.request("GET", "/slow")
+        assert asyncio.get_running_loop().time() - t0 < 2.0
+        assert pool._np.busy == 0 and not pool._idle
+    finally:
+        hold.set()
+        await pool.close()
+        srv.close()
+
+
+async def test_pool_cancelled_request_does_not_return_its_connection():
+    got = asyncio.Event()
+    closed = asyncio.Event()
+
+    async def handle(reader, writer):
+        await _read_request(reader)
+        got.set()
+        try:
+            await reader.read()  # EOF when the client drops the connection
+        finally:
+            closed.set()
+            writer.close()
+
+    srv, port = await _server(handle)
+    pool = HttpPool(f"http://127.0.0.1:{port}", native=True)
+    try:
+        task = asyncio.ensure_future(pool.request("GET", "/hang"))
+        await asyncio.wait_for(got.wait(), 5)
+        task.cancel()
+        with pytest.raises(asyncio.CancelledError):
+            await task
+        await asyncio.wait_for(closed.wait(), 5)
+        assert pool._np.busy == 0 and not pool._idle
+    finally:
+        await pool.close()
+        srv.close()
+
+
+async def test_pool_closed_while_busy_closes_the_connection_after_its_response():
+    srv, port, seen, conns = await _capture_server(delay=0.1)
+    pool = HttpPool(f"http://127.0.0.1:{port}", native=True)
+    try:
+        task = asyncio.ensure_future(pool.request("GET", "/x"))
+        await asyncio.sleep(0.03)
+        await pool.close()
+        assert (await task)[0] == 200  # the exchange in flight completes
+        assert not pool._idle and pool._np.busy == 0
+        await asyncio.sleep(0.05)
+        assert conns[0].is_closing()
+    finally:
+        srv.close()
+
+
+async def test_pool_ssl_generation_retires_idle_connections():
+    srv, port, seen, conns = await _capture_server()
+    pool = HttpPool(f"http://127.0.0.1:{port}", native=True)
+    try:
+        await pool.request("GET", "/a")
+        assert len(pool._idle) == 1
+        pool._np.ssl_gen += 1  # what set_ssl does for a rotated client certificate
+        pool._np.close_idle()
+        assert not pool._idle
+        await pool.request("GET", "/b")
+        # the new connection was made for the pool's old generation (pool._ssl_gen is still 0):
+        # it is closed when its response completes instead of going back to the idle list
+        assert pool.connects == 2 and not pool._idle
+    finally:
+        await pool.close()
+        srv.close()
+
+
+async def test_pool_objects_are_released():
+    """No references leak through the busy/idle lists: after many requests and a close, the
+    pool and its connections are freed by reference counting and the cycle collector."""
+    import gc
+    import weakref
+
+    srv, port, seen, _ = await _capture_server()
+    pool = HttpPool(f"http://127.0.0.1:{port}", native=True)
+    for _ in range(200):
+        await pool.request("POST", "/x", b"{}")
+    refs = [weakref.ref(c) for c in pool._idle] + [weakref.ref(pool._np)]
+    await pool.close()
+    del pool
+    gc.collect()
+    assert all(r() is None for r in refs)
+    srv.close()
