@@ -8,10 +8,12 @@ every entry point with mutated and generated inputs:
 
 * ``_httpcodec``: byte-level mutations of valid requests/responses (fuzz);
 * ``_netconn``: mutated responses and watch streams delivered over a socketpair in random
-  splits to native connections on a live event loop, closed by either side at random;
+  splits to native connections on a live event loop, closed by either side at random; the
+  keep-alive ``Pool`` under deadline sweeps, abandoned requests and idle retirement;
 * ``_fastjson``: random JSON trees through loads/dumpb/dumpb_shared/deepcopy/
   json_equal/create_merge_patch, plus malformed documents;
-* ``_cron_engine``: random and malformed cron specs through parse/next/missed.
+* ``_cron_engine``: random and malformed cron specs through parse/next/missed, mutated and
+  out-of-range RFC 3339 timestamps through rfc3339_z/format_rfc3339;
 
 Any memory error or undefined behaviour aborts with the sanitizer report.
 ``make sanitize`` runs it.  Host code only: the operator has no GPU code.
@@ -148,6 +150,10 @@ def drive(scratch: str, iters: int) -> None:
             h.missed(t, 0, t2, 0, 0)
             t = t2
         ce.bulk_next([h, h], [t, t + 1], [0, 5], 0)
+    # RFC 3339 timestamps: mutated strings, and formatting across the representable range
+    for _ in range(iters // 4):
+        ce.rfc3339_z(_mutate(rng, b"2026-01-01T12:00:00Z").decode("latin-1"))
+        ce.format_rfc3339(rng.randint(-2**62, 2**62), rng.randint(-5, 2 * 10**9), rng.randint(-400000, 400000))
     net = drive_netconn(rng, iters // 20)
     print(f"sanitize ok: {iters} http, {iters // 4} json, {iters // 4} cron, {net} connection cases", flush=True)
 
@@ -214,6 +220,68 @@ def drive_netconn(rng: random.Random, cases: int) -> int:
             b.close()
             if fut.done() and not fut.cancelled():
                 fut.exception()
+        await run_pool(loop)
+
+    async def run_pool(loop) -> None:
+        """The keep-alive pool: requests on idle and fresh connections, mutated responses,
+        deadline sweeps, abandoned requests, peers that hang up, idle retirement, abort."""
+        import time
+
+        pool = ncm.Pool(rng.randint(0, 2), 0.5)
+        pool.set_fixed("/base", "Host: x\r\nUser-Agent: t\r\n")
+        peers = {}  # Conn -> its server-side socket
+        futs = []
+        for _ in range(cases):
+            method = rng.choice(["GET", "POST", "PATCH", "DELETE"])
+            body = b'{"a":1}' if rng.random() < 0.5 else None
+            fut = pool.request(method, "/p", body, "application/json", "application/json")
+            if fut is None:
+                a, b = socket.socketpair()
+                a.setblocking(False)
+                b.setblocking(False)
+                c = ncm.Conn(loop, a.detach())
+                peers[c] = b
+                fut = pool.request_on(c, method, "/p", body, "application/merge-patch+json", "application/json")
+            else:
+                c = next(k for k in peers if k.fut is fut)
+            futs.append(fut)
+            b = peers[c]
+            data = _mutate(rng, rng.choice(seeds[:4]))
+            pos = 0
+            while pos < len(data) and not fut.done():
+                n = rng.randint(1, 64)
+                try:
+                    b.send(data[pos:pos + n])
+                except OSError:
+                    break
+                pos += n
+                await asyncio.sleep(0)
+                r = rng.random()
+                if r < 0.03:
+                    pool.sweep(time.monotonic() + 10)  # past every deadline
+                elif r < 0.05:
+                    pool.discard(fut)
+                elif r < 0.06:
+                    pool.close_idle()
+            await asyncio.sleep(0)
+            try:
+                b.recv(65536)  # drain the request bytes
+            except OSError:
+                pass
+            if rng.random() < 0.2 or c.fd < 0:
+                b.close()
+            if fut.done() and not fut.cancelled():
+                fut.exception()
+            for k in [k for k, v in peers.items() if v.fileno() < 0 or k.fd < 0]:
+                k.close()
+                peers.pop(k).close()
+        pool.abort()
+        for k, v in peers.items():
+            k.close()
+            v.close()
+        for f in futs:
+            if f.done() and not f.cancelled():
+                f.exception()
 
     asyncio.run(run())
     return cases
