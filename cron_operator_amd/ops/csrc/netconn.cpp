@@ -1329,6 +1329,10 @@ bool build_request(PoolObject* p, PyObject* const* a, std::string* out) {
 PyObject* pool_start(PoolObject* p, ConnObject* c, const std::string& req) {
   PyObject* f = new_future(c);
   if (!f) {
+    PyObject *type, *value, *tb;
+    PyErr_Fetch(&type, &value, &tb);
+    close_io(c);  // neither pooled nor in flight any more: unregister it
+    PyErr_Restore(type, value, tb);
     Py_DECREF(c);
     return nullptr;
   }
@@ -1465,7 +1469,14 @@ PyObject* pool_request_on(PoolObject* self, PyObject* const* args, Py_ssize_t na
     return nullptr;
   }
   std::string req;
-  if (!build_request(self, args + 1, &req)) return nullptr;
+  if (!build_request(self, args + 1, &req)) {
+    // a fresh connection nobody else holds: do not leave it registered with the loop
+    PyObject *type, *value, *tb;
+    PyErr_Fetch(&type, &value, &tb);  // closing calls into the loop: keep the error aside
+    close_io(c);
+    PyErr_Restore(type, value, tb);
+    return nullptr;
+  }
   if (c->fd < 0 || !c->alive) return failed_future(c, conn_failed("connection is closed", true, c->used > 0));
   Py_INCREF(c);
   return pool_start(self, c, req);

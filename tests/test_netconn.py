@@ -578,3 +578,22 @@ async def test_pool_objects_are_released():
     gc.collect()
     assert all(r() is None for r in refs)
     srv.close()
+
+
+async def test_pool_unencodable_path_fails_like_the_python_path_without_leaking():
+    srv, port, seen, conns = await _capture_server()
+    try:
+        for native in (True, False):
+            pool = HttpPool(f"http://127.0.0.1:{port}", native=native)
+            try:
+                with pytest.raises(UnicodeEncodeError):
+                    await pool.request("GET", "/café☃")
+                if native:
+                    assert pool._np.busy == 0 and not pool._idle
+                assert (await pool.request("GET", "/ok"))[0] == 200
+            finally:
+                await pool.close()
+        await asyncio.sleep(0.05)
+        assert all(c.is_closing() for c in conns[:1])  # the native pool's first connection was closed
+    finally:
+        srv.close()
