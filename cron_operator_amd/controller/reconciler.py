@@ -375,6 +375,10 @@ class CronReconciler(Reconciler):
         # key -> (spec dict of the cached Cron, its parsed CronSpec): the Cron informer's codec hands
         # back the same spec object while the spec bytes do not change, so it is parsed once
         self._spec_memo: Dict[str, Tuple[Dict[str, Any], Any]] = {}
+        # metric children the hot path updates (label sets fixed)
+        self._m_patch_ok = metrics.child(metrics.STATUS_PATCHES, "ok")
+        self._m_patch_skipped = metrics.child(metrics.STATUS_PATCHES, "skipped")
+        self._m_sched_lat = metrics.child(metrics.SCHEDULE_LATENCY, "cron")
         # key -> (template workload dict, policy, its GVK): checked once per template object
         self._gvk_memo: Dict[str, Tuple[Any, WorkloadPolicy, GroupVersionKind]] = {}
         # tick bookkeeping for latency: key -> (tick unix ns, wall perf_counter when it became due)
@@ -408,8 +412,8 @@ class CronReconciler(Reconciler):
                 return Result()
             parsed = None
             spec = None
+            key = f"{req.namespace}/{req.name}"
             if self.opts.classification_cache:
-                key = f"{req.namespace}/{req.name}"
                 memo = self._parsed_status.get(key)
                 if memo is not None:
                     ov = self._own_rv.get(key)
@@ -437,7 +441,7 @@ class CronReconciler(Reconciler):
                 # B2: deferred status patch when status changed semantically (cron_controller.go:107-120)
                 if not old_status.semantic_equal(cron.status):
                     try:
-                        await self._patch_status(old_obj, cron, log)  # overlaps the running GC DELETEs
+                        await self._patch_status(old_obj, cron, log, key)  # overlaps the running GC DELETEs
                     except Exception as pe:  # noqa: BLE001
                         perr = RuntimeError(f"failed to patch Cron status: {pe}")
                         perr.__cause__ = pe
@@ -476,7 +480,7 @@ class CronReconciler(Reconciler):
         DELETEs nor mistakes their outcome for the caller's)."""
         await aio.wait_all(gc)
 
-    async def _patch_status(self, old_obj: Dict[str, Any], cron: Cron, log: Logger) -> None:
+    async def _patch_status(self, old_obj: Dict[str, Any], cron: Cron, log: Logger, key: str = "") -> None:
         new_status = cron.status.to_dict(shared=True)
         old_status = old_obj.get("status") or {}
         codecs = self.codecs
@@ -484,27 +488,32 @@ class CronReconciler(Reconciler):
         patch = jsonutil.create_merge_patch({"status": old_status}, {"status": new_status} if new_status else {},
                                             codecs is not None)
         m = old_obj.get("metadata") or {}
-        key = f"{m.get('namespace', '')}/{m.get('name', '')}"
+        if not key:
+            key = f"{m.get('namespace', '')}/{m.get('name', '')}"
         if self.opts.classification_cache:
             self._parsed_status[key] = (new_status, cron.status.snapshot())
         if not patch and self.opts.skip_noop_patch:
             self.stats["noop_patches_skipped"] += 1
-            metrics.child(metrics.STATUS_PATCHES, "skipped").inc()
+            self._m_patch_skipped.inc()
             return
         if self.opts.own_write_filter:
             # recorded before the call: the watch event can overtake the PATCH response
             self.own_writes[key] = (m.get("generation"), new_status)
         body: Any = codecs.status_patch.dumpb(patch) if codecs is not None else patch
         try:
-            with (tracing.span("patch_status", bytes=len(body) if body.__class__ is bytes else
-                               len(jsonutil.dumps(patch))) if tracing.get_tracer().enabled else tracing.NOOP):
+            if tracing.get_tracer().enabled:
+                with tracing.span("patch_status", bytes=len(body) if body.__class__ is bytes else
+                                  len(jsonutil.dumps(patch))):
+                    await self.client.patch(CRON_GVR, m.get("namespace", ""), m.get("name", ""), body, "merge",
+                                            "status", discard_response=True)
+            else:
                 await self.client.patch(CRON_GVR, m.get("namespace", ""), m.get("name", ""), body, "merge",
                                         "status", discard_response=True)
         except Exception:
             self.own_writes.pop(key, None)
             raise
         self.stats["patches"] += 1
-        metrics.child(metrics.STATUS_PATCHES, "ok").inc()
+        self._m_patch_ok.inc()
 
     def is_own_write(self, old: Optional[Dict[str, Any]], new: Dict[str, Any]) -> bool:
         """Predicate helper: is this Cron update exactly our last status write?
@@ -735,7 +744,7 @@ class CronReconciler(Reconciler):
                     resource_version=cm.get("resourceVersion", "") if self.opts.active_ref_resource_version else ""))
             if self.latency_observer is not None:
                 self.latency_observer(self._ckey(cron), missed_run, created)
-            metrics.child(metrics.SCHEDULE_LATENCY, "cron").observe(
+            self._m_sched_lat.observe(
                 max(0.0, (self.clock.now_ns() - missed_run.unix_nano()) / 1e9))
         except BaseException as e:  # API or transport error, or cancellation: nothing is in flight
             if self.opts.expectations:

@@ -51,6 +51,9 @@ class CronEngine:
 
     # -- parse with LRU cache (errors are cached too: a bad spec stays bad)
     def parse(self, spec: str) -> _Parsed:
+        hit = self._cache.get(spec)  # a single dict read is atomic: the hot path takes no lock
+        if hit.__class__ is _Parsed:
+            return hit  # (recency is only refreshed on the locked path: eviction is roughly LRU)
         with self._mu:
             hit = self._cache.get(spec)
             if hit is not None:
