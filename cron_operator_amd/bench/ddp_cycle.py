@@ -162,8 +162,17 @@ async def run_ddp_cycle(nproc: int = 1, cpu: bool = False, timeout: float = 600.
         if len(new) != 1:
             raise AssertionError(f"resume should run exactly one job, found {new}")
         await finish_running()
-        st = status()
-        hist = [(h["object"]["name"], h["status"]) for h in st.get("history") or []]
+        # the job's completion reaches the Cron through a watch event and one more reconcile:
+        # on a loaded machine that can trail the settle, so wait for it (bounded)
+        want = [(first[0], "Succeeded"), (new[0], "Succeeded")]
+        deadline = time.perf_counter() + 60.0
+        while True:
+            st = status()
+            hist = [(h["object"]["name"], h["status"]) for h in st.get("history") or []]
+            if (hist == want and not st.get("active")) or time.perf_counter() > deadline:
+                break
+            await asyncio.sleep(0.05)
+            await env.settle()
         results = {k.split("/", 1)[1]: v for k, v in trainer.results.items()}
         out = {"jobs": resumed, "history": hist, "active": len(st.get("active") or []),
                "exit_codes": {j: results.get(j, (False, [], 0))[1] for j in resumed},

@@ -1407,6 +1407,211 @@ struct MemoObject {
   MemoTable* table;
 };
 
+// ---------------------------------------------------------------------------------------------
+// store_apply: the bookkeeping of one informer event (runtime/informer.py Informer._apply) on the
+// informer's own dicts -- the store key (`ns/name`, or `name` without a namespace), the store
+// write or delete, the derived-memo drop, and the namespace and label indexes -- so that only
+// the event handlers stay in Python.  Anything irregular (metadata, namespace, name or label of
+// an unexpected type) returns None before a single dict is touched, and the Python path decides.
+
+PyObject *s_metadata_key, *s_namespace_key, *s_name_key, *s_labels_key, *s_empty;  // interned at import
+
+// obj["metadata"] as a dict (nullptr: absent or falsy -> empty; `bad`: present but not a dict)
+PyObject* meta_of(PyObject* obj, bool* bad) {
+  PyObject* m = PyDict_GetItemWithError(obj, s_metadata_key);
+  if (!m) return nullptr;  // absent (or a lookup error, surfaced by the caller's PyErr_Occurred)
+  if (PyDict_CheckExact(m)) return PyDict_GET_SIZE(m) ? m : nullptr;
+  const int t = PyObject_IsTrue(m);
+  if (t != 0) *bad = true;  // truthy non-dict: Python's `.get` would raise
+  return nullptr;
+}
+
+// m.get(k, "") as an exact str (nullptr + bad when present but not a str)
+PyObject* str_field(PyObject* m, PyObject* k, bool* bad) {
+  if (!m) return nullptr;
+  PyObject* v = PyDict_GetItemWithError(m, k);
+  if (!v) return nullptr;
+  if (!PyUnicode_CheckExact(v)) {
+    *bad = true;
+    return nullptr;
+  }
+  return v;
+}
+
+// The store key; nullptr + bad on irregular input.  New reference.
+PyObject* store_key(PyObject* m, bool* bad) {
+  PyObject* ns = str_field(m, s_namespace_key, bad);
+  PyObject* name = str_field(m, s_name_key, bad);
+  if (*bad) return nullptr;
+  if (!name) name = s_empty;
+  if (!ns || PyUnicode_GET_LENGTH(ns) == 0) {
+    Py_INCREF(name);
+    return name;
+  }
+  return PyUnicode_FromFormat("%U/%U", ns, name);
+}
+
+// The index values of `m` for one indexer: label == nullptr -> [namespace]; else
+// [ns/<label value>] or [] (returned as a new str, or nullptr for "no value").  bad on irregular.
+PyObject* index_value(PyObject* m, PyObject* label, bool* bad, bool* none) {
+  PyObject* ns = str_field(m, s_namespace_key, bad);
+  if (*bad) return nullptr;
+  if (!label) {
+    *none = false;
+    PyObject* v = ns ? ns : s_empty;
+    Py_INCREF(v);
+    return v;
+  }
+  PyObject* labels = m ? PyDict_GetItemWithError(m, s_labels_key) : nullptr;
+  if (labels && !PyDict_CheckExact(labels)) {
+    if (PyObject_IsTrue(labels) != 0) {
+      *bad = true;
+      return nullptr;
+    }
+    labels = nullptr;
+  }
+  PyObject* v = labels ? PyDict_GetItemWithError(labels, label) : nullptr;
+  if (!v || v == Py_None) {
+    *none = true;
+    return nullptr;
+  }
+  if (!PyUnicode_CheckExact(v)) {
+    *bad = true;
+    return nullptr;
+  }
+  *none = false;
+  return PyUnicode_FromFormat("%U/%U", ns ? ns : s_empty, v);
+}
+
+bool index_remove(PyObject* idx, PyObject* value, PyObject* key) {
+  PyObject* s = PyDict_GetItemWithError(idx, value);
+  if (!s) return !PyErr_Occurred();
+  if (PySet_Discard(s, key) < 0) return false;
+  if (PySet_GET_SIZE(s) == 0 && PyDict_DelItem(idx, value) < 0) return false;
+  return true;
+}
+
+bool index_add(PyObject* idx, PyObject* value, PyObject* key) {
+  PyObject* s = PyDict_GetItemWithError(idx, value);
+  if (!s) {
+    if (PyErr_Occurred()) return false;
+    s = PySet_New(nullptr);
+    if (!s) return false;
+    const int r = PyDict_SetItem(idx, value, s);
+    Py_DECREF(s);
+    if (r < 0) return false;
+  }
+  return PySet_Add(s, key) == 0;
+}
+
+// store_apply(store, derived, indices, spec, deleting, obj) -> (key, old) | None
+//   spec: tuple of (index name, label or None); None: the namespace index
+PyObject* py_store_apply(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 6 || !PyDict_CheckExact(args[0]) || !PyDict_CheckExact(args[1]) || !PyDict_CheckExact(args[2]) ||
+      !PyTuple_CheckExact(args[3])) {
+    PyErr_SetString(PyExc_TypeError, "store_apply(store, derived, indices, spec, deleting, obj)");
+    return nullptr;
+  }
+  PyObject *store = args[0], *derived = args[1], *indices = args[2], *spec = args[3], *obj = args[5];
+  const int deleting = PyObject_IsTrue(args[4]);
+  if (deleting < 0) return nullptr;
+  if (!PyDict_CheckExact(obj)) Py_RETURN_NONE;
+  bool bad = false;
+  PyObject* m = meta_of(obj, &bad);
+  if (PyErr_Occurred()) return nullptr;
+  PyObject* key = bad ? nullptr : store_key(m, &bad);
+  if (!key) {
+    if (PyErr_Occurred()) return nullptr;
+    Py_RETURN_NONE;
+  }
+  PyObject* old = PyDict_GetItemWithError(store, key);  // borrowed
+  if (!old && PyErr_Occurred()) {
+    Py_DECREF(key);
+    return nullptr;
+  }
+  PyObject* om = nullptr;
+  if (old) {
+    if (!PyDict_CheckExact(old)) {
+      Py_DECREF(key);
+      Py_RETURN_NONE;
+    }
+    om = meta_of(old, &bad);
+  }
+  const Py_ssize_t ni = PyTuple_GET_SIZE(spec);
+  // index values, all computed (and validated) before anything changes
+  std::vector<PyObject*> names(ni), ov(ni, nullptr), nv(ni, nullptr), idxs(ni);
+  std::vector<char> is_ns(ni), have_ov(ni, 0), have_nv(ni, 0);
+  bool ok = !bad && !PyErr_Occurred();
+  for (Py_ssize_t i = 0; ok && i < ni; ++i) {
+    PyObject* e = PyTuple_GET_ITEM(spec, i);
+    if (!PyTuple_CheckExact(e) || PyTuple_GET_SIZE(e) != 2) {
+      ok = false;
+      break;
+    }
+    names[i] = PyTuple_GET_ITEM(e, 0);
+    PyObject* label = PyTuple_GET_ITEM(e, 1);
+    is_ns[i] = label == Py_None;
+    idxs[i] = PyDict_GetItemWithError(indices, names[i]);
+    if (!idxs[i] || !PyDict_CheckExact(idxs[i])) {
+      ok = false;
+      break;
+    }
+    bool none = false;
+    const bool update = old && !deleting;
+    if (old && !(update && is_ns[i])) {
+      ov[i] = index_value(om, is_ns[i] ? nullptr : label, &bad, &none);
+      have_ov[i] = !none && ov[i];
+    }
+    if (!deleting && !(update && is_ns[i])) {
+      none = false;
+      nv[i] = index_value(m, is_ns[i] ? nullptr : label, &bad, &none);
+      have_nv[i] = !none && nv[i];
+    }
+    if (bad || PyErr_Occurred()) ok = false;
+  }
+  PyObject* result = nullptr;
+  if (ok) {
+    bool done = true;
+    Py_XINCREF(old);  // the store drops or replaces its reference below; we return it
+    if (deleting) {
+      if (old) {
+        done = PyDict_DelItem(store, key) == 0;
+        if (done) {
+          PyObject* d = PyDict_GetItemWithError(derived, key);
+          if (d) done = PyDict_DelItem(derived, key) == 0;
+          else done = !PyErr_Occurred();
+        }
+        for (Py_ssize_t i = 0; done && i < ni; ++i)
+          if (have_ov[i]) done = index_remove(idxs[i], ov[i], key);
+      }
+    } else {
+      done = PyDict_SetItem(store, key, obj) == 0;
+      for (Py_ssize_t i = 0; done && i < ni; ++i) {
+        if (old && is_ns[i]) continue;  // the key carries the namespace: an update cannot move it
+        if (old) {
+          const bool same = have_ov[i] == have_nv[i] &&
+                            (!have_ov[i] || PyUnicode_Compare(ov[i], nv[i]) == 0);
+          if (same) continue;
+          if (have_ov[i]) done = index_remove(idxs[i], ov[i], key);
+        }
+        if (done && have_nv[i]) done = index_add(idxs[i], nv[i], key);
+      }
+    }
+    if (done) result = PyTuple_Pack(2, key, old ? old : Py_None);
+    Py_XDECREF(old);
+    if (!done && !PyErr_Occurred()) PyErr_SetString(PyExc_RuntimeError, "store_apply failed");
+  } else if (!PyErr_Occurred()) {
+    result = Py_None;
+    Py_INCREF(result);
+  }
+  Py_XDECREF(key);
+  for (Py_ssize_t i = 0; i < ni; ++i) {
+    Py_XDECREF(ov[i]);
+    Py_XDECREF(nv[i]);
+  }
+  return result;
+}
+
 void memo_dealloc(PyObject* self) {
   delete reinterpret_cast<MemoObject*>(self)->table;
   Py_TYPE(self)->tp_free(self);
@@ -1645,6 +1850,9 @@ PyMethodDef methods[] = {
     {"dumpb_shared", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(py_dumpb_shared)),
      METH_FASTCALL, "dumpb of an immutable tree, reusing the bytes of subtrees cached by identity"},
     {"clear_key_cache", py_clear_key_cache, METH_NOARGS, "drop the interned-key cache"},
+    {"store_apply", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(py_store_apply)), METH_FASTCALL,
+     "store_apply(store, derived, indices, spec, deleting, obj) -> (key, old) | None: an informer event's "
+     "store/index bookkeeping"},
     {"kubeflow_summary", py_kubeflow_summary, METH_O,
      "kubeflow_summary(status) -> None | (finished, last_type, n_conditions, completion_time, terminal_ltt)"},
     {"set_gc_untrack", py_set_gc_untrack, METH_O,
@@ -1677,6 +1885,11 @@ PyMODINIT_FUNC PyInit__fastjson(void) {
   CodecType.tp_call = codec_call;
   CodecType.tp_vectorcall_offset = offsetof(CodecObject, vectorcall);
   if (PyType_Ready(&MemoType) < 0 || PyType_Ready(&CodecType) < 0) return nullptr;
+  if (!(s_metadata_key = PyUnicode_InternFromString("metadata")) ||
+      !(s_namespace_key = PyUnicode_InternFromString("namespace")) ||
+      !(s_name_key = PyUnicode_InternFromString("name")) || !(s_labels_key = PyUnicode_InternFromString("labels")) ||
+      !(s_empty = PyUnicode_InternFromString("")))
+    return nullptr;
   PyObject* m = PyModule_Create(&moddef);
   if (!m) return nullptr;
   Py_INCREF(&MemoType);

@@ -69,6 +69,7 @@ def label_index(label: str) -> IndexFunc:
         v = (m.get("labels") or {}).get(label)
         return [] if v is None else [f"{m.get('namespace', '')}/{v}"]
 
+    fn.label = label  # type: ignore[attr-defined]  # lets the native bookkeeping index it too
     return fn
 
 
@@ -146,6 +147,7 @@ class Informer:
         self.indexers: Dict[str, IndexFunc] = {NAMESPACE_INDEX: namespace_index}
         self.indexers.update(indexers or {})
         self.indices: Dict[str, Dict[str, Set[str]]] = {n: {} for n in self.indexers}
+        self._native_spec()
         self.handlers: List[EventHandler] = []
         self.synced = asyncio.Event()
         # the outcome of the most recent LIST: ``list_error`` is its error (None after a
@@ -172,6 +174,23 @@ class Informer:
             for v in fn(obj):
                 idx.setdefault(v, set()).add(k)
         self.indices[name] = idx
+        self._native_spec()
+
+    def _native_spec(self) -> None:
+        """Use the native event bookkeeping (``_fastjson.store_apply``: key, store, derived
+        memo, indexes) when every indexer is one it knows -- the namespace index or a label
+        index; any other index function keeps the Python path."""
+        spec = []
+        for name, fn in self.indexers.items():
+            if fn is namespace_index:
+                spec.append((name, None))
+            elif isinstance(getattr(fn, "label", None), str):
+                spec.append((name, fn.label))  # type: ignore[attr-defined]
+            else:
+                self._napply, self._nspec = None, ()
+                return
+        self._napply = jsonutil.store_apply
+        self._nspec = tuple(spec)
 
     def _index(self, key: str, obj: Optional[Dict[str, Any]], old: Optional[Dict[str, Any]]) -> None:
         for name, fn in self.indexers.items():
@@ -245,9 +264,32 @@ class Informer:
     def _apply(self, etype: str, obj: Dict[str, Any]) -> None:
         if self.transform is not None and not self._pretransformed:
             obj = self.transform(obj)
+        self.events += 1
+        na = self._napply
+        if na is not None:
+            # key, store write/delete, derived-memo drop and index upkeep in one native call
+            r = na(self.store, self.derived, self.indices, self._nspec, etype == "DELETED", obj)
+            if r is not None:
+                key, old = r
+                if etype == "DELETED":
+                    if old is not None:
+                        for h in self.handlers:
+                            if h.on_delete:
+                                h.on_delete(obj)
+                    return
+                if self.derive is not None:
+                    self.derived[key] = self.derive(obj)
+                if old is None:
+                    for h in self.handlers:
+                        if h.on_add:
+                            h.on_add(obj)
+                else:
+                    for h in self.handlers:
+                        if h.on_update:
+                            h.on_update(old, obj)
+                return
         key = obj_key(obj)
         old = self.store.get(key)
-        self.events += 1
         if etype == "DELETED":
             if old is None:
                 return

@@ -251,10 +251,13 @@ create_merge_patch = py_create_merge_patch
 Codec: Any = PyCodec
 Memo: Any = PyMemo
 NATIVE = False
+# informer-event bookkeeping (runtime/informer.py); None without the native module
+store_apply: Any = None
 
 
 def _try_native() -> None:
     global deepcopy, json_equal, create_merge_patch, loads, dumps, dumpb, dumpb_shared, Codec, Memo, NATIVE
+    global store_apply
     import os
 
     if os.environ.get("CRON_OPERATOR_FASTJSON", "auto").lower() == "python":
@@ -276,6 +279,7 @@ def _try_native() -> None:
     dumpb_shared = mod.dumpb_shared
     Codec = mod.Codec
     Memo = mod.Memo
+    store_apply = getattr(mod, "store_apply", None)
     NATIVE = True
 
 

@@ -11,7 +11,8 @@ every entry point with mutated and generated inputs:
   splits to native connections on a live event loop, closed by either side at random; the
   keep-alive ``Pool`` under deadline sweeps, abandoned requests and idle retirement;
 * ``_fastjson``: random JSON trees through loads/dumpb/dumpb_shared/deepcopy/
-  json_equal/create_merge_patch, plus malformed documents;
+  json_equal/create_merge_patch, plus malformed documents; the informer bookkeeping
+  (store_apply) over malformed objects;
 * ``_cron_engine``: random and malformed cron specs through parse/next/missed, mutated and
   out-of-range RFC 3339 timestamps through rfc3339_z/format_rfc3339;
 
@@ -126,6 +127,18 @@ def drive(scratch: str, iters: int) -> None:
                   "completionTime": rng.choice(times + [None])}
         fj.kubeflow_summary(status)
         fj.kubeflow_summary(_tree(rng))
+    # informer-event bookkeeping over random (often malformed) objects
+    store, derived, indices = {}, {}, {"namespace": {}, "cron": {}}
+    spec = (("namespace", None), ("cron", "c"))
+    for _ in range(iters // 4):
+        labels = rng.choice([None, {"c": rng.choice(["x", "y", 2])}, []])
+        name, ns = rng.choice(["a", "b", 1]), rng.choice(["n", "", None])
+        meta = rng.choice([None, {}, [], "m", {"name": name, "namespace": ns, "labels": labels}])
+        obj = {"metadata": meta} if meta is not None else {}
+        fj.store_apply(store, derived, indices, spec, rng.random() < 0.3, obj)
+        if rng.random() < 0.01:
+            store.clear()
+            indices = {"namespace": {}, "cron": {}}
     # the shared-value cache: strings handed out, dropped, evicted and handed out again
     vals = [f"v{i}" for i in range(40000)] + ["kubeflow.org/v1", "PyTorchJob", "Succeeded"] * 100
     for rnd in range(3):
