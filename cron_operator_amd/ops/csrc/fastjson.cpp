@@ -1612,6 +1612,31 @@ PyObject* py_store_apply(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
   return result;
 }
 
+// pick(mapping, keys) -> [mapping[k] for k in keys] (KeyError for a missing key)
+PyObject* py_pick(PyObject*, PyObject* const* args, Py_ssize_t nargs) {
+  if (nargs != 2 || !PyDict_Check(args[0])) {
+    PyErr_SetString(PyExc_TypeError, "pick(dict, keys)");
+    return nullptr;
+  }
+  PyObject* it = PyObject_GetIter(args[1]);
+  if (!it) return nullptr;
+  PyObject* out = PyList_New(0);
+  PyObject* k;
+  while (out && (k = PyIter_Next(it))) {
+    PyObject* v = PyDict_GetItemWithError(args[0], k);
+    if (!v) {
+      if (!PyErr_Occurred()) PyErr_SetObject(PyExc_KeyError, k);
+      Py_CLEAR(out);
+    } else if (PyList_Append(out, v) < 0) {
+      Py_CLEAR(out);
+    }
+    Py_DECREF(k);
+  }
+  Py_DECREF(it);
+  if (out && PyErr_Occurred()) Py_CLEAR(out);
+  return out;
+}
+
 void memo_dealloc(PyObject* self) {
   delete reinterpret_cast<MemoObject*>(self)->table;
   Py_TYPE(self)->tp_free(self);
@@ -1850,6 +1875,8 @@ PyMethodDef methods[] = {
     {"dumpb_shared", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(py_dumpb_shared)),
      METH_FASTCALL, "dumpb of an immutable tree, reusing the bytes of subtrees cached by identity"},
     {"clear_key_cache", py_clear_key_cache, METH_NOARGS, "drop the interned-key cache"},
+    {"pick", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(py_pick)), METH_FASTCALL,
+     "pick(dict, keys) -> [dict[k] for k in keys]"},
     {"store_apply", reinterpret_cast<PyCFunction>(reinterpret_cast<void (*)(void)>(py_store_apply)), METH_FASTCALL,
      "store_apply(store, derived, indices, spec, deleting, obj) -> (key, old) | None: an informer event's "
      "store/index bookkeeping"},

@@ -244,9 +244,7 @@ class Informer:
 
     def derived_by_index(self, index: str, value: str) -> List[Any]:
         """``derive(obj)`` of every object under ``value`` of ``index``."""
-        keys = self.indices.get(index, {}).get(value, ())
-        d = self.derived
-        return [d[k] for k in keys]
+        return jsonutil.pick(self.derived, self.indices.get(index, {}).get(value, ()))
 
     def by_index(self, index: str, value: str, copy: bool = True) -> List[Dict[str, Any]]:
         keys = self.indices.get(index, {}).get(value, ())

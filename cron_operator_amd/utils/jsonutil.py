@@ -255,9 +255,17 @@ NATIVE = False
 store_apply: Any = None
 
 
+def py_pick(d: Dict[Any, Any], keys: Any) -> list:
+    """``[d[k] for k in keys]``."""
+    return [d[k] for k in keys]
+
+
+pick: Any = py_pick
+
+
 def _try_native() -> None:
     global deepcopy, json_equal, create_merge_patch, loads, dumps, dumpb, dumpb_shared, Codec, Memo, NATIVE
-    global store_apply
+    global store_apply, pick
     import os
 
     if os.environ.get("CRON_OPERATOR_FASTJSON", "auto").lower() == "python":
@@ -280,6 +288,7 @@ def _try_native() -> None:
     Codec = mod.Codec
     Memo = mod.Memo
     store_apply = getattr(mod, "store_apply", None)
+    pick = getattr(mod, "pick", py_pick)
     NATIVE = True
 
 

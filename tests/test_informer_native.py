@@ -108,3 +108,15 @@ def test_unknown_index_function_keeps_the_python_path():
     assert inf2._napply is not None
     inf2.add_indexer("custom", lambda o: ["k"])
     assert inf2._napply is None
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.dictionaries(st.text(max_size=3), st.integers()), st.sets(st.text(max_size=3), max_size=8))
+def test_pick_matches_the_comprehension(d, keys):
+    try:
+        want = [d[k] for k in keys]
+    except KeyError:
+        with pytest.raises(KeyError):
+            jsonutil.pick(d, keys)
+        return
+    assert jsonutil.pick(d, keys) == want == jsonutil.py_pick(d, keys)
