@@ -735,15 +735,34 @@ class HttpPool:
         status, raw, _ = await self.request_full(method, path, body, content_type)
         return status, raw
 
+    def start(self, method: str, path: str, body: Optional[bytes] = None, content_type: str = "application/json",
+              accept: str = "application/json") -> Optional["asyncio.Future[Tuple[int, bytes, Optional[int]]]"]:
+        """The native pool's request on an idle connection, sent now: the response future, or
+        None (no native pool, or nothing idle -- use :meth:`request_full`).  A caller awaiting
+        it retries a ``ConnectionFailed(no_response, reused)`` once with ``request_full(...,
+        fresh=True)`` and, when cancelled, hands the future to :meth:`discard`."""
+        np = self._np
+        if np is None:
+            return None
+        fut = np.request(method, path, body, content_type, accept)
+        if fut is not None and self._sweeper is None:
+            self._sweeper = asyncio.get_running_loop().call_later(self._sweep_every, self._sweep)
+        return fut
+
+    def discard(self, fut: "asyncio.Future[Any]") -> None:
+        """The request of ``fut`` (from :meth:`start`) was abandoned: close its connection."""
+        if self._np is not None:
+            self._np.discard(fut)
+
     async def request_full(self, method: str, path: str, body: Optional[bytes] = None,
                            content_type: str = "application/json",
-                           accept: str = "application/json") -> Tuple[int, bytes, Optional[int]]:
-        """``(status, body, Retry-After seconds or None)``."""
+                           accept: str = "application/json", fresh: bool = False) -> Tuple[int, bytes, Optional[int]]:
+        """``(status, body, Retry-After seconds or None)``.  ``fresh``: on a new connection."""
         np = self._np
         if np is not None:
             # native pool: head built, idle connection taken, sent, and given back when the
             # response completes -- all in C++; Python only connects when no connection is idle
-            fut = np.request(method, path, body, content_type, accept)
+            fut = None if fresh else np.request(method, path, body, content_type, accept)
             if fut is None:
                 fut = np.request_on(await self._connect(), method, path, body, content_type, accept)
             if self._sweeper is None:
@@ -771,7 +790,7 @@ class HttpPool:
             data = (head + ("Content-Length: 0\r\n\r\n" if method in ("POST", "PUT", "PATCH") else "\r\n")
                     ).encode("latin-1")
         loop = asyncio.get_running_loop()
-        for attempt in (0, 1):
+        for attempt in ((1,) if fresh else (0, 1)):
             conn = self._take_idle() if attempt == 0 else None
             if conn is None:
                 conn = await self._connect()

@@ -254,8 +254,23 @@ class HttpTransport(Transport):
                     if cfg.exec_provider is not None and cfg.exec_stale():
                         await self._fresh_exec()  # expired while waiting out Retry-After: refresh off the loop
                     pool = self._fast_pool()  # a token rotated meanwhile is stamped on the retry
+                # an idle native connection takes the request at once (no extra coroutine frame)
+                fut = pool.start(method, target, data, ctype, accept)
                 try:
-                    status, raw, retry_after = await pool.request_full(method, target, data, ctype, accept)
+                    if fut is not None:
+                        try:
+                            status, raw, retry_after = await fut
+                        except ConnectionFailed as e:
+                            if not (e.no_response and e.reused):
+                                raise
+                            # a stale keep-alive connection: once more on a fresh one
+                            status, raw, retry_after = await pool.request_full(method, target, data, ctype, accept,
+                                                                               fresh=True)
+                        except asyncio.CancelledError:
+                            pool.discard(fut)  # abandoned mid-exchange: the connection cannot be reused
+                            raise
+                    else:
+                        status, raw, retry_after = await pool.request_full(method, target, data, ctype, accept)
                 except (ConnectionFailed, OSError, asyncio.TimeoutError) as e:
                     raise errors.ApiError(503, "ServiceUnavailable", f"connection error: {e}") from None
                 if retry_after is None or not (status == 429 or status >= 500) or attempt >= self.max_retries:

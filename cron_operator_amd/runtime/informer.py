@@ -446,8 +446,7 @@ class Informer:
                                     break
                                 continue
                             self._last_item = loop.time()
-                            for etype, obj in batch:
-                                self._on_item(etype, obj)
+                            self._on_batch(batch)
                     else:
                         async for etype, obj in w:
                             self._last_item = loop.time()
@@ -474,6 +473,18 @@ class Informer:
                 need_list = need_list or not self.last_rv
                 await asyncio.sleep(backoff * (1 + random.random()))
                 backoff = min(backoff * 2, 30.0)
+
+    def _on_batch(self, batch: List[Tuple[str, Dict[str, Any]]]) -> None:
+        """Every event of one wake-up, in order (:meth:`_on_item` without a call per event)."""
+        apply = self._apply
+        for etype, obj in batch:
+            if etype == "ERROR":
+                raise errors.ApiError.from_status(int(obj.get("code") or 500), obj)
+            rv = (obj.get("metadata") or {}).get("resourceVersion")
+            if etype != "BOOKMARK":
+                apply(etype, obj)
+            if rv:
+                self.last_rv = rv
 
     def _on_item(self, etype: str, obj: Dict[str, Any]) -> None:
         """One watch event: apply it (BOOKMARKs only move the resume point); ERROR raises."""
