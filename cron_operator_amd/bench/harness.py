@@ -688,6 +688,13 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
 
 
 def run_sync(cfg: BenchConfig, on_step=None) -> BenchResult:
+    if cfg.transport == "http":
+        # the operator (in this process with one shard, else in shard_worker processes) runs on the
+        # native loop core like `cron-operator start`; the fake apiserver process keeps asyncio's
+        # stock loop (an in-memory transport would put the fixture on this loop: left stock)
+        from ..runtime import aioloop
+
+        aioloop.install()
     return asyncio.run(run(cfg, on_step))
 
 

@@ -170,6 +170,9 @@ async def main() -> int:
 
 
 if __name__ == "__main__":
+    from ..runtime import aioloop
+
+    aioloop.install()  # an operator process: the native loop core, as `cron-operator start` uses
     _prof = os.environ.get("CRON_BENCH_SHARD_PROFILE")
     if _prof:  # cProfile of the whole worker (setup included): <prefix>.<pid>.pstats
         import cProfile

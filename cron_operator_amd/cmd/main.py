@@ -514,6 +514,9 @@ def main(argv: Optional[List[str]] = None) -> int:
             return 2
         if a.cron_engine != "auto":
             os.environ["CRON_OPERATOR_ENGINE"] = a.cron_engine
+        from ..runtime import aioloop
+
+        aioloop.install()  # the operator's loop: native call_soon/_run_once (runtime/aioloop.py)
         if a.shard_processes > 1:
             return asyncio.run(run_supervisor(a, list(argv)))
         if a.shard_processes < 1:

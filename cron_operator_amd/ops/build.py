@@ -29,6 +29,7 @@ EXTENSIONS: Dict[str, List[str]] = {
     "_fastjson": ["fastjson.cpp"],
     "_httpcodec": ["httpcodec.cpp"],
     "_netconn": ["netconn.cpp"],
+    "_aioloop": ["aioloop.cpp"],
 }
 # headers each extension includes (a change rebuilds it)
 HEADERS: Dict[str, List[str]] = {

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Host sanitizer run of the native extensions (ASan + UBSan).
 
-Builds ``_cron_engine``, ``_fastjson``, ``_httpcodec`` and ``_netconn`` from ``ops/csrc`` with
+Builds ``_cron_engine``, ``_fastjson``, ``_httpcodec``, ``_netconn`` and ``_aioloop`` from ``ops/csrc`` with
 ``-fsanitize=address,undefined`` into a scratch directory, re-executes itself with
 the sanitizer runtimes preloaded (CPython itself is not instrumented), and drives
 every entry point with mutated and generated inputs:
@@ -13,6 +13,8 @@ every entry point with mutated and generated inputs:
 * ``_fastjson``: random JSON trees through loads/dumpb/dumpb_shared/deepcopy/
   json_equal/create_merge_patch, plus malformed documents; the informer bookkeeping
   (store_apply) over malformed objects;
+* ``_aioloop``: random programs of call_soon/call_at/cancel/raising callbacks/readers on the
+  native loop core (also the loop the ``_netconn`` cases run on), handle reprs and collection;
 * ``_cron_engine``: random and malformed cron specs through parse/next/missed, mutated and
   out-of-range RFC 3339 timestamps through rfc3339_z/format_rfc3339;
 
@@ -31,7 +33,7 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "cron_operator_amd", "ops", "csrc")
 EXTS = {"_cron_engine": "cron_engine.cpp", "_fastjson": "fastjson.cpp", "_httpcodec": "httpcodec.cpp",
-        "_netconn": "netconn.cpp"}
+        "_netconn": "netconn.cpp", "_aioloop": "aioloop.cpp"}
 LIBS = {"_netconn": ["-lssl", "-lcrypto"]}
 
 
@@ -167,8 +169,84 @@ def drive(scratch: str, iters: int) -> None:
     for _ in range(iters // 4):
         ce.rfc3339_z(_mutate(rng, b"2026-01-01T12:00:00Z").decode("latin-1"))
         ce.format_rfc3339(rng.randint(-2**62, 2**62), rng.randint(-5, 2 * 10**9), rng.randint(-400000, 400000))
+    loops = drive_aioloop(rng, iters // 20)
     net = drive_netconn(rng, iters // 20)
-    print(f"sanitize ok: {iters} http, {iters // 4} json, {iters // 4} cron, {net} connection cases", flush=True)
+    print(f"sanitize ok: {iters} http, {iters // 4} json, {iters // 4} cron, {loops} loop programs, "
+          f"{net} connection cases", flush=True)
+
+
+def _native_loop_cls():
+    import asyncio
+    import heapq
+    import selectors
+    from asyncio import base_events, format_helpers
+
+    import _aioloop  # noqa: E402
+
+    _aioloop.configure(selectors.EpollSelector, heapq.heappop, heapq.heapify, format_helpers._format_callback_source,
+                       base_events.BaseEventLoop.call_soon, base_events.BaseEventLoop._run_once)
+
+    class SanitizedLoop(_aioloop.LoopCore, asyncio.SelectorEventLoop):
+        pass
+
+    return SanitizedLoop
+
+
+def drive_aioloop(rng: random.Random, cases: int) -> int:
+    """Random programs on the native loop core: call_soon with and without a context, timers
+    due now and later, cancellations (before and while queued), raising callbacks, readers on
+    socketpairs (some cancelled in place), nested scheduling, reprs, and collection."""
+    import asyncio
+    import contextvars
+    import gc
+    import socket
+
+    cls = _native_loop_cls()
+
+    async def program(loop) -> None:
+        loop.set_exception_handler(lambda _l, _c: None)
+        handles, socks = [], []
+        for _ in range(rng.randint(1, 60)):
+            op = rng.random()
+            if op < 0.35:
+                ctx = contextvars.copy_context() if rng.random() < 0.3 else None
+                handles.append(loop.call_soon(lambda d=rng.randint(0, 3): d and loop.call_soon(print, end=""),
+                                              context=ctx))
+            elif op < 0.5:
+                handles.append(loop.call_at(loop.time() + rng.uniform(-1, 0.003), lambda: None))
+            elif op < 0.65 and handles:
+                h = rng.choice(handles)
+                h.cancel()
+                repr(h)
+            elif op < 0.75:
+                handles.append(loop.call_soon(lambda: 1 / 0))
+            elif op < 0.85:
+                a, b = socket.socketpair()
+                a.setblocking(False)
+                socks += [a, b]
+                loop.add_reader(a.fileno(), lambda s=a: s.recv(64))
+                if rng.random() < 0.3:
+                    loop._selector.get_key(a.fileno()).data[0].cancel()
+                b.send(b"x")
+            else:
+                await asyncio.sleep(0)
+        await asyncio.sleep(0.005)
+        for s in socks:
+            try:
+                loop.remove_reader(s.fileno())
+            except (KeyError, ValueError, OSError):
+                pass
+            s.close()
+
+    for _ in range(cases):
+        loop = cls()
+        try:
+            loop.run_until_complete(program(loop))
+        finally:
+            loop.close()
+        del loop
+    gc.collect()
+    return cases
 
 
 def drive_netconn(rng: random.Random, cases: int) -> int:
@@ -296,7 +374,11 @@ def drive_netconn(rng: random.Random, cases: int) -> int:
             if f.done() and not f.cancelled():
                 f.exception()
 
-    asyncio.run(run())
+    loop = _native_loop_cls()()
+    try:
+        loop.run_until_complete(run())
+    finally:
+        loop.close()
     return cases
 
 

@@ -21,6 +21,12 @@ from cron_operator_amd.utils.logging import new_from_options, set_logger  # noqa
 
 set_logger(new_from_options(encoder="console", level="error", stream=open(os.devnull, "w")))
 
+# every asyncio test runs on the operator's loop (native call_soon/_run_once, runtime/aioloop.py)
+# unless CRON_OPERATOR_NATIVE_LOOP=python selects asyncio's stock loop (CI runs both tiers)
+from cron_operator_amd.runtime import aioloop as _aioloop  # noqa: E402
+
+_aioloop.install()
+
 
 # Property tests draw the same examples on every run (a CI run must not turn red on a
 # fresh random draw); HYPOTHESIS_RANDOM=1 explores new examples when hunting for bugs.
