@@ -30,6 +30,7 @@ EXTENSIONS: Dict[str, List[str]] = {
     "_httpcodec": ["httpcodec.cpp"],
     "_netconn": ["netconn.cpp"],
     "_aioloop": ["aioloop.cpp"],
+    "_promlite": ["promlite.cpp"],
 }
 # headers each extension includes (a change rebuilds it)
 HEADERS: Dict[str, List[str]] = {

@@ -131,7 +131,7 @@ class _Metric(Collector):
         out.append(f"{self.name}{_labels(self.labelnames, key)} {_fmt(child.value)}")
 
 
-class _CounterChild:
+class _PyCounterChild:
     __slots__ = ("value",)
 
     def __init__(self) -> None:
@@ -156,7 +156,7 @@ class Counter(_Metric):
         self._only().inc(amount)
 
 
-class _GaugeChild:
+class _PyGaugeChild:
     __slots__ = ("value",)
 
     def __init__(self) -> None:
@@ -191,7 +191,7 @@ class Gauge(_Metric):
         self._only().set(value)
 
 
-class _HistogramChild:
+class _PyHistogramChild:
     __slots__ = ("bounds", "counts", "sum", "count")
 
     def __init__(self, bounds: Tuple[float, ...]) -> None:
@@ -204,6 +204,29 @@ class _HistogramChild:
         self.counts[bisect_left(self.bounds, v)] += 1  # le semantics: v <= bound
         self.sum += v
         self.count += 1
+
+
+def _series_classes():
+    """The series classes: ``_promlite``'s (``ops/csrc/promlite.cpp``: one C call per update) or
+    the Python ones above, which are their oracle (``CRON_OPERATOR_NATIVE_METRICS=python``)."""
+    want = os.environ.get("CRON_OPERATOR_NATIVE_METRICS", "auto").lower()
+    if want != "python":
+        try:
+            from ..ops import build as _build
+
+            if _build.needs_build("_promlite"):
+                _build.build_extension("_promlite")
+            from ..ops import _promlite  # type: ignore[attr-defined]
+
+            return _promlite.Counter, _promlite.Gauge, _promlite.Histogram
+        except Exception:  # noqa: BLE001 - the Python series remain
+            if want == "native":
+                raise
+    return _PyCounterChild, _PyGaugeChild, _PyHistogramChild
+
+
+_CounterChild, _GaugeChild, _HistogramChild = _series_classes()
+NATIVE = _CounterChild is not _PyCounterChild
 
 
 class Histogram(_Metric):

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Host sanitizer run of the native extensions (ASan + UBSan).
 
-Builds ``_cron_engine``, ``_fastjson``, ``_httpcodec``, ``_netconn`` and ``_aioloop`` from ``ops/csrc`` with
-``-fsanitize=address,undefined`` into a scratch directory, re-executes itself with
+Builds ``_cron_engine``, ``_fastjson``, ``_httpcodec``, ``_netconn``, ``_aioloop`` and ``_promlite``
+from ``ops/csrc`` with ``-fsanitize=address,undefined`` into a scratch directory, re-executes itself with
 the sanitizer runtimes preloaded (CPython itself is not instrumented), and drives
 every entry point with mutated and generated inputs:
 
@@ -15,6 +15,7 @@ every entry point with mutated and generated inputs:
   (store_apply) over malformed objects;
 * ``_aioloop``: random programs of call_soon/call_at/cancel/raising callbacks/readers on the
   native loop core (also the loop the ``_netconn`` cases run on), handle reprs and collection;
+* ``_promlite``: random bounds and values (NaN, infinities, ints) through the metric series;
 * ``_cron_engine``: random and malformed cron specs through parse/next/missed, mutated and
   out-of-range RFC 3339 timestamps through rfc3339_z/format_rfc3339;
 
@@ -33,7 +34,7 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "cron_operator_amd", "ops", "csrc")
 EXTS = {"_cron_engine": "cron_engine.cpp", "_fastjson": "fastjson.cpp", "_httpcodec": "httpcodec.cpp",
-        "_netconn": "netconn.cpp", "_aioloop": "aioloop.cpp"}
+        "_netconn": "netconn.cpp", "_aioloop": "aioloop.cpp", "_promlite": "promlite.cpp"}
 LIBS = {"_netconn": ["-lssl", "-lcrypto"]}
 
 
@@ -169,6 +170,20 @@ def drive(scratch: str, iters: int) -> None:
     for _ in range(iters // 4):
         ce.rfc3339_z(_mutate(rng, b"2026-01-01T12:00:00Z").decode("latin-1"))
         ce.format_rfc3339(rng.randint(-2**62, 2**62), rng.randint(-5, 2 * 10**9), rng.randint(-400000, 400000))
+    import _promlite as pm  # noqa: E402
+
+    for _ in range(iters // 20):
+        h = pm.Histogram(tuple(sorted(rng.uniform(-10, 10) for _ in range(rng.randint(0, 12)))))
+        c, g = pm.Counter(), pm.Gauge()
+        for _ in range(rng.randint(0, 30)):
+            v = rng.choice([rng.uniform(-20, 20), float("nan"), float("inf"), -float("inf"), rng.randint(-5, 5)])
+            h.observe(v)
+            g.set(v)
+            try:
+                c.inc(v)
+            except ValueError:
+                pass
+        h.counts, h.sum, h.count, c.get(), g.get()
     loops = drive_aioloop(rng, iters // 20)
     net = drive_netconn(rng, iters // 20)
     print(f"sanitize ok: {iters} http, {iters // 4} json, {iters // 4} cron, {loops} loop programs, "

@@ -109,3 +109,76 @@ def test_available_cpus_reads_cgroup_quotas(tmp_path):
     a = build_parser().parse_args(["start", "--shard-processes", "auto"])
     assert a.shard_processes >= 1
     assert build_parser().parse_args(["start", "--shard-processes", "3"]).shard_processes == 3
+
+
+# ---------------------------------------------------------------- native series vs their Python twins
+
+_native = pytest.mark.skipif(not pl.NATIVE, reason="_promlite not built or disabled")
+_num = st.one_of(st.floats(allow_nan=True, allow_infinity=True), st.integers(-10**6, 10**6))
+
+
+@_native
+@settings(max_examples=200, deadline=None)
+@given(bounds=st.lists(st.floats(-1e6, 1e6, allow_nan=False), min_size=1, max_size=20).map(lambda b: tuple(sorted(b))),
+       values=st.lists(_num, max_size=60))
+def test_native_histogram_matches_python_series(bounds, values):
+    nat, py = pl._HistogramChild(bounds), pl._PyHistogramChild(bounds)
+    for v in values:
+        nat.observe(v)
+        py.observe(v)
+    assert nat.counts == py.counts and nat.count == py.count and nat.bounds == py.bounds
+    assert (nat.sum == py.sum) or (nat.sum != nat.sum and py.sum != py.sum)  # NaN sums stay NaN
+
+
+@_native
+@settings(max_examples=200, deadline=None)
+@given(ops=st.lists(st.tuples(st.sampled_from(["inc", "dec", "set", "inc1"]), _num), max_size=40))
+def test_native_counter_and_gauge_match_python_series(ops):
+    pairs = [(pl._CounterChild(), pl._PyCounterChild()), (pl._GaugeChild(), pl._PyGaugeChild())]
+    for op, v in ops:
+        for nat, py in pairs:
+            fn = op[:3]
+            if not hasattr(py, fn):
+                continue
+            outcomes = []
+            for s in (nat, py):
+                try:
+                    getattr(s, fn)() if op == "inc1" else getattr(s, fn)(v)
+                    outcomes.append(None)
+                except ValueError as e:
+                    outcomes.append(str(e))
+            assert outcomes[0] == outcomes[1]
+            assert (nat.value == py.value) or (nat.value != nat.value and py.value != py.value)
+            assert nat.get() == nat.value or nat.value != nat.value
+
+
+@_native
+def test_native_series_render_like_python_series(monkeypatch):
+    def expo():
+        reg = pl.Registry()
+        c = pl.Counter("c_total", "c", ["code"], registry=reg)
+        g = pl.Gauge("g", "g", registry=reg)
+        h = pl.Histogram("h_seconds", "h", ["verb"], buckets=(0.1, 1.0), registry=reg)
+        c.labels("200").inc(3)
+        g.set(7)
+        g.dec(2.5)
+        for v in (0.05, 0.1, 0.5, 3.0):
+            h.labels("GET").observe(v)
+        return reg.exposition()
+
+    native = expo()
+    monkeypatch.setattr(pl, "_CounterChild", pl._PyCounterChild)
+    monkeypatch.setattr(pl, "_GaugeChild", pl._PyGaugeChild)
+    monkeypatch.setattr(pl, "_HistogramChild", pl._PyHistogramChild)
+    assert native == expo()
+
+
+@_native
+def test_native_series_refuse_bad_arguments():
+    with pytest.raises(ValueError, match="counters can only increase"):
+        pl._CounterChild().inc(-1)
+    with pytest.raises(TypeError):
+        pl._CounterChild().inc("x")
+    with pytest.raises(ValueError):
+        pl._HistogramChild((2.0, 1.0))
+    assert pl._GaugeChild().set("2.5") is None  # float(value), like the Python series
