@@ -451,6 +451,12 @@ class Informer:
                         async for etype, obj in w:
                             self._last_item = loop.time()
                             self._on_item(etype, obj)
+                except BaseException:
+                    # an ERROR event, a failing handler or a cancel ends this watch: close it, or its
+                    # connection stays registered with the loop and keeps buffering events nobody
+                    # takes (the next attempt resumes from last_rv on a new one)
+                    w.stop()
+                    raise
                 finally:
                     self._disarm_watchdog()
                 backoff = 0.1

@@ -308,3 +308,64 @@ async def test_http_watch_carries_timeout_and_survives_a_silent_connection():
         await inf.stop()
         await client.close()
         await app.stop()
+
+
+async def test_failing_event_handler_closes_its_watch_and_the_informer_resumes():
+    """A handler exception ends the watch loop's attempt: the stream it was reading is closed
+    (not left registered with the loop buffering events nobody takes) and the next attempt
+    resumes from the last applied resourceVersion, so no event is lost."""
+    from cron_operator_amd.apiserver.http import APIServerApp
+    from cron_operator_amd.runtime.client import Client
+    from cron_operator_amd.runtime.http import HttpTransport
+    from cron_operator_amd.runtime.informer import EventHandler, Informer
+    from cron_operator_amd.runtime.kubeconfig import RestConfig
+
+    CM = GroupVersionResource("", "v1", "configmaps")
+    env = TestEnv()
+    app = APIServerApp(env.server)
+    port = await app.start("127.0.0.1", 0)
+    client = Client(HttpTransport(RestConfig(host=f"http://127.0.0.1:{port}")), qps=-1)
+    streams = []
+    orig_watch = client.transport.watch
+
+    async def spy_watch(gvr, namespace="", params=None, **kw):
+        s = await orig_watch(gvr, namespace, params, **kw)
+        stops = []
+        real_stop = s.stop
+        s.stop = lambda: (stops.append(1), real_stop())  # type: ignore[assignment]
+        streams.append(stops)
+        return s
+
+    client.transport.watch = spy_watch  # type: ignore[assignment]
+    inf = Informer(client, CM, NS)
+    boom = [True]
+    added = []
+
+    def on_add(o):
+        name = o["metadata"]["name"]
+        if name == "bad" and boom[0]:
+            boom[0] = False
+            raise RuntimeError("handler bug")
+        added.append(name)
+
+    inf.add_handler(EventHandler(on_add=on_add))
+    try:
+        inf.start()
+        await asyncio.wait_for(inf.synced.wait(), 10)
+        for _ in range(500):
+            await asyncio.sleep(0.01)
+            if streams:
+                break
+        for name in ("bad", "after"):
+            env.server.create(CM, NS, {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": name}})
+        for _ in range(300):
+            await asyncio.sleep(0.02)
+            if len(streams) >= 2 and "after" in added:
+                break
+        assert streams[0], "the watch whose handler failed was not closed"
+        assert len(streams) >= 2 and "after" in added
+        assert inf.get(NS, "bad") is not None and inf.get(NS, "after") is not None
+    finally:
+        await inf.stop()
+        await client.close()
+        await app.stop()
