@@ -31,6 +31,7 @@ EXTENSIONS: Dict[str, List[str]] = {
     "_netconn": ["netconn.cpp"],
     "_aioloop": ["aioloop.cpp"],
     "_promlite": ["promlite.cpp"],
+    "_workqueue": ["workqueue.cpp"],
 }
 # headers each extension includes (a change rebuilds it)
 HEADERS: Dict[str, List[str]] = {

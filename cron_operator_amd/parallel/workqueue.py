@@ -26,6 +26,7 @@ from __future__ import annotations
 import asyncio
 import heapq
 import itertools
+import os
 import time
 from collections import deque
 from typing import Deque, Dict, Hashable, List, Optional, Set, Tuple
@@ -40,9 +41,31 @@ class ShutDown(Exception):
     pass
 
 
+_EMPTY = object()  # get(): nothing queued
+
+
+def _new_core(depth, adds, latency, work):
+    """A ``_workqueue.Core`` (``ops/csrc/workqueue.cpp``), or None without the extension or with
+    ``CRON_OPERATOR_NATIVE_QUEUE=python``."""
+    want = os.environ.get("CRON_OPERATOR_NATIVE_QUEUE", "auto").lower()
+    if want == "python":
+        return None
+    try:
+        from ..ops import build as _build
+
+        if _build.needs_build("_workqueue"):
+            _build.build_extension("_workqueue")
+        from ..ops import _workqueue  # type: ignore[attr-defined]
+    except Exception:  # noqa: BLE001 - the Python core remains
+        if want == "native":
+            raise
+        return None
+    return _workqueue.Core(depth, adds, latency, work, _EMPTY)
+
+
 class WorkQueue:
     def __init__(self, name: str = "", clock: Optional[Clock] = None, rate_limiter: Optional[RateLimiter] = None,
-                 controller: str = ""):
+                 controller: str = "", native: Optional[bool] = None):
         self.name = name
         self.clock = clock or RealClock()
         self.rate_limiter = rate_limiter or default_controller_rate_limiter()
@@ -68,12 +91,27 @@ class WorkQueue:
         self._m_retries = metrics.WQ_RETRIES.labels(*lbl)
         self._m_unfinished = metrics.WQ_UNFINISHED.labels(*lbl)
         self._m_longest = metrics.WQ_LONGEST.labels(*lbl)
-        self.adds = 0
-        self.gets = 0
+        self._adds = 0
+        self._gets = 0
+        # the queueing core (dedupe, parking, priorities, metering) in C++ when built; the
+        # Python methods below are its fallback and oracle (CRON_OPERATOR_NATIVE_QUEUE=python)
+        self._core = _new_core(self._m_depth, self._m_adds, self._m_latency, self._m_work) \
+            if native is not False else None
+        if self._core is not None:
+            self.add = self._core.add  # type: ignore[method-assign]
+            self.done = self._core.done  # type: ignore[method-assign]
+
+    @property
+    def adds(self) -> int:
+        return self._core.adds if self._core is not None else self._adds
+
+    @property
+    def gets(self) -> int:
+        return self._core.gets if self._core is not None else self._gets
 
     # ------------------------------------------------------------------ core queue
     def __len__(self) -> int:
-        return len(self._queued)
+        return len(self._core) if self._core is not None else len(self._queued)
 
     def _push(self, item: Hashable, priority: int) -> None:
         entry = (-priority, next(self._seq))
@@ -98,41 +136,55 @@ class WorkQueue:
         if item in self._processing:
             prev = self._dirty.get(item)
             if prev is None:
-                self.adds += 1
+                self._adds += 1
                 self._m_adds.inc()
             self._dirty[item] = priority if prev is None else max(prev, priority)
             return
-        self.adds += 1
+        self._adds += 1
         self._m_adds.inc()
         self._push(item, priority)
 
     async def get(self) -> Hashable:
         """Next key (waits).  Raises :class:`ShutDown` once shut down and drained."""
+        core = self._core
+        pop = core.pop if core is not None else self._pop
         while True:
-            while self._heap:
-                negp, seq, item = heapq.heappop(self._heap)
-                live = self._queued.get(item)
-                if live is None or live != (negp, seq):
-                    continue  # stale entry
-                del self._queued[item]
-                self._processing.add(item)
-                now = time.perf_counter()
-                t_add = self._added_at.pop(item, now)
-                self._m_latency.observe(now - t_add)
-                self._started_at[item] = now
-                self._m_depth.set(len(self._queued))
-                self.gets += 1
+            item = pop()
+            if item is not _EMPTY:
                 return item
             if self._shutdown:
                 raise ShutDown()
             fut = asyncio.get_running_loop().create_future()
-            self._waiters.append(fut)
+            if core is not None:
+                core.add_waiter(fut)
+            else:
+                self._waiters.append(fut)
             try:
                 await fut
             except asyncio.CancelledError:
-                if fut in self._waiters:
+                if core is not None:
+                    core.remove_waiter(fut)
+                elif fut in self._waiters:
                     self._waiters.remove(fut)
                 raise
+
+    def _pop(self) -> Hashable:
+        """The most urgent queued key, now processing; ``_EMPTY`` when nothing is queued."""
+        while self._heap:
+            negp, seq, item = heapq.heappop(self._heap)
+            live = self._queued.get(item)
+            if live is None or live != (negp, seq):
+                continue  # stale entry
+            del self._queued[item]
+            self._processing.add(item)
+            now = time.perf_counter()
+            t_add = self._added_at.pop(item, now)
+            self._m_latency.observe(now - t_add)
+            self._started_at[item] = now
+            self._m_depth.set(len(self._queued))
+            self._gets += 1
+            return item
+        return _EMPTY
 
     def done(self, item: Hashable) -> None:
         self._processing.discard(item)
@@ -147,6 +199,8 @@ class WorkQueue:
         self._shutdown = True
         if self._timer is not None:
             self._timer.cancel()
+        if self._core is not None:
+            self._core.shutdown()
         while self._waiters:
             fut = self._waiters.popleft()
             if not fut.done():
@@ -157,15 +211,18 @@ class WorkQueue:
         return self._shutdown
 
     def processing(self) -> int:
-        return len(self._processing)
+        return self._core.processing() if self._core is not None else len(self._processing)
 
     def idle(self) -> bool:
         """Nothing queued, parked or in flight (delayed items do not count)."""
+        if self._core is not None:
+            return self._core.idle()
         return not self._queued and not self._processing and not self._dirty
 
     def update_unfinished_metrics(self) -> None:
         now = time.perf_counter()
-        ages = [now - t for t in self._started_at.values()]
+        started = self._core.started() if self._core is not None else self._started_at.values()
+        ages = [now - t for t in started]
         self._m_unfinished.set(sum(ages))
         self._m_longest.set(max(ages) if ages else 0.0)
 

@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Host sanitizer run of the native extensions (ASan + UBSan).
 
-Builds ``_cron_engine``, ``_fastjson``, ``_httpcodec``, ``_netconn``, ``_aioloop`` and ``_promlite``
-from ``ops/csrc`` with ``-fsanitize=address,undefined`` into a scratch directory, re-executes itself with
+Builds ``_cron_engine``, ``_fastjson``, ``_httpcodec``, ``_netconn``, ``_aioloop``, ``_promlite`` and
+``_workqueue`` from ``ops/csrc`` with ``-fsanitize=address,undefined`` into a scratch directory, re-executes itself with
 the sanitizer runtimes preloaded (CPython itself is not instrumented), and drives
 every entry point with mutated and generated inputs:
 
@@ -16,6 +16,8 @@ every entry point with mutated and generated inputs:
 * ``_aioloop``: random programs of call_soon/call_at/cancel/raising callbacks/readers on the
   native loop core (also the loop the ``_netconn`` cases run on), handle reprs and collection;
 * ``_promlite``: random bounds and values (NaN, infinities, ints) through the metric series;
+* ``_workqueue``: random add/pop/done/shutdown sequences with priorities, waiters and
+  cancelled waiters;
 * ``_cron_engine``: random and malformed cron specs through parse/next/missed, mutated and
   out-of-range RFC 3339 timestamps through rfc3339_z/format_rfc3339;
 
@@ -34,7 +36,8 @@ import tempfile
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "cron_operator_amd", "ops", "csrc")
 EXTS = {"_cron_engine": "cron_engine.cpp", "_fastjson": "fastjson.cpp", "_httpcodec": "httpcodec.cpp",
-        "_netconn": "netconn.cpp", "_aioloop": "aioloop.cpp", "_promlite": "promlite.cpp"}
+        "_netconn": "netconn.cpp", "_aioloop": "aioloop.cpp", "_promlite": "promlite.cpp",
+        "_workqueue": "workqueue.cpp"}
 LIBS = {"_netconn": ["-lssl", "-lcrypto"]}
 
 
@@ -72,6 +75,20 @@ def _tree(rng: random.Random, depth: int = 0):
     if r < 0.65:
         return {rng.choice("abcdefgh") + str(i): _tree(rng, depth + 1) for i in range(rng.randint(0, 5))}
     return [_tree(rng, depth + 1) for _ in range(rng.randint(0, 5))]
+
+
+class FakeFuture:
+    """The future interface the work-queue core calls (done / set_result)."""
+
+    def __init__(self) -> None:
+        self.result = None
+        self._done = False
+
+    def done(self) -> bool:
+        return self._done
+
+    def set_result(self, v) -> None:
+        self._done, self.result = True, v
 
 
 def drive(scratch: str, iters: int) -> None:
@@ -184,6 +201,28 @@ def drive(scratch: str, iters: int) -> None:
             except ValueError:
                 pass
         h.counts, h.sum, h.count, c.get(), g.get()
+    import _workqueue as wqm  # noqa: E402
+
+    empty = object()
+    for _ in range(iters // 20):
+        q = wqm.Core(pm.Gauge(), pm.Counter(), pm.Histogram((0.1, 1.0)), pm.Histogram((0.1, 1.0)), empty)
+        for _ in range(rng.randint(0, 60)):
+            op, k = rng.random(), ("ns", f"k{rng.randint(0, 6)}")
+            if op < 0.4:
+                q.add(k, rng.randint(-3, 3))
+            elif op < 0.65:
+                q.pop()
+            elif op < 0.85:
+                q.done(k)
+            elif op < 0.9:
+                fut = FakeFuture()
+                q.add_waiter(fut)
+                if rng.random() < 0.5:
+                    q.remove_waiter(fut)
+            elif op < 0.92:
+                q.shutdown()
+            else:
+                len(q), q.processing(), q.idle(), q.started()
     loops = drive_aioloop(rng, iters // 20)
     net = drive_netconn(rng, iters // 20)
     print(f"sanitize ok: {iters} http, {iters // 4} json, {iters // 4} cron, {loops} loop programs, "
