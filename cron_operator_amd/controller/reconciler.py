@@ -943,7 +943,13 @@ class CronReconciler(Reconciler):
         limit = cron.spec.history_limit if cron.spec.history_limit is not None else MAX_INT
         cut = len(terminated) - limit  # the oldest `cut` children are beyond the history limit
         if cut > 0:
+            memo = self.codecs.memo if self.codecs is not None else None
             for info in terminated[:cut]:
+                he = info.history_entry
+                if memo is not None and he is not None and he._json is not None:
+                    # its status-history entry leaves for good: the codecs' memo need not keep it
+                    # (else dead entries fill the table -- ~1 KiB per fire -- until collisions evict them)
+                    memo.forget(he._json)
                 w = info.obj
                 m = w.get("metadata") or {}  # type: ignore[union-attr]
                 wgvk = GroupVersionKind.from_object(w)

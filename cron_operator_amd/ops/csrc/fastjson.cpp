@@ -500,6 +500,20 @@ struct MemoTable {
     by_obj[ptr_hash(o) & mask] = static_cast<uint32_t>(i + 1);
     ++stores;
   }
+  // drop the slot holding exactly `o` (found through the pointer map; false when that entry was
+  // overwritten meanwhile -- the slot is then reclaimed by the next collision instead)
+  bool forget(const PyObject* o) {
+    uint32_t& ref = by_obj[ptr_hash(o) & mask];
+    if (ref == 0) return false;
+    MemoSlot& sl = slots[ref - 1];
+    if (sl.obj != o) return false;
+    ref = 0;
+    std::string().swap(sl.bytes);  // release the buffer, not just the length
+    sl.hash = 0;
+    sl.canonical = false;
+    Py_CLEAR(sl.obj);
+    return true;
+  }
   // this encoder's bytes for exactly `o`, or nullptr
   const std::string* canonical_bytes(const PyObject* o) {
     const uint32_t i = by_obj[ptr_hash(o) & mask];
@@ -1672,9 +1686,15 @@ PyObject* memo_clear(PyObject* self, PyObject*) {
   Py_RETURN_NONE;
 }
 
+PyObject* memo_forget(PyObject* self, PyObject* o) {
+  return PyBool_FromLong(reinterpret_cast<MemoObject*>(self)->table->forget(o));
+}
+
 PyMethodDef memo_methods[] = {
     {"stats", memo_stats, METH_NOARGS, "hits, misses, stores, used and total slots"},
     {"clear", memo_clear, METH_NOARGS, "drop every remembered object"},
+    {"forget", memo_forget, METH_O,
+     "forget(obj) -> bool: drop the entry remembering exactly obj (a value that will not be met again)"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyTypeObject MemoType = {PyVarObject_HEAD_INIT(nullptr, 0)};

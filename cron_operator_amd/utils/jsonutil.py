@@ -200,6 +200,9 @@ class PyMemo:
     def stats(self) -> Dict[str, int]:
         return {"hits": 0, "misses": 0, "stores": 0, "used": 0, "slots": self.slots}
 
+    def forget(self, obj: Any) -> bool:
+        return False
+
     def clear(self) -> None:
         pass
 

@@ -135,6 +135,10 @@ def drive(scratch: str, iters: int) -> None:
         assert codec.dumpb(doc) == fj.dumpb(doc)  # second time: memo values copied by identity
         back = codec.loads(codec.dumpb(doc))
         assert back["h"] == hist and "s" not in back
+        for v in hist + [doc["m"], back["m"]]:  # forgotten values re-encode byte-exactly
+            if rng.random() < 0.5:
+                memo.forget(v)
+        assert codec.dumpb(doc) == fj.dumpb(doc)
     # kubeflow job-status summaries over random (often ill-typed) statuses
     times = ["2026-01-01T12:00:00Z", "2026-01-01T12:00:00.123+02:00", "2026-13-01T00:00:00Z", "", "x" * 30,
              "2026-01-01T12:00:00Z\n", "٢٠٢٦-01-01T12:00:00Z"]

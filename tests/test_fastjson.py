@@ -248,6 +248,50 @@ def test_codec_memo_reuses_objects_across_documents_and_from_the_encoder():
     assert memo.stats()["used"] == 0
 
 
+
+def test_memo_forget_drops_exactly_that_entry():
+    memo = m.Memo()
+    enc = m.Codec(memo_paths=[("status", "history", "*")], memo=memo)
+    dec = m.Codec(memo_paths=[("object", "status", "history", "*")], memo=memo)
+    entries = [{"uid": f"u{i}", "status": "Succeeded"} for i in range(3)]
+    enc.dumpb({"status": {"history": entries}})
+    used = memo.stats()["used"]
+    assert memo.forget(entries[0]) is True and memo.stats()["used"] == used - 1
+    assert memo.forget(entries[0]) is False and memo.forget({"uid": "u1", "status": "Succeeded"}) is False
+    ev = json.dumps({"type": "MODIFIED", "object": {"status": {"history": entries}}}, separators=(",", ":"))
+    _, o = dec(ev.encode())
+    # the forgotten entry decodes afresh (equal, not identical); the others are still shared
+    assert o["status"]["history"] == entries
+    assert o["status"]["history"][0] is not entries[0]
+    assert o["status"]["history"][1] is entries[1] and o["status"]["history"][2] is entries[2]
+    # and the encoder re-encodes it (byte-exact) instead of copying remembered bytes
+    assert enc.dumpb({"status": {"history": entries}}) == \
+        json.dumps({"status": {"history": entries}}, separators=(",", ":")).encode()
+
+
+def test_reconciler_forgets_history_entries_it_rotates_out():
+    """A Cron's history keeps historyLimit entries; the entries it drops are forgotten by the
+    shared wire memo, so the memo holds the live set instead of every entry ever written."""
+    from cron_operator_amd.bench.harness import BenchConfig, run_sync
+    from cron_operator_amd.controller import reconciler as rc
+
+    made = []
+    orig = rc.WireCodecs.__init__
+
+    def spy(self, *a, **k):
+        orig(self, *a, **k)
+        made.append(self)
+
+    rc.WireCodecs.__init__ = spy
+    try:
+        run_sync(BenchConfig(n_crons=30, steps=30, warmup=1, shards=1, transport="http"))
+    finally:
+        rc.WireCodecs.__init__ = orig
+    used = [c.memo.stats()["used"] for c in made]
+    # live: 10 history entries + a few per-Cron values (labels, owner references, spec) each;
+    # without forgetting, 30 more entries per tick stay (~1250 after 30 ticks)
+    assert used and max(used) < 30 * 16, used
+
 @settings(max_examples=200, deadline=None)
 @given(st.lists(json_values, max_size=4), json_values)
 def test_codec_encoder_reuses_remembered_bytes_by_identity(entries, other):
