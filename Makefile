@@ -161,6 +161,11 @@ kind-create-cluster: ## Create a kind cluster for e2e runs against a real apiser
 kind-load-image: docker-build ## Load the operator image into the kind cluster.
 	kind load docker-image $(IMG) --name $(KIND_CLUSTER)
 
+.PHONY: test-e2e-cluster
+test-e2e-cluster: kind-load-image deploy ## Real-cluster e2e (test/e2e analog): pod Running/Ready, authn'd /metrics via a curl pod, a Cron fires.
+	kubectl -n cron-operator-system rollout status deploy/cron-operator-controller-manager --timeout=180s
+	E2E_CLUSTER=1 $(PYTHON) -m pytest tests/test_e2e_cluster.py -v -p no:cacheprovider
+
 .PHONY: kind-delete-cluster
 kind-delete-cluster: ## Delete the kind cluster.
 	kind delete cluster --name $(KIND_CLUSTER)
