@@ -32,6 +32,15 @@ gloo barriers; there is no device work to ``torch.cuda.synchronize()``.
 busy), so it is the number that measures the product; it runs in the same invocation
 on the same Crons, after the timed run (``--single-process none`` skips it).
 
+``deployment_*``: the headline and its denominator run against a fake apiserver that
+answers as fast as its Python CPU allows, so the 60-70x ``vs_baseline`` mostly measures
+the fixture's O(namespace) label-selected LIST (the reference LISTs live on every
+reconcile).  A real cluster is latency-bound: TLS on every connection and an etcd
+quorum write behind every mutation.  ``deployment_value`` / ``deployment_baseline_value``
+are both algorithms in that shape (one process each, TLS + the harness's ``etcd`` latency
+model), run in this same invocation after the timed run; ``vs_baseline_deployment`` is
+their ratio (``--deployment none`` skips them).
+
 ``vs_baseline``: the reference publishes no numbers, so the denominator
 is the reference *algorithm* (``--mode reference``: live LIST per reconcile, status
 churn, no event filtering) run by this same invocation on the same Crons, after the
@@ -167,6 +176,11 @@ def main() -> int:
                          "rather than the fake apiserver")
     ap.add_argument("--single-steps", type=int, default=10)
     ap.add_argument("--single-warmup", type=int, default=3)
+    ap.add_argument("--deployment", choices=["measure", "none"], default="measure",
+                    help="also run both algorithms deployment-shaped (1 process, TLS + etcd latency model) in "
+                         "this invocation, outside the headline's timed region: deployment_* keys")
+    ap.add_argument("--deployment-steps", type=int, default=3)
+    ap.add_argument("--deployment-baseline-steps", type=int, default=2)
     ap.add_argument("--baseline-steps", type=int, default=2)
     ap.add_argument("--baseline-warmup", type=int, default=1)
     ap.add_argument("--out", default="", help="also write the full result JSON here")
@@ -181,7 +195,7 @@ def main() -> int:
         print(f"bench.py: --gpus {a.gpus} but WORLD_SIZE={world}; refusing to report n_gpus={a.gpus}",
               file=sys.stderr)
         return 2
-    from cron_operator_amd.bench.harness import BenchConfig, run_sync
+    from cron_operator_amd.bench.harness import LATENCY_PROFILES, BenchConfig, run_sync
 
     if a.shards <= 0:
         from cron_operator_amd.runtime.supervisor import available_cpus
@@ -247,6 +261,23 @@ def main() -> int:
         mine["ref_fires"] = bcfg.n_crons * bcfg.steps
         mine["ref_p50"] = bres.p50_latency_ms
         mine["ref_req_per_fire"] = bres.api_requests_per_fire
+
+    # deployment-shaped pair: TLS + etcd latency, one process, both algorithms (untimed for the headline)
+    if a.deployment == "measure" and a.transport == "http":
+        for tag, mode, steps in (("dep", "optimized", a.deployment_steps),
+                                 ("dep_ref", "reference", a.deployment_baseline_steps)):
+            dcfg = BenchConfig(n_crons=a.crons, steps=steps, warmup=1, history_limit=a.history_limit, mode=mode,
+                               transport="http", qps=a.qps, burst=a.burst, workers=a.workers,
+                               namespace=f"bench-{tag.replace('_', '-')}-r{rank}", shards=1,
+                               apiserver_latency="etcd", tls=True)
+            _barrier(dist)
+            dres = run_sync(dcfg)
+            _barrier(dist)
+            mine[f"{tag}_elapsed_s"] = dres.elapsed_s
+            mine[f"{tag}_fires"] = dcfg.n_crons * dcfg.steps
+            mine[f"{tag}_p50"] = dres.p50_latency_ms
+            mine[f"{tag}_p99"] = dres.p99_latency_ms
+            mine[f"{tag}_req_per_fire"] = dres.api_requests_per_fire
     if dist is not None:
         allr = [None] * world
         dist.all_gather_object(allr, mine)
@@ -317,6 +348,23 @@ def main() -> int:
                                                                  / sp_fires, 4),
                 "single_process_apiserver_busy_frac": round(max(r["sp_cpu_api"] / r["sp_elapsed_s"]
                                                                 for r in allr), 3),
+            })
+        if "dep_fires" in allr[0] and "dep_ref_fires" in allr[0]:
+            dv = sum(r["dep_fires"] for r in allr) / max(r["dep_elapsed_s"] for r in allr)
+            dbv = sum(r["dep_ref_fires"] for r in allr) / max(r["dep_ref_elapsed_s"] for r in allr)
+            out.update({
+                "deployment_config": {"operator_processes": 1, "tls": True, "apiserver_latency": "etcd",
+                                      "latency_model_s": LATENCY_PROFILES["etcd"],
+                                      "workers": a.workers, "qps": a.qps},
+                "deployment_value": round(dv, 2),
+                "deployment_p50_ms": round(max(r["dep_p50"] for r in allr), 2),
+                "deployment_p99_ms": round(max(r["dep_p99"] for r in allr), 2),
+                "deployment_api_requests_per_fire": round(sum(r["dep_req_per_fire"] for r in allr) / len(allr), 3),
+                "deployment_baseline_value": round(dbv, 2),
+                "deployment_baseline_p50_ms": round(max(r["dep_ref_p50"] for r in allr), 2),
+                "deployment_baseline_api_requests_per_fire": round(
+                    sum(r["dep_ref_req_per_fire"] for r in allr) / len(allr), 3),
+                "vs_baseline_deployment": round(dv / dbv, 3) if dbv else None,
             })
         print(json.dumps(out), flush=True)
         if a.out:

@@ -90,6 +90,7 @@ class BenchConfig:
     transport: str = "http"          # http | memory
     qps: float = -1.0                # client QPS (-1 = unthrottled)
     burst: int = 50
+    max_inflight: int = 64           # client cap on concurrent requests (cmd/main.py DEFAULT_MAX_INFLIGHT)
     workers: int = 10
     namespace: str = "bench"
     log_level: str = "error"
@@ -341,7 +342,7 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
 
         remote = _RemoteServer(tls=cfg.tls)
         remote.start()
-        transport = HttpTransport(remote.rest_config(), pool_size=max(16, cfg.workers * 2))
+        transport = HttpTransport(remote.rest_config(), pool_size=max(16, cfg.workers * 2, cfg.max_inflight))
         sslctx = remote.ssl_context()
         admin = aiohttp.ClientSession(connector=aiohttp.TCPConnector(ssl=sslctx) if sslctx else None)
 
@@ -423,7 +424,7 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
             await setup_client.close()
             return await _run_sharded(cfg, remote, admin, set_time, complete_jobs, on_step)
 
-        client = Client(transport, qps=cfg.qps, burst=cfg.burst)
+        client = Client(transport, qps=cfg.qps, burst=cfg.burst, max_inflight=cfg.max_inflight)
         opts = ReconcilerOptions.reference() if cfg.mode == "reference" else ReconcilerOptions()
         mgr = Manager(client, ManagerOptions(clock=clock, max_concurrent_reconciles=cfg.workers,
                                              health_probe_bind_address="0", metrics_bind_address="0",
@@ -588,6 +589,7 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
                 "--namespace", cfg.namespace, "--shard-index", str(i), "--shard-count", str(cfg.shards),
                 "--start-ns", str(T0_NS + NANOS // 2), "--workers", str(cfg.workers),
                 "--history-limit", str(cfg.history_limit), "--qps", str(cfg.qps), "--burst", str(cfg.burst),
+                "--max-inflight", str(cfg.max_inflight),
                 "--mode", cfg.mode, "--routing", cfg.shard_routing,
                 *(["--ca-file", remote.ca_file] if remote.ca_file else []),
                 env=env, stdin=asyncio.subprocess.PIPE, stdout=asyncio.subprocess.PIPE,

@@ -40,6 +40,7 @@ async def main() -> int:
     ap.add_argument("--history-limit", type=int, default=10)
     ap.add_argument("--qps", type=float, default=-1.0)
     ap.add_argument("--burst", type=int, default=50)
+    ap.add_argument("--max-inflight", type=int, default=64)
     ap.add_argument("--mode", default="optimized")
     ap.add_argument("--routing", default="hash", choices=["hash", "labels"])
     ap.add_argument("--ca-file", default="", help="https --url: verify the apiserver against this CA (as localhost)")
@@ -62,7 +63,8 @@ async def main() -> int:
     if a.ca_file:
         with open(a.ca_file, "rb") as fh:
             rc = RestConfig(host=a.url, ca_data=fh.read(), tls_server_name="localhost")
-    client = Client(HttpTransport(rc, pool_size=max(16, a.workers * 2)), qps=a.qps, burst=a.burst)
+    client = Client(HttpTransport(rc, pool_size=max(16, a.workers * 2, a.max_inflight)), qps=a.qps, burst=a.burst,
+                    max_inflight=a.max_inflight)
     opts = ReconcilerOptions.reference() if a.mode == "reference" else ReconcilerOptions()
     mgr = Manager(client, ManagerOptions(clock=clock, max_concurrent_reconciles=a.workers,
                                          health_probe_bind_address="0", metrics_bind_address="0",

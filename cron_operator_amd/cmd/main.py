@@ -8,7 +8,8 @@ flag of the reference keeps its name, default and meaning:
 flag                            default      reference
 ==============================  ===========  ==========================================
 --max-concurrent-reconciles     10           start.go:215
---qps / --burst                 30 / 50      start.go:218-219
+--qps / --burst                 150 / 300    start.go:218-219 (30 / 50 there; sized here for 1000+
+                                             minutely Crons, see docs/operations.md "Sizing qps")
 --metrics-bind-address          "0"          start.go:220 (0 disables)
 --health-probe-bind-address     ":8081"      start.go:222
 --leader-elect                  false        start.go:223
@@ -22,7 +23,7 @@ flag                            default      reference
 Additions: ``--kubeconfig``, ``--namespace`` (restrict the cache),
 ``--leader-elect-namespace``, ``--compat-mode`` (``reference`` restores every
 reference quirk, see :class:`~cron_operator_amd.controller.reconciler.ReconcilerOptions`),
-``--cron-engine``.  Extra subcommands: ``fake-apiserver`` (serve the in-process
+``--cron-engine``, ``--max-inflight-requests``.  Extra subcommands: ``fake-apiserver`` (serve the in-process
 apiserver over HTTP with the CRDs installed), ``crd`` (print the CRD) and
 ``version``.
 
@@ -68,6 +69,14 @@ def _processes(v: str) -> int:
         raise argparse.ArgumentTypeError(f"invalid --shard-processes {v!r} (an integer or 'auto')") from None
 
 
+# client sizing (docs/operations.md "Sizing qps"): ~4 requests per Cron fire, so 150 QPS carries
+# 2250 minutely Crons at 100% of the budget and 1000 at 45%; the burst absorbs a tick's first
+# CREATEs.  The reference ships 30 / 50 (start.go:218-219), which tops out near 450 Crons.
+DEFAULT_QPS = 150.0
+DEFAULT_BURST = 300
+DEFAULT_MAX_INFLIGHT = 64
+
+
 def build_parser() -> argparse.ArgumentParser:
     root = argparse.ArgumentParser(prog="cron-operator", description="Cron operator for scheduled ML training jobs "
                                                                      "(apps.kubedl.io/v1alpha1 Cron).")
@@ -76,9 +85,13 @@ def build_parser() -> argparse.ArgumentParser:
     st = sub.add_parser("start", help="Start manager")
     st.add_argument("--max-concurrent-reconciles", type=int, default=10,
                     help="The maximum number of concurrent reconciles for controller.")
-    st.add_argument("--qps", type=float, default=30.0, help="Maximum QPS to the Kubernetes API server from this "
-                                                            "client.")
-    st.add_argument("--burst", type=int, default=50, help="Maximum burst for throttle.")
+    st.add_argument("--qps", type=float, default=DEFAULT_QPS,
+                    help="Maximum QPS to the Kubernetes API server from this client. About 4 requests per Cron "
+                         "fire: N minutely Crons need N/15 QPS (default: 1000 Crons at 45%% of the budget).")
+    st.add_argument("--burst", type=int, default=DEFAULT_BURST, help="Maximum burst for throttle.")
+    st.add_argument("--max-inflight-requests", type=int, default=DEFAULT_MAX_INFLIGHT,
+                    help="Maximum concurrent API requests (watches excluded); more wait in priority order "
+                         "(tick CREATEs first). 0: unlimited.")
     st.add_argument("--metrics-bind-address", default="0", help="The address the metrics endpoint binds to. Use "
                                                                 ":8443 for HTTPS or :8080 for HTTP, or leave as 0 to "
                                                                 "disable the metrics service.")
@@ -231,7 +244,7 @@ async def run_start(a: argparse.Namespace) -> int:
     except ValueError as e:
         log.error(e, "invalid --sync-period")
         return 2
-    client = Client(HttpTransport(cfg), qps=a.qps, burst=a.burst)
+    client = Client(HttpTransport(cfg), qps=a.qps, burst=a.burst, max_inflight=a.max_inflight_requests)
     mopts = ManagerOptions(namespace=a.namespace, leader_election=a.leader_elect,
                            leader_election_namespace=a.leader_elect_namespace,
                            metrics_bind_address=a.metrics_bind_address, secure_metrics=a.metrics_secure,
@@ -303,7 +316,7 @@ async def run_supervisor(a: argparse.Namespace, argv: List[str]) -> int:
             except ConfigError as e:
                 log.error(e, "unable to get kubeconfig")
                 return 1
-            client = Client(HttpTransport(cfg), qps=a.qps, burst=a.burst)
+            client = Client(HttpTransport(cfg), qps=a.qps, burst=a.burst, max_inflight=a.max_inflight_requests)
         metrics = MetricsServer(a.metrics_bind_address, secure=a.metrics_secure, cert_dir=a.metrics_cert_path,
                                 cert_name=a.metrics_cert_name, key_name=a.metrics_cert_key, client=client,
                                 enable_http2=a.enable_http2)

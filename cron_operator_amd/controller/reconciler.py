@@ -30,7 +30,24 @@ option                     default here                           reference
 ``wire_codecs``            watch events decoded by plan: child     every event decoded whole
                            ``spec`` skipped, Cron ``spec`` and
                            status history entries reused by bytes
+``defer_status_write``     the status PATCH and GC DELETEs after   the worker waits for the deferred
+                           a reconcile run as a deferred tail:     status patch (``:107-120``) after
+                           the worker is freed, the key stays      the CREATE (``:229-238``)
+                           processing until they land
+``request_priorities``     tick CREATEs (and Replace DELETEs) go   one FIFO token bucket for every
+                           first on a backed-up QPS bucket;        request
+                           status PATCHes / GC DELETEs / events
+                           yield to them
 =========================  =====================================  =======================================
+
+``defer_status_write`` (with a controller that accepts tails, ``runtime/controller.py``):
+a fire reconcile otherwise holds its worker for two sequential write round trips --
+the CREATE, then the status PATCH that records ``lastScheduleTime``.  The PATCH (and
+any history-GC DELETE still in flight) becomes the reconcile's *tail*: the worker takes
+the next Cron at once, while this Cron's key stays processing in the work queue until
+the tail has landed, so a requeue of the key during the tail is parked and never starts
+a second reconcile of it.  Under apiserver latency a tick's CREATEs then go out at
+workers / (one round trip) instead of workers / (two round trips).
 
 ``overlap_gc_deletes``: a GC DELETE's outcome feeds nothing else in the
 reconcile -- the reference only logs its error and drops the child from
@@ -69,7 +86,7 @@ import functools
 import json
 import operator
 from dataclasses import dataclass, field
-from typing import Any, Callable, Dict, List, Optional, Tuple
+from typing import Any, Awaitable, Callable, Dict, List, Optional, Tuple
 
 from ..api import errors
 from ..api.meta import (
@@ -104,6 +121,7 @@ from ..runtime import metrics, tracing
 from ..runtime.client import Client
 from ..runtime.controller import Reconciler, Request, Result
 from ..runtime.events import Normal, Warning, EventRecorder
+from ..runtime.ratelimit import PRIORITY_HIGH, PRIORITY_LOW, PRIORITY_NORMAL
 from ..runtime.informer import Cache, Informer
 from ..utils import aio, gctune, jsonutil
 from ..utils.clock import Clock, RealClock
@@ -160,6 +178,8 @@ def child_info(w: Dict[str, Any], gvk: GroupVersionKind, policy: WorkloadPolicy)
         sort_key = creation_timestamp(w).key()
     except Exception as e:  # noqa: BLE001 - kf.ConversionError, or a malformed object
         err = e
+        cls = None  # never "finished" with an error: it would reach history and fail there
+        sort_key = (0, 0)
     info = _ChildInfo(m.get("resourceVersion", ""), cls, sort_key, GroupVersionKind.from_object(w))
     info.obj = w
     info.name = m.get("name", "")
@@ -209,6 +229,8 @@ class ReconcilerOptions:
     overlap_gc_deletes: bool = True
     slim_child_cache: bool = True
     wire_codecs: bool = True
+    defer_status_write: bool = True
+    request_priorities: bool = True
     # cache mode: how long a reconcile waits for a new child informer's first LIST before
     # it falls back to a live LIST; a LIST that *fails* (403, 404, 5xx) is returned as the
     # reconcile's error at once, like the reference's live LIST (cron_controller.go:129-133)
@@ -226,6 +248,7 @@ class ReconcilerOptions:
                                  fold_created_into_active=False, skip_expected_events=False,
                                  classification_cache=False, dedupe_ran_tick=False,
                                  overlap_gc_deletes=False, slim_child_cache=False, wire_codecs=False,
+                                 defer_status_write=False, request_priorities=False,
                                  workload=WorkloadPolicy.reference())
 
 
@@ -355,6 +378,12 @@ class CronReconciler(Reconciler):
         self.codecs: Optional[WireCodecs] = codecs if codecs is not None or not self.opts.wire_codecs else \
             WireCodecs(self.opts.slim_child_cache)
         self.expect = Expectations(self.opts.expectation_ttl, self.clock)
+        # set by the controller wiring (setup_with_manager): its Controller accepts Result.tail,
+        # so with defer_status_write the reconcile hands its last writes back as a tail
+        self.defer_tails = False
+        prio = self.opts.request_priorities
+        self._p_create = PRIORITY_HIGH if prio else PRIORITY_NORMAL    # a tick's CREATE, Replace DELETEs
+        self._p_deferrable = PRIORITY_LOW if prio else PRIORITY_NORMAL  # status PATCH, history-GC DELETEs
         self.child_informers: Dict[GroupVersionKind, Informer] = {}
         self.on_child_informer: Optional[Callable[[GroupVersionKind, Informer], None]] = None
         # the child informers' selector, and labels stamped on every child (label-routed sharding)
@@ -433,11 +462,20 @@ class CronReconciler(Reconciler):
             result = Result()
             err: Optional[BaseException] = None
             gc: Optional[List["asyncio.Future[None]"]] = [] if self.opts.overlap_gc_deletes else None
+            deferring = self.defer_tails and self.opts.defer_status_write
+            fire: Optional[List[Callable[[], Awaitable[Result]]]] = [] if deferring else None
             try:
                 try:
-                    result = await self._sync(cron, log, gc)
+                    result = await self._sync(cron, log, gc, fire)
                 except Exception as e:  # noqa: BLE001 - joined with the patch error below
                     err = e
+                if deferring and err is None and (fire or gc or not old_status.semantic_equal(cron.status)):
+                    # the writes as a deferred tail: the controller frees this worker and keeps
+                    # the key processing until the CREATE, the status PATCH and the GC DELETEs land
+                    tail = asyncio.ensure_future(self._tail(old_obj, old_status, cron, log, key, gc,
+                                                            fire[0] if fire else None, result))
+                    gc = None  # owned by the tail now
+                    return dataclasses.replace(result, tail=tail)
                 # B2: deferred status patch when status changed semantically (cron_controller.go:107-120)
                 if not old_status.semantic_equal(cron.status):
                     try:
@@ -461,6 +499,39 @@ class CronReconciler(Reconciler):
             return result
         finally:
             log.info("Finish reconciling Cron")
+
+    async def _tail(self, old_obj: Dict[str, Any], old_status: CronStatus, cron: Cron, log: Logger, key: str,
+                    gc: Optional[List["asyncio.Future[None]"]], fire: Optional[Callable[[], Awaitable[Result]]],
+                    result: Result) -> Result:
+        """The writes of a reconcile whose worker has moved on (``defer_status_write``): the
+        tick's Replace DELETEs and CREATE (B16-B20, ``cron_controller.go:210-238``), then the
+        status PATCH (B2, ``:107-120``) -- which runs even when the CREATE failed, as the
+        reference's deferred patch does -- and the overlapped GC DELETEs.  Resolves to the
+        reconcile's Result, or raises its (joined) error; the controller requeues it with
+        backoff, like the reference's returned error."""
+        err: Optional[BaseException] = None
+        try:
+            if fire is not None:
+                try:
+                    result = await fire()
+                except Exception as e:  # noqa: BLE001 - joined with the patch error below
+                    err = e
+            if not old_status.semantic_equal(cron.status):
+                try:
+                    await self._patch_status(old_obj, cron, log, key)
+                except Exception as pe:  # noqa: BLE001
+                    perr = RuntimeError(f"failed to patch Cron status: {pe}")
+                    perr.__cause__ = pe
+                    err = JoinedError(err, perr) if err is not None else perr
+            if gc:
+                await self._await_gc(gc)
+        except asyncio.CancelledError:
+            if gc:
+                aio.cancel_all(gc)
+            raise
+        if err is not None:
+            raise err
+        return result
 
     async def _get_cron(self, req: Request) -> Optional[Dict[str, Any]]:
         if self.cron_informer is not None:
@@ -505,10 +576,10 @@ class CronReconciler(Reconciler):
                 with tracing.span("patch_status", bytes=len(body) if body.__class__ is bytes else
                                   len(jsonutil.dumps(patch))):
                     await self.client.patch(CRON_GVR, m.get("namespace", ""), m.get("name", ""), body, "merge",
-                                            "status", discard_response=True)
+                                            "status", discard_response=True, priority=self._p_deferrable)
             else:
                 await self.client.patch(CRON_GVR, m.get("namespace", ""), m.get("name", ""), body, "merge",
-                                        "status", discard_response=True)
+                                        "status", discard_response=True, priority=self._p_deferrable)
         except Exception:
             self.own_writes.pop(key, None)
             raise
@@ -541,7 +612,10 @@ class CronReconciler(Reconciler):
         return True
 
     # ------------------------------------------------------------------ the algorithm
-    async def _sync(self, cron: Cron, log: Logger, gc: Optional[List["asyncio.Future[None]"]] = None) -> Result:
+    async def _sync(self, cron: Cron, log: Logger, gc: Optional[List["asyncio.Future[None]"]] = None,
+                    fire: Optional[List[Callable[[], Awaitable[Result]]]] = None) -> Result:
+        """B3-B20.  ``fire`` (a list): a decided fire (B16-B20, API writes) is not run but
+        appended there as a coroutine function for the caller's deferred tail."""
         policy = self.opts.workload
         # spans (and the attributes they would carry) only when tracing is on
         traced = tracing.get_tracer().enabled
@@ -684,6 +758,17 @@ class CronReconciler(Reconciler):
             log.v(1).info(f"Skip creating new {gvk.kind} due to concurrency policy forbid", active=len(active))
             return scheduled
 
+        if fire is not None:
+            fire.append(functools.partial(self._fire, cron, gvk, active, missed_run, next_run, now, log, scheduled))
+            return scheduled
+        return await self._fire(cron, gvk, active, missed_run, next_run, now, log, scheduled)
+
+    async def _fire(self, cron: Cron, gvk: GroupVersionKind, active: List[Child], missed_run: GoTime,
+                    next_run: GoTime, now: GoTime, log: Logger, scheduled: Result) -> Result:
+        """B16-B20 (``cron_controller.go:210-238``): Replace, build the job, CREATE it, and
+        advance ``lastScheduleTime``."""
+        traced = tracing.get_tracer().enabled
+        chatty = log.enabled()
         # B16 (cron_controller.go:210-220)
         if cron.spec.concurrency_policy == ConcurrentPolicyReplace:
             for info in active:
@@ -695,7 +780,8 @@ class CronReconciler(Reconciler):
                     self.expect.expect_delete(self._ckey(cron), uid)
                 try:
                     await self.client.delete(gvk, m.get("namespace", ""), m.get("name", ""),
-                                             propagation_policy="Background", discard_response=True)
+                                             propagation_policy="Background", discard_response=True,
+                                             priority=self._p_create)
                     self.stats["deletes"] += 1
                     metrics.child(metrics.WORKLOADS_DELETED, gvk.kind, "replace").inc()
                 except errors.ApiError as e:
@@ -724,7 +810,8 @@ class CronReconciler(Reconciler):
             with (tracing.span("create_workload", kind=gvk.kind, name=wm.get("name", ""),
                                tick=missed_run.rfc3339()) if traced else tracing.NOOP) as sp:
                 created = await self.client.create(gvk, workload, wm.get("namespace", ""),
-                                                   decoder=self.codecs.child_object if self.codecs else None)
+                                                   decoder=self.codecs.child_object if self.codecs else None,
+                                                   priority=self._p_create)
                 if traced:
                     sp.set(tick_to_create_ms=(self.clock.now_ns() - missed_run.unix_nano()) / 1e6)
             self.stats["creates"] += 1
@@ -746,8 +833,11 @@ class CronReconciler(Reconciler):
                 self.latency_observer(self._ckey(cron), missed_run, created)
             self._m_sched_lat.observe(
                 max(0.0, (self.clock.now_ns() - missed_run.unix_nano()) / 1e9))
-        except BaseException as e:  # API or transport error, or cancellation: nothing is in flight
-            if self.opts.expectations:
+        except BaseException as e:  # API or transport error, or cancellation
+            if self.opts.expectations and not isinstance(e, asyncio.CancelledError):
+                # an API or transport error: nothing is in flight.  A cancelled CREATE (shutdown,
+                # leader loss) may already be stored: its pending mark stays until the informer
+                # sees the job or the TTL passes
                 self.expect.drop_pending(self._ckey(cron), wm.get("name", ""))
             if isinstance(e, errors.ApiError) and errors.is_already_exists(e):
                 log.info(f"{gvk.kind} already exists", **{gvk.kind: ref})
@@ -1010,7 +1100,8 @@ class CronReconciler(Reconciler):
         if self.opts.expectations:  # before the call: the watch event may beat the response
             self.expect.expect_delete(self._ckey(cron), uid)
         try:
-            await self.client.delete(gvk, namespace, name, propagation_policy="Background", discard_response=True)
+            await self.client.delete(gvk, namespace, name, propagation_policy="Background", discard_response=True,
+                                     priority=self._p_deferrable)
             self.stats["deletes"] += 1
             metrics.child(metrics.WORKLOADS_DELETED, gvk.kind, "history").inc()
         except asyncio.CancelledError:

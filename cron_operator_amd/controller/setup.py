@@ -49,6 +49,7 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
     rec = CronReconciler(mgr.client, mgr.cache, mgr.get_event_recorder_for(CONTROLLER_NAME), mgr.clock, engine,
                          opts, cron_inf, codecs)
     ctrl = Controller(CONTROLLER_NAME, rec, mgr.clock, mgr.opts.max_concurrent_reconciles, log)
+    rec.defer_tails = True  # this controller takes Result.tail (ReconcilerOptions.defer_status_write)
     ctrl.set_log_constructor(log_constructor(log, "Cron"))
     assigner: Optional[sharding.ShardAssigner] = None
     if count > 1:
@@ -60,6 +61,11 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
         await assigner.watch(mgr.cache, CRON_GVK, child=False)
         mgr.add(assigner.run)
     rec.shard_assigner = assigner
+    if assigner is not None:
+        def observed(gvk: GroupVersionKind, ns: str, name: str) -> bool:
+            inf = rec.child_informers.get(gvk)
+            return inf is not None and inf.get(ns, name, copy=False) is not None
+        assigner.observed = observed
 
     preds = []
     if opts.own_write_filter:
@@ -100,6 +106,8 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
             def observe_add(o) -> None:
                 if exp.created:
                     exp.observe_add(key_of(o), (o.get("metadata") or {}).get("uid", ""))
+                if exp.pending:  # a CREATE whose response never came (cancelled): the job is here
+                    exp.drop_pending(key_of(o), (o.get("metadata") or {}).get("name", ""))
 
             def observe_delete(o) -> None:
                 if exp.created or exp.deleted:

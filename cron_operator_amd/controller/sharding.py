@@ -3,11 +3,11 @@
 The reference runs one leader-elected replica; this operator can split
 its Crons across ``--shard-count`` replicas.  Two routings exist:
 
-``hash`` (default, :func:`cron_operator_amd.runtime.controller.shard_of`)
+``hash`` (:func:`cron_operator_amd.runtime.controller.shard_of`)
     every shard's informers hold *all* Crons and children, and the event handler
     drops the keys of other shards.  Nothing is written to user objects, but N
     shards decode and cache N times the watch traffic.
-``labels`` (this module)
+``labels`` (default; this module)
     every Cron and child carries ``kubedl.io/shard=<index>-of-<count>`` and shard
     *i*'s informers select on its own value, so the apiserver sends each event to
     one shard only.  Total operator work stays O(events) as shards are added.
@@ -24,11 +24,21 @@ relabelled the same way, keyed by their ``kubedl.io/cron-name`` label.
 
 A change of ``--shard-count`` needs every shard restarted with the new count, as
 with hash routing; objects are then relabelled in the background.
+
+**Assignment order.**  A Cron is labelled only after its own unassigned children are
+labelled *and* this shard's child informers hold them: were the Cron to join the
+shard's Cron informer first, its reconcile would list no running child -- under
+``Forbid`` it would start a second job beside the running one, under ``Replace`` it
+would miss the job it must delete, and ``status.active``/``history`` would drop
+entries.  This matters on the first start with label routing (a fresh install or an
+upgrade from hash routing, where every object is unlabelled) and after a change of
+shard count.  The wait for the informers is bounded (``observe_timeout``); a child
+deleted meanwhile never shows up there and only costs that bound.
 """
 from __future__ import annotations
 
 import asyncio
-from typing import Any, Dict, List, Optional, Set, Tuple
+from typing import Any, Callable, Dict, List, Optional, Set, Tuple
 
 from ..api import errors
 from ..api.meta import GroupVersionKind
@@ -36,6 +46,7 @@ from ..api.v1alpha1.groupversion import LABEL_CRON_NAME, LABEL_PREFIX_KUBEDL
 from ..runtime.client import Client
 from ..runtime.controller import shard_of
 from ..runtime.informer import Cache, EventHandler, Informer
+from ..utils import aio
 from ..utils.logging import Logger, get_logger
 
 LABEL_SHARD = LABEL_PREFIX_KUBEDL + "/shard"
@@ -78,7 +89,7 @@ class ShardAssigner:
     """Labels this shard's unassigned Crons and children (a leader-only runnable)."""
 
     def __init__(self, client: Client, index: int, count: int, workers: int = 4,
-                 retry_delay: float = 1.0, logger: Optional[Logger] = None):
+                 retry_delay: float = 1.0, logger: Optional[Logger] = None, observe_timeout: float = 10.0):
         if count < 1 or not 0 <= index < count:
             raise ValueError(f"invalid shard {index}/{count}")
         self.client = client
@@ -94,6 +105,16 @@ class ShardAssigner:
         self.labelled = 0
         self.errors = 0
         self._bg: Set[asyncio.Task] = set()
+        self.observe_timeout = observe_timeout
+        self._child_kinds: Set[GroupVersionKind] = set()
+        # (namespace, cron) -> child keys queued for labelling / labelled but maybe not observed yet
+        self._children_left: Dict[Tuple[str, str], Set[Tuple[GroupVersionKind, str, str]]] = {}
+        self._children_done: Dict[Tuple[str, str], List[Tuple[GroupVersionKind, str, str]]] = {}
+        # Crons parked until their children are labelled: (namespace, cron) -> the Cron's key
+        self._parked: Dict[Tuple[str, str], Tuple[GroupVersionKind, str, str]] = {}
+        self._child_owner: Dict[Tuple[GroupVersionKind, str, str], Tuple[str, str]] = {}
+        # does this shard's child informer hold the (labelled) child?  set by setup_with_manager
+        self.observed: Optional[Callable[[GroupVersionKind, str, str], bool]] = None
 
     def watch_soon(self, cache: Cache, gvk: GroupVersionKind, child: bool) -> asyncio.Task:
         """:meth:`watch` as a task the assigner holds on to (the loop keeps only weak
@@ -111,6 +132,8 @@ class ShardAssigner:
         sel = f"{LABEL_CRON_NAME},{unassigned_selector(self.count)}" if child else unassigned_selector(self.count)
         inf = await cache.get_informer(gvk, label_selector=sel, transform=metadata_only)
         self.informers[gvk] = inf
+        if child:
+            self._child_kinds.add(gvk)
         inf.add_handler(EventHandler(on_add=lambda o: self._offer(gvk, o, child),
                                      on_update=lambda _old, o: self._offer(gvk, o, child)))
         for o in list(inf.store.values()):
@@ -126,28 +149,70 @@ class ShardAssigner:
         if not self.owns(obj, child):
             return
         m = obj.get("metadata") or {}
-        key = (gvk, m.get("namespace", ""), m.get("name", ""))
+        ns = m.get("namespace", "")
+        key = (gvk, ns, m.get("name", ""))
         if key not in self._queued:
             self._queued.add(key)
+            if child:
+                ck = (ns, (m.get("labels") or {}).get(LABEL_CRON_NAME, ""))
+                self._children_left.setdefault(ck, set()).add(key)
+                self._child_owner[key] = ck
             self._queue.put_nowait(key)
 
     def pending(self) -> int:
         return len(self._queued)
 
     async def run(self) -> None:
+        # every unassigned child must be known before any Cron is labelled (assignment order)
+        await asyncio.gather(*(inf.synced.wait() for inf in list(self.informers.values())))
         tasks: List[asyncio.Task] = [asyncio.get_running_loop().create_task(self._worker())
                                      for _ in range(self.workers)]
         try:
             await asyncio.gather(*tasks)
         finally:
-            for t in tasks:
-                t.cancel()
+            # awaited, not only cancelled: no label PATCH may land after shutdown
+            await aio.cancel_and_wait(*tasks)
+
+    def _child_finished(self, key: Tuple[GroupVersionKind, str, str], labelled: bool) -> None:
+        """A child key left the queue (labelled, or gone): release its Cron when it was the last."""
+        ck = self._child_owner.pop(key, None)
+        left = self._children_left.get(ck) if ck is not None else None
+        if left is None:
+            return
+        left.discard(key)
+        if labelled:
+            self._children_done.setdefault(ck, []).append(key)  # type: ignore[arg-type]
+        if not left:
+            del self._children_left[ck]  # type: ignore[arg-type]
+            cron_key = self._parked.pop(ck, None)  # type: ignore[arg-type]
+            if cron_key is not None:
+                self._queue.put_nowait(cron_key)
+
+    async def _children_observed(self, ns: str, cron: str) -> None:
+        """Wait (bounded) until this shard's child informers hold the Cron's relabelled children."""
+        done = self._children_done.pop((ns, cron), None)
+        if not done or self.observed is None:
+            return
+        loop = asyncio.get_running_loop()
+        deadline = loop.time() + self.observe_timeout
+        while not all(self.observed(g, n, nm) for g, n, nm in done):
+            if loop.time() >= deadline:
+                self.log.info("Relabelled children not observed in time; assigning the Cron anyway",
+                              namespace=ns, cron=cron)
+                return
+            await asyncio.sleep(0.02)
 
     async def _worker(self) -> None:
         patch = {"metadata": {"labels": {LABEL_SHARD: self.value}}}
         while True:
             key = await self._queue.get()
             gvk, ns, name = key
+            child = gvk in self._child_kinds
+            if not child:
+                if self._children_left.get((ns, name)):
+                    self._parked[(ns, name)] = key  # re-queued by the last child's _child_finished
+                    continue
+                await self._children_observed(ns, name)
             try:
                 await self.client.patch(gvk, ns, name, patch, "merge", discard_response=True)
                 self.labelled += 1
@@ -160,10 +225,16 @@ class ShardAssigner:
                     if inf is not None and inf.get(ns, name, copy=False) is not None:
                         self._queue.put_nowait(key)  # still unassigned: retry
                         continue
+                if child:
+                    self._child_finished(key, False)
+                self._queued.discard(key)
+                continue
             except Exception as e:  # noqa: BLE001 - transport errors: retry later
                 self.errors += 1
                 self.log.error(e, "Failed to assign shard", kind=gvk.kind, namespace=ns, name=name)
                 await asyncio.sleep(self.retry_delay)
                 self._queue.put_nowait(key)
                 continue
+            if child:
+                self._child_finished(key, True)
             self._queued.discard(key)

@@ -25,7 +25,7 @@ from ..api.meta import GroupVersion, GroupVersionKind, GroupVersionResource
 from ..utils import jsonutil
 from ..utils.gotime import format_duration
 from . import metrics, tracing
-from .ratelimit import TokenBucket, make_client_limiter
+from .ratelimit import PRIORITY_NORMAL, InflightGate, TokenBucket, make_client_limiter
 
 GVRorGVK = Union[GroupVersionResource, GroupVersionKind]
 
@@ -281,9 +281,13 @@ class Client:
     """The controller's API client (controller-runtime ``client.Client`` analog)."""
 
     def __init__(self, transport: Transport, qps: float = 30.0, burst: int = 50,
-                 limiter: Optional[TokenBucket] = None, mapper: Optional[RESTMapper] = None):
+                 limiter: Optional[TokenBucket] = None, mapper: Optional[RESTMapper] = None,
+                 max_inflight: int = 0):
+        """``max_inflight`` > 0 caps concurrent requests (watches excluded); excess requests
+        wait in priority order (:class:`~.ratelimit.InflightGate`)."""
         self.transport = transport
         self.limiter = limiter if limiter is not None else make_client_limiter(qps, burst)
+        self.inflight: Optional[InflightGate] = InflightGate(max_inflight) if max_inflight > 0 else None
         self.mapper = mapper or RESTMapper(transport)
         self.host = getattr(transport, "host", "in-memory")
         cfg = getattr(transport, "config", None)
@@ -307,9 +311,9 @@ class Client:
         return (await self.mapper.resource_for(target))[0]
 
     async def _throttle(self, verb: str, gvr: GroupVersionResource, namespace: str, name: str,
-                        subresource: str) -> None:
+                        subresource: str, priority: int = PRIORITY_NORMAL) -> None:
         if self.limiter is not None:
-            d = await self.limiter.wait()
+            d = await self.limiter.wait(priority)
             m = self._m_rl.get(verb)
             if m is None:
                 m = self._m_rl[verb] = metrics.REST_RATE_LIMIT.labels(verb, self.host)
@@ -341,9 +345,21 @@ class Client:
                "delete": "DELETE", "deletecollection": "DELETE"}
 
     async def _do(self, verb: str, gvr: GroupVersionResource, namespace: str = "", name: str = "",
-                  subresource: str = "", body: Any = None, params: Optional[Dict[str, Any]] = None) -> Any:
+                  subresource: str = "", body: Any = None, params: Optional[Dict[str, Any]] = None,
+                  priority: int = PRIORITY_NORMAL) -> Any:
         if self.limiter is not None:
-            await self._throttle(verb, gvr, namespace, name, subresource)
+            await self._throttle(verb, gvr, namespace, name, subresource, priority)
+        gate = self.inflight
+        if gate is not None:
+            await gate.acquire(priority)
+            try:
+                return await self._send(verb, gvr, namespace, name, subresource, body, params)
+            finally:
+                gate.release()
+        return await self._send(verb, gvr, namespace, name, subresource, body, params)
+
+    async def _send(self, verb: str, gvr: GroupVersionResource, namespace: str, name: str, subresource: str,
+                    body: Any, params: Optional[Dict[str, Any]]) -> Any:
         self.requests += 1
         rbv = self.requests_by_verb
         rbv[verb] = rbv.get(verb, 0) + 1
@@ -392,9 +408,10 @@ class Client:
         ms[1].observe(time.perf_counter() - t0)
 
     # -- verbs
-    async def get(self, target: GVRorGVK, namespace: str, name: str) -> Dict[str, Any]:
+    async def get(self, target: GVRorGVK, namespace: str, name: str,
+                  priority: int = PRIORITY_NORMAL) -> Dict[str, Any]:
         gvr = self._gvr_now(target) or await self._gvr(target)
-        return await self._do("get", gvr, namespace, name)
+        return await self._do("get", gvr, namespace, name, priority=priority)
 
     async def list(self, target: GVRorGVK, namespace: str = "", label_selector: Optional[str] = None,
                    field_selector: Optional[str] = None, limit: int = 0,
@@ -440,9 +457,10 @@ class Client:
         return out
 
     async def create(self, target: GVRorGVK, obj: Dict[str, Any], namespace: Optional[str] = None,
-                     dry_run: bool = False, decoder: Any = None) -> Dict[str, Any]:
+                     dry_run: bool = False, decoder: Any = None, priority: int = PRIORITY_NORMAL) -> Dict[str, Any]:
         """``decoder``: a ``jsonutil.Codec`` for the returned object, e.g. one that skips the
-        ``spec`` the caller never reads (HTTP transports; others return the whole object)."""
+        ``spec`` the caller never reads (HTTP transports; others return the whole object).
+        ``priority``: the request's class on a backed-up QPS bucket (``ratelimit.PRIORITY_*``)."""
         ns = namespace if namespace is not None else (obj.get("metadata") or {}).get("namespace", "")
         gvr = self._gvr_now(target) or await self._gvr(target)
         params: Optional[Dict[str, Any]] = None
@@ -450,16 +468,18 @@ class Client:
             params = {"dryRun": "All"} if dry_run else {}
             if decoder is not None:
                 params[DECODE] = decoder
-        return await self._do("create", gvr, ns, body=obj, params=params)
+        return await self._do("create", gvr, ns, body=obj, params=params, priority=priority)
 
-    async def update(self, target: GVRorGVK, obj: Dict[str, Any], subresource: str = "") -> Dict[str, Any]:
+    async def update(self, target: GVRorGVK, obj: Dict[str, Any], subresource: str = "",
+                     priority: int = PRIORITY_NORMAL) -> Dict[str, Any]:
         m = obj.get("metadata") or {}
         gvr = self._gvr_now(target) or await self._gvr(target)
         return await self._do("update", gvr, m.get("namespace", ""), m.get("name", ""),
-                              subresource, body=obj)
+                              subresource, body=obj, priority=priority)
 
     async def patch(self, target: GVRorGVK, namespace: str, name: str, patch: Any, patch_type: str = MERGE,
-                    subresource: str = "", discard_response: bool = False) -> Dict[str, Any]:
+                    subresource: str = "", discard_response: bool = False,
+                    priority: int = PRIORITY_NORMAL) -> Dict[str, Any]:
         """``discard_response``: the caller does not read the result, so an HTTP transport
         need not decode the returned object (it is still received, and errors still raise).
         ``patch`` may be bytes already encoded by the caller (``Codec.dumpb``)."""
@@ -468,10 +488,11 @@ class Client:
             params[DISCARD] = True
         gvr = self._gvr_now(target) or await self._gvr(target)
         return await self._do("patch", gvr, namespace, name, subresource, body=patch,
-                              params=params)
+                              params=params, priority=priority)
 
     async def delete(self, target: GVRorGVK, namespace: str, name: str, propagation_policy: Optional[str] = None,
-                     preconditions: Optional[Dict[str, str]] = None, discard_response: bool = False) -> Any:
+                     preconditions: Optional[Dict[str, str]] = None, discard_response: bool = False,
+                     priority: int = PRIORITY_NORMAL) -> Any:
         opts: Dict[str, Any] = {}
         if propagation_policy:
             opts["propagationPolicy"] = propagation_policy
@@ -479,7 +500,7 @@ class Client:
             opts["preconditions"] = preconditions
         gvr = self._gvr_now(target) or await self._gvr(target)
         return await self._do("delete", gvr, namespace, name, body=opts or None,
-                              params={DISCARD: True} if discard_response else None)
+                              params={DISCARD: True} if discard_response else None, priority=priority)
 
     async def delete_all_of(self, target: GVRorGVK, namespace: str = "", label_selector: Optional[str] = None) -> Any:
         params = {"labelSelector": label_selector} if label_selector else {}

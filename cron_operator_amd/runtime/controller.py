@@ -15,6 +15,18 @@ worker loop it drives [ext]:
 * ``controller_runtime_*`` and ``workqueue_*`` metrics, per-request loggers from
   a log constructor (``internal/controller/util.go:27-41``) with a
   ``reconcileID``.
+
+**Deferred tails.**  A reconcile may hand back its last writes instead of waiting for
+them: ``Result.tail`` is a future that finishes those writes and resolves to the final
+:class:`Result` (or raises the reconcile's error).  The worker is then free to take the
+next key at once, while the key itself stays *processing* in the queue until the tail
+has finished -- the queue parks any new add of that key ("dirty") exactly as it does
+during the reconcile proper, so per-key serialisation and the no-duplicate guarantee
+are unchanged.  The reference's deferred status patch (``cron_controller.go:107-120``)
+runs on the worker goroutine after the CREATE (``:229-238``): under apiserver latency a
+fire then holds a worker for two sequential write round trips; with a tail it holds it
+for one.  ``max_tails`` bounds the tails in flight (past it a worker awaits its own
+tail inline, which is the plain behaviour).
 """
 from __future__ import annotations
 
@@ -45,6 +57,8 @@ class Result:
     requeue: bool = False
     requeue_after: float = 0.0  # seconds
     requeue_after_ns: int = 0   # exact form (schedule requeues land on the tick)
+    # a future finishing the reconcile's last writes; resolves to the final Result (see module doc)
+    tail: Optional["asyncio.Future[Result]"] = None
 
     def after_ns(self) -> int:
         return self.requeue_after_ns or int(self.requeue_after * 1e9)
@@ -89,7 +103,8 @@ def shard_of(namespace: str, name: str, count: int) -> int:
 
 class Controller:
     def __init__(self, name: str, reconciler: Reconciler, clock: Clock, max_concurrent_reconciles: int = 1,
-                 logger: Optional[Logger] = None, recover_panic: bool = True, queue: Optional[WorkQueue] = None):
+                 logger: Optional[Logger] = None, recover_panic: bool = True, queue: Optional[WorkQueue] = None,
+                 max_tails: int = 0):
         self.name = name
         self.reconciler = reconciler
         self.shard: Tuple[int, int] = (0, 1)
@@ -104,6 +119,10 @@ class Controller:
         self._sources: List[Tuple[Informer, EventHandler]] = []
         self._workers: List[asyncio.Task] = []
         self.active = 0
+        # deferred tails in flight (key stays processing until each one finishes); 0 -> default bound
+        self.max_tails = max_tails if max_tails > 0 else max(1024, 100 * self.max_concurrent)
+        self._tails: Dict["asyncio.Future[Result]", Tuple[Request, Logger, float]] = {}
+        self.tails_started = 0
         self.reconciles = 0
         self.errors = 0
         self.started = False
@@ -219,8 +238,13 @@ class Controller:
             c = self._m_total[label] = metrics.RECONCILE_TOTAL.labels(self.name, label)
         c.inc()
 
-    async def process_one(self, req: Request) -> None:
-        q = self.queue
+    def in_flight(self) -> int:
+        """Reconciles running on a worker plus deferred tails still writing."""
+        return self.active + len(self._tails)
+
+    async def process_one(self, req: Request) -> bool:
+        """Reconcile ``req``.  False: the reconcile left a deferred tail, which calls
+        ``queue.done(req)`` itself when it finishes; True: the caller calls it."""
         log = self._logger_for(req)
         self.active += 1
         self._m_active.value = float(self.active)
@@ -233,21 +257,56 @@ class Controller:
                     result = await self.reconciler.reconcile(req, log)
                     if result is None:
                         result = Result()
-                    sp.set(requeue_after_ms=result.after_ns() / 1e6)
+                    sp.set(requeue_after_ms=result.after_ns() / 1e6, deferred_tail=result.tail is not None)
             else:
                 result = await self.reconciler.reconcile(req, log)
                 if result is None:
                     result = Result()
+            tail = result.tail
+            if tail is not None and len(self._tails) >= self.max_tails:
+                result = await tail  # too many tails in flight: finish this one on the worker
+                tail = None
         except asyncio.CancelledError:
             raise
         except Exception as e:  # noqa: BLE001 - recover like RecoverPanic
             err = e
+            tail = None
             if not self.recover_panic:
                 raise
         finally:
             self.active -= 1
             self._m_active.value = float(self.active)
-            self._m_time.observe(time.perf_counter() - t0)
+        if tail is not None:
+            self._tails[tail] = (req, log, t0)
+            self.tails_started += 1
+            tail.add_done_callback(self._tail_done)
+            return False
+        self._finish(req, log, t0, result, err)
+        return True
+
+    def _tail_done(self, tail: "asyncio.Future[Result]") -> None:
+        """A deferred tail finished: handle its result and release its key."""
+        entry = self._tails.pop(tail, None)
+        if entry is None:
+            return
+        req, log, t0 = entry
+        try:
+            if tail.cancelled():  # shutdown / leader loss: the key is simply released
+                return
+            err = tail.exception()
+            result = None if err is not None else (tail.result() or Result())
+            try:
+                self._finish(req, log, t0, result, err)
+            except Exception as e:  # noqa: BLE001 - a done callback must not raise into the loop
+                log.error(e, "Failed to handle a deferred reconcile result")
+        finally:
+            self.queue.done(req)
+
+    def _finish(self, req: Request, log: Logger, t0: float, result: Optional[Result],
+                err: Optional[BaseException]) -> None:
+        """Result handling after a reconcile (and its tail) finished."""
+        q = self.queue
+        self._m_time.observe(time.perf_counter() - t0)
         self.reconciles += 1
         if err is not None:
             self.errors += 1
@@ -262,11 +321,11 @@ class Controller:
                 log.error(err, "Observed a panic", stacktrace="".join(traceback.format_exception(err))[-2000:])
             else:
                 log.error(err, "Reconciler error")
-        elif result.after_ns() > 0:
+        elif result.after_ns() > 0:  # type: ignore[union-attr]
             q.forget(req)
-            q.add_at(req, self.clock.now_ns() + result.after_ns(), PRIORITY_SCHEDULE)
+            q.add_at(req, self.clock.now_ns() + result.after_ns(), PRIORITY_SCHEDULE)  # type: ignore[union-attr]
             self._count("requeue_after")
-        elif result.requeue:
+        elif result.requeue:  # type: ignore[union-attr]
             q.add_rate_limited(req, PRIORITY_EVENT)
             self._count("requeue")
         else:
@@ -282,10 +341,12 @@ class Controller:
                 req = await q.get()
             except ShutDown:
                 return
+            release = True
             try:
-                await self.process_one(req)
+                release = await self.process_one(req)
             finally:
-                q.done(req)
+                if release:
+                    q.done(req)
 
     def start(self) -> None:
         if self.started:
@@ -306,7 +367,9 @@ class Controller:
     async def stop(self) -> None:
         self.queue.shutdown()
         workers, self._workers = self._workers, []
-        await aio.cancel_and_wait(*workers)
+        # deferred tails are cancelled with the workers (controller-runtime cancels the context
+        # of every in-flight reconcile); their done callbacks release the keys
+        await aio.cancel_and_wait(*workers, *list(self._tails))
         self.started = False
 
     async def wait_idle(self, settle: float = 0.0, timeout: float = 60.0) -> bool:

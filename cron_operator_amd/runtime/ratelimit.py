@@ -4,6 +4,18 @@
   that client-go puts in front of every API request; the reference configures
   it with ``--qps 30 --burst 50`` (``cmd/operator/start.go:152-154,218-219``).
   A negative qps disables throttling (client-go semantics).
+
+  Unlike client-go's bucket (one FIFO of sleepers), a request waiting for a token
+  carries a **priority**: when the bucket is backed up, tokens go to
+  :data:`PRIORITY_HIGH` waiters first (a tick's CREATE, the lease renewal), then
+  :data:`PRIORITY_NORMAL` (reads, informer LIST/WATCH), then :data:`PRIORITY_LOW`
+  (writes a reconcile can defer: status PATCHes, history-GC DELETEs, events) -- FIFO
+  within a class.  Under throttling a tick's jobs are then created at the full QPS
+  instead of sharing it with the bookkeeping writes around them, so schedule->create
+  latency is bounded by *creates* per QPS, not by all requests per QPS.  A low waiter
+  older than ``max_defer`` seconds is served before everything else, so deferrable
+  writes are delayed, never starved.  With no backlog a request takes a token at
+  once, whatever its priority, exactly as before.
 * :class:`ItemExponentialFailureRateLimiter`, :class:`BucketRateLimiter`,
   :class:`MaxOfRateLimiter` -- the workqueue's default controller limiter
   (per-item exponential backoff 5ms..1000s, max'd with an overall 10 qps /
@@ -17,11 +29,63 @@ from __future__ import annotations
 import asyncio
 import threading
 import time
-from typing import Dict, Hashable, List, Optional
+from collections import deque
+from typing import Deque, Dict, Hashable, List, Optional, Tuple
+
+PRIORITY_LOW = 0
+PRIORITY_NORMAL = 1
+PRIORITY_HIGH = 2
 
 
-class TokenBucket:
-    def __init__(self, qps: float, burst: int):
+class _PriorityWaiters:
+    """Three FIFO classes of waiting futures; :meth:`_next` serves the most urgent class, or a
+    low waiter older than ``max_defer`` seconds before anything else (delayed, never starved)."""
+
+    def __init__(self, max_defer: float):
+        self.max_defer = max_defer
+        # waiters per priority class (index = priority): (future, enqueue monotonic time)
+        self._waiters: Tuple[Deque[Tuple["asyncio.Future[None]", float]], ...] = (deque(), deque(), deque())
+        self._n_waiting = 0
+        self.granted_by_priority = [0, 0, 0]
+        self.aged_grants = 0  # low-priority grants promoted by max_defer
+
+    @property
+    def waiting(self) -> int:
+        """Requests queued right now."""
+        return self._n_waiting
+
+    def _enqueue(self, priority: int, now: float) -> "asyncio.Future[None]":
+        fut = asyncio.get_running_loop().create_future()
+        self._waiters[priority].append((fut, now))
+        self._n_waiting += 1
+        return fut
+
+    def _discard(self, priority: int, fut: "asyncio.Future[None]") -> None:
+        q = self._waiters[priority]
+        for i, (f, _) in enumerate(q):
+            if f is fut:
+                del q[i]
+                self._n_waiting -= 1
+                return
+
+    def _next(self) -> Optional[Tuple["asyncio.Future[None]", int]]:
+        """Pop the waiter to serve: an over-aged low waiter, else the most urgent class."""
+        low = self._waiters[PRIORITY_LOW]
+        if low and time.monotonic() - low[0][1] > self.max_defer:
+            self.aged_grants += 1
+            self._n_waiting -= 1
+            return low.popleft()[0], PRIORITY_LOW
+        for p in (PRIORITY_HIGH, PRIORITY_NORMAL, PRIORITY_LOW):
+            q = self._waiters[p]
+            if q:
+                self._n_waiting -= 1
+                return q.popleft()[0], p
+        return None
+
+
+class TokenBucket(_PriorityWaiters):
+    def __init__(self, qps: float, burst: int, max_defer: float = 20.0):
+        super().__init__(max_defer)
         self.qps = float(qps)
         self.burst = max(1, int(burst))
         self._tokens = float(self.burst)
@@ -29,6 +93,7 @@ class TokenBucket:
         self._lock = threading.Lock()
         self.total_wait = 0.0
         self.accepted = 0
+        self._timer: Optional[asyncio.TimerHandle] = None
 
     @property
     def unlimited(self) -> bool:
@@ -57,16 +122,68 @@ class TokenBucket:
                 return True
             return False
 
-    async def wait(self) -> float:
+    def _refill(self, now: float) -> None:
+        self._tokens = min(float(self.burst), self._tokens + (now - self._last) * self.qps)
+        self._last = now
+
+    async def wait(self, priority: int = PRIORITY_NORMAL) -> float:
+        """Take one token, waiting for it if the bucket is empty; returns the wait in seconds."""
         if self.unlimited:
             return 0.0
         if self.qps == 0:
             raise ValueError("qps 0 would block forever")
-        d = self._reserve()
-        if d > 0:
-            self.total_wait += d
-            await asyncio.sleep(d)
+        now = time.monotonic()
+        if not self._n_waiting:
+            with self._lock:
+                self._refill(now)
+                if self._tokens >= 1.0:
+                    self._tokens -= 1.0
+                    self.accepted += 1
+                    self.granted_by_priority[priority] += 1
+                    return 0.0
+        loop = asyncio.get_running_loop()
+        fut = self._enqueue(priority, now)
+        self._arm(loop)
+        try:
+            await fut
+        except asyncio.CancelledError:
+            if not fut.done() or fut.cancelled():
+                self._discard(priority, fut)
+            else:  # granted and cancelled in the same turn: hand the token back
+                with self._lock:
+                    self._tokens += 1.0
+                    self.accepted -= 1
+                self._arm(loop)
+            raise
+        d = time.monotonic() - now
+        self.total_wait += d
         return d
+
+    def _arm(self, loop: asyncio.AbstractEventLoop) -> None:
+        """Schedule the next grant for when a token is due (one timer for all waiters)."""
+        if self._timer is not None or not self._n_waiting:
+            return
+        with self._lock:
+            self._refill(time.monotonic())
+            delay = 0.0 if self._tokens >= 1.0 else (1.0 - self._tokens) / self.qps
+        self._timer = loop.call_later(delay, self._grant, loop)
+
+    def _grant(self, loop: asyncio.AbstractEventLoop) -> None:
+        self._timer = None
+        with self._lock:
+            self._refill(time.monotonic())
+            while self._tokens >= 1.0 and self._n_waiting:
+                nxt = self._next()
+                if nxt is None:
+                    break
+                fut, p = nxt
+                if fut.done():  # cancelled while queued
+                    continue
+                self._tokens -= 1.0
+                self.accepted += 1
+                self.granted_by_priority[p] += 1
+                fut.set_result(None)
+        self._arm(loop)
 
     def when(self) -> float:
         """Non-blocking reservation (seconds until the token is due)."""
@@ -75,13 +192,57 @@ class TokenBucket:
         return self._reserve()
 
 
-def make_client_limiter(qps: float, burst: int) -> Optional[TokenBucket]:
+class InflightGate(_PriorityWaiters):
+    """At most ``limit`` requests in flight; the rest wait in priority order (the client's
+    cap on concurrent API requests -- deferred reconcile tails can have many writes ready at
+    once, and an HTTP/1.1 pool would otherwise open one connection per request)."""
+
+    def __init__(self, limit: int, max_defer: float = 20.0):
+        super().__init__(max_defer)
+        self.limit = max(1, int(limit))
+        self.inflight = 0
+        self.peak = 0
+
+    async def acquire(self, priority: int = PRIORITY_NORMAL) -> None:
+        if self.inflight < self.limit and not self._n_waiting:
+            self.inflight += 1
+            self.granted_by_priority[priority] += 1
+            if self.inflight > self.peak:
+                self.peak = self.inflight
+            return
+        fut = self._enqueue(priority, time.monotonic())
+        try:
+            await fut
+        except asyncio.CancelledError:
+            if fut.done() and not fut.cancelled():
+                self.release()  # granted and cancelled in the same turn: pass the slot on
+            else:
+                self._discard(priority, fut)
+            raise
+
+    def release(self) -> None:
+        self.inflight -= 1
+        while self._n_waiting and self.inflight < self.limit:
+            nxt = self._next()
+            if nxt is None:
+                break
+            fut, p = nxt
+            if fut.done():  # cancelled while queued
+                continue
+            self.inflight += 1
+            self.granted_by_priority[p] += 1
+            if self.inflight > self.peak:
+                self.peak = self.inflight
+            fut.set_result(None)
+
+
+def make_client_limiter(qps: float, burst: int, max_defer: float = 20.0) -> Optional[TokenBucket]:
     """client-go: qps==0 -> default 5/10; qps<0 -> no limiter."""
     if qps == 0:
         qps, burst = 5.0, 10
     if qps < 0:
         return None
-    return TokenBucket(qps, burst)
+    return TokenBucket(qps, burst, max_defer)
 
 
 # --------------------------------------------------------------------------- workqueue limiters

@@ -21,6 +21,13 @@ latency too.  Each row here is one harness run:
     transports instead of the native connections (``_netconn``);
 ``tls+etcd``
     TLS and the ``etcd`` latency model together -- the closest shape to a cluster.
+``chart-defaults-1000``
+    BASELINE config 4 as the chart installs it: 1000 Crons, one process, TLS + ``etcd``
+    latency, the chart's shipped ``qps``/``burst`` (``charts/cron-operator/values.yaml``).
+    Done when every Cron fires every tick (the harness fails a step otherwise), each
+    tick's work (completion + fire phase) takes <= 45 s of wall time, and p50
+    tick->create <= 6 s.  The reference row runs the reference algorithm at the same
+    budget (10 requests per fire).
 
 ``optimized`` rows are this operator, ``reference`` rows the reference algorithm
 (``ReconcilerOptions.reference()``), both with 10 workers on one replica unless the
@@ -54,12 +61,24 @@ ROWS = [
     ("tls+etcd", "reference", 1, 1000, -1.0, 50, "etcd", 3, 1, True, True),
     ("tls+etcd", "optimized", 1, 1000, -1.0, 50, "etcd", 5, 2, True, True),
     ("tls+etcd", "optimized", 3, 1000, -1.0, 50, "etcd", 5, 2, True, True),
+    ("chart-defaults-1000", "optimized", 1, 1000, "chart", "chart", "etcd", 5, 1, True, True),
+    ("chart-defaults-1000", "reference", 1, 1000, "chart", "chart", "etcd", 1, 1, True, True),
 ]
+
+
+def chart_client_values():
+    """(qps, burst) the chart ships (``charts/cron-operator/values.yaml``)."""
+    import yaml
+
+    with open(os.path.join(ROOT, "charts", "cron-operator", "values.yaml")) as fh:
+        v = yaml.safe_load(fh)
+    return float(v["qps"]), int(v["burst"])
 
 
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="", help="comma-separated config names to run")
+    ap.add_argument("--mode", default="", help="only rows of this algorithm (optimized / reference)")
     ap.add_argument("--scale", type=float, default=1.0, help="multiply Cron counts (quick local runs)")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
@@ -71,7 +90,11 @@ def main() -> int:
     for name, mode, shards, n, qps, burst, lat, steps, warmup, tls, native in ROWS:
         if only and name not in only:
             continue
+        if a.mode and mode != a.mode:
+            continue
         n = max(1, int(n * a.scale))
+        if qps == "chart":
+            qps, burst = chart_client_values()
         t0 = time.perf_counter()
         r = run_sync(BenchConfig(n_crons=n, steps=steps, warmup=warmup, mode=mode, qps=qps, burst=burst,
                                  shards=shards, apiserver_latency=lat, tls=tls, native_http=native))
@@ -83,11 +106,15 @@ def main() -> int:
                "api_requests_per_fire": r.api_requests_per_fire, "reconciles_per_fire": r.reconciles_per_fire,
                "operator_cpu_ms_per_fire": r.cpu_s_operator * 1000 / fires,
                "apiserver_busy_frac": r.cpu_s_apiserver / r.elapsed_s,
+               "max_step_s": round(max(r.step_ms) / 1000, 2) if r.step_ms else None,
+               "step_s": [round(x / 1000, 2) for x in r.step_ms],
+               "phase_s": {k: [round(x / 1000, 2) for x in v] for k, v in r.phase_ms.items()},
                "wall_s": round(time.perf_counter() - t0, 1)}
         rows.append(row)
         print(f"{name:>14} {mode:>9} x{shards} n={n:>5}: {r.cron_reconciles_per_s:9.1f} cron-reconciles/s  "
               f"p50 {r.p50_latency_ms:8.1f} ms  {r.api_requests_per_fire:.1f} req/fire  "
-              f"operator {row['operator_cpu_ms_per_fire']:.3f} ms CPU/fire", flush=True)
+              f"operator {row['operator_cpu_ms_per_fire']:.3f} ms CPU/fire  max step {row['max_step_s']} s",
+              flush=True)
     print()
     print("| config | algorithm | replicas | Crons | cron-reconciles/s | p50 tick→create ms | p99 ms "
           "| API req/fire | reconciles/fire | operator CPU ms/fire | apiserver busy |")

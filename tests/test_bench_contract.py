@@ -49,6 +49,13 @@ def test_single_rank_line():
     assert d["single_process_value"] > 0 and d["single_process_p50_ms"] > 0
     assert d["single_process_p99_ms"] >= d["single_process_p50_ms"]
     assert d["single_process_operator_cpu_ms_per_fire"] > 0 and 0 < d["single_process_apiserver_busy_frac"] < 2
+    # the deployment-shaped pair (TLS + etcd latency, one process, both algorithms), same invocation
+    assert d["deployment_config"]["tls"] is True and d["deployment_config"]["apiserver_latency"] == "etcd"
+    assert d["deployment_value"] > 0 and d["deployment_baseline_value"] > 0
+    assert abs(d["vs_baseline_deployment"] - d["deployment_value"] / d["deployment_baseline_value"]) \
+        < 0.01 * d["vs_baseline_deployment"] + 0.002
+    assert d["deployment_baseline_api_requests_per_fire"] > d["deployment_api_requests_per_fire"]
+    assert d["deployment_p50_ms"] > 0 and d["deployment_baseline_p50_ms"] > 0
 
 
 def test_recorded_baseline_option():

@@ -99,11 +99,12 @@ async def test_controller_stop_does_not_wait_for_held_deletes():
     env.server.faults.latency["delete"] = HOLD_S
     await env.start_manager()
     await _spin_until(lambda: len(started) >= 3)
-    assert env.controller.active == 1  # the reconcile is parked on its GC DELETEs
+    # the reconcile's tail is parked on its GC DELETEs (the worker itself moved on)
+    assert env.controller.in_flight() == 1 and env.controller.queue.processing() == 1
     t0 = time.perf_counter()
     await asyncio.wait_for(env.controller.stop(), 1.0)
     assert time.perf_counter() - t0 < 1.0
-    assert env.controller.active == 0
+    assert env.controller.in_flight() == 0
     env.server.faults.clear()
     await env.stop()
 
@@ -124,7 +125,7 @@ async def test_leader_loss_ends_manager_within_renew_deadline_despite_held_delet
     await env.start_manager(leader_election=True, leader_election_namespace=NS, leader_election_identity="me",
                             lease_duration=15, renew_deadline=10, retry_period=2)
     await _spin_until(lambda: len(started) >= 3)
-    assert env.manager.elector.is_leader and env.controller.active == 1
+    assert env.manager.elector.is_leader and env.controller.in_flight() == 1
     # a forced loss: another holder overwrites the lease record
     lease = env.server.get(LEASES, NS, "619a52b8.kubedl.io")
     lease["spec"]["holderIdentity"] = "usurper"

@@ -1,0 +1,127 @@
+"""The shipped chart's client budget sustains the fleet it claims: no tick collapses.
+
+BASELINE config 4 is 1000 Crons on ``* * * * *`` with historyLimit=10.  The operator
+makes about 5 API requests per fire against a training-operator that marks jobs
+Running and then Succeeded (CREATE; status PATCH; PATCH when the job's resourceVersion
+in ``status.active`` changes; PATCH moving it to history; history-GC DELETE).  At the
+reference's ``--qps 30`` (``/root/reference/charts/cron-operator/values.yaml:62-68``,
+``/root/reference/cmd/operator/start.go:218-219``) that is ~167 s of requests per
+minute: ticks collapse, and the reconciler's catch-up (``cron_controller.go:408-436``)
+runs only the last missed tick -- scheduled runs are lost without an error.
+
+This test runs that ratio **time-compressed**: ``N`` Crons with the client budget scaled
+by ``N/1000`` (burst) and by ``N/1000 x C`` (QPS), and one virtual minute every ``60/C``
+seconds of real time -- a tick's requests take the same fraction of the minute as 1000
+Crons at the chart's values.  The virtual clock advances on its own, whether or not the
+operator has finished, so a collapse shows up as a missing job name.  The chart's values
+must create every Cron's job for every tick within 45 s (scaled) of the tick; the
+reference's 30/50 must not (the control that proves the test can fail).
+"""
+from __future__ import annotations
+
+import asyncio
+import os
+import statistics
+import time
+
+import yaml
+
+from cron_operator_amd.api.meta import GroupVersionResource
+from cron_operator_amd.api.v1alpha1 import LABEL_CRON_NAME, new_cron
+from cron_operator_amd.runtime.ratelimit import TokenBucket
+from cron_operator_amd.testing.env import TestEnv
+from cron_operator_amd.trainingop.operator import FakeTrainingOperator
+from cron_operator_amd.utils.gotime import NANOS
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NS = "default"
+PT = GroupVersionResource("kubeflow.org", "v1", "pytorchjobs")
+PT_TMPL = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+           "spec": {"pytorchReplicaSpecs": {"Master": {"replicas": 1}}}}
+
+FLEET = 1000       # the Crons the chart claims (BASELINE config 4)
+N = 60             # Crons in this run
+C = 20             # time compression: one virtual minute per 3 s of real time
+TICKS = 4
+STEP_S = 60 / C / 60  # real seconds per virtual second
+
+
+def chart_client_values():
+    with open(os.path.join(ROOT, "charts", "cron-operator", "values.yaml")) as fh:
+        v = yaml.safe_load(fh)
+    return float(v["qps"]), int(v["burst"])
+
+
+async def _run(qps: float, burst: int):
+    """-> (created {(cron, name)}, tick -> [create latency s], per-tick expected names)."""
+    env = TestEnv()
+    sq, sb = qps * N * C / FLEET, max(1, round(burst * N / FLEET))
+    env.client.limiter = TokenBucket(sq, sb, max_defer=20.0 / C)
+    trainer = FakeTrainingOperator(env.new_client(), env.clock, mode="timed", duration=30)
+    created = {}
+    orig = env.server.create
+
+    def create(gvr, ns, obj, *a, **kw):
+        out = orig(gvr, ns, obj, *a, **kw)
+        if gvr.resource == "pytorchjobs":
+            m = out["metadata"]
+            created[m["name"]] = (m["labels"][LABEL_CRON_NAME], time.perf_counter())
+        return out
+
+    env.server.create = create  # type: ignore[assignment]
+    setup = env.new_client()
+    for i in range(N):
+        c = new_cron(f"c{i:03d}", NS, "* * * * *", PT_TMPL, history_limit=2)
+        await setup.create(GroupVersionResource("apps.kubedl.io", "v1alpha1", "crons"), c.to_dict(), NS)
+    await trainer.start()
+    await env.start_manager()
+    await env.settle()
+    tick_wall = {}
+    start_min = env.clock.now_ns() // NANOS // 60 * 60
+    try:
+        # virtual time runs at C x real time for TICKS minutes, then up to just before the next tick
+        for _ in range(TICKS * 60 + 50):
+            env.clock.advance(1)
+            now_s = env.clock.now_ns() // NANOS
+            if now_s % 60 == 0:
+                tick_wall[now_s] = time.perf_counter()
+            await asyncio.sleep(STEP_S)
+    finally:
+        await trainer.stop()
+        await env.stop()
+    lat = {}
+    missing = []
+    for k in range(1, TICKS + 1):
+        tick = start_min + 60 * k
+        lat[k] = []
+        for i in range(N):
+            name = f"c{i:03d}-{tick + 60}"  # B18: named for Next(tick)
+            hit = created.get(name)
+            if hit is None:
+                missing.append(name)
+            else:
+                lat[k].append(hit[1] - tick_wall[tick])
+    return missing, lat
+
+
+async def test_chart_defaults_sustain_1000_minutely_crons_time_compressed():
+    qps, burst = chart_client_values()
+    missing, lat = await _run(qps, burst)
+    assert missing == [], f"ticks collapsed at qps={qps} burst={burst}: {missing[:10]}"
+    for k, xs in lat.items():
+        # real time x C = the full-scale wall time of the tick's work
+        assert max(xs) * C <= 45.0, (k, max(xs) * C)
+        assert statistics.median(xs) * C <= 6.0, (k, statistics.median(xs) * C)
+
+
+async def test_reference_client_budget_collapses_ticks_at_the_same_fleet():
+    """The control: the reference chart's 30/50 cannot carry 1000 minutely Crons."""
+    missing, _ = await _run(30.0, 50)
+    assert missing, "expected collapsed ticks at the reference's qps 30 / burst 50"
+
+
+def test_cli_flag_defaults_match_the_chart():
+    from cron_operator_amd.cmd.main import build_parser
+
+    a = build_parser().parse_args(["start"])
+    assert (a.qps, a.burst) == chart_client_values()

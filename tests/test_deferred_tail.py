@@ -1,0 +1,189 @@
+"""Deferred reconcile tails: a fire's writes do not hold a worker, and never break per-key
+serialisation.
+
+Reference: the reconcile's status patch is deferred to the end of ``Reconcile``
+(``/root/reference/internal/controller/cron_controller.go:107-120``) and runs on the
+worker after the CREATE (``:229-238``), so each fire holds a worker for two sequential
+write round trips.  Here the CREATE, the status PATCH and the GC DELETEs become the
+reconcile's tail (``ReconcilerOptions.defer_status_write``, ``runtime/controller.py``):
+the worker moves on, the key stays *processing* in the work queue until the tail lands.
+"""
+from __future__ import annotations
+
+import asyncio
+from collections import Counter
+
+import pytest
+
+from cron_operator_amd.api.meta import GroupVersionResource
+from cron_operator_amd.api.v1alpha1 import CRON_GVR, LABEL_CRON_NAME, new_cron
+from cron_operator_amd.controller.reconciler import CronReconciler, ReconcilerOptions
+from cron_operator_amd.cron.engine import NativeEngine
+from cron_operator_amd.runtime.controller import Request
+from cron_operator_amd.runtime.events import FakeRecorder
+from cron_operator_amd.testing.env import TestEnv
+from cron_operator_amd.utils.logging import get_logger
+
+NS = "default"
+PT = GroupVersionResource("kubeflow.org", "v1", "pytorchjobs")
+PT_TMPL = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+           "spec": {"pytorchReplicaSpecs": {"Master": {"replicas": 1}}}}
+
+
+def _jobs(env, cron):
+    return sorted(o["metadata"]["name"] for o in
+                  env.server.list(PT, NS, label_selector=f"{LABEL_CRON_NAME}={cron}")["items"])
+
+
+def _spy(env):
+    """Count reconcile starts per key and fail if one starts while the key's tail is in flight."""
+    ctrl = env.controller
+    starts: Counter = Counter()
+    overlaps = []
+    orig = ctrl.reconciler.reconcile
+
+    async def spy(req, log):
+        if any(r == req for r, _, _ in ctrl._tails.values()):
+            overlaps.append(req)
+        starts[req.name] += 1
+        return await orig(req, log)
+
+    ctrl.reconciler.reconcile = spy
+    return starts, overlaps
+
+
+async def _until(pred, timeout=5.0):
+    loop = asyncio.get_running_loop()
+    end = loop.time() + timeout
+    while not pred():
+        if loop.time() > end:
+            raise AssertionError("condition not reached")
+        await asyncio.sleep(0.002)
+
+
+async def test_one_worker_creates_every_tick_while_status_writes_are_held():
+    """One worker, 4 Crons, every status PATCH held 0.3 s by the apiserver: all four jobs are
+    created before the first PATCH lands -- the worker is never parked on a PATCH."""
+    env = TestEnv()
+    for i in range(4):
+        await env.create_cron(new_cron(f"c{i}", NS, "*/1 * * * *", PT_TMPL))
+    await env.start_manager(max_concurrent=1)
+    await env.settle()
+    env.server.faults.latency["patch"] = 0.3
+    try:
+        env.clock.advance(60)
+        await _until(lambda: sum(len(_jobs(env, f"c{i}")) for i in range(4)) == 4, 2.0)
+        # every PATCH is still held: each key is still processing, no worker is busy
+        assert env.controller.queue.processing() == 4
+        assert env.controller.active == 0 and env.controller.in_flight() == 4
+        for i in range(4):
+            assert not (env.server.get(CRON_GVR, NS, f"c{i}").get("status") or {}).get("lastScheduleTime")
+        env.server.faults.latency.clear()
+        await _until(lambda: env.controller.queue.idle(), 3.0)
+        for i in range(4):
+            assert env.server.get(CRON_GVR, NS, f"c{i}")["status"]["lastScheduleTime"]
+    finally:
+        env.server.faults.latency.clear()
+        await env.stop()
+
+
+async def test_requeue_during_held_patch_never_starts_a_second_reconcile():
+    """A held PATCH plus a storm of requeues of the same key: the key is parked until the tail
+    lands, then reconciled once more (not concurrently, and without a second job)."""
+    env = TestEnv()
+    await env.create_cron(new_cron("h", NS, "*/1 * * * *", PT_TMPL, concurrency_policy="Allow"))
+    await env.start_manager(max_concurrent=4)
+    await env.settle()
+    starts, overlaps = _spy(env)
+    env.server.faults.latency["patch"] = 0.2
+    try:
+        env.clock.advance(60)
+        await _until(lambda: len(_jobs(env, "h")) == 1, 2.0)
+        assert env.controller.in_flight() == 1
+        n0 = starts["h"]
+        for _ in range(50):
+            env.controller.queue.add(Request(NS, "h"))
+            await asyncio.sleep(0.001)
+        assert starts["h"] == n0  # parked behind the tail
+        env.server.faults.latency.clear()
+        await env.settle()
+        assert starts["h"] <= n0 + 1
+        assert overlaps == []
+        assert _jobs(env, "h") == ["h-1767268920"]
+    finally:
+        env.server.faults.latency.clear()
+        await env.stop()
+
+
+async def test_failed_deferred_patch_is_retried_and_the_tick_not_run_twice():
+    """The tail's status PATCH fails: the reconcile error is counted, the key is requeued with
+    backoff, and the retry records the tick (the job already exists) instead of running it again."""
+    env = TestEnv()
+    await env.create_cron(new_cron("f", NS, "*/1 * * * *", PT_TMPL, concurrency_policy="Replace"))
+    await env.start_manager()
+    await env.settle()
+    env.server.faults.add(verb="patch", resource="crons", subresource="status", code=500, times=1)
+    env.clock.advance(60)
+    await _until(lambda: env.controller.errors >= 1, 2.0)
+    await env.advance(1)  # the 5 ms backoff runs on the queue's (virtual) clock
+    assert _jobs(env, "f") == ["f-1767268920"]
+    assert env.server.get(CRON_GVR, NS, "f")["status"]["lastScheduleTime"]
+    assert env.controller.result_counts.get("error", 0) >= 1
+    await env.stop()
+
+
+@pytest.mark.parametrize("latency", [0.0, 0.005])
+async def test_no_duplicates_with_tails_under_write_latency_and_storms(latency):
+    """The SURVEY 5.2 stress, with every write held by the apiserver: one job per Cron per tick."""
+    env = TestEnv()
+    n = 24
+    for i in range(n):
+        await env.create_cron(new_cron(f"s{i}", NS, "*/1 * * * *", PT_TMPL))
+    await env.start_manager(max_concurrent=8)
+    await env.settle()
+    starts, overlaps = _spy(env)
+    for verb in ("create", "patch", "delete"):
+        env.server.faults.latency[verb] = latency
+    try:
+        for tick in range(1, 4):
+            env.clock.advance(60)
+            for _ in range(5):
+                for i in range(n):
+                    env.controller.queue.add(Request(NS, f"s{i}"))
+                await asyncio.sleep(0.002)
+            await _until(lambda: env.controller.queue.idle() and env.controller.in_flight() == 0, 10.0)
+            await env.settle()
+            for i in range(n):
+                assert len(_jobs(env, f"s{i}")) == tick, (f"s{i}", tick)
+        assert overlaps == []
+    finally:
+        env.server.faults.latency.clear()
+        await env.stop()
+
+
+async def test_direct_reconcile_calls_stay_synchronous():
+    """Called directly (envtest style, no controller), a reconcile finishes its writes before
+    returning -- no tail, as in the reference's tests (cron_controller_test.go:84-109)."""
+    env = TestEnv()
+    await env.create_cron(new_cron("d", NS, "*/1 * * * *", PT_TMPL))
+    env.clock.advance(60)
+    r = CronReconciler(env.client, None, FakeRecorder(), env.clock, NativeEngine(), ReconcilerOptions(list_mode="live"))
+    res = await r.reconcile(Request(NS, "d"), get_logger())
+    assert res.tail is None and res.requeue_after_ns > 0
+    assert len(_jobs(env, "d")) == 1
+    assert env.server.get(CRON_GVR, NS, "d")["status"]["lastScheduleTime"]
+
+
+async def test_stop_cancels_held_tails_and_releases_their_keys():
+    env = TestEnv()
+    for i in range(3):
+        await env.create_cron(new_cron(f"x{i}", NS, "*/1 * * * *", PT_TMPL))
+    await env.start_manager()
+    await env.settle()
+    env.server.faults.latency["create"] = 30.0
+    env.clock.advance(60)
+    await _until(lambda: env.controller.in_flight() == 3, 2.0)
+    await asyncio.wait_for(env.controller.stop(), 1.0)
+    assert env.controller.in_flight() == 0 and env.controller.queue.processing() == 0
+    env.server.faults.latency.clear()
+    await env.stop()

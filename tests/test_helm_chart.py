@@ -49,6 +49,10 @@ def test_replicas_and_pull_policy():
     ({"maxConcurrentReconciles": 20}, "--max-concurrent-reconciles=20"),
     ({"qps": 100}, "--qps=100"),
     ({"burst": 200}, "--burst=200"),
+    ({}, "--qps=150"),
+    ({}, "--burst=300"),
+    ({}, "--max-inflight-requests=64"),
+    ({"maxInflightRequests": 0}, "--max-inflight-requests=0"),
     ({"compatMode": "reference"}, "--compat-mode=reference"),
     ({"extraArgs": ["--namespace=team-a"]}, "--namespace=team-a"),
     ({"sharding": {"processes": 4, "routing": "labels"}}, "--shard-processes=4"),

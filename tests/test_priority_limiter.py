@@ -1,0 +1,162 @@
+"""Request priorities on the client's QPS bucket and in-flight cap.
+
+The reference throttles every request through one FIFO token bucket (client-go's
+``flowcontrol.NewTokenBucketRateLimiter``, configured at
+``/root/reference/cmd/operator/start.go:152-154,218-219``).  Here a backed-up bucket
+serves a tick's CREATEs before the writes a reconcile can defer (status PATCHes,
+history-GC DELETEs), FIFO within a class, and ages deferrable writes so they are
+delayed, never starved (``runtime/ratelimit.py``).
+"""
+from __future__ import annotations
+
+import asyncio
+
+from cron_operator_amd.api.meta import GroupVersionResource
+from cron_operator_amd.api.v1alpha1 import CRON_GVR, new_cron
+from cron_operator_amd.runtime.ratelimit import (PRIORITY_HIGH, PRIORITY_LOW, PRIORITY_NORMAL, InflightGate,
+                                                 TokenBucket)
+from cron_operator_amd.testing.env import TestEnv
+
+NS = "default"
+PT = GroupVersionResource("kubeflow.org", "v1", "pytorchjobs")
+PT_TMPL = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+           "spec": {"pytorchReplicaSpecs": {"Master": {"replicas": 1}}}}
+
+
+async def _drain_bucket(b: TokenBucket) -> None:
+    while b._tokens >= 1.0:
+        await b.wait(PRIORITY_NORMAL)
+
+
+async def test_backlogged_bucket_serves_high_before_normal_before_low():
+    b = TokenBucket(200.0, 1)
+    await _drain_bucket(b)
+    order = []
+
+    async def req(tag, prio):
+        await b.wait(prio)
+        order.append(tag)
+
+    tasks = [asyncio.ensure_future(req(f"low{i}", PRIORITY_LOW)) for i in range(3)]
+    tasks += [asyncio.ensure_future(req(f"norm{i}", PRIORITY_NORMAL)) for i in range(2)]
+    tasks += [asyncio.ensure_future(req(f"high{i}", PRIORITY_HIGH)) for i in range(3)]
+    await asyncio.wait_for(asyncio.gather(*tasks), 5)
+    assert order == ["high0", "high1", "high2", "norm0", "norm1", "low0", "low1", "low2"]
+    assert b.waiting == 0
+    assert b.granted_by_priority[PRIORITY_HIGH] == 3
+
+
+async def test_idle_bucket_grants_at_once_whatever_the_priority():
+    b = TokenBucket(1.0, 5)
+    for p in (PRIORITY_LOW, PRIORITY_NORMAL, PRIORITY_HIGH):
+        assert await b.wait(p) == 0.0
+    assert b.accepted == 3
+
+
+async def test_aged_low_waiter_is_served_before_new_high_ones():
+    b = TokenBucket(100.0, 1, max_defer=0.05)
+    await _drain_bucket(b)
+    order = []
+
+    async def req(tag, prio):
+        await b.wait(prio)
+        order.append(tag)
+
+    low = asyncio.ensure_future(req("low", PRIORITY_LOW))
+    highs = []
+    # a steady stream of HIGH requests that alone would keep the bucket busy
+    for i in range(20):
+        highs.append(asyncio.ensure_future(req(f"h{i}", PRIORITY_HIGH)))
+        await asyncio.sleep(0.01)
+    await asyncio.wait_for(asyncio.gather(low, *highs), 5)
+    assert "low" in order and order.index("low") < len(order) - 1, order
+    assert b.aged_grants >= 1
+
+
+async def test_cancelled_waiter_leaves_no_trace():
+    b = TokenBucket(20.0, 1)
+    await _drain_bucket(b)
+    t = asyncio.ensure_future(b.wait(PRIORITY_LOW))
+    await asyncio.sleep(0)
+    assert b.waiting == 1
+    t.cancel()
+    await asyncio.gather(t, return_exceptions=True)
+    assert b.waiting == 0
+    # the next waiter still gets its token within one refill period
+    assert await asyncio.wait_for(b.wait(PRIORITY_HIGH), 1.0) < 0.2
+
+
+async def test_inflight_gate_caps_and_orders_by_priority():
+    g = InflightGate(2)
+    await g.acquire(PRIORITY_NORMAL)
+    await g.acquire(PRIORITY_NORMAL)
+    order = []
+
+    async def req(tag, prio):
+        await g.acquire(prio)
+        order.append(tag)
+
+    ts = [asyncio.ensure_future(req("low", PRIORITY_LOW)), asyncio.ensure_future(req("high", PRIORITY_HIGH))]
+    await asyncio.sleep(0)
+    assert g.inflight == 2 and g.waiting == 2
+    g.release()
+    await asyncio.sleep(0)
+    assert order == ["high"]
+    g.release()
+    await asyncio.wait_for(asyncio.gather(*ts), 1)
+    assert order == ["high", "low"] and g.inflight == 2 and g.peak == 2
+
+
+async def test_inflight_gate_cancelled_grant_passes_the_slot_on():
+    g = InflightGate(1)
+    await g.acquire()
+    t1 = asyncio.ensure_future(g.acquire(PRIORITY_LOW))
+    t2 = asyncio.ensure_future(g.acquire(PRIORITY_LOW))
+    await asyncio.sleep(0)
+    g.release()  # grants t1 ...
+    t1.cancel()  # ... which is cancelled before it runs: the slot goes to t2
+    await asyncio.gather(t1, return_exceptions=True)
+    await asyncio.wait_for(t2, 1)
+    assert g.inflight == 1
+
+
+async def test_throttled_operator_creates_the_tick_before_its_status_writes():
+    """20 Crons fire at once on a 40-QPS client with no burst to spare: the server sees the
+    tick's CREATEs ahead of the status PATCHes that record them (the reference's single FIFO
+    interleaves them, so its last CREATE waits behind ~half the PATCHes)."""
+    env = TestEnv(qps=40, burst=1)
+    seen = []
+    orig = env.server.create
+    orig_patch = env.server.patch
+
+    def create(gvr, ns, obj, *a, **kw):
+        if gvr.resource == "pytorchjobs":
+            seen.append("C")
+        return orig(gvr, ns, obj, *a, **kw)
+
+    def patch(gvr, ns, name, body, ptype="merge", sub="", *a, **kw):
+        if gvr.resource == "crons" and sub == "status":
+            seen.append("P")
+        return orig_patch(gvr, ns, name, body, ptype, sub, *a, **kw)
+
+    env.server.create = create  # type: ignore[assignment]
+    env.server.patch = patch  # type: ignore[assignment]
+    setup = env.new_client()
+    for i in range(20):
+        await setup.create(CRON_GVR, new_cron(f"c{i:02d}", NS, "*/1 * * * *", PT_TMPL).to_dict(), NS)
+    try:
+        await env.start_manager()
+        await env.settle()
+        seen.clear()
+        env.clock.advance(60)
+        for _ in range(400):
+            await asyncio.sleep(0.01)
+            if seen.count("C") == 20 and seen.count("P") >= 20:
+                break
+        assert seen.count("C") == 20, seen
+        last_create = max(i for i, x in enumerate(seen) if x == "C")
+        patches_before = seen[:last_create].count("P")
+        assert patches_before <= 2, "".join(seen)
+        assert env.client.limiter.granted_by_priority[PRIORITY_HIGH] >= 20
+    finally:
+        await env.stop()
