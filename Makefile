@@ -7,6 +7,8 @@ IMG_REGISTRY ?= docker.io
 IMG_REPOSITORY ?= cron-operator-amd/cron-operator
 IMG_TAG ?= $(patsubst v%,%,$(VERSION))
 IMG ?= $(IMG_REGISTRY)/$(IMG_REPOSITORY):$(IMG_TAG)
+# the MI355X payload image the examples/mi355x Crons run (Dockerfile.payload)
+PAYLOAD_IMG ?= $(IMG_REGISTRY)/cron-operator-amd/cron-operator-mi355x-payload:$(IMG_TAG)
 CONTAINER_TOOL ?= docker
 PYTHON ?= python3
 PYTEST_ARGS ?= -q
@@ -107,6 +109,14 @@ docker-build: ## Build the operator image.
 .PHONY: docker-push
 docker-push: ## Push the operator image.
 	$(CONTAINER_TOOL) push $(IMG)
+
+.PHONY: docker-build-payload
+docker-build-payload: ## Build the MI355X payload image the examples/mi355x Crons run.
+	$(CONTAINER_TOOL) build -f Dockerfile.payload -t $(PAYLOAD_IMG) .
+
+.PHONY: docker-push-payload
+docker-push-payload: ## Push the MI355X payload image.
+	$(CONTAINER_TOOL) push $(PAYLOAD_IMG)
 
 PLATFORMS ?= linux/amd64,linux/arm64
 .PHONY: docker-buildx

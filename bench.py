@@ -127,6 +127,13 @@ def _dist():
     return dist, dist.get_rank(), dist.get_world_size()
 
 
+def _progress(rank: int, msg: str) -> None:
+    """One progress line on stderr (stdout carries only the JSON line): a long invocation
+    is never silent for minutes."""
+    if rank == 0:
+        print(f"bench.py: {msg}", file=sys.stderr, flush=True)
+
+
 def _barrier(dist) -> None:
     if dist is not None:
         dist.barrier()
@@ -151,6 +158,10 @@ def main() -> int:
     ap.add_argument("--workers", type=int, default=10, help="--max-concurrent-reconciles")
     ap.add_argument("--qps", type=float, default=-1.0, help="client QPS (-1: unthrottled)")
     ap.add_argument("--burst", type=int, default=50)
+    ap.add_argument("--max-inflight", type=int, default=64,
+                    help="client cap on concurrent API requests (--max-inflight-requests; 0: unlimited)")
+    ap.add_argument("--no-defer", action="store_true",
+                    help="A/B: reconcile writes on the worker (ReconcilerOptions.defer_status_write=False)")
     ap.add_argument("--transport", choices=["http", "memory"], default="http")
     ap.add_argument("--mode", choices=["optimized", "reference"], default="optimized")
     ap.add_argument("--shards", type=int, default=0,
@@ -206,7 +217,8 @@ def main() -> int:
     cfg = BenchConfig(n_crons=a.crons, steps=a.steps, warmup=a.warmup, history_limit=a.history_limit,
                       mode=a.mode, transport=a.transport, qps=a.qps, burst=a.burst, workers=a.workers,
                       namespace=f"bench-r{rank}", shards=a.shards if a.transport == "http" else 1,
-                      shard_routing=a.shard_routing, apiserver_latency=a.apiserver_latency, tls=a.tls)
+                      shard_routing=a.shard_routing, apiserver_latency=a.apiserver_latency, tls=a.tls,
+                      max_inflight=a.max_inflight, defer_writes=not a.no_defer)
 
     def on_step(k: int, dt: float, timed: bool) -> None:
         # bracket the K timed steps with barriers so every rank times the same window: the
@@ -222,6 +234,8 @@ def main() -> int:
     _sync_device()
     _barrier(dist)
     wall = time.perf_counter() - t0
+    _progress(rank, f"headline done: {cfg.n_crons * cfg.steps / res.elapsed_s:.1f} cron-reconciles/s "
+                    f"(rank 0), {wall:.1f} s")
 
     mine = {"elapsed_s": res.elapsed_s, "fires": cfg.n_crons * cfg.steps,
             "reconciles": res.raw_reconciles_per_s * res.elapsed_s, "p50": res.p50_latency_ms,
@@ -236,10 +250,12 @@ def main() -> int:
             scfg = BenchConfig(n_crons=a.crons, steps=a.single_steps, warmup=a.single_warmup,
                                history_limit=a.history_limit, mode=a.mode, transport=a.transport, qps=a.qps,
                                burst=a.burst, workers=a.workers, namespace=f"bench-1p-r{rank}", shards=1,
-                               apiserver_latency=a.apiserver_latency, tls=a.tls)
+                               apiserver_latency=a.apiserver_latency, tls=a.tls, max_inflight=a.max_inflight,
+                               defer_writes=not a.no_defer)
             _barrier(dist)
             sres = run_sync(scfg)
             _barrier(dist)
+            _progress(rank, f"single process done: {scfg.n_crons * scfg.steps / sres.elapsed_s:.1f}")
         mine["sp_elapsed_s"] = sres.elapsed_s
         mine["sp_fires"] = scfg.n_crons * scfg.steps
         mine["sp_p50"] = sres.p50_latency_ms
@@ -257,6 +273,7 @@ def main() -> int:
         _barrier(dist)
         bres = run_sync(bcfg)
         _barrier(dist)
+        _progress(rank, f"reference algorithm done: {bcfg.n_crons * bcfg.steps / bres.elapsed_s:.1f}")
         mine["ref_elapsed_s"] = bres.elapsed_s
         mine["ref_fires"] = bcfg.n_crons * bcfg.steps
         mine["ref_p50"] = bres.p50_latency_ms
@@ -268,11 +285,13 @@ def main() -> int:
                                  ("dep_ref", "reference", a.deployment_baseline_steps)):
             dcfg = BenchConfig(n_crons=a.crons, steps=steps, warmup=1, history_limit=a.history_limit, mode=mode,
                                transport="http", qps=a.qps, burst=a.burst, workers=a.workers,
+                               max_inflight=a.max_inflight, defer_writes=not a.no_defer,
                                namespace=f"bench-{tag.replace('_', '-')}-r{rank}", shards=1,
                                apiserver_latency="etcd", tls=True)
             _barrier(dist)
             dres = run_sync(dcfg)
             _barrier(dist)
+            _progress(rank, f"deployment-shaped {mode} done: {dcfg.n_crons * dcfg.steps / dres.elapsed_s:.1f}")
             mine[f"{tag}_elapsed_s"] = dres.elapsed_s
             mine[f"{tag}_fires"] = dcfg.n_crons * dcfg.steps
             mine[f"{tag}_p50"] = dres.p50_latency_ms

@@ -91,6 +91,7 @@ class BenchConfig:
     qps: float = -1.0                # client QPS (-1 = unthrottled)
     burst: int = 50
     max_inflight: int = 64           # client cap on concurrent requests (cmd/main.py DEFAULT_MAX_INFLIGHT)
+    defer_writes: bool = True        # optimized mode: ReconcilerOptions.defer_status_write (A/B switch)
     workers: int = 10
     namespace: str = "bench"
     log_level: str = "error"
@@ -425,7 +426,8 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
             return await _run_sharded(cfg, remote, admin, set_time, complete_jobs, on_step)
 
         client = Client(transport, qps=cfg.qps, burst=cfg.burst, max_inflight=cfg.max_inflight)
-        opts = ReconcilerOptions.reference() if cfg.mode == "reference" else ReconcilerOptions()
+        opts = ReconcilerOptions.reference() if cfg.mode == "reference" else \
+            ReconcilerOptions(defer_status_write=cfg.defer_writes)
         mgr = Manager(client, ManagerOptions(clock=clock, max_concurrent_reconciles=cfg.workers,
                                              health_probe_bind_address="0", metrics_bind_address="0",
                                              namespace=cfg.namespace))
@@ -589,7 +591,7 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
                 "--namespace", cfg.namespace, "--shard-index", str(i), "--shard-count", str(cfg.shards),
                 "--start-ns", str(T0_NS + NANOS // 2), "--workers", str(cfg.workers),
                 "--history-limit", str(cfg.history_limit), "--qps", str(cfg.qps), "--burst", str(cfg.burst),
-                "--max-inflight", str(cfg.max_inflight),
+                "--max-inflight", str(cfg.max_inflight), *([] if cfg.defer_writes else ["--no-defer"]),
                 "--mode", cfg.mode, "--routing", cfg.shard_routing,
                 *(["--ca-file", remote.ca_file] if remote.ca_file else []),
                 env=env, stdin=asyncio.subprocess.PIPE, stdout=asyncio.subprocess.PIPE,

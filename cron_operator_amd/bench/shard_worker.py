@@ -41,6 +41,7 @@ async def main() -> int:
     ap.add_argument("--qps", type=float, default=-1.0)
     ap.add_argument("--burst", type=int, default=50)
     ap.add_argument("--max-inflight", type=int, default=64)
+    ap.add_argument("--no-defer", action="store_true", help="ReconcilerOptions.defer_status_write=False (A/B)")
     ap.add_argument("--mode", default="optimized")
     ap.add_argument("--routing", default="hash", choices=["hash", "labels"])
     ap.add_argument("--ca-file", default="", help="https --url: verify the apiserver against this CA (as localhost)")
@@ -65,7 +66,8 @@ async def main() -> int:
             rc = RestConfig(host=a.url, ca_data=fh.read(), tls_server_name="localhost")
     client = Client(HttpTransport(rc, pool_size=max(16, a.workers * 2, a.max_inflight)), qps=a.qps, burst=a.burst,
                     max_inflight=a.max_inflight)
-    opts = ReconcilerOptions.reference() if a.mode == "reference" else ReconcilerOptions()
+    opts = ReconcilerOptions.reference() if a.mode == "reference" else \
+        ReconcilerOptions(defer_status_write=not a.no_defer)
     mgr = Manager(client, ManagerOptions(clock=clock, max_concurrent_reconciles=a.workers,
                                          health_probe_bind_address="0", metrics_bind_address="0",
                                          namespace=a.namespace, shard_index=a.shard_index,

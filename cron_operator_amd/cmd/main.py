@@ -280,7 +280,10 @@ async def run_start(a: argparse.Namespace) -> int:
             loop.add_signal_handler(sig, on_signal)
         except (NotImplementedError, RuntimeError):
             pass
-    log.info("starting manager")
+    from ..ops import aioloop_native, netconn_native
+
+    log.info("starting manager", **{"event loop": aioloop_native.status(),
+                                    "http connections": netconn_native.status()})
     try:
         await mgr.start()
     except LeaderElectionLost:

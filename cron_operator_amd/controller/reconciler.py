@@ -40,7 +40,8 @@ option                     default here                           reference
                            yield to them
 =========================  =====================================  =======================================
 
-``defer_status_write`` (with a controller that accepts tails, ``runtime/controller.py``):
+``defer_status_write`` (with a controller that accepts tails, ``runtime/controller.py``, and
+while the client's in-flight cap is not the bottleneck -- ``Client.gate_saturated``):
 a fire reconcile otherwise holds its worker for two sequential write round trips --
 the CREATE, then the status PATCH that records ``lastScheduleTime``.  The PATCH (and
 any history-GC DELETE still in flight) becomes the reconcile's *tail*: the worker takes
@@ -462,7 +463,7 @@ class CronReconciler(Reconciler):
             result = Result()
             err: Optional[BaseException] = None
             gc: Optional[List["asyncio.Future[None]"]] = [] if self.opts.overlap_gc_deletes else None
-            deferring = self.defer_tails and self.opts.defer_status_write
+            deferring = self.defer_tails and self.opts.defer_status_write and not self.client.gate_saturated()
             fire: Optional[List[Callable[[], Awaitable[Result]]]] = [] if deferring else None
             try:
                 try:
@@ -472,10 +473,10 @@ class CronReconciler(Reconciler):
                 if deferring and err is None and (fire or gc or not old_status.semantic_equal(cron.status)):
                     # the writes as a deferred tail: the controller frees this worker and keeps
                     # the key processing until the CREATE, the status PATCH and the GC DELETEs land
-                    tail = asyncio.ensure_future(self._tail(old_obj, old_status, cron, log, key, gc,
-                                                            fire[0] if fire else None, result))
+                    tail = asyncio.get_running_loop().create_task(
+                        self._tail(old_obj, old_status, cron, log, key, gc, fire[0] if fire else None, result))
                     gc = None  # owned by the tail now
-                    return dataclasses.replace(result, tail=tail)
+                    return Result(result.requeue, result.requeue_after, result.requeue_after_ns, tail)
                 # B2: deferred status patch when status changed semantically (cron_controller.go:107-120)
                 if not old_status.semantic_equal(cron.status):
                     try:

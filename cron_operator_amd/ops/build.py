@@ -38,10 +38,11 @@ HEADERS: Dict[str, List[str]] = {
     "_httpcodec": ["httpframe.h"],
     "_netconn": ["httpframe.h"],
 }
-# extra linker inputs: _netconn speaks TLS through the system OpenSSL (the libssl CPython's own
-# ssl module is linked against, so SSL_CTX objects built by ssl.SSLContext are shared)
+# extra linker inputs: _netconn speaks TLS through the system OpenSSL and builds its own SSL_CTX
+# (TlsContext); an ssl.SSLContext is used only when CPython's _ssl resolves to the same libssl
+# (checked at configure() with dlopen/dlsym)
 LIBS: Dict[str, List[str]] = {
-    "_netconn": ["-lssl", "-lcrypto"],
+    "_netconn": ["-lssl", "-lcrypto", "-ldl"],
 }
 
 

@@ -13,9 +13,13 @@
 //     registered with the loop once (`loop.add_reader(fd, conn._on_readable)`); a readiness
 //     callback receives, frames and completes the in-flight response in C++;
 //   * TLS is OpenSSL on the socket itself (non-blocking `SSL_connect`/`SSL_read`/`SSL_write`),
-//     configured by the caller's `ssl.SSLContext` -- the `SSL_CTX` Python built from the
-//     kubeconfig (CA, client certificate, verify mode, ALPN) is used as is, and hostname
-//     checks and SNI follow what `SSLContext.wrap_socket(server_hostname=...)` does;
+//     configured by a `TlsContext`: an `SSL_CTX` this extension builds from the kubeconfig's
+//     PEM material (CA, client certificate and key, verify mode, ALPN) with the libssl it is
+//     linked against.  Hostname checks and SNI follow what
+//     `SSLContext.wrap_socket(server_hostname=...)` does.  A plain `ssl.SSLContext` is accepted
+//     only when CPython's `_ssl` module is provably linked to that same libssl (configure()
+//     checks the version and that `_ssl`'s `SSL_CTX_new` is ours); otherwise the caller keeps
+//     asyncio's TLS transports -- its `SSL_CTX` is never touched;
 //   * request mode: `send(data) -> Future[(status, body, retry_after)]`, Content-Length,
 //     chunked and read-until-close bodies, interim 1xx responses skipped, keep-alive;
 //   * stream mode (`open_stream(data, decode) -> Future[status]`): the body of a watch is
@@ -36,8 +40,11 @@
 #include <structmember.h>
 
 #include <arpa/inet.h>
+#include <dlfcn.h>
 #include <errno.h>
+#include <openssl/crypto.h>
 #include <openssl/err.h>
+#include <openssl/pem.h>
 #include <openssl/ssl.h>
 #include <openssl/x509v3.h>
 #include <sys/socket.h>
@@ -98,7 +105,7 @@ struct ConnObject {
   PyObject_HEAD
   Core* core;
   PyObject* loop;
-  PyObject* ssl_ctx;   // the Python ssl.SSLContext (keeps its SSL_CTX alive)
+  PyObject* ssl_ctx;   // the TlsContext / ssl.SSLContext (keeps its SSL_CTX alive)
   SSL* ssl;
   int fd;
   int mode;
@@ -138,6 +145,8 @@ struct PoolObject {
 };
 
 PyObject* g_timeout_error = nullptr;  // asyncio.TimeoutError, for the deadline sweep
+// configure(): CPython's _ssl module runs on this extension's libssl (same build, same symbols)
+bool g_shared_openssl = false;
 
 // The exchange on `s` ended (response completed or connection lost): leave the pool's busy
 // list, and go back to the idle list when reusable (closed otherwise).  May drop the last
@@ -767,10 +776,169 @@ void read_ready(ConnObject* s) {
 
 // ----------------------------------------------------------------------------- the type
 
+// ----------------------------------------------------------------------------- TlsContext
+
+// An SSL_CTX built here from PEM bytes, so the TLS state and the code driving it come from
+// one libssl whatever OpenSSL the interpreter's own ssl module uses.
+struct TlsCtxObject {
+  PyObject_HEAD
+  SSL_CTX* ctx;
+};
+
+PyTypeObject TlsCtxType = {
+    PyVarObject_HEAD_INIT(nullptr, 0)
+    "_netconn.TlsContext",                 /* tp_name */
+    sizeof(TlsCtxObject),                  /* tp_basicsize */
+};
+
+std::string openssl_errors() {
+  std::string msg;
+  char buf[256];
+  unsigned long e;
+  while ((e = ERR_get_error()) != 0) {
+    ERR_error_string_n(e, buf, sizeof buf);
+    if (!msg.empty()) msg += "; ";
+    msg += buf;
+  }
+  return msg;
+}
+
+int tls_fail(const std::string& what) {
+  const std::string msg = what + (ERR_peek_error() ? ": " + openssl_errors() : std::string());
+  if (g_ssl_error) {
+    PyObject* exc = ssl_error(msg);
+    if (exc) {
+      PyErr_SetObject(reinterpret_cast<PyObject*>(Py_TYPE(exc)), exc);
+      Py_DECREF(exc);
+    }
+  } else {
+    PyErr_SetString(PyExc_ValueError, msg.c_str());
+  }
+  return -1;
+}
+
+// Every certificate of a PEM bundle into the context's trust store; -1 on none or a bad one.
+int add_ca_pem(SSL_CTX* ctx, const char* data, Py_ssize_t len) {
+  BIO* bio = BIO_new_mem_buf(data, static_cast<int>(len));
+  if (!bio) return tls_fail("BIO_new_mem_buf failed");
+  X509_STORE* store = SSL_CTX_get_cert_store(ctx);
+  int n = 0;
+  for (;;) {
+    X509* x = PEM_read_bio_X509(bio, nullptr, nullptr, nullptr);
+    if (!x) break;
+    const int ok = X509_STORE_add_cert(store, x);
+    X509_free(x);
+    if (ok != 1) {
+      BIO_free(bio);
+      return tls_fail("cannot add a CA certificate");
+    }
+    ++n;
+  }
+  BIO_free(bio);
+  if (n == 0) return tls_fail("no CA certificate in the certificate-authority data");
+  ERR_clear_error();  // the PEM end-of-data "error" after the last certificate
+  return 0;
+}
+
+// The client certificate (first PEM block), its chain (the rest) and the private key.
+int use_client_pem(SSL_CTX* ctx, const char* cert, Py_ssize_t cert_len, const char* key, Py_ssize_t key_len) {
+  BIO* bio = BIO_new_mem_buf(cert, static_cast<int>(cert_len));
+  if (!bio) return tls_fail("BIO_new_mem_buf failed");
+  X509* leaf = PEM_read_bio_X509(bio, nullptr, nullptr, nullptr);
+  if (!leaf || SSL_CTX_use_certificate(ctx, leaf) != 1) {
+    if (leaf) X509_free(leaf);
+    BIO_free(bio);
+    return tls_fail("cannot load the client certificate");
+  }
+  X509_free(leaf);
+  for (;;) {
+    X509* x = PEM_read_bio_X509(bio, nullptr, nullptr, nullptr);
+    if (!x) break;
+    if (SSL_CTX_add_extra_chain_cert(ctx, x) != 1) {  // takes ownership on success
+      X509_free(x);
+      BIO_free(bio);
+      return tls_fail("cannot add a client chain certificate");
+    }
+  }
+  BIO_free(bio);
+  ERR_clear_error();
+  // the key: its own data, or a PEM bundle holding certificate and key together
+  bio = key_len > 0 ? BIO_new_mem_buf(key, static_cast<int>(key_len))
+                    : BIO_new_mem_buf(cert, static_cast<int>(cert_len));
+  if (!bio) return tls_fail("BIO_new_mem_buf failed");
+  EVP_PKEY* pk = PEM_read_bio_PrivateKey(bio, nullptr, nullptr, nullptr);
+  BIO_free(bio);
+  if (!pk || SSL_CTX_use_PrivateKey(ctx, pk) != 1) {
+    if (pk) EVP_PKEY_free(pk);
+    return tls_fail("cannot load the client key");
+  }
+  EVP_PKEY_free(pk);
+  if (SSL_CTX_check_private_key(ctx) != 1) return tls_fail("the client key does not match its certificate");
+  return 0;
+}
+
+// TlsContext(cadata=None, cafile=None, certdata=None, keydata=None, verify=True)
+int tls_init(TlsCtxObject* self, PyObject* args, PyObject* kw) {
+  static const char* kwlist[] = {"cadata", "cafile", "certdata", "keydata", "verify", nullptr};
+  const char *ca = nullptr, *cafile = nullptr, *cert = nullptr, *key = nullptr;
+  Py_ssize_t ca_len = 0, cert_len = 0, key_len = 0;
+  int verify = 1;
+  if (!PyArg_ParseTupleAndKeywords(args, kw, "|z#zz#z#p", const_cast<char**>(kwlist), &ca, &ca_len, &cafile,
+                                   &cert, &cert_len, &key, &key_len, &verify))
+    return -1;
+  if (self->ctx) {
+    PyErr_SetString(PyExc_RuntimeError, "TlsContext is already initialised");
+    return -1;
+  }
+  SSL_CTX* ctx = SSL_CTX_new(TLS_client_method());
+  if (!ctx) return tls_fail("SSL_CTX_new failed");
+  self->ctx = ctx;  // freed by dealloc on any failure below
+  SSL_CTX_set_min_proto_version(ctx, TLS1_2_VERSION);
+  SSL_CTX_set_options(ctx, SSL_OP_NO_COMPRESSION);
+  SSL_CTX_set_mode(ctx, SSL_MODE_RELEASE_BUFFERS);
+  if (verify) {
+    SSL_CTX_set_verify(ctx, SSL_VERIFY_PEER, nullptr);
+    if (ca && ca_len > 0) {
+      if (add_ca_pem(ctx, ca, ca_len) < 0) return -1;
+    } else if (cafile && *cafile) {
+      if (SSL_CTX_load_verify_locations(ctx, cafile, nullptr) != 1) return tls_fail("cannot load the CA file");
+    } else if (SSL_CTX_set_default_verify_paths(ctx) != 1) {
+      return tls_fail("cannot load the system CA certificates");
+    }
+  } else {
+    SSL_CTX_set_verify(ctx, SSL_VERIFY_NONE, nullptr);
+  }
+  if (cert && cert_len > 0 && use_client_pem(ctx, cert, cert_len, key, key_len) < 0) return -1;
+  static const unsigned char kAlpn[] = {8, 'h', 't', 't', 'p', '/', '1', '.', '1'};
+  if (SSL_CTX_set_alpn_protos(ctx, kAlpn, sizeof kAlpn) != 0) return tls_fail("cannot set ALPN");
+  return 0;
+}
+
+void tls_dealloc(TlsCtxObject* self) {
+  if (self->ctx) SSL_CTX_free(self->ctx);
+  Py_TYPE(self)->tp_free(reinterpret_cast<PyObject*>(self));
+}
+
+PyObject* tls_verify(TlsCtxObject* self, void*) {
+  if (!self->ctx) Py_RETURN_NONE;
+  return PyBool_FromLong((SSL_CTX_get_verify_mode(self->ctx) & SSL_VERIFY_PEER) != 0);
+}
+
+PyGetSetDef kTlsGetSet[] = {
+    {"verify", reinterpret_cast<getter>(tls_verify), nullptr, "peer certificates are verified", nullptr},
+    {nullptr, nullptr, nullptr, nullptr, nullptr},
+};
+
 SSL_CTX* ssl_ctx_of(PyObject* ctx) {
-  // ssl.SSLContext subclasses _ssl._SSLContext, whose C struct starts with the SSL_CTX pointer
-  // right after the object header; the match with the Python-visible options and verify mode
-  // guards the layout assumption.
+  // A TlsContext built here, or -- only when configure() proved CPython's _ssl shares this
+  // extension's libssl -- the SSL_CTX of an ssl.SSLContext: _ssl._SSLContext's C struct starts
+  // with the SSL_CTX pointer right after the object header, and the match with the
+  // Python-visible options and verify mode guards that layout assumption.
+  if (PyObject_TypeCheck(ctx, &TlsCtxType)) {
+    SSL_CTX* sc = reinterpret_cast<TlsCtxObject*>(ctx)->ctx;
+    if (!sc) PyErr_SetString(PyExc_ValueError, "TlsContext is not initialised");
+    return sc;
+  }
   bool is_ctx = false;
   for (PyTypeObject* t = Py_TYPE(ctx); t; t = t->tp_base)
     if (std::strcmp(t->tp_name, "_ssl._SSLContext") == 0) {
@@ -778,7 +946,11 @@ SSL_CTX* ssl_ctx_of(PyObject* ctx) {
       break;
     }
   if (!is_ctx) {
-    PyErr_SetString(PyExc_TypeError, "ssl_context must be an ssl.SSLContext");
+    PyErr_SetString(PyExc_TypeError, "ssl_context must be a TlsContext or an ssl.SSLContext");
+    return nullptr;
+  }
+  if (!g_shared_openssl) {
+    PyErr_SetString(PyExc_TypeError, "CPython's ssl module uses another OpenSSL than _netconn");
     return nullptr;
   }
   SSL_CTX* sc = *reinterpret_cast<SSL_CTX**>(reinterpret_cast<char*>(ctx) + sizeof(PyObject));
@@ -1601,9 +1773,26 @@ PyTypeObject PoolType = {
 };
 
 // configure(ConnectionFailed, HttpStatusError, SSLError)
+// Does CPython's _ssl extension (its file: `ssl_path`) resolve SSL_CTX_new to the very function
+// this extension calls, and report the same OpenSSL build number?  Only then may an
+// ssl.SSLContext's SSL_CTX be driven from here.
+bool same_openssl(const char* ssl_path, unsigned long long py_version) {
+  if (!ssl_path || !*ssl_path) return false;
+  if (py_version != static_cast<unsigned long long>(OpenSSL_version_num())) return false;
+  void* h = dlopen(ssl_path, RTLD_NOW | RTLD_NOLOAD);
+  if (!h) return false;
+  void* theirs = dlsym(h, "SSL_CTX_new");
+  dlclose(h);
+  return theirs != nullptr && theirs == reinterpret_cast<void*>(&SSL_CTX_new);
+}
+
+// configure(ConnectionFailed, HttpStatusError, SSLError[, TimeoutError[, ssl_module_path,
+//           ssl_openssl_version_number]])
 PyObject* configure(PyObject*, PyObject* args) {
   PyObject *cf, *se, *sslerr, *te = nullptr;
-  if (!PyArg_ParseTuple(args, "OOO|O", &cf, &se, &sslerr, &te)) return nullptr;
+  const char* ssl_path = nullptr;
+  unsigned long long py_version = 0;
+  if (!PyArg_ParseTuple(args, "OOO|OzK", &cf, &se, &sslerr, &te, &ssl_path, &py_version)) return nullptr;
   Py_INCREF(cf);
   Py_INCREF(se);
   Py_INCREF(sslerr);
@@ -1612,21 +1801,31 @@ PyObject* configure(PyObject*, PyObject* args) {
   Py_XSETREF(g_status_error, se);
   Py_XSETREF(g_ssl_error, sslerr);
   Py_XSETREF(g_timeout_error, te);
+  g_shared_openssl = same_openssl(ssl_path, py_version);
   Py_RETURN_NONE;
 }
 
-// ssl_context_supported(ctx) -> bool: can Conn use this ssl.SSLContext natively?
+// ssl_context_supported(ctx) -> bool: can Conn use this TlsContext / ssl.SSLContext natively?
 PyObject* ssl_context_supported(PyObject*, PyObject* ctx) {
   if (ssl_ctx_of(ctx)) Py_RETURN_TRUE;
   PyErr_Clear();
   Py_RETURN_FALSE;
 }
 
+// openssl() -> (OpenSSL_version_num(), OpenSSL_version(OPENSSL_VERSION), shares CPython's _ssl)
+PyObject* openssl_info(PyObject*, PyObject*) {
+  return Py_BuildValue("(KsO)", static_cast<unsigned long long>(OpenSSL_version_num()),
+                       OpenSSL_version(OPENSSL_VERSION), g_shared_openssl ? Py_True : Py_False);
+}
+
 PyMethodDef kMethods[] = {
     {"configure", configure, METH_VARARGS,
-     "configure(ConnectionFailed, HttpStatusError, SSLError[, TimeoutError])"},
+     "configure(ConnectionFailed, HttpStatusError, SSLError[, TimeoutError[, ssl_module_path, "
+     "ssl_openssl_version_number]])"},
     {"ssl_context_supported", ssl_context_supported, METH_O,
-     "ssl_context_supported(ctx) -> bool: the SSLContext's SSL_CTX can be used natively"},
+     "ssl_context_supported(ctx) -> bool: the context's SSL_CTX can be used natively"},
+    {"openssl", openssl_info, METH_NOARGS,
+     "openssl() -> (version number, version text, shared with CPython's ssl module)"},
     {nullptr, nullptr, 0, nullptr},
 };
 
@@ -1648,6 +1847,13 @@ PyMODINIT_FUNC PyInit__netconn(void) {
       !intern(&s_on_readable, "_on_readable") || !intern(&s_on_writable, "_on_writable") ||
       !intern(&s_options, "options") || !intern(&s_verify_mode, "verify_mode"))
     return nullptr;
+  TlsCtxType.tp_dealloc = reinterpret_cast<destructor>(tls_dealloc);
+  TlsCtxType.tp_flags = Py_TPFLAGS_DEFAULT;
+  TlsCtxType.tp_doc = "An SSL_CTX built by _netconn from PEM material (the linked libssl).";
+  TlsCtxType.tp_getset = kTlsGetSet;
+  TlsCtxType.tp_init = reinterpret_cast<initproc>(tls_init);
+  TlsCtxType.tp_new = PyType_GenericNew;
+  if (PyType_Ready(&TlsCtxType) < 0) return nullptr;
   ConnType.tp_dealloc = reinterpret_cast<destructor>(conn_dealloc);
   ConnType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_BASETYPE | Py_TPFLAGS_HAVE_GC;
   ConnType.tp_doc = "One HTTP/1.1 client connection driven by an asyncio loop.";
@@ -1683,6 +1889,12 @@ PyMODINIT_FUNC PyInit__netconn(void) {
   Py_INCREF(&PoolType);
   if (PyModule_AddObject(m, "Pool", reinterpret_cast<PyObject*>(&PoolType)) < 0) {
     Py_DECREF(&PoolType);
+    Py_DECREF(m);
+    return nullptr;
+  }
+  Py_INCREF(&TlsCtxType);
+  if (PyModule_AddObject(m, "TlsContext", reinterpret_cast<PyObject*>(&TlsCtxType)) < 0) {
+    Py_DECREF(&TlsCtxType);
     Py_DECREF(m);
     return nullptr;
   }

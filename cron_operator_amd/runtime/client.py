@@ -297,6 +297,17 @@ class Client:
         self._m_verb: Dict[str, Tuple[Dict[str, Any], Any]] = {}  # verb -> ({code: counter}, latency histogram)
         self._m_rl: Dict[str, Any] = {}
 
+    def gate_saturated(self) -> bool:
+        """Is the in-flight cap the bottleneck right now (every slot taken, QPS bucket idle)?
+        A reconcile then runs its writes on its worker instead of as a deferred tail: more
+        queued requests would only wait in the gate (and cost CPU), not reorder anything --
+        reordering happens while the QPS bucket is backed up, and there tails are cheap."""
+        g = self.inflight
+        if g is None or g.inflight + g.waiting < g.limit:
+            return False
+        lim = self.limiter
+        return lim is None or not lim.waiting
+
     # -- plumbing
     def _gvr_now(self, target: GVRorGVK) -> Optional[GroupVersionResource]:
         """The resource of ``target`` without a discovery round trip (None: not known yet)."""

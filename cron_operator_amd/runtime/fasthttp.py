@@ -501,9 +501,12 @@ class HttpPool:
 
     def __init__(self, base_url: str, ssl_context: Optional[_ssl.SSLContext] = None,
                  headers: Optional[Dict[str, str]] = None, max_idle: int = 64, timeout: float = 60.0,
-                 server_hostname: Optional[str] = None, proxy: str = "", native: Optional[bool] = None):
+                 server_hostname: Optional[str] = None, proxy: str = "", native: Optional[bool] = None,
+                 tls_material: Optional[Dict[str, Any]] = None):
         """``native``: use ``_netconn`` connections (None: whenever the extension is built and it
-        can drive the TLS context; True: required)."""
+        can drive the TLS context; True: required).  ``tls_material``: the PEM material behind
+        ``ssl_context`` (``RestConfig.tls_material``): native TLS then runs on an ``SSL_CTX`` the
+        extension builds itself (``_netconn.TlsContext``) instead of the ``ssl.SSLContext``'s."""
         u = urlsplit(base_url)
         self.scheme = u.scheme or "http"
         self.host = u.hostname or "127.0.0.1"
@@ -528,6 +531,8 @@ class HttpPool:
             if self.scheme == "http":
                 self._target = f"http://{self._hosthdr}{self.base_path}"
         self._np = None  # the native pool (request path in C++) when the native connections serve
+        self._tls_material = tls_material if self.scheme == "https" else None
+        self._native_tls: Any = None  # _netconn.TlsContext built from _tls_material
         self.set_headers(headers)
         self._pidle: Deque[_Conn] = deque()
         self.max_idle = max_idle
@@ -552,7 +557,11 @@ class HttpPool:
 
         want = self._want_native
         mod = netconn_native.load() if want is not False else None
-        ok = mod is not None and (self.ssl is None or mod.ssl_context_supported(self.ssl))
+        self._native_tls = None
+        if mod is not None and self.ssl is not None and self._tls_material is not None:
+            self._native_tls = netconn_native.tls_context(self._tls_material)
+        ok = mod is not None and (self.ssl is None or self._native_tls is not None
+                                  or mod.ssl_context_supported(self.ssl))
         if want and not ok:
             raise RuntimeError("native HTTP connections unavailable for this pool "
                                f"(extension {'missing' if mod is None else 'loaded'})")
@@ -578,10 +587,11 @@ class HttpPool:
         if self._np is not None:
             self._np.set_fixed(self._target, self._fixed)
 
-    def set_ssl(self, ctx: _ssl.SSLContext) -> None:
+    def set_ssl(self, ctx: _ssl.SSLContext, tls_material: Optional[Dict[str, Any]] = None) -> None:
         """New connections handshake with ``ctx`` (a rotated client certificate); idle
         connections made with the old one are closed, busy ones when they are given back."""
         self.ssl = ctx
+        self._tls_material = tls_material
         self._ssl_gen += 1
         self._pick_native()
         if self._np is not None:
@@ -702,8 +712,11 @@ class HttpPool:
             if ctx is None:
                 conn = self._netconn.Conn(loop, sock.fileno())
             else:
-                conn = self._netconn.Conn(loop, sock.fileno(), ctx, self.server_hostname or self.host,
-                                          ctx.check_hostname, ctx.hostname_checks_common_name)
+                # the extension's own SSL_CTX when it has the PEM material; the hostname policy
+                # is the ssl.SSLContext's either way
+                conn = self._netconn.Conn(loop, sock.fileno(), self._native_tls or ctx,
+                                          self.server_hostname or self.host, ctx.check_hostname,
+                                          ctx.hostname_checks_common_name)
         except BaseException:
             sock.close()
             raise

@@ -158,7 +158,7 @@ class HttpTransport(Transport):
             self._pool = HttpPool(self.config.host, ssl_context=self.config.ssl_context() or None,
                                   headers=self.config.auth_headers(self._token), max_idle=self._pool_size,
                                   timeout=self._timeout, server_hostname=self.config.tls_server_name or None,
-                                  proxy=self._proxy or "")
+                                  proxy=self._proxy or "", tls_material=self.config.tls_material())
             self._cert_generation = self.config.cert_generation
         elif self.config.rotating:
             self._rotate_token()
@@ -173,7 +173,7 @@ class HttpTransport(Transport):
             self._cert_generation = self.config.cert_generation
             ctx = self.config.ssl_context()
             if ctx is not None:
-                self._pool.set_ssl(ctx)
+                self._pool.set_ssl(ctx, self.config.tls_material())
         if tok == self._token:
             return
         self._token = tok

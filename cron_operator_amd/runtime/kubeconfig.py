@@ -274,6 +274,27 @@ class RestConfig:
             fh.write(data)
         return path
 
+    def tls_material(self) -> Optional[Dict[str, Any]]:
+        """The PEM material :meth:`ssl_context` is built from, for the native connections'
+        own ``SSL_CTX`` (``ops/netconn_native.tls_context``): ``cadata``/``cafile``,
+        ``certdata``/``keydata`` (bytes; files read), ``verify`` and ``check_hostname``."""
+        if not self.host.startswith("https://"):
+            return None
+        cert_data, key_data = self.client_cert()
+        if not cert_data:
+            cert_data, key_data = self.cert_data, self.key_data
+            if self.cert_file:
+                with open(self.cert_file, "rb") as fh:
+                    cert_data = fh.read()
+                key_data = b""
+                if self.key_file:
+                    with open(self.key_file, "rb") as fh:
+                        key_data = fh.read()
+        return {"cadata": None if self.insecure else (self.ca_data or None),
+                "cafile": None if self.insecure or self.ca_data else (self.ca_file or None),
+                "certdata": cert_data or None, "keydata": key_data or None,
+                "verify": not self.insecure, "check_hostname": not self.insecure}
+
     def ssl_context(self) -> Optional[ssl.SSLContext]:
         if not self.host.startswith("https://"):
             return None

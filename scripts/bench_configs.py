@@ -96,8 +96,11 @@ def main() -> int:
         if qps == "chart":
             qps, burst = chart_client_values()
         t0 = time.perf_counter()
+        def on_step(k, dt, timed, _name=name, _mode=mode):
+            print(f"  {_name} {_mode} step {k}: {dt:.2f} s{'' if timed else ' (warmup)'}", flush=True)
+
         r = run_sync(BenchConfig(n_crons=n, steps=steps, warmup=warmup, mode=mode, qps=qps, burst=burst,
-                                 shards=shards, apiserver_latency=lat, tls=tls, native_http=native))
+                                 shards=shards, apiserver_latency=lat, tls=tls, native_http=native), on_step)
         fires = n * steps
         row = {"config": name, "mode": mode, "shards": shards, "n_crons": n, "qps": qps, "burst": burst,
                "apiserver_latency": lat, "tls": tls, "native_http": native, "steps": steps,

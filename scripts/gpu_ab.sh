@@ -1,8 +1,9 @@
 #!/bin/bash
 # One gpurun call: paired A/B of the 1-process 1000-Cron bench on the box.  ab_base/ holds an
 # older tree (git archive <rev> | tar -x -C ab_base; git-ignored, shipped with the snapshot).
-# ARMS lists the arms run in turn each round: "base", "head", or "head:VAR=value" (head with an
-# environment override, e.g. head:CRON_OPERATOR_NATIVE_HTTP=python).
+# ARMS lists the arms run in turn each round: "base", "head", "head:VAR=value" (head with an
+# environment override, e.g. head:CRON_OPERATOR_NATIVE_HTTP=python) or "head@--arg=v,--flag"
+# (head with extra bench.py arguments, comma-separated).
 #   TAG=r3b ROUNDS=4 ARMS="base head:CRON_OPERATOR_NATIVE_HTTP=python head" bash scripts/gpu_ab.sh
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -18,14 +19,16 @@ for d in ab_base .; do
 done
 for i in $(seq "$ROUNDS"); do
   for arm in $ARMS; do
-    d=.; envs=()
+    d=.; envs=(); extra=()
     case "$arm" in
       base) d=ab_base ;;
       head:*) envs=("${arm#head:}") ;;
+      head@*) IFS=, read -r -a extra <<< "${arm#head@}" ;;
     esac
-    name=$(echo "$arm" | tr ':=' '__')
+    name=$(echo "$arm" | tr ':=@,' '____' | tr -d '-')
     (cd "$d" && env "${envs[@]}" PYTHONPATH=$PWD timeout -k 10 300 python bench.py --shards ${SHARDS:-1} --steps 10 \
-        --warmup 3 --baseline none > "$OUT/${name}_$i.log" 2>&1)
+        --warmup 3 --baseline none --single-process none $([ "$d" = . ] && echo --deployment none) "${extra[@]}" \
+        > "$OUT/${name}_$i.log" 2>&1)
     rc=$?; [ $rc -eq 0 ] || { echo "$name round $i rc=$rc"; exit $rc; }
     python - "$OUT/${name}_$i.log" "$name" "$i" <<'PY'
 import json, sys

@@ -1,0 +1,48 @@
+#!/bin/bash
+# One gpurun call of round 4.  STEPS selects what runs (space-separated):
+#   tests   GPU test tier (payload on the MI355X), smoke()
+#   bench   the driver's bench invocation (20 timed steps), JSON kept
+#   configs deployment-shaped rows (etcd latency, TLS, chart defaults at 1000 Crons)
+#   rocprof kernel stats of the scheduled payload (rocprofv3 --kernel-trace --stats)
+# Stops at the first failure; every GPU step has its own time limit.
+#   TAG=r4a STEPS="tests bench" bash scripts/gpu_r4.sh
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export PYTHONPATH=$PWD
+export TMPDIR=/tmp
+TAG=${TAG:-r4}
+STEPS=${STEPS:-"tests bench"}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+step() { echo "== $1 $(date +%T)"; }
+check() { local rc=$1; echo "$2 rc=$rc"; [ "$rc" = 0 ] || exit "$rc"; }
+
+for s in $STEPS; do
+  case $s in
+    tests)
+      step "gpu tests"
+      timeout -k 10 600 python -u -m pytest tests/test_gpu.py -m gpu -x -v -p no:cacheprovider \
+        --timeout 120 --timeout-method thread > "$OUT/gpu_tests.log" 2>&1
+      check $? tests; tail -3 "$OUT/gpu_tests.log"
+      step smoke
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+      check $? smoke; tail -3 "$OUT/smoke.log" ;;
+    bench)
+      step bench
+      timeout -k 10 900 python bench.py --gpus 1 --steps 20 --warmup 5 --out "$OUT/bench.json" \
+        > "$OUT/bench.log" 2> "$OUT/bench.err"
+      check $? bench; cat "$OUT/bench.err"; tail -1 "$OUT/bench.log" | cut -c1-600 ;;
+    configs)
+      step configs
+      timeout -k 10 1100 python -u scripts/bench_configs.py --only "${CONFIGS:-etcd-latency,chart-defaults-1000}" \
+        ${CONFIG_MODE:+--mode $CONFIG_MODE} --out "$OUT/configs.json" > "$OUT/configs.log" 2>&1
+      check $? configs; tail -8 "$OUT/configs.log" ;;
+    rocprof)
+      step rocprof
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o payload -- \
+        python -m cron_operator_amd.models.payloads.train_smoke > "$OUT/rocprof.log" 2>&1
+      check $? rocprof; find "$OUT/prof" -name "*kernel_stats.csv" | head -2 ;;
+    *) echo "unknown step $s"; exit 2 ;;
+  esac
+done
+echo "== done $(date +%T)"

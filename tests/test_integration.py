@@ -471,3 +471,64 @@ async def test_shard_assigner_holds_background_watch_tasks():
     await asyncio.sleep(0)
     assert not asg._bg and asg.informers[gvk] is inf
     await cache.stop()
+
+
+async def test_upgrade_from_hash_to_label_routing_keeps_running_children_in_view():
+    """a hash-routed sharded fleet with running jobs restarts with label routing.
+    Every object is unlabelled then; the child label PATCHes are slow (0.2 s each).  A Cron
+    must not join its shard's informer before its running child does: under Forbid no second
+    job may start while the first runs, and status.active never drops the running job."""
+    from cron_operator_amd.controller.setup import setup_with_manager
+    from cron_operator_amd.controller.sharding import LABEL_SHARD
+    from cron_operator_amd.runtime.client import Client, InMemoryTransport
+    from cron_operator_amd.runtime.manager import Manager, ManagerOptions
+
+    clock = FakeClock(1767268805 * 10**9)
+    env = TestEnv(clock=clock)
+    n = 8
+    for i in range(n):
+        await env.create_cron(new_cron(f"u{i}", NS, "*/1 * * * *", PT_TMPL, concurrency_policy="Forbid"))
+
+    class SlowChildLabels(InMemoryTransport):
+        async def request(self, verb, gvr, namespace="", name="", subresource="", body=None, params=None):
+            if verb == "patch" and gvr.resource == "pytorchjobs" and not subresource:
+                await asyncio.sleep(0.2)  # the shard assigner's label PATCH of a child
+            return await super().request(verb, gvr, namespace, name, subresource, body, params)
+
+    async def run(routing, minutes, slow=False):
+        mgrs, tasks, ctrls = [], [], []
+        for idx in range(2):
+            client = Client(SlowChildLabels(env.server) if slow else InMemoryTransport(env.server), qps=-1)
+            m = Manager(client, ManagerOptions(clock=clock, shard_index=idx, shard_count=2, shard_routing=routing,
+                                               health_probe_bind_address="0", metrics_bind_address="0"))
+            ctrls.append((await setup_with_manager(m))[0])
+            mgrs.append(m)
+            tasks.append(asyncio.get_running_loop().create_task(m.start()))
+        for m in mgrs:
+            await asyncio.wait_for(m.started.wait(), 10)
+        actives = []
+        for _ in range(minutes):
+            for _ in range(60):
+                clock.advance(1)
+                await asyncio.sleep(0.001)
+                for i in range(n):
+                    st = env.server.get(CRON_GVR, NS, f"u{i}").get("status") or {}
+                    actives.append((i, len(st.get("active") or [])))
+            await _quiesce(env, ctrls)
+        for m in mgrs:
+            m.stop()
+        for t in tasks:
+            await asyncio.wait_for(t, 10)
+        return actives
+
+    await run("hash", 1)  # the first tick: one running job per Cron (nothing completes them)
+    first = {i: names(env.server, PT, f"u{i}") for i in range(n)}
+    assert all(len(v) == 1 for v in first.values()), first
+    actives = await run("labels", 2, slow=True)
+    for i in range(n):
+        assert names(env.server, PT, f"u{i}") == first[i], f"u{i}: Forbid violated after the routing change"
+    # from the moment the job exists its Cron lists it as active, through the relabelling
+    assert all(k == 1 for _, k in actives), [x for x in actives if x[1] != 1][:5]
+    for o in env.server.list(PT, NS)["items"] + env.server.list(CRON_GVR, NS)["items"]:
+        assert LABEL_SHARD in o["metadata"]["labels"]
+    env.server.close_all_watches()

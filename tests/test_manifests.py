@@ -159,3 +159,99 @@ def test_native_extensions_clean_under_asan_ubsan():
     out = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "sanitize.py")], capture_output=True,
                          text=True, timeout=600, env=env)
     assert out.returncode == 0 and "sanitize ok" in out.stdout, out.stdout[-2000:] + out.stderr[-4000:]
+
+
+# ----------------------------------------------------------------------------- payload image
+
+PAYLOAD_REPO = "cron-operator-amd/cron-operator-mi355x-payload"
+
+
+def _payload_image_files():
+    """Files Dockerfile.payload puts into the image (destination paths) and its PYTHONPATH."""
+    import shlex
+
+    with open(os.path.join(ROOT, "Dockerfile.payload")) as fh:
+        text = fh.read().replace("\\\n", " ")
+    files, pythonpath = set(), None
+    for line in text.splitlines():
+        words = shlex.split(line, comments=True)
+        if not words:
+            continue
+        if words[0] == "COPY":
+            srcs, dst = words[1:-1], words[-1]
+            for src in srcs:
+                assert os.path.isfile(os.path.join(ROOT, src)), f"COPY source {src} missing"
+                files.add(os.path.join(dst, os.path.basename(src)) if dst.endswith("/") else dst)
+        if words[0] == "ENV":
+            for w in words[1:]:
+                if w.startswith("PYTHONPATH="):
+                    pythonpath = w.split("=", 1)[1]
+    return files, pythonpath
+
+
+def _module_of(ctr):
+    argv = list(ctr.get("command") or []) + list(ctr.get("args") or [])
+    for i, w in enumerate(argv):
+        if w == "-m":
+            return argv[i + 1]
+    return None
+
+
+def _mi355x_containers():
+    out = []
+    for name in sorted(os.listdir(os.path.join(ROOT, "examples", "mi355x"))):
+        with open(os.path.join(ROOT, "examples", "mi355x", name)) as fh:
+            c = yaml.safe_load(fh)
+        for rtype, rs in c["spec"]["template"]["workload"]["spec"]["pytorchReplicaSpecs"].items():
+            for ctr in rs["template"]["spec"]["containers"]:
+                out.append((f"{name}:{rtype}", ctr))
+    return out
+
+
+@pytest.mark.parametrize("where,ctr", _mi355x_containers(), ids=lambda x: x if isinstance(x, str) else "")
+def test_mi355x_example_command_resolves_inside_its_image(where, ctr):
+    """Every MI355X example runs the payload image, and the module it runs is in that image
+    on its PYTHONPATH, as a package chain with every __init__.py."""
+    files, pythonpath = _payload_image_files()
+    assert pythonpath, "Dockerfile.payload sets no PYTHONPATH"
+    image = ctr["image"]
+    assert image.split("/", 1)[1].rsplit(":", 1)[0] == PAYLOAD_REPO, (where, image)
+    with open(os.path.join(ROOT, "VERSION")) as fh:
+        assert image.rsplit(":", 1)[1] == fh.read().strip().lstrip("v"), (where, image)
+    mod = _module_of(ctr)
+    assert mod, where
+    parts = mod.split(".")
+    assert os.path.join(pythonpath, *parts) + ".py" in files, (where, mod)
+    for i in range(1, len(parts)):
+        assert os.path.join(pythonpath, *parts[:i], "__init__.py") in files, (where, parts[:i])
+
+
+def test_payload_modules_need_only_stdlib_and_torch():
+    """The payload image is the ROCm PyTorch base plus these files: their imports must be
+    satisfiable there (standard library, torch, the payload package itself)."""
+    import ast
+    import sys
+
+    files, _ = _payload_image_files()
+    allowed = set(sys.stdlib_module_names) | {"torch", "cron_operator_amd", "__future__"}
+    for dst in files:
+        rel = dst.split("/cron_operator_amd/", 1)[1]
+        with open(os.path.join(ROOT, "cron_operator_amd", rel)) as fh:
+            tree = ast.parse(fh.read())
+        for node in ast.walk(tree):
+            names = []
+            if isinstance(node, ast.Import):
+                names = [a.name for a in node.names]
+            elif isinstance(node, ast.ImportFrom) and node.level == 0:
+                names = [node.module or ""]
+            for n in names:
+                assert n.split(".")[0] in allowed, (rel, n)
+                if n.startswith("cron_operator_amd"):
+                    assert n.startswith("cron_operator_amd.models.payloads") or n == "cron_operator_amd", (rel, n)
+
+
+def test_makefile_payload_image_matches_the_examples():
+    with open(os.path.join(ROOT, "Makefile")) as fh:
+        mk = fh.read()
+    assert "docker-build-payload:" in mk and "-f Dockerfile.payload" in mk
+    assert f"PAYLOAD_IMG ?= $(IMG_REGISTRY)/{PAYLOAD_REPO}:$(IMG_TAG)" in mk
