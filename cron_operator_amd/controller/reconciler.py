@@ -30,25 +30,24 @@ option                     default here                           reference
 ``wire_codecs``            watch events decoded by plan: child     every event decoded whole
                            ``spec`` skipped, Cron ``spec`` and
                            status history entries reused by bytes
-``defer_status_write``     the status PATCH and GC DELETEs after   the worker waits for the deferred
-                           a reconcile run as a deferred tail:     status patch (``:107-120``) after
-                           the worker is freed, the key stays      the CREATE (``:229-238``)
-                           processing until they land
+``defer_status_write``     once only API writes are left (the      the worker waits for the deferred
+                           CREATE, the status PATCH, GC DELETEs)   status patch (``:107-120``) after
+                           the reconcile releases its worker       the CREATE (``:229-238``)
+                           slot; the key stays processing
 ``request_priorities``     tick CREATEs (and Replace DELETEs) go   one FIFO token bucket for every
                            first on a backed-up QPS bucket;        request
                            status PATCHes / GC DELETEs / events
                            yield to them
 =========================  =====================================  =======================================
 
-``defer_status_write`` (with a controller that accepts tails, ``runtime/controller.py``, and
-while the client's in-flight cap is not the bottleneck -- ``Client.gate_saturated``):
-a fire reconcile otherwise holds its worker for two sequential write round trips --
-the CREATE, then the status PATCH that records ``lastScheduleTime``.  The PATCH (and
-any history-GC DELETE still in flight) becomes the reconcile's *tail*: the worker takes
-the next Cron at once, while this Cron's key stays processing in the work queue until
-the tail has landed, so a requeue of the key during the tail is parked and never starts
-a second reconcile of it.  Under apiserver latency a tick's CREATEs then go out at
-workers / (one round trip) instead of workers / (two round trips).
+``defer_status_write`` (under a controller worker, ``runtime/controller.py`` ``release_worker``,
+and while the client's in-flight cap is not the bottleneck -- ``Client.gate_saturated``): a
+fire reconcile otherwise holds its worker slot for two sequential write round trips -- the
+CREATE, then the status PATCH that records ``lastScheduleTime``.  Once the fire is decided,
+the reconcile hands its slot to the next queued Cron and finishes its writes on its own; its
+key stays processing in the work queue until it returns, so a requeue of the key meanwhile
+is parked and never starts a second reconcile of it.  Under apiserver latency a tick's
+CREATEs then go out at the client's in-flight cap instead of at workers / (two round trips).
 
 ``overlap_gc_deletes``: a GC DELETE's outcome feeds nothing else in the
 reconcile -- the reference only logs its error and drops the child from
@@ -87,7 +86,7 @@ import functools
 import json
 import operator
 from dataclasses import dataclass, field
-from typing import Any, Awaitable, Callable, Dict, List, Optional, Tuple
+from typing import Any, Callable, Dict, List, Optional, Tuple
 
 from ..api import errors
 from ..api.meta import (
@@ -120,7 +119,7 @@ from ..models.workload import (
 )
 from ..runtime import metrics, tracing
 from ..runtime.client import Client
-from ..runtime.controller import Reconciler, Request, Result
+from ..runtime.controller import Reconciler, Request, Result, release_worker
 from ..runtime.events import Normal, Warning, EventRecorder
 from ..runtime.ratelimit import PRIORITY_HIGH, PRIORITY_LOW, PRIORITY_NORMAL
 from ..runtime.informer import Cache, Informer
@@ -379,9 +378,6 @@ class CronReconciler(Reconciler):
         self.codecs: Optional[WireCodecs] = codecs if codecs is not None or not self.opts.wire_codecs else \
             WireCodecs(self.opts.slim_child_cache)
         self.expect = Expectations(self.opts.expectation_ttl, self.clock)
-        # set by the controller wiring (setup_with_manager): its Controller accepts Result.tail,
-        # so with defer_status_write the reconcile hands its last writes back as a tail
-        self.defer_tails = False
         prio = self.opts.request_priorities
         self._p_create = PRIORITY_HIGH if prio else PRIORITY_NORMAL    # a tick's CREATE, Replace DELETEs
         self._p_deferrable = PRIORITY_LOW if prio else PRIORITY_NORMAL  # status PATCH, history-GC DELETEs
@@ -463,20 +459,15 @@ class CronReconciler(Reconciler):
             result = Result()
             err: Optional[BaseException] = None
             gc: Optional[List["asyncio.Future[None]"]] = [] if self.opts.overlap_gc_deletes else None
-            deferring = self.defer_tails and self.opts.defer_status_write and not self.client.gate_saturated()
-            fire: Optional[List[Callable[[], Awaitable[Result]]]] = [] if deferring else None
+            # with a controller worker: hand the worker slot on before the API writes
+            release = self.opts.defer_status_write and not self.client.gate_saturated()
             try:
                 try:
-                    result = await self._sync(cron, log, gc, fire)
+                    result = await self._sync(cron, log, gc, release)
                 except Exception as e:  # noqa: BLE001 - joined with the patch error below
                     err = e
-                if deferring and err is None and (fire or gc or not old_status.semantic_equal(cron.status)):
-                    # the writes as a deferred tail: the controller frees this worker and keeps
-                    # the key processing until the CREATE, the status PATCH and the GC DELETEs land
-                    tail = asyncio.get_running_loop().create_task(
-                        self._tail(old_obj, old_status, cron, log, key, gc, fire[0] if fire else None, result))
-                    gc = None  # owned by the tail now
-                    return Result(result.requeue, result.requeue_after, result.requeue_after_ns, tail)
+                if release and (gc or not old_status.semantic_equal(cron.status)):
+                    release_worker()  # only writes are left: another Cron may use the slot
                 # B2: deferred status patch when status changed semantically (cron_controller.go:107-120)
                 if not old_status.semantic_equal(cron.status):
                     try:
@@ -500,39 +491,6 @@ class CronReconciler(Reconciler):
             return result
         finally:
             log.info("Finish reconciling Cron")
-
-    async def _tail(self, old_obj: Dict[str, Any], old_status: CronStatus, cron: Cron, log: Logger, key: str,
-                    gc: Optional[List["asyncio.Future[None]"]], fire: Optional[Callable[[], Awaitable[Result]]],
-                    result: Result) -> Result:
-        """The writes of a reconcile whose worker has moved on (``defer_status_write``): the
-        tick's Replace DELETEs and CREATE (B16-B20, ``cron_controller.go:210-238``), then the
-        status PATCH (B2, ``:107-120``) -- which runs even when the CREATE failed, as the
-        reference's deferred patch does -- and the overlapped GC DELETEs.  Resolves to the
-        reconcile's Result, or raises its (joined) error; the controller requeues it with
-        backoff, like the reference's returned error."""
-        err: Optional[BaseException] = None
-        try:
-            if fire is not None:
-                try:
-                    result = await fire()
-                except Exception as e:  # noqa: BLE001 - joined with the patch error below
-                    err = e
-            if not old_status.semantic_equal(cron.status):
-                try:
-                    await self._patch_status(old_obj, cron, log, key)
-                except Exception as pe:  # noqa: BLE001
-                    perr = RuntimeError(f"failed to patch Cron status: {pe}")
-                    perr.__cause__ = pe
-                    err = JoinedError(err, perr) if err is not None else perr
-            if gc:
-                await self._await_gc(gc)
-        except asyncio.CancelledError:
-            if gc:
-                aio.cancel_all(gc)
-            raise
-        if err is not None:
-            raise err
-        return result
 
     async def _get_cron(self, req: Request) -> Optional[Dict[str, Any]]:
         if self.cron_informer is not None:
@@ -614,9 +572,9 @@ class CronReconciler(Reconciler):
 
     # ------------------------------------------------------------------ the algorithm
     async def _sync(self, cron: Cron, log: Logger, gc: Optional[List["asyncio.Future[None]"]] = None,
-                    fire: Optional[List[Callable[[], Awaitable[Result]]]] = None) -> Result:
-        """B3-B20.  ``fire`` (a list): a decided fire (B16-B20, API writes) is not run but
-        appended there as a coroutine function for the caller's deferred tail."""
+                    release: bool = False) -> Result:
+        """B3-B20.  ``release``: hand the controller worker slot on once a fire is decided (only
+        API writes are left: B16-B20, then the status PATCH)."""
         policy = self.opts.workload
         # spans (and the attributes they would carry) only when tracing is on
         traced = tracing.get_tracer().enabled
@@ -759,9 +717,8 @@ class CronReconciler(Reconciler):
             log.v(1).info(f"Skip creating new {gvk.kind} due to concurrency policy forbid", active=len(active))
             return scheduled
 
-        if fire is not None:
-            fire.append(functools.partial(self._fire, cron, gvk, active, missed_run, next_run, now, log, scheduled))
-            return scheduled
+        if release:
+            release_worker()
         return await self._fire(cron, gvk, active, missed_run, next_run, now, log, scheduled)
 
     async def _fire(self, cron: Cron, gvk: GroupVersionKind, active: List[Child], missed_run: GoTime,

@@ -49,7 +49,6 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
     rec = CronReconciler(mgr.client, mgr.cache, mgr.get_event_recorder_for(CONTROLLER_NAME), mgr.clock, engine,
                          opts, cron_inf, codecs)
     ctrl = Controller(CONTROLLER_NAME, rec, mgr.clock, mgr.opts.max_concurrent_reconciles, log)
-    rec.defer_tails = True  # this controller takes Result.tail (ReconcilerOptions.defer_status_write)
     ctrl.set_log_constructor(log_constructor(log, "Cron"))
     assigner: Optional[sharding.ShardAssigner] = None
     if count > 1:

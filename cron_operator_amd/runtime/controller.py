@@ -16,30 +16,33 @@ worker loop it drives [ext]:
   a log constructor (``internal/controller/util.go:27-41``) with a
   ``reconcileID``.
 
-**Deferred tails.**  A reconcile may hand back its last writes instead of waiting for
-them: ``Result.tail`` is a future that finishes those writes and resolves to the final
-:class:`Result` (or raises the reconcile's error).  The worker is then free to take the
-next key at once, while the key itself stays *processing* in the queue until the tail
-has finished -- the queue parks any new add of that key ("dirty") exactly as it does
-during the reconcile proper, so per-key serialisation and the no-duplicate guarantee
-are unchanged.  The reference's deferred status patch (``cron_controller.go:107-120``)
-runs on the worker goroutine after the CREATE (``:229-238``): under apiserver latency a
-fire then holds a worker for two sequential write round trips; with a tail it holds it
-for one.  ``max_tails`` bounds the tails in flight (past it a worker awaits its own
-tail inline, which is the plain behaviour).
+**Released worker slots.**  ``--max-concurrent-reconciles`` bounds the reconciles that are
+*deciding* (reading caches, computing status).  A reconcile about to do nothing but API writes
+may call :func:`release_worker`: its worker slot goes to the next queued key at once, while
+the reconcile finishes its writes on the same task.  The key stays *processing* in the queue
+until that reconcile returns -- the queue parks any new add of the key ("dirty") exactly as
+before -- so per-key serialisation and the no-duplicate guarantee are unchanged.  The
+reference's deferred status patch (``cron_controller.go:107-120``) runs on the worker after
+the CREATE (``:229-238``): under apiserver latency a fire holds a worker for two sequential
+write round trips; with a released slot it holds it for none.  ``max_released`` bounds the
+reconciles writing after a release (the controller runs that many extra worker tasks; with
+all of them busy, new keys wait for a worker as usual).  Workers are long-lived tasks: a
+release costs two counter updates, not a task.
 """
 from __future__ import annotations
 
 import asyncio
+import contextvars
 import time
 import traceback
 import uuid
 from dataclasses import dataclass
 from functools import lru_cache
-from typing import Any, Awaitable, Callable, Dict, List, Optional, Tuple
+from collections import deque
+from typing import Any, Awaitable, Callable, Deque, Dict, List, Optional, Tuple
 
 from ..api.meta import GroupVersionKind, NamespacedName, controller_ref
-from ..parallel.workqueue import ShutDown, WorkQueue
+from ..parallel.workqueue import WorkQueue
 from ..utils import aio
 from ..utils.clock import Clock
 from ..utils.logging import Logger, get_logger, log_constructor
@@ -57,14 +60,42 @@ class Result:
     requeue: bool = False
     requeue_after: float = 0.0  # seconds
     requeue_after_ns: int = 0   # exact form (schedule requeues land on the tick)
-    # a future finishing the reconcile's last writes; resolves to the final Result (see module doc)
-    tail: Optional["asyncio.Future[Result]"] = None
 
     def after_ns(self) -> int:
         return self.requeue_after_ns or int(self.requeue_after * 1e9)
 
     def is_zero(self) -> bool:
         return not self.requeue and self.after_ns() == 0
+
+
+class _Slot:
+    """One worker's claim on a ``--max-concurrent-reconciles`` slot for one reconcile."""
+
+    __slots__ = ("ctrl", "held")
+
+    def __init__(self, ctrl: "Controller"):
+        self.ctrl = ctrl
+        self.held = True
+
+    def release(self) -> bool:
+        if not self.held:
+            return False
+        self.held = False
+        self.ctrl._on_release()
+        self.ctrl._slot_release()
+        return True
+
+
+_SLOT: "contextvars.ContextVar[Optional[_Slot]]" = contextvars.ContextVar("cron_operator_worker_slot",
+                                                                            default=None)
+
+
+def release_worker() -> bool:
+    """Give this reconcile's worker slot to the next queued key; the caller keeps running (its
+    key stays processing until it returns).  False outside a controller worker, or when the
+    slot was already released."""
+    slot = _SLOT.get()
+    return slot is not None and slot.release()
 
 
 class TerminalError(Exception):
@@ -104,7 +135,7 @@ def shard_of(namespace: str, name: str, count: int) -> int:
 class Controller:
     def __init__(self, name: str, reconciler: Reconciler, clock: Clock, max_concurrent_reconciles: int = 1,
                  logger: Optional[Logger] = None, recover_panic: bool = True, queue: Optional[WorkQueue] = None,
-                 max_tails: int = 0):
+                 max_released: int = 0):
         self.name = name
         self.reconciler = reconciler
         self.shard: Tuple[int, int] = (0, 1)
@@ -119,10 +150,12 @@ class Controller:
         self._sources: List[Tuple[Informer, EventHandler]] = []
         self._workers: List[asyncio.Task] = []
         self.active = 0
-        # deferred tails in flight (key stays processing until each one finishes); 0 -> default bound
-        self.max_tails = max_tails if max_tails > 0 else max(1024, 100 * self.max_concurrent)
-        self._tails: Dict["asyncio.Future[Result]", Tuple[Request, Logger, float]] = {}
-        self.tails_started = 0
+        # reconciles still writing after release_worker() (their keys stay processing); 0 -> default
+        self.max_released = max_released if max_released > 0 else max(1024, 100 * self.max_concurrent)
+        self.released = 0        # writing after a release, right now
+        self.releases = 0        # release_worker() calls, total
+        self._free_slots = self.max_concurrent
+        self._slot_waiters: Deque[asyncio.Future] = deque()
         self.reconciles = 0
         self.errors = 0
         self.started = False
@@ -239,15 +272,44 @@ class Controller:
         c.inc()
 
     def in_flight(self) -> int:
-        """Reconciles running on a worker plus deferred tails still writing."""
-        return self.active + len(self._tails)
+        """Reconciles holding a worker slot plus released ones still writing."""
+        return self.active + self.released
 
-    async def process_one(self, req: Request) -> bool:
-        """Reconcile ``req``.  False: the reconcile left a deferred tail, which calls
-        ``queue.done(req)`` itself when it finishes; True: the caller calls it."""
+    # ------------------------------------------------------------------ worker slots
+    async def _slot_acquire(self) -> None:
+        if self._free_slots > 0 and not self._slot_waiters:
+            self._free_slots -= 1
+            return
+        fut = asyncio.get_running_loop().create_future()
+        self._slot_waiters.append(fut)
+        try:
+            await fut
+        except asyncio.CancelledError:
+            if fut.done() and not fut.cancelled():
+                self._slot_release()  # granted and cancelled in the same turn: pass it on
+            elif fut in self._slot_waiters:
+                self._slot_waiters.remove(fut)
+            raise
+
+    def _slot_release(self) -> None:
+        while self._slot_waiters:
+            fut = self._slot_waiters.popleft()
+            if not fut.done():
+                fut.set_result(None)  # the slot moves to this waiter
+                return
+        self._free_slots += 1
+
+    def _on_release(self) -> None:
+        self.active -= 1
+        self.released += 1
+        self.releases += 1
+        self._m_active.value = float(self.active)
+
+    async def process_one(self, req: Request) -> None:
         log = self._logger_for(req)
         self.active += 1
         self._m_active.value = float(self.active)
+        slot = _SLOT.get()
         t0 = time.perf_counter()
         result: Optional[Result] = None
         err: Optional[BaseException] = None
@@ -257,54 +319,29 @@ class Controller:
                     result = await self.reconciler.reconcile(req, log)
                     if result is None:
                         result = Result()
-                    sp.set(requeue_after_ms=result.after_ns() / 1e6, deferred_tail=result.tail is not None)
+                    sp.set(requeue_after_ms=result.after_ns() / 1e6,
+                           released_worker=slot is not None and not slot.held)
             else:
                 result = await self.reconciler.reconcile(req, log)
                 if result is None:
                     result = Result()
-            tail = result.tail
-            if tail is not None and len(self._tails) >= self.max_tails:
-                result = await tail  # too many tails in flight: finish this one on the worker
-                tail = None
         except asyncio.CancelledError:
             raise
         except Exception as e:  # noqa: BLE001 - recover like RecoverPanic
             err = e
-            tail = None
             if not self.recover_panic:
                 raise
         finally:
-            self.active -= 1
-            self._m_active.value = float(self.active)
-        if tail is not None:
-            self._tails[tail] = (req, log, t0)
-            self.tails_started += 1
-            tail.add_done_callback(self._tail_done)
-            return False
+            if slot is not None and not slot.held:
+                self.released -= 1
+            else:
+                self.active -= 1
+                self._m_active.value = float(self.active)
         self._finish(req, log, t0, result, err)
-        return True
-
-    def _tail_done(self, tail: "asyncio.Future[Result]") -> None:
-        """A deferred tail finished: handle its result and release its key."""
-        entry = self._tails.pop(tail, None)
-        if entry is None:
-            return
-        req, log, t0 = entry
-        try:
-            if tail.cancelled():  # shutdown / leader loss: the key is simply released
-                return
-            err = tail.exception()
-            result = None if err is not None else (tail.result() or Result())
-            try:
-                self._finish(req, log, t0, result, err)
-            except Exception as e:  # noqa: BLE001 - a done callback must not raise into the loop
-                log.error(e, "Failed to handle a deferred reconcile result")
-        finally:
-            self.queue.done(req)
 
     def _finish(self, req: Request, log: Logger, t0: float, result: Optional[Result],
                 err: Optional[BaseException]) -> None:
-        """Result handling after a reconcile (and its tail) finished."""
+        """Result handling after a reconcile finished."""
         q = self.queue
         self._m_time.observe(time.perf_counter() - t0)
         self.reconciles += 1
@@ -335,25 +372,34 @@ class Controller:
             self.on_result(req, result, err)
 
     async def _worker(self) -> None:
+        """Take a slot, then a key; reconcile it (the reconcile may hand its slot on early with
+        :func:`release_worker`); release the key and the slot."""
         q = self.queue
         while True:
+            await self._slot_acquire()
             try:
                 req = await q.get()
-            except ShutDown:
+            except BaseException:  # ShutDown or cancellation: the slot goes back
+                self._slot_release()
                 return
-            release = True
+            slot = _Slot(self)
+            token = _SLOT.set(slot)
             try:
-                release = await self.process_one(req)
+                await self.process_one(req)
             finally:
-                if release:
-                    q.done(req)
+                _SLOT.reset(token)
+                q.done(req)
+                if slot.held:
+                    slot.held = False
+                    self._slot_release()
 
     def start(self) -> None:
         if self.started:
             return
         self.started = True
         loop = asyncio.get_running_loop()
-        for i in range(self.max_concurrent):
+        # max_concurrent workers decide at any time; max_released more may still be writing
+        for i in range(self.max_concurrent + self.max_released):
             self._workers.append(loop.create_task(self._worker(), name=f"{self.name}-worker-{i}"))
         self._workers.append(loop.create_task(self._unfinished_loop(), name=f"{self.name}-metrics"))
 
@@ -367,9 +413,8 @@ class Controller:
     async def stop(self) -> None:
         self.queue.shutdown()
         workers, self._workers = self._workers, []
-        # deferred tails are cancelled with the workers (controller-runtime cancels the context
-        # of every in-flight reconcile); their done callbacks release the keys
-        await aio.cancel_and_wait(*workers, *list(self._tails))
+        # controller-runtime cancels the context of every in-flight reconcile, released or not
+        await aio.cancel_and_wait(*workers)
         self.started = False
 
     async def wait_idle(self, settle: float = 0.0, timeout: float = 60.0) -> bool:

@@ -1,12 +1,13 @@
-"""Deferred reconcile tails: a fire's writes do not hold a worker, and never break per-key
-serialisation.
+"""Released worker slots: a fire's writes do not hold a ``--max-concurrent-reconciles`` slot,
+and never break per-key serialisation.
 
 Reference: the reconcile's status patch is deferred to the end of ``Reconcile``
 (``/root/reference/internal/controller/cron_controller.go:107-120``) and runs on the
 worker after the CREATE (``:229-238``), so each fire holds a worker for two sequential
-write round trips.  Here the CREATE, the status PATCH and the GC DELETEs become the
-reconcile's tail (``ReconcilerOptions.defer_status_write``, ``runtime/controller.py``):
-the worker moves on, the key stays *processing* in the work queue until the tail lands.
+write round trips.  Here, once only API writes are left (the CREATE, the status PATCH, the
+GC DELETEs), the reconcile releases its slot (``ReconcilerOptions.defer_status_write``,
+``runtime/controller.py`` ``release_worker``): the next key starts, while this key stays
+*processing* in the work queue until the writes land.
 """
 from __future__ import annotations
 
@@ -36,17 +37,23 @@ def _jobs(env, cron):
 
 
 def _spy(env):
-    """Count reconcile starts per key and fail if one starts while the key's tail is in flight."""
+    """Count reconcile starts per key and record any start while the same key is still in a
+    reconcile (released or not) -- a per-key serialisation violation."""
     ctrl = env.controller
     starts: Counter = Counter()
+    running: Counter = Counter()
     overlaps = []
     orig = ctrl.reconciler.reconcile
 
     async def spy(req, log):
-        if any(r == req for r, _, _ in ctrl._tails.values()):
+        if running[req]:
             overlaps.append(req)
         starts[req.name] += 1
-        return await orig(req, log)
+        running[req] += 1
+        try:
+            return await orig(req, log)
+        finally:
+            running[req] -= 1
 
     ctrl.reconciler.reconcile = spy
     return starts, overlaps
@@ -73,9 +80,9 @@ async def test_one_worker_creates_every_tick_while_status_writes_are_held():
     try:
         env.clock.advance(60)
         await _until(lambda: sum(len(_jobs(env, f"c{i}")) for i in range(4)) == 4, 2.0)
-        # every PATCH is still held: each key is still processing, no worker is busy
+        # every PATCH is still held: each key is still processing, no slot is taken
         assert env.controller.queue.processing() == 4
-        assert env.controller.active == 0 and env.controller.in_flight() == 4
+        assert env.controller.active == 0 and env.controller.released == 4
         for i in range(4):
             assert not (env.server.get(CRON_GVR, NS, f"c{i}").get("status") or {}).get("lastScheduleTime")
         env.server.faults.latency.clear()
@@ -169,12 +176,12 @@ async def test_direct_reconcile_calls_stay_synchronous():
     env.clock.advance(60)
     r = CronReconciler(env.client, None, FakeRecorder(), env.clock, NativeEngine(), ReconcilerOptions(list_mode="live"))
     res = await r.reconcile(Request(NS, "d"), get_logger())
-    assert res.tail is None and res.requeue_after_ns > 0
+    assert res.requeue_after_ns > 0
     assert len(_jobs(env, "d")) == 1
     assert env.server.get(CRON_GVR, NS, "d")["status"]["lastScheduleTime"]
 
 
-async def test_stop_cancels_held_tails_and_releases_their_keys():
+async def test_stop_cancels_released_reconciles_and_releases_their_keys():
     env = TestEnv()
     for i in range(3):
         await env.create_cron(new_cron(f"x{i}", NS, "*/1 * * * *", PT_TMPL))
