@@ -292,8 +292,10 @@ class Controller:
             raise
 
     def _slot_release(self) -> None:
+        # LIFO: the worker that parked last takes the slot -- a handful of hot worker tasks
+        # cycle while the spares (max_released of them) stay parked and cold
         while self._slot_waiters:
-            fut = self._slot_waiters.popleft()
+            fut = self._slot_waiters.pop()
             if not fut.done():
                 fut.set_result(None)  # the slot moves to this waiter
                 return

@@ -11,12 +11,20 @@ build image, so this checks the rules that matter for this codebase with
 * F811-ish duplicate top-level function/class definitions,
 * E501 line longer than 120 columns,
 * W291/W293 trailing whitespace, W292 missing final newline, tabs in indentation,
-* B006 mutable default arguments.
+* B006 mutable default arguments,
+* D001 (documentation evidence): in ``docs/*.md``, ``README.md`` and ``BASELINE.md`` every
+  paragraph, list item or table row that states a *measured* figure (throughput in
+  cron-reconciles/s or fires/s, latency as p50/p99, operator CPU per fire, RSS in MiB/KiB,
+  busy fractions) cites its evidence -- a ``profiles/...`` file, a driver record
+  (``BENCH_rNN.json`` etc.) or a test/script that produces it -- and every ``profiles/...``
+  path the docs name exists.  ``profiles/`` itself holds at most ``MAX_PROFILES`` files,
+  each cited somewhere in the docs (D002).
 """
 from __future__ import annotations
 
 import ast
 import os
+import re
 import sys
 from typing import List, Set, Tuple
 
@@ -24,6 +32,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DIRS = ["cron_operator_amd", "tests", "scripts"]
 FILES = ["bench.py", "__graft_entry__.py"]
 MAX_LINE = 120
+DOCS = ["README.md", "BASELINE.md"]
+MAX_PROFILES = 30
 
 
 def py_files() -> List[str]:
@@ -136,6 +146,76 @@ def fix_file(path: str) -> bool:
     return False
 
 
+# a measured figure: a number with a measurement unit, or a p50/p99 value
+_MEASURE = re.compile(r"\d[\d,.]*\s*(?:cron-reconciles/s|fires/s|MiB\b|KiB\b|ms (?:of )?(?:operator )?CPU)"
+                      r"|\bp(?:50|99)\b[^|]{0,20}?\d[\d,.]*\s*m?s\b|\b\d\.\d+ busy|busy \d\.\d+")
+_EVIDENCE = re.compile(r"profiles/[\w.\-/*]+|\b(?:BENCH|SCALE|GPUTEST|MULTICHIP)_r\d+\.json|tests/test_\w+\.py"
+                       r"|scripts/\w+\.py|test_\w+")
+_PROFILE_REF = re.compile(r"profiles/[\w.\-]+")
+
+
+def doc_files() -> List[str]:
+    out = [os.path.join(ROOT, f) for f in DOCS]
+    d = os.path.join(ROOT, "docs")
+    out.extend(os.path.join(d, f) for f in sorted(os.listdir(d)) if f.endswith(".md"))
+    return out
+
+
+def _blocks(text: str) -> List[Tuple[int, str]]:
+    """(first line number, text) of each paragraph, list item and table row."""
+    out: List[Tuple[int, str]] = []
+    cur: List[str] = []
+    start = 0
+    in_code = False
+    for i, line in enumerate(text.splitlines(), 1):
+        if line.startswith("```"):
+            in_code = not in_code
+            continue
+        if in_code:
+            continue
+        s = line.strip()
+        new_item = s.startswith(("|", "* ", "- ", "#")) or re.match(r"\d+\. ", s) is not None
+        if not s or new_item:
+            if cur:
+                out.append((start, " ".join(cur)))
+            cur = []
+        if s:
+            if not cur:
+                start = i
+            cur.append(s)
+            if s.startswith(("|", "#")):
+                out.append((start, " ".join(cur)))
+                cur = []
+    if cur:
+        out.append((start, " ".join(cur)))
+    return out
+
+
+def check_docs() -> List[Tuple[str, int, str, str]]:
+    problems: List[Tuple[str, int, str, str]] = []
+    cited: Set[str] = set()
+    for path in doc_files():
+        with open(path, encoding="utf-8") as fh:
+            text = fh.read()
+        rel = os.path.relpath(path, ROOT)
+        for ln, block in _blocks(text):
+            for ref in _PROFILE_REF.findall(block):
+                ref = ref.rstrip(".")
+                cited.add(ref)
+                if not os.path.exists(os.path.join(ROOT, ref)):
+                    problems.append((rel, ln, "D001", f"cites missing {ref}"))
+            if _MEASURE.search(block) and not _EVIDENCE.search(block):
+                problems.append((rel, ln, "D001", f"measured figure without evidence: {block[:90]!r}"))
+    pdir = os.path.join(ROOT, "profiles")
+    files = sorted(f for f in os.listdir(pdir) if not f.startswith("."))
+    if len(files) > MAX_PROFILES:
+        problems.append(("profiles", 0, "D002", f"{len(files)} files (at most {MAX_PROFILES})"))
+    for f in files:
+        if f"profiles/{f}" not in cited:
+            problems.append(("profiles", 0, "D002", f"{f} is not cited by any doc"))
+    return problems
+
+
 def main(argv: List[str]) -> int:
     files = py_files()
     if "--fix" in argv:
@@ -148,10 +228,13 @@ def main(argv: List[str]) -> int:
         for ln, code, msg in check_file(f):
             print(f"{os.path.relpath(f, ROOT)}:{ln}: {code} {msg}")
             n += 1
+    for rel, ln, code, msg in check_docs():
+        print(f"{rel}:{ln}: {code} {msg}")
+        n += 1
     if n:
         print(f"{n} problem(s)")
         return 1
-    print(f"lint ok ({len(files)} files)")
+    print(f"lint ok ({len(files)} files, {len(doc_files())} docs)")
     return 0
 
 
