@@ -39,7 +39,7 @@ for s in $STEPS; do
       check $? configs; tail -8 "$OUT/configs.log" ;;
     rocprof)
       step rocprof
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o payload -- \
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o payload -- \
         python -m cron_operator_amd.models.payloads.train_smoke > "$OUT/rocprof.log" 2>&1
       check $? rocprof; find "$OUT/prof" -name "*kernel_stats.csv" | head -2 ;;
     *) echo "unknown step $s"; exit 2 ;;
