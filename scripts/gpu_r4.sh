@@ -4,6 +4,9 @@
 #   bench   the driver's bench invocation (20 timed steps), JSON kept
 #   configs deployment-shaped rows (etcd latency, TLS, chart defaults at 1000 Crons)
 #   rocprof kernel stats of the scheduled payload (rocprofv3 --kernel-trace --stats)
+#   soak    80 ticks, 3 shards (peak RSS per shard, no drift)
+#   baseline all five BASELINE.json configs in both reconciler modes (scripts/baseline_configs.py)
+#   scale   cron-reconciles/s at 1 / 10 / 100 / 1000 Crons, both modes (scripts/bench_scale.py)
 # Stops at the first failure; every GPU step has its own time limit.
 #   TAG=r4a STEPS="tests bench" bash scripts/gpu_r4.sh
 set -o pipefail
@@ -42,6 +45,21 @@ for s in $STEPS; do
       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o payload -- \
         python -m cron_operator_amd.models.payloads.train_smoke > "$OUT/rocprof.log" 2>&1
       check $? rocprof; find "$OUT/prof" -name "*kernel_stats.csv" | head -2 ;;
+    soak)
+      step soak
+      timeout -k 10 600 python bench.py --steps 80 --warmup 3 --baseline none --single-process none \
+        --deployment none --out "$OUT/soak80.json" > "$OUT/soak80.log" 2> "$OUT/soak80.err"
+      check $? soak; tail -1 "$OUT/soak80.log" | cut -c1-300 ;;
+    baseline)
+      step baseline
+      timeout -k 10 900 python -u scripts/baseline_configs.py --out "$OUT/baseline_configs.json" \
+        > "$OUT/baseline_configs.log" 2>&1
+      check $? baseline; tail -15 "$OUT/baseline_configs.log" ;;
+    scale)
+      step scale
+      timeout -k 10 900 python -u scripts/bench_scale.py --steps 3 --warmup 1 --out "$OUT/scale.json" \
+        > "$OUT/scale.log" 2>&1
+      check $? scale; tail -12 "$OUT/scale.log" ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
