@@ -16,7 +16,8 @@ build image, so this checks the rules that matter for this codebase with
   paragraph, list item or table row that states a *measured* figure (throughput in
   cron-reconciles/s or fires/s, latency as p50/p99, operator CPU per fire, RSS in MiB/KiB,
   busy fractions) cites its evidence -- a ``profiles/...`` file, a driver record
-  (``BENCH_rNN.json`` etc.) or a test/script that produces it -- and every ``profiles/...``
+  (``BENCH_rNN.json`` etc.) or a test/script that produces it (a table row may rely on the
+  paragraph that introduces its table) -- and every ``profiles/...``
   path the docs name exists.  ``profiles/`` itself holds at most ``MAX_PROFILES`` files,
   each cited somewhere in the docs (D002).
 """
@@ -198,13 +199,18 @@ def check_docs() -> List[Tuple[str, int, str, str]]:
         with open(path, encoding="utf-8") as fh:
             text = fh.read()
         rel = os.path.relpath(path, ROOT)
+        caption = False  # the paragraph introducing the current table cites evidence
         for ln, block in _blocks(text):
             for ref in _PROFILE_REF.findall(block):
                 ref = ref.rstrip(".")
                 cited.add(ref)
                 if not os.path.exists(os.path.join(ROOT, ref)):
                     problems.append((rel, ln, "D001", f"cites missing {ref}"))
-            if _MEASURE.search(block) and not _EVIDENCE.search(block):
+            has = _EVIDENCE.search(block) is not None
+            row = block.startswith("|")
+            if not row and not block.startswith("#"):
+                caption = has
+            if _MEASURE.search(block) and not has and not (row and caption):
                 problems.append((rel, ln, "D001", f"measured figure without evidence: {block[:90]!r}"))
     pdir = os.path.join(ROOT, "profiles")
     files = sorted(f for f in os.listdir(pdir) if not f.startswith("."))

@@ -428,3 +428,43 @@ def test_install_is_what_the_suite_and_the_operator_use():
 
     if aioloop.install():
         assert asyncio.run(probe())
+
+
+def test_interpreter_gate_versions():
+    """The native core mirrors CPython 3.10's private asyncio internals: only that
+    interpreter qualifies."""
+    from cron_operator_amd.ops import aioloop_native as an
+
+    assert an.interpreter_supported((3, 10), "CPython")
+    for v, impl in (((3, 11), "CPython"), ((3, 12), "CPython"), ((3, 9), "CPython"), ((3, 10), "PyPy")):
+        assert not an.interpreter_supported(v, impl), (v, impl)
+
+
+def test_interpreter_gate_falls_back_to_asyncio_loop(monkeypatch):
+    """On an interpreter the core was not written for, the loader never imports the extension:
+    the operator runs on asyncio's own loop (and says why); =native refuses instead."""
+    import asyncio
+
+    from cron_operator_amd.ops import aioloop_native as an
+    from cron_operator_amd.runtime import aioloop as rl
+
+    monkeypatch.setattr(an, "interpreter_supported", lambda *a, **k: False)
+    monkeypatch.setattr(rl, "_loop_cls", None)
+    an._reset_for_tests()
+    try:
+        assert an.load() is None
+        assert an.status().startswith("asyncio: ") and "not one of the versions" in an.status()
+        loop = rl.new_event_loop()
+        try:
+            assert type(loop) is asyncio.SelectorEventLoop
+            assert loop.run_until_complete(asyncio.sleep(0, result=7)) == 7
+        finally:
+            loop.close()
+        an._reset_for_tests()
+        monkeypatch.setenv("CRON_OPERATOR_NATIVE_LOOP", "native")
+        with pytest.raises(RuntimeError, match="native event loop unavailable"):
+            an.load()
+    finally:
+        monkeypatch.undo()
+        an._reset_for_tests()
+        an.load()

@@ -213,6 +213,13 @@ def test_child_info_never_raises_inside_the_informer():
     assert info.err is not None and info.name == "x"
     odd = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob", "metadata": ["not", "a", "map"]}
     child_info(odd, gvk, WorkloadPolicy())  # must not raise
+    # a readable, finished status but a malformed creationTimestamp: an error, never "finished"
+    # (a finished child goes to history, whose entry needs the timestamp)
+    done = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+            "metadata": {"name": "y", "uid": "v", "creationTimestamp": "yesterday"},
+            "status": {"conditions": [{"type": "Succeeded", "status": "True"}]}}
+    info = child_info(done, gvk, WorkloadPolicy())
+    assert info.err is not None and info.cls is None and not info.finished
 
 
 async def test_sequential_gc_survives_a_transport_error():

@@ -192,5 +192,7 @@ async def test_stop_cancels_released_reconciles_and_releases_their_keys():
     await _until(lambda: env.controller.in_flight() == 3, 2.0)
     await asyncio.wait_for(env.controller.stop(), 1.0)
     assert env.controller.in_flight() == 0 and env.controller.queue.processing() == 0
+    # the cancelled CREATEs may already be stored: their pending marks stay (TTL / informer)
+    assert sum(len(v) for v in env.reconciler.expect.pending.values()) == 3
     env.server.faults.latency.clear()
     await env.stop()
