@@ -65,7 +65,7 @@ test-gpu: build ## GPU tier on an MI355X (scheduled payload on cuda:0, RCCL DDP,
 
 .PHONY: test-gpu-remote
 test-gpu-remote: build ## Run the GPU tier + bench + smoke on a gpurun MI355X box.
-	$(GPURUN) --timeout 1200 -- 'bash scripts/gpu_round.sh'
+	$(GPURUN) --timeout 1200 -- 'STEPS="tests bench rocprof" bash scripts/gpu_run.sh'
 
 .PHONY: sanity-check
 sanity-check: manifests ## CI sanity: generated files must be committed (no diff after `make manifests`).

@@ -1,5 +1,5 @@
 #!/bin/bash
-# One gpurun call of round 4.  STEPS selects what runs (space-separated):
+# One gpurun call.  STEPS selects what runs (space-separated):
 #   tests   GPU test tier (payload on the MI355X), smoke()
 #   bench   the driver's bench invocation (20 timed steps), JSON kept
 #   configs deployment-shaped rows (etcd latency, TLS, chart defaults at 1000 Crons)
@@ -8,7 +8,7 @@
 #   baseline all five BASELINE.json configs in both reconciler modes (scripts/baseline_configs.py)
 #   scale   cron-reconciles/s at 1 / 10 / 100 / 1000 Crons, both modes (scripts/bench_scale.py)
 # Stops at the first failure; every GPU step has its own time limit.
-#   TAG=r4a STEPS="tests bench" bash scripts/gpu_r4.sh
+#   TAG=r4a STEPS="tests bench" bash scripts/gpu_run.sh
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export PYTHONPATH=$PWD
