@@ -532,3 +532,47 @@ async def test_upgrade_from_hash_to_label_routing_keeps_running_children_in_view
     for o in env.server.list(PT, NS)["items"] + env.server.list(CRON_GVR, NS)["items"]:
         assert LABEL_SHARD in o["metadata"]["labels"]
     env.server.close_all_watches()
+
+
+async def test_shard_assigner_shutdown_leaves_no_label_patch_in_flight():
+    """Stopping the assigner (leader loss, shutdown) cancels its workers *and waits for them*:
+    once ``run`` has returned, no label PATCH is still running or lands later."""
+    from cron_operator_amd.api.v1alpha1 import CRON_GVK
+    from cron_operator_amd.controller.sharding import LABEL_SHARD, ShardAssigner
+    from cron_operator_amd.runtime.informer import Cache
+
+    env = TestEnv()
+    for i in range(6):
+        await env.create_cron(new_cron(f"a{i}", NS, "*/1 * * * *", PT_TMPL))
+    client = env.new_client()
+    started, finished = [], []
+    orig = client.patch
+
+    async def slow_patch(gvk, ns, name, *a, **kw):
+        started.append(name)
+        await asyncio.sleep(0.3)  # a label PATCH the apiserver holds
+        out = await orig(gvk, ns, name, *a, **kw)
+        finished.append(name)
+        return out
+
+    client.patch = slow_patch  # type: ignore[assignment]
+    cache = Cache(env.new_client(), NS)
+    asg = ShardAssigner(client, 0, 1)
+    await asg.watch(cache, CRON_GVK, child=False)
+    cache.start()
+    task = asyncio.get_running_loop().create_task(asg.run())
+    for _ in range(200):
+        if started:
+            break
+        await asyncio.sleep(0.005)
+    assert started, "no label PATCH started"
+    task.cancel()
+    await asyncio.gather(task, return_exceptions=True)
+    in_flight = [t for t in asyncio.all_tasks() if "_worker" in repr(t.get_coro()) and not t.done()]
+    assert in_flight == []
+    n = len(finished)
+    await asyncio.sleep(0.5)  # nothing lands after run() returned
+    assert len(finished) == n
+    labelled = [o for o in env.server.list(CRON_GVR, NS)["items"] if LABEL_SHARD in (o["metadata"].get("labels") or {})]
+    assert len(labelled) == n
+    await cache.stop()
