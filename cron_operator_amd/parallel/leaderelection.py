@@ -27,6 +27,7 @@ from typing import Any, Awaitable, Callable, Dict, Optional
 from ..api import errors
 from ..api.meta import GroupVersionResource
 from ..runtime import metrics
+from ..runtime.ratelimit import PRIORITY_HIGH
 from ..utils import aio, jsonutil
 from ..utils.clock import Clock, RealClock
 from ..utils.gotime import NANOS, UTC, GoTime, parse_rfc3339
@@ -134,7 +135,7 @@ class LeaderElector:
         body = dict(lease)
         body["spec"] = spec
         try:
-            updated = await self.client.update(LEASES, body)
+            updated = await self.client.update(LEASES, body, priority=PRIORITY_HIGH)
         except errors.ApiError as e:
             self.log.v(1).info("lease update failed", error=str(e))
             return False
@@ -153,7 +154,7 @@ class LeaderElector:
             self.log.v(1).info("optimistic lease renewal failed, falling back to GET")
         # 2. read (or create) the lease
         try:
-            lease = await self.client.get(LEASES, self.namespace, self.name)
+            lease = await self.client.get(LEASES, self.namespace, self.name, priority=PRIORITY_HIGH)
         except errors.ApiError as e:
             if not errors.is_not_found(e):
                 self.log.error(e, "error retrieving resource lock")
@@ -162,7 +163,7 @@ class LeaderElector:
             body = {"apiVersion": "coordination.k8s.io/v1", "kind": "Lease",
                     "metadata": {"name": self.name, "namespace": self.namespace}, "spec": spec}
             try:
-                created = await self.client.create(LEASES, body, self.namespace)
+                created = await self.client.create(LEASES, body, self.namespace, priority=PRIORITY_HIGH)
             except errors.ApiError as ce:
                 self.log.v(1).info("lease create lost the race", error=str(ce))
                 return False
@@ -251,14 +252,14 @@ class LeaderElector:
         if not self.is_leader:
             return
         try:
-            lease = await self.client.get(LEASES, self.namespace, self.name)
+            lease = await self.client.get(LEASES, self.namespace, self.name, priority=PRIORITY_HIGH)
             spec = lease.get("spec") or {}
             if spec.get("holderIdentity") != self.identity:
                 return
             now = self.clock.now_ns()
             spec.update({"holderIdentity": "", "leaseDurationSeconds": 1, "renewTime": _micro(now),
                          "acquireTime": _micro(now)})
-            await self.client.update(LEASES, lease)
+            await self.client.update(LEASES, lease, priority=PRIORITY_HIGH)
         except errors.ApiError as e:
             self.log.error(e, "failed to release lease")
         self.is_leader = False

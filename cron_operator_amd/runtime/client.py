@@ -25,7 +25,7 @@ from ..api.meta import GroupVersion, GroupVersionKind, GroupVersionResource
 from ..utils import jsonutil
 from ..utils.gotime import format_duration
 from . import metrics, tracing
-from .ratelimit import PRIORITY_NORMAL, InflightGate, TokenBucket, make_client_limiter
+from .ratelimit import PRIORITY_HIGH, PRIORITY_LOW, PRIORITY_NORMAL, InflightGate, TokenBucket, make_client_limiter
 
 GVRorGVK = Union[GroupVersionResource, GroupVersionKind]
 
@@ -296,6 +296,19 @@ class Client:
         self.requests_by_verb: Dict[str, int] = {}
         self._m_verb: Dict[str, Tuple[Dict[str, Any], Any]] = {}  # verb -> ({code: counter}, latency histogram)
         self._m_rl: Dict[str, Any] = {}
+        self._observe_gates()
+
+    def _observe_gates(self) -> None:
+        """Scrape-time series of the request gates (``rest_client_requests_in_flight`` /
+        ``_waiting``): read from the gates when /metrics is served, no per-request cost."""
+        if self.inflight is not None:
+            metrics.REST_INFLIGHT.observe((self.host,), self.inflight, lambda g: g.inflight)
+        for gate_name, gate in (("rate_limiter", self.limiter), ("in_flight", self.inflight)):
+            if gate is None:
+                continue
+            for prio, label in ((PRIORITY_HIGH, "high"), (PRIORITY_NORMAL, "normal"), (PRIORITY_LOW, "low")):
+                metrics.REST_WAITING.observe((self.host, gate_name, label), gate,
+                                             lambda g, p=prio: len(g._waiters[p]))
 
     def gate_saturated(self) -> bool:
         """Is the in-flight cap the bottleneck right now (every slot taken, QPS bucket idle)?

@@ -156,6 +156,8 @@ class Controller:
         self.releases = 0        # release_worker() calls, total
         self._free_slots = self.max_concurrent
         self._slot_waiters: Deque[asyncio.Future] = deque()
+        metrics.RECONCILES_WRITING.observe((name,), self, lambda c: c.released)
+        metrics.WORKER_RELEASES.observe((name,), self, lambda c: c.releases)
         self.reconciles = 0
         self.errors = 0
         self.started = False

@@ -26,7 +26,7 @@ from ..utils.clock import Clock, RealClock
 from ..utils.gotime import GoTime, UTC
 from ..utils.logging import get_logger
 from .client import Client
-from .ratelimit import TokenBucket
+from .ratelimit import PRIORITY_LOW, TokenBucket
 
 EVENTS_GVR = GroupVersionResource("", "v1", "events")
 
@@ -146,7 +146,8 @@ class Broadcaster:
         if seen is not None:
             ens, ename, count = seen
             try:
-                await self.client.patch(EVENTS_GVR, ens, ename, {"count": count + 1, "lastTimestamp": now})
+                await self.client.patch(EVENTS_GVR, ens, ename, {"count": count + 1, "lastTimestamp": now},
+                                        priority=PRIORITY_LOW)
                 self._seen[key] = (ens, ename, count + 1)
                 self._seen.move_to_end(key)
                 self.written += 1
@@ -161,7 +162,7 @@ class Broadcaster:
               "involvedObject": inv, "reason": reason, "message": message, "type": etype,
               "source": {"component": component}, "firstTimestamp": now, "lastTimestamp": now, "count": 1,
               "reportingComponent": component, "reportingInstance": ""}
-        await self.client.create(EVENTS_GVR, ev, ns)
+        await self.client.create(EVENTS_GVR, ev, ns, priority=PRIORITY_LOW)  # yields to a tick's CREATEs
         self.written += 1
         self._seen[key] = (ns, name, 1)
         if len(self._seen) > self._cache_size:

@@ -26,7 +26,7 @@ workloads created/deleted, missed ticks and status patches.
 """
 from __future__ import annotations
 
-from .promlite import Counter, Gauge, Histogram, ProcessCollector, PythonCollector, Registry
+from .promlite import Counter, Gauge, Histogram, ObservedGauge, ProcessCollector, PythonCollector, Registry
 
 REGISTRY = Registry()
 ProcessCollector(registry=REGISTRY)
@@ -102,6 +102,19 @@ WORKLOADS_DELETED = Counter("cron_operator_workloads_deleted_total", "Workloads 
 MISSED_TICKS = Counter("cron_operator_missed_ticks_total", "Scheduled ticks collapsed into a later run.",
                        registry=REGISTRY)
 STATUS_PATCHES = Counter("cron_operator_status_patches_total", "Cron status writes.", ["result"], registry=REGISTRY)
+# released worker slots (runtime/controller.py release_worker) and the client's request gates
+# (runtime/ratelimit.py), read at scrape time
+RECONCILES_WRITING = ObservedGauge("cron_operator_reconciles_writing",
+                                   "Reconciles that released their worker slot and are finishing their API writes.",
+                                   ["controller"], registry=REGISTRY)
+WORKER_RELEASES = ObservedGauge("cron_operator_worker_releases_total",
+                                "Reconciles that released their worker slot once only API writes were left.",
+                                ["controller"], kind="counter", registry=REGISTRY)
+REST_INFLIGHT = ObservedGauge("rest_client_requests_in_flight", "API requests in flight (watches excluded).",
+                              ["host"], registry=REGISTRY)
+REST_WAITING = ObservedGauge("rest_client_requests_waiting",
+                             "API requests waiting on the client's QPS bucket or in-flight cap, by priority.",
+                             ["host", "gate", "priority"], registry=REGISTRY)
 
 
 _CHILDREN: dict = {}

@@ -21,7 +21,7 @@ import platform
 import resource
 import threading
 from bisect import bisect_left
-from typing import Dict, Iterable, List, Optional, Sequence, Tuple
+from typing import Any, Dict, Iterable, List, Optional, Sequence, Tuple
 
 INF = float("inf")
 DEFAULT_BUCKETS = (0.005, 0.01, 0.025, 0.05, 0.075, 0.1, 0.25, 0.5, 0.75, 1.0, 2.5, 5.0, 7.5, 10.0)
@@ -254,6 +254,45 @@ class Histogram(_Metric):
         out.append(f"{self.name}_bucket{_labels(self.labelnames, key, ('le', '+Inf'))} {child.count}")
         out.append(f"{self.name}_sum{_labels(self.labelnames, key)} {_fmt(child.sum)}")
         out.append(f"{self.name}_count{_labels(self.labelnames, key)} {child.count}")
+
+
+class ObservedGauge(Collector):
+    """Series read from live objects at scrape time (no per-event update cost): each
+    :meth:`observe` binds a label set to ``fn(obj)`` for an object held weakly, so a
+    controller or client that goes away drops its series.  ``kind`` is ``gauge`` or
+    ``counter``."""
+
+    def __init__(self, name: str, documentation: str, labelnames: Sequence[str] = (), kind: str = "gauge",
+                 registry: Optional[Registry] = None):
+        self.name = name
+        self.documentation = documentation
+        self.labelnames = tuple(labelnames)
+        self.kind = kind
+        self._bound: Dict[Tuple[str, ...], Tuple[Any, Any]] = {}
+        if registry is not None:
+            registry.register(self)
+
+    def names(self) -> Iterable[str]:
+        return (self.name,)
+
+    def observe(self, labels: Sequence[str], obj: Any, fn: Any) -> None:
+        import weakref
+
+        self._bound[tuple(str(v) for v in labels)] = (weakref.ref(obj), fn)
+
+    def value(self, *labels: str) -> Optional[float]:
+        hit = self._bound.get(tuple(labels))
+        obj = hit[0]() if hit is not None else None
+        return None if obj is None else float(hit[1](obj))  # type: ignore[index]
+
+    def render(self, out: List[str]) -> None:
+        out.append(f"# HELP {self.name} {_escape_help(self.documentation)}")
+        out.append(f"# TYPE {self.name} {self.kind}")
+        for key, (ref, fn) in sorted(self._bound.items()):
+            obj = ref()
+            if obj is None:
+                continue
+            out.append(f"{self.name}{_labels(self.labelnames, key)} {_fmt(float(fn(obj)))}")
 
 
 class ProcessCollector(Collector):

@@ -13,6 +13,7 @@ import asyncio
 
 from cron_operator_amd.api.meta import GroupVersionResource
 from cron_operator_amd.api.v1alpha1 import CRON_GVR, new_cron
+from cron_operator_amd.runtime import metrics
 from cron_operator_amd.runtime.ratelimit import (PRIORITY_HIGH, PRIORITY_LOW, PRIORITY_NORMAL, InflightGate,
                                                  TokenBucket)
 from cron_operator_amd.testing.env import TestEnv
@@ -149,8 +150,10 @@ async def test_throttled_operator_creates_the_tick_before_its_status_writes():
         await env.settle()
         seen.clear()
         env.clock.advance(60)
+        waiting_high = 0.0
         for _ in range(400):
             await asyncio.sleep(0.01)
+            waiting_high = max(waiting_high, metrics.REST_WAITING.value("in-memory", "rate_limiter", "high") or 0)
             if seen.count("C") == 20 and seen.count("P") >= 20:
                 break
         assert seen.count("C") == 20, seen
@@ -158,5 +161,8 @@ async def test_throttled_operator_creates_the_tick_before_its_status_writes():
         patches_before = seen[:last_create].count("P")
         assert patches_before <= 2, "".join(seen)
         assert env.client.limiter.granted_by_priority[PRIORITY_HIGH] >= 20
+        # the scrape-time series show the backlog and the released worker slots
+        assert waiting_high >= 1
+        assert metrics.WORKER_RELEASES.value("cron") >= 20
     finally:
         await env.stop()
