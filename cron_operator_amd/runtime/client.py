@@ -308,7 +308,7 @@ class Client:
                 continue
             for prio, label in ((PRIORITY_HIGH, "high"), (PRIORITY_NORMAL, "normal"), (PRIORITY_LOW, "low")):
                 metrics.REST_WAITING.observe((self.host, gate_name, label), gate,
-                                             lambda g, p=prio: len(g._waiters[p]))
+                                             lambda g, p=prio: g.waiting_at(p))
 
     def gate_saturated(self) -> bool:
         """Is the in-flight cap the bottleneck right now (every slot taken, QPS bucket idle)?

@@ -54,6 +54,11 @@ class _PriorityWaiters:
         """Requests queued right now."""
         return self._n_waiting
 
+    def waiting_at(self, priority: int) -> int:
+        """Requests of one priority class queued right now (cancelled ones may still count
+        until the next grant passes them)."""
+        return len(self._waiters[priority])
+
     def _enqueue(self, priority: int, now: float) -> "asyncio.Future[None]":
         fut = asyncio.get_running_loop().create_future()
         self._waiters[priority].append((fut, now))
