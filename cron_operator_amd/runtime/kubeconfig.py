@@ -188,8 +188,8 @@ class RestConfig:
     insecure: bool = False
     tls_server_name: str = ""
     proxy_url: str = ""                   # kubeconfig ``proxy-url``: every request, no NO_PROXY
-    qps: float = 30.0
-    burst: int = 50
+    qps: float = 150.0                    # cmd/main.py DEFAULT_QPS / DEFAULT_BURST
+    burst: int = 300
     user_agent: str = "cron-operator-amd"
     exec_provider: Optional[ExecProvider] = None
     _file_token: str = ""

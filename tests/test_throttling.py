@@ -3,8 +3,9 @@
 The reference configures its client with ``--qps 30 --burst 50``
 (``/root/reference/cmd/operator/start.go:152-154,218-219``); client-go then logs
 ``Waited for <d> due to client-side throttling ...`` when a request waits on that
-bucket for long [ext, rest/request.go].  At the chart's ``qps: 30`` a 1000-Cron
-minutely workload needs ~67 QPS, so this log is how an operator says it is starved.
+bucket for long [ext, rest/request.go].  At the reference chart's ``qps: 30`` a 1000-Cron
+minutely workload would need ~83 QPS (this chart ships 150, ``tests/test_chart_sizing.py``),
+so this log is how an under-budgeted operator says it is starved.
 """
 from __future__ import annotations
 
