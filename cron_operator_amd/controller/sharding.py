@@ -113,6 +113,7 @@ class ShardAssigner:
         # Crons parked until their children are labelled: (namespace, cron) -> the Cron's key
         self._parked: Dict[Tuple[str, str], Tuple[GroupVersionKind, str, str]] = {}
         self._child_owner: Dict[Tuple[GroupVersionKind, str, str], Tuple[str, str]] = {}
+        self._cron_gvk: Optional[GroupVersionKind] = None
         # does this shard's child informer hold the (labelled) child?  set by setup_with_manager
         self.observed: Optional[Callable[[GroupVersionKind, str, str], bool]] = None
 
@@ -134,6 +135,8 @@ class ShardAssigner:
         self.informers[gvk] = inf
         if child:
             self._child_kinds.add(gvk)
+        else:
+            self._cron_gvk = gvk
         inf.add_handler(EventHandler(on_add=lambda o: self._offer(gvk, o, child),
                                      on_update=lambda _old, o: self._offer(gvk, o, child)))
         for o in list(inf.store.values()):
@@ -180,7 +183,10 @@ class ShardAssigner:
         if left is None:
             return
         left.discard(key)
-        if labelled:
+        cron_key = (self._cron_gvk, ck[0], ck[1]) if ck is not None else None  # type: ignore[index]
+        if labelled and cron_key in self._queued:
+            # the Cron waits for its labelling: it waits for these children to be observed too
+            # (an already-assigned Cron, or an orphan child's missing Cron, has nothing to wait for)
             self._children_done.setdefault(ck, []).append(key)  # type: ignore[arg-type]
         if not left:
             del self._children_left[ck]  # type: ignore[arg-type]

@@ -42,7 +42,7 @@ from collections import deque
 from typing import Any, Awaitable, Callable, Deque, Dict, List, Optional, Tuple
 
 from ..api.meta import GroupVersionKind, NamespacedName, controller_ref
-from ..parallel.workqueue import WorkQueue
+from ..parallel.workqueue import ShutDown, WorkQueue
 from ..utils import aio
 from ..utils.clock import Clock
 from ..utils.logging import Logger, get_logger, log_constructor
@@ -383,9 +383,12 @@ class Controller:
             await self._slot_acquire()
             try:
                 req = await q.get()
-            except BaseException:  # ShutDown or cancellation: the slot goes back
+            except ShutDown:
                 self._slot_release()
                 return
+            except BaseException:  # cancellation: the slot goes back
+                self._slot_release()
+                raise
             slot = _Slot(self)
             token = _SLOT.set(slot)
             try:
