@@ -7,6 +7,8 @@
 #   soak    80 ticks, 3 shards (peak RSS per shard, no drift)
 #   baseline all five BASELINE.json configs in both reconciler modes (scripts/baseline_configs.py)
 #   scale   cron-reconciles/s at 1 / 10 / 100 / 1000 Crons, both modes (scripts/bench_scale.py)
+#   ranks   the driver's multi-rank line (torch.distributed.run, N=2 and 4 CPU-only ranks): the
+#           N=8 scaling run is the driver's; RANKS overrides the list
 # Stops at the first failure; every GPU step has its own time limit.
 #   TAG=r4a STEPS="tests bench" bash scripts/gpu_run.sh
 set -o pipefail
@@ -60,6 +62,14 @@ for s in $STEPS; do
       timeout -k 10 900 python -u scripts/bench_scale.py --steps 3 --warmup 1 --out "$OUT/scale.json" \
         > "$OUT/scale.log" 2>&1
       check $? scale; tail -12 "$OUT/scale.log" ;;
+    ranks)
+      for n in ${RANKS:-2 4}; do
+        step "ranks $n"
+        timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" \
+          --master-addr 127.0.0.1 --master-port $((29500 + n)) bench.py --gpus "$n" --steps 20 --warmup 5 \
+          --out "$OUT/ranks$n.json" > "$OUT/ranks$n.log" 2> "$OUT/ranks$n.err"
+        check $? "ranks $n"; grep '^{' "$OUT/ranks$n.log" | cut -c1-400
+      done ;;
     *) echo "unknown step $s"; exit 2 ;;
   esac
 done
