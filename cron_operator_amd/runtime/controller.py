@@ -379,22 +379,28 @@ class Controller:
         """Take a slot, then a key; reconcile it (the reconcile may hand its slot on early with
         :func:`release_worker`); release the key and the slot."""
         q = self.queue
+        slot = _Slot(self)  # one per worker task, in the task's own context
+        slot.held = False
+        _SLOT.set(slot)
         while True:
-            await self._slot_acquire()
+            if self._free_slots > 0 and not self._slot_waiters:  # _slot_acquire's fast path, inline
+                self._free_slots -= 1
+            else:
+                await self._slot_acquire()
+            slot.held = True
             try:
                 req = await q.get()
             except ShutDown:
+                slot.held = False
                 self._slot_release()
                 return
             except BaseException:  # cancellation: the slot goes back
+                slot.held = False
                 self._slot_release()
                 raise
-            slot = _Slot(self)
-            token = _SLOT.set(slot)
             try:
                 await self.process_one(req)
             finally:
-                _SLOT.reset(token)
                 q.done(req)
                 if slot.held:
                     slot.held = False

@@ -10,6 +10,10 @@ every entry point with mutated and generated inputs:
 * ``_netconn``: mutated responses and watch streams delivered over a socketpair in random
   splits to native connections on a live event loop, closed by either side at random; the
   keep-alive ``Pool`` under deadline sweeps, abandoned requests and idle retirement;
+  ``TlsContext`` built from mutated PEM material (CA bundles, certificate chains, keys), and
+  real TLS handshakes + requests on the extension's own ``SSL_CTX`` against a Python TLS
+  server, with and without host-name checks; ``configure``'s shared-OpenSSL probe
+  (``dlopen``/``dlsym`` of CPython's ``_ssl``);
 * ``_fastjson``: random JSON trees through loads/dumpb/dumpb_shared/deepcopy/
   json_equal/create_merge_patch, plus malformed documents; the informer bookkeeping
   (store_apply) over malformed objects;
@@ -38,7 +42,7 @@ CSRC = os.path.join(ROOT, "cron_operator_amd", "ops", "csrc")
 EXTS = {"_cron_engine": "cron_engine.cpp", "_fastjson": "fastjson.cpp", "_httpcodec": "httpcodec.cpp",
         "_netconn": "netconn.cpp", "_aioloop": "aioloop.cpp", "_promlite": "promlite.cpp",
         "_workqueue": "workqueue.cpp"}
-LIBS = {"_netconn": ["-lssl", "-lcrypto"]}
+LIBS = {"_netconn": ["-lssl", "-lcrypto", "-ldl"]}
 
 
 def build(out_dir: str) -> None:
@@ -229,8 +233,9 @@ def drive(scratch: str, iters: int) -> None:
                 len(q), q.processing(), q.idle(), q.started()
     loops = drive_aioloop(rng, iters // 20)
     net = drive_netconn(rng, iters // 20)
+    tls = drive_tls(rng, iters // 40, scratch)
     print(f"sanitize ok: {iters} http, {iters // 4} json, {iters // 4} cron, {loops} loop programs, "
-          f"{net} connection cases", flush=True)
+          f"{net} connection cases, {tls} TLS cases", flush=True)
 
 
 def _native_loop_cls():
@@ -438,6 +443,101 @@ def drive_netconn(rng: random.Random, cases: int) -> int:
     finally:
         loop.close()
     return cases
+
+
+def drive_tls(rng: random.Random, cases: int, scratch: str) -> int:
+    """TlsContext over mutated PEM material, then handshakes and requests on its SSL_CTX."""
+    import asyncio
+    import ssl
+
+    import _netconn as ncm  # noqa: E402
+
+    sys.path.insert(0, ROOT)
+    from cron_operator_amd.runtime.servers import self_signed_cert
+
+    os.makedirs(os.path.join(scratch, "srv"), exist_ok=True)
+    os.makedirs(os.path.join(scratch, "cli"), exist_ok=True)
+    scert, skey = self_signed_cert(os.path.join(scratch, "srv"), host="localhost")
+    ccert, ckey = self_signed_cert(os.path.join(scratch, "cli"), host="operator")
+    pem = {k: open(v, "rb").read() for k, v in (("s", scert), ("sk", skey), ("c", ccert), ("ck", ckey))}
+
+    class ConnectionFailed(Exception):
+        def __init__(self, msg, no_response, reused):
+            super().__init__(msg)
+
+    class HttpStatusError(Exception):
+        def __init__(self, status, body):
+            super().__init__(status)
+
+    import _ssl
+
+    ncm.configure(ConnectionFailed, HttpStatusError, ssl.SSLError, asyncio.TimeoutError, _ssl.__file__,
+                  ssl.OPENSSL_VERSION_NUMBER)
+    ncm.configure(ConnectionFailed, HttpStatusError, ssl.SSLError, asyncio.TimeoutError, "/nonexistent.so", 1)
+    built = 0
+    for _ in range(cases):
+        kw = {}
+        for field, src in (("cadata", "s"), ("certdata", "c"), ("keydata", "ck")):
+            r = rng.random()
+            if r < 0.3:
+                continue
+            data = pem[src]
+            if r < 0.7:
+                data = _mutate(rng, data)
+            elif r < 0.8:
+                data = data + data
+            kw[field] = data
+        kw["verify"] = rng.random() < 0.8
+        try:
+            ncm.TlsContext(**kw)
+            built += 1
+        except (ssl.SSLError, ValueError):
+            pass
+    ncm.configure(ConnectionFailed, HttpStatusError, ssl.SSLError, asyncio.TimeoutError, _ssl.__file__,
+                  ssl.OPENSSL_VERSION_NUMBER)
+
+    async def run() -> int:
+        loop = asyncio.get_running_loop()
+        sctx = ssl.create_default_context(ssl.Purpose.CLIENT_AUTH)
+        sctx.load_cert_chain(scert, skey)
+
+        async def handle(reader, writer):
+            try:
+                while True:
+                    head = await reader.readuntil(b"\r\n\r\n")
+                    path = head.split(b" ")[1]
+                    writer.write(b"HTTP/1.1 200 OK\r\nContent-Length: %d\r\n\r\n" % len(path) + path)
+                    await writer.drain()
+            except (asyncio.IncompleteReadError, ConnectionResetError, ssl.SSLError, OSError):
+                pass
+            writer.close()
+
+        srv = await asyncio.start_server(handle, "127.0.0.1", 0, ssl=sctx)
+        port = srv.sockets[0].getsockname()[1]
+        ok = 0
+        for i in range(max(4, cases // 50)):
+            import socket
+
+            good_ca = rng.random() < 0.8
+            tctx = ncm.TlsContext(cadata=pem["s"] if good_ca else pem["c"], certdata=pem["c"], keydata=pem["ck"])
+            sock = socket.create_connection(("127.0.0.1", port))
+            sock.setblocking(False)
+            host = "localhost" if rng.random() < 0.8 else "elsewhere.example"
+            conn = ncm.Conn(loop, sock.detach(), tctx, host, True, False)
+            try:
+                await asyncio.wait_for(conn.handshake(), 5)
+                res = await asyncio.wait_for(conn.send(b"GET /r%d HTTP/1.1\r\nHost: x\r\n\r\n" % i), 5)
+                ok += res[0] == 200
+            except (ssl.SSLError, ConnectionFailed, asyncio.TimeoutError, OSError):
+                pass
+            finally:
+                conn.close()
+        srv.close()
+        await srv.wait_closed()
+        return ok
+
+    handshakes = asyncio.run(run())
+    return built + handshakes
 
 
 def main() -> int:
