@@ -166,3 +166,65 @@ async def test_throttled_operator_creates_the_tick_before_its_status_writes():
         assert metrics.WORKER_RELEASES.value("cron") >= 20
     finally:
         await env.stop()
+
+
+def test_priority_gates_grant_every_live_waiter_in_class_order():
+    """Property: for random arrival sequences of prioritised requests, some cancelled while
+    waiting, both gates grant every live waiter exactly once, FIFO within a class, and never
+    grant a lower class while a higher-class waiter is queued (no aging in this window)."""
+    from hypothesis import given, settings
+    from hypothesis import strategies as st
+
+    ops = st.lists(st.tuples(st.sampled_from([PRIORITY_LOW, PRIORITY_NORMAL, PRIORITY_HIGH]), st.booleans()),
+                   min_size=1, max_size=40)
+
+    async def run(kind, seq):
+        gate = TokenBucket(2000.0, 1, max_defer=60.0) if kind == "bucket" else InflightGate(1)
+        if kind == "bucket":
+            await _drain_bucket(gate)
+        else:
+            await gate.acquire()  # occupy the only slot: everything below queues
+        granted = []
+        queued = {}
+
+        async def req(i, prio):
+            if kind == "bucket":
+                await gate.wait(prio)
+            else:
+                await gate.acquire(prio)
+            # at grant time no live waiter of a higher class may still be queued
+            higher = [j for j, (p, done) in queued.items() if p > prio and not done and j != i]
+            granted.append((i, prio, higher))
+            queued[i] = (prio, True)
+            if kind == "gate":
+                gate.release()
+
+        tasks = []
+        for i, (prio, cancel) in enumerate(seq):
+            queued[i] = (prio, False)
+            tasks.append((asyncio.ensure_future(req(i, prio)), cancel))
+        await asyncio.sleep(0)
+        for t, cancel in tasks:
+            if cancel:
+                t.cancel()
+        for i, (t, cancel) in enumerate(tasks):
+            if cancel:
+                queued[i] = (queued[i][0], True)  # a cancelled waiter no longer blocks anyone
+        if kind == "gate":
+            gate.release()
+        await asyncio.wait_for(asyncio.gather(*(t for t, _ in tasks), return_exceptions=True), 5)
+        live = [i for i, (t, c) in enumerate(tasks) if not t.cancelled()]
+        assert sorted(i for i, _, _ in granted) == live
+        for i, prio, higher in granted:
+            assert not higher, (kind, i, prio, higher)
+        for p in (PRIORITY_LOW, PRIORITY_NORMAL, PRIORITY_HIGH):
+            order = [i for i, q, _ in granted if q == p]
+            assert order == sorted(order), (kind, p, order)
+        assert gate.waiting == 0
+
+    @settings(max_examples=40, deadline=None)
+    @given(ops, st.sampled_from(["bucket", "gate"]))
+    def check(seq, kind):
+        asyncio.run(run(kind, seq))
+
+    check()
