@@ -297,6 +297,11 @@ class Client:
         self._m_verb: Dict[str, Tuple[Dict[str, Any], Any]] = {}  # verb -> ({code: counter}, latency histogram)
         self._m_rl: Dict[str, Any] = {}
         self._observe_gates()
+        # Retry-After retries (429 / 5xx from an apiserver shedding load, client-go rest.Request):
+        # an HTTP transport leaves them to the client, so each attempt is throttled and gated anew
+        self._retries_here = hasattr(transport, "retry_in_client")
+        if self._retries_here:
+            transport.retry_in_client = True  # type: ignore[attr-defined]
 
     def _observe_gates(self) -> None:
         """Scrape-time series of the request gates (``rest_client_requests_in_flight`` /
@@ -371,16 +376,30 @@ class Client:
     async def _do(self, verb: str, gvr: GroupVersionResource, namespace: str = "", name: str = "",
                   subresource: str = "", body: Any = None, params: Optional[Dict[str, Any]] = None,
                   priority: int = PRIORITY_NORMAL) -> Any:
-        if self.limiter is not None:
-            await self._throttle(verb, gvr, namespace, name, subresource, priority)
-        gate = self.inflight
-        if gate is not None:
-            await gate.acquire(priority)
+        attempt = 0
+        while True:
+            if self.limiter is not None:
+                await self._throttle(verb, gvr, namespace, name, subresource, priority)
+            gate = self.inflight
             try:
-                return await self._send(verb, gvr, namespace, name, subresource, body, params)
-            finally:
-                gate.release()
-        return await self._send(verb, gvr, namespace, name, subresource, body, params)
+                if gate is None:
+                    return await self._send(verb, gvr, namespace, name, subresource, body, params)
+                await gate.acquire(priority)
+                try:
+                    return await self._send(verb, gvr, namespace, name, subresource, body, params)
+                finally:
+                    gate.release()
+            except errors.ApiError as e:
+                if not self._retries_here or e.retry_after is None or not (e.code == 429 or e.code >= 500) \
+                        or attempt >= self.transport.max_retries:  # type: ignore[attr-defined]
+                    raise
+                wait, code = max(0, e.retry_after), e.code
+            # client-go: wait out Retry-After, then the retry passes the rate limiter again -- and
+            # here the in-flight gate: no slot is held while the apiserver asks us to back off
+            attempt += 1
+            self.transport.retries += 1  # type: ignore[attr-defined]
+            metrics.REST_RETRIES.labels(str(code), self._METHOD.get(verb, verb.upper()), self.host).inc()
+            await asyncio.sleep(wait)
 
     async def _send(self, verb: str, gvr: GroupVersionResource, namespace: str, name: str, subresource: str,
                     body: Any, params: Optional[Dict[str, Any]]) -> Any:

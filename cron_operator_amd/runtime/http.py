@@ -139,6 +139,9 @@ class HttpTransport(Transport):
         # up to maxRetries (10) times -- how an apiserver under API Priority and Fairness sheds load
         self.max_retries = max_retries
         self.retries = 0
+        # set by a Client that retries itself (Client._do): each retry then goes through the QPS
+        # bucket and the in-flight gate again, and no gate slot is held while Retry-After elapses
+        self.retry_in_client = False
         self.host = config.host.split("://", 1)[-1]
         self._pool_size = pool_size
         self._timeout = timeout
@@ -273,7 +276,8 @@ class HttpTransport(Transport):
                         status, raw, retry_after = await pool.request_full(method, target, data, ctype, accept)
                 except (ConnectionFailed, OSError, asyncio.TimeoutError) as e:
                     raise errors.ApiError(503, "ServiceUnavailable", f"connection error: {e}") from None
-                if retry_after is None or not (status == 429 or status >= 500) or attempt >= self.max_retries:
+                if retry_after is None or not (status == 429 or status >= 500) or attempt >= self.max_retries \
+                        or self.retry_in_client:
                     break
                 attempt += 1
                 self.retries += 1
@@ -286,7 +290,10 @@ class HttpTransport(Transport):
                     err_body: Any = jsonutil.loads(raw)
                 except ValueError:
                     err_body = raw.decode(errors="replace")
-                raise errors.ApiError.from_status(status, err_body)
+                err = errors.ApiError.from_status(status, err_body)
+                if err.retry_after is None and retry_after is not None:
+                    err.retry_after = retry_after  # the Retry-After header (a Status body may omit it)
+                raise err
             if params.get(DISCARD):
                 return None
             if not raw:

@@ -228,3 +228,36 @@ def test_priority_gates_grant_every_live_waiter_in_class_order():
         asyncio.run(run(kind, seq))
 
     check()
+
+
+async def test_retry_after_wait_holds_no_inflight_slot_and_is_throttled_again():
+    """A 429 + Retry-After (an apiserver shedding load under APF): while the client waits it out,
+    its in-flight slot serves other requests, and the retry passes the QPS bucket again
+    (client-go throttles every attempt)."""
+    import time
+
+    from cron_operator_amd.apiserver.http import APIServerApp
+    from cron_operator_amd.runtime.client import Client
+    from cron_operator_amd.runtime.http import HttpTransport
+    from cron_operator_amd.runtime.kubeconfig import RestConfig
+
+    env = TestEnv()
+    app = APIServerApp(env.server)
+    port = await app.start("127.0.0.1", 0)
+    tr = HttpTransport(RestConfig(host=f"http://127.0.0.1:{port}"))
+    client = Client(tr, qps=1000, burst=10, max_inflight=1)
+    try:
+        await env.client.create(CRON_GVR, new_cron("x", NS, "*/1 * * * *", PT_TMPL).to_dict(), NS)
+        env.server.faults.add(verb="list", resource="crons", code=429, reason="TooManyRequests", times=1,
+                              retry_after=1)
+        t0 = time.perf_counter()
+        slow = asyncio.ensure_future(client.list(CRON_GVR, NS))
+        await asyncio.sleep(0.1)  # the LIST got its 429 and is waiting out Retry-After: 1
+        got = await asyncio.wait_for(client.get(CRON_GVR, NS, "x"), 0.5)  # the slot is free meanwhile
+        assert got["metadata"]["name"] == "x" and time.perf_counter() - t0 < 0.9
+        assert len((await slow)["items"]) == 1 and time.perf_counter() - t0 >= 1.0
+        assert tr.retries == 1
+        assert client.limiter.accepted == 3  # LIST, GET, and the LIST's retry
+    finally:
+        await client.close()
+        await app.stop()
