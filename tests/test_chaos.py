@@ -83,11 +83,18 @@ def check_invariants(env, crons, seen, once=True):
             assert prev == uid, f"{jname} was created twice"
 
 
-@pytest.mark.parametrize("mode", ["optimized", "reference"])
+@pytest.mark.parametrize("mode", ["optimized", "optimized-gated", "reference"])
 @pytest.mark.timeout(300)
 async def test_converges_under_faults(mode):
-    opts = ReconcilerOptions() if mode == "optimized" else ReconcilerOptions.reference()
-    env = TestEnv(gc=True)
+    """``optimized-gated``: the operator's client also has a QPS bucket and a tight in-flight cap
+    (4), so released worker slots, request priorities and gate saturation all run under the
+    faults too."""
+    from cron_operator_amd.runtime.ratelimit import InflightGate
+
+    opts = ReconcilerOptions.reference() if mode == "reference" else ReconcilerOptions()
+    env = TestEnv(gc=True, qps=2000 if mode == "optimized-gated" else -1, burst=100)
+    if mode == "optimized-gated":
+        env.client.inflight = InflightGate(4)
     crons = {}
     for i in range(18):
         policy = POLICIES[i % 3]
@@ -97,7 +104,7 @@ async def test_converges_under_faults(mode):
                                        history_limit=HISTORY))
     await env.start_manager(opts, max_concurrent=8)
     await env.settle()
-    inject(env, seed=11 if mode == "optimized" else 12)
+    inject(env, seed={"optimized": 11, "optimized-gated": 13}.get(mode, 12))
     seen = {}
     minutes = 6
     for minute in range(minutes):
@@ -109,7 +116,7 @@ async def test_converges_under_faults(mode):
                 env.server.close_all_watches()  # every informer must relist and resume
             await env.settle(timeout=60)
             if sec % 10 == 0:
-                check_invariants(env, crons, seen, once=mode == "optimized")
+                check_invariants(env, crons, seen, once=mode != "reference")
     # faults stop: everything must converge within a couple of minutes of backoff
     env.server.faults.clear()
     for _ in range(180):
@@ -119,7 +126,7 @@ async def test_converges_under_faults(mode):
     for _ in range(30):
         env.clock.advance(1)
         await env.settle(timeout=60)
-    check_invariants(env, crons, seen, once=mode == "optimized")
+    check_invariants(env, crons, seen, once=mode != "reference")
 
     last_tick = GoTime((env.clock.now_ns() // NANOS) // 60 * 60, 0, UTC)
     for name, policy in crons.items():
