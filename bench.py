@@ -289,8 +289,15 @@ def main() -> int:
                                namespace=f"bench-{tag.replace('_', '-')}-r{rank}", shards=1,
                                apiserver_latency="etcd", tls=True)
             _barrier(dist)
-            dres = run_sync(dcfg)
+            try:
+                dres = run_sync(dcfg)
+            except Exception as e:  # noqa: BLE001 - an extra comparison must not cost the headline line
+                dres = None
+                mine[f"{tag}_error"] = f"{type(e).__name__}: {e}"[:300]
             _barrier(dist)
+            if dres is None:
+                _progress(rank, f"deployment-shaped {mode} failed: {mine[f'{tag}_error']}")
+                continue
             _progress(rank, f"deployment-shaped {mode} done: {dcfg.n_crons * dcfg.steps / dres.elapsed_s:.1f}")
             mine[f"{tag}_elapsed_s"] = dres.elapsed_s
             mine[f"{tag}_fires"] = dcfg.n_crons * dcfg.steps
@@ -368,7 +375,10 @@ def main() -> int:
                 "single_process_apiserver_busy_frac": round(max(r["sp_cpu_api"] / r["sp_elapsed_s"]
                                                                 for r in allr), 3),
             })
-        if "dep_fires" in allr[0] and "dep_ref_fires" in allr[0]:
+        dep_errors = sorted({r[k] for r in allr for k in ("dep_error", "dep_ref_error") if k in r})
+        if dep_errors:
+            out["deployment_error"] = "; ".join(dep_errors)
+        elif all("dep_fires" in r and "dep_ref_fires" in r for r in allr) and allr[0].get("dep_fires"):
             dv = sum(r["dep_fires"] for r in allr) / max(r["dep_elapsed_s"] for r in allr)
             dbv = sum(r["dep_ref_fires"] for r in allr) / max(r["dep_ref_elapsed_s"] for r in allr)
             out.update({
