@@ -9,6 +9,8 @@ IMG_TAG ?= $(patsubst v%,%,$(VERSION))
 IMG ?= $(IMG_REGISTRY)/$(IMG_REPOSITORY):$(IMG_TAG)
 # the MI355X payload image the examples/mi355x Crons run (Dockerfile.payload)
 PAYLOAD_IMG ?= $(IMG_REGISTRY)/cron-operator-amd/cron-operator-mi355x-payload:$(IMG_TAG)
+# the ROCm PyTorch base of the payload image: pin it to the release your nodes' driver supports
+ROCM_PYTORCH_IMAGE ?= rocm/pytorch:latest
 CONTAINER_TOOL ?= docker
 PYTHON ?= python3
 PYTEST_ARGS ?= -q
@@ -112,7 +114,7 @@ docker-push: ## Push the operator image.
 
 .PHONY: docker-build-payload
 docker-build-payload: ## Build the MI355X payload image the examples/mi355x Crons run.
-	$(CONTAINER_TOOL) build -f Dockerfile.payload -t $(PAYLOAD_IMG) .
+	$(CONTAINER_TOOL) build -f Dockerfile.payload --build-arg ROCM_PYTORCH_IMAGE=$(ROCM_PYTORCH_IMAGE) -t $(PAYLOAD_IMG) .
 
 .PHONY: docker-push-payload
 docker-push-payload: ## Push the MI355X payload image.
