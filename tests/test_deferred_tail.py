@@ -196,3 +196,39 @@ async def test_stop_cancels_released_reconciles_and_releases_their_keys():
     assert sum(len(v) for v in env.reconciler.expect.pending.values()) == 3
     env.server.faults.latency.clear()
     await env.stop()
+
+
+@pytest.mark.parametrize("workers", [2, 4])
+async def test_released_slots_halve_tick_to_create_under_write_latency(workers):
+    """The round-3 verdict's done-when, as a CPU test: with every write held 20 ms by the
+    apiserver, the median tick->create of a 40-Cron tick at least halves once reconciles release
+    their worker slot before the writes (``defer_status_write``), at the same requests per fire."""
+    import statistics
+    import time
+
+    async def tick(defer):
+        env = TestEnv()
+        for i in range(40):
+            await env.create_cron(new_cron(f"l{i:02d}", NS, "*/1 * * * *", PT_TMPL))
+        await env.start_manager(ReconcilerOptions(defer_status_write=defer), max_concurrent=workers)
+        await env.settle()
+        lat = []
+        t0 = [0.0]
+        env.reconciler.latency_observer = lambda key, missed, created: lat.append(time.perf_counter() - t0[0])
+        for verb in ("create", "patch", "delete"):
+            env.server.faults.latency[verb] = 0.02
+        try:
+            req0 = env.client.requests
+            t0[0] = time.perf_counter()
+            env.clock.advance(60)
+            await _until(lambda: len(lat) == 40, 10.0)
+            await _until(lambda: env.controller.queue.idle() and env.controller.in_flight() == 0, 10.0)
+            return statistics.median(lat), env.client.requests - req0
+        finally:
+            env.server.faults.latency.clear()
+            await env.stop()
+
+    p50_held, req_held = await tick(False)
+    p50_released, req_released = await tick(True)
+    assert req_released == req_held
+    assert p50_released <= 0.5 * p50_held, (p50_released, p50_held)
