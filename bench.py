@@ -41,6 +41,12 @@ are both algorithms in that shape (one process each, TLS + the harness's ``etcd`
 model), run in this same invocation after the timed run; ``vs_baseline_deployment`` is
 their ratio (``--deployment none`` skips them).
 
+``payload_ddp``: last of all, untimed, when the node has a GPU per rank, rank 0 runs the
+payload the operator schedules (``models/payloads/ddp_train.py``: DDP over RCCL, one process
+per GPU) as a time-limited child job on those GPUs and reports whether its ranks stayed in
+sync and a 256 MB all-reduce's bus bandwidth -- so the driver's N-GPU runs also exercise
+RCCL over xGMI at N ranks (``--payload-probe none`` skips it).
+
 ``vs_baseline``: the reference publishes no numbers, so the denominator
 is the reference *algorithm* (``--mode reference``: live LIST per reconcile, status
 churn, no event filtering) run by this same invocation on the same Crons, after the
@@ -105,6 +111,69 @@ def _spawn_ranks(n: int) -> int:
         shutil.rmtree(rdzv_dir, ignore_errors=True)
     bad = [rc for rc in rcs if rc != 0]
     return bad[0] if bad else 0
+
+
+def _payload_probe(world: int, timeout_s: float, cpu: bool = False, allreduce_mb: int = 256,
+                   steps: int = 20) -> dict:
+    """Untimed, after everything else: the scheduled workload's own data path on this node.
+
+    The operator never touches the GPU; what it schedules does (``examples/mi355x``: a nightly
+    PyTorchJob of one process per GPU, DDP over RCCL/xGMI).  When this node has a GPU per rank,
+    rank 0 launches that payload (``models/payloads/ddp_train.py``) as a CHILD
+    ``torch.distributed.run`` with ``world`` processes, one per GPU, in its own session and under a
+    hard time limit, and reports its result: ranks in sync, the distinct devices used, and the
+    bus bandwidth of a 256 MB bf16 all-reduce.  A failure or timeout is reported, never raised:
+    it must not cost the headline line."""
+    import signal
+    import socket
+    import subprocess
+
+    if not cpu:
+        if not os.path.exists("/dev/kfd"):
+            return {"skipped": "no GPU on this node"}
+        try:
+            import torch
+
+            visible = torch.cuda.device_count()  # counting does not initialise the GPU in this process
+        except Exception as e:  # noqa: BLE001
+            return {"skipped": f"torch: {type(e).__name__}"}
+        if visible < world:
+            return {"skipped": f"{visible} visible GPUs < {world} ranks"}
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    drop = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "GROUP_WORLD_SIZE",
+            "ROLE_RANK", "ROLE_WORLD_SIZE", "ROLE_NAME", "MASTER_ADDR", "MASTER_PORT", "BENCH_RDZV_FILE")
+    env = {k: v for k, v in os.environ.items() if k not in drop and not k.startswith("TORCHELASTIC_")}
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(world),
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           "-m", "cron_operator_amd.models.payloads.ddp_train", "--steps", str(steps),
+           "--allreduce-mb", str(allreduce_mb)] + (["--cpu", "--hidden", "64", "--batch", "4"] if cpu else [])
+    t0 = time.perf_counter()
+    p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                         text=True, start_new_session=True)
+    try:
+        out, _ = p.communicate(timeout=timeout_s)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.communicate()
+        return {"error": f"timed out after {timeout_s:.0f} s", "world": world}
+    res: dict = {"rc": p.returncode, "wall_s": round(time.perf_counter() - t0, 1)}
+    for line in out.splitlines():
+        if line.startswith(("DDP_OK ", "DDP_FAIL ")):
+            tag, _, body = line.partition(" ")
+            try:
+                info = json.loads(body)
+            except ValueError:
+                break
+            res.update({"ok": tag == "DDP_OK" and p.returncode == 0, "world": info.get("world"),
+                        "backend": info.get("backend"), "distinct_devices": len(set(info.get("devices") or [])),
+                        "ddp_steps_per_s": round(info.get("steps_per_s", 0.0), 2),
+                        "allreduce": info.get("allreduce")})
+            return res
+    res["error"] = (out.strip().splitlines() or ["no output"])[-1][:300]
+    return res
 
 
 def _dist():
@@ -194,6 +263,10 @@ def main() -> int:
     ap.add_argument("--deployment-baseline-steps", type=int, default=2)
     ap.add_argument("--baseline-steps", type=int, default=2)
     ap.add_argument("--baseline-warmup", type=int, default=1)
+    ap.add_argument("--payload-probe", choices=["auto", "none"], default="auto",
+                    help="after everything else, when the node has a GPU per rank, run the scheduled DDP "
+                         "payload over RCCL on them (child process, time-limited) and report payload_ddp")
+    ap.add_argument("--payload-timeout", type=float, default=240.0)
     ap.add_argument("--out", default="", help="also write the full result JSON here")
     a = ap.parse_args()
 
@@ -395,6 +468,10 @@ def main() -> int:
                     sum(r["dep_ref_req_per_fire"] for r in allr) / len(allr), 3),
                 "vs_baseline_deployment": round(dv / dbv, 3) if dbv else None,
             })
+        if a.payload_probe == "auto":
+            _progress(rank, f"payload probe: DDP over RCCL on {world} GPU(s), limit {a.payload_timeout:.0f} s")
+            out["payload_ddp"] = _payload_probe(world, a.payload_timeout)
+            _progress(rank, f"payload probe: {out['payload_ddp']}")
         print(json.dumps(out), flush=True)
         if a.out:
             with open(a.out, "w") as fh:

@@ -22,6 +22,31 @@ import sys
 import time
 
 
+def _allreduce_busbw(torch, dist, dev, mb: int, world: int, iters: int = 10, warmup: int = 3) -> dict:
+    """Time ``iters`` all-reduces of one ``mb``-MB bf16 buffer -- the size class of a DDP gradient
+    bucket -- and return the ring bus bandwidth ``2(n-1)/n * bytes / t`` (the per-link figure to
+    hold against xGMI's ~153 GB/s per link), the max over ranks of each rank's mean time."""
+    n = max(1, mb * 1024 * 1024 // 2)
+    buf = torch.ones(n, dtype=torch.bfloat16, device=dev)
+    for _ in range(warmup):
+        dist.all_reduce(buf)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        dist.all_reduce(buf)
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)
+    dt = torch.tensor([(time.perf_counter() - t0) / iters], dtype=torch.float64, device=dev)
+    dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+    t = float(dt.item())
+    nbytes = n * 2
+    return {"mb": mb, "iters": iters, "ms": round(t * 1000, 3),
+            "algbw_gbs": round(nbytes / t / 1e9, 2),
+            "busbw_gbs": round(2 * (world - 1) / world * nbytes / t / 1e9, 2) if world > 1 else None}
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
@@ -30,6 +55,9 @@ def main(argv=None) -> int:
     ap.add_argument("--layers", type=int, default=4)
     ap.add_argument("--bucket-mb", type=int, default=100)
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--allreduce-mb", type=int, default=0,
+                    help="after training, time an all-reduce of this many MB of bf16 and report its bus "
+                         "bandwidth (0: skip)")
     a = ap.parse_args(argv)
 
     import torch
@@ -81,11 +109,13 @@ def main(argv=None) -> int:
         ident = f"cpu:{rank}"
     devices = [None] * world
     dist.all_gather_object(devices, ident)
+    allreduce = _allreduce_busbw(torch, dist, dev, a.allreduce_mb, world) if a.allreduce_mb > 0 else None
     if rank == 0:
         print("DDP_OK " if in_sync else "DDP_FAIL ", json.dumps({
             "world": world, "backend": dist.get_backend(), "device": str(dev), "devices": devices,
             "visible_devices": torch.cuda.device_count() if use_gpu else 0, "loss": float(loss.detach()),
-            "steps_per_s": a.steps / dt, "samples_per_s": a.steps * a.batch * world / dt}), flush=True)
+            "steps_per_s": a.steps / dt, "samples_per_s": a.steps * a.batch * world / dt,
+            "allreduce": allreduce}), flush=True)
     dist.destroy_process_group()
     return 0 if in_sync else 1
 

@@ -56,6 +56,8 @@ def test_single_rank_line():
         < 0.01 * d["vs_baseline_deployment"] + 0.002
     assert d["deployment_baseline_api_requests_per_fire"] > d["deployment_api_requests_per_fire"]
     assert d["deployment_p50_ms"] > 0 and d["deployment_baseline_p50_ms"] > 0
+    # the scheduled payload's RCCL probe runs only where every rank has a GPU (not in this container)
+    assert "payload_ddp" in d and ("skipped" in d["payload_ddp"] or d["payload_ddp"].get("ok") is True)
 
 
 def test_recorded_baseline_option():
@@ -112,3 +114,22 @@ def test_two_ranks_aggregate():
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json_line(r.stdout)  # rank 0 only
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 40 and d["config"]["parallelism"] == "ranks2x3shards"
+
+
+def test_payload_probe_runs_the_ddp_payload_as_a_clean_child_job(monkeypatch):
+    """The probe a rank-0 of a launched bench starts: a child ``torch.distributed.run`` of the DDP
+    payload that must not inherit the bench's own rendezvous (RANK/WORLD_SIZE/MASTER_PORT/
+    TORCHELASTIC_* of the outer launcher).  On CPU (``cpu=True``: gloo) it trains in sync on 2
+    ranks and reports the all-reduce bus bandwidth; a time limit is reported, not raised."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    for k, v in {"RANK": "0", "LOCAL_RANK": "0", "WORLD_SIZE": "8", "MASTER_PORT": "1", "MASTER_ADDR": "10.9.9.9",
+                 "TORCHELASTIC_RUN_ID": "outer", "PYTHONPATH": _env()["PYTHONPATH"]}.items():
+        monkeypatch.setenv(k, v)
+    r = bench._payload_probe(2, 150, cpu=True, allreduce_mb=1, steps=2)
+    assert r.get("ok") is True, r
+    assert r["world"] == 2 and r["backend"] == "gloo" and r["distinct_devices"] == 2
+    assert r["allreduce"]["mb"] == 1 and r["allreduce"]["busbw_gbs"] > 0
+    slow = bench._payload_probe(2, 0.5, cpu=True, allreduce_mb=1, steps=2)
+    assert slow.get("error", "").startswith("timed out"), slow
