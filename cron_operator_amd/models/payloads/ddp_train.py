@@ -116,6 +116,9 @@ def main(argv=None) -> int:
             "visible_devices": torch.cuda.device_count() if use_gpu else 0, "loss": float(loss.detach()),
             "steps_per_s": a.steps / dt, "samples_per_s": a.steps * a.batch * world / dt,
             "allreduce": allreduce}), flush=True)
+    # every rank leaves its last collective before any rank tears its connections down: a gloo
+    # peer that closes while another still reads from it can abort that rank (SIGABRT) at exit
+    dist.barrier()
     dist.destroy_process_group()
     return 0 if in_sync else 1
 
