@@ -44,7 +44,7 @@ def _allreduce_busbw(torch, dist, dev, mb: int, world: int, iters: int = 10, war
     nbytes = n * 2
     return {"mb": mb, "iters": iters, "ms": round(t * 1000, 3),
             "algbw_gbs": round(nbytes / t / 1e9, 2),
-            "busbw_gbs": round(2 * (world - 1) / world * nbytes / t / 1e9, 2) if world > 1 else None}
+            "busbw_gbs": round(2 * (world - 1) / world * nbytes / t / 1e9, 2)}
 
 
 def main(argv=None) -> int:
@@ -109,7 +109,10 @@ def main(argv=None) -> int:
         ident = f"cpu:{rank}"
     devices = [None] * world
     dist.all_gather_object(devices, ident)
-    allreduce = _allreduce_busbw(torch, dist, dev, a.allreduce_mb, world) if a.allreduce_mb > 0 else None
+    allreduce = None
+    if a.allreduce_mb > 0:  # one rank has no peer to exchange with: its "all-reduce" moves nothing
+        allreduce = (_allreduce_busbw(torch, dist, dev, a.allreduce_mb, world) if world > 1
+                     else {"mb": a.allreduce_mb, "skipped": "world 1: no peers"})
     if rank == 0:
         print("DDP_OK " if in_sync else "DDP_FAIL ", json.dumps({
             "world": world, "backend": dist.get_backend(), "device": str(dev), "devices": devices,
