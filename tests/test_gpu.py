@@ -8,7 +8,7 @@ operator process ran on its native components:
 * the full scheduled-training scenario (Cron -> PyTorchJob -> payload on the
   GPU -> history ``Succeeded``);
 * a 1-rank RCCL DDP payload run (``backend=nccl`` is RCCL on ROCm);
-* a short headline-bench run on the box (native engine loaded).
+* a short headline-bench run on the box (native engine loaded, its payload probe over RCCL).
 """
 from __future__ import annotations
 
@@ -138,3 +138,6 @@ def test_headline_bench_short_run():
     res = json.loads(out.stdout.strip().splitlines()[-1])
     assert res["value"] > 0 and res["cron_engine"] == "native"
     assert res["baseline_source"].startswith("measured") and res["vs_baseline"] > 1
+    # the untimed payload probe ran the scheduled DDP payload over RCCL on this box's GPU
+    probe = res["payload_ddp"]
+    assert probe.get("ok") is True and probe["backend"] == "nccl" and probe["world"] == 1, probe
