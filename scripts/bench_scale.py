@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Scaling curve: the headline bench at 1 / 10 / 100 / 1000 Cron CRs.
+"""Scaling curve: the headline bench at 1 / 10 / 100 / 1000 Cron CRs (``--sizes``; 10000 for
+the large-fleet row).
 
 BASELINE.json asks for reconciles/sec and tick->create latency "at 1, 10, 100
 and 1000 concurrent Cron CRs with the scaling curve reported".  This runs
@@ -12,6 +13,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import resource
 import sys
 import time
 
@@ -49,12 +51,17 @@ def main() -> int:
                          "apiserver_cpu_ms_per_fire": r.cpu_s_apiserver * 1000 / (n * steps),
                          "operator_gc": r.operator_gc, "phase_ms": r.phase_ms,
                          # peak RSS of each operator shard process (sharded runs only)
-                         "operator_maxrss_mib": r.operator_maxrss_mib})
+                         "operator_maxrss_mib": r.operator_maxrss_mib,
+                         # one process: the operator runs in this process (with the harness's own
+                         # bookkeeping; the apiserver is another process): an upper bound, cumulative
+                         "this_process_peak_rss_mib": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+                                                            / 1024, 1)})
             print(f"{mode:>9} n={n:>5}: {r.cron_reconciles_per_s:9.1f} cron-reconciles/s  "
                   f"p50 {r.p50_latency_ms:8.1f} ms  p99 {r.p99_latency_ms:8.1f} ms  "
                   f"{r.api_requests_per_fire:.1f} req/fire  operator {r.cpu_s_operator * 1000 / (n * steps):.3f} "
                   f"ms CPU/fire, apiserver {r.cpu_s_apiserver * 1000 / (n * steps):.3f}, GC {r.operator_gc}"
-                  + (f", shard peak RSS {r.operator_maxrss_mib} MiB" if r.operator_maxrss_mib else ""),
+                  + (f", shard peak RSS {r.operator_maxrss_mib} MiB" if r.operator_maxrss_mib else
+                     f", process peak RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024:.0f} MiB"),
                   flush=True)
     print()
     print("| mode | Crons | cron-reconciles/s | p50 tick→create ms | p99 ms | ms/tick | API req/fire "

@@ -7,6 +7,7 @@
 #   soak    80 ticks, 3 shards (peak RSS per shard, no drift)
 #   baseline all five BASELINE.json configs in both reconciler modes (scripts/baseline_configs.py)
 #   scale   cron-reconciles/s at 1 / 10 / 100 / 1000 Crons, both modes (scripts/bench_scale.py)
+#   scale10k  10000 Crons, this operator only: one process and 3 shards (peak RSS)
 #   ranks   the driver's multi-rank line (torch.distributed.run, N=2 and 4 CPU-only ranks): the
 #           N=8 scaling run is the driver's; RANKS overrides the list
 # Stops at the first failure; every GPU step has its own time limit.
@@ -62,6 +63,14 @@ for s in $STEPS; do
       timeout -k 10 900 python -u scripts/bench_scale.py --steps 3 --warmup 1 --out "$OUT/scale.json" \
         > "$OUT/scale.log" 2>&1
       check $? scale; tail -12 "$OUT/scale.log" ;;
+    scale10k)
+      step scale10k
+      timeout -k 10 900 python -u scripts/bench_scale.py --sizes 10000 --modes optimized --steps 3 --warmup 1 \
+        --out "$OUT/scale10k.json" > "$OUT/scale10k.log" 2>&1
+      check $? scale10k; tail -4 "$OUT/scale10k.log"
+      timeout -k 10 900 python -u scripts/bench_scale.py --sizes 10000 --modes optimized --steps 3 --warmup 1 \
+        --shards 3 --out "$OUT/scale10k_3shards.json" > "$OUT/scale10k_3shards.log" 2>&1
+      check $? scale10k_3shards; tail -4 "$OUT/scale10k_3shards.log" ;;
     ranks)
       for n in ${RANKS:-2 4}; do
         step "ranks $n"
