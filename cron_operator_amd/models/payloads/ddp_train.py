@@ -50,6 +50,8 @@ def _allreduce_busbw(torch, dist, dev, mb: int, world: int, iters: int = 10, war
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed steps first (kernel selection, RCCL setup); default 3 on GPUs, 0 on CPU")
     ap.add_argument("--batch", type=int, default=32, help="per-rank batch")
     ap.add_argument("--hidden", type=int, default=1024)
     ap.add_argument("--layers", type=int, default=4)
@@ -85,14 +87,22 @@ def main(argv=None) -> int:
     gen = torch.Generator(device="cpu").manual_seed(rank)
     x = torch.randn(a.batch, a.hidden, generator=gen).to(dev)
     y = torch.randn(a.batch, a.hidden, generator=gen).to(dev)
-    t0 = time.perf_counter()
-    loss = None
-    for _ in range(a.steps):
+    def step():
         with torch.autocast(device_type=dev.type, dtype=torch.bfloat16, enabled=use_gpu):
-            loss = torch.nn.functional.mse_loss(ddp(x).float(), y)
+            out = torch.nn.functional.mse_loss(ddp(x).float(), y)
         opt.zero_grad(set_to_none=True)
-        loss.backward()
+        out.backward()
         opt.step()
+        return out
+
+    loss = None
+    for _ in range(a.warmup if a.warmup is not None else (3 if use_gpu else 0)):
+        loss = step()
+    if use_gpu:
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = step()
     if use_gpu:
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
