@@ -60,10 +60,10 @@ def _version(name: str, status: Dict[str, Any], storage: bool) -> Dict[str, Any]
                 "status": status}}}}
 
 
-def _crd(plural: str, kind: str, versions: List[Dict[str, Any]]) -> Dict[str, Any]:
+def _crd(plural: str, kind: str, versions: List[Dict[str, Any]], group: str = KUBEFLOW_GROUP) -> Dict[str, Any]:
     return {"apiVersion": "apiextensions.k8s.io/v1", "kind": "CustomResourceDefinition",
-            "metadata": {"name": f"{plural}.{KUBEFLOW_GROUP}"},
-            "spec": {"group": KUBEFLOW_GROUP, "scope": "Namespaced",
+            "metadata": {"name": f"{plural}.{group}"},
+            "spec": {"group": group, "scope": "Namespaced",
                      "names": {"kind": kind, "listKind": kind + "List", "plural": plural,
                                "singular": kind.lower()},
                      "versions": versions}}
@@ -83,3 +83,9 @@ def kubeflow_crds() -> List[Dict[str, Any]]:
     out.append(_crd("mpijobs", "MPIJob", [_version("v1alpha1", mpi_v1alpha1_status_schema(), False),
                                           _version("v1", job_status_schema(), True)]))
     return out
+
+
+def job_crd(group: str, version: str, plural: str, kind: str) -> Dict[str, Any]:
+    """A job kind of another operator with the kubeflow JobStatus shape -- e.g. KubeDL's
+    ``xdl.kubedl.io`` XDLJob, which the reference chart's ClusterRole grants."""
+    return _crd(plural, kind, [_version(version, job_status_schema(), True)], group)

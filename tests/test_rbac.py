@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import asyncio
 import os
+from typing import Any, Dict, Optional
 
 import pytest
 import yaml
@@ -151,7 +152,9 @@ def _apply(srv: APIServer, objs):
         srv.create(gvr, ns, o)
 
 
-async def _operator_fires_under(srv: APIServer, clock: FakeClock, lease_ns: str) -> None:
+async def _operator_fires_under(srv: APIServer, clock: FakeClock, lease_ns: str,
+                                workload: Optional[Dict[str, Any]] = None,
+                                gvr: GroupVersionResource = PT) -> None:
     app = APIServerApp(srv)
     port = await app.start("127.0.0.1", 0)
     admin = Client(HttpTransport(RestConfig(host=f"http://127.0.0.1:{port}", bearer_token="admin")), qps=-1)
@@ -166,8 +169,8 @@ async def _operator_fires_under(srv: APIServer, clock: FakeClock, lease_ns: str)
         cron = {"apiVersion": "apps.kubedl.io/v1alpha1", "kind": "Cron",
                 "metadata": {"name": "rbac", "namespace": "default"},
                 "spec": {"schedule": "* * * * *", "concurrencyPolicy": "Replace", "historyLimit": 0,
-                         "template": {"workload": {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
-                                                   "spec": {"pytorchReplicaSpecs": {}}}}}}
+                         "template": {"workload": workload or {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+                                                               "spec": {"pytorchReplicaSpecs": {}}}}}}
         await admin.create(CRON_GVR, cron, "default")
 
         async def advance(seconds: int) -> None:
@@ -178,7 +181,7 @@ async def _operator_fires_under(srv: APIServer, clock: FakeClock, lease_ns: str)
 
         await advance(60)
         for _ in range(400):
-            items = (await admin.list(PT, "default", label_selector=f"{LABEL_CRON_NAME}=rbac"))["items"]
+            items = (await admin.list(gvr, "default", label_selector=f"{LABEL_CRON_NAME}=rbac"))["items"]
             if items:
                 break
             await asyncio.sleep(0.01)
@@ -188,7 +191,7 @@ async def _operator_fires_under(srv: APIServer, clock: FakeClock, lease_ns: str)
         await advance(60)
         for _ in range(400):
             names = [o["metadata"]["name"] for o in
-                     (await admin.list(PT, "default", label_selector=f"{LABEL_CRON_NAME}=rbac"))["items"]]
+                     (await admin.list(gvr, "default", label_selector=f"{LABEL_CRON_NAME}=rbac"))["items"]]
             if names and first not in names:
                 break
             await asyncio.sleep(0.01)
@@ -227,6 +230,29 @@ async def test_helm_install_rbac_suffices():
     srv.create_namespace("cron-operator")
     _apply(srv, objs)
     await _operator_fires_under(srv, clock, "cron-operator")
+
+
+async def test_helm_install_rbac_covers_the_reference_charts_other_job_groups():
+    """The reference chart grants KubeDL's ``xdl.kubedl.io`` XDLJob (``charts/cron-operator/
+    templates/cluster_role.yaml:89-106``): a Cron templating one fires and replaces it under
+    this chart's RBAC alone."""
+    from cron_operator_amd.trainingop.crds import job_crd
+
+    docs = render_chart(os.path.join(ROOT, "charts", "cron-operator"), {}, release="cron-operator",
+                        namespace="cron-operator")
+    objs = [o for lst in docs.values() for o in lst]
+    sa = next(o for o in objs if o["kind"] == "ServiceAccount")
+    for o in objs:
+        if o["kind"] not in ("ClusterRole", "ClusterRoleBinding"):
+            o.setdefault("metadata", {}).setdefault("namespace", "cron-operator")
+    clock, srv = _server("cron-operator", sa["metadata"]["name"])
+    srv.install_crd(job_crd("xdl.kubedl.io", "v1alpha1", "xdljobs", "XDLJob"))
+    srv.create_namespace("cron-operator")
+    _apply(srv, objs)
+    await _operator_fires_under(srv, clock, "cron-operator",
+                                workload={"apiVersion": "xdl.kubedl.io/v1alpha1", "kind": "XDLJob",
+                                          "spec": {"xdlReplicaSpecs": {}}},
+                                gvr=GroupVersionResource("xdl.kubedl.io", "v1alpha1", "xdljobs"))
 
 
 async def test_operator_denied_without_binding():

@@ -121,3 +121,26 @@ async def test_mi355x_examples_are_valid_kubeflow_jobs_under_reference_crds():
         assert any(h["status"] == "Succeeded" for h in st.get("history") or []), (name, st)
     await trainer.stop()
     await env.stop()
+
+
+def test_chart_rbac_grants_every_rule_of_the_reference_chart():
+    """A Cron whose template names any kind the reference's Helm ClusterRole grants
+    (``charts/cron-operator/templates/cluster_role.yaml``: kubeflow.org jobs, KubeDL's XDLJob,
+    the xgboost-operator's XGBoostJob, events, leases, Crons) is creatable by this chart's
+    operator too, so a switch-over keeps every working Cron working.  Child ``/status``
+    subresources are read only here (the reference grants ``update`` it never uses)."""
+    from cron_operator_amd.controller.rbac import RULES
+
+    with open(os.path.join(REF, "charts", "cron-operator", "templates", "cluster_role.yaml")) as fh:
+        ref_rules = yaml.safe_load(fh.read().split("\nrules:\n", 1)[1])
+    granted = {(g, r, v) for rule in RULES for g in rule["apiGroups"] for r in rule["resources"]
+               for v in rule["verbs"]}
+    missing = []
+    for rule in ref_rules:
+        for g in rule["apiGroups"]:
+            for r in rule["resources"]:
+                child_status = r.endswith("/status") and not r.startswith("crons")
+                for v in (["get"] if child_status else rule["verbs"]):
+                    if (g, r, v) not in granted:
+                        missing.append((g, r, v))
+    assert not missing, missing
