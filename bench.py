@@ -377,6 +377,14 @@ def main() -> int:
             mine[f"{tag}_p50"] = dres.p50_latency_ms
             mine[f"{tag}_p99"] = dres.p99_latency_ms
             mine[f"{tag}_req_per_fire"] = dres.api_requests_per_fire
+    # the scheduled payload over RCCL on this node's GPUs (untimed, last): rank 0 runs it while
+    # the other ranks wait at the barrier, so no rank tears its process group down early
+    probe = None
+    if a.payload_probe == "auto" and rank == 0:
+        _progress(rank, f"payload probe: DDP over RCCL on {world} GPU(s), limit {a.payload_timeout:.0f} s")
+        probe = _payload_probe(world, a.payload_timeout)
+        _progress(rank, f"payload probe: {probe}")
+    _barrier(dist)
     if dist is not None:
         allr = [None] * world
         dist.all_gather_object(allr, mine)
@@ -468,15 +476,16 @@ def main() -> int:
                     sum(r["dep_ref_req_per_fire"] for r in allr) / len(allr), 3),
                 "vs_baseline_deployment": round(dv / dbv, 3) if dbv else None,
             })
-        if a.payload_probe == "auto":
-            _progress(rank, f"payload probe: DDP over RCCL on {world} GPU(s), limit {a.payload_timeout:.0f} s")
-            out["payload_ddp"] = _payload_probe(world, a.payload_timeout)
-            _progress(rank, f"payload probe: {out['payload_ddp']}")
+        if probe is not None:
+            out["payload_ddp"] = probe
         print(json.dumps(out), flush=True)
         if a.out:
             with open(a.out, "w") as fh:
                 json.dump({"summary": out, "rank0": res.to_dict()}, fh, indent=1)
     if dist is not None:
+        # every rank is past its last collective (and rank 0 has printed) before any rank tears
+        # its gloo connections down: a peer closing early can abort a rank still reading
+        dist.barrier()
         dist.destroy_process_group()
     return 0
 
