@@ -2,8 +2,8 @@
 # One gpurun call: paired A/B of the 1-process 1000-Cron bench on the box.  ab_base/ holds an
 # older tree (git archive <rev> | tar -x -C ab_base; git-ignored, shipped with the snapshot).
 # ARMS lists the arms run in turn each round: "base", "head", "head:VAR=value" (head with an
-# environment override, e.g. head:CRON_OPERATOR_NATIVE_HTTP=python) or "head@--arg=v,--flag"
-# (head with extra bench.py arguments, comma-separated).
+# environment override, e.g. head:CRON_OPERATOR_NATIVE_HTTP=python) or "head@--arg=v,--flag" /
+# "base@--arg=v" (that tree with extra bench.py arguments, comma-separated).
 #   TAG=r3b ROUNDS=4 ARMS="base head:CRON_OPERATOR_NATIVE_HTTP=python head" bash scripts/gpu_ab.sh
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -14,7 +14,7 @@ ARMS=${ARMS:-base head}
 OUT=$PWD/gpurun_out/$TAG
 mkdir -p "$OUT"
 for d in ab_base .; do
-  [ "$d" = ab_base ] && [[ " $ARMS " != *" base "* ]] && continue
+  [ "$d" = ab_base ] && [[ " $ARMS " != *" base "* && " $ARMS " != *" base@"* ]] && continue
   (cd "$d" && timeout -k 10 300 python -m cron_operator_amd.ops.build > "$OUT/build_$(basename "$(realpath "$d")").log" 2>&1) || exit $?
 done
 for i in $(seq "$ROUNDS"); do
@@ -22,12 +22,13 @@ for i in $(seq "$ROUNDS"); do
     d=.; envs=(); extra=()
     case "$arm" in
       base) d=ab_base ;;
+      base@*) d=ab_base; IFS=, read -r -a extra <<< "${arm#base@}" ;;
       head:*) envs=("${arm#head:}") ;;
       head@*) IFS=, read -r -a extra <<< "${arm#head@}" ;;
     esac
     name=$(echo "$arm" | tr ':=@,' '____' | tr -d '-')
     (cd "$d" && env "${envs[@]}" PYTHONPATH=$PWD timeout -k 10 300 python bench.py --shards ${SHARDS:-1} --steps 10 \
-        --warmup 3 --baseline none --single-process none $([ "$d" = . ] && echo --deployment none) "${extra[@]}" \
+        --warmup 3 --baseline none --single-process none $([ "$d" = . ] && echo --deployment none --payload-probe none) "${extra[@]}" \
         > "$OUT/${name}_$i.log" 2>&1)
     rc=$?; [ $rc -eq 0 ] || { echo "$name round $i rc=$rc"; exit $rc; }
     python - "$OUT/${name}_$i.log" "$name" "$i" <<'PY'
