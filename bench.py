@@ -263,9 +263,10 @@ def main() -> int:
     ap.add_argument("--deployment-baseline-steps", type=int, default=2)
     ap.add_argument("--baseline-steps", type=int, default=2)
     ap.add_argument("--baseline-warmup", type=int, default=1)
-    ap.add_argument("--payload-probe", choices=["auto", "none"], default="auto",
+    ap.add_argument("--payload-probe", choices=["auto", "cpu", "none"], default="auto",
                     help="after everything else, when the node has a GPU per rank, run the scheduled DDP "
-                         "payload over RCCL on them (child process, time-limited) and report payload_ddp")
+                         "payload over RCCL on them (child process, time-limited) and report payload_ddp; "
+                         "'cpu' runs it over gloo on the CPU (a rehearsal of the multi-rank path)")
     ap.add_argument("--payload-timeout", type=float, default=240.0)
     ap.add_argument("--out", default="", help="also write the full result JSON here")
     a = ap.parse_args()
@@ -380,9 +381,12 @@ def main() -> int:
     # the scheduled payload over RCCL on this node's GPUs (untimed, last): rank 0 runs it while
     # the other ranks wait at the barrier, so no rank tears its process group down early
     probe = None
-    if a.payload_probe == "auto" and rank == 0:
-        _progress(rank, f"payload probe: DDP over RCCL on {world} GPU(s), limit {a.payload_timeout:.0f} s")
-        probe = _payload_probe(world, a.payload_timeout)
+    if a.payload_probe != "none" and rank == 0:
+        cpu = a.payload_probe == "cpu"
+        _progress(rank, f"payload probe: DDP over {'gloo on the CPU' if cpu else f'RCCL on {world} GPU(s)'}, "
+                        f"limit {a.payload_timeout:.0f} s")
+        probe = (_payload_probe(world, a.payload_timeout, cpu=True, allreduce_mb=4, steps=2) if cpu
+                 else _payload_probe(world, a.payload_timeout))
         _progress(rank, f"payload probe: {probe}")
     _barrier(dist)
     if dist is not None:

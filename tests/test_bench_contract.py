@@ -104,16 +104,21 @@ def test_gpus_mismatching_world_size_is_refused():
 
 
 def test_two_ranks_aggregate():
+    """The driver's launcher, 2 ranks; the payload probe rehearsed over gloo (``--payload-probe
+    cpu``): rank 0 runs a 2-process DDP child job while rank 1 waits at the barrier, and both
+    tear down together after the line is printed."""
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
-                        "--steps", "2", "--warmup", "1", "--crons", "20"], cwd=ROOT, env=_env(),
-                       capture_output=True, text=True, timeout=600)
+                        "--steps", "2", "--warmup", "1", "--crons", "20", "--payload-probe", "cpu"], cwd=ROOT,
+                       env=_env(), capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     d = _json_line(r.stdout)  # rank 0 only
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 40 and d["config"]["parallelism"] == "ranks2x3shards"
+    probe = d["payload_ddp"]
+    assert probe.get("ok") is True and probe["world"] == 2 and probe["backend"] == "gloo", probe
 
 
 def test_payload_probe_runs_the_ddp_payload_as_a_clean_child_job(monkeypatch):
