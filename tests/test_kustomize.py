@@ -290,3 +290,28 @@ def test_reference_config_tree_builds_with_this_renderer():
     assert args[0] == "--metrics-bind-address=:8443" and "start" in args and "--leader-elect" in args
     ns = build_parser().parse_args(cobra_order(args))
     assert ns.metrics_bind_address == ":8443" and ns.leader_elect
+
+
+def test_alert_rules_use_metrics_the_operator_exports():
+    """``deploy/kustomize/prometheus/rules.yaml``: every series an alert expression reads is one
+    this operator registers (a renamed metric would leave an alert silently never firing), and
+    the Lease name is the operator's."""
+    import re
+
+    import cron_operator_amd.runtime.metrics as m
+    from cron_operator_amd.runtime.manager import DEFAULT_LEADER_ELECTION_ID as LEADER_ELECTION_ID
+
+    objs = build(os.path.join(ROOT, "deploy", "kustomize", "prometheus"))
+    (rule,) = [o for o in objs if o["kind"] == "PrometheusRule"]
+    exported = set(m.REGISTRY._names)
+    alerts = [r for g in rule["spec"]["groups"] for r in g["rules"]]
+    assert {a["alert"] for a in alerts} >= {"CronOperatorMissedTicks", "CronOperatorClientThrottled",
+                                           "CronOperatorNoLeader"}
+    promql = {"sum", "rate", "increase", "max", "by", "le", "histogram_quantile"}
+    for a in alerts:
+        names = {n for n in re.findall(r"[a-z_][a-z0-9_]*(?=[\[{(\s]|$)", a["expr"]) if n not in promql}
+        names = {re.sub(r"_(bucket|sum|count)$", "", n) if n.endswith(("_bucket", "_sum", "_count")) and
+                 re.sub(r"_(bucket|sum|count)$", "", n) in exported else n for n in names}
+        assert names and names <= exported, (a["alert"], names - exported)
+        assert a["labels"]["severity"] in ("warning", "critical") and a["annotations"]["summary"]
+    assert LEADER_ELECTION_ID in next(a["expr"] for a in alerts if a["alert"] == "CronOperatorNoLeader")
