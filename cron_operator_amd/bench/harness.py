@@ -139,6 +139,10 @@ class BenchResult:
     operator_maxrss_mib: List[float] = field(default_factory=list)
     # cyclic-GC collections per generation and pause time in the operator process(es), timed region
     operator_gc: Dict[str, Any] = field(default_factory=dict)
+    # one process: a starting (or newly elected) operator over the seeded cluster -- seconds from
+    # Manager.start() to synced caches, and to the first pass over every Cron done (the queue idle)
+    startup_sync_s: float = 0.0
+    startup_first_pass_s: float = 0.0
 
     def to_dict(self) -> Dict[str, Any]:
         return asdict(self)
@@ -432,8 +436,10 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
                                              health_probe_bind_address="0", metrics_bind_address="0",
                                              namespace=cfg.namespace))
         ctrl, rec = await setup_with_manager(mgr, opts)
+        t_start0 = time.perf_counter()
         mgr_task = asyncio.get_running_loop().create_task(mgr.start())
         await asyncio.wait_for(mgr.started.wait(), 120)
+        startup_sync_s = time.perf_counter() - t_start0
         cron_inf = rec.cron_informer
         assert cron_inf is not None
 
@@ -472,7 +478,8 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
                     return
                 await asyncio.sleep(0.002)
 
-        await ctrl.wait_idle(timeout=120)
+        await ctrl.wait_idle(timeout=600)
+        startup_first_pass_s = time.perf_counter() - t_start0
 
         # ---------------------------------------------------------------- steps
         total = cfg.warmup + cfg.steps
@@ -537,7 +544,8 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
             api_requests_per_fire=requests / fires, api_requests_by_verb=by_verb,
             reconciles_per_fire=reconciles / fires, step_ms=step_ms, phase_ms=phase_ms,
             engine=default_engine().name, fastjson_native=jsonutil.NATIVE,
-            cpu_s_operator=cpu1[0] - cpu0[0], cpu_s_apiserver=cpu1[1] - cpu0[1], operator_gc=gc_stats)
+            cpu_s_operator=cpu1[0] - cpu0[0], cpu_s_apiserver=cpu1[1] - cpu0[1], operator_gc=gc_stats,
+            startup_sync_s=startup_sync_s, startup_first_pass_s=startup_first_pass_s)
         mgr.stop()
         try:
             await asyncio.wait_for(mgr_task, 30)

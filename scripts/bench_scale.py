@@ -52,6 +52,8 @@ def main() -> int:
                          "operator_gc": r.operator_gc, "phase_ms": r.phase_ms,
                          # peak RSS of each operator shard process (sharded runs only)
                          "operator_maxrss_mib": r.operator_maxrss_mib,
+                         # one process: start (or fail-over) over the seeded cluster
+                         "startup_sync_s": r.startup_sync_s, "startup_first_pass_s": r.startup_first_pass_s,
                          # one process: the operator runs in this process (with the harness's own
                          # bookkeeping; the apiserver is another process): an upper bound, cumulative
                          "this_process_peak_rss_mib": round(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
@@ -61,7 +63,8 @@ def main() -> int:
                   f"{r.api_requests_per_fire:.1f} req/fire  operator {r.cpu_s_operator * 1000 / (n * steps):.3f} "
                   f"ms CPU/fire, apiserver {r.cpu_s_apiserver * 1000 / (n * steps):.3f}, GC {r.operator_gc}"
                   + (f", shard peak RSS {r.operator_maxrss_mib} MiB" if r.operator_maxrss_mib else
-                     f", process peak RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024:.0f} MiB"),
+                     f", process peak RSS {resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024:.0f} MiB, "
+                     f"start: caches synced {r.startup_sync_s:.2f} s, first pass {r.startup_first_pass_s:.2f} s"),
                   flush=True)
     print()
     print("| mode | Crons | cron-reconciles/s | p50 tick→create ms | p99 ms | ms/tick | API req/fire "
