@@ -40,7 +40,8 @@ class TemplateError(Exception):
 # --------------------------------------------------------------------------- lexing
 
 
-_ACTION = re.compile(r"\{\{(-\s)?(.*?)(\s-)?\}\}", re.S)
+# an action ends at the first "}}" outside a string literal ({{ "}}" }} prints "}}", as in Go)
+_ACTION = re.compile(r"\{\{(-\s)?((?:\"(?:[^\"\\]|\\.)*\"|`[^`]*`|.)*?)(\s-)?\}\}", re.S)
 
 
 def _split(src: str) -> List[Tuple[str, str]]:

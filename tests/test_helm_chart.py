@@ -245,3 +245,35 @@ def test_reference_helm_unittest_suites_pass_against_this_chart(tmp_path):
     passed, failed, results = run_all(str(chart))
     assert failed == 0, [(r.suite, r.name, r.failures) for r in results if not r.passed]
     assert passed >= 20
+
+
+def test_monitoring_objects_are_off_by_default_and_match_the_kustomize_ones():
+    """``metrics.serviceMonitor`` / ``metrics.prometheusRule`` (new): nothing by default (the
+    reference chart has neither); enabled, the ServiceMonitor scrapes the metrics Service's
+    port and the PrometheusRule carries exactly the alerts of
+    ``deploy/kustomize/prometheus/rules.yaml``, with Prometheus's ``{{ $value }}`` left for
+    Prometheus to expand."""
+    import yaml
+
+    kinds = {o["kind"] for lst in render_chart(CHART, {}).values() for o in lst}
+    assert not kinds & {"ServiceMonitor", "PrometheusRule"}
+    docs = render_chart(CHART, {"metrics": {"serviceMonitor": {"enabled": True, "labels": {"release": "kp"}},
+                                            "prometheusRule": {"enabled": True}}})
+    objs = {o["kind"]: o for lst in docs.values() for o in lst}
+    sm = objs["ServiceMonitor"]
+    svc = objs["Service"]
+    assert sm["metadata"]["labels"]["release"] == "kp"
+    assert sm["spec"]["selector"]["matchLabels"].items() <= svc["metadata"]["labels"].items()
+    assert sm["spec"]["endpoints"][0]["port"] == svc["spec"]["ports"][0]["name"] == "metrics"
+    with open(os.path.join(os.path.dirname(os.path.dirname(CHART)), "deploy", "kustomize", "prometheus",
+                           "rules.yaml")) as fh:
+        want = yaml.safe_load(fh)["spec"]
+    assert objs["PrometheusRule"]["spec"] == want
+    assert "{{ $value }}" in objs["PrometheusRule"]["spec"]["groups"][0]["rules"][0]["annotations"]["description"]
+
+
+def test_action_ends_outside_string_literals():
+    """Go's lexer: ``}}`` inside a quoted string does not end the action."""
+    e = Engine()
+    t = e.add_template('a {{ "{{" }} $v {{ "}}" }} b {{- " x" -}} c {{ `}}` }}')
+    assert e.render(t, {}) == "a {{ $v }} b xc }}"
