@@ -190,6 +190,9 @@ def build_parser() -> argparse.ArgumentParser:
     hm.add_argument("--set", action="append", default=[], help="key.path=value overrides")
     hm.add_argument("-f", "--values", action="append", default=[], help="values file(s)")
     sub.add_parser("version", help="Print the version")
+    from .preflight import add_parser as add_preflight
+
+    add_preflight(sub)
     return root
 
 
@@ -468,7 +471,7 @@ def _helm_template(a: argparse.Namespace) -> int:
     return 0
 
 
-SUBCOMMANDS = ("start", "fake-apiserver", "get", "crd", "kustomize", "helm-template", "version")
+SUBCOMMANDS = ("start", "fake-apiserver", "get", "crd", "kustomize", "helm-template", "version", "preflight")
 
 
 def cobra_order(argv: List[str]) -> List[str]:
@@ -501,6 +504,10 @@ def main(argv: Optional[List[str]] = None) -> int:
         return 0
     if a.command == "get":
         return asyncio.run(run_get(a))
+    if a.command == "preflight":
+        from .preflight import run as run_preflight
+
+        return asyncio.run(run_preflight(a))
     if a.command == "kustomize":
         from ..utils.kustomize import build_yaml, enable_optional
 

@@ -1,0 +1,189 @@
+"""``cron-operator preflight``: check a cluster before this operator takes it over.
+
+A cluster run by the reference operator (or by this one, before an upgrade) holds Crons
+whose templates name workload kinds.  Before switching (``docs/migration.md``), this reads
+the cluster with the caller's kubeconfig -- nothing is written -- and reports, per kind the
+templates use, whether the apiserver serves it and whether the operator's RBAC
+(``controller/rbac.py`` ``RULES``, as the chart and kustomize installs grant it, plus any
+``rbac.extraWorkloadRules``) lets it create, watch and delete that kind; every schedule
+that does not parse (the reference's ``cron.ParseStandard`` grammar,
+``internal/controller/cron_controller.go:184-190``); templates that set ``metadata.name``
+(the reference's ``OverridePolicy``: such a Cron runs as Forbid, ``cron_controller.go:355-370``);
+and who holds the leader Lease.  Exit status 1 when a Cron would fail to run.
+"""
+from __future__ import annotations
+
+import argparse
+import sys
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Tuple
+
+from ..api import errors
+from ..api.meta import GroupVersionKind, GroupVersionResource
+from ..api.v1alpha1 import CRON_GVR
+from ..apiserver.rbac import rule_allows
+from ..controller.rbac import RULES
+from ..cron.parser import CronParseError, parse_standard
+from ..models.workload import WorkloadError, get_workload_gvk
+from ..runtime.client import Client, NoKindMatchError
+from ..runtime.manager import DEFAULT_LEADER_ELECTION_ID
+
+# what the reconciler does with a template's kind: LIST/WATCH it (informer), CREATE it on a tick,
+# DELETE it (history GC, Replace), GET it (deduplication after a lost response)
+NEEDED_VERBS = ("get", "list", "watch", "create", "delete")
+LEASES = GroupVersionResource("coordination.k8s.io", "v1", "leases")
+
+
+@dataclass
+class KindReport:
+    gvk: GroupVersionKind
+    crons: List[str] = field(default_factory=list)
+    resource: str = ""
+    served: bool = False
+    missing_verbs: List[str] = field(default_factory=list)
+
+    @property
+    def ok(self) -> bool:
+        return self.served and not self.missing_verbs
+
+
+@dataclass
+class Report:
+    crons: int = 0
+    kinds: Dict[GroupVersionKind, KindReport] = field(default_factory=dict)
+    bad_schedules: List[Tuple[str, str, str]] = field(default_factory=list)   # (cron, schedule, error)
+    bad_templates: List[Tuple[str, str]] = field(default_factory=list)        # (cron, error)
+    named_templates: List[str] = field(default_factory=list)                  # run as Forbid
+    lease: Optional[Dict[str, Any]] = None
+    errors: List[str] = field(default_factory=list)
+
+    @property
+    def ok(self) -> bool:
+        return not (self.errors or self.bad_schedules or self.bad_templates or
+                    any(not k.ok for k in self.kinds.values()))
+
+
+def rbac_missing(group: str, resource: str, rules: List[Dict[str, Any]]) -> List[str]:
+    """Verbs of :data:`NEEDED_VERBS` none of ``rules`` grants on ``group/resource``."""
+    return [v for v in NEEDED_VERBS
+            if not any(rule_allows(r, {"verb": v, "group": group, "resource": resource, "namespace": "x"})
+                       for r in rules)]
+
+
+async def preflight(client: Client, namespace: str = "", rules: Optional[List[Dict[str, Any]]] = None,
+                    lease_namespace: str = "") -> Report:
+    """Read-only checks of the Crons in ``namespace`` ("" = all) against ``rules`` (default: the
+    operator's own RBAC)."""
+    rules = list(RULES) if rules is None else rules
+    rep = Report()
+    try:
+        crons = (await client.list(CRON_GVR, namespace)).get("items") or []
+    except errors.ApiError as e:
+        rep.errors.append(f"cannot list crons.apps.kubedl.io: {e}")
+        return rep
+    rep.crons = len(crons)
+    for c in crons:
+        m = c.get("metadata") or {}
+        key = f"{m.get('namespace', '')}/{m.get('name', '')}"
+        spec = c.get("spec") or {}
+        sched = spec.get("schedule", "")
+        try:
+            parse_standard(sched)
+        except (CronParseError, ValueError) as e:
+            rep.bad_schedules.append((key, sched, str(e)))
+        wl = (spec.get("template") or {}).get("workload")
+        try:
+            gvk = get_workload_gvk(wl)
+        except WorkloadError as e:
+            rep.bad_templates.append((key, str(e)))
+            continue
+        if isinstance(wl, dict) and (wl.get("metadata") or {}).get("name"):
+            rep.named_templates.append(key)
+        rep.kinds.setdefault(gvk, KindReport(gvk)).crons.append(key)
+    for gvk, kr in rep.kinds.items():
+        try:
+            gvr, _ = await client.mapper.resource_for(gvk)
+        except NoKindMatchError:
+            continue
+        kr.served, kr.resource = True, gvr.resource
+        kr.missing_verbs = rbac_missing(gvk.group, gvr.resource, rules)
+    if lease_namespace:
+        try:
+            lease = await client.get(LEASES, lease_namespace, DEFAULT_LEADER_ELECTION_ID)
+            rep.lease = lease.get("spec") or {}
+        except errors.ApiError as e:
+            if e.code != 404:
+                rep.errors.append(f"cannot read Lease {lease_namespace}/{DEFAULT_LEADER_ELECTION_ID}: {e}")
+    return rep
+
+
+def render(rep: Report, lease_namespace: str = "") -> str:
+    out = [f"Crons: {rep.crons}"]
+    if rep.kinds:
+        out.append("")
+        out.append(f"{'KIND':<40} {'RESOURCE':<28} {'CRONS':>5}  {'SERVED':<6}  RBAC")
+        for gvk, kr in sorted(rep.kinds.items(), key=lambda x: (x[0].group, x[0].kind)):
+            kind = f"{gvk.kind}.{gvk.group or 'core'}/{gvk.version}"
+            rbac = "ok" if not kr.missing_verbs else "missing " + ",".join(kr.missing_verbs)
+            out.append(f"{kind:<40} {kr.resource or '-':<28} {len(kr.crons):>5}  {'yes' if kr.served else 'NO':<6}  "
+                       f"{rbac if kr.served else '-'}")
+    for key, sched, err in rep.bad_schedules:
+        out.append(f"error: {key}: schedule {sched!r} does not parse: {err}")
+    for key, err in rep.bad_templates:
+        out.append(f"error: {key}: {err}")
+    for gvk, kr in rep.kinds.items():
+        if not kr.served:
+            out.append(f"error: {gvk.kind}.{gvk.group} is not served by this cluster; "
+                       f"{len(kr.crons)} Cron(s) would fail to create it: {', '.join(kr.crons[:5])}")
+        elif kr.missing_verbs:
+            out.append(f"error: the operator's RBAC lacks {','.join(kr.missing_verbs)} on "
+                       f"{kr.resource}.{gvk.group}; add it to rbac.extraWorkloadRules")
+    for key in rep.named_templates:
+        out.append(f"note: {key}: the template sets metadata.name, so the Cron runs as Forbid (OverridePolicy)")
+    if lease_namespace:
+        if rep.lease:
+            out.append(f"lease {lease_namespace}/{DEFAULT_LEADER_ELECTION_ID}: held by "
+                       f"{rep.lease.get('holderIdentity', '?')}, renewed {rep.lease.get('renewTime', '?')}, "
+                       f"duration {rep.lease.get('leaseDurationSeconds', '?')} s")
+        else:
+            out.append(f"lease {lease_namespace}/{DEFAULT_LEADER_ELECTION_ID}: none (no operator is leading)")
+    out.extend(f"error: {e}" for e in rep.errors)
+    out.append("preflight: ok" if rep.ok else "preflight: FAILED")
+    return "\n".join(out) + "\n"
+
+
+def add_parser(sub: Any) -> None:
+    pf = sub.add_parser("preflight", help="Check a cluster's Crons before this operator takes it over "
+                                          "(read-only)")
+    pf.add_argument("--kubeconfig", default="")
+    pf.add_argument("-n", "--namespace", default="", help="only this namespace (default: all)")
+    pf.add_argument("--lease-namespace", default="",
+                    help="also report the holder of the leader Lease in this namespace")
+    pf.add_argument("--extra-rules", default="",
+                    help="YAML list of {apiGroups, resources} rules, as the chart's rbac.extraWorkloadRules")
+
+
+async def run(a: argparse.Namespace) -> int:
+    import yaml
+
+    from ..runtime.http import HttpTransport
+    from ..runtime.kubeconfig import ConfigError, get_config
+
+    try:
+        cfg = get_config(a.kubeconfig)
+    except ConfigError as e:
+        print(f"error: {e}", file=sys.stderr)
+        return 1
+    rules = list(RULES)
+    if a.extra_rules:
+        with open(a.extra_rules) as fh:
+            for r in yaml.safe_load(fh) or []:
+                rules.append({"apiGroups": r.get("apiGroups") or [], "resources": r.get("resources") or [],
+                              "verbs": ["get", "list", "watch", "create", "update", "patch", "delete"]})
+    client = Client(HttpTransport(cfg), qps=-1)
+    try:
+        rep = await preflight(client, a.namespace, rules, a.lease_namespace)
+    finally:
+        await client.close()
+    sys.stdout.write(render(rep, a.lease_namespace))
+    return 0 if rep.ok else 1

@@ -1,0 +1,127 @@
+"""``cron-operator preflight``: the read-only check before a switch-over (docs/migration.md).
+
+A cluster holds Crons of every case the check distinguishes: a PyTorchJob (served,
+granted), KubeDL's XDLJob (served; granted since the chart grants what the reference chart
+does), a RayJob (served, not granted unless ``rbac.extraWorkloadRules`` adds it), a kind no
+CRD serves, an unparsable schedule, a template without ``kind``, and a template that sets
+``metadata.name`` (run as Forbid, the reference's OverridePolicy).
+"""
+from __future__ import annotations
+
+import asyncio
+import os
+import subprocess
+import sys
+
+from cron_operator_amd.api.meta import GroupVersionKind, GroupVersionResource
+from cron_operator_amd.api.v1alpha1 import CRON_GVR
+from cron_operator_amd.cmd.preflight import LEASES, preflight, rbac_missing, render
+from cron_operator_amd.controller.rbac import RULES
+from cron_operator_amd.runtime.manager import DEFAULT_LEADER_ELECTION_ID
+from cron_operator_amd.testing.env import TestEnv
+from cron_operator_amd.trainingop.crds import job_crd
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+NS = "default"
+
+
+def _cron(name, schedule, workload):
+    return {"apiVersion": "apps.kubedl.io/v1alpha1", "kind": "Cron", "metadata": {"name": name, "namespace": NS},
+            "spec": {"schedule": schedule, "template": {"workload": workload}}}
+
+
+def _job(api_version, kind, **meta):
+    return {"apiVersion": api_version, "kind": kind, "metadata": meta, "spec": {}}
+
+
+async def _seed(env: TestEnv) -> None:
+    env.server.install_crd(job_crd("xdl.kubedl.io", "v1alpha1", "xdljobs", "XDLJob"))
+    env.server.install_crd(job_crd("ray.io", "v1", "rayjobs", "RayJob"))
+    crons = [
+        _cron("pt", "*/5 * * * *", _job("kubeflow.org/v1", "PyTorchJob")),
+        _cron("pt-named", "0 3 * * *", _job("kubeflow.org/v1", "PyTorchJob", name="fixed")),
+        _cron("xdl", "CRON_TZ=Asia/Shanghai 30 2 * * *", _job("xdl.kubedl.io/v1alpha1", "XDLJob")),
+        _cron("ray", "@hourly", _job("ray.io/v1", "RayJob")),
+        _cron("nokind", "*/1 * * * *", _job("example.com/v1", "FooJob")),
+        _cron("badsched", "61 * * * *", _job("kubeflow.org/v1", "TFJob")),
+        _cron("notemplate", "*/1 * * * *", {"apiVersion": "kubeflow.org/v1"}),
+    ]
+    for c in crons:
+        await env.client.create(CRON_GVR, c, NS)
+
+
+async def test_preflight_reports_every_case():
+    env = TestEnv()
+    await _seed(env)
+    env.server.create(LEASES, NS, {"apiVersion": "coordination.k8s.io/v1", "kind": "Lease",
+                                   "metadata": {"name": DEFAULT_LEADER_ELECTION_ID, "namespace": NS},
+                                   "spec": {"holderIdentity": "cron-operator-abc_1", "leaseDurationSeconds": 15}})
+    rep = await preflight(env.client, "", lease_namespace=NS)
+    assert rep.crons == 7 and not rep.ok
+    kinds = {g.kind: k for g, k in rep.kinds.items()}
+    assert kinds["PyTorchJob"].ok and sorted(kinds["PyTorchJob"].crons) == ["default/pt", "default/pt-named"]
+    assert kinds["XDLJob"].ok and kinds["XDLJob"].resource == "xdljobs"
+    assert kinds["RayJob"].served and kinds["RayJob"].missing_verbs == ["get", "list", "watch", "create", "delete"]
+    assert not kinds["FooJob"].served
+    assert [b[0] for b in rep.bad_schedules] == ["default/badsched"]
+    assert [b[0] for b in rep.bad_templates] == ["default/notemplate"]
+    assert rep.named_templates == ["default/pt-named"]
+    assert rep.lease["holderIdentity"] == "cron-operator-abc_1"
+    text = render(rep, NS)
+    assert "FooJob.example.com is not served" in text and "lacks get,list,watch,create,delete on rayjobs.ray.io" in text
+    assert "runs as Forbid" in text and "held by cron-operator-abc_1" in text and text.endswith("preflight: FAILED\n")
+
+
+async def test_preflight_passes_once_the_gaps_are_closed():
+    """The RayJob covered by an extra rule and the broken Crons removed: the cluster is ready."""
+    env = TestEnv()
+    await _seed(env)
+    for name in ("nokind", "badsched", "notemplate"):
+        env.server.delete(CRON_GVR, NS, name)
+    rules = list(RULES) + [{"apiGroups": ["ray.io"], "resources": ["rayjobs"],
+                            "verbs": ["get", "list", "watch", "create", "update", "patch", "delete"]}]
+    rep = await preflight(env.client, NS, rules)
+    assert rep.ok, render(rep)
+    assert render(rep).endswith("preflight: ok\n")
+
+
+def test_rbac_missing_uses_the_operator_rules():
+    assert rbac_missing("kubeflow.org", "pytorchjobs", RULES) == []
+    assert rbac_missing("xgboostjob.kubeflow.org", "xgboostjobs", RULES) == []
+    assert rbac_missing("ray.io", "rayjobs", RULES) == ["get", "list", "watch", "create", "delete"]
+
+
+async def test_preflight_cli_over_http(tmp_path):
+    """``python -m cron_operator_amd preflight --kubeconfig ...`` against the fake apiserver over
+    HTTP: the table, the errors, exit status 1; with ``--extra-rules`` and the bad Crons gone, 0."""
+    from cron_operator_amd.apiserver.http import APIServerApp
+    from cron_operator_amd.runtime.kubeconfig import write_kubeconfig
+
+    env = TestEnv()
+    await _seed(env)
+    app = APIServerApp(env.server)
+    port = await app.start("127.0.0.1", 0)
+    kcfg = tmp_path / "kubeconfig"
+    write_kubeconfig(str(kcfg), f"http://127.0.0.1:{port}")
+    envv = dict(os.environ, PYTHONPATH=ROOT)
+    try:
+        cmd = [sys.executable, "-m", "cron_operator_amd", "preflight", "--kubeconfig", str(kcfg)]
+        r = await asyncio.to_thread(subprocess.run, cmd, capture_output=True, text=True, timeout=120, env=envv)
+        assert r.returncode == 1, r.stdout + r.stderr
+        assert "XDLJob.xdl.kubedl.io/v1alpha1" in r.stdout and "FooJob.example.com is not served" in r.stdout
+        for name in ("nokind", "badsched", "notemplate"):
+            env.server.delete(CRON_GVR, NS, name)
+        extra = tmp_path / "extra.yaml"
+        extra.write_text("- apiGroups: [ray.io]\n  resources: [rayjobs]\n")
+        r = await asyncio.to_thread(subprocess.run, cmd + ["--extra-rules", str(extra)], capture_output=True,
+                                    text=True, timeout=120, env=envv)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert r.stdout.endswith("preflight: ok\n")
+    finally:
+        await app.stop()
+
+
+def test_gvk_keys_are_hashable_values():
+    # the report keys kinds by GroupVersionKind: equal kinds from different Crons share a row
+    assert GroupVersionKind("a", "v1", "K") == GroupVersionKind("a", "v1", "K")
+    assert GroupVersionResource("a", "v1", "ks") != GroupVersionResource("a", "v1", "k")
