@@ -16,17 +16,13 @@ from __future__ import annotations
 import argparse
 import sys
 from dataclasses import dataclass, field
-from typing import Any, Dict, List, Optional, Tuple
+from typing import TYPE_CHECKING, Any, Dict, List, Optional, Tuple
 
-from ..api import errors
 from ..api.meta import GroupVersionKind, GroupVersionResource
-from ..api.v1alpha1 import CRON_GVR
-from ..apiserver.rbac import rule_allows
-from ..controller.rbac import RULES
-from ..cron.parser import CronParseError, parse_standard
-from ..models.workload import WorkloadError, get_workload_gvk
-from ..runtime.client import Client, NoKindMatchError
-from ..runtime.manager import DEFAULT_LEADER_ELECTION_ID
+
+# the operator's runtime is imported when the check runs, not when the CLI builds its parser
+if TYPE_CHECKING:
+    from ..runtime.client import Client
 
 # what the reconciler does with a template's kind: LIST/WATCH it (informer), CREATE it on a tick,
 # DELETE it (history GC, Replace), GET it (deduplication after a lost response)
@@ -63,17 +59,32 @@ class Report:
                     any(not k.ok for k in self.kinds.values()))
 
 
+def _lease_name() -> str:
+    from ..runtime.manager import DEFAULT_LEADER_ELECTION_ID
+
+    return DEFAULT_LEADER_ELECTION_ID
+
+
 def rbac_missing(group: str, resource: str, rules: List[Dict[str, Any]]) -> List[str]:
     """Verbs of :data:`NEEDED_VERBS` none of ``rules`` grants on ``group/resource``."""
+    from ..apiserver.rbac import rule_allows
+
     return [v for v in NEEDED_VERBS
             if not any(rule_allows(r, {"verb": v, "group": group, "resource": resource, "namespace": "x"})
                        for r in rules)]
 
 
-async def preflight(client: Client, namespace: str = "", rules: Optional[List[Dict[str, Any]]] = None,
+async def preflight(client: "Client", namespace: str = "", rules: Optional[List[Dict[str, Any]]] = None,
                     lease_namespace: str = "") -> Report:
     """Read-only checks of the Crons in ``namespace`` ("" = all) against ``rules`` (default: the
     operator's own RBAC)."""
+    from ..api import errors
+    from ..api.v1alpha1 import CRON_GVR
+    from ..controller.rbac import RULES
+    from ..cron.parser import CronParseError, parse_standard
+    from ..models.workload import WorkloadError, get_workload_gvk
+    from ..runtime.client import NoKindMatchError
+
     rules = list(RULES) if rules is None else rules
     rep = Report()
     try:
@@ -109,11 +120,11 @@ async def preflight(client: Client, namespace: str = "", rules: Optional[List[Di
         kr.missing_verbs = rbac_missing(gvk.group, gvr.resource, rules)
     if lease_namespace:
         try:
-            lease = await client.get(LEASES, lease_namespace, DEFAULT_LEADER_ELECTION_ID)
+            lease = await client.get(LEASES, lease_namespace, _lease_name())
             rep.lease = lease.get("spec") or {}
         except errors.ApiError as e:
             if e.code != 404:
-                rep.errors.append(f"cannot read Lease {lease_namespace}/{DEFAULT_LEADER_ELECTION_ID}: {e}")
+                rep.errors.append(f"cannot read Lease {lease_namespace}/{_lease_name()}: {e}")
     return rep
 
 
@@ -142,11 +153,11 @@ def render(rep: Report, lease_namespace: str = "") -> str:
         out.append(f"note: {key}: the template sets metadata.name, so the Cron runs as Forbid (OverridePolicy)")
     if lease_namespace:
         if rep.lease:
-            out.append(f"lease {lease_namespace}/{DEFAULT_LEADER_ELECTION_ID}: held by "
+            out.append(f"lease {lease_namespace}/{_lease_name()}: held by "
                        f"{rep.lease.get('holderIdentity', '?')}, renewed {rep.lease.get('renewTime', '?')}, "
                        f"duration {rep.lease.get('leaseDurationSeconds', '?')} s")
         else:
-            out.append(f"lease {lease_namespace}/{DEFAULT_LEADER_ELECTION_ID}: none (no operator is leading)")
+            out.append(f"lease {lease_namespace}/{_lease_name()}: none (no operator is leading)")
     out.extend(f"error: {e}" for e in rep.errors)
     out.append("preflight: ok" if rep.ok else "preflight: FAILED")
     return "\n".join(out) + "\n"
@@ -166,6 +177,8 @@ def add_parser(sub: Any) -> None:
 async def run(a: argparse.Namespace) -> int:
     import yaml
 
+    from ..controller.rbac import RULES
+    from ..runtime.client import Client
     from ..runtime.http import HttpTransport
     from ..runtime.kubeconfig import ConfigError, get_config
 
