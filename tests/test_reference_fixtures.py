@@ -144,3 +144,24 @@ def test_chart_rbac_grants_every_rule_of_the_reference_chart():
                     if (g, r, v) not in granted:
                         missing.append((g, r, v))
     assert not missing, missing
+
+
+def test_chart_values_have_every_key_of_the_reference_chart():
+    """A values file written for the reference chart keeps working: every key (nested) of its
+    ``values.yaml`` exists here with the same type (docs/migration.md)."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(REF, "charts", "cron-operator", "values.yaml")) as fh:
+        ref = yaml.safe_load(fh)
+    with open(os.path.join(root, "charts", "cron-operator", "values.yaml")) as fh:
+        ours = yaml.safe_load(fh)
+
+    def walk(a, b, path):
+        for k, v in a.items():
+            assert k in b, f"missing value {path}{k}"
+            if isinstance(v, dict) and v:
+                assert isinstance(b[k], dict), f"{path}{k} is not a map here"
+                walk(v, b[k], f"{path}{k}.")
+            elif v is not None and b[k] is not None:
+                assert type(b[k]) is type(v) or {type(b[k]), type(v)} <= {int, float}, f"{path}{k} changed type"
+
+    walk(ref, ours, "")
