@@ -116,6 +116,11 @@ async def preflight(client: "Client", namespace: str = "", rules: Optional[List[
             gvr, _ = await client.mapper.resource_for(gvk)
         except NoKindMatchError:
             continue
+        except errors.ApiError as e:  # discovery itself failed (403, 5xx): say so, do not guess
+            rep.errors.append(f"cannot discover {gvk.group}/{gvk.version}: {e}")
+            kr.served = True  # unknown, reported as an error above rather than as "not served"
+            kr.resource = "?"
+            continue
         kr.served, kr.resource = True, gvr.resource
         kr.missing_verbs = rbac_missing(gvk.group, gvr.resource, rules)
     if lease_namespace:

@@ -125,3 +125,18 @@ def test_gvk_keys_are_hashable_values():
     # the report keys kinds by GroupVersionKind: equal kinds from different Crons share a row
     assert GroupVersionKind("a", "v1", "K") == GroupVersionKind("a", "v1", "K")
     assert GroupVersionResource("a", "v1", "ks") != GroupVersionResource("a", "v1", "k")
+
+
+async def test_discovery_failure_is_an_error_not_a_missing_kind():
+    from cron_operator_amd.api import errors
+
+    env = TestEnv()
+    await env.client.create(CRON_GVR, _cron("pt", "*/5 * * * *", _job("kubeflow.org/v1", "PyTorchJob")), NS)
+
+    async def broken(gvk):
+        raise errors.ApiError(503, "ServiceUnavailable", "discovery down")
+
+    env.client.mapper.resource_for = broken  # type: ignore[assignment]
+    rep = await preflight(env.client)
+    assert not rep.ok and any("cannot discover kubeflow.org/v1" in e for e in rep.errors)
+    assert "is not served" not in render(rep)
