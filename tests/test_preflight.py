@@ -13,7 +13,6 @@ import os
 import subprocess
 import sys
 
-from cron_operator_amd.api.meta import GroupVersionKind, GroupVersionResource
 from cron_operator_amd.api.v1alpha1 import CRON_GVR
 from cron_operator_amd.cmd.preflight import LEASES, preflight, rbac_missing, render
 from cron_operator_amd.controller.rbac import RULES
@@ -119,12 +118,6 @@ async def test_preflight_cli_over_http(tmp_path):
         assert r.stdout.endswith("preflight: ok\n")
     finally:
         await app.stop()
-
-
-def test_gvk_keys_are_hashable_values():
-    # the report keys kinds by GroupVersionKind: equal kinds from different Crons share a row
-    assert GroupVersionKind("a", "v1", "K") == GroupVersionKind("a", "v1", "K")
-    assert GroupVersionResource("a", "v1", "ks") != GroupVersionResource("a", "v1", "k")
 
 
 async def test_discovery_failure_is_an_error_not_a_missing_kind():
