@@ -231,6 +231,9 @@ class ReconcilerOptions:
     wire_codecs: bool = True
     defer_status_write: bool = True
     request_priorities: bool = True
+    # a Cron that cannot run (unparsable schedule, template without a kind) gets a Warning event
+    # (InvalidSchedule / InvalidTemplate) for `kubectl describe`; the reference only logs it
+    explain_errors: bool = True
     # cache mode: how long a reconcile waits for a new child informer's first LIST before
     # it falls back to a live LIST; a LIST that *fails* (403, 404, 5xx) is returned as the
     # reconcile's error at once, like the reference's live LIST (cron_controller.go:129-133)
@@ -248,7 +251,7 @@ class ReconcilerOptions:
                                  fold_created_into_active=False, skip_expected_events=False,
                                  classification_cache=False, dedupe_ran_tick=False,
                                  overlap_gc_deletes=False, slim_child_cache=False, wire_codecs=False,
-                                 defer_status_write=False, request_priorities=False,
+                                 defer_status_write=False, request_priorities=False, explain_errors=False,
                                  workload=WorkloadPolicy.reference())
 
 
@@ -590,6 +593,8 @@ class CronReconciler(Reconciler):
                 gvk = get_workload_gvk(wl, policy)
             except WorkloadError as e:
                 log.error(e, "Failed to get workload GVK")
+                if self.opts.explain_errors:
+                    self.recorder.event(cron.to_dict(), Warning, "InvalidTemplate", str(e))
                 return Result()
             if wl.__class__ is dict:
                 gm[ck] = (wl, policy, gvk)
@@ -693,6 +698,8 @@ class CronReconciler(Reconciler):
             missed_run, next_run = self.get_next_schedule(cron, now, log)
         except ScheduleError as e:
             log.error(e, "Failed to figure out CronJob schedule")
+            if self.opts.explain_errors:
+                self.recorder.event(cron.to_dict(), Warning, "InvalidSchedule", str(e))
             return Result()
 
         # B13 (cron_controller.go:192)

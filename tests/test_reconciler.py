@@ -363,6 +363,27 @@ async def test_b12_schedule_error_logged_not_requeued():
 
 
 @pytest.mark.parametrize("mode", MODES)
+async def test_unrunnable_cron_explained_by_a_warning_event(mode):
+    """B3/B12 errors are only logged by the reference (``cron_controller.go:122-126,184-190``);
+    the default mode also records a Warning event on the Cron, so ``kubectl describe cron``
+    says why it never runs.  Reference mode stays silent, as the reference is."""
+    rig = Rig(MODES[mode])
+    await rig.create(schedule="61 * * * *")
+    await rig.reconcile()
+    tmpl = Rig(MODES[mode])
+    c = new_cron(NAME, NS, "*/1 * * * *", {"kind": "PyTorchJob"})
+    await tmpl.env.create_cron(c)
+    await tmpl.reconcile()
+    got = [(e[1], e[2]) for e in rig.rec_events.events + tmpl.rec_events.events]
+    if mode == "optimized":
+        assert got == [("Warning", "InvalidSchedule"), ("Warning", "InvalidTemplate")]
+        assert "unparsable cron" in rig.rec_events.events[0][3]
+        assert "missing apiVersion or kind" in tmpl.rec_events.events[0][3]
+    else:
+        assert got == []
+
+
+@pytest.mark.parametrize("mode", MODES)
 async def test_b13_b14_requeue_after_next_tick(mode):
     rig = Rig(MODES[mode])
     await rig.create()  # created at 12:00:05, clock at 12:00:05
