@@ -36,8 +36,8 @@ pytestmark = [
 # names rendered by deploy/kustomize/default (namePrefix cron-operator-, namespace below)
 NAMESPACE = os.environ.get("E2E_NAMESPACE", "cron-operator-system")
 PREFIX = "cron-operator-"
-SERVICE_ACCOUNT = PREFIX + "controller"
-METRICS_SERVICE = PREFIX + "controller-manager-metrics"
+SERVICE_ACCOUNT = PREFIX + "controller-manager"
+METRICS_SERVICE = PREFIX + "controller-manager-metrics-service"
 METRICS_ROLE = PREFIX + "metrics-reader"
 METRICS_BINDING = PREFIX + "e2e-metrics-binding"
 POD_SELECTOR = "app.kubernetes.io/name=cron-operator"

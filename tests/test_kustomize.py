@@ -198,7 +198,7 @@ def test_cert_manager_metrics_and_servicemonitor_tls(tmp_path):
     objs = build_sorted(enable_optional(DEFAULT, str(tmp_path / "tree")))
     svc = [o for o in by_kind(objs, "Service") if "metrics" in o["metadata"]["name"]][0]
     host = f"{svc['metadata']['name']}.cron-operator-system.svc"
-    assert host == "cron-operator-controller-manager-metrics.cron-operator-system.svc"
+    assert host == "cron-operator-controller-manager-metrics-service.cron-operator-system.svc"
     cert = by_kind(objs, "Certificate")[0]
     assert cert["spec"]["dnsNames"] == [host, host + ".cluster.local"]
     assert cert["spec"]["secretName"] == "metrics-server-cert"
@@ -315,3 +315,13 @@ def test_alert_rules_use_metrics_the_operator_exports():
         assert names and names <= exported, (a["alert"], names - exported)
         assert a["labels"]["severity"] in ("warning", "critical") and a["annotations"]["summary"]
     assert LEADER_ELECTION_ID in next(a["expr"] for a in alerts if a["alert"] == "CronOperatorNoLeader")
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/config/default"), reason="reference checkout not mounted")
+def test_default_install_names_every_object_as_the_reference_does():
+    """``make deploy`` over a cluster the reference's kustomize install runs replaces its objects
+    in place (docs/migration.md): the default overlay renders the same (kind, name) set -- the
+    ServiceAccount, the leader-election and metrics-auth roles and bindings, the metrics Service."""
+    ref = {(o["kind"], o["metadata"]["name"]) for o in build("/root/reference/config/default")}
+    ours = {(o["kind"], o["metadata"]["name"]) for o in build(os.path.join(ROOT, "deploy", "kustomize", "default"))}
+    assert ref == ours, (sorted(ref - ours), sorted(ours - ref))

@@ -213,7 +213,7 @@ async def _operator_fires_under(srv: APIServer, clock: FakeClock, lease_ns: str,
 
 
 async def test_kustomize_install_rbac_suffices():
-    clock, srv = _server("cron-operator-system", "cron-operator-controller")
+    clock, srv = _server("cron-operator-system", "cron-operator-controller-manager")
     _apply(srv, build_sorted(os.path.join(ROOT, "deploy", "kustomize", "default")))
     await _operator_fires_under(srv, clock, "cron-operator-system")
 
