@@ -423,7 +423,7 @@ class Engine:
         return cur
 
     def _arg(self, tok, dot, scope):
-        k, v = tok
+        k, v = tok[0], tok[1]  # ("subfield", pipe, field) carries a third element
         if k == "str":
             return json.loads(v) if v.startswith('"') else v[1:-1]
         if k == "char":

@@ -277,3 +277,30 @@ def test_action_ends_outside_string_literals():
     e = Engine()
     t = e.add_template('a {{ "{{" }} $v {{ "}}" }} b {{- " x" -}} c {{ `}}` }}')
     assert e.render(t, {}) == "a {{ $v }} b xc }}"
+
+
+def test_subfield_of_a_parenthesised_pipeline_as_an_argument():
+    e = Engine()
+    t = e.add_template('{{ printf "%s!" (.m).k }}')
+    assert e.render(t, {"m": {"k": "v"}}) == "v!"
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/charts/cron-operator"), reason="reference checkout not mounted")
+@pytest.mark.parametrize("release", ["cron-operator", "nightly"])
+def test_helm_upgrade_over_the_reference_release_keeps_names_and_selector(release):
+    """``helm upgrade <release> charts/cron-operator`` over a reference release: the same
+    objects by (kind, name), and the same Deployment selector -- a Deployment's selector is
+    immutable, so a different one would make the upgrade fail (docs/migration.md)."""
+    ref = render_chart("/root/reference/charts/cron-operator", {}, release=release, namespace="ns")
+    ours = render_chart(CHART, {}, release=release, namespace="ns")
+
+    def names(docs):
+        return {(o["kind"], o["metadata"]["name"]) for lst in docs.values() for o in lst}
+
+    def dep(docs):
+        return next(o for lst in docs.values() for o in lst if o["kind"] == "Deployment")
+
+    assert names(ref) == names(ours)
+    assert dep(ref)["spec"]["selector"] == dep(ours)["spec"]["selector"]
+    assert dep(ref)["spec"]["template"]["spec"]["serviceAccountName"] == \
+        dep(ours)["spec"]["template"]["spec"]["serviceAccountName"]
