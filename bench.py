@@ -227,7 +227,7 @@ def main() -> int:
     ap.add_argument("--workers", type=int, default=10, help="--max-concurrent-reconciles")
     ap.add_argument("--qps", type=float, default=-1.0, help="client QPS (-1: unthrottled)")
     ap.add_argument("--burst", type=int, default=50)
-    ap.add_argument("--max-inflight", type=int, default=64,
+    ap.add_argument("--max-inflight", type=int, default=128,
                     help="client cap on concurrent API requests (--max-inflight-requests; 0: unlimited)")
     ap.add_argument("--no-defer", action="store_true",
                     help="A/B: reconcile writes on the worker (ReconcilerOptions.defer_status_write=False)")

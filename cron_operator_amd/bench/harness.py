@@ -90,7 +90,7 @@ class BenchConfig:
     transport: str = "http"          # http | memory
     qps: float = -1.0                # client QPS (-1 = unthrottled)
     burst: int = 50
-    max_inflight: int = 64           # client cap on concurrent requests (cmd/main.py DEFAULT_MAX_INFLIGHT)
+    max_inflight: int = 128          # client cap on concurrent requests (cmd/main.py DEFAULT_MAX_INFLIGHT)
     defer_writes: bool = True        # optimized mode: ReconcilerOptions.defer_status_write (A/B switch)
     workers: int = 10
     namespace: str = "bench"

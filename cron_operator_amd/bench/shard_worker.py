@@ -40,7 +40,7 @@ async def main() -> int:
     ap.add_argument("--history-limit", type=int, default=10)
     ap.add_argument("--qps", type=float, default=-1.0)
     ap.add_argument("--burst", type=int, default=50)
-    ap.add_argument("--max-inflight", type=int, default=64)
+    ap.add_argument("--max-inflight", type=int, default=128)
     ap.add_argument("--no-defer", action="store_true", help="ReconcilerOptions.defer_status_write=False (A/B)")
     ap.add_argument("--mode", default="optimized")
     ap.add_argument("--routing", default="hash", choices=["hash", "labels"])

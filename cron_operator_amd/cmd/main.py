@@ -74,7 +74,7 @@ def _processes(v: str) -> int:
 # CREATEs.  The reference ships 30 / 50 (start.go:218-219), which tops out near 450 Crons.
 DEFAULT_QPS = 150.0
 DEFAULT_BURST = 300
-DEFAULT_MAX_INFLIGHT = 64
+DEFAULT_MAX_INFLIGHT = 128
 
 
 def build_parser() -> argparse.ArgumentParser:
@@ -247,7 +247,8 @@ async def run_start(a: argparse.Namespace) -> int:
     except ValueError as e:
         log.error(e, "invalid --sync-period")
         return 2
-    client = Client(HttpTransport(cfg), qps=a.qps, burst=a.burst, max_inflight=a.max_inflight_requests)
+    client = Client(HttpTransport(cfg, pool_size=max(64, a.max_inflight_requests)), qps=a.qps, burst=a.burst,
+                    max_inflight=a.max_inflight_requests)
     mopts = ManagerOptions(namespace=a.namespace, leader_election=a.leader_elect,
                            leader_election_namespace=a.leader_elect_namespace,
                            metrics_bind_address=a.metrics_bind_address, secure_metrics=a.metrics_secure,
@@ -322,7 +323,8 @@ async def run_supervisor(a: argparse.Namespace, argv: List[str]) -> int:
             except ConfigError as e:
                 log.error(e, "unable to get kubeconfig")
                 return 1
-            client = Client(HttpTransport(cfg), qps=a.qps, burst=a.burst, max_inflight=a.max_inflight_requests)
+            client = Client(HttpTransport(cfg, pool_size=max(64, a.max_inflight_requests)), qps=a.qps, burst=a.burst,
+                            max_inflight=a.max_inflight_requests)
         metrics = MetricsServer(a.metrics_bind_address, secure=a.metrics_secure, cert_dir=a.metrics_cert_path,
                                 cert_name=a.metrics_cert_name, key_name=a.metrics_cert_key, client=client,
                                 enable_http2=a.enable_http2)

@@ -51,7 +51,7 @@ def test_replicas_and_pull_policy():
     ({"burst": 200}, "--burst=200"),
     ({}, "--qps=150"),
     ({}, "--burst=300"),
-    ({}, "--max-inflight-requests=64"),
+    ({}, "--max-inflight-requests=128"),
     ({"maxInflightRequests": 0}, "--max-inflight-requests=0"),
     ({"compatMode": "reference"}, "--compat-mode=reference"),
     ({"extraArgs": ["--namespace=team-a"]}, "--namespace=team-a"),
