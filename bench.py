@@ -41,6 +41,16 @@ are both algorithms in that shape (one process each, TLS + the harness's ``etcd`
 model), run in this same invocation after the timed run; ``vs_baseline_deployment`` is
 their ratio (``--deployment none`` skips them).
 
+Job lifecycle.  The headline (and its single-process and reference runs) keeps the rounds 1-4
+step: each job of the previous tick is marked Succeeded in one write (``--lifecycle instant``).
+The deployment-shaped pair runs the realistic sequence (``--deployment-lifecycle realistic``):
+the training-operator's ``Created``, one ``replicaStatuses`` write per pod, ``Running``, then
+``Succeeded``, each absorbed by the operator before the next.  Every such write changes the job's
+resourceVersion, which the reference folds into ``status.active`` (``cron_controller.go:284-304``):
+it pays a reconcile, a live LIST and a status PATCH per write, this operator nothing
+(``deployment_api_requests_per_fire``).  The harness's own write calls are not timed; the
+operator's absorption of each write is.
+
 ``payload_ddp``: last of all, untimed, when the node has a GPU per rank, rank 0 runs the
 payload the operator schedules (``models/payloads/ddp_train.py``: DDP over RCCL, one process
 per GPU) as a time-limited child job on those GPUs and reports whether its ranks stayed in
@@ -217,6 +227,25 @@ def _sync_device() -> None:
             torch.cuda.synchronize()
 
 
+def _latency_ceiling(allr, workers: int, crons: int, history_limit: int, model: dict):
+    """Fires/s (all ranks) the reference algorithm could reach if its only cost were the
+    latency model's wait per request: ``workers`` reconciles at a time, each awaiting its
+    requests one after another (``cron_controller.go:90-239``).  A label-selected LIST also
+    pays ``list_per_object`` per object in the namespace (``crons x (historyLimit + 1)`` jobs)."""
+    total = 0.0
+    for r in allr:
+        by_verb = r.get("dep_ref_by_verb") or {}
+        fires = r.get("dep_ref_fires") or 0
+        if not fires:
+            return None
+        wait = sum(n * model.get(v, 0.0) for v, n in by_verb.items())
+        wait += by_verb.get("list", 0) * model.get("list_per_object", 0.0) * crons * (history_limit + 1)
+        if wait <= 0:
+            return None
+        total += workers * fires / wait
+    return round(total, 2)
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[1])
     ap.add_argument("--gpus", type=int, default=1)
@@ -268,6 +297,13 @@ def main() -> int:
                          "payload over RCCL on them (child process, time-limited) and report payload_ddp; "
                          "'cpu' runs it over gloo on the CPU (a rehearsal of the multi-rank path)")
     ap.add_argument("--payload-timeout", type=float, default=240.0)
+    ap.add_argument("--lifecycle", choices=["realistic", "instant"], default="instant",
+                    help="how each tick's jobs run before the next tick in the headline, single-process and "
+                         "reference runs: 'instant' (default; the rounds 1-4 step, kept comparable) -- one "
+                         "Succeeded write per job; 'realistic' -- the training-operator's status writes (Created, "
+                         "one replicaStatuses write per pod, Running, Succeeded), each absorbed by the operator")
+    ap.add_argument("--deployment-lifecycle", choices=["realistic", "instant"], default="realistic",
+                    help="the same for the deployment-shaped pair (default realistic)")
     ap.add_argument("--out", default="", help="also write the full result JSON here")
     a = ap.parse_args()
 
@@ -292,7 +328,7 @@ def main() -> int:
                       mode=a.mode, transport=a.transport, qps=a.qps, burst=a.burst, workers=a.workers,
                       namespace=f"bench-r{rank}", shards=a.shards if a.transport == "http" else 1,
                       shard_routing=a.shard_routing, apiserver_latency=a.apiserver_latency, tls=a.tls,
-                      max_inflight=a.max_inflight, defer_writes=not a.no_defer)
+                      max_inflight=a.max_inflight, defer_writes=not a.no_defer, lifecycle=a.lifecycle)
 
     def on_step(k: int, dt: float, timed: bool) -> None:
         # bracket the K timed steps with barriers so every rank times the same window: the
@@ -325,7 +361,7 @@ def main() -> int:
                                history_limit=a.history_limit, mode=a.mode, transport=a.transport, qps=a.qps,
                                burst=a.burst, workers=a.workers, namespace=f"bench-1p-r{rank}", shards=1,
                                apiserver_latency=a.apiserver_latency, tls=a.tls, max_inflight=a.max_inflight,
-                               defer_writes=not a.no_defer)
+                               defer_writes=not a.no_defer, lifecycle=a.lifecycle)
             _barrier(dist)
             sres = run_sync(scfg)
             _barrier(dist)
@@ -343,7 +379,7 @@ def main() -> int:
         bcfg = BenchConfig(n_crons=a.crons, steps=a.baseline_steps, warmup=a.baseline_warmup,
                            history_limit=a.history_limit, mode="reference", transport=a.transport, qps=a.qps,
                            burst=a.burst, workers=a.workers, namespace=f"bench-ref-r{rank}", shards=1,
-                           tls=a.tls)
+                           tls=a.tls, lifecycle=a.lifecycle)
         _barrier(dist)
         bres = run_sync(bcfg)
         _barrier(dist)
@@ -361,7 +397,7 @@ def main() -> int:
                                transport="http", qps=a.qps, burst=a.burst, workers=a.workers,
                                max_inflight=a.max_inflight, defer_writes=not a.no_defer,
                                namespace=f"bench-{tag.replace('_', '-')}-r{rank}", shards=1,
-                               apiserver_latency="etcd", tls=True)
+                               apiserver_latency="etcd", tls=True, lifecycle=a.deployment_lifecycle)
             _barrier(dist)
             try:
                 dres = run_sync(dcfg)
@@ -378,6 +414,9 @@ def main() -> int:
             mine[f"{tag}_p50"] = dres.p50_latency_ms
             mine[f"{tag}_p99"] = dres.p99_latency_ms
             mine[f"{tag}_req_per_fire"] = dres.api_requests_per_fire
+            mine[f"{tag}_cpu_api"] = dres.cpu_s_apiserver
+            mine[f"{tag}_by_verb"] = dres.api_requests_by_verb
+            mine[f"{tag}_reconciles_per_fire"] = dres.reconciles_per_fire
     # the scheduled payload over RCCL on this node's GPUs (untimed, last): rank 0 runs it while
     # the other ranks wait at the barrier, so no rank tears its process group down early
     probe = None
@@ -428,7 +467,7 @@ def main() -> int:
                        "operator_shards": cfg.shards,
                        "shard_routing": cfg.shard_routing if cfg.shards > 1 else None,
                        "apiserver_latency": cfg.apiserver_latency,
-                       "tls": cfg.tls, "qps": cfg.qps},
+                       "tls": cfg.tls, "qps": cfg.qps, "job_lifecycle": cfg.lifecycle},
             "p50_schedule_to_create_ms": round(max(r["p50"] for r in allr), 2),
             "p99_schedule_to_create_ms": round(max(r["p99"] for r in allr), 2),
             "raw_reconciles_per_s": round(sum(r["reconciles"] for r in allr) / t_max, 2),
@@ -469,7 +508,8 @@ def main() -> int:
             out.update({
                 "deployment_config": {"operator_processes": 1, "tls": True, "apiserver_latency": "etcd",
                                       "latency_model_s": LATENCY_PROFILES["etcd"],
-                                      "workers": a.workers, "qps": a.qps},
+                                      "workers": a.workers, "qps": a.qps,
+                                      "job_lifecycle": a.deployment_lifecycle},
                 "deployment_value": round(dv, 2),
                 "deployment_p50_ms": round(max(r["dep_p50"] for r in allr), 2),
                 "deployment_p99_ms": round(max(r["dep_p99"] for r in allr), 2),
@@ -479,6 +519,19 @@ def main() -> int:
                 "deployment_baseline_api_requests_per_fire": round(
                     sum(r["dep_ref_req_per_fire"] for r in allr) / len(allr), 3),
                 "vs_baseline_deployment": round(dv / dbv, 3) if dbv else None,
+                # both arms must be latency-bound, not fixture-bound: the fake apiserver's CPU
+                # seconds per wall second over each arm's timed region (max over ranks)
+                "deployment_apiserver_busy_frac": round(max(r["dep_cpu_api"] / r["dep_elapsed_s"] for r in allr), 3),
+                "deployment_baseline_apiserver_busy_frac": round(
+                    max(r["dep_ref_cpu_api"] / r["dep_ref_elapsed_s"] for r in allr), 3),
+                "deployment_reconciles_per_fire": round(sum(r["dep_reconciles_per_fire"] for r in allr) / len(allr), 3),
+                "deployment_baseline_reconciles_per_fire": round(
+                    sum(r["dep_ref_reconciles_per_fire"] for r in allr) / len(allr), 3),
+                # the reference algorithm's analytical ceiling under the same latency model: each
+                # of its `workers` reconciles awaits its requests in turn, so it cannot exceed
+                # workers / (model latency of its requests per fire) fires/s per rank
+                "deployment_baseline_latency_ceiling": _latency_ceiling(allr, a.workers, a.crons,
+                                                                         a.history_limit, LATENCY_PROFILES["etcd"]),
             })
         if probe is not None:
             out["payload_ddp"] = probe

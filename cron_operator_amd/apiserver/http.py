@@ -305,6 +305,13 @@ class APIServerApp:
             self._authorize(req, {"verb": verb, "group": gvr.group, "resource": gvr.resource, "subresource": sub,
                                   "namespace": ns, "name": name})
         delay = s.faults.delay_for(verb) if s.faults.latency else 0.0
+        if verb == "list" and delay:
+            # a real apiserver filters a label-selected LIST by scanning every object of the
+            # resource in the namespace (watch cache or etcd range): charged per object scanned,
+            # as latency, while this fixture answers it from a label index
+            per = s.faults.latency.get("list_per_object", 0.0)
+            if per:
+                delay += per * s.count(gvr, ns or None)
         if delay > 0:
             return asyncio.ensure_future(self._delayed(delay, req, gvr, ns, name, sub, verb))
         return self._verb(req, gvr, ns, name, sub, verb)
@@ -444,6 +451,29 @@ class APIServerApp:
             finally:
                 s.copy_responses = s.copy_inputs = True
             return _json({"completed": n})
+        if what == "lifecycle" and req.method == "POST":
+            # bench helper: write stage ``stage`` of the training-operator's status sequence
+            # (trainingop.operator.lifecycle_statuses; -1 = the final Succeeded write) to every
+            # job without completionTime; returns each written job's new resourceVersion
+            body = self._body(req) or {}
+            from ..trainingop.operator import lifecycle_status
+
+            gvr = GroupVersionResource(body.get("group", "kubeflow.org"), body.get("version", "v1"),
+                                       body.get("resource", "pytorchjobs"))
+            stage = int(body.get("stage", -1))
+            rvs: Dict[str, str] = {}
+            s.copy_responses = s.copy_inputs = False
+            try:
+                for obj in list(s.objects(gvr, body.get("namespace"))):
+                    if (obj.get("status") or {}).get("completionTime"):
+                        continue
+                    m = obj["metadata"]
+                    st = lifecycle_status(obj, stage, body.get("start") or "", body.get("end") or "")
+                    out = s.patch(gvr, m["namespace"], m["name"], {"status": st}, "merge", "status")
+                    rvs[f"{m['namespace']}/{m['name']}"] = out["metadata"]["resourceVersion"]
+            finally:
+                s.copy_responses = s.copy_inputs = True
+            return _json({"resourceVersions": rvs})
         if what == "profile" and req.method == "POST":
             # cProfile of this process between "start" and "stop" (the bench profiles its timed steps)
             import cProfile

@@ -260,6 +260,9 @@ class APIServer:
         self._by_kind: Dict[Tuple[str, str, str], ResourceInfo] = {}
         # (group, resource) -> namespace -> name -> stored object (never mutated in place)
         self._data: Dict[Tuple[str, str], Dict[str, Dict[str, Dict[str, Any]]]] = defaultdict(dict)
+        # (group, resource) -> label key -> value -> namespace -> names: the label index a LIST
+        # that pins key=value reads instead of scanning the namespace (_label_index)
+        self._label_idx: Dict[Tuple[str, str], Dict[str, Dict[str, Dict[str, Set[str]]]]] = {}
         self._watchers: Dict[Tuple[str, str], List[Watcher]] = defaultdict(list)
         # per resource: (selector groups to always check, {label key: {value: groups pinned to it}})
         self._watch_plan: Dict[Tuple[str, str], Any] = {}
@@ -333,7 +336,48 @@ class APIServer:
         return self._bucket(ri).get(ns if ri.namespaced else "", {}).get(name)
 
     def _put_raw(self, ri: ResourceInfo, ns: str, obj: Dict[str, Any]) -> None:
-        self._bucket(ri).setdefault(ns if ri.namespaced else "", {})[obj["metadata"]["name"]] = obj
+        ns = ns if ri.namespaced else ""
+        objs = self._bucket(ri).setdefault(ns, {})
+        name = obj["metadata"]["name"]
+        old = objs.get(name)
+        objs[name] = obj
+        idx = self._label_idx.get((ri.group, ri.resource))
+        if idx:
+            self._reindex(idx, ns, name, old, obj)
+
+    @staticmethod
+    def _reindex(idx: Dict[str, Dict[str, Dict[str, Set[str]]]], ns: str, name: str,
+                 old: Optional[Dict[str, Any]], new: Optional[Dict[str, Any]]) -> None:
+        """Move ``ns/name`` between the label-index sets of every indexed key whose value changed."""
+        ol = ((old.get("metadata") or {}).get("labels") or {}) if old is not None else None
+        nl = ((new.get("metadata") or {}).get("labels") or {}) if new is not None else None
+        if ol is not None and nl is not None and (ol is nl or ol == nl):
+            return
+        for key, by_val in idx.items():
+            ov = ol.get(key) if ol is not None else None
+            nv = nl.get(key) if nl is not None else None
+            if ov == nv and ol is not None and nl is not None:
+                continue
+            if ov is not None:
+                s = by_val.get(ov, {}).get(ns)
+                if s is not None:
+                    s.discard(name)
+            if nv is not None:
+                by_val.setdefault(nv, {}).setdefault(ns, set()).add(name)
+
+    def _label_index(self, ri: ResourceInfo, key: str) -> Dict[str, Dict[str, Set[str]]]:
+        """``value -> namespace -> names`` of the objects labelled ``key`` (built on first use by
+        a LIST that pins ``key=value``, then kept up to date by every write)."""
+        idx = self._label_idx.setdefault((ri.group, ri.resource), {})
+        by_val = idx.get(key)
+        if by_val is None:
+            by_val = idx[key] = {}
+            for ns, objs in self._bucket(ri).items():
+                for name, obj in objs.items():
+                    v = ((obj.get("metadata") or {}).get("labels") or {}).get(key)
+                    if v is not None:
+                        by_val.setdefault(v, {}).setdefault(ns, set()).add(name)
+        return by_val
 
     def _new_namespace(self, name: str) -> Dict[str, Any]:
         return {"apiVersion": "v1", "kind": "Namespace",
@@ -529,9 +573,13 @@ class APIServer:
                 raise errors.bad_request("invalid continue token") from None
         items: List[Dict[str, Any]] = []
         more = None
+        pin = pred.pinned
+        by_ns = self._label_index(ri, pin[0]).get(pin[1], {}) if pin is not None else None
         for ns in spaces:
             objs = bucket.get(ns) or {}
-            for name in sorted(objs.keys()) if (limit or continue_) else objs.keys():
+            names = objs.keys() if by_ns is None else by_ns.get(ns, ())
+            # index hits in key order, as etcd returns a range (and as paging needs)
+            for name in sorted(names) if (limit or continue_ or by_ns is not None) else names:
                 if start_after is not None and f"{ns}/{name}" <= start_after:
                     continue
                 obj = objs[name]
@@ -778,6 +826,9 @@ class APIServer:
 
     def _remove(self, ri: ResourceInfo, ns: str, name: str, old: Dict[str, Any]) -> Dict[str, Any]:
         self._bucket(ri).get(ns, {}).pop(name, None)
+        idx = self._label_idx.get((ri.group, ri.resource))
+        if idx:
+            self._reindex(idx, ns if ri.namespaced else "", name, old, None)
         rv = self._next_rv()
         # stored objects are immutable: the tombstone shares everything but its metadata
         gone_obj = dict(old)

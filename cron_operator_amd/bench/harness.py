@@ -6,9 +6,13 @@ reconciles/sec and the p50 schedule->create latency.
 
 One **step** is one schedule tick across all Crons, in virtual time:
 
-1. the timer starts; cluster side, the fake training-operator marks every job
-   of the previous tick Succeeded (apiserver work, not operator work, but kept
-   inside the timed region -- conservative);
+1. the timer starts; cluster side, the jobs of the previous tick run: with
+   ``lifecycle="realistic"`` the training-operator's writes (Created, one
+   ``replicaStatuses`` write per pod, Running) reach every job one stage at a time
+   and the operator absorbs each before the next (the harness's write calls are
+   excluded from the timed region -- another controller's requests -- the
+   operator's absorption is not); then every job is marked Succeeded (apiserver
+   work, not operator work, but kept inside the timed region -- conservative);
 2. the operator's clock (and the apiserver's) jumps to the next minute
    boundary, which fires every Cron's ``RequeueAfter``;
 3. the operator reconciles: moves finished jobs into ``status.history``,
@@ -62,9 +66,15 @@ T0_NS = 1767268800 * NANOS
 # "etcd" is an ASSUMED model of a small kube-apiserver + etcd on SSD -- writes pay a quorum
 # fsync, reads come from the watch cache / etcd range -- not a measurement; it turns the bench
 # from CPU-bound into latency-bound, where request count per fire and worker count dominate.
+# ``list_per_object``: a label-selected LIST is answered by scanning every object of the resource
+# in the namespace (kube-apiserver filters the watch cache -- or an etcd range -- by label; there
+# is no label index), charged per object scanned (ASSUMED 1 us: a watch-cache label filter; an
+# etcd range read and decode costs several times that).  The fake apiserver itself answers from
+# a label index, so that scan is latency here, not fixture CPU.
 LATENCY_PROFILES: Dict[str, Dict[str, float]] = {
     "none": {},
-    "etcd": {"create": 0.008, "update": 0.006, "patch": 0.006, "delete": 0.006, "get": 0.001, "list": 0.004},
+    "etcd": {"create": 0.008, "update": 0.006, "patch": 0.006, "delete": 0.006, "get": 0.001, "list": 0.004,
+             "list_per_object": 1e-6},
 }
 
 
@@ -112,6 +122,11 @@ class BenchConfig:
     tls: bool = False
     # the operator's apiserver connections: native (_netconn) or asyncio's transports (A/B rows)
     native_http: bool = True
+    # how the previous tick's jobs run before the tick: "realistic" -- the training-operator's
+    # status sequence (Created, one replicaStatuses write per pod, Running, then Succeeded:
+    # trainingop.operator.lifecycle_statuses), each write absorbed by the operator before the
+    # next; "instant" -- a single Succeeded write (rounds 1-4)
+    lifecycle: str = "realistic"
 
 
 @dataclass
@@ -265,6 +280,62 @@ class SettleTracker:
             self.pending |= {k for k in self.keys if k not in self.inf.store}
 
 
+class RvTracker:
+    """The children whose latest write (a training-operator status write) the operator's job
+    informer has not seen yet: ``begin`` takes ``{namespace/name: resourceVersion}`` of the
+    writes, an event handler drops a key once its object reaches that version (O(1) per
+    event).  Keys the informer does not hold (another shard's jobs) are not waited for."""
+
+    def __init__(self, informer):
+        from ..runtime.informer import EventHandler
+
+        self.inf = informer
+        self.want: Dict[str, int] = {}
+        self.pending: set = set()
+        informer.add_handler(EventHandler(on_add=self._on, on_update=lambda old, new: self._on(new)))
+
+    @staticmethod
+    def _rv(obj: Dict[str, Any]) -> int:
+        try:
+            return int((obj.get("metadata") or {}).get("resourceVersion") or 0)
+        except ValueError:
+            return 0
+
+    def _on(self, obj: Dict[str, Any]) -> None:
+        if not self.pending:
+            return
+        from ..runtime.informer import obj_key
+
+        k = obj_key(obj)
+        w = self.want.get(k)
+        if w is not None and self._rv(obj) >= w:
+            self.pending.discard(k)
+
+    def begin(self, rvs: Dict[str, Any]) -> None:
+        self.want = {k: int(v) for k, v in rvs.items()}
+        store = self.inf.store
+        self.pending = {k for k, w in self.want.items() if k in store and self._rv(store[k]) < w}
+
+
+def job_informer(mgr, rec, gvr: GroupVersionResource = None):
+    """The operator's own informer of the bench's job kind (cache mode: the label-indexed child
+    informer; live mode: the owned-kind watch) -- not a shard assigner's "unassigned" watch."""
+    gvr = gvr or PYTORCHJOBS
+    for inf in list(rec.child_informers.values()) + mgr.cache.informers():
+        if inf.target == gvr and "notin" not in (inf.label_selector or ""):
+            return inf
+    raise RuntimeError(f"no informer for {gvr}")
+
+
+def lifecycle_stages(cfg: "BenchConfig") -> int:
+    """Training-operator status writes per job before the final Succeeded one (0: instant)."""
+    if cfg.lifecycle != "realistic":
+        return 0
+    from ..trainingop.operator import lifecycle_statuses
+
+    return len(lifecycle_statuses(pytorchjob_template(), "", "")) - 1
+
+
 def fired_pred(tick_ns: int, want_hist: int):
     """Status of a Cron that ran tick ``tick_ns``: one active job, ``want_hist`` in history."""
     from ..utils.gotime import UTC, GoTime
@@ -357,10 +428,38 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
             async with admin.post(remote.url + "/debug/fake/clock", json={"nowNs": ns}) as r:
                 await r.read()
 
-    async def complete_jobs(tick_ns: int) -> None:
+    def _ts(ns: int) -> str:
         from ..utils.gotime import UTC, GoTime
 
-        ts = GoTime(tick_ns // NANOS, 0, UTC).rfc3339()
+        return GoTime(ns // NANOS, 0, UTC).rfc3339()
+
+    async def job_stage(stage: int, start_ns: int, end_ns: int) -> Dict[str, Any]:
+        """Write lifecycle stage ``stage`` (-1: Succeeded) to every unfinished job; returns
+        ``{namespace/name: resourceVersion}`` of the writes."""
+        start, end = _ts(start_ns), _ts(end_ns)
+        if server is not None:
+            from ..trainingop.operator import lifecycle_status
+
+            rvs: Dict[str, Any] = {}
+            for obj in list(server.objects(PYTORCHJOBS, cfg.namespace)):
+                if (obj.get("status") or {}).get("completionTime"):
+                    continue
+                m = obj["metadata"]
+                out = server.patch(PYTORCHJOBS, cfg.namespace, m["name"],
+                                   {"status": lifecycle_status(obj, stage, start, end)}, "merge", "status")
+                rvs[f"{cfg.namespace}/{m['name']}"] = out["metadata"]["resourceVersion"]
+            return rvs
+        async with admin.post(remote.url + "/debug/fake/lifecycle",
+                              json={"namespace": cfg.namespace, "stage": stage, "start": start,
+                                    "end": end}) as r:
+            return (await r.json())["resourceVersions"]
+
+    async def complete_jobs(tick_ns: int) -> None:
+        ts = _ts(tick_ns)
+        if cfg.lifecycle == "realistic":
+            # the jobs of the previous tick were admitted a second after it
+            await job_stage(-1, tick_ns - 29 * NANOS, tick_ns)
+            return
         if server is not None:
             from ..trainingop.operator import finished_status
 
@@ -427,7 +526,7 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
             if remote is None:
                 raise ValueError("shards > 1 needs transport='http'")
             await setup_client.close()
-            return await _run_sharded(cfg, remote, admin, set_time, complete_jobs, on_step)
+            return await _run_sharded(cfg, remote, admin, set_time, complete_jobs, on_step, job_stage)
 
         client = Client(transport, qps=cfg.qps, burst=cfg.burst, max_inflight=cfg.max_inflight)
         opts = ReconcilerOptions.reference() if cfg.mode == "reference" else \
@@ -478,6 +577,28 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
                     return
                 await asyncio.sleep(0.002)
 
+        n_pre = lifecycle_stages(cfg)
+        rv_tracker = RvTracker(job_informer(mgr, rec)) if n_pre else None
+        write_cpu = [0.0]  # apiserver CPU s inside the harness's lifecycle write calls
+
+        async def run_lifecycle(tick_ns: int, deadline: float) -> float:
+            """The previous tick's jobs start: each training-operator write reaches every job,
+            then the operator absorbs it (its informer saw every write, nothing queued).
+            Returns the seconds spent inside the harness's write calls."""
+            writes = 0.0
+            for s in range(n_pre):
+                w0 = time.perf_counter()
+                c0 = _cpu_times(remote)[1]
+                rvs = await job_stage(s, tick_ns - 59 * NANOS, tick_ns - 30 * NANOS)
+                writes += time.perf_counter() - w0
+                write_cpu[0] += _cpu_times(remote)[1] - c0
+                rv_tracker.begin(rvs)
+                while rv_tracker.pending or not ctrl.queue.idle() or ctrl.in_flight():
+                    if time.monotonic() > deadline:
+                        raise TimeoutError(f"lifecycle stage {s} was not absorbed")
+                    await asyncio.sleep(0.002)
+            return writes
+
         await ctrl.wait_idle(timeout=600)
         startup_first_pass_s = time.perf_counter() - t_start0
 
@@ -488,7 +609,10 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
         rec0 = req0 = 0
         reqv0: Dict[str, int] = {}
         t_start = 0.0
+        excluded = 0.0  # timed steps: seconds inside the harness's lifecycle write calls
         phase_ms: Dict[str, List[float]] = {"completion": [], "fire": []}
+        if n_pre:
+            phase_ms["lifecycle_writes"] = []
         for k in range(1, total + 1):
             tick_ns = T0_NS + k * 60 * NANOS
             if k == cfg.warmup + 1:
@@ -500,12 +624,19 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
                 rec0 = ctrl.reconciles
                 req0 = client.requests
                 reqv0 = dict(client.requests_by_verb)
+                write_cpu[0] = 0.0
                 t_start = time.perf_counter()
             deadline = time.monotonic() + cfg.step_timeout
             t0 = time.perf_counter()
+            writes = 0.0
             if k > 1:
-                # the previous tick's jobs finish half a minute before this tick (cluster side; the
-                # apiserver work of marking them is inside the timed region -- conservative)
+                # the previous tick's jobs run (realistic lifecycle: the operator's absorption of
+                # each write is timed, the harness's write calls themselves are not -- they are
+                # another controller's requests) and finish half a minute before this tick
+                # (cluster side; the apiserver work of that last write is inside the timed
+                # region -- conservative)
+                if n_pre:
+                    writes = await run_lifecycle(tick_ns, deadline)
                 await complete_jobs(tick_ns - 30 * NANOS)
                 await set_time(tick_ns - 30 * NANOS)
                 await wait_completed(deadline)
@@ -516,15 +647,18 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
             await set_time(tick_ns)
             await wait_settled(tick_ns, k, deadline)
             t2 = time.perf_counter()
-            dt = t2 - t0
+            dt = t2 - t0 - writes
             if k > cfg.warmup:
                 step_ms.append(dt * 1000)
-                phase_ms["completion"].append((t1 - t0) * 1000)
+                phase_ms["completion"].append((t1 - t0 - writes) * 1000)
                 phase_ms["fire"].append((t2 - t1) * 1000)
+                if n_pre:
+                    phase_ms["lifecycle_writes"].append(writes * 1000)
+                excluded += writes
                 timed_lat.extend(lat)
             if on_step is not None:
                 on_step(k, dt, k > cfg.warmup)
-        elapsed = time.perf_counter() - t_start
+        elapsed = time.perf_counter() - t_start - excluded
         cpu1 = _cpu_times(remote)
         gc_stats = gcs.stop().to_dict() if cfg.warmup < total else {}
         if cfg.apiserver_profile and admin is not None:
@@ -544,7 +678,7 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
             api_requests_per_fire=requests / fires, api_requests_by_verb=by_verb,
             reconciles_per_fire=reconciles / fires, step_ms=step_ms, phase_ms=phase_ms,
             engine=default_engine().name, fastjson_native=jsonutil.NATIVE,
-            cpu_s_operator=cpu1[0] - cpu0[0], cpu_s_apiserver=cpu1[1] - cpu0[1], operator_gc=gc_stats,
+            cpu_s_operator=cpu1[0] - cpu0[0], cpu_s_apiserver=cpu1[1] - cpu0[1] - write_cpu[0], operator_gc=gc_stats,
             startup_sync_s=startup_sync_s, startup_first_pass_s=startup_first_pass_s)
         mgr.stop()
         try:
@@ -581,7 +715,7 @@ class _Shard:
 
 
 async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_time, complete_jobs,
-                       on_step) -> BenchResult:
+                       on_step, job_stage=None) -> BenchResult:
     """The step loop of :func:`run` with the operator split over ``cfg.shards`` processes."""
     from ..cron.engine import default_engine
     from ..utils import jsonutil
@@ -613,6 +747,7 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
                                    for s in shards))
             return list(await asyncio.gather(*(s.recv(cfg.step_timeout) for s in shards)))
 
+        n_pre = lifecycle_stages(cfg)
         total = cfg.warmup + cfg.steps
         step_ms: List[float] = []
         phase_ms: Dict[str, List[float]] = {"completion": [], "fire": []}
@@ -621,6 +756,10 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
         last: List[Dict[str, Any]] = []
         api0 = api1 = 0.0
         t_start = 0.0
+        excluded = 0.0
+        write_cpu = 0.0
+        if n_pre:
+            phase_ms["lifecycle_writes"] = []
         for k in range(1, total + 1):
             tick_ns = T0_NS + k * 60 * NANOS
             if k == cfg.warmup + 1:
@@ -633,7 +772,17 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
                 api0 = _cpu_times(remote)[1]
                 t_start = time.perf_counter()
             t0 = time.perf_counter()
+            writes = 0.0
             if k > 1:
+                for st in range(n_pre):  # the previous tick's jobs start (realistic lifecycle)
+                    w0 = time.perf_counter()
+                    c0 = _cpu_times(remote)[1]
+                    rvs = await job_stage(st, tick_ns - 59 * NANOS, tick_ns - 30 * NANOS)
+                    writes += time.perf_counter() - w0  # the harness's write call: not timed
+                    if k > cfg.warmup:
+                        write_cpu += _cpu_times(remote)[1] - c0
+                    await asyncio.gather(*(s.send({"cmd": "absorb", "rvs": rvs}) for s in shards))
+                    await asyncio.gather(*(s.recv(cfg.step_timeout) for s in shards))
                 await complete_jobs(tick_ns - 30 * NANOS)
                 await set_time(tick_ns - 30 * NANOS)
                 await phase(tick_ns - 30 * NANOS, "completion", tick_ns)
@@ -644,14 +793,17 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
             if k == cfg.warmup:
                 base = last
             if k > cfg.warmup:
-                step_ms.append((t2 - t0) * 1000)
-                phase_ms["completion"].append((t1 - t0) * 1000)
+                step_ms.append((t2 - t0 - writes) * 1000)
+                phase_ms["completion"].append((t1 - t0 - writes) * 1000)
                 phase_ms["fire"].append((t2 - t1) * 1000)
+                if n_pre:
+                    phase_ms["lifecycle_writes"].append(writes * 1000)
+                excluded += writes
                 for r in last:
                     timed_lat.extend(r["lat"])
             if on_step is not None:
-                on_step(k, t2 - t0, k > cfg.warmup)
-        elapsed = time.perf_counter() - t_start
+                on_step(k, t2 - t0 - writes, k > cfg.warmup)
+        elapsed = time.perf_counter() - t_start - excluded
         api1 = _cpu_times(remote)[1]
         if cfg.shard_profile:
             await asyncio.gather(*(s.send({"cmd": "profile", "action": "stop",
@@ -679,7 +831,8 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
             api_requests_per_fire=requests / fires, api_requests_by_verb=by_verb,
             reconciles_per_fire=reconciles / fires, step_ms=step_ms, phase_ms=phase_ms,
             engine=default_engine().name, fastjson_native=jsonutil.NATIVE,
-            cpu_s_operator=sum(r["cpu"] - b["cpu"] for r, b in zip(last, base)), cpu_s_apiserver=api1 - api0,
+            cpu_s_operator=sum(r["cpu"] - b["cpu"] for r, b in zip(last, base)),
+            cpu_s_apiserver=api1 - api0 - write_cpu,
             operator_maxrss_mib=[round(r.get("maxrss_mib", 0.0), 1) for r in last],
             operator_gc={"collections": [sum(r.get("gc_collections", [0, 0, 0])[g] - b.get("gc_collections",
                                                                                             [0, 0, 0])[g]

@@ -11,6 +11,9 @@ over a line protocol on stdin/stdout:
     set this shard's (fake) clock and reply once every Cron it owns has settled
     for the phase: ``{"ok": true, "lat": [s, ...], "reconciles": n, "requests": n,
     "by_verb": {...}, "cpu": s, "maxrss_mib": peak RSS}`` (counters cumulative since start);
+``{"cmd": "absorb", "rvs": {"<namespace>/<job>": resourceVersion, ...}}``
+    reply ``{"ok": true}`` once this shard's job informer saw each of those writes (of the jobs
+    it holds) and nothing is queued or in flight -- a lifecycle stage absorbed;
 ``{"cmd": "stop"}``
     shut the manager down and exit.
 
@@ -98,9 +101,10 @@ async def main() -> int:
         await asyncio.sleep(0.05)
     await ctrl.wait_idle(timeout=120)
 
-    from .harness import SettleTracker, completed_pred, fired_pred
+    from .harness import RvTracker, SettleTracker, completed_pred, fired_pred, job_informer
 
     tracker = SettleTracker(cron_inf, owned_keys)
+    rv_tracker = RvTracker(job_informer(mgr, rec))
     n_owned = len(owned_keys)
     lat: List[float] = []
     tick_wall = [0.0]
@@ -148,6 +152,13 @@ async def main() -> int:
                 prof.disable()
                 prof.dump_stats(msg["path"])
                 prof = None
+            out.write(json.dumps({"ok": True}) + "\n")
+            out.flush()
+            continue
+        if msg.get("cmd") == "absorb":  # a training-operator write reached every job: absorb it
+            rv_tracker.begin(msg.get("rvs") or {})
+            while rv_tracker.pending or not ctrl.queue.idle() or ctrl.in_flight():
+                await asyncio.sleep(0.002)
             out.write(json.dumps({"ok": True}) + "\n")
             out.flush()
             continue

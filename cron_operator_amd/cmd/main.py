@@ -2,7 +2,12 @@
 
 Reference: ``cmd/main.go:31-55`` (cobra root that prints help without a
 subcommand) and ``cmd/operator/start.go:61-265`` (the ``start`` command).  Every
-flag of the reference keeps its name, default and meaning:
+flag of the reference keeps its name and meaning, and every default but two: ``--qps`` /
+``--burst`` ship 150 / 300 instead of 30 / 50 (sized for 1000+ minutely Crons; a drop-in
+switch-over may send up to 5x the reference's client-side request rate, see
+docs/migration.md "Changed defaults").  ``--max-concurrent-reconciles`` bounds the reconciles
+*deciding* at once; a reconcile left with only API writes hands its slot on, and up to
+``max(1024, 100 x N)`` of those may be writing (``runtime/controller.py``):
 
 ==============================  ===========  ==========================================
 flag                            default      reference
@@ -84,7 +89,10 @@ def build_parser() -> argparse.ArgumentParser:
 
     st = sub.add_parser("start", help="Start manager")
     st.add_argument("--max-concurrent-reconciles", type=int, default=10,
-                    help="The maximum number of concurrent reconciles for controller.")
+                    help="The maximum number of concurrent reconciles for controller (reconciles deciding "
+                         "at once; one left with only API writes hands its slot on, and up to max(1024, 100 x "
+                         "this) such reconciles may be writing, their requests bounded by --qps and "
+                         "--max-inflight-requests).")
     st.add_argument("--qps", type=float, default=DEFAULT_QPS,
                     help="Maximum QPS to the Kubernetes API server from this client. About 4 requests per Cron "
                          "fire: N minutely Crons need N/15 QPS (default: 1000 Crons at 45%% of the budget).")

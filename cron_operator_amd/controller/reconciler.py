@@ -38,6 +38,14 @@ option                     default here                           reference
                            first on a backed-up QPS bucket;        request
                            status PATCHes / GC DELETEs / events
                            yield to them
+``active_ref_resource_``   ``first``: an active ref keeps the      ``live``: rebuilt with the child's
+``version``                resourceVersion the child entered       current resourceVersion on every
+                           ``status.active`` with (Kubernetes      reconcile (``:284-304``), so every
+                           CronJob semantics)                      training-operator status write costs
+                                                                   the Cron a status PATCH
+``skip_unchanged_child_``  a child update that changes nothing a   every owned-child event requeues
+``updates``                reconcile reads (Created / replica      the Cron (B22)
+                           counts / Running writes) is dropped
 =========================  =====================================  =======================================
 
 ``defer_status_write`` (under a controller worker, ``runtime/controller.py`` ``release_worker``,
@@ -219,7 +227,15 @@ class ReconcilerOptions:
     skip_noop_patch: bool = True
     own_write_filter: bool = True
     dynamic_watches: bool = True
-    active_ref_resource_version: bool = True
+    # status.active[].resourceVersion: "first" -- the version the child had when it became active
+    # (as Kubernetes' CronJob controller records it); "live" -- its current version, rebuilt on
+    # every reconcile (cron_controller.go:284-304: each status write of the training-operator then
+    # costs the Cron a status PATCH); "omit" -- left empty
+    active_ref_resource_version: str = "first"
+    # a child update that changes nothing a reconcile reads (classification, completion time,
+    # labels, owner, deletion) does not requeue the Cron -- the training-operator's Created /
+    # replicaStatuses / Running writes -- unless active refs track the live resourceVersion
+    skip_unchanged_child_updates: bool = True
     expectations: bool = True
     expectation_ttl: float = 300.0           # seconds on the injected clock
     fold_created_into_active: bool = True    # add the just-created child to status.active right away
@@ -247,6 +263,7 @@ class ReconcilerOptions:
     @staticmethod
     def reference() -> "ReconcilerOptions":
         return ReconcilerOptions(list_mode="live", finished_time="now", skip_noop_patch=False,
+                                 active_ref_resource_version="live", skip_unchanged_child_updates=False,
                                  own_write_filter=False, dynamic_watches=False, expectations=False,
                                  fold_created_into_active=False, skip_expected_events=False,
                                  classification_cache=False, dedupe_ran_tick=False,
@@ -661,6 +678,7 @@ class CronReconciler(Reconciler):
                 continue
             info.obj = w  # this reconcile's copy (a live LIST returns new objects every time)
             info.name = m.get("name", "")
+            info.uid = m.get("uid", "")
             (terminated if info.finished else active).append(info)
         chatty = log.enabled()  # info logging on: skip building messages nobody writes otherwise
         if chatty:
@@ -793,7 +811,8 @@ class CronReconciler(Reconciler):
                 cron.status.active.append(ObjectReference(
                     api_version=cgvk.api_version, kind=cgvk.kind, name=cm.get("name", ""),
                     namespace=cm.get("namespace", ""), uid=cm.get("uid", ""),
-                    resource_version=cm.get("resourceVersion", "") if self.opts.active_ref_resource_version else ""))
+                    resource_version=cm.get("resourceVersion", "")
+                    if self.opts.active_ref_resource_version != "omit" else ""))
             if self.latency_observer is not None:
                 self.latency_observer(self._ckey(cron), missed_run, created)
             self._m_sched_lat.observe(
@@ -961,8 +980,16 @@ class CronReconciler(Reconciler):
         if not presorted:
             self._sort(active)
         refs = []
-        with_rv = self.opts.active_ref_resource_version
+        rv_mode = self.opts.active_ref_resource_version
+        with_rv = rv_mode != "omit"
+        # "first": a child already listed keeps the reference it entered status.active with
+        prev = {r.uid: r for r in cron.status.active if r.uid} if rv_mode == "first" and cron.status.active \
+            else None
         for info in active:
+            ref = prev.get(info.uid) if prev else None
+            if ref is not None:
+                refs.append(ref)
+                continue
             ref = info.active_ref
             if ref is None:
                 w = info.obj

@@ -23,6 +23,7 @@ from ..api import errors
 from ..api.meta import GroupVersionKind
 from ..api.v1alpha1 import CRON_GVK, LABEL_CRON_NAME
 from ..cron.engine import CronEngine
+from ..models.workload import WorkloadPolicy, classify
 from ..runtime.controller import Controller
 from ..runtime.informer import EventHandler, Informer, label_index, strip_managed_fields
 from ..runtime.manager import Manager
@@ -31,6 +32,28 @@ from . import sharding
 from .reconciler import CHILD_INDEX, CronReconciler, ReconcilerOptions, WireCodecs, slim_child
 
 CONTROLLER_NAME = "cron"
+
+# child metadata a reconcile reads: identity, the cron-name label and owner (which Cron lists it),
+# creation time (history order), deletion
+_CHILD_META = ("name", "namespace", "uid", "labels", "ownerReferences", "creationTimestamp",
+               "deletionTimestamp")
+
+
+def child_update_matters(old, new, gvk: GroupVersionKind, policy: WorkloadPolicy) -> bool:
+    """Can this child update change its Cron's reconcile?  Not when the child stays running and
+    nothing a reconcile reads moved: its active ref keeps the resourceVersion it entered
+    ``status.active`` with (``active_ref_resource_version="first"``), and an unfinished child's
+    status feeds nothing else.  The training-operator's Created / replicaStatuses / Running
+    writes are such updates (``/root/reference/test/crds/kubeflow.org_pytorchjobs.yaml:4739-4828``);
+    the reference requeues the Cron on each (``cron_controller.go:70-77``, no predicates)."""
+    om, nm = old.get("metadata") or {}, new.get("metadata") or {}
+    for k in _CHILD_META:
+        if om.get(k) != nm.get(k):
+            return True
+    try:
+        return classify(old, gvk, policy).finished or classify(new, gvk, policy).finished
+    except Exception:  # noqa: BLE001 - an unreadable status: let the reconcile report it
+        return True
 
 
 async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] = None,
@@ -60,10 +83,14 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
         await assigner.watch(mgr.cache, CRON_GVK, child=False)
         mgr.add(assigner.run)
     rec.shard_assigner = assigner
-    if assigner is not None:
+    if assigner is not None and opts.list_mode == "cache":
+        # a Cron joins this shard only once its relabelled children are in this shard's child
+        # informers.  A kind with no informer yet is not waited for: the first reconcile that
+        # needs it starts the informer and waits for its LIST, which holds the child.  Live mode
+        # (--compat-mode reference) LISTs children from the apiserver: nothing to wait for.
         def observed(gvk: GroupVersionKind, ns: str, name: str) -> bool:
             inf = rec.child_informers.get(gvk)
-            return inf is not None and inf.get(ns, name, copy=False) is not None
+            return inf is None or inf.get(ns, name, copy=False) is not None
         assigner.observed = observed
 
     preds = []
@@ -95,6 +122,12 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
                     return not ex.deleted or not ex.matches_deleted(key_of(new), new)
                 return True
             owned_preds.append(not_expected)
+        if opts.skip_unchanged_child_updates and opts.active_ref_resource_version != "live":
+            policy = opts.workload
+
+            def changed(event: str, old, new, g=gvk) -> bool:
+                return event != "update" or old is None or child_update_matters(old, new, g, policy)
+            owned_preds.append(changed)
         ctrl.watch_owned(inf, CRON_GVK, owned_preds)
         if assigner is not None:
             assigner.watch_soon(mgr.cache, gvk, child=True)

@@ -33,7 +33,9 @@ would miss the job it must delete, and ``status.active``/``history`` would drop
 entries.  This matters on the first start with label routing (a fresh install or an
 upgrade from hash routing, where every object is unlabelled) and after a change of
 shard count.  The wait for the informers is bounded (``observe_timeout``); a child
-deleted meanwhile never shows up there and only costs that bound.
+deleted meanwhile never shows up there and only costs that bound.  A child whose label
+PATCH keeps failing (403, a webhook's 422) is given up after ``max_child_attempts``:
+its Cron is then assigned without it instead of being parked for good.
 """
 from __future__ import annotations
 
@@ -89,7 +91,8 @@ class ShardAssigner:
     """Labels this shard's unassigned Crons and children (a leader-only runnable)."""
 
     def __init__(self, client: Client, index: int, count: int, workers: int = 4,
-                 retry_delay: float = 1.0, logger: Optional[Logger] = None, observe_timeout: float = 10.0):
+                 retry_delay: float = 1.0, logger: Optional[Logger] = None, observe_timeout: float = 10.0,
+                 max_child_attempts: int = 5):
         if count < 1 or not 0 <= index < count:
             raise ValueError(f"invalid shard {index}/{count}")
         self.client = client
@@ -106,6 +109,12 @@ class ShardAssigner:
         self.errors = 0
         self._bg: Set[asyncio.Task] = set()
         self.observe_timeout = observe_timeout
+        # a child whose label PATCH keeps failing (403 on a kind without patch rights, 422 from
+        # an admission webhook) is given up after this many attempts, so its Cron is not parked
+        # for good; a later event on the child offers it again
+        self.max_child_attempts = max(1, max_child_attempts)
+        self._attempts: Dict[Tuple[GroupVersionKind, str, str], int] = {}
+        self.abandoned = 0
         self._child_kinds: Set[GroupVersionKind] = set()
         # (namespace, cron) -> child keys queued for labelling / labelled but maybe not observed yet
         self._children_left: Dict[Tuple[str, str], Set[Tuple[GroupVersionKind, str, str]]] = {}
@@ -228,19 +237,40 @@ class ShardAssigner:
                     self.log.error(e, "Failed to assign shard", kind=gvk.kind, namespace=ns, name=name)
                     await asyncio.sleep(self.retry_delay)
                     inf = self.informers.get(gvk)
-                    if inf is not None and inf.get(ns, name, copy=False) is not None:
+                    if inf is not None and inf.get(ns, name, copy=False) is not None \
+                            and not (child and self._give_up(key)):
                         self._queue.put_nowait(key)  # still unassigned: retry
                         continue
                 if child:
                     self._child_finished(key, False)
+                self._attempts.pop(key, None)
                 self._queued.discard(key)
                 continue
             except Exception as e:  # noqa: BLE001 - transport errors: retry later
                 self.errors += 1
                 self.log.error(e, "Failed to assign shard", kind=gvk.kind, namespace=ns, name=name)
                 await asyncio.sleep(self.retry_delay)
+                if child and self._give_up(key):
+                    self._child_finished(key, False)
+                    self._attempts.pop(key, None)
+                    self._queued.discard(key)
+                    continue
                 self._queue.put_nowait(key)
                 continue
             if child:
                 self._child_finished(key, True)
+            self._attempts.pop(key, None)
             self._queued.discard(key)
+
+    def _give_up(self, key: Tuple[GroupVersionKind, str, str]) -> bool:
+        """Count a failed label PATCH of child ``key``; True once it reached ``max_child_attempts``
+        (the caller then releases the child's Cron, which is assigned without it)."""
+        n = self._attempts.get(key, 0) + 1
+        if n < self.max_child_attempts:
+            self._attempts[key] = n
+            return False
+        self.abandoned += 1
+        gvk, ns, name = key
+        self.log.info("Giving up labelling a child; its Cron is assigned without it", kind=gvk.kind,
+                      namespace=ns, name=name, attempts=n)
+        return True

@@ -106,6 +106,9 @@ class LeaderElector:
         self.observed_spec: Optional[Dict[str, Any]] = None
         self.observed_time_ns = 0
         self._lease: Optional[Dict[str, Any]] = None
+        # the longest successful renewal window so far (injected clock, seconds): a renewal that
+        # waits behind other traffic shows here long before it reaches renew_deadline
+        self.max_renew_s = 0.0
         self._m = metrics.LEADER_STATUS.labels(name)
         self.log = get_logger("leaderelection").with_values(lease=f"{namespace}/{name}", identity=self.identity)
 
@@ -224,9 +227,16 @@ class LeaderElector:
     async def renew_once(self) -> bool:
         """One renewal window: try now, then every ``retryPeriod``, all of it (in-flight
         requests included) bounded by ``renewDeadline``."""
-        deadline = self.clock.now_ns() + int(self.renew_deadline * NANOS)
+        t0 = self.clock.now_ns()
+        deadline = t0 + int(self.renew_deadline * NANOS)
         while True:
             if await self._try_until(deadline):
+                took = (self.clock.now_ns() - t0) / NANOS
+                if took > self.max_renew_s:
+                    self.max_renew_s = took
+                if took > self.retry_period:
+                    self.log.info("slow lease renewal", seconds=round(took, 3),
+                                  renewDeadline=self.renew_deadline)
                 return True
             if self.clock.now_ns() >= deadline:
                 return False

@@ -282,9 +282,11 @@ class Client:
 
     def __init__(self, transport: Transport, qps: float = 30.0, burst: int = 50,
                  limiter: Optional[TokenBucket] = None, mapper: Optional[RESTMapper] = None,
-                 max_inflight: int = 0):
+                 max_inflight: int = 0, gauges: bool = True):
         """``max_inflight`` > 0 caps concurrent requests (watches excluded); excess requests
-        wait in priority order (:class:`~.ratelimit.InflightGate`)."""
+        wait in priority order (:class:`~.ratelimit.InflightGate`).  ``gauges``: publish this
+        client's gates as ``rest_client_requests_{in_flight,waiting}`` (the main client does; a
+        derived side client does not overwrite its series)."""
         self.transport = transport
         self.limiter = limiter if limiter is not None else make_client_limiter(qps, burst)
         self.inflight: Optional[InflightGate] = InflightGate(max_inflight) if max_inflight > 0 else None
@@ -296,7 +298,8 @@ class Client:
         self.requests_by_verb: Dict[str, int] = {}
         self._m_verb: Dict[str, Tuple[Dict[str, Any], Any]] = {}  # verb -> ({code: counter}, latency histogram)
         self._m_rl: Dict[str, Any] = {}
-        self._observe_gates()
+        if gauges:
+            self._observe_gates()
         # Retry-After retries (429 / 5xx from an apiserver shedding load, client-go rest.Request):
         # an HTTP transport leaves them to the client, so each attempt is throttled and gated anew
         self._retries_here = hasattr(transport, "retry_in_client")
@@ -314,6 +317,20 @@ class Client:
             for prio, label in ((PRIORITY_HIGH, "high"), (PRIORITY_NORMAL, "normal"), (PRIORITY_LOW, "low")):
                 metrics.REST_WAITING.observe((self.host, gate_name, label), gate,
                                              lambda g, p=prio: g.waiting_at(p))
+
+    def derive(self) -> "Client":
+        """A side client over the same transport (connections, credentials, REST mapping) with
+        its **own** QPS bucket of the same ``qps``/``burst`` and **no** in-flight cap.
+
+        controller-runtime builds the leader-election resource lock from a copy of the rest
+        config (``leaderelection.NewResourceLock`` -> ``NewForConfig``) [ext], so the Lease
+        requests get a token bucket of their own: the reference's ``--qps``/``--burst``
+        (``/root/reference/cmd/operator/start.go:152-154``) bound the reconciler's traffic
+        and, separately, the lock's -- a throttled tick can never hold a renewal back."""
+        lim = self.limiter
+        side = Client(self.transport, limiter=TokenBucket(lim.qps, lim.burst, lim.max_defer) if lim else None,
+                      qps=-1 if lim is None else lim.qps, mapper=self.mapper, gauges=False)
+        return side
 
     def gate_saturated(self) -> bool:
         """Is the in-flight cap the bottleneck right now (every slot taken, QPS bucket idle)?

@@ -25,9 +25,17 @@ before -- so per-key serialisation and the no-duplicate guarantee are unchanged.
 reference's deferred status patch (``cron_controller.go:107-120``) runs on the worker after
 the CREATE (``:229-238``): under apiserver latency a fire holds a worker for two sequential
 write round trips; with a released slot it holds it for none.  ``max_released`` bounds the
-reconciles writing after a release (the controller runs that many extra worker tasks; with
-all of them busy, new keys wait for a worker as usual).  Workers are long-lived tasks: a
-release costs two counter updates, not a task.
+reconciles writing after a release (with that many writing, new keys wait for a worker as
+usual).  Workers are long-lived tasks started on demand: ``max_concurrent`` at start, and one
+more only when a release finds no parked worker to take its slot -- a controller whose
+reconciler never releases (``--compat-mode reference``) runs exactly ``max_concurrent``, and
+one that does keeps as many spares as releases ever overlapped.  A release costs two counter
+updates, not a task.
+
+The bound is deliberately not the client's in-flight cap: under a backed-up QPS bucket the
+released reconciles' writes wait *in the bucket*, where a tick's CREATEs overtake status
+PATCHes (``runtime/ratelimit.py``); capping writers at the in-flight cap would move that
+wait back into the work queue, where it is FIFO.
 """
 from __future__ import annotations
 
@@ -156,6 +164,7 @@ class Controller:
         self.releases = 0        # release_worker() calls, total
         self._free_slots = self.max_concurrent
         self._slot_waiters: Deque[asyncio.Future] = deque()
+        self._spawned = 0  # worker tasks started (max_concurrent at start, more on demand)
         metrics.RECONCILES_WRITING.observe((name,), self, lambda c: c.released)
         metrics.WORKER_RELEASES.observe((name,), self, lambda c: c.releases)
         self.reconciles = 0
@@ -308,6 +317,15 @@ class Controller:
         self.released += 1
         self.releases += 1
         self._m_active.value = float(self.active)
+        if not self._slot_waiters and self.started and self._spawned < self.max_concurrent + self.max_released:
+            # no parked worker to take the slot about to be freed: start one (spare workers
+            # exist only as many as releases ever overlapped, up to max_released)
+            self._spawn_worker()
+
+    def _spawn_worker(self) -> None:
+        self._workers.append(asyncio.get_running_loop().create_task(
+            self._worker(), name=f"{self.name}-worker-{self._spawned}"))
+        self._spawned += 1
 
     async def process_one(self, req: Request) -> None:
         log = self._logger_for(req)
@@ -411,9 +429,11 @@ class Controller:
             return
         self.started = True
         loop = asyncio.get_running_loop()
-        # max_concurrent workers decide at any time; max_released more may still be writing
-        for i in range(self.max_concurrent + self.max_released):
-            self._workers.append(loop.create_task(self._worker(), name=f"{self.name}-worker-{i}"))
+        # max_concurrent workers decide at any time; up to max_released more are started on
+        # demand, when a release finds no parked worker to hand its slot to (_on_release)
+        self._spawned = 0
+        for _ in range(self.max_concurrent):
+            self._spawn_worker()
         self._workers.append(loop.create_task(self._unfinished_loop(), name=f"{self.name}-metrics"))
 
     async def _unfinished_loop(self, interval: float = 0.5) -> None:

@@ -70,8 +70,15 @@ class ManagerOptions:
 
 
 class Manager:
-    def __init__(self, client: Client, options: Optional[ManagerOptions] = None):
+    def __init__(self, client: Client, options: Optional[ManagerOptions] = None,
+                 lease_client: Optional[Client] = None):
+        """``lease_client``: the client the leader elector uses.  Default: derived from
+        ``client`` when the election starts (:meth:`Client.derive`) -- same connections and
+        credentials, its own QPS bucket, no in-flight cap -- as controller-runtime gives the
+        resource lock a client of its own (``/root/reference/cmd/operator/start.go:156-177``
+        [ext]).  Passing ``client`` itself shares the reconciler's budget (a test control)."""
         self.client = client
+        self.lease_client = lease_client
         self.opts = options or ManagerOptions()
         self.clock = self.opts.clock
         self.cache = Cache(client, self.opts.namespace, self.opts.sync_period, self.clock,
@@ -145,7 +152,9 @@ class Manager:
                 ns = self.opts.leader_election_namespace or in_cluster_namespace()
                 lease = self.opts.leader_election_id if self.opts.shard_count <= 1 else \
                     f"{self.opts.leader_election_id}-shard-{self.opts.shard_index}"
-                self.elector = LeaderElector(self.client, lease, ns,
+                if self.lease_client is None:
+                    self.lease_client = self.client.derive()
+                self.elector = LeaderElector(self.lease_client, lease, ns,
                                              self.opts.leader_election_identity, self.clock,
                                              self.opts.lease_duration, self.opts.renew_deadline,
                                              self.opts.retry_period,

@@ -8,8 +8,9 @@ the reference tests cannot observe a job finishing.  This component fills
 that gap in three modes:
 
 * ``manual`` -- the test/bench calls :meth:`complete` / :meth:`complete_all`;
-* ``timed``  -- jobs become Running at once and Succeeded after ``duration``
-  seconds of (possibly virtual) clock time;
+* ``timed``  -- jobs go through the training-operator's status sequence (Created, one
+  ``replicaStatuses`` write per pod, Running: :func:`lifecycle_statuses`) and become
+  Succeeded ``duration`` seconds of (possibly virtual) clock time after admission;
 * ``real``   -- each replica's container ``command``/``args`` runs as a local
   subprocess with the env the training-operator injects for PyTorchJob
   (``MASTER_ADDR``/``MASTER_PORT``/``WORLD_SIZE``/``RANK``); the job succeeds or
@@ -83,12 +84,88 @@ def finished_status(kind: str, name: str, ts: str, succeeded: bool, start: Optio
     return st
 
 
+def replica_counts(obj: Dict[str, Any]) -> List[Tuple[str, int]]:
+    """``[(replica type, replicas)]`` of a Kubeflow job, master-like types first."""
+    spec = obj.get("spec") or {}
+    specs = next((v for k, v in spec.items() if k.endswith("ReplicaSpecs") and isinstance(v, dict)), None) \
+        if isinstance(spec, dict) else None
+    if not specs:
+        return []
+    order = sorted(specs, key=lambda t: _MASTER_TYPES.index(t) if t in _MASTER_TYPES else 99)
+    return [(t, int((specs[t] or {}).get("replicas", 1) or 1)) for t in order]
+
+
+def lifecycle_statuses(obj: Dict[str, Any], start: str, end: str, succeeded: bool = True) -> List[Dict[str, Any]]:
+    """The status writes the Kubeflow training-operator makes over one job's life, in order.
+
+    ``Created`` on admission (with ``startTime`` and an empty ``replicaStatuses`` entry per
+    replica type); one write per pod as it starts (``replicaStatuses[type].active`` counting up);
+    ``Running``; then ``Succeeded`` / ``Failed`` with ``completionTime`` (the ``JobStatus``
+    schema of ``/root/reference/test/crds/kubeflow.org_pytorchjobs.yaml:4739-4828``).  Every
+    write changes the job's resourceVersion: an operator that folds it into ``status.active``
+    pays a Cron status PATCH per write (reference ``cron_controller.go:284-304``)."""
+    kind, name = obj.get("kind", ""), (obj.get("metadata") or {}).get("name", "")
+    created = _cond("Created", f"{kind}Created", f"{kind} {name} is created.", start)
+    reps = replica_counts(obj)
+    rs: Dict[str, Dict[str, Any]] = {t: {} for t, _ in reps}
+
+    def snap(conds: List[Dict[str, Any]]) -> Dict[str, Any]:
+        return {"conditions": [dict(c) for c in conds], "startTime": start,
+                "replicaStatuses": {t: dict(v) for t, v in rs.items()}}
+
+    out = [snap([created])]
+    for t, n in reps:
+        for i in range(n):
+            rs[t]["active"] = i + 1
+            out.append(snap([created]))
+    running = _cond("Running", f"{kind}Running", f"{kind} {name} is running.", start)
+    out.append(snap([created, running]))
+    for t, n in reps:
+        rs[t] = {"succeeded": n} if succeeded else {"failed": n}
+    fin = finished_status(kind, name, end, succeeded, start)
+    fin["replicaStatuses"] = {t: dict(v) for t, v in rs.items()}
+    out.append(fin)
+    return out
+
+
+def lifecycle_status(obj: Dict[str, Any], stage: int, start: str, end: str,
+                     reps: Optional[List[Tuple[str, int]]] = None) -> Dict[str, Any]:
+    """Stage ``stage`` of :func:`lifecycle_statuses` (negative: from the end) without building the
+    others -- the bench writes one stage to every job at a time.  ``reps``: the job's
+    :func:`replica_counts`, when the caller knows them already."""
+    reps = replica_counts(obj) if reps is None else reps
+    n = 3 + sum(k for _, k in reps)
+    if stage < 0:
+        stage += n
+    if not 0 <= stage < n:
+        raise IndexError(stage)
+    if stage == n - 1:
+        return lifecycle_statuses(obj, start, end)[-1]
+    kind, name = obj.get("kind", ""), (obj.get("metadata") or {}).get("name", "")
+    conds = [_cond("Created", f"{kind}Created", f"{kind} {name} is created.", start)]
+    if stage == n - 2:
+        conds.append(_cond("Running", f"{kind}Running", f"{kind} {name} is running.", start))
+    left = stage if stage < n - 2 else n
+    rs: Dict[str, Dict[str, Any]] = {}
+    for t, k in reps:
+        take = min(k, left)
+        left -= take
+        rs[t] = {"active": take} if take else {}
+    return {"conditions": conds, "startTime": start, "replicaStatuses": rs}
+
+
 class FakeTrainingOperator:
     def __init__(self, client: Client, clock: Optional[Clock] = None, mode: str = "manual", duration: float = 30.0,
                  namespace: str = "", kinds: Optional[List[GroupVersionResource]] = None,
-                 workdir: Optional[str] = None, env: Optional[Dict[str, str]] = None, timeout: float = 900.0):
+                 workdir: Optional[str] = None, env: Optional[Dict[str, str]] = None, timeout: float = 900.0,
+                 lifecycle: str = "realistic"):
+        """``lifecycle`` (timed mode): ``realistic`` writes the training-operator's status
+        sequence (:func:`lifecycle_statuses`); ``instant`` only Running, then Succeeded."""
         if mode not in ("manual", "timed", "real"):
             raise ValueError(f"unknown mode {mode}")
+        if lifecycle not in ("realistic", "instant"):
+            raise ValueError(f"unknown lifecycle {lifecycle}")
+        self.lifecycle = lifecycle
         self.client = client
         self.clock = clock or RealClock()
         self.mode = mode
@@ -159,9 +236,22 @@ class FakeTrainingOperator:
 
     async def _drive_timed(self, gvr: GroupVersionResource, obj: Dict[str, Any]) -> None:
         m = obj["metadata"]
-        await self.mark_running(gvr, obj)
+        if self.lifecycle == "instant" or _mpi_v1alpha1(gvr):
+            await self.mark_running(gvr, obj)
+            await self.clock.sleep(self.duration)
+            await self.complete(gvr, m["namespace"], m["name"], True)
+            return
+        # the training-operator's write sequence as the pods start (each its own write and
+        # resourceVersion, awaited in turn; no clock time passes, so a test's virtual clock
+        # sees Running at once as before), then Succeeded ``duration`` seconds after admission
+        start_ns = self.clock.now_ns()
+        start = _now_str(self.clock)
+        end = GoTime((start_ns + int(self.duration * 1e9)) // 1_000_000_000, 0, UTC).rfc3339()
+        stages = lifecycle_statuses(obj, start, end, True)
+        for st in stages[:-1]:
+            await self._write_status(gvr, m["namespace"], m["name"], st)
         await self.clock.sleep(self.duration)
-        await self.complete(gvr, m["namespace"], m["name"], True)
+        await self._write_status(gvr, m["namespace"], m["name"], stages[-1])
 
     # ------------------------------------------------------------------ real mode
     def _replica_processes(self, obj: Dict[str, Any]) -> List[Tuple[str, int, Dict[str, Any]]]:

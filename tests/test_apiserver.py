@@ -526,3 +526,50 @@ def test_indexed_watch_fanout_matches_per_watcher_selectors(ops, sels):
             etype, obj = w.queue.get_nowait()
             got.append((etype, obj["metadata"]["name"]))
         assert got == want[j], sels[j]
+
+
+def test_label_index_answers_pinned_selectors_like_a_scan():
+    """A LIST that pins ``key=value`` reads the label index (built on first use, kept current by
+    every write); its answer equals a full scan's, in key order, across label edits, deletes,
+    namespaces and paging."""
+    import random
+
+    from cron_operator_amd.api.selectors import compile_selectors
+
+    s = mk()
+    s.create_namespace("other")
+    rng = random.Random(3)
+    live = {}
+    for step in range(400):
+        ns = rng.choice(["default", "other"])
+        name = f"c{rng.randrange(40)}"
+        op = rng.random()
+        cur = live.get((ns, name))
+        if cur is None:
+            labels = {"k": rng.choice(["a", "b"]), "z": "1"} if rng.random() < 0.8 else {"z": "1"}
+            live[(ns, name)] = s.create(CM, ns, cm(name, labels))
+        elif op < 0.4:
+            s.delete(CM, ns, name)
+            del live[(ns, name)]
+        else:
+            v = rng.choice(["a", "b", None])
+            live[(ns, name)] = s.patch(CM, ns, name, {"metadata": {"labels": {"k": v}}}, "merge")
+        if step % 20 == 0:
+            for sel in ("k=a", "k=b", "k=a,z=1", "k=a,z!=1"):
+                for lns in ("default", "other", None):
+                    got = [(o["metadata"]["namespace"], o["metadata"]["name"]) for o in s.list(CM, lns, sel)["items"]]
+                    pred = compile_selectors(sel, None)
+                    want = sorted((k for k, o in live.items() if (lns is None or k[0] == lns) and pred(o)),
+                                  key=lambda k: (k[0], k[1]) if lns is None else k[1])
+                    if lns is None:
+                        assert sorted(got) == sorted(want), (sel, lns)
+                    else:
+                        assert got == sorted(want, key=lambda k: k[1]), (sel, lns)
+    assert ("", "configmaps") in s._label_idx and "k" in s._label_idx[("", "configmaps")]
+    page = s.list(CM, "default", "k=a", limit=2)
+    names = [o["metadata"]["name"] for o in page["items"]]
+    while page["metadata"].get("continue"):
+        page = s.list(CM, "default", "k=a", limit=2, continue_=page["metadata"]["continue"])
+        names += [o["metadata"]["name"] for o in page["items"]]
+    assert names == sorted(n for (ns, n), o in live.items() if ns == "default"
+                           and (o["metadata"].get("labels") or {}).get("k") == "a")

@@ -52,10 +52,12 @@ def chart_client_values():
     return float(v["qps"]), int(v["burst"])
 
 
-async def _run(qps: float, burst: int):
-    """-> (created {(cron, name)}, tick -> [create latency s], per-tick expected names)."""
+async def _run(qps: float, burst: int, fleet: int = FLEET, leader_elect: bool = False,
+               shared_lease_client: bool = False, stats: dict = None):
+    """-> (missing job names, tick -> [create latency s]).  ``stats`` (if given) receives the
+    leader elector's record: ``lost``, ``max_renew_s`` (virtual seconds), ``renewals``."""
     env = TestEnv()
-    sq, sb = qps * N * C / FLEET, max(1, round(burst * N / FLEET))
+    sq, sb = qps * N * C / fleet, max(1, round(burst * N / fleet))
     env.client.limiter = TokenBucket(sq, sb, max_defer=20.0 / C)
     trainer = FakeTrainingOperator(env.new_client(), env.clock, mode="timed", duration=30)
     created = {}
@@ -74,7 +76,21 @@ async def _run(qps: float, burst: int):
         c = new_cron(f"c{i:03d}", NS, "* * * * *", PT_TMPL, history_limit=2)
         await setup.create(GroupVersionResource("apps.kubedl.io", "v1alpha1", "crons"), c.to_dict(), NS)
     await trainer.start()
-    await env.start_manager()
+    if leader_elect:
+        # the chart's Deployment runs --leader-elect (values.yaml leaderElection.enable: true);
+        # lease timings are controller-runtime's 15 / 10 / 2 s, on the same virtual clock
+        from cron_operator_amd.controller.setup import setup_with_manager
+        from cron_operator_amd.runtime.manager import Manager, ManagerOptions
+
+        mopts = ManagerOptions(clock=env.clock, leader_election=True, leader_election_namespace=NS,
+                               leader_election_identity="leader", health_probe_bind_address="0",
+                               metrics_bind_address="0")
+        env.manager = Manager(env.client, mopts, lease_client=env.client if shared_lease_client else None)
+        env.controller, env.reconciler = await setup_with_manager(env.manager)
+        env._mgr_task = asyncio.get_running_loop().create_task(env.manager.start())
+        await asyncio.wait_for(env.manager.started.wait(), 30)
+    else:
+        await env.start_manager()
     await env.settle()
     tick_wall = {}
     start_min = env.clock.now_ns() // NANOS // 60 * 60
@@ -87,6 +103,10 @@ async def _run(qps: float, burst: int):
                 tick_wall[now_s] = time.perf_counter()
             await asyncio.sleep(STEP_S)
     finally:
+        el = env.manager.elector if env.manager is not None else None
+        if stats is not None and el is not None:
+            stats.update(lost=el.lost.is_set(), leader=el.is_leader, max_renew_s=el.max_renew_s,
+                         retry_period=el.retry_period)
         await trainer.stop()
         await env.stop()
     lat = {}
@@ -118,6 +138,30 @@ async def test_reference_client_budget_collapses_ticks_at_the_same_fleet():
     """The control: the reference chart's 30/50 cannot carry 1000 minutely Crons."""
     missing, _ = await _run(30.0, 50)
     assert missing, "expected collapsed ticks at the reference's qps 30 / burst 50"
+
+
+CLAIMED = 1800  # the fleet values.yaml's qps comment claims at 100% of the budget
+
+
+async def test_leader_keeps_the_lease_at_twice_the_claimed_fleet():
+    """Leader election on (as the chart installs it), chart qps/burst, 2x the claimed fleet: the
+    ticks overrun the budget, but the Lease rides a client of its own (controller-runtime's
+    separately built lock client, ``/root/reference/cmd/operator/start.go:156-177``), so the
+    leader never loses it and no renewal takes longer than ``retryPeriod``."""
+    qps, burst = chart_client_values()
+    stats: dict = {}
+    await _run(qps, burst, fleet=2 * CLAIMED, leader_elect=True, stats=stats)
+    assert stats["leader"] and not stats["lost"], stats
+    assert stats["max_renew_s"] < stats["retry_period"], stats
+
+
+async def test_shared_client_lease_lapses_behind_a_throttled_tick():
+    """The control: the same run with the Lease on the reconciler's own client (one QPS bucket,
+    renewals FIFO with the tick's CREATEs) loses leadership."""
+    qps, burst = chart_client_values()
+    stats: dict = {}
+    await _run(qps, burst, fleet=2 * CLAIMED, leader_elect=True, shared_lease_client=True, stats=stats)
+    assert stats["lost"] and not stats["leader"], stats
 
 
 def test_cli_flag_defaults_match_the_chart():

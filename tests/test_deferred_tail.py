@@ -232,3 +232,31 @@ async def test_released_slots_halve_tick_to_create_under_write_latency(workers):
     p50_released, req_released = await tick(True)
     assert req_released == req_held
     assert p50_released <= 0.5 * p50_held, (p50_released, p50_held)
+
+
+async def test_spare_workers_start_on_demand_only():
+    """spare worker tasks are started when a release finds no parked worker, not up
+    front -- a reference-mode controller (no releases) runs exactly ``max_concurrent`` workers,
+    and the optimized one only as many spares as releases overlapped (here: 4 held tails)."""
+    for opts, want in ((ReconcilerOptions.reference(), 2), (ReconcilerOptions(), None)):
+        env = TestEnv()
+        for i in range(4):
+            await env.create_cron(new_cron(f"w{i}", NS, "*/1 * * * *", PT_TMPL))
+        await env.start_manager(opts, max_concurrent=2)
+        await env.settle()
+        ctrl = env.controller
+        assert ctrl._spawned == 2
+        env.server.faults.latency["patch"] = 0.2
+        try:
+            env.clock.advance(60)
+            await _until(lambda: sum(len(_jobs(env, f"w{i}")) for i in range(4)) == 4, 3.0)
+            if want is None:
+                assert ctrl.released == 4
+                assert 2 < ctrl._spawned <= 2 + 4  # spares for the overlapping tails, no more
+            else:
+                assert ctrl._spawned == want and ctrl.released == 0
+            env.server.faults.latency.clear()
+            await _until(lambda: ctrl.queue.idle() and ctrl.in_flight() == 0, 5.0)
+        finally:
+            env.server.faults.latency.clear()
+            await env.stop()

@@ -576,3 +576,89 @@ async def test_shard_assigner_shutdown_leaves_no_label_patch_in_flight():
     labelled = [o for o in env.server.list(CRON_GVR, NS)["items"] if LABEL_SHARD in (o["metadata"].get("labels") or {})]
     assert len(labelled) == n
     await cache.stop()
+
+
+async def test_reference_mode_with_label_sharding_assigns_crons_without_waiting():
+    """ADVICE r4: in live-list mode (``--compat-mode reference``) there are no child informers;
+    a Cron with relabelled children must not wait ``observe_timeout`` for an informer that
+    will never hold them."""
+    import time
+
+    from cron_operator_amd.controller.reconciler import ReconcilerOptions
+    from cron_operator_amd.controller.setup import setup_with_manager
+    from cron_operator_amd.controller.sharding import LABEL_SHARD
+    from cron_operator_amd.runtime.manager import Manager, ManagerOptions
+
+    env = TestEnv()
+    n = 8
+    for i in range(n):
+        await env.create_cron(new_cron(f"l{i}", NS, "*/1 * * * *", PT_TMPL))
+        env.server.create(PT, NS, {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+                                   "metadata": {"name": f"l{i}-1", "labels": {LABEL_CRON_NAME: f"l{i}"}},
+                                   "spec": {"pytorchReplicaSpecs": {"Master": {"replicas": 1}}}})
+    mgrs, tasks = [], []
+    t0 = time.monotonic()
+    for idx in range(2):
+        m = Manager(env.new_client(), ManagerOptions(clock=env.clock, shard_index=idx, shard_count=2,
+                                                     shard_routing="labels", health_probe_bind_address="0",
+                                                     metrics_bind_address="0"))
+        await setup_with_manager(m, ReconcilerOptions.reference())
+        mgrs.append(m)
+        tasks.append(asyncio.get_running_loop().create_task(m.start()))
+    try:
+        while True:
+            crons = env.server.list(CRON_GVR, NS)["items"]
+            if all(LABEL_SHARD in (o["metadata"].get("labels") or {}) for o in crons):
+                break
+            assert time.monotonic() - t0 < 3.0, "Crons waited for child informers that live mode never starts"
+            await asyncio.sleep(0.01)
+    finally:
+        for m in mgrs:
+            m.stop()
+        for t in tasks:
+            await asyncio.wait_for(t, 10)
+        env.server.close_all_watches()
+
+
+async def test_shard_assigner_gives_up_a_child_it_may_not_label():
+    """a child whose label PATCH keeps failing (403) is given up after
+    ``max_child_attempts``: its Cron is assigned anyway instead of being parked forever."""
+    from cron_operator_amd.api import errors as api_errors
+    from cron_operator_amd.api.meta import GroupVersionKind
+    from cron_operator_amd.api.v1alpha1 import CRON_GVK
+    from cron_operator_amd.controller.sharding import LABEL_SHARD, ShardAssigner
+    from cron_operator_amd.runtime.informer import Cache
+
+    env = TestEnv()
+    await env.create_cron(new_cron("f0", NS, "*/1 * * * *", PT_TMPL))
+    env.server.create(PT, NS, {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+                               "metadata": {"name": "f0-1", "labels": {LABEL_CRON_NAME: "f0"}},
+                               "spec": {"pytorchReplicaSpecs": {"Master": {"replicas": 1}}}})
+    client = env.new_client()
+    orig = client.patch
+    denied = []
+
+    async def patch(gvk, ns, name, *a, **kw):
+        if getattr(gvk, "kind", "") == "PyTorchJob" or getattr(gvk, "resource", "") == "pytorchjobs":
+            denied.append(name)
+            raise api_errors.ApiError(403, "Forbidden", f"pytorchjobs {name!r} is forbidden")
+        return await orig(gvk, ns, name, *a, **kw)
+
+    client.patch = patch  # type: ignore[assignment]
+    cache = Cache(env.new_client(), NS)
+    asg = ShardAssigner(client, 0, 1, retry_delay=0.01, max_child_attempts=3)
+    await asg.watch(cache, CRON_GVK, child=False)
+    await asg.watch(cache, GroupVersionKind("kubeflow.org", "v1", "PyTorchJob"), child=True)
+    cache.start()
+    task = asyncio.get_running_loop().create_task(asg.run())
+    try:
+        for _ in range(300):
+            if LABEL_SHARD in (env.server.get(CRON_GVR, NS, "f0")["metadata"].get("labels") or {}):
+                break
+            await asyncio.sleep(0.01)
+        assert LABEL_SHARD in (env.server.get(CRON_GVR, NS, "f0")["metadata"].get("labels") or {})
+        assert len(denied) == 3 and asg.abandoned == 1
+    finally:
+        task.cancel()
+        await asyncio.gather(task, return_exceptions=True)
+        await cache.stop()

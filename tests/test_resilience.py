@@ -183,14 +183,16 @@ async def test_leader_steps_down_within_renew_deadline_when_lease_updates_hang()
         await env.advance(1)
     renew_time = env.server.get(LEASES, NS, "619a52b8.kubedl.io")["spec"]["renewTime"]
     hang = asyncio.Event()
-    orig_update = env.client.update
+    lease_client = env.manager.lease_client  # the elector's own client (Client.derive)
+    assert lease_client is not None and lease_client is not env.client
+    orig_update = lease_client.update
 
     async def hung_update(target, obj, *a, **kw):
         if target == LEASES:
             await hang.wait()
         return await orig_update(target, obj, *a, **kw)
 
-    env.client.update = hung_update  # type: ignore[assignment]
+    lease_client.update = hung_update  # type: ignore[assignment]
     stopped_after = None
     for sec in range(1, 30):
         env.clock.advance(1)
