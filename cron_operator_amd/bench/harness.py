@@ -127,6 +127,16 @@ class BenchConfig:
     # trainingop.operator.lifecycle_statuses), each write absorbed by the operator before the
     # next; "instant" -- a single Succeeded write (rounds 1-4)
     lifecycle: str = "realistic"
+    # burst tokens deferrable (low-priority) writes may not spend (cmd/main.py --tick-burst-reserve)
+    tick_reserve: int = -1
+    # run even a single shard in its own process (bench/shard_worker.py): its peak RSS is then
+    # the operator's alone (operator_maxrss_mib), not the harness's
+    operator_process: bool = False
+    # optimized mode: ReconcilerOptions.compact_child_status (A/B switch of the child-cache trim)
+    compact_children: bool = True
+    # one process: run leader election (the chart's default) on the operator's Lease; the result
+    # reports whether it was ever lost and the longest renewal
+    leader_elect: bool = False
 
 
 @dataclass
@@ -158,6 +168,9 @@ class BenchResult:
     # Manager.start() to synced caches, and to the first pass over every Cron done (the queue idle)
     startup_sync_s: float = 0.0
     startup_first_pass_s: float = 0.0
+    # leader_elect: the Lease was lost at some point / the longest successful renewal window (s)
+    lease_lost: Optional[bool] = None
+    lease_max_renew_s: Optional[float] = None
 
     def to_dict(self) -> Dict[str, Any]:
         return asdict(self)
@@ -395,7 +408,7 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
     from ..runtime.client import Client, InMemoryTransport
     from ..runtime.manager import Manager, ManagerOptions
     from ..utils import gctune, jsonutil
-    from ..utils.clock import FakeClock
+    from ..utils.clock import FakeClock, RealClock
 
     clock = FakeClock(T0_NS)
     remote: Optional[_RemoteServer] = None
@@ -522,18 +535,22 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
             async with admin.post(remote.url + "/debug/fake/faults", json={"latency": latency}) as r:
                 await r.read()
 
-        if cfg.shards > 1:
+        if cfg.shards > 1 or cfg.operator_process:
             if remote is None:
-                raise ValueError("shards > 1 needs transport='http'")
+                raise ValueError("shards > 1 / operator_process need transport='http'")
             await setup_client.close()
             return await _run_sharded(cfg, remote, admin, set_time, complete_jobs, on_step, job_stage)
 
-        client = Client(transport, qps=cfg.qps, burst=cfg.burst, max_inflight=cfg.max_inflight)
+        client = Client(transport, qps=cfg.qps, burst=cfg.burst, max_inflight=cfg.max_inflight,
+                        low_reserve=cfg.tick_reserve)
         opts = ReconcilerOptions.reference() if cfg.mode == "reference" else \
-            ReconcilerOptions(defer_status_write=cfg.defer_writes)
+            ReconcilerOptions(defer_status_write=cfg.defer_writes, compact_child_status=cfg.compact_children)
         mgr = Manager(client, ManagerOptions(clock=clock, max_concurrent_reconciles=cfg.workers,
                                              health_probe_bind_address="0", metrics_bind_address="0",
-                                             namespace=cfg.namespace))
+                                             namespace=cfg.namespace, leader_election=cfg.leader_elect,
+                                             leader_election_namespace=cfg.namespace,
+                                             leader_election_identity="bench-operator",
+                                             leader_election_clock=RealClock()))
         ctrl, rec = await setup_with_manager(mgr, opts)
         t_start0 = time.perf_counter()
         mgr_task = asyncio.get_running_loop().create_task(mgr.start())
@@ -680,6 +697,9 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
             engine=default_engine().name, fastjson_native=jsonutil.NATIVE,
             cpu_s_operator=cpu1[0] - cpu0[0], cpu_s_apiserver=cpu1[1] - cpu0[1] - write_cpu[0], operator_gc=gc_stats,
             startup_sync_s=startup_sync_s, startup_first_pass_s=startup_first_pass_s)
+        if mgr.elector is not None:
+            res.lease_lost = mgr.elector.lost.is_set() or not mgr.elector.is_leader
+            res.lease_max_renew_s = mgr.elector.max_renew_s
         mgr.stop()
         try:
             await asyncio.wait_for(mgr_task, 30)
@@ -733,7 +753,9 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
                 "--namespace", cfg.namespace, "--shard-index", str(i), "--shard-count", str(cfg.shards),
                 "--start-ns", str(T0_NS + NANOS // 2), "--workers", str(cfg.workers),
                 "--history-limit", str(cfg.history_limit), "--qps", str(cfg.qps), "--burst", str(cfg.burst),
-                "--max-inflight", str(cfg.max_inflight), *([] if cfg.defer_writes else ["--no-defer"]),
+                "--max-inflight", str(cfg.max_inflight), "--tick-reserve", str(cfg.tick_reserve),
+                *([] if cfg.defer_writes else ["--no-defer"]),
+                *([] if cfg.compact_children else ["--no-compact"]),
                 "--mode", cfg.mode, "--routing", cfg.shard_routing,
                 *(["--ca-file", remote.ca_file] if remote.ca_file else []),
                 env=env, stdin=asyncio.subprocess.PIPE, stdout=asyncio.subprocess.PIPE,

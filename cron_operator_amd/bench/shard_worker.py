@@ -44,7 +44,9 @@ async def main() -> int:
     ap.add_argument("--qps", type=float, default=-1.0)
     ap.add_argument("--burst", type=int, default=50)
     ap.add_argument("--max-inflight", type=int, default=128)
+    ap.add_argument("--tick-reserve", type=int, default=-1, help="--tick-burst-reserve of the operator's client")
     ap.add_argument("--no-defer", action="store_true", help="ReconcilerOptions.defer_status_write=False (A/B)")
+    ap.add_argument("--no-compact", action="store_true", help="ReconcilerOptions.compact_child_status=False (A/B)")
     ap.add_argument("--mode", default="optimized")
     ap.add_argument("--routing", default="hash", choices=["hash", "labels"])
     ap.add_argument("--ca-file", default="", help="https --url: verify the apiserver against this CA (as localhost)")
@@ -68,9 +70,9 @@ async def main() -> int:
         with open(a.ca_file, "rb") as fh:
             rc = RestConfig(host=a.url, ca_data=fh.read(), tls_server_name="localhost")
     client = Client(HttpTransport(rc, pool_size=max(16, a.workers * 2, a.max_inflight)), qps=a.qps, burst=a.burst,
-                    max_inflight=a.max_inflight)
+                    max_inflight=a.max_inflight, low_reserve=a.tick_reserve)
     opts = ReconcilerOptions.reference() if a.mode == "reference" else \
-        ReconcilerOptions(defer_status_write=not a.no_defer)
+        ReconcilerOptions(defer_status_write=not a.no_defer, compact_child_status=not a.no_compact)
     mgr = Manager(client, ManagerOptions(clock=clock, max_concurrent_reconciles=a.workers,
                                          health_probe_bind_address="0", metrics_bind_address="0",
                                          namespace=a.namespace, shard_index=a.shard_index,

@@ -28,9 +28,9 @@ flag                            default      reference
 Additions: ``--kubeconfig``, ``--namespace`` (restrict the cache),
 ``--leader-elect-namespace``, ``--compat-mode`` (``reference`` restores every
 reference quirk, see :class:`~cron_operator_amd.controller.reconciler.ReconcilerOptions`),
-``--cron-engine``, ``--max-inflight-requests``.  Extra subcommands: ``fake-apiserver`` (serve the in-process
-apiserver over HTTP with the CRDs installed), ``crd`` (print the CRD) and
-``version``.
+``--cron-engine``, ``--max-inflight-requests``, ``--tick-burst-reserve``.  Extra subcommands:
+``fake-apiserver`` (serve the in-process apiserver over HTTP with the CRDs installed), ``crd``
+(print the CRD) and ``version``.
 
 Flag syntax follows pflag: ``--flag value``, ``--flag=value`` and bare boolean
 flags (``--leader-elect``, ``--metrics-secure=false``).
@@ -97,6 +97,10 @@ def build_parser() -> argparse.ArgumentParser:
                     help="Maximum QPS to the Kubernetes API server from this client. About 4 requests per Cron "
                          "fire: N minutely Crons need N/15 QPS (default: 1000 Crons at 45%% of the budget).")
     st.add_argument("--burst", type=int, default=DEFAULT_BURST, help="Maximum burst for throttle.")
+    st.add_argument("--tick-burst-reserve", type=int, default=-1,
+                    help="Burst tokens that deferrable writes (status PATCHes, history-GC DELETEs, events) may "
+                         "not spend: they run at the --qps refill rate and leave the burst to the next schedule "
+                         "tick's CREATEs. -1 (default): the whole burst; 0: off.")
     st.add_argument("--max-inflight-requests", type=int, default=DEFAULT_MAX_INFLIGHT,
                     help="Maximum concurrent API requests (watches excluded); more wait in priority order "
                          "(tick CREATEs first). 0: unlimited.")
@@ -256,7 +260,7 @@ async def run_start(a: argparse.Namespace) -> int:
         log.error(e, "invalid --sync-period")
         return 2
     client = Client(HttpTransport(cfg, pool_size=max(64, a.max_inflight_requests)), qps=a.qps, burst=a.burst,
-                    max_inflight=a.max_inflight_requests)
+                    max_inflight=a.max_inflight_requests, low_reserve=a.tick_burst_reserve)
     mopts = ManagerOptions(namespace=a.namespace, leader_election=a.leader_elect,
                            leader_election_namespace=a.leader_elect_namespace,
                            metrics_bind_address=a.metrics_bind_address, secure_metrics=a.metrics_secure,

@@ -10,6 +10,15 @@ that does not parse (the reference's ``cron.ParseStandard`` grammar,
 ``internal/controller/cron_controller.go:184-190``); templates that set ``metadata.name``
 (the reference's ``OverridePolicy``: such a Cron runs as Forbid, ``cron_controller.go:355-370``);
 and who holds the leader Lease.  Exit status 1 when a Cron would fail to run.
+
+It also sizes the client budget (``--qps`` / ``--burst``, the chart's defaults unless given):
+from the schedules it parses it finds the busiest minute of the next day and warns when that
+minute's fires x :data:`REQUESTS_PER_FIRE` exceed a minute of ``--qps`` -- ticks then
+collapse and runs are lost without an error (the reference's catch-up runs only the last
+missed tick, ``internal/controller/cron_controller.go:408-436``) -- or when its fires exceed
+``--burst`` (the last CREATEs land (fires - burst) / qps seconds after the tick).  An upgrade
+that keeps the reference's ``qps: 30`` (``/root/reference/cmd/operator/start.go:218-219``)
+collapses ticks from about 450 minutely Crons.
 """
 from __future__ import annotations
 
@@ -28,6 +37,11 @@ if TYPE_CHECKING:
 # DELETE it (history GC, Replace), GET it (deduplication after a lost response)
 NEEDED_VERBS = ("get", "list", "watch", "create", "delete")
 LEASES = GroupVersionResource("coordination.k8s.io", "v1", "leases")
+# API requests per Cron fire in the default mode: the CREATE, the status PATCH recording it, the
+# status PATCH moving the finished job to history, the history-GC DELETE (bench.py
+# api_requests_per_fire / deployment_api_requests_per_fire, realistic job lifecycle: 4.0)
+REQUESTS_PER_FIRE = 4.0
+HORIZON_MINUTES = 24 * 60  # the busiest minute is looked for over the next day
 
 
 @dataclass
@@ -52,6 +66,10 @@ class Report:
     named_templates: List[str] = field(default_factory=list)                  # run as Forbid
     lease: Optional[Dict[str, Any]] = None
     errors: List[str] = field(default_factory=list)
+    # client budget: the busiest minute's fires (and when), and the warnings it raises
+    peak_fires_per_minute: int = 0
+    peak_minute: str = ""
+    budget_warnings: List[str] = field(default_factory=list)
 
     @property
     def ok(self) -> bool:
@@ -74,8 +92,50 @@ def rbac_missing(group: str, resource: str, rules: List[Dict[str, Any]]) -> List
                        for r in rules)]
 
 
+def peak_fires(schedules: List[Any], now: Any, engine: Any = None,
+               horizon_minutes: int = HORIZON_MINUTES) -> Tuple[int, Any]:
+    """(most fires in one minute over the next ``horizon_minutes``, that minute's start).  A
+    schedule fires at most once a minute (seconds are fixed at 0), so each contributes at
+    most ``horizon_minutes`` ticks."""
+    from collections import Counter
+
+    from ..cron.engine import default_engine
+    from ..utils.gotime import GoTime
+
+    eng = engine or default_engine()
+    end = now.sec + horizon_minutes * 60
+    per_minute: Counter = Counter()
+    for sched in schedules:
+        t = now
+        for _ in range(horizon_minutes + 1):
+            t = eng.next(sched, t)
+            if t.is_zero() or t.sec > end:
+                break
+            per_minute[t.sec // 60] += 1
+    if not per_minute:
+        return 0, None
+    minute, n = max(per_minute.items(), key=lambda kv: (kv[1], -kv[0]))
+    return n, GoTime(minute * 60, 0, now.loc)
+
+
+def budget_warnings(fires: int, qps: float, burst: int, requests_per_fire: float = REQUESTS_PER_FIRE) -> List[str]:
+    """Warnings for a minute with ``fires`` Cron fires under a ``qps`` / ``burst`` client."""
+    out = []
+    if qps <= 0 or fires <= 0:
+        return out
+    need = fires * requests_per_fire / 60.0
+    if need > qps:
+        out.append(f"the busiest minute has {fires} fires x {requests_per_fire:g} API requests = {need:.0f} QPS, "
+                   f"more than --qps {qps:g}: ticks collapse and scheduled runs are lost; set qps >= "
+                   f"{need:.0f} (helm: qps), or shard the fleet (sharding.count)")
+    if fires > burst:
+        out.append(f"the busiest minute's {fires} CREATEs exceed --burst {burst}: the last lands about "
+                   f"{(fires - burst) / qps:.1f} s after the tick (raise burst to {fires} for all at once)")
+    return out
+
+
 async def preflight(client: "Client", namespace: str = "", rules: Optional[List[Dict[str, Any]]] = None,
-                    lease_namespace: str = "") -> Report:
+                    lease_namespace: str = "", qps: float = 0.0, burst: int = 0, now: Any = None) -> Report:
     """Read-only checks of the Crons in ``namespace`` ("" = all) against ``rules`` (default: the
     operator's own RBAC)."""
     from ..api import errors
@@ -93,6 +153,15 @@ async def preflight(client: "Client", namespace: str = "", rules: Optional[List[
         rep.errors.append(f"cannot list crons.apps.kubedl.io: {e}")
         return rep
     rep.crons = len(crons)
+    from ..cron.engine import ScheduleError, default_engine
+    from ..utils.gotime import LOCAL, parse_rfc3339
+
+    engine = default_engine()
+    if now is None:
+        from ..utils.clock import RealClock
+
+        now = RealClock().now(LOCAL)
+    scheds: List[Any] = []
     for c in crons:
         m = c.get("metadata") or {}
         key = f"{m.get('namespace', '')}/{m.get('name', '')}"
@@ -102,6 +171,19 @@ async def preflight(client: "Client", namespace: str = "", rules: Optional[List[
             parse_standard(sched)
         except (CronParseError, ValueError) as e:
             rep.bad_schedules.append((key, sched, str(e)))
+        else:
+            deadline = spec.get("deadline")
+            past = False
+            if isinstance(deadline, str) and deadline:
+                try:
+                    past = now.after(parse_rfc3339(deadline))
+                except ValueError:
+                    past = False
+            if not spec.get("suspend") and not past:
+                try:
+                    scheds.append(engine.parse(sched))
+                except ScheduleError:
+                    pass
         wl = (spec.get("template") or {}).get("workload")
         try:
             gvk = get_workload_gvk(wl)
@@ -123,6 +205,10 @@ async def preflight(client: "Client", namespace: str = "", rules: Optional[List[
             continue
         kr.served, kr.resource = True, gvr.resource
         kr.missing_verbs = rbac_missing(gvk.group, gvr.resource, rules)
+    if qps > 0 and scheds:
+        rep.peak_fires_per_minute, peak = peak_fires(scheds, now, engine)
+        rep.peak_minute = peak.rfc3339() if peak is not None else ""
+        rep.budget_warnings = budget_warnings(rep.peak_fires_per_minute, qps, burst)
     if lease_namespace:
         try:
             lease = await client.get(LEASES, lease_namespace, _lease_name())
@@ -156,6 +242,11 @@ def render(rep: Report, lease_namespace: str = "") -> str:
                        f"{kr.resource}.{gvk.group}; add it to rbac.extraWorkloadRules")
     for key in rep.named_templates:
         out.append(f"note: {key}: the template sets metadata.name, so the Cron runs as Forbid (OverridePolicy)")
+    if rep.peak_fires_per_minute:
+        out.append(f"busiest minute (next {HORIZON_MINUTES // 60} h): {rep.peak_fires_per_minute} fires at "
+                   f"{rep.peak_minute}")
+    for w in rep.budget_warnings:
+        out.append(f"warning: {w}")
     if lease_namespace:
         if rep.lease:
             out.append(f"lease {lease_namespace}/{_lease_name()}: held by "
@@ -177,6 +268,12 @@ def add_parser(sub: Any) -> None:
                     help="also report the holder of the leader Lease in this namespace")
     pf.add_argument("--extra-rules", default="",
                     help="YAML list of {apiGroups, resources} rules, as the chart's rbac.extraWorkloadRules")
+    from .main import DEFAULT_BURST, DEFAULT_QPS
+
+    pf.add_argument("--qps", type=float, default=DEFAULT_QPS,
+                    help="the operator's --qps to size against (helm: qps; the reference ships 30)")
+    pf.add_argument("--burst", type=int, default=DEFAULT_BURST,
+                    help="the operator's --burst to size against (helm: burst; the reference ships 50)")
 
 
 async def run(a: argparse.Namespace) -> int:
@@ -200,7 +297,7 @@ async def run(a: argparse.Namespace) -> int:
                               "verbs": ["get", "list", "watch", "create", "update", "patch", "delete"]})
     client = Client(HttpTransport(cfg), qps=-1)
     try:
-        rep = await preflight(client, a.namespace, rules, a.lease_namespace)
+        rep = await preflight(client, a.namespace, rules, a.lease_namespace, qps=a.qps, burst=a.burst)
     finally:
         await client.close()
     sys.stdout.write(render(rep, a.lease_namespace))

@@ -116,6 +116,7 @@ from ..api.v1alpha1 import (
 )
 from ..cron.engine import CronEngine, ScheduleError, default_engine
 from ..models import kubeflow as kf
+from ..models.workload import _summary as workload_summary
 from ..models.workload import (
     Classification,
     WorkloadError,
@@ -182,7 +183,12 @@ def child_info(w: Dict[str, Any], gvk: GroupVersionKind, policy: WorkloadPolicy)
     cls: Optional[Classification] = None
     sort_key: Any = (0, 0)
     try:
-        cls = classify(w, gvk, policy)
+        hit = _CLS_MEMO[0]
+        if hit is not None and hit[0] is w:
+            cls = hit[1]  # classified by the informer transform a moment ago (compact_child)
+            _CLS_MEMO[0] = None
+        else:
+            cls = classify(w, gvk, policy)
         sort_key = creation_timestamp(w).key()
     except Exception as e:  # noqa: BLE001 - kf.ConversionError, or a malformed object
         err = e
@@ -210,6 +216,85 @@ def slim_child(obj: Dict[str, Any]) -> Dict[str, Any]:
     if type(m) is dict and "managedFields" in m:
         del m["managedFields"]
     return obj
+
+
+_COND_KEEP = ("type", "status", "lastTransitionTime")
+_TERMINAL_TYPES = frozenset(("Succeeded", "Failed", "Complete"))
+_STATUS_KEEP = ("completionTime", "phase", "launcherStatus")
+
+
+def compact_status(st: Dict[str, Any]) -> Optional[Dict[str, Any]]:
+    """The part of a child's ``status`` that :func:`~cron_operator_amd.models.workload.classify`
+    reads: the terminal conditions (``Succeeded``/``Failed``/``Complete`` that are ``True``) and
+    the last condition, each as type / status / lastTransitionTime; ``completionTime``; a Pod's
+    ``phase``; an MPIJob v1alpha1's ``launcherStatus``.  Messages, reasons, ``replicaStatuses``
+    and start times -- most of a finished job's status -- are never read.  None: not a shape
+    this trims (the caller keeps the status as it is)."""
+    out: Dict[str, Any] = {}
+    conds = st.get("conditions")
+    if conds is not None:
+        if type(conds) is not list:
+            return None
+        keep = []
+        last = len(conds) - 1
+        for i, c in enumerate(conds):
+            if type(c) is not dict:
+                return None
+            if i == last or (c.get("status") == "True" and c.get("type") in _TERMINAL_TYPES):
+                keep.append({k: c[k] for k in _COND_KEEP if k in c})
+        out["conditions"] = keep
+    for k in _STATUS_KEEP:
+        if k in st:
+            out[k] = st[k]
+    return out
+
+
+def compact_child(gvk: GroupVersionKind, policy: WorkloadPolicy) -> Callable[[Dict[str, Any]], Dict[str, Any]]:
+    """Informer transform for the children of kind ``gvk``: :func:`slim_child`, and the status
+    trimmed to what classifies it (:func:`compact_status`) -- kept whole when the trim would
+    change the classification or the status does not convert (the reconcile then reports it).
+    ``ReconcilerOptions.compact_child_status``: about 60% of a cached finished job is status a
+    reconcile never reads (a 10,000-Cron fleet caches 110,000 jobs)."""
+    summary = workload_summary
+
+    def transform(obj: Dict[str, Any]) -> Dict[str, Any]:
+        slim_child(obj)
+        st = obj.get("status")
+        if type(st) is not dict or not st:
+            return obj
+        try:
+            full = classify(obj, gvk, policy)
+        except Exception:  # noqa: BLE001 - an unreadable status stays whole for the reconcile to report
+            return obj
+        _CLS_MEMO[0] = (obj, full)  # child_info() of this object reuses it
+        small = compact_status(st)
+        if small is None:
+            return obj
+        sm = summary(st)
+        if sm is not None:
+            # an exactly-typed kubeflow status: the trim keeps every True terminal condition and
+            # the last one, so the summary (finished, last type, completion / terminal times) is
+            # the same by construction -- checked natively, not by a second classification
+            sm2 = summary(small)
+            ok = sm2 is not None and (sm2[0], sm2[1], sm2[3], sm2[4]) == (sm[0], sm[1], sm[3], sm[4])
+            obj["status"] = small
+        else:
+            obj["status"] = small
+            try:
+                same = classify(obj, gvk, policy)
+                ok = (same.finished, same.status, same.finished_at) == (full.finished, full.status,
+                                                                         full.finished_at)
+            except Exception:  # noqa: BLE001
+                ok = False
+        if not ok:
+            obj["status"] = st
+        return obj
+    return transform
+
+
+# (object, its Classification) of the child compact_child() transformed last: the informer derives
+# the child's memo (child_info) right after transforming it, so the classification is reused
+_CLS_MEMO: List[Any] = [None]
 
 
 class JoinedError(Exception):
@@ -244,6 +329,9 @@ class ReconcilerOptions:
     dedupe_ran_tick: bool = True
     overlap_gc_deletes: bool = True
     slim_child_cache: bool = True
+    # (with slim_child_cache and classification_cache) cached children keep only the status
+    # fields their classification reads (compact_child)
+    compact_child_status: bool = True
     wire_codecs: bool = True
     defer_status_write: bool = True
     request_priorities: bool = True
@@ -267,7 +355,8 @@ class ReconcilerOptions:
                                  own_write_filter=False, dynamic_watches=False, expectations=False,
                                  fold_created_into_active=False, skip_expected_events=False,
                                  classification_cache=False, dedupe_ran_tick=False,
-                                 overlap_gc_deletes=False, slim_child_cache=False, wire_codecs=False,
+                                 overlap_gc_deletes=False, slim_child_cache=False, compact_child_status=False,
+                                 wire_codecs=False,
                                  defer_status_write=False, request_priorities=False, explain_errors=False,
                                  workload=WorkloadPolicy.reference())
 
@@ -721,7 +810,9 @@ class CronReconciler(Reconciler):
             return Result()
 
         # B13 (cron_controller.go:192)
-        scheduled = Result(requeue_after_ns=next_run.sub(now))
+        # the tick as an absolute time too: the deferred writes may keep this reconcile running
+        # past `now` (controller-runtime adds RequeueAfter when Reconcile returns, B13)
+        scheduled = Result(requeue_after_ns=next_run.sub(now), requeue_at_ns=next_run.unix_nano())
         if log.enabled():
             log = log.with_values(now=now.rfc3339(nanos=True), **{"next run": next_run.rfc3339()})
 
@@ -867,6 +958,15 @@ class CronReconciler(Reconciler):
     def _ckey(cron: Cron) -> str:
         return f"{cron.namespace}/{cron.name}"
 
+    def child_transform(self, gvk: GroupVersionKind) -> Optional[Callable[[Dict[str, Any]], Dict[str, Any]]]:
+        """The informer transform of ``gvk``'s children under these options."""
+        o = self.opts
+        if not o.slim_child_cache:
+            return None
+        if o.compact_child_status and o.classification_cache:
+            return compact_child(gvk, o.workload)
+        return slim_child
+
     async def child_informer(self, gvk: GroupVersionKind) -> Informer:
         inf = self.child_informers.get(gvk)
         if inf is None:
@@ -875,7 +975,7 @@ class CronReconciler(Reconciler):
 
             inf = await self.cache.get_informer(gvk, label_selector=self.child_selector,
                                                 indexers={CHILD_INDEX: label_index(LABEL_CRON_NAME)},
-                                                transform=slim_child if self.opts.slim_child_cache else None,
+                                                transform=self.child_transform(gvk),
                                                 decoder=self.codecs.child_event if self.codecs else None)
             self.child_informers[gvk] = inf
             inf.start()

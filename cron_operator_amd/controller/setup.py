@@ -29,7 +29,7 @@ from ..runtime.informer import EventHandler, Informer, label_index, strip_manage
 from ..runtime.manager import Manager
 from ..utils.logging import get_logger, log_constructor
 from . import sharding
-from .reconciler import CHILD_INDEX, CronReconciler, ReconcilerOptions, WireCodecs, slim_child
+from .reconciler import CHILD_INDEX, CronReconciler, ReconcilerOptions, WireCodecs
 
 CONTROLLER_NAME = "cron"
 
@@ -39,7 +39,7 @@ _CHILD_META = ("name", "namespace", "uid", "labels", "ownerReferences", "creatio
                "deletionTimestamp")
 
 
-def child_update_matters(old, new, gvk: GroupVersionKind, policy: WorkloadPolicy) -> bool:
+def child_update_matters(old, new, gvk: GroupVersionKind, policy: WorkloadPolicy, new_info=None) -> bool:
     """Can this child update change its Cron's reconcile?  Not when the child stays running and
     nothing a reconcile reads moved: its active ref keeps the resourceVersion it entered
     ``status.active`` with (``active_ref_resource_version="first"``), and an unfinished child's
@@ -51,7 +51,13 @@ def child_update_matters(old, new, gvk: GroupVersionKind, policy: WorkloadPolicy
         if om.get(k) != nm.get(k):
             return True
     try:
-        return classify(old, gvk, policy).finished or classify(new, gvk, policy).finished
+        # ``new_info``: the child informer's memo of ``new`` (child_info), computed already
+        if new_info is not None and new_info.obj is new:
+            if new_info.err is not None or new_info.finished:
+                return True
+        elif classify(new, gvk, policy).finished:
+            return True
+        return classify(old, gvk, policy).finished
     except Exception:  # noqa: BLE001 - an unreadable status: let the reconcile report it
         return True
 
@@ -125,8 +131,12 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
         if opts.skip_unchanged_child_updates and opts.active_ref_resource_version != "live":
             policy = opts.workload
 
-            def changed(event: str, old, new, g=gvk) -> bool:
-                return event != "update" or old is None or child_update_matters(old, new, g, policy)
+            def changed(event: str, old, new, g=gvk, i=inf) -> bool:
+                if event != "update" or old is None:
+                    return True
+                m = new.get("metadata") or {}
+                return child_update_matters(old, new, g, policy,
+                                            i.derived.get(f"{m.get('namespace', '')}/{m.get('name', '')}"))
             owned_preds.append(changed)
         ctrl.watch_owned(inf, CRON_GVK, owned_preds)
         if assigner is not None:
@@ -156,7 +166,7 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
             if opts.list_mode == "cache":
                 inf = await mgr.cache.get_informer(gvk, label_selector=rec.child_selector,
                                                    indexers={CHILD_INDEX: label_index(LABEL_CRON_NAME)},
-                                                   transform=slim_child if opts.slim_child_cache else None,
+                                                   transform=rec.child_transform(gvk),
                                                    decoder=codecs.child_event if codecs is not None else None)
                 rec.child_informers[gvk] = inf
             else:

@@ -282,13 +282,14 @@ class Client:
 
     def __init__(self, transport: Transport, qps: float = 30.0, burst: int = 50,
                  limiter: Optional[TokenBucket] = None, mapper: Optional[RESTMapper] = None,
-                 max_inflight: int = 0, gauges: bool = True):
+                 max_inflight: int = 0, gauges: bool = True, low_reserve: int = 0):
         """``max_inflight`` > 0 caps concurrent requests (watches excluded); excess requests
         wait in priority order (:class:`~.ratelimit.InflightGate`).  ``gauges``: publish this
         client's gates as ``rest_client_requests_{in_flight,waiting}`` (the main client does; a
-        derived side client does not overwrite its series)."""
+        derived side client does not overwrite its series).  ``low_reserve``: burst tokens a
+        low-priority request may not spend (:class:`~.ratelimit.TokenBucket`; -1: the whole burst)."""
         self.transport = transport
-        self.limiter = limiter if limiter is not None else make_client_limiter(qps, burst)
+        self.limiter = limiter if limiter is not None else make_client_limiter(qps, burst, low_reserve=low_reserve)
         self.inflight: Optional[InflightGate] = InflightGate(max_inflight) if max_inflight > 0 else None
         self.mapper = mapper or RESTMapper(transport)
         self.host = getattr(transport, "host", "in-memory")

@@ -68,6 +68,10 @@ class Result:
     requeue: bool = False
     requeue_after: float = 0.0  # seconds
     requeue_after_ns: int = 0   # exact form (schedule requeues land on the tick)
+    # absolute form (clock ns): the requeue lands here however long the reconcile took to return
+    # -- a schedule requeue computed before a reconcile's deferred writes (which may wait on a
+    # throttled client for seconds) would otherwise land that much after the tick
+    requeue_at_ns: int = 0
 
     def after_ns(self) -> int:
         return self.requeue_after_ns or int(self.requeue_after * 1e9)
@@ -382,7 +386,8 @@ class Controller:
                 log.error(err, "Reconciler error")
         elif result.after_ns() > 0:  # type: ignore[union-attr]
             q.forget(req)
-            q.add_at(req, self.clock.now_ns() + result.after_ns(), PRIORITY_SCHEDULE)  # type: ignore[union-attr]
+            at = result.requeue_at_ns or self.clock.now_ns() + result.after_ns()  # type: ignore[union-attr]
+            q.add_at(req, at, PRIORITY_SCHEDULE)
             self._count("requeue_after")
         elif result.requeue:  # type: ignore[union-attr]
             q.add_rate_limited(req, PRIORITY_EVENT)

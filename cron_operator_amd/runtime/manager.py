@@ -46,6 +46,9 @@ class ManagerOptions:
     renew_deadline: float = 10.0
     retry_period: float = 2.0
     leader_election_release_on_cancel: bool = False
+    # the elector's clock (default: ``clock``): a harness that jumps the schedule clock over
+    # virtual minutes keeps lease timing on real time
+    leader_election_clock: Optional[Clock] = None
     metrics_bind_address: str = "0"
     secure_metrics: bool = True
     metrics_cert_path: str = ""
@@ -155,7 +158,8 @@ class Manager:
                 if self.lease_client is None:
                     self.lease_client = self.client.derive()
                 self.elector = LeaderElector(self.lease_client, lease, ns,
-                                             self.opts.leader_election_identity, self.clock,
+                                             self.opts.leader_election_identity,
+                                             self.opts.leader_election_clock or self.clock,
                                              self.opts.lease_duration, self.opts.renew_deadline,
                                              self.opts.retry_period,
                                              self.opts.leader_election_release_on_cancel)

@@ -15,7 +15,10 @@
   latency is bounded by *creates* per QPS, not by all requests per QPS.  A low waiter
   older than ``max_defer`` seconds is served before everything else, so deferrable
   writes are delayed, never starved.  With no backlog a request takes a token at
-  once, whatever its priority, exactly as before.
+  once, whatever its priority, exactly as before -- except that with ``low_reserve``
+  a low request leaves that many tokens in the bucket: the operator's client keeps its
+  whole burst for the next tick's CREATEs (``--tick-burst-reserve``), and status
+  PATCHes / GC DELETEs run at the refill rate instead of draining it just before a tick.
 * :class:`ItemExponentialFailureRateLimiter`, :class:`BucketRateLimiter`,
   :class:`MaxOfRateLimiter` -- the workqueue's default controller limiter
   (per-item exponential backoff 5ms..1000s, max'd with an overall 10 qps /
@@ -73,8 +76,9 @@ class _PriorityWaiters:
                 self._n_waiting -= 1
                 return
 
-    def _next(self) -> Optional[Tuple["asyncio.Future[None]", int]]:
-        """Pop the waiter to serve: an over-aged low waiter, else the most urgent class."""
+    def _next(self, low_ok: bool = True) -> Optional[Tuple["asyncio.Future[None]", int]]:
+        """Pop the waiter to serve: an over-aged low waiter, else the most urgent class
+        (``low_ok`` False: a low waiter that is not over-aged is not served now)."""
         low = self._waiters[PRIORITY_LOW]
         if low and time.monotonic() - low[0][1] > self.max_defer:
             self.aged_grants += 1
@@ -83,16 +87,24 @@ class _PriorityWaiters:
         for p in (PRIORITY_HIGH, PRIORITY_NORMAL, PRIORITY_LOW):
             q = self._waiters[p]
             if q:
+                if p == PRIORITY_LOW and not low_ok:
+                    return None
                 self._n_waiting -= 1
                 return q.popleft()[0], p
         return None
 
 
 class TokenBucket(_PriorityWaiters):
-    def __init__(self, qps: float, burst: int, max_defer: float = 20.0):
+    """``low_reserve``: tokens a :data:`PRIORITY_LOW` request may not spend -- it takes one only
+    while at least ``1 + low_reserve`` are left (an over-aged one excepted).  Deferrable writes
+    then run at the refill rate without draining the burst, and the next schedule tick finds the
+    bucket full for its CREATEs (``-1``: the whole burst, ``burst - 1``)."""
+
+    def __init__(self, qps: float, burst: int, max_defer: float = 20.0, low_reserve: int = 0):
         super().__init__(max_defer)
         self.qps = float(qps)
         self.burst = max(1, int(burst))
+        self.low_reserve = self.burst - 1 if low_reserve < 0 else min(int(low_reserve), self.burst - 1)
         self._tokens = float(self.burst)
         self._last = time.monotonic()
         self._lock = threading.Lock()
@@ -138,16 +150,26 @@ class TokenBucket(_PriorityWaiters):
         if self.qps == 0:
             raise ValueError("qps 0 would block forever")
         now = time.monotonic()
-        if not self._n_waiting:
+        w = self._waiters
+        if priority == PRIORITY_LOW:
+            fast, need = not self._n_waiting, 1.0 + self.low_reserve
+        else:  # only waiters of its own class or a more urgent one go first (held low ones do not)
+            fast = not w[PRIORITY_HIGH] and (priority == PRIORITY_HIGH or not w[PRIORITY_NORMAL])
+            need = 1.0
+        if fast:
             with self._lock:
                 self._refill(now)
-                if self._tokens >= 1.0:
+                if self._tokens >= need:
                     self._tokens -= 1.0
                     self.accepted += 1
                     self.granted_by_priority[priority] += 1
                     return 0.0
         loop = asyncio.get_running_loop()
         fut = self._enqueue(priority, now)
+        if priority != PRIORITY_LOW and self._timer is not None:
+            # the armed grant may be timed for held low waiters (the reserve refilled): re-time it
+            self._timer.cancel()
+            self._timer = None
         self._arm(loop)
         try:
             await fut
@@ -169,8 +191,18 @@ class TokenBucket(_PriorityWaiters):
         if self._timer is not None or not self._n_waiting:
             return
         with self._lock:
-            self._refill(time.monotonic())
-            delay = 0.0 if self._tokens >= 1.0 else (1.0 - self._tokens) / self.qps
+            now = time.monotonic()
+            self._refill(now)
+            w = self._waiters
+            need = 1.0
+            if not w[PRIORITY_HIGH] and not w[PRIORITY_NORMAL]:
+                need += self.low_reserve  # only low waiters: due when the reserve is refilled ...
+            delay = max(0.0, (need - self._tokens) / self.qps)
+            low = w[PRIORITY_LOW]
+            if need > 1.0 and low:
+                # ... or when the oldest of them is over-aged (it may spend the reserve then)
+                aged_at = max(0.0, low[0][1] + self.max_defer - now) + 1e-4
+                delay = min(delay, max(aged_at, (1.0 - self._tokens) / self.qps))
         self._timer = loop.call_later(delay, self._grant, loop)
 
     def _grant(self, loop: asyncio.AbstractEventLoop) -> None:
@@ -178,7 +210,7 @@ class TokenBucket(_PriorityWaiters):
         with self._lock:
             self._refill(time.monotonic())
             while self._tokens >= 1.0 and self._n_waiting:
-                nxt = self._next()
+                nxt = self._next(self._tokens >= 1.0 + self.low_reserve)
                 if nxt is None:
                     break
                 fut, p = nxt
@@ -241,13 +273,14 @@ class InflightGate(_PriorityWaiters):
             fut.set_result(None)
 
 
-def make_client_limiter(qps: float, burst: int, max_defer: float = 20.0) -> Optional[TokenBucket]:
+def make_client_limiter(qps: float, burst: int, max_defer: float = 20.0,
+                        low_reserve: int = 0) -> Optional[TokenBucket]:
     """client-go: qps==0 -> default 5/10; qps<0 -> no limiter."""
     if qps == 0:
         qps, burst = 5.0, 10
     if qps < 0:
         return None
-    return TokenBucket(qps, burst, max_defer)
+    return TokenBucket(qps, burst, max_defer, low_reserve)
 
 
 # --------------------------------------------------------------------------- workqueue limiters

@@ -29,6 +29,10 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--transport", default="http")
     ap.add_argument("--shards", type=int, default=1, help="operator shard processes")
+    ap.add_argument("--operator-process", action="store_true",
+                    help="run a single shard in its own process too (its peak RSS is the operator's alone)")
+    ap.add_argument("--lifecycle", choices=["realistic", "instant"], default="instant")
+    ap.add_argument("--no-compact", action="store_true", help="A/B: ReconcilerOptions.compact_child_status=False")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
 
@@ -41,7 +45,9 @@ def main() -> int:
             # small fleets get more ticks so percentiles rest on >= ~30 samples
             steps = max(a.steps, min(30, -(-30 // n)))
             r = run_sync(BenchConfig(n_crons=n, steps=steps, warmup=a.warmup, mode=mode, transport=a.transport,
-                                     shards=a.shards if a.transport == "http" else 1))
+                                     shards=a.shards if a.transport == "http" else 1,
+                                     operator_process=a.operator_process, lifecycle=a.lifecycle,
+                                     compact_children=not a.no_compact))
             rows.append({"mode": mode, "n_crons": n, "steps": steps, "cron_reconciles_per_s": r.cron_reconciles_per_s,
                          "raw_reconciles_per_s": r.raw_reconciles_per_s, "p50_ms": r.p50_latency_ms,
                          "p99_ms": r.p99_latency_ms, "ms_per_step": r.ms_per_step,

@@ -53,12 +53,13 @@ def chart_client_values():
 
 
 async def _run(qps: float, burst: int, fleet: int = FLEET, leader_elect: bool = False,
-               shared_lease_client: bool = False, stats: dict = None):
+               shared_lease_client: bool = False, stats: dict = None, reserve: int = -1):
     """-> (missing job names, tick -> [create latency s]).  ``stats`` (if given) receives the
     leader elector's record: ``lost``, ``max_renew_s`` (virtual seconds), ``renewals``."""
     env = TestEnv()
     sq, sb = qps * N * C / fleet, max(1, round(burst * N / fleet))
-    env.client.limiter = TokenBucket(sq, sb, max_defer=20.0 / C)
+    # the operator's client as `cron-operator start` builds it (--tick-burst-reserve -1 by default)
+    env.client.limiter = TokenBucket(sq, sb, max_defer=20.0 / C, low_reserve=reserve)
     trainer = FakeTrainingOperator(env.new_client(), env.clock, mode="timed", duration=30)
     created = {}
     orig = env.server.create
@@ -131,7 +132,10 @@ async def test_chart_defaults_sustain_1000_minutely_crons_time_compressed():
     for k, xs in lat.items():
         # real time x C = the full-scale wall time of the tick's work
         assert max(xs) * C <= 45.0, (k, max(xs) * C)
-        assert statistics.median(xs) * C <= 6.0, (k, statistics.median(xs) * C)
+        # the burst is kept for the tick (--tick-burst-reserve): at full scale the median CREATE
+        # lands ~1.4 s after the tick (round-4 verdict: <= 1.5 s; 3.3 s when status writes
+        # drained the burst first); the bound leaves room for a loaded CI box
+        assert statistics.median(xs) * C <= 2.5, (k, statistics.median(xs) * C)
 
 
 async def test_reference_client_budget_collapses_ticks_at_the_same_fleet():

@@ -260,3 +260,28 @@ async def test_spare_workers_start_on_demand_only():
         finally:
             env.server.faults.latency.clear()
             await env.stop()
+
+
+async def test_schedule_requeue_lands_on_the_tick_however_long_the_writes_took():
+    """A fire's status PATCH waits 6 s (a throttled client): the reconcile returns 6 s after it
+    computed ``RequeueAfter = next - now``.  The requeue is the tick itself (``Result.requeue_at_ns``)
+    -- before the fix it landed 6 s late, and every tick after a slow write fired that much later."""
+    env = TestEnv()
+    await env.create_cron(new_cron("t", NS, "*/1 * * * *", PT_TMPL))
+    await env.start_manager()
+    await env.settle()
+    orig = env.server.patch
+    slow = [True]
+
+    def patch(gvr, ns, name, body, ptype="merge", sub=None):
+        if slow[0] and gvr.resource == "crons" and sub == "status":
+            slow[0] = False
+            env.clock.advance(6)  # virtual time passes while the write waits
+        return orig(gvr, ns, name, body, ptype, sub)
+
+    env.server.patch = patch  # type: ignore[assignment]
+    await env.advance(60)      # tick 1 fires; its status write takes 6 s
+    assert _jobs(env, "t") == ["t-1767268920"]
+    await env.advance(60 - 6)  # exactly the next tick (12:02:00)
+    assert _jobs(env, "t") == ["t-1767268920", "t-1767268980"], "the next tick fired late"
+    await env.stop()

@@ -133,3 +133,39 @@ async def test_discovery_failure_is_an_error_not_a_missing_kind():
     rep = await preflight(env.client)
     assert not rep.ok and any("cannot discover kubeflow.org/v1" in e for e in rep.errors)
     assert "is not served" not in render(rep)
+
+
+async def test_preflight_warns_when_the_client_budget_cannot_carry_the_fleet():
+    """Round-4 verdict #6: an upgrade that keeps the reference's ``qps: 30 / burst: 50``
+    (``/root/reference/cmd/operator/start.go:218-219``) collapses ticks at 1000 minutely Crons;
+    preflight finds the busiest minute from the schedules and warns.  The chart's defaults carry
+    the same fleet: no warning about lost runs."""
+    from cron_operator_amd.api.v1alpha1 import new_cron
+    from cron_operator_amd.cmd.main import DEFAULT_BURST, DEFAULT_QPS
+
+    env = TestEnv()
+    tmpl = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob", "spec": {}}
+    for i in range(1000):
+        env.server.create(CRON_GVR, NS, new_cron(f"m{i:04d}", NS, "* * * * *", tmpl).to_dict())
+    env.server.create(CRON_GVR, NS, new_cron("nightly", NS, "0 3 * * *", tmpl).to_dict())
+    paused = new_cron("paused", NS, "* * * * *", tmpl).to_dict()
+    paused["spec"]["suspend"] = True  # a suspended Cron does not fire
+    env.server.create(CRON_GVR, NS, paused)
+    now = env.clock.now(__import__("cron_operator_amd.utils.gotime", fromlist=["UTC"]).UTC)
+    ref = await preflight(env.client, NS, qps=30, burst=50, now=now)
+    assert ref.peak_fires_per_minute == 1001  # every minutely Cron plus the nightly one at 03:00
+    assert any("ticks collapse" in w for w in ref.budget_warnings), ref.budget_warnings
+    text = render(ref)
+    assert "warning: the busiest minute has 1001 fires" in text and "set qps >= 67" in text
+    chart = await preflight(env.client, NS, qps=DEFAULT_QPS, burst=DEFAULT_BURST, now=now)
+    assert not any("ticks collapse" in w for w in chart.budget_warnings), chart.budget_warnings
+    assert chart.ok and ref.ok  # a warning, not a failing check
+
+
+def test_preflight_budget_math():
+    from cron_operator_amd.cmd.preflight import budget_warnings
+
+    assert budget_warnings(1000, 150, 300)[0].startswith("the busiest minute's 1000 CREATEs exceed --burst 300")
+    assert len(budget_warnings(1000, 150, 300)) == 1   # within the QPS budget, beyond the burst
+    assert budget_warnings(200, 150, 300) == []
+    assert len(budget_warnings(2300, 150, 300)) == 2   # 2300 x 4 / 60 = 153 QPS > 150

@@ -261,3 +261,48 @@ async def test_retry_after_wait_holds_no_inflight_slot_and_is_throttled_again():
     finally:
         await client.close()
         await app.stop()
+
+
+async def test_low_reserve_keeps_the_burst_for_the_next_tick():
+    """Round-4 verdict #3: deferrable writes run at the refill rate without draining the burst,
+    so the tick's CREATEs that follow a wave of status PATCHes find the whole burst."""
+    import time
+
+    def run(reserve):
+        async def go():
+            b = TokenBucket(200.0, 20, low_reserve=reserve)
+            t0 = time.monotonic()
+            # a wave of 40 deferrable writes (the previous jobs' completions) ...
+            await asyncio.gather(*(b.wait(PRIORITY_LOW) for _ in range(40)))
+            low_done = time.monotonic() - t0
+            # ... then the tick: 20 CREATEs
+            t1 = time.monotonic()
+            waits = await asyncio.gather(*(b.wait(PRIORITY_HIGH) for _ in range(20)))
+            return low_done, time.monotonic() - t1, max(waits)
+        return asyncio.get_running_loop().create_task(go())
+
+    low_a, tick_a, _ = await run(0)       # the burst absorbs the writes; the tick waits ~0.1 s
+    low_b, tick_b, worst = await run(-1)  # the writes pace at 200/s; the tick gets the burst
+    assert tick_a >= 0.07 and tick_b < 0.02 and worst < 0.02, (tick_a, tick_b, worst)
+    assert low_b <= 40 / 200.0 + 0.1  # the writes still run at the refill rate
+    assert low_b >= low_a
+
+
+async def test_low_reserve_does_not_hold_high_or_normal_and_ages_low():
+    """Held low waiters never delay a more urgent request, and a low waiter older than
+    ``max_defer`` spends the reserve (delayed, never starved)."""
+    b = TokenBucket(50.0, 10, max_defer=0.1, low_reserve=-1)
+    assert b.low_reserve == 9
+    await b.wait(PRIORITY_HIGH)  # 9 left: a low request now has to wait for the bucket to refill
+    low = asyncio.ensure_future(b.wait(PRIORITY_LOW))
+    await asyncio.sleep(0)
+    assert not low.done()
+    assert await asyncio.wait_for(b.wait(PRIORITY_HIGH), 0.05) == 0.0  # not behind the held low one
+    assert await asyncio.wait_for(b.wait(PRIORITY_NORMAL), 0.05) == 0.0
+    # drain to below the reserve and keep HIGH traffic away: the low waiter ages out at max_defer
+    while b._tokens >= 1.0:
+        await b.wait(PRIORITY_HIGH)
+    waited = await asyncio.wait_for(low, 1.0)
+    # the reserve refills in 0.2 s; the waiter is served at max_defer (0.1 s), out of the reserve
+    assert 0.09 <= waited < 0.18, waited
+    assert b.aged_grants == 1
