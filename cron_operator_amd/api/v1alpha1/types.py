@@ -27,6 +27,7 @@ precision and an empty list equals a missing one.
 """
 from __future__ import annotations
 
+import dataclasses
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Union
 
@@ -56,7 +57,7 @@ def _t_eq(a: Optional[GoTime], b: Optional[GoTime]) -> bool:
     return a.sec == b.sec and a.nsec == b.nsec
 
 
-@dataclass
+@dataclass(slots=True)
 class ObjectReference:
     kind: str = ""
     namespace: str = ""
@@ -91,7 +92,7 @@ class ObjectReference:
                                resource_version=d.get("resourceVersion", ""), field_path=d.get("fieldPath", ""))
 
 
-@dataclass
+@dataclass(slots=True)
 class TypedLocalObjectReference:
     kind: str = ""
     name: str = ""
@@ -110,7 +111,7 @@ class TypedLocalObjectReference:
         return TypedLocalObjectReference(kind=d.get("kind", ""), name=d.get("name", ""), api_group=d.get("apiGroup"))
 
 
-@dataclass
+@dataclass(slots=True)
 class CronHistory:
     object: TypedLocalObjectReference = field(default_factory=TypedLocalObjectReference)
     status: str = ""
@@ -149,7 +150,7 @@ class CronHistory:
                 and _t_eq(self.created, o.created) and _t_eq(self.finished, o.finished))
 
 
-@dataclass
+@dataclass(slots=True)
 class CronStatus:
     active: List[ObjectReference] = field(default_factory=list)
     history: List[CronHistory] = field(default_factory=list)
@@ -180,8 +181,8 @@ class CronStatus:
                           last_schedule_time=time_from_json(d.get("lastScheduleTime")))
 
     def deepcopy(self) -> "CronStatus":
-        return CronStatus(active=[ObjectReference(**vars(a)) for a in self.active],
-                          history=[CronHistory(object=TypedLocalObjectReference(**vars(h.object)), status=h.status,
+        return CronStatus(active=[dataclasses.replace(a) for a in self.active],
+                          history=[CronHistory(object=dataclasses.replace(h.object), status=h.status,
                                                uid=h.uid, created=h.created, finished=h.finished)
                                    for h in self.history],
                           last_schedule_time=self.last_schedule_time)

@@ -477,6 +477,11 @@ class APIServer:
             self._watch_plan.pop(key, None)
 
     def _index_owners(self, ri: ResourceInfo, obj: Optional[Dict[str, Any]], old: Optional[Dict[str, Any]]) -> None:
+        if old is not None and obj is not None:
+            om, nm = old.get("metadata") or {}, obj.get("metadata") or {}
+            oo, no = om.get("ownerReferences"), nm.get("ownerReferences")
+            if (oo is no or oo == no) and om.get("name") == nm.get("name"):
+                return  # an update that keeps its owners (status writes): nothing to re-file
         if old is not None:
             m = old.get("metadata") or {}
             ref = (ri.group, ri.resource, m.get("namespace", ""), m.get("name", ""))

@@ -162,6 +162,10 @@ class BenchResult:
     cpu_s_apiserver: float = 0.0
     # peak RSS of each operator shard process (sharded runs; the in-process run shares the harness)
     operator_maxrss_mib: List[float] = field(default_factory=list)
+    # shard processes: peak RSS once caches were synced and the first pass done (start-up's share
+    # of the peak), and resident size at the end of the run
+    operator_ready_maxrss_mib: List[float] = field(default_factory=list)
+    operator_rss_mib: List[float] = field(default_factory=list)
     # cyclic-GC collections per generation and pause time in the operator process(es), timed region
     operator_gc: Dict[str, Any] = field(default_factory=dict)
     # one process: a starting (or newly elected) operator over the seeded cluster -- seconds from
@@ -856,6 +860,8 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
             cpu_s_operator=sum(r["cpu"] - b["cpu"] for r, b in zip(last, base)),
             cpu_s_apiserver=api1 - api0 - write_cpu,
             operator_maxrss_mib=[round(r.get("maxrss_mib", 0.0), 1) for r in last],
+            operator_ready_maxrss_mib=[round(r.get("maxrss_mib", 0.0), 1) for r in ready],
+            operator_rss_mib=[round(r.get("rss_mib", 0.0), 1) for r in last],
             operator_gc={"collections": [sum(r.get("gc_collections", [0, 0, 0])[g] - b.get("gc_collections",
                                                                                             [0, 0, 0])[g]
                                              for r, b in zip(last, base)) for g in range(3)],

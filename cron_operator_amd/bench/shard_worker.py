@@ -32,6 +32,38 @@ import time
 from typing import List
 
 
+def _trace_dump(tag: str) -> None:
+    """``CRON_BENCH_TRACEMALLOC=<prefix>`` (set before start): the 25 biggest allocation sites,
+    by traceback, appended to ``<prefix>.<pid>.txt`` at ``ready`` and at ``end``."""
+    prefix = os.environ.get("CRON_BENCH_TRACEMALLOC")
+    if not prefix:
+        return
+    import gc
+    import tracemalloc
+
+    gc.collect()
+    snap = tracemalloc.take_snapshot()
+    stats = snap.statistics("traceback")
+    with open(f"{prefix}.{os.getpid()}.txt", "a") as fh:
+        fh.write(f"== {tag}: traced {sum(x.size for x in stats) / 2**20:.1f} MiB, rss {_rss_mib():.1f} MiB\n")
+        for x in stats[:25]:
+            fh.write(f"{x.size / 2**20:8.2f} MiB {x.count:8d}  " +
+                     " <- ".join(f"{f.filename.rsplit('/', 2)[-1]}:{f.lineno}" for f in x.traceback) + "\n")
+
+
+def _maxrss_mib() -> float:
+    return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024
+
+
+def _rss_mib() -> float:
+    """Resident size now (``/proc/self/statm``), next to the peak."""
+    try:
+        with open("/proc/self/statm") as fh:
+            return int(fh.read().split()[1]) * os.sysconf("SC_PAGE_SIZE") / 2**20
+    except (OSError, ValueError, IndexError):
+        return 0.0
+
+
 async def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--url", required=True)
@@ -121,7 +153,9 @@ async def main() -> int:
 
     gcs = GcStats().start()
     out = sys.stdout
-    out.write(json.dumps({"ready": True, "owned": n_owned}) + "\n")
+    _trace_dump("ready")
+    out.write(json.dumps({"ready": True, "owned": n_owned, "maxrss_mib": _maxrss_mib(), "rss_mib": _rss_mib()})
+              + "\n")
     out.flush()
 
     loop = asyncio.get_running_loop()
@@ -175,8 +209,9 @@ async def main() -> int:
                                   "requests": client.requests, "by_verb": dict(client.requests_by_verb),
                                   "cpu": time.process_time(), "gc_s": gcs.seconds,
                                   "gc_collections": list(gcs.collections),
-                                  "maxrss_mib": resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024}) + "\n")
+                                  "maxrss_mib": _maxrss_mib(), "rss_mib": _rss_mib()}) + "\n")
             out.flush()
+    _trace_dump("end")
     mgr.stop()
     try:
         await asyncio.wait_for(task, 30)
@@ -187,6 +222,10 @@ async def main() -> int:
 
 
 if __name__ == "__main__":
+    if os.environ.get("CRON_BENCH_TRACEMALLOC"):
+        import tracemalloc
+
+        tracemalloc.start(6)
     from ..runtime import aioloop
 
     aioloop.install()  # an operator process: the native loop core, as `cron-operator start` uses

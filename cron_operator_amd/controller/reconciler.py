@@ -379,6 +379,13 @@ class WireCodecs:
         self.child_event = jsonutil.Codec(skip=[("object",) + p for p in child_skip],
                                           memo_paths=[("object",) + p for p in child_memo], memo=self.memo)
         self.child_object = jsonutil.Codec(skip=child_skip, memo_paths=child_memo, memo=self.memo)
+        # LIST pages: the same plans under items/* (the initial LIST of 110,000 jobs shares labels
+        # and owner references as the watch events do, and never builds a spec)
+        self.child_list = jsonutil.Codec(skip=[("items", "*") + p for p in child_skip],
+                                         memo_paths=[("items", "*") + p for p in child_memo], memo=self.memo)
+        self.cron_list = jsonutil.Codec(skip=[("items", "*") + mf] if slim else [],
+                                        memo_paths=[("items", "*", "spec"), ("items", "*", "status", "history", "*")],
+                                        memo=self.memo)
         self.status_patch = jsonutil.Codec(memo_paths=[("status", "history", "*")], memo=self.memo)
 
 
@@ -976,7 +983,8 @@ class CronReconciler(Reconciler):
             inf = await self.cache.get_informer(gvk, label_selector=self.child_selector,
                                                 indexers={CHILD_INDEX: label_index(LABEL_CRON_NAME)},
                                                 transform=self.child_transform(gvk),
-                                                decoder=self.codecs.child_event if self.codecs else None)
+                                                decoder=self.codecs.child_event if self.codecs else None,
+                                                list_decoder=self.codecs.child_list if self.codecs else None)
             self.child_informers[gvk] = inf
             inf.start()
             if self.on_child_informer is not None:

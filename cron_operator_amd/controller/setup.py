@@ -74,7 +74,8 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
     cron_inf = await mgr.cache.get_informer(CRON_GVK,
                                             label_selector=sharding.shard_selector(index, count) if by_label else None,
                                             transform=strip_managed_fields if opts.slim_child_cache else None,
-                                            decoder=codecs.cron_event if codecs is not None else None)
+                                            decoder=codecs.cron_event if codecs is not None else None,
+                                            list_decoder=codecs.cron_list if codecs is not None else None)
     rec = CronReconciler(mgr.client, mgr.cache, mgr.get_event_recorder_for(CONTROLLER_NAME), mgr.clock, engine,
                          opts, cron_inf, codecs)
     ctrl = Controller(CONTROLLER_NAME, rec, mgr.clock, mgr.opts.max_concurrent_reconciles, log)
@@ -167,7 +168,8 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
                 inf = await mgr.cache.get_informer(gvk, label_selector=rec.child_selector,
                                                    indexers={CHILD_INDEX: label_index(LABEL_CRON_NAME)},
                                                    transform=rec.child_transform(gvk),
-                                                   decoder=codecs.child_event if codecs is not None else None)
+                                                   decoder=codecs.child_event if codecs is not None else None,
+                                                   list_decoder=codecs.child_list if codecs is not None else None)
                 rec.child_informers[gvk] = inf
             else:
                 inf = await mgr.cache.get_informer(gvk, label_selector=rec.child_selector if by_label else None)

@@ -476,8 +476,12 @@ class Client:
 
     async def list(self, target: GVRorGVK, namespace: str = "", label_selector: Optional[str] = None,
                    field_selector: Optional[str] = None, limit: int = 0,
-                   continue_: Optional[str] = None) -> Dict[str, Any]:
+                   continue_: Optional[str] = None, decoder: Any = None) -> Dict[str, Any]:
+        """``decoder``: a ``jsonutil.Codec`` for the response body (HTTP transports; paths
+        under ``items/*``), e.g. one sharing recurring subtrees with an informer's watch codec."""
         params: Dict[str, Any] = {}
+        if decoder is not None:
+            params[DECODE] = decoder
         if label_selector:
             params["labelSelector"] = label_selector
         if field_selector:

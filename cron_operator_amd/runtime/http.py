@@ -316,7 +316,10 @@ class HttpTransport(Transport):
                 raw = await resp.read()
         except aiohttp.ClientConnectionError as e:
             raise errors.ApiError(503, "ServiceUnavailable", f"connection error: {e}") from None
-        return jsonutil.loads(raw) if raw else None
+        if not raw:
+            return None
+        dec = params.get(DECODE) if params else None
+        return dec.loads(raw) if dec is not None else jsonutil.loads(raw)
 
     async def watch(self, gvr: GroupVersionResource, namespace: str = "",
                     params: Optional[Dict[str, Any]] = None, decoder: Any = None) -> WatchStream:

@@ -110,11 +110,14 @@ class Informer:
                  page_size: int = 500, name: str = "", resync_period: float = 0.0,
                  clock: Optional[Clock] = None, transform: Optional[Transform] = None,
                  min_watch_timeout: float = MIN_WATCH_TIMEOUT, watch_idle_timeout: float = WATCH_IDLE_TIMEOUT,
-                 decoder: Any = None):
+                 decoder: Any = None, list_decoder: Any = None):
         self.client = client
         # watch-event decoder for byte transports (a jsonutil.Codec): it may skip subtrees no
-        # consumer reads and reuse memoised ones; None decodes plainly
+        # consumer reads and reuse memoised ones; None decodes plainly.  ``list_decoder`` does
+        # the same for LIST pages (paths under ``items/*``): the initial LIST then shares what
+        # later watch events share (a child's labels and owner references with its siblings')
         self.decoder = decoder
+        self.list_decoder = list_decoder
         self._watch_kw: Dict[str, Any] = {"decoder": decoder} if decoder is not None else {}
         # watch liveness: every WATCH asks the server to end it after a random
         # [min, 2*min) seconds (client-go reflector), and a watch silent for
@@ -356,7 +359,7 @@ class Informer:
         tf = self.transform
         while True:
             page = await self.client.list(self.target, self.namespace, self.label_selector,
-                                          limit=self.page_size, continue_=cont)
+                                          limit=self.page_size, continue_=cont, decoder=self.list_decoder)
             if tf is not None:
                 page["items"] = [tf(o) for o in page.get("items") or []]
             if out is None:
@@ -580,7 +583,8 @@ class Cache:
 
     async def get_informer(self, target: Any, label_selector: Optional[str] = None,
                            indexers: Optional[Dict[str, IndexFunc]] = None,
-                           transform: Optional[Transform] = None, decoder: Any = None) -> Informer:
+                           transform: Optional[Transform] = None, decoder: Any = None,
+                           list_decoder: Any = None) -> Informer:
         """The shared informer for ``(target, namespace, selector)``.  ``transform`` and
         ``decoder`` apply when this call creates it (like ``cache.Options.ByObject[...].Transform``)."""
         gvr = await self._resolve(target)
@@ -591,7 +595,7 @@ class Cache:
                            name=f"{gvr.resource}.{gvr.group}" if gvr.group else gvr.resource,
                            resync_period=self.resync_period, clock=self.clock, transform=transform,
                            min_watch_timeout=self.min_watch_timeout, watch_idle_timeout=self.watch_idle_timeout,
-                           decoder=decoder)
+                           decoder=decoder, list_decoder=list_decoder)
             self._informers[key] = inf
             if self._started:
                 inf.start()

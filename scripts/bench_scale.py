@@ -58,6 +58,8 @@ def main() -> int:
                          "operator_gc": r.operator_gc, "phase_ms": r.phase_ms,
                          # peak RSS of each operator shard process (sharded runs only)
                          "operator_maxrss_mib": r.operator_maxrss_mib,
+                         "operator_ready_maxrss_mib": r.operator_ready_maxrss_mib,
+                         "operator_rss_mib": r.operator_rss_mib,
                          # one process: start (or fail-over) over the seeded cluster
                          "startup_sync_s": r.startup_sync_s, "startup_first_pass_s": r.startup_first_pass_s,
                          # one process: the operator runs in this process (with the harness's own

@@ -212,6 +212,7 @@ def check_docs() -> List[Tuple[str, int, str, str]]:
                 caption = has
             if _MEASURE.search(block) and not has and not (row and caption):
                 problems.append((rel, ln, "D001", f"measured figure without evidence: {block[:90]!r}"))
+    problems.extend(check_current_tables())
     pdir = os.path.join(ROOT, "profiles")
     files = sorted(f for f in os.listdir(pdir) if not f.startswith("."))
     if len(files) > MAX_PROFILES:
@@ -220,6 +221,39 @@ def check_docs() -> List[Tuple[str, int, str, str]]:
         if f"profiles/{f}" not in cited:
             problems.append(("profiles", 0, "D002", f"{f} is not cited by any doc"))
     return problems
+
+
+def latest_driver_record() -> str:
+    """``BENCH_rNN.json`` of the latest round the driver has recorded ("" if none)."""
+    rounds = [int(m.group(1)) for f in os.listdir(ROOT) for m in [re.match(r"BENCH_r(\d+)\.json$", f)] if m]
+    return f"BENCH_r{max(rounds):02d}.json" if rounds else ""
+
+
+def check_current_tables() -> List[Tuple[str, int, str, str]]:
+    """D003: a section headed "Current ..." must rest on the latest driver record -- cite
+    ``BENCH_r<latest>.json`` -- so a "current" table cannot outlive the run that superseded it."""
+    latest = latest_driver_record()
+    if not latest:
+        return []
+    out: List[Tuple[str, int, str, str]] = []
+    for path in doc_files():
+        with open(path, encoding="utf-8") as fh:
+            lines = fh.read().splitlines()
+        rel = os.path.relpath(path, ROOT)
+        for i, line in enumerate(lines):
+            m = re.match(r"(#+)\s+(.*)", line)
+            if not m or not re.search(r"\bcurrent\b", m.group(2), re.I):
+                continue
+            level = len(m.group(1))
+            body = []
+            for nxt in lines[i + 1:]:
+                h = re.match(r"(#+)\s", nxt)
+                if h and len(h.group(1)) <= level:
+                    break
+                body.append(nxt)
+            if latest not in "\n".join(body):
+                out.append((rel, i + 1, "D003", f"'{m.group(2)}' does not cite the latest driver record {latest}"))
+    return out
 
 
 def main(argv: List[str]) -> int:

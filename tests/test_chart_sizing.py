@@ -9,6 +9,9 @@ reference's ``--qps 30`` (``/root/reference/charts/cron-operator/values.yaml:62-
 minute: ticks collapse, and the reconciler's catch-up (``cron_controller.go:408-436``)
 runs only the last missed tick -- scheduled runs are lost without an error.
 
+(Round 5: running-job status writes no longer cost the operator a PATCH -- 4 requests per
+fire, ``tests/test_lifecycle.py`` -- and deferrable writes leave the burst to the tick.)
+
 This test runs that ratio **time-compressed**: ``N`` Crons with the client budget scaled
 by ``N/1000`` (burst) and by ``N/1000 x C`` (QPS), and one virtual minute every ``60/C``
 seconds of real time -- a tick's requests take the same fraction of the minute as 1000
@@ -144,7 +147,7 @@ async def test_reference_client_budget_collapses_ticks_at_the_same_fleet():
     assert missing, "expected collapsed ticks at the reference's qps 30 / burst 50"
 
 
-CLAIMED = 1800  # the fleet values.yaml's qps comment claims at 100% of the budget
+CLAIMED = 2250  # the fleet values.yaml's qps comment claims at 100% of the budget (N/15 QPS)
 
 
 async def test_leader_keeps_the_lease_at_twice_the_claimed_fleet():
