@@ -172,6 +172,11 @@ class BenchResult:
     # Manager.start() to synced caches, and to the first pass over every Cron done (the queue idle)
     startup_sync_s: float = 0.0
     startup_first_pass_s: float = 0.0
+    # one process, throttled: the client bucket's tokens and waiters (low/normal/high) at each
+    # timed tick, and each tick's p50 tick->create
+    tick_tokens: List[float] = field(default_factory=list)
+    tick_waiting: List[List[int]] = field(default_factory=list)
+    tick_p50_ms: List[float] = field(default_factory=list)
     # leader_elect: the Lease was lost at some point / the longest successful renewal window (s)
     lease_lost: Optional[bool] = None
     lease_max_renew_s: Optional[float] = None
@@ -631,6 +636,9 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
         reqv0: Dict[str, int] = {}
         t_start = 0.0
         excluded = 0.0  # timed steps: seconds inside the harness's lifecycle write calls
+        tick_tokens: List[float] = []
+        tick_waiting: List[List[int]] = []
+        tick_p50_ms: List[float] = []
         phase_ms: Dict[str, List[float]] = {"completion": [], "fire": []}
         if n_pre:
             phase_ms["lifecycle_writes"] = []
@@ -665,9 +673,16 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
             lat.clear()
             creates_this_tick[0] = 0
             tick_wall[0] = t1
+            lim = client.limiter
+            if lim is not None and k > cfg.warmup:  # the bucket the tick's CREATEs find
+                lim._refill(time.monotonic())
+                tick_tokens.append(round(lim._tokens, 1))
+                tick_waiting.append([lim.waiting_at(p) for p in (0, 1, 2)])
             await set_time(tick_ns)
             await wait_settled(tick_ns, k, deadline)
             t2 = time.perf_counter()
+            if k > cfg.warmup and lat:
+                tick_p50_ms.append(round(_pct(lat, 50) * 1000, 1))
             dt = t2 - t0 - writes
             if k > cfg.warmup:
                 step_ms.append(dt * 1000)
@@ -701,6 +716,7 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
             engine=default_engine().name, fastjson_native=jsonutil.NATIVE,
             cpu_s_operator=cpu1[0] - cpu0[0], cpu_s_apiserver=cpu1[1] - cpu0[1] - write_cpu[0], operator_gc=gc_stats,
             startup_sync_s=startup_sync_s, startup_first_pass_s=startup_first_pass_s)
+        res.tick_tokens, res.tick_waiting, res.tick_p50_ms = tick_tokens, tick_waiting, tick_p50_ms
         if mgr.elector is not None:
             res.lease_lost = mgr.elector.lost.is_set() or not mgr.elector.is_leader
             res.lease_max_renew_s = mgr.elector.max_renew_s

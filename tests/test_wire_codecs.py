@@ -104,3 +104,51 @@ async def test_reference_mode_decodes_plainly():
     assert rec.codecs is None
     assert jsonutil.json_equal(cached["status"], stored["status"])
     assert children and all("spec" in c for c in children)
+
+
+async def test_initial_list_shares_labels_and_owners_and_trims_status():
+    """A starting operator over an existing fleet: the child informer's first LIST is decoded with
+    the same memo plans as its watch events (``WireCodecs.child_list``), so the jobs of one Cron
+    share one labels dict and one ownerReferences list, no spec is built, and each job's status is
+    trimmed to what classifies it (``compact_child``) -- the memory a 10,000-Cron fleet caches."""
+    from cron_operator_amd.api.meta import new_controller_ref
+    from cron_operator_amd.api.v1alpha1 import CRON_GVK
+    from cron_operator_amd.apiserver.http import APIServerApp
+    from cron_operator_amd.runtime.client import Client
+    from cron_operator_amd.runtime.http import HttpTransport
+    from cron_operator_amd.runtime.kubeconfig import RestConfig
+
+    env = TestEnv()
+    cron = await env.create_cron(new_cron("c", NS, "*/1 * * * *", PT_TMPL, history_limit=5))
+    for i in range(4):
+        name = f"c-{1767268800 + 60 * i}"
+        job = jsonutil.deepcopy(PT_TMPL)
+        job["metadata"] = {"name": name, "namespace": NS, "labels": {LABEL_CRON_NAME: "c"},
+                           "ownerReferences": [new_controller_ref(cron, CRON_GVK)]}
+        env.server.create(PT, NS, job)
+        env.server.patch(PT, NS, name, {"status": finished_status("PyTorchJob", name, "2026-01-01T12:00:30Z", True)},
+                         "merge", "status")
+    app = APIServerApp(env.server)
+    port = await app.start("127.0.0.1", 0)
+    client = Client(HttpTransport(RestConfig(host=f"http://127.0.0.1:{port}")), qps=-1)
+    mgr = Manager(client, ManagerOptions(clock=env.clock, health_probe_bind_address="0", metrics_bind_address="0"))
+    ctrl, rec = await setup_with_manager(mgr, ReconcilerOptions())
+    task = asyncio.get_running_loop().create_task(mgr.start())
+    try:
+        await asyncio.wait_for(mgr.started.wait(), 20)
+        inf = next(iter(rec.child_informers.values()))
+        kids = inf.list(NS, copy=False)
+        assert len(kids) == 4 and all("spec" not in k for k in kids)
+        for k in kids:
+            st = k["status"]
+            assert set(st) <= {"conditions", "completionTime"}, st
+            assert [c["type"] for c in st["conditions"]] == ["Succeeded"]  # the terminal (= last) one
+            assert set(st["conditions"][0]) <= {"type", "status", "lastTransitionTime"}
+        if jsonutil.NATIVE:
+            assert len({id(k["metadata"]["labels"]) for k in kids}) == 1
+            assert len({id(k["metadata"]["ownerReferences"]) for k in kids}) == 1
+    finally:
+        mgr.stop()
+        await asyncio.wait({task}, timeout=10)
+        await client.close()
+        await app.stop()
