@@ -171,6 +171,7 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
                                                    decoder=codecs.child_event if codecs is not None else None,
                                                    list_decoder=codecs.child_list if codecs is not None else None)
                 rec.child_informers[gvk] = inf
+                rec.ensure_derive(inf, gvk)
             else:
                 inf = await mgr.cache.get_informer(gvk, label_selector=rec.child_selector if by_label else None)
             if assigner is not None:

@@ -136,6 +136,7 @@ class Informer:
         # classification) take them from ``derived`` instead of re-reading the object
         self.derive: Optional[Callable[[Dict[str, Any]], Any]] = None
         self.derived: Dict[str, Any] = {}
+        self._prederived: Dict[int, Any] = {}  # id(LIST item) -> derived right after its transform
         self.resync_period = resync_period
         self.clock = clock
         self._resync_timer: Optional[TimerHandle] = None
@@ -279,7 +280,8 @@ class Informer:
                                 h.on_delete(obj)
                     return
                 if self.derive is not None:
-                    self.derived[key] = self.derive(obj)
+                    pre = self._prederived.pop(id(obj), None) if self._prederived else None
+                    self.derived[key] = pre if pre is not None else self.derive(obj)
                 if old is None:
                     for h in self.handlers:
                         if h.on_add:
@@ -304,7 +306,8 @@ class Informer:
             return
         self.store[key] = obj
         if self.derive is not None:
-            self.derived[key] = self.derive(obj)
+            pre = self._prederived.pop(id(obj), None) if self._prederived else None
+            self.derived[key] = pre if pre is not None else self.derive(obj)
         self._index(key, obj, old)
         if old is None:
             for h in self.handlers:
@@ -350,6 +353,13 @@ class Informer:
             self._apply("DELETED", self.store[key])
 
     # ------------------------------------------------------------------ reflector
+    def _transform_derive(self, tf: Transform, obj: Dict[str, Any]) -> Dict[str, Any]:
+        """A LIST item transformed and derived at once, as a watch event is: a transform may hand
+        the derive function what only the untransformed object had (``compact_child``)."""
+        out = tf(obj)
+        self._prederived[id(out)] = self.derive(out)  # type: ignore[misc]
+        return out
+
     async def _list_pages(self) -> Dict[str, Any]:
         """Paged LIST (client-go pager) whose items are transformed page by page, as each page
         arrives: a large initial LIST then never holds every untrimmed object at once (the
@@ -361,7 +371,9 @@ class Informer:
             page = await self.client.list(self.target, self.namespace, self.label_selector,
                                           limit=self.page_size, continue_=cont, decoder=self.list_decoder)
             if tf is not None:
-                page["items"] = [tf(o) for o in page.get("items") or []]
+                items = [tf(o) for o in page.get("items") or []] if self.derive is None else \
+                    [self._transform_derive(tf, o) for o in page.get("items") or []]
+                page["items"] = items
             if out is None:
                 out = page
             else:
@@ -395,6 +407,7 @@ class Informer:
             self._replace(lst.get("items") or [])
         finally:
             self._pretransformed = False
+            self._prederived.clear()  # items _replace skipped (unchanged) were derived for nothing
         self.last_rv = (lst.get("metadata") or {}).get("resourceVersion", "")
         if not self.synced.is_set():
             self.synced.set()

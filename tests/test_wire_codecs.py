@@ -144,6 +144,11 @@ async def test_initial_list_shares_labels_and_owners_and_trims_status():
             assert set(st) <= {"conditions", "completionTime"}, st
             assert [c["type"] for c in st["conditions"]] == ["Succeeded"]  # the terminal (= last) one
             assert set(st["conditions"][0]) <= {"type", "status", "lastTransitionTime"}
+        # every finished job shares one read-only status; its memo has the completion time
+        assert len({id(k["status"]) for k in kids}) == 1
+        for info in inf.derived.values():
+            assert info.finished and info.cls.status == "Succeeded"
+            assert info.cls.finished_at is not None and info.cls.finished_at.rfc3339() == "2026-01-01T12:00:30Z"
         if jsonutil.NATIVE:
             assert len({id(k["metadata"]["labels"]) for k in kids}) == 1
             assert len({id(k["metadata"]["ownerReferences"]) for k in kids}) == 1
