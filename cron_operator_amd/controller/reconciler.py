@@ -218,6 +218,10 @@ def slim_child(obj: Dict[str, Any]) -> Dict[str, Any]:
     return obj
 
 
+# the child metadata read anywhere: its key, version, creation (history order) and deletion, the
+# cron-name label (index) and the controller owner (event mapping)
+CHILD_METADATA = ("name", "namespace", "uid", "resourceVersion", "creationTimestamp", "deletionTimestamp",
+                  "labels", "ownerReferences")
 _COND_KEEP = ("type", "status", "lastTransitionTime")
 _TERMINAL_TYPES = frozenset(("Succeeded", "Failed", "Complete"))
 _STATUS_KEEP = ("completionTime", "phase", "launcherStatus")
@@ -260,6 +264,12 @@ def compact_child(gvk: GroupVersionKind, policy: WorkloadPolicy) -> Callable[[Di
 
     def transform(obj: Dict[str, Any]) -> Dict[str, Any]:
         slim_child(obj)
+        m = obj.get("metadata")
+        if type(m) is dict and len(m) > 7:
+            # only the metadata a reconcile (and the informer, the event predicates, expectations)
+            # reads: annotations -- kubectl's last-applied-configuration holds a whole manifest --
+            # finalizers, generation and the like are dropped
+            obj["metadata"] = {k: m[k] for k in CHILD_METADATA if k in m}
         st = obj.get("status")
         if type(st) is not dict or not st:
             return obj

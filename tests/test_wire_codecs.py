@@ -124,6 +124,7 @@ async def test_initial_list_shares_labels_and_owners_and_trims_status():
         name = f"c-{1767268800 + 60 * i}"
         job = jsonutil.deepcopy(PT_TMPL)
         job["metadata"] = {"name": name, "namespace": NS, "labels": {LABEL_CRON_NAME: "c"},
+                           "annotations": {"kubectl.kubernetes.io/last-applied-configuration": "{}" * 200},
                            "ownerReferences": [new_controller_ref(cron, CRON_GVK)]}
         env.server.create(PT, NS, job)
         env.server.patch(PT, NS, name, {"status": finished_status("PyTorchJob", name, "2026-01-01T12:00:30Z", True)},
@@ -139,6 +140,9 @@ async def test_initial_list_shares_labels_and_owners_and_trims_status():
         inf = next(iter(rec.child_informers.values()))
         kids = inf.list(NS, copy=False)
         assert len(kids) == 4 and all("spec" not in k for k in kids)
+        # metadata: only what is read (no annotations, generation, managedFields)
+        assert all(set(k["metadata"]) <= {"name", "namespace", "uid", "resourceVersion", "creationTimestamp",
+                                          "labels", "ownerReferences"} for k in kids), kids[0]["metadata"]
         for k in kids:
             st = k["status"]
             assert set(st) <= {"conditions", "completionTime"}, st
