@@ -126,15 +126,18 @@ class CronHistory:
         """JSON form; ``shared=True`` returns one cached dict per entry (read-only for callers)."""
         if shared and self._json is not None:
             return self._json
+        # keys in sorted order, as a real apiserver serves a custom resource back (encoding/json
+        # of unstructured content): the watch echo of a status write is then byte-identical to
+        # what the wire codec remembered for this entry, and decodes to this very dict
         d: Dict[str, Any] = {}
-        if self.uid:
-            d["uid"] = self.uid
-        d["object"] = self.object.to_dict()
-        d["status"] = self.status
         if self.created is not None:
             d["created"] = time_to_json(self.created)
         if self.finished is not None:
             d["finished"] = time_to_json(self.finished)
+        d["object"] = self.object.to_dict()
+        d["status"] = self.status
+        if self.uid:
+            d["uid"] = self.uid
         if shared:
             self._json = d
         return d

@@ -177,6 +177,7 @@ class BenchResult:
     tick_tokens: List[float] = field(default_factory=list)
     tick_waiting: List[List[int]] = field(default_factory=list)
     tick_p50_ms: List[float] = field(default_factory=list)
+    tick_lat_q_ms: List[List[float]] = field(default_factory=list)
     # leader_elect: the Lease was lost at some point / the longest successful renewal window (s)
     lease_lost: Optional[bool] = None
     lease_max_renew_s: Optional[float] = None
@@ -639,6 +640,7 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
         tick_tokens: List[float] = []
         tick_waiting: List[List[int]] = []
         tick_p50_ms: List[float] = []
+        tick_lat_q_ms: List[List[float]] = []  # per tick: tick->create at 0/10/30/50/90/100 %
         phase_ms: Dict[str, List[float]] = {"completion": [], "fire": []}
         if n_pre:
             phase_ms["lifecycle_writes"] = []
@@ -683,6 +685,7 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
             t2 = time.perf_counter()
             if k > cfg.warmup and lat:
                 tick_p50_ms.append(round(_pct(lat, 50) * 1000, 1))
+                tick_lat_q_ms.append([round(_pct(lat, q) * 1000, 1) for q in (0, 10, 30, 50, 90, 100)])
             dt = t2 - t0 - writes
             if k > cfg.warmup:
                 step_ms.append(dt * 1000)
@@ -717,6 +720,7 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
             cpu_s_operator=cpu1[0] - cpu0[0], cpu_s_apiserver=cpu1[1] - cpu0[1] - write_cpu[0], operator_gc=gc_stats,
             startup_sync_s=startup_sync_s, startup_first_pass_s=startup_first_pass_s)
         res.tick_tokens, res.tick_waiting, res.tick_p50_ms = tick_tokens, tick_waiting, tick_p50_ms
+        res.tick_lat_q_ms = tick_lat_q_ms
         if mgr.elector is not None:
             res.lease_lost = mgr.elector.lost.is_set() or not mgr.elector.is_leader
             res.lease_max_renew_s = mgr.elector.max_renew_s

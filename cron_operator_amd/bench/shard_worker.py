@@ -51,6 +51,163 @@ def _trace_dump(tag: str) -> None:
                      " <- ".join(f"{f.filename.rsplit('/', 2)[-1]}:{f.lineno}" for f in x.traceback) + "\n")
 
 
+_TRACE = {"fires": 0, "snap": None}
+
+
+def _trace_diff(first: int, last: int) -> None:
+    """With tracemalloc on: snapshot after fire ``first`` and, after fire ``last``, append the
+    25 biggest growths between the two (by traceback) to ``<prefix>.<pid>.txt``."""
+    import gc
+    import tracemalloc
+
+    _TRACE["fires"] += 1
+    n = _TRACE["fires"]
+    if n not in (first, last):
+        return
+    gc.collect()
+    snap = tracemalloc.take_snapshot()
+    if n == first:
+        _TRACE["snap"] = snap
+        return
+    stats = snap.compare_to(_TRACE["snap"], "traceback")
+    with open(f"{os.environ['CRON_BENCH_TRACEMALLOC']}.{os.getpid()}.txt", "a") as fh:
+        fh.write(f"== growth fire {first} -> {last}: {sum(x.size_diff for x in stats) / 2**20:.2f} MiB, "
+                 f"rss {_rss_mib():.1f}\n")
+        for x in stats[:25]:
+            fh.write(f"{x.size_diff / 2**20:8.2f} MiB {x.count_diff:8d}  " +
+                     " <- ".join(f"{f.filename.rsplit('/', 2)[-1]}:{f.lineno}" for f in reversed(x.traceback))
+                     + "\n")
+    _TRACE["snap"] = None
+
+
+def _mem_dump(tag: str, mgr, rec) -> None:
+    """``CRON_BENCH_MEMDUMP=<prefix>``: per informer, the objects cached and their deep size
+    (each object counted once, in the first place it is reached), the wire memo, the
+    reconciler's memos, the derived child memos by slot, pymalloc's arena statistics, the live
+    futures and container types, appended to ``<prefix>.<pid>.txt`` (plus the RSS after every
+    phase and what the process held at the phase's highest RSS).  A diagnostic: the walk
+    itself raises the peak RSS it reports."""
+    prefix = os.environ.get("CRON_BENCH_MEMDUMP")
+    if not prefix:
+        return
+    import gc
+    from collections import Counter
+
+    gc.collect()
+    seen: set = set()
+
+    def deep(o) -> int:
+        stack, total = [o], 0
+        while stack:
+            x = stack.pop()
+            i = id(x)
+            if i in seen:
+                continue
+            seen.add(i)
+            total += sys.getsizeof(x)
+            if isinstance(x, dict):
+                stack.extend(x.keys())
+                stack.extend(x.values())
+            elif isinstance(x, (list, tuple, set, frozenset)):
+                stack.extend(x)
+            elif hasattr(x, "__slots__"):
+                stack.extend(getattr(x, s) for s in x.__slots__ if hasattr(x, s))
+            elif hasattr(x, "__dict__") and not isinstance(x, type):
+                stack.append(x.__dict__)
+        return total
+
+    with open(f"{prefix}.{os.getpid()}.txt", "a") as fh:
+        fh.write(f"== {tag}: rss {_rss_mib():.1f} MiB\n")
+        for name, inf in sorted(mgr.cache._informers.items(), key=lambda kv: str(kv[0])):
+            st = deep(inf.store) / 2**20
+            dv = deep(inf.derived) / 2**20
+            stale = sum(1 for k, d in inf.derived.items() if getattr(d, "obj", None) is not None
+                        and d.obj is not inf.store.get(k))
+            fh.write(f"  informer {name}: {len(inf.store)} objects store {st:.2f} MiB derived {dv:.2f} MiB"
+                     f" (derived of another version: {stale})\n")
+        if rec.codecs is not None:
+            fh.write(f"  wire memo: {rec.codecs.memo.stats()}\n")
+        for attr, val in sorted(vars(rec).items()):
+            if isinstance(val, (dict, list, set)) and len(val) > 100:
+                fh.write(f"  rec.{attr}: {len(val)} entries {deep(val) / 2**20:.2f} MiB\n")
+        for name, inf in sorted(mgr.cache._informers.items(), key=lambda kv: str(kv[0])):
+            if not inf.store:
+                continue
+            keys = sorted(inf.store)
+            for k in (keys[0], keys[-1]):
+                o = inf.store[k]
+                seen.clear()
+                parts = {f: deep(v) for f, v in o.items()} if isinstance(o, dict) else {}
+                seen.clear()
+                d = inf.derived.get(k)
+                fh.write(f"  sample {k}: {parts} derived {deep(d) if d is not None else 0} "
+                         f"{type(d).__name__}\n    {json.dumps(o, default=str)[:1500]}\n")
+                if d is not None:
+                    kinds = [(s, type(getattr(d, s, None)).__name__) for s in getattr(d, "__slots__", ())]
+                    fh.write(f"    derived: {kinds}\n")
+        # the unique bytes of each derived slot, stores walked first: the oldest and the newest
+        # finished child (LIST-decoded vs watch-decoded)
+        seen.clear()
+        for inf in mgr.cache._informers.values():
+            deep(inf.store)
+        for inf in mgr.cache._informers.values():
+            fin = [(int((inf.store[k].get("metadata") or {}).get("resourceVersion") or 0), k)
+                   for k, d in inf.derived.items() if getattr(d, "finished", False)]
+            if not fin:
+                continue
+            fin.sort()
+            groups: dict = {}
+            for k, d in inf.derived.items():
+                g = groups.setdefault(bool(getattr(d, "finished", False)), [0, 0, Counter()])
+                g[0] += 1
+                for s in d.__slots__:
+                    n = deep(getattr(d, s, None))
+                    g[1] += n
+                    g[2][s] += n
+            for f, (n, b, per) in groups.items():
+                fh.write(f"  derived finished={f}: {n} memos, {b / max(1, n):.0f} B each: "
+                         + str({s: round(v / max(1, n)) for s, v in per.items()}) + "\n")
+            for _, k in (fin[0], fin[-1]):
+                d = inf.derived[k]
+                fh.write(f"  derived {k}: " + str({s: deep(getattr(d, s, None)) for s in d.__slots__}) + "\n")
+                he = getattr(d, "history_entry", None)
+                if he is not None:
+                    fh.write(f"    history_entry: {he!r}\n")
+        seen.clear()
+        # pymalloc's own accounting (arenas vs allocated blocks: what fragmentation costs)
+        r, w = os.pipe()
+        saved = os.dup(2)
+        os.dup2(w, 2)
+        try:
+            sys._debugmallocstats()
+        finally:
+            os.dup2(saved, 2)
+            os.close(w)
+            os.close(saved)
+        txt = b""
+        while True:
+            chunk = os.read(r, 1 << 16)
+            if not chunk:
+                break
+            txt += chunk
+        os.close(r)
+        tail = [ln for ln in txt.decode(errors="replace").splitlines() if ln.startswith(("#", "Total"))
+                or "arenas" in ln or "bytes in" in ln]
+        fh.write("  pymalloc: " + " | ".join(x.strip() for x in tail[-14:]) + "\n")
+        futs = [o for o in gc.get_objects() if type(o).__name__ == "Future"]
+        fh.write(f"  futures alive: {len(futs)} done {sum(1 for f in futs if f.done())}\n")
+        for f in futs[:: max(1, len(futs) // 4)][:4]:
+            refs = [r for r in gc.get_referrers(f) if r is not futs]
+            names = [type(r).__name__ + ":" + str(getattr(r, "cr_code", getattr(r, "f_code", "")))[:60]
+                     for r in refs][:4]
+            fh.write(f"    future done={f.done()} referrers: {names}\n")
+            for r in refs[:2]:
+                rr = [type(x).__name__ for x in gc.get_referrers(r) if x is not refs][:5]
+                fh.write(f"      {type(r).__name__} <- {rr}\n")
+        cnt = Counter(type(o).__name__ for o in gc.get_objects())
+        fh.write("  gc objects: " + ", ".join(f"{k} {v}" for k, v in cnt.most_common(12)) + "\n")
+
+
 def _maxrss_mib() -> float:
     return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024
 
@@ -154,11 +311,31 @@ async def main() -> int:
     gcs = GcStats().start()
     out = sys.stdout
     _trace_dump("ready")
+    _mem_dump("ready", mgr, rec)
     out.write(json.dumps({"ready": True, "owned": n_owned, "maxrss_mib": _maxrss_mib(), "rss_mib": _rss_mib()})
               + "\n")
     out.flush()
 
     loop = asyncio.get_running_loop()
+    peak = [0.0, ""]
+    if os.environ.get("CRON_BENCH_MEMDUMP"):
+        async def sample() -> None:  # what the process held at its highest RSS
+            while True:
+                await asyncio.sleep(0.01)
+                r = _rss_mib()
+                if r > peak[0]:
+                    pend = []
+                    for inf in mgr.cache._informers.values():
+                        w = getattr(getattr(inf, "_watch", None), "_s", None)
+                        n = getattr(w, "_n", None)
+                        pend.append(getattr(n, "pending", -1) if n is not None else -1)
+                    lim, gate = client.limiter, client.inflight
+                    peak[0], peak[1] = r, (
+                        f"rss {r:.1f} active {ctrl.active} released {ctrl.released} queue {len(ctrl.queue)} "
+                        f"tasks {len(asyncio.all_tasks())} limiter waiting {lim.waiting if lim else 0} "
+                        f"inflight {gate.inflight if gate else 0} gate waiting {gate.waiting if gate else 0} "
+                        f"watch pending {pend}")
+        sampler = loop.create_task(sample())  # noqa: F841
     reader = asyncio.StreamReader()
     await loop.connect_read_pipe(lambda: asyncio.StreamReaderProtocol(reader), sys.stdin)
 
@@ -204,6 +381,17 @@ async def main() -> int:
             tick_wall[0] = time.perf_counter()
             clock.set(int(msg["ns"]))
             await settled(msg.get("phase", "fire"), int(msg.get("tick_ns", msg["ns"])))
+            if os.environ.get("CRON_BENCH_TRIM"):
+                import ctypes
+                ctypes.CDLL("libc.so.6").malloc_trim(0)
+            if os.environ.get("CRON_BENCH_TRACEMALLOC") and msg.get("phase", "fire") == "fire":
+                _trace_diff(int(os.environ.get("CRON_BENCH_TRACE_FROM", "3")),
+                            int(os.environ.get("CRON_BENCH_TRACE_TO", "9")))
+            if os.environ.get("CRON_BENCH_MEMDUMP"):
+                with open(f"{os.environ['CRON_BENCH_MEMDUMP']}.{os.getpid()}.txt", "a") as fh:
+                    fh.write(f"  {msg.get('phase', 'fire')} {msg['ns']}: rss {_rss_mib():.1f} "
+                             f"maxrss {_maxrss_mib():.1f} | peak: {peak[1]}\n")
+                peak[0] = 0.0
             # counters are cumulative: the harness differences them over its timed window
             out.write(json.dumps({"ok": True, "lat": lat, "reconciles": ctrl.reconciles,
                                   "requests": client.requests, "by_verb": dict(client.requests_by_verb),
@@ -212,6 +400,7 @@ async def main() -> int:
                                   "maxrss_mib": _maxrss_mib(), "rss_mib": _rss_mib()}) + "\n")
             out.flush()
     _trace_dump("end")
+    _mem_dump("end", mgr, rec)
     mgr.stop()
     try:
         await asyncio.wait_for(task, 30)

@@ -101,6 +101,7 @@ from ..api.meta import (
     GroupVersionKind,
     creation_timestamp,
     set_controller_reference,
+    time_from_json,
 )
 from ..api.v1alpha1 import (
     CRON_GVK,
@@ -189,7 +190,7 @@ def child_info(w: Dict[str, Any], gvk: GroupVersionKind, policy: WorkloadPolicy)
             _CLS_MEMO[0] = None
         else:
             cls = classify(w, gvk, policy)
-        sort_key = creation_timestamp(w).key()
+        sort_key = _sort_key(m.get("creationTimestamp"))
     except Exception as e:  # noqa: BLE001 - kf.ConversionError, or a malformed object
         err = e
         cls = None  # never "finished" with an error: it would reach history and fail there
@@ -200,6 +201,34 @@ def child_info(w: Dict[str, Any], gvk: GroupVersionKind, policy: WorkloadPolicy)
     info.uid = m.get("uid", "")
     info.err = err
     return info
+
+
+def _sort_key(ts: Any) -> Tuple[int, int]:
+    """History order of a child created at ``ts`` (its ``creationTimestamp``): one shared tuple
+    per timestamp -- the children a tick creates share their creation second."""
+    k = _SORT_KEYS.get(ts) if ts.__class__ is str else None
+    if k is None:
+        t = time_from_json(ts) if ts else None
+        k = t.key() if t is not None else GoTime.zero().key()  # as creation_timestamp() reads it
+        if ts.__class__ is str:
+            if len(_SORT_KEYS) >= 4096:
+                _SORT_KEYS.clear()
+            _SORT_KEYS[ts] = k
+    return k
+
+
+_SORT_KEYS: Dict[str, Tuple[int, int]] = {}
+
+
+def _gv_str(gvk: GroupVersionKind) -> str:
+    """``group/version`` of ``gvk``, one shared string per kind (every history entry holds it)."""
+    s = _GV_STR.get(gvk)
+    if s is None:
+        s = _GV_STR[gvk] = str(gvk.group_version())
+    return s
+
+
+_GV_STR: Dict[GroupVersionKind, str] = {}
 
 
 # A child as the status sync sees it: its object (``obj``), classification (``cls``/``finished``)
@@ -404,8 +433,10 @@ class WireCodecs:
     back when the watch echoes the same bytes.  ``slim`` also skips what the caches drop
     anyway: a child's ``spec`` and every ``managedFields``."""
 
-    def __init__(self, slim: bool = True, memo_slots: int = 1 << 16):
-        self.memo = jsonutil.Memo(memo_slots)
+    def __init__(self, slim: bool = True, memo_slots: int = 1 << 14, memo_max_slots: int = 1 << 19):
+        # grows with the fleet: ~12 values per Cron (its history entries, a labels map and an owner
+        # reference) stay remembered up to ~40,000 Crons per process
+        self.memo = jsonutil.Memo(memo_slots, memo_max_slots)
         mf = ("metadata", "managedFields")
         child_skip = [("spec",), mf] if slim else []
         child_memo = [("metadata", "labels"), ("metadata", "ownerReferences")]
@@ -720,6 +751,10 @@ class CronReconciler(Reconciler):
             return False
         if not jsonutil.json_equal(new.get("status") or {}, status):
             return False
+        if status and new.get("status") is not status:
+            # the cached object keeps the status dict we wrote (equal, just compared) instead of
+            # its decoded copy: active refs and lists held once per Cron, not twice
+            new["status"] = status
         self._own_rv[key] = (m.get("resourceVersion", ""), status)
         return True
 
@@ -1217,7 +1252,7 @@ class CronReconciler(Reconciler):
         m = w.get("metadata") or {}
         wgvk = GroupVersionKind.from_object(w)
         entry = CronHistory(uid=m.get("uid", ""),
-                            object=TypedLocalObjectReference(api_group=wgvk.group_version().__str__(),
+                            object=TypedLocalObjectReference(api_group=_gv_str(wgvk),
                                                              kind=wgvk.kind, name=m.get("name", "")),
                             status=c.status, created=creation_timestamp(w))
         if c.finished:

@@ -126,7 +126,7 @@ def sort_by_creation_timestamp(workloads: List[Dict[str, Any]]) -> None:
     workloads.sort(key=lambda w: creation_timestamp(w).key())
 
 
-@dataclass
+@dataclass(slots=True)
 class Classification:
     finished: bool
     status: str                      # history.status: last condition type (or phase)

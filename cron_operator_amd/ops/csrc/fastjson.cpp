@@ -49,6 +49,7 @@
 #include <algorithm>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -440,8 +441,10 @@ inline uint64_t span_hash(const char* p, size_t n) {
 
 struct MemoSlot {
   uint64_t hash = 0;
-  std::string bytes;
+  char* bytes = nullptr;    // malloc'd copy of the value's JSON (nullptr: empty slot)
   PyObject* obj = nullptr;  // strong ref
+  uint32_t len = 0;
+  uint32_t stamp = 0;       // table clock at the last hit / store (least recently used goes first)
   bool canonical = false;   // `bytes` is this encoder's own output for `obj` (not a peer's encoding)
 };
 
@@ -449,79 +452,217 @@ struct MemoSlot {
 // it meets again (by identity) instead of encoding it anew.  A slot holds a strong reference to
 // its object, so a pointer match is that very object; memo values are never mutated (the
 // contract above), so their canonical bytes stay exact.
+//
+// 4-way set associative, least recently used way replaced.  Once half full, the table doubles (up to
+// `max_slots`) instead of replacing a way that was used within the last table-size operations: the working set
+// -- a 10,000-Cron shard remembers ~10 history entries plus a labels map and an owner reference
+// per Cron, ~120,000 values -- then fits instead of thrashing (a missed label map is a fresh copy
+// in every cached child).  The object -> slot index is an exact open-addressed map, so
+// forget() always drops the entry of a value that rotated out and the live count stays the
+// working set (40-byte slots; the bytes live in their own allocation).
 struct MemoTable {
+  static constexpr size_t kWays = 4;
+  static constexpr uint32_t kTomb = 0xFFFFFFFFu;
   std::vector<MemoSlot> slots;
-  std::vector<uint32_t> by_obj;  // direct-mapped: pointer hash -> slot index + 1 (0: empty)
-  size_t mask = 0;
-  uint64_t hits = 0, misses = 0, stores = 0, reuses = 0;
+  std::vector<uint32_t> by_obj;  // open addressing: slot index + 1; 0 empty, kTomb deleted
+  size_t mask = 0, omask = 0, max_slots = 0, used = 0, tombs = 0;
+  uint32_t clock = 0;
+  uint64_t hits = 0, misses = 0, stores = 0, reuses = 0, evictions = 0, grows = 0;
 
-  explicit MemoTable(size_t n) {
+  static size_t pow2(size_t n) {
     size_t cap = 64;
     while (cap < n) cap <<= 1;
+    return cap;
+  }
+  MemoTable(size_t n, size_t max_n) {
+    const size_t cap = pow2(n);
+    max_slots = std::max(cap, pow2(max_n));
     slots.resize(cap);
-    by_obj.assign(cap, 0);
+    by_obj.assign(cap * 2, 0);
     mask = cap - 1;
+    omask = cap * 2 - 1;
   }
   ~MemoTable() { clear(); }
+  static void release(MemoSlot& sl) {
+    Py_CLEAR(sl.obj);
+    std::free(sl.bytes);
+    sl.bytes = nullptr;
+    sl.len = 0;
+    sl.hash = 0;
+    sl.canonical = false;
+  }
   void clear() {
-    for (auto& sl : slots) {
-      Py_CLEAR(sl.obj);
-      sl.bytes.clear();
-      sl.bytes.shrink_to_fit();
-      sl.hash = 0;
-      sl.canonical = false;
-    }
+    for (auto& sl : slots) release(sl);
     std::fill(by_obj.begin(), by_obj.end(), 0);
+    used = 0;
+    tombs = 0;
   }
   static inline size_t ptr_hash(const PyObject* o) {
     uint64_t x = reinterpret_cast<uintptr_t>(o) >> 4;
     x *= 0x9E3779B97F4A7C15ULL;
     return static_cast<size_t>(x >> 17);
   }
+  inline size_t bucket(uint64_t h) const { return static_cast<size_t>(h) & mask & ~(kWays - 1); }
+  // position in by_obj of the entry for `o`, or SIZE_MAX
+  size_t find_obj(const PyObject* o) const {
+    for (size_t i = ptr_hash(o) & omask;; i = (i + 1) & omask) {
+      const uint32_t e = by_obj[i];
+      if (e == 0) return SIZE_MAX;
+      if (e != kTomb && slots[e - 1].obj == o) return i;
+    }
+  }
+  void map_obj(size_t slot) {
+    const PyObject* o = slots[slot].obj;
+    const size_t at = find_obj(o);
+    if (at != SIZE_MAX) {  // the same object under other bytes: the newest slot answers for it
+      by_obj[at] = static_cast<uint32_t>(slot + 1);
+      return;
+    }
+    for (size_t i = ptr_hash(o) & omask;; i = (i + 1) & omask) {
+      const uint32_t e = by_obj[i];
+      if (e == 0 || e == kTomb) {
+        if (e == kTomb) --tombs;
+        by_obj[i] = static_cast<uint32_t>(slot + 1);
+        return;
+      }
+    }
+  }
+  void unmap_obj(size_t slot) {
+    const size_t at = find_obj(slots[slot].obj);
+    if (at != SIZE_MAX && by_obj[at] == slot + 1) {
+      by_obj[at] = kTomb;
+      ++tombs;
+    }
+  }
+  // (once the slots are consistent again: after a store or a forget)
+  inline void maybe_reindex() {
+    if (tombs > by_obj.size() / 4) reindex();
+  }
+  void reindex() {
+    std::fill(by_obj.begin(), by_obj.end(), 0);
+    tombs = 0;
+    for (size_t i = 0; i < slots.size(); ++i)
+      if (slots[i].obj != nullptr) map_obj(i);
+  }
+  static inline bool same(const MemoSlot& sl, const char* p, size_t n, uint64_t h) {
+    return sl.obj != nullptr && sl.hash == h && sl.len == n && std::memcmp(sl.bytes, p, n) == 0;
+  }
   PyObject* find(const char* p, size_t n, uint64_t h) {  // borrowed
-    const size_t i = h & mask;
-    MemoSlot& sl = slots[i];
-    if (sl.obj != nullptr && sl.hash == h && sl.bytes.size() == n && std::memcmp(sl.bytes.data(), p, n) == 0) {
-      ++hits;
-      by_obj[ptr_hash(sl.obj) & mask] = static_cast<uint32_t>(i + 1);
-      return sl.obj;
+    const size_t b = bucket(h);
+    for (size_t w = 0; w < kWays; ++w) {
+      MemoSlot& sl = slots[b + w];
+      if (same(sl, p, n, h)) {
+        ++hits;
+        sl.stamp = ++clock;
+        return sl.obj;
+      }
     }
     ++misses;
     return nullptr;
   }
-  void store(const char* p, size_t n, uint64_t h, PyObject* o, bool canonical) {
-    const size_t i = h & mask;
-    MemoSlot& sl = slots[i];
-    Py_INCREF(o);
-    Py_XSETREF(sl.obj, o);
-    sl.hash = h;
-    sl.bytes.assign(p, n);
-    sl.canonical = canonical;
-    by_obj[ptr_hash(o) & mask] = static_cast<uint32_t>(i + 1);
-    ++stores;
+  // double the table (every remembered value re-placed; one that finds its new set full is dropped)
+  void grow() {
+    std::vector<MemoSlot> old;
+    old.swap(slots);
+    const size_t cap = old.size() * 2;
+    slots.resize(cap);
+    by_obj.assign(cap * 2, 0);
+    mask = cap - 1;
+    omask = cap * 2 - 1;
+    used = 0;
+    tombs = 0;
+    ++grows;
+    for (auto& o : old) {
+      if (o.obj == nullptr) continue;
+      const size_t b = bucket(o.hash);
+      size_t w = 0;
+      while (w < kWays && slots[b + w].obj != nullptr) ++w;
+      if (w == kWays) {
+        release(o);
+        continue;
+      }
+      slots[b + w] = o;
+      o.obj = nullptr;
+      o.bytes = nullptr;
+      map_obj(b + w);
+      ++used;
+    }
   }
-  // drop the slot holding exactly `o` (found through the pointer map; false when that entry was
-  // overwritten meanwhile -- the slot is then reclaimed by the next collision instead)
+  void store(const char* p, size_t n, uint64_t h, PyObject* o, bool canonical) {
+    if (n > 0xFFFFFFFFu) return;
+    const size_t b = bucket(h);
+    size_t pick = kWays;
+    for (size_t w = 0; w < kWays; ++w) {  // the same bytes again: replace that entry
+      if (same(slots[b + w], p, n, h)) {
+        pick = w;
+        break;
+      }
+    }
+    if (pick == kWays) {
+      for (size_t w = 0; w < kWays; ++w) {
+        if (slots[b + w].obj == nullptr) {
+          pick = w;
+          break;
+        }
+      }
+    }
+    if (pick == kWays) {
+      size_t lru = 0;
+      for (size_t w = 1; w < kWays; ++w)
+        if (static_cast<uint32_t>(clock - slots[b + w].stamp) > static_cast<uint32_t>(clock - slots[b + lru].stamp))
+          lru = w;
+      if (used * 2 > slots.size() && slots.size() < max_slots &&
+          static_cast<uint32_t>(clock - slots[b + lru].stamp) < slots.size()) {
+        grow();
+        store(p, n, h, o, canonical);
+        return;
+      }
+      pick = lru;
+      ++evictions;
+    }
+    char* copy = static_cast<char*>(std::malloc(n ? n : 1));
+    if (copy == nullptr) return;  // out of memory: simply not remembered
+    std::memcpy(copy, p, n);
+    const size_t i = b + pick;
+    MemoSlot& sl = slots[i];
+    if (sl.obj != nullptr) {
+      unmap_obj(i);
+      release(sl);
+    } else {
+      ++used;
+    }
+    Py_INCREF(o);
+    sl.obj = o;
+    sl.bytes = copy;
+    sl.len = static_cast<uint32_t>(n);
+    sl.hash = h;
+    sl.canonical = canonical;
+    sl.stamp = ++clock;
+    map_obj(i);
+    ++stores;
+    maybe_reindex();
+  }
+  // drop the slot holding exactly `o` (false: nothing remembers it)
   bool forget(const PyObject* o) {
-    uint32_t& ref = by_obj[ptr_hash(o) & mask];
-    if (ref == 0) return false;
-    MemoSlot& sl = slots[ref - 1];
-    if (sl.obj != o) return false;
-    ref = 0;
-    std::string().swap(sl.bytes);  // release the buffer, not just the length
-    sl.hash = 0;
-    sl.canonical = false;
-    Py_CLEAR(sl.obj);
+    const size_t at = find_obj(o);
+    if (at == SIZE_MAX) return false;
+    const size_t i = by_obj[at] - 1;
+    by_obj[at] = kTomb;
+    release(slots[i]);
+    --used;
+    ++tombs;
+    maybe_reindex();
     return true;
   }
-  // this encoder's bytes for exactly `o`, or nullptr
-  const std::string* canonical_bytes(const PyObject* o) {
-    const uint32_t i = by_obj[ptr_hash(o) & mask];
-    if (i == 0) return nullptr;
-    const MemoSlot& sl = slots[i - 1];
-    if (sl.obj != o || !sl.canonical) return nullptr;
+  // this encoder's bytes for exactly `o` (nullptr when not remembered or a peer's bytes)
+  const MemoSlot* canonical_bytes(const PyObject* o) {
+    const size_t at = find_obj(o);
+    if (at == SIZE_MAX) return nullptr;
+    MemoSlot& sl = slots[by_obj[at] - 1];
+    if (!sl.canonical) return nullptr;
     ++reuses;
-    return &sl.bytes;
+    sl.stamp = ++clock;
+    return &sl;
   }
 };
 
@@ -1141,9 +1282,9 @@ struct Encoder {
     }
     if (node >= 0 && plan->act(node) == kActMemo) {
       if (memo != nullptr) {
-        const std::string* b = memo->canonical_bytes(o);
+        const MemoSlot* b = memo->canonical_bytes(o);
         if (b != nullptr) {
-          out.append(*b);
+          out.append(b->bytes, b->len);
           return true;
         }
       }
@@ -1657,28 +1798,32 @@ void memo_dealloc(PyObject* self) {
 }
 
 PyObject* memo_new(PyTypeObject* type, PyObject* args, PyObject* kwds) {
-  static const char* kw[] = {"slots", nullptr};
-  Py_ssize_t n = 1 << 16;
-  if (!PyArg_ParseTupleAndKeywords(args, kwds, "|n", const_cast<char**>(kw), &n)) return nullptr;
-  if (n < 1 || n > (1 << 24)) {
-    PyErr_SetString(PyExc_ValueError, "slots must be in [1, 2**24]");
+  static const char* kw[] = {"slots", "max_slots", nullptr};
+  Py_ssize_t n = 1 << 14, max_n = -1;
+  if (!PyArg_ParseTupleAndKeywords(args, kwds, "|nn", const_cast<char**>(kw), &n, &max_n)) return nullptr;
+  if (max_n < 0) max_n = std::max<Py_ssize_t>(n, 1 << 19);
+  if (n < 1 || n > (1 << 24) || max_n < n || max_n > (1 << 24)) {
+    PyErr_SetString(PyExc_ValueError, "slots must be in [1, 2**24] and max_slots in [slots, 2**24]");
     return nullptr;
   }
   PyObject* self = type->tp_alloc(type, 0);
   if (!self) return nullptr;
-  reinterpret_cast<MemoObject*>(self)->table = new MemoTable(static_cast<size_t>(n));
+  reinterpret_cast<MemoObject*>(self)->table = new MemoTable(static_cast<size_t>(n), static_cast<size_t>(max_n));
   return self;
 }
 
 PyObject* memo_stats(PyObject* self, PyObject*) {
   MemoTable* t = reinterpret_cast<MemoObject*>(self)->table;
   size_t used = 0;
-  for (const auto& sl : t->slots) used += sl.obj != nullptr;
-  return Py_BuildValue("{s:K,s:K,s:K,s:K,s:n,s:n}", "hits", static_cast<unsigned long long>(t->hits), "misses",
-                       static_cast<unsigned long long>(t->misses), "stores",
+  for (const auto& sl : t->slots) used += sl.obj != nullptr;  // (== t->used)
+  return Py_BuildValue("{s:K,s:K,s:K,s:K,s:K,s:K,s:n,s:n,s:n}", "hits", static_cast<unsigned long long>(t->hits),
+                       "misses", static_cast<unsigned long long>(t->misses), "stores",
                        static_cast<unsigned long long>(t->stores), "reuses",
-                       static_cast<unsigned long long>(t->reuses), "used", static_cast<Py_ssize_t>(used),
-                       "slots", static_cast<Py_ssize_t>(t->slots.size()));
+                       static_cast<unsigned long long>(t->reuses), "evictions",
+                       static_cast<unsigned long long>(t->evictions), "grows",
+                       static_cast<unsigned long long>(t->grows), "used", static_cast<Py_ssize_t>(used),
+                       "slots", static_cast<Py_ssize_t>(t->slots.size()),
+                       "max_slots", static_cast<Py_ssize_t>(t->max_slots));
 }
 
 PyObject* memo_clear(PyObject* self, PyObject*) {
@@ -1915,7 +2060,7 @@ PyMODINIT_FUNC PyInit__fastjson(void) {
   MemoType.tp_name = "_fastjson.Memo";
   MemoType.tp_basicsize = sizeof(MemoObject);
   MemoType.tp_flags = Py_TPFLAGS_DEFAULT;
-  MemoType.tp_doc = "Memo(slots=65536): bytes -> decoded object table shared by Codecs";
+  MemoType.tp_doc = "Memo(slots=16384, max_slots=524288): bytes -> decoded object table shared by Codecs (grows to max_slots)";
   MemoType.tp_new = memo_new;
   MemoType.tp_dealloc = memo_dealloc;
   MemoType.tp_methods = memo_methods;

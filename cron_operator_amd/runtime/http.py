@@ -2,20 +2,18 @@
 
 Works against a real kube-apiserver (kubeconfig / in-cluster config) and the
 framework's fake apiserver served by :mod:`cron_operator_amd.apiserver.http`.
-Request/response verbs go through the lean keep-alive pool of
-:mod:`.fasthttp` (``fast=True``, the default) or aiohttp (``fast=False``);
-watch streams use aiohttp and are read line by line (newline-delimited JSON)
-with a large line limit so big objects fit.
+Requests, watch streams and discovery go through the lean keep-alive pool of
+:mod:`.fasthttp` (``fast=True``, the default) or aiohttp (``fast=False``, imported only
+then: it costs a process ~13 MiB); aiohttp watch streams are read line by line
+(newline-delimited JSON) with a large line limit so big objects fit.
 """
 from __future__ import annotations
 
 import asyncio
 import json
 import re
-from typing import Any, Dict, List, Optional, Tuple
+from typing import TYPE_CHECKING, Any, Dict, List, Optional, Tuple
 from urllib.parse import quote
-
-import aiohttp
 
 from ..api import errors
 from ..api.meta import GroupVersion, GroupVersionResource
@@ -24,6 +22,9 @@ from . import metrics
 from .client import ACCEPT, DECODE, DISCARD, PATCH_CONTENT_TYPES, Transport, WatchStream
 from .fasthttp import ConnectionFailed, HttpPool, HttpStatusError, Stream, encode_query
 from .kubeconfig import RestConfig
+
+if TYPE_CHECKING:
+    import aiohttp
 
 
 _PREFIXES: Dict[Tuple[GroupVersionResource, str], str] = {}
@@ -73,6 +74,8 @@ class _HttpWatch(WatchStream):
         self._decode = decoder or _decode_event
 
     async def __anext__(self) -> Tuple[str, Dict[str, Any]]:
+        import aiohttp
+
         if self._done:
             raise StopAsyncIteration
         while True:
@@ -211,6 +214,8 @@ class HttpTransport(Transport):
         return kw
 
     def _sess(self) -> aiohttp.ClientSession:
+        import aiohttp
+
         if self.config.rotating and self._session is not None:
             self._rotate_token()
         if self._session is None or self._session.closed:
@@ -300,6 +305,8 @@ class HttpTransport(Transport):
                 return None
             dec = params.get(DECODE)
             return dec.loads(raw) if dec is not None else jsonutil.loads(raw)
+        import aiohttp
+
         url = self.config.host + path
         headers = {"Accept": params.get(ACCEPT) or "application/json"}
         data = None
@@ -338,6 +345,8 @@ class HttpTransport(Transport):
             except (ConnectionFailed, OSError, asyncio.TimeoutError) as e:
                 raise errors.ApiError(503, "ServiceUnavailable", f"connection error: {e}") from None
             return _FastWatch(stream)
+        import aiohttp
+
         url = self.config.host + resource_path(gvr, namespace)
         timeout = aiohttp.ClientTimeout(total=None, sock_connect=self._timeout)
         try:
@@ -356,6 +365,19 @@ class HttpTransport(Transport):
             await self._fresh_exec()
         path = f"/api/{group_version.version}" if not group_version.group else \
             f"/apis/{group_version.group}/{group_version.version}"
+        if self.fast:
+            try:
+                status, raw, _ = await self._fast_pool().request_full("GET", path, None, "application/json",
+                                                                      "application/json")
+            except (ConnectionFailed, OSError, asyncio.TimeoutError) as e:
+                raise errors.ApiError(503, "ServiceUnavailable", f"connection error: {e}") from None
+            if status >= 400:
+                if status == 401:
+                    self._unauthorized()
+                raise _status_error(status, raw)
+            return (jsonutil.loads(raw) if raw else {}).get("resources") or []
+        import aiohttp
+
         try:
             async with self._sess().get(self.config.host + path, **self._tls_kw()) as resp:
                 if resp.status >= 400:

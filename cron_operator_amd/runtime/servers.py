@@ -12,6 +12,8 @@
   SubjectAccessReview (``start.go:127-133``).  Without ``--metrics-cert-path`` a
   self-signed certificate is generated (openssl), as controller-runtime does.
   ``--metrics-bind-address=0`` disables the server.
+
+Both run on :mod:`.miniweb` (asyncio, HTTP/1.1), not a web framework.
 """
 from __future__ import annotations
 
@@ -22,12 +24,11 @@ import subprocess
 import tempfile
 from typing import Any, Awaitable, Callable, Dict, Optional, Tuple
 
-from aiohttp import web
-
 from ..api import errors
 from ..api.meta import GroupVersionResource
 from ..utils.logging import get_logger
 from . import metrics
+from . import miniweb as web
 
 Check = Callable[[], Optional[str]]  # returns None when healthy, else a reason
 
@@ -74,11 +75,11 @@ class ProbeServer:
         self.bind = bind
         self.healthz: Dict[str, Check] = {}
         self.readyz: Dict[str, Check] = {}
-        self._runner: Optional[web.AppRunner] = None
+        self._server: Optional[web.Server] = None
         self.port: Optional[int] = None
 
-    def app(self) -> web.Application:
-        app = web.Application()
+    def app(self) -> web.Router:
+        app = web.Router()
 
         def handler(checks: Dict[str, Check], kind: str):
             async def h(req: web.Request) -> web.Response:
@@ -92,10 +93,10 @@ class ProbeServer:
                 return web.Response(status=code, text=body)
             return h
 
-        app.router.add_get("/healthz", handler(self.healthz, "healthz"))
-        app.router.add_get("/healthz/{check}", handler(self.healthz, "healthz"))
-        app.router.add_get("/readyz", handler(self.readyz, "readyz"))
-        app.router.add_get("/readyz/{check}", handler(self.readyz, "readyz"))
+        app.add_get("/healthz", handler(self.healthz, "healthz"))
+        app.add_get("/healthz/{check}", handler(self.healthz, "healthz"))
+        app.add_get("/readyz", handler(self.readyz, "readyz"))
+        app.add_get("/readyz/{check}", handler(self.readyz, "readyz"))
 
         async def traces(req: web.Request) -> web.Response:
             from . import tracing
@@ -107,30 +108,21 @@ class ProbeServer:
                 return web.json_response({"spans": t.spans()})
             return web.json_response(t.chrome_trace())
 
-        app.router.add_get("/debug/traces", traces)
+        app.add_get("/debug/traces", traces)
         return app
 
     async def start(self) -> None:
         addr = parse_bind_address(self.bind)
         if addr is None:
             return
-        self._runner = web.AppRunner(self.app(), access_log=None)
-        await self._runner.setup()
-        site = web.TCPSite(self._runner, addr[0], addr[1])
-        await site.start()
-        self.port = _bound_port(site)
+        self._server = web.Server(self.app())
+        await self._server.start(addr[0], addr[1])
+        self.port = self._server.port
 
     async def stop(self) -> None:
-        if self._runner is not None:
-            await self._runner.cleanup()
-            self._runner = None
-
-
-def _bound_port(site: web.TCPSite) -> Optional[int]:
-    server = getattr(site, "_server", None)
-    if server is not None and server.sockets:
-        return server.sockets[0].getsockname()[1]
-    return None
+        if self._server is not None:
+            await self._server.stop()
+            self._server = None
 
 
 def self_signed_cert(directory: str, host: str = "localhost") -> Tuple[str, str]:
@@ -164,7 +156,7 @@ class MetricsServer:
         self.key_name = key_name
         self.client = client  # for TokenReview / SubjectAccessReview
         self.enable_http2 = enable_http2
-        self._runner: Optional[web.AppRunner] = None
+        self._server: Optional[web.Server] = None
         self._tmp: Optional[tempfile.TemporaryDirectory] = None
         self.port: Optional[int] = None
         self.extra_handlers: Dict[str, Callable[[web.Request], Awaitable[web.Response]]] = {}
@@ -199,8 +191,8 @@ class MetricsServer:
             return web.Response(status=403, text=f'Authorization denied for user {user.get("username", "")}\n')
         return None
 
-    def app(self) -> web.Application:
-        app = web.Application()
+    def app(self) -> web.Router:
+        app = web.Router()
 
         async def handle(req: web.Request) -> web.Response:
             denied = await self._authorize(req)
@@ -209,9 +201,9 @@ class MetricsServer:
             body = metrics.exposition()
             return web.Response(body=body, headers={"Content-Type": "text/plain; version=0.0.4; charset=utf-8"})
 
-        app.router.add_get("/metrics", self.handler or handle)
+        app.add_get("/metrics", self.handler or handle)
         for path, h in self.extra_handlers.items():
-            app.router.add_get(path, h)
+            app.add_get(path, h)
         return app
 
     def _ssl(self) -> Optional[ssl.SSLContext]:
@@ -227,7 +219,7 @@ class MetricsServer:
         if self.cert_dir:
             metrics.CERT_READS.inc()
         ctx.load_cert_chain(crt, key)
-        # HTTP/2 is off unless --enable-http2 (start.go:83-98); aiohttp speaks HTTP/1.1 only
+        # HTTP/2 is off unless --enable-http2 (start.go:83-98); this server speaks HTTP/1.1 only
         ctx.set_alpn_protocols(["http/1.1"])
         self._ctx = ctx
         return ctx
@@ -296,11 +288,9 @@ class MetricsServer:
             return
         if self.enable_http2:
             self.log.info("HTTP/2 requested but the metrics server only serves HTTP/1.1")
-        self._runner = web.AppRunner(self.app(), access_log=None)
-        await self._runner.setup()
-        site = web.TCPSite(self._runner, addr[0], addr[1], ssl_context=self._ssl())
-        await site.start()
-        self.port = _bound_port(site)
+        self._server = web.Server(self.app())
+        await self._server.start(addr[0], addr[1], ssl_context=self._ssl())
+        self.port = self._server.port
         if self.secure and self.cert_dir and self.cert_poll_interval > 0:
             self._cert_watch = asyncio.get_running_loop().create_task(self._watch_certs(
                 os.path.join(self.cert_dir, self.cert_name), os.path.join(self.cert_dir, self.key_name)))
@@ -310,9 +300,9 @@ class MetricsServer:
         if self._cert_watch is not None:
             self._cert_watch.cancel()
             self._cert_watch = None
-        if self._runner is not None:
-            await self._runner.cleanup()
-            self._runner = None
+        if self._server is not None:
+            await self._server.stop()
+            self._server = None
         if self._tmp is not None:
             self._tmp.cleanup()
             self._tmp = None

@@ -27,13 +27,14 @@ import os
 import signal
 import sys
 import time
-from typing import Dict, List, Optional, Tuple
-
-import aiohttp
-from aiohttp import web
+from typing import TYPE_CHECKING, Dict, List, Optional, Tuple
 
 from ..utils.logging import get_logger
+from . import miniweb as web
 from .servers import MetricsServer, ProbeServer
+
+if TYPE_CHECKING:  # the scraping client is imported by the supervisor only (Supervisor.run)
+    import aiohttp
 
 RESTART_BACKOFF = (1.0, 30.0)
 
@@ -212,6 +213,8 @@ class Supervisor:
         return f"shard processes not ready: {bad}" if bad else None
 
     async def _poll_ready(self) -> None:
+        import aiohttp
+
         while not self._stopping.is_set():
             for c in self.children:
                 ok = False
@@ -228,6 +231,8 @@ class Supervisor:
                 pass
 
     async def scrape(self) -> str:
+        import aiohttp
+
         async def one(c: _Child) -> Tuple[str, str]:
             if not c.running or not c.metrics_port:
                 return str(c.index), ""
@@ -274,6 +279,8 @@ class Supervisor:
                     pass
 
     async def run(self) -> int:
+        import aiohttp
+
         self._session = aiohttp.ClientSession(timeout=aiohttp.ClientTimeout(total=5))
         if self.metrics is not None:
             async def handle(req: web.Request) -> web.Response:

@@ -194,11 +194,13 @@ def dumpb_shared(obj: Any, cache: Dict[int, Any], volatile_keys: Any = ()) -> by
 class PyMemo:
     """Python twin of the native ``Memo`` (no reuse: every value is built afresh)."""
 
-    def __init__(self, slots: int = 1 << 16):
+    def __init__(self, slots: int = 1 << 14, max_slots: int = 1 << 19):
         self.slots = slots
+        self.max_slots = max(slots, max_slots)
 
     def stats(self) -> Dict[str, int]:
-        return {"hits": 0, "misses": 0, "stores": 0, "used": 0, "slots": self.slots}
+        return {"hits": 0, "misses": 0, "stores": 0, "reuses": 0, "evictions": 0, "grows": 0, "used": 0,
+                "slots": self.slots, "max_slots": self.max_slots}
 
     def forget(self, obj: Any) -> bool:
         return False

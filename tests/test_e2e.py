@@ -296,11 +296,14 @@ def test_shard_processes_in_one_pod(cluster):
                                       f"619a52b8.kubedl.io-shard-{i}")
             assert lease["spec"]["holderIdentity"]
 
+        def merged() -> bool:  # every shard process has reconciled and answered the scrape
+            st, b = _get(f"http://127.0.0.1:{mport}/metrics")
+            return st == 200 and all(
+                f'controller_runtime_reconcile_total{{shard="{i}",controller="cron",result="requeue_after"}}' in b
+                for i in range(3))
+        _wait(merged, 30, "merged metrics of the 3 shard processes", proc)
         status, body = _get(f"http://127.0.0.1:{mport}/metrics")
         assert status == 200
-        for i in range(3):
-            assert f'controller_runtime_reconcile_total{{shard="{i}",controller="cron",result="requeue_after"}}' \
-                in body
         assert body.count("# TYPE controller_runtime_reconcile_total counter") == 1
 
         # a shard process dies: health reports it, the supervisor restarts it
