@@ -178,6 +178,7 @@ class BenchResult:
     tick_waiting: List[List[int]] = field(default_factory=list)
     tick_p50_ms: List[float] = field(default_factory=list)
     tick_lat_q_ms: List[List[float]] = field(default_factory=list)
+    tick_timeline: List[Dict[str, Any]] = field(default_factory=list)
     # leader_elect: the Lease was lost at some point / the longest successful renewal window (s)
     lease_lost: Optional[bool] = None
     lease_max_renew_s: Optional[float] = None
@@ -641,6 +642,47 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
         tick_waiting: List[List[int]] = []
         tick_p50_ms: List[float] = []
         tick_lat_q_ms: List[List[float]] = []  # per tick: tick->create at 0/10/30/50/90/100 %
+        tick_timeline: List[Dict[str, Any]] = []  # the first timed tick, sampled every 250 ms
+        gc_in_tick = [0, 0.0]
+
+        async def sample_tick(t1: float) -> None:
+            """Creates done, limiter and gate state, controller state and the event loop's
+            lateness, every 250 ms for the first 4 s of a tick (where a tick's time goes)."""
+            import gc as _gc
+
+            def cb(phase: str, info: Dict[str, Any]) -> None:
+                if phase == "start":
+                    gc_in_tick[1] -= time.perf_counter()
+                else:
+                    gc_in_tick[0] += 1
+                    gc_in_tick[1] += time.perf_counter()
+
+            _gc.callbacks.append(cb)
+            try:
+                lim, gate = client.limiter, client.inflight
+                nxt = t1 + 0.25
+                lag = 0.0
+                while time.perf_counter() - t1 < 4.0:
+                    w0 = time.perf_counter()
+                    await asyncio.sleep(0.005)
+                    lag = max(lag, time.perf_counter() - w0 - 0.005)
+                    now = time.perf_counter()
+                    if now < nxt:
+                        continue
+                    nxt += 0.25
+                    if lim is not None:
+                        lim._refill(time.monotonic())
+                    tick_timeline.append({
+                        "t_ms": round((now - t1) * 1000), "creates": creates_this_tick[0],
+                        "tokens": round(lim._tokens, 1) if lim is not None else None,
+                        "waiting": [lim.waiting_at(p) for p in (0, 1, 2)] if lim is not None else None,
+                        "inflight": gate.inflight if gate is not None else None,
+                        "gate_waiting": gate.waiting if gate is not None else None,
+                        "active": ctrl.active, "released": ctrl.released, "queue": len(ctrl.queue),
+                        "max_loop_lag_ms": round(lag * 1000, 1), "gc": list(gc_in_tick)})
+                    lag = 0.0
+            finally:
+                _gc.callbacks.remove(cb)
         phase_ms: Dict[str, List[float]] = {"completion": [], "fire": []}
         if n_pre:
             phase_ms["lifecycle_writes"] = []
@@ -680,9 +722,14 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
                 lim._refill(time.monotonic())
                 tick_tokens.append(round(lim._tokens, 1))
                 tick_waiting.append([lim.waiting_at(p) for p in (0, 1, 2)])
+            sampler = None
+            if k == cfg.warmup + 1:  # the first timed tick: what the operator held, every 250 ms
+                sampler = asyncio.get_running_loop().create_task(sample_tick(t1))
             await set_time(tick_ns)
             await wait_settled(tick_ns, k, deadline)
             t2 = time.perf_counter()
+            if sampler is not None:
+                sampler.cancel()
             if k > cfg.warmup and lat:
                 tick_p50_ms.append(round(_pct(lat, 50) * 1000, 1))
                 tick_lat_q_ms.append([round(_pct(lat, q) * 1000, 1) for q in (0, 10, 30, 50, 90, 100)])
@@ -721,6 +768,7 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
             startup_sync_s=startup_sync_s, startup_first_pass_s=startup_first_pass_s)
         res.tick_tokens, res.tick_waiting, res.tick_p50_ms = tick_tokens, tick_waiting, tick_p50_ms
         res.tick_lat_q_ms = tick_lat_q_ms
+        res.tick_timeline = tick_timeline
         if mgr.elector is not None:
             res.lease_lost = mgr.elector.lost.is_set() or not mgr.elector.is_leader
             res.lease_max_renew_s = mgr.elector.max_renew_s

@@ -643,14 +643,17 @@ class CronReconciler(Reconciler):
             result = Result()
             err: Optional[BaseException] = None
             gc: Optional[List["asyncio.Future[None]"]] = [] if self.opts.overlap_gc_deletes else None
-            # with a controller worker: hand the worker slot on before the API writes
+            # with a controller worker: hand the worker slot on before the API writes -- before a
+            # tick's CREATE unless the in-flight cap is the bottleneck right now (the CREATE then
+            # runs on this worker), and always before the deferrable writes: they may wait for
+            # the tick's token reserve, which no decision on this worker should wait behind
             release = self.opts.defer_status_write and not self.client.gate_saturated()
             try:
                 try:
                     result = await self._sync(cron, log, gc, release)
                 except Exception as e:  # noqa: BLE001 - joined with the patch error below
                     err = e
-                if release and (gc or not old_status.semantic_equal(cron.status)):
+                if self.opts.defer_status_write and (gc or not old_status.semantic_equal(cron.status)):
                     release_worker()  # only writes are left: another Cron may use the slot
                 # B2: deferred status patch when status changed semantically (cron_controller.go:107-120)
                 if not old_status.semantic_equal(cron.status):

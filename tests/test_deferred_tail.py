@@ -285,3 +285,28 @@ async def test_schedule_requeue_lands_on_the_tick_however_long_the_writes_took()
     await env.advance(60 - 6)  # exactly the next tick (12:02:00)
     assert _jobs(env, "t") == ["t-1767268920", "t-1767268980"], "the next tick fired late"
     await env.stop()
+
+
+async def test_a_reconcile_that_kept_its_slot_for_the_create_releases_it_before_deferrable_writes():
+    """Box finding (chart-defaults-1000, r5f): reconciles that start while the in-flight cap is
+    saturated keep their worker for the CREATE (``gate_saturated``), and used to keep it through
+    the status PATCH too -- which, with the tick reserve, waits until the bucket refills: every
+    worker parked on a held PATCH and the tick stalled ~1.8 s.  The slot is now handed on before
+    the deferrable writes whatever the decision at the start was."""
+    env = TestEnv()
+    for i in range(4):
+        await env.create_cron(new_cron(f"g{i}", NS, "*/1 * * * *", PT_TMPL))
+    await env.start_manager(max_concurrent=1)
+    await env.settle()
+    env.client.gate_saturated = lambda: True  # type: ignore[method-assign]
+    env.server.faults.latency["patch"] = 1.0
+    try:
+        env.clock.advance(60)
+        # one worker, every PATCH held 1 s: the four CREATEs still go out within well under 1 s
+        await _until(lambda: sum(len(_jobs(env, f"g{i}")) for i in range(4)) == 4, 0.8)
+        assert env.controller.active == 0 and env.controller.released == 4
+        env.server.faults.latency.clear()
+        await _until(lambda: env.controller.queue.idle() and env.controller.in_flight() == 0, 5.0)
+    finally:
+        env.server.faults.latency.clear()
+        await env.stop()
