@@ -127,6 +127,8 @@ class BenchConfig:
     # trainingop.operator.lifecycle_statuses), each write absorbed by the operator before the
     # next; "instant" -- a single Succeeded write (rounds 1-4)
     lifecycle: str = "realistic"
+    # sample the first timed tick every 250 ms (BenchResult.tick_timeline; bench_configs rows)
+    tick_timeline: bool = False
     # burst tokens deferrable (low-priority) writes may not spend (cmd/main.py --tick-burst-reserve)
     tick_reserve: int = -1
     # run even a single shard in its own process (bench/shard_worker.py): its peak RSS is then
@@ -723,7 +725,7 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
                 tick_tokens.append(round(lim._tokens, 1))
                 tick_waiting.append([lim.waiting_at(p) for p in (0, 1, 2)])
             sampler = None
-            if k == cfg.warmup + 1:  # the first timed tick: what the operator held, every 250 ms
+            if cfg.tick_timeline and k == cfg.warmup + 1:  # the first timed tick, every 250 ms
                 sampler = asyncio.get_running_loop().create_task(sample_tick(t1))
             await set_time(tick_ns)
             await wait_settled(tick_ns, k, deadline)

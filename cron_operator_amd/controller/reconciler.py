@@ -251,6 +251,9 @@ def slim_child(obj: Dict[str, Any]) -> Dict[str, Any]:
 # cron-name label (index) and the controller owner (event mapping)
 CHILD_METADATA = ("name", "namespace", "uid", "resourceVersion", "creationTimestamp", "deletionTimestamp",
                   "labels", "ownerReferences")
+# the metadata keys a child commonly carries besides those (skipped at decode when compacting)
+CHILD_METADATA_DROPPED = ("generation", "annotations", "finalizers", "generateName", "selfLink",
+                          "deletionGracePeriodSeconds")
 _COND_KEEP = ("type", "status", "lastTransitionTime")
 _TERMINAL_TYPES = frozenset(("Succeeded", "Failed", "Complete"))
 _STATUS_KEEP = ("completionTime", "phase", "launcherStatus")
@@ -413,6 +416,10 @@ class ReconcilerOptions:
         GroupVersionKind("kubeflow.org", "v1", "TFJob"),
     )
 
+    def compact_metadata(self) -> bool:
+        """Children are cached through :func:`compact_child` (metadata whitelist included)."""
+        return self.slim_child_cache and self.compact_child_status and self.classification_cache
+
     @staticmethod
     def reference() -> "ReconcilerOptions":
         return ReconcilerOptions(list_mode="live", finished_time="now", skip_noop_patch=False,
@@ -433,12 +440,17 @@ class WireCodecs:
     back when the watch echoes the same bytes.  ``slim`` also skips what the caches drop
     anyway: a child's ``spec`` and every ``managedFields``."""
 
-    def __init__(self, slim: bool = True, memo_slots: int = 1 << 14, memo_max_slots: int = 1 << 19):
+    def __init__(self, slim: bool = True, memo_slots: int = 1 << 14, memo_max_slots: int = 1 << 19,
+                 compact_metadata: bool = False):
         # grows with the fleet: ~12 values per Cron (its history entries, a labels map and an owner
         # reference) stay remembered up to ~40,000 Crons per process
         self.memo = jsonutil.Memo(memo_slots, memo_max_slots)
         mf = ("metadata", "managedFields")
         child_skip = [("spec",), mf] if slim else []
+        if compact_metadata:
+            # what compact_child() drops from a child's metadata anyway, never built: the cached
+            # child then keeps its decoded metadata dict instead of a filtered copy per event
+            child_skip += [("metadata", k) for k in CHILD_METADATA_DROPPED]
         child_memo = [("metadata", "labels"), ("metadata", "ownerReferences")]
         self.cron_event = jsonutil.Codec(skip=[("object",) + mf] if slim else [],
                                          memo_paths=[("object", "spec"), ("object", "status", "history", "*")],
@@ -560,7 +572,7 @@ class CronReconciler(Reconciler):
         self.cron_informer = cron_informer
         # setup_with_manager passes the instance its Cron informer decodes with (one shared memo)
         self.codecs: Optional[WireCodecs] = codecs if codecs is not None or not self.opts.wire_codecs else \
-            WireCodecs(self.opts.slim_child_cache)
+            WireCodecs(self.opts.slim_child_cache, compact_metadata=self.opts.compact_metadata())
         self.expect = Expectations(self.opts.expectation_ttl, self.clock)
         prio = self.opts.request_priorities
         self._p_create = PRIORITY_HIGH if prio else PRIORITY_NORMAL    # a tick's CREATE, Replace DELETEs
@@ -1045,7 +1057,7 @@ class CronReconciler(Reconciler):
         o = self.opts
         if not o.slim_child_cache:
             return None
-        if o.compact_child_status and o.classification_cache:
+        if o.compact_metadata():
             return compact_child(gvk, o.workload)
         return slim_child
 

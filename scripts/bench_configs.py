@@ -112,7 +112,8 @@ def main() -> int:
 
         r = run_sync(BenchConfig(n_crons=n, steps=steps, warmup=warmup, mode=mode, qps=qps, burst=burst,
                                  shards=shards, apiserver_latency=lat, tls=tls, native_http=native,
-                                 lifecycle=a.lifecycle, leader_elect="leader-elect" in name), on_step)
+                                 lifecycle=a.lifecycle, leader_elect="leader-elect" in name,
+                                 tick_timeline=shards == 1), on_step)
         fires = n * steps
         row = {"config": name, "mode": mode, "shards": shards, "n_crons": n, "qps": qps, "burst": burst,
                "apiserver_latency": lat, "tls": tls, "native_http": native, "steps": steps,

@@ -17,6 +17,13 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "scripts"))
 
 
+def lifecycle_kw(a) -> dict:
+    """``lifecycle`` for BenchConfig when this tree's harness has the field (older trees: none)."""
+    from cron_operator_amd.bench import harness
+
+    return {"lifecycle": a.lifecycle} if "lifecycle" in harness.BenchConfig.__dataclass_fields__ else {}
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--fires", type=int, default=200)
@@ -24,6 +31,8 @@ def main() -> int:
     ap.add_argument("--bench", type=int, default=0, metavar="CRONS",
                     help="count the whole operator process of the headline bench instead (one process, CRONS "
                          "Crons, 3 timed steps; the fake apiserver's own process is not counted)")
+    ap.add_argument("--lifecycle", default="instant", choices=["instant", "realistic"],
+                    help="--bench: the jobs' status sequence (the headline's is instant)")
     a = ap.parse_args()
     import cProfile
 
@@ -73,7 +82,7 @@ def main() -> int:
                 win.disable()
 
         harness.run_sync(harness.BenchConfig(n_crons=a.bench, steps=steps, warmup=warmup, history_limit=10,
-                                             transport="http", shards=1), on_step=on_step)
+                                             transport="http", shards=1, **lifecycle_kw(a)), on_step=on_step)
         fires = a.bench * steps
         print(f"per fire: {counts['op'] / fires:.0f} bytecodes, {counts['ccall'] / fires:.0f} C calls", flush=True)
         for co, n in by_code.most_common(a.top):

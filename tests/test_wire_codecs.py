@@ -161,3 +161,26 @@ async def test_initial_list_shares_labels_and_owners_and_trims_status():
         await asyncio.wait({task}, timeout=10)
         await client.close()
         await app.stop()
+
+
+def test_compacting_codecs_never_build_the_child_metadata_the_cache_drops():
+    """With the compact child cache, the keys compact_child() would drop from a child's metadata
+    (generation, annotations such as kubectl's last-applied manifest, finalizers, ...) are
+    skipped while decoding: the cached child keeps its decoded metadata dict, no filtered copy."""
+    import json
+
+    from cron_operator_amd.controller.reconciler import CHILD_METADATA, CHILD_METADATA_DROPPED, WireCodecs
+
+    meta = {"name": "j", "namespace": "ns", "uid": "u", "resourceVersion": "5", "generation": 1,
+            "creationTimestamp": "2026-01-01T00:00:00Z", "labels": {"a": "b"},
+            "annotations": {"kubectl.kubernetes.io/last-applied-configuration": "{}"}, "finalizers": ["x"],
+            "ownerReferences": [{"kind": "Cron", "name": "c", "uid": "cu", "controller": True}]}
+    obj = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob", "metadata": meta, "spec": {"x": 1}}
+    line = json.dumps({"type": "ADDED", "object": obj}).encode()
+    _, got = WireCodecs(compact_metadata=True).child_event(line)
+    assert set(got["metadata"]) == {k for k in CHILD_METADATA if k in meta}
+    assert not set(got["metadata"]) & set(CHILD_METADATA_DROPPED) and "spec" not in got
+    page = json.dumps({"kind": "List", "metadata": {}, "items": [obj]}).encode()
+    assert set(WireCodecs(compact_metadata=True).child_list.loads(page)["items"][0]["metadata"]) == set(got["metadata"])
+    _, full = WireCodecs().child_event(line)  # without the compact cache: all of it
+    assert set(full["metadata"]) == set(meta)
