@@ -47,9 +47,8 @@ def child_update_matters(old, new, gvk: GroupVersionKind, policy: WorkloadPolicy
     writes are such updates (``/root/reference/test/crds/kubeflow.org_pytorchjobs.yaml:4739-4828``);
     the reference requeues the Cron on each (``cron_controller.go:70-77``, no predicates)."""
     om, nm = old.get("metadata") or {}, new.get("metadata") or {}
-    for k in _CHILD_META:
-        if om.get(k) != nm.get(k):
-            return True
+    if om is not nm and [*map(om.get, _CHILD_META)] != [*map(nm.get, _CHILD_META)]:  # compared in C
+        return True
     try:
         # ``new_info``: the child informer's memo of ``new`` (child_info), computed already
         if new_info is not None and new_info.obj is new:
@@ -118,28 +117,29 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
             m = obj.get("metadata") or {}
             return f"{m.get('namespace', '')}/{(m.get('labels') or {}).get(LABEL_CRON_NAME, '')}"
 
-        owned_preds = []
-        if opts.expectations and opts.skip_expected_events:
-            # events that only confirm what the reconciler already folded into status
-            def not_expected(event: str, old, new) -> bool:
-                ex = rec.expect
-                if event == "create":
-                    return not (ex.pending or ex.created) or not ex.matches_created(key_of(new), new)
-                if event == "delete":
-                    return not ex.deleted or not ex.matches_deleted(key_of(new), new)
-                return True
-            owned_preds.append(not_expected)
-        if opts.skip_unchanged_child_updates and opts.active_ref_resource_version != "live":
-            policy = opts.workload
+        # one predicate for the child events (no per-event loop over several): creates and deletes
+        # that only confirm what the reconciler already folded into status are dropped, and so are
+        # updates that change nothing a reconcile reads
+        skip_expected = opts.expectations and opts.skip_expected_events
+        skip_unchanged = opts.skip_unchanged_child_updates and opts.active_ref_resource_version != "live"
+        policy = opts.workload
+        ex = rec.expect
 
-            def changed(event: str, old, new, g=gvk, i=inf) -> bool:
-                if event != "update" or old is None:
+        def owned_event(event: str, old, new, g=gvk, i=inf) -> bool:
+            if event == "update":
+                if not skip_unchanged or old is None:
                     return True
                 m = new.get("metadata") or {}
                 return child_update_matters(old, new, g, policy,
                                             i.derived.get(f"{m.get('namespace', '')}/{m.get('name', '')}"))
-            owned_preds.append(changed)
-        ctrl.watch_owned(inf, CRON_GVK, owned_preds)
+            if not skip_expected:
+                return True
+            if event == "create":
+                return not (ex.pending or ex.created) or not ex.matches_created(key_of(new), new)
+            if event == "delete":
+                return not ex.deleted or not ex.matches_deleted(key_of(new), new)
+            return True
+        ctrl.watch_owned(inf, CRON_GVK, [owned_event] if skip_expected or skip_unchanged else [])
         if assigner is not None:
             assigner.watch_soon(mgr.cache, gvk, child=True)
         if opts.expectations:
