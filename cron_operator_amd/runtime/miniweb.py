@@ -19,6 +19,8 @@ from urllib.parse import parse_qsl, unquote
 
 MAX_HEAD = 16 * 1024  # request line + headers
 MAX_BODY = 1 << 20    # a GET with a body is read and ignored up to this size
+IDLE_TIMEOUT = 75.0   # a keep-alive connection with no request in flight is closed after this
+REQUEST_TIMEOUT = 30.0  # a request must be complete (head and body) this long after its first byte
 _REASONS = {200: "OK", 400: "Bad Request", 401: "Unauthorized", 403: "Forbidden", 404: "Not Found",
             405: "Method Not Allowed", 413: "Payload Too Large", 431: "Request Header Fields Too Large",
             500: "Internal Server Error", 503: "Service Unavailable"}
@@ -104,14 +106,32 @@ class _Conn(asyncio.Protocol):
         self.busy = False
         self.closing = False
         self.task: Optional[asyncio.Task] = None
+        self.timer: Optional[asyncio.TimerHandle] = None
+        self.reading = False  # a request's first bytes arrived, the rest not yet
+
+    def _arm(self, seconds: float) -> None:
+        """(Re)start the connection's deadline: an idle keep-alive connection, or a request that
+        trickles in (a slow client holding the port), is closed when it passes."""
+        if self.timer is not None:
+            self.timer.cancel()
+        self.timer = asyncio.get_running_loop().call_later(seconds, self._expire)
+
+    def _expire(self) -> None:
+        self.timer = None
+        if not self.busy and self.t is not None:
+            self.t.close()
 
     def connection_made(self, transport: asyncio.BaseTransport) -> None:
         self.t = transport  # type: ignore[assignment]
         self.s._conns.add(self)
+        self._arm(IDLE_TIMEOUT)
 
     def connection_lost(self, exc: Optional[BaseException]) -> None:
         self.s._conns.discard(self)
         self.closing = True
+        if self.timer is not None:
+            self.timer.cancel()
+            self.timer = None
         if self.task is not None and not self.task.done():
             self.task.cancel()
 
@@ -121,6 +141,9 @@ class _Conn(asyncio.Protocol):
             self._fail(413)
             return
         if not self.busy:
+            if not self.reading:
+                self.reading = True
+                self._arm(REQUEST_TIMEOUT)
             self._next()
 
     def _fail(self, status: int) -> None:
@@ -156,6 +179,10 @@ class _Conn(asyncio.Protocol):
         if len(self.buf) < end + 4 + n:
             return  # the (ignored) body is still arriving
         del self.buf[:end + 4 + n]
+        self.reading = False
+        if self.timer is not None:
+            self.timer.cancel()
+            self.timer = None
         keep = version == "HTTP/1.1" and headers.get("connection", "").lower() != "close"
         path, _, qs = target.partition("?")
         req = Request(method, unquote(path), dict(parse_qsl(qs, keep_blank_values=True)), headers)
@@ -192,8 +219,14 @@ class _Conn(asyncio.Protocol):
             return
         self.busy = False
         self.task = None
-        if self.buf and not self.closing:
+        if self.closing:
+            return
+        if self.buf:
+            self.reading = True
+            self._arm(REQUEST_TIMEOUT)
             self._next()
+        else:
+            self._arm(IDLE_TIMEOUT)
 
 
 def _head(status: int, headers: Dict[str, str], length: int) -> bytes:
