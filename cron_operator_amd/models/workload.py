@@ -126,7 +126,7 @@ def sort_by_creation_timestamp(workloads: List[Dict[str, Any]]) -> None:
     workloads.sort(key=lambda w: creation_timestamp(w).key())
 
 
-@dataclass(slots=True)
+@dataclass(slots=True, frozen=True)
 class Classification:
     finished: bool
     status: str                      # history.status: last condition type (or phase)
@@ -161,6 +161,9 @@ def _native_summary():
 _summary = _native_summary()
 
 
+_FINISHED: Dict[Tuple[Any, Any], "Classification"] = {}
+
+
 def classify(workload: Dict[str, Any], gvk: GroupVersionKind, policy: WorkloadPolicy) -> Classification:
     """Active/terminated decision for one child.  Raises ``kf.ConversionError``
     when the status does not convert (the reconciler then skips the child)."""
@@ -170,7 +173,15 @@ def classify(workload: Dict[str, Any], gvk: GroupVersionKind, policy: WorkloadPo
         finished, last, nconds, comp, tltt = sm
         if finished:
             t = comp if comp is not None else tltt
-            return Classification(True, last, parse_rfc3339(t) if t is not None else None)
+            # one shared (read-only) classification per outcome and completion second: the jobs a
+            # tick started mostly finish together, and every finished child is cached
+            key = (last, t)
+            c = _FINISHED.get(key)
+            if c is None:
+                if len(_FINISHED) >= 4096:
+                    _FINISHED.clear()
+                c = _FINISHED[key] = Classification(True, last, parse_rfc3339(t) if t is not None else None)
+            return c
         has_conditions = nconds > 0
     else:
         st = kf.get_job_status(workload)
@@ -194,9 +205,24 @@ def classify(workload: Dict[str, Any], gvk: GroupVersionKind, policy: WorkloadPo
             phase = raw.get("phase")
             if phase in ("Succeeded", "Failed"):
                 return Classification(True, phase, None)
-            return Classification(False, phase or last, None)
+            return _unfinished(phase or last)
     if policy.mpi_launcher_status and gvk.kind == "MPIJob" and not has_conditions:
         ls = raw.get("launcherStatus")
         if ls in (kf.JobSucceeded, kf.JobFailed):
             return Classification(True, ls, _parse_time(raw.get("completionTime")))
-    return Classification(False, last, None)
+    return _unfinished(last)
+
+
+def _unfinished(status: Any) -> Classification:
+    """The shared classification of a child still running with last condition ``status``."""
+    if status.__class__ is not str:
+        return Classification(False, status, None)
+    c = _UNFINISHED.get(status)
+    if c is None:
+        c = Classification(False, status, None)
+        if len(_UNFINISHED) < 256:
+            _UNFINISHED[status] = c
+    return c
+
+
+_UNFINISHED: Dict[Any, Classification] = {}
