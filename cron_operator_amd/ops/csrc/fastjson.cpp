@@ -453,7 +453,7 @@ struct MemoSlot {
 // its object, so a pointer match is that very object; memo values are never mutated (the
 // contract above), so their canonical bytes stay exact.
 //
-// 4-way set associative, least recently used way replaced.  Once half full, the table doubles (up to
+// 4-way set associative with two candidate sets per value, least recently used way replaced.  Once half full, the table doubles (up to
 // `max_slots`) instead of replacing a way that was used within the last table-size operations: the working set
 // -- a 10,000-Cron shard remembers ~10 history entries plus a labels map and an owner reference
 // per Cron, ~120,000 values -- then fits instead of thrashing (a missed label map is a fresh copy
@@ -502,7 +502,11 @@ struct MemoTable {
     x *= 0x9E3779B97F4A7C15ULL;
     return static_cast<size_t>(x >> 17);
   }
+  // two candidate sets per value (two-choice hashing: a set overflows far less often than with one)
   inline size_t bucket(uint64_t h) const { return static_cast<size_t>(h) & mask & ~(kWays - 1); }
+  inline size_t bucket2(uint64_t h) const {
+    return static_cast<size_t>((h >> 32) ^ (h * 0x9E3779B97F4A7C15ULL >> 29)) & mask & ~(kWays - 1);
+  }
   // position in by_obj of the entry for `o`, or SIZE_MAX
   size_t find_obj(const PyObject* o) const {
     for (size_t i = ptr_hash(o) & omask;; i = (i + 1) & omask) {
@@ -548,13 +552,15 @@ struct MemoTable {
     return sl.obj != nullptr && sl.hash == h && sl.len == n && std::memcmp(sl.bytes, p, n) == 0;
   }
   PyObject* find(const char* p, size_t n, uint64_t h) {  // borrowed
-    const size_t b = bucket(h);
-    for (size_t w = 0; w < kWays; ++w) {
-      MemoSlot& sl = slots[b + w];
-      if (same(sl, p, n, h)) {
-        ++hits;
-        sl.stamp = ++clock;
-        return sl.obj;
+    const size_t bs[2] = {bucket(h), bucket2(h)};
+    for (const size_t b : bs) {
+      for (size_t w = 0; w < kWays; ++w) {
+        MemoSlot& sl = slots[b + w];
+        if (same(sl, p, n, h)) {
+          ++hits;
+          sl.stamp = ++clock;
+          return sl.obj;
+        }
       }
     }
     ++misses;
@@ -574,56 +580,52 @@ struct MemoTable {
     ++grows;
     for (auto& o : old) {
       if (o.obj == nullptr) continue;
-      const size_t b = bucket(o.hash);
-      size_t w = 0;
-      while (w < kWays && slots[b + w].obj != nullptr) ++w;
-      if (w == kWays) {
+      size_t at = SIZE_MAX;
+      for (const size_t b : {bucket(o.hash), bucket2(o.hash)}) {
+        for (size_t w = 0; w < kWays && at == SIZE_MAX; ++w)
+          if (slots[b + w].obj == nullptr) at = b + w;
+      }
+      if (at == SIZE_MAX) {
         release(o);
         continue;
       }
-      slots[b + w] = o;
+      slots[at] = o;
       o.obj = nullptr;
       o.bytes = nullptr;
-      map_obj(b + w);
+      map_obj(at);
       ++used;
     }
   }
   void store(const char* p, size_t n, uint64_t h, PyObject* o, bool canonical) {
     if (n > 0xFFFFFFFFu) return;
-    const size_t b = bucket(h);
-    size_t pick = kWays;
-    for (size_t w = 0; w < kWays; ++w) {  // the same bytes again: replace that entry
-      if (same(slots[b + w], p, n, h)) {
-        pick = w;
-        break;
-      }
+    const size_t bs[2] = {bucket(h), bucket2(h)};
+    size_t i = SIZE_MAX;
+    for (const size_t b : bs) {  // the same bytes again: replace that entry
+      for (size_t w = 0; w < kWays && i == SIZE_MAX; ++w)
+        if (same(slots[b + w], p, n, h)) i = b + w;
     }
-    if (pick == kWays) {
-      for (size_t w = 0; w < kWays; ++w) {
-        if (slots[b + w].obj == nullptr) {
-          pick = w;
-          break;
-        }
-      }
+    for (const size_t b : bs) {  // else a free way of either set
+      for (size_t w = 0; w < kWays && i == SIZE_MAX; ++w)
+        if (slots[b + w].obj == nullptr) i = b + w;
     }
-    if (pick == kWays) {
-      size_t lru = 0;
-      for (size_t w = 1; w < kWays; ++w)
-        if (static_cast<uint32_t>(clock - slots[b + w].stamp) > static_cast<uint32_t>(clock - slots[b + lru].stamp))
-          lru = w;
+    if (i == SIZE_MAX) {  // else the least recently used of the 8
+      size_t lru = bs[0];
+      for (const size_t b : bs)
+        for (size_t w = 0; w < kWays; ++w)
+          if (static_cast<uint32_t>(clock - slots[b + w].stamp) > static_cast<uint32_t>(clock - slots[lru].stamp))
+            lru = b + w;
       if (used * 2 > slots.size() && slots.size() < max_slots &&
-          static_cast<uint32_t>(clock - slots[b + lru].stamp) < slots.size()) {
+          static_cast<uint32_t>(clock - slots[lru].stamp) < slots.size()) {
         grow();
         store(p, n, h, o, canonical);
         return;
       }
-      pick = lru;
+      i = lru;
       ++evictions;
     }
     char* copy = static_cast<char*>(std::malloc(n ? n : 1));
     if (copy == nullptr) return;  // out of memory: simply not remembered
     std::memcpy(copy, p, n);
-    const size_t i = b + pick;
     MemoSlot& sl = slots[i];
     if (sl.obj != nullptr) {
       unmap_obj(i);

@@ -338,3 +338,33 @@ def test_merge_patch_share_equals_copy(old, new):
     shared = m.create_merge_patch(old, new, True)
     assert shared == m.create_merge_patch(old, new) == jsonutil.py_create_merge_patch(old, new)
     assert jsonutil.py_create_merge_patch(old, new, True) == shared
+
+
+def test_memo_grows_with_its_working_set_and_forgets_exactly():
+    """The memo starts small, doubles once half full instead of evicting values still in use
+    (up to max_slots), and forget() drops exactly the entry of each value -- used returns to 0."""
+    memo = m.Memo(64, 4096)
+    enc = m.Codec(memo_paths=[("h", "*")], memo=memo)
+    dec = m.Codec(memo_paths=[("h", "*")], memo=memo)
+    entries = [{"uid": f"u{i}", "status": "Succeeded", "n": i} for i in range(1000)]
+    for i in range(0, 1000, 50):
+        enc.dumpb({"h": entries[i:i + 50]})
+    st = memo.stats()
+    assert st["grows"] >= 4 and st["slots"] >= 2048 and st["used"] >= 990, st
+    # the watch echo of every entry decodes to the encoder's own dicts
+    got = dec.loads(json.dumps({"h": entries}, separators=(",", ":")))["h"]
+    shared = sum(a is b for a, b in zip(got, entries))
+    assert shared >= 990
+    for e in entries:
+        memo.forget(e)
+    # left: only the decoder's own copies of the few entries that had been evicted
+    assert memo.stats()["used"] == len(entries) - shared
+
+
+def test_memo_is_bounded_by_max_slots():
+    memo = m.Memo(64, 256)
+    enc = m.Codec(memo_paths=[("h", "*")], memo=memo)
+    for i in range(0, 5000, 100):
+        enc.dumpb({"h": [{"uid": f"v{j}"} for j in range(i, i + 100)]})
+    st = memo.stats()
+    assert st["slots"] == 256 and st["used"] <= 256 and st["evictions"] > 0, st
