@@ -130,7 +130,8 @@ def drive(scratch: str, iters: int) -> None:
         except (ValueError, RecursionError):
             pass
     # plan-driven codecs: memo paths remembered by the encoder, reused by identity and by bytes
-    memo = fj.Memo(256)
+    # (a small table: growth, set overflow, LRU eviction and the object index's rebuilds all run)
+    memo = fj.Memo(64, 512)
     codec = fj.Codec(skip=[("s",)], memo_paths=[("h", "*"), ("m",)], memo=memo)
     for _ in range(iters // 8):
         hist = [_tree(rng) for _ in range(rng.randint(0, 4))]
