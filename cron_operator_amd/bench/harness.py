@@ -181,6 +181,8 @@ class BenchResult:
     tick_p50_ms: List[float] = field(default_factory=list)
     tick_lat_q_ms: List[List[float]] = field(default_factory=list)
     tick_timeline: List[Dict[str, Any]] = field(default_factory=list)
+    limiter_max_wait_s: List[float] = field(default_factory=list)  # per priority [low, normal, high]
+    limiter_aged_grants: int = 0
     # leader_elect: the Lease was lost at some point / the longest successful renewal window (s)
     lease_lost: Optional[bool] = None
     lease_max_renew_s: Optional[float] = None
@@ -770,6 +772,9 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
             startup_sync_s=startup_sync_s, startup_first_pass_s=startup_first_pass_s)
         res.tick_tokens, res.tick_waiting, res.tick_p50_ms = tick_tokens, tick_waiting, tick_p50_ms
         res.tick_lat_q_ms = tick_lat_q_ms
+        if client.limiter is not None:  # the longest waits of the run, warm-up included
+            res.limiter_max_wait_s = [round(x, 3) for x in client.limiter.max_wait_by_priority]
+            res.limiter_aged_grants = client.limiter.aged_grants
         res.tick_timeline = tick_timeline
         if mgr.elector is not None:
             res.lease_lost = mgr.elector.lost.is_set() or not mgr.elector.is_leader

@@ -109,6 +109,7 @@ class TokenBucket(_PriorityWaiters):
         self._last = time.monotonic()
         self._lock = threading.Lock()
         self.total_wait = 0.0
+        self.max_wait_by_priority = [0.0, 0.0, 0.0]  # the longest wait per priority class (s)
         self.accepted = 0
         self._timer: Optional[asyncio.TimerHandle] = None
 
@@ -184,6 +185,8 @@ class TokenBucket(_PriorityWaiters):
             raise
         d = time.monotonic() - now
         self.total_wait += d
+        if d > self.max_wait_by_priority[priority]:
+            self.max_wait_by_priority[priority] = d
         return d
 
     def _arm(self, loop: asyncio.AbstractEventLoop) -> None:

@@ -125,6 +125,7 @@ def main() -> int:
                "lease_lost": r.lease_lost, "lease_max_renew_s": r.lease_max_renew_s,
                "tick_tokens": r.tick_tokens, "tick_waiting": r.tick_waiting, "tick_p50_ms": r.tick_p50_ms,
                "tick_lat_q_ms": r.tick_lat_q_ms, "tick_timeline": r.tick_timeline,
+               "limiter_max_wait_s": r.limiter_max_wait_s, "limiter_aged_grants": r.limiter_aged_grants,
                "max_step_s": round(max(r.step_ms) / 1000, 2) if r.step_ms else None,
                "step_s": [round(x / 1000, 2) for x in r.step_ms],
                "phase_s": {k: [round(x / 1000, 2) for x in v] for k, v in r.phase_ms.items()},

@@ -107,6 +107,9 @@ async def _run(qps: float, burst: int, fleet: int = FLEET, leader_elect: bool = 
                 tick_wall[now_s] = time.perf_counter()
             await asyncio.sleep(STEP_S)
     finally:
+        if stats is not None:  # deferrable writes: the longest wait (full-scale seconds), aged grants
+            stats.update(aged_grants=env.client.limiter.aged_grants,
+                         low_max_wait_s=env.client.limiter.max_wait_by_priority[0] * C)
         el = env.manager.elector if env.manager is not None else None
         if stats is not None and el is not None:
             stats.update(lost=el.lost.is_set(), leader=el.is_leader, max_renew_s=el.max_renew_s,
@@ -130,8 +133,11 @@ async def _run(qps: float, burst: int, fleet: int = FLEET, leader_elect: bool = 
 
 async def test_chart_defaults_sustain_1000_minutely_crons_time_compressed():
     qps, burst = chart_client_values()
-    missing, lat = await _run(qps, burst)
+    stats: dict = {}
+    missing, lat = await _run(qps, burst, stats=stats)
     assert missing == [], f"ticks collapsed at qps={qps} burst={burst}: {missing[:10]}"
+    # the reserve delays deferrable writes, never past max_defer (none had to be aged ahead)
+    assert stats["aged_grants"] == 0, stats
     for k, xs in lat.items():
         # real time x C = the full-scale wall time of the tick's work
         assert max(xs) * C <= 45.0, (k, max(xs) * C)

@@ -94,6 +94,9 @@ async def test_cron_events_carry_the_reconcilers_own_history_entries():
         assert all(h is e._json for h, e in zip(hist, parsed.history)), "history entries were rebuilt"
         st = rec.codecs.memo.stats()
         assert st["hits"] > 0 and st["stores"] > 0
+    # the echo of our last status write is cached as the very status dict written (active refs
+    # and lists are held once per Cron, not twice)
+    assert cached["status"] is rec._parsed_status[key][0]
     # children: spec never built, everything the reconciler reads is there
     assert children and all("spec" not in c and c["metadata"]["labels"][LABEL_CRON_NAME] == "c" for c in children)
 
