@@ -87,6 +87,23 @@ def metadata_only(obj: Dict[str, Any]) -> Dict[str, Any]:
             "metadata": {k: m[k] for k in _KEPT_METADATA if k in m}}
 
 
+_DROPPED = (("spec",), ("status",), ("metadata", "managedFields"), ("metadata", "annotations"))
+_CODECS: List[Any] = []
+
+
+def _metadata_codecs() -> Tuple[Any, Any]:
+    """(watch event, LIST page) codecs of the unassigned watches: an object's spec, status,
+    managed fields and annotations are never built.  On a first start with label routing
+    every shard LISTs the whole unlabelled fleet through these watches; decoding it whole,
+    page by page, set each shard process's peak (and so its resident size) by the fleet."""
+    if not _CODECS:
+        from ..utils import jsonutil
+
+        _CODECS.extend((jsonutil.Codec(skip=[("object",) + p for p in _DROPPED]),
+                        jsonutil.Codec(skip=[("items", "*") + p for p in _DROPPED])))
+    return _CODECS[0], _CODECS[1]
+
+
 class ShardAssigner:
     """Labels this shard's unassigned Crons and children (a leader-only runnable)."""
 
@@ -140,7 +157,9 @@ class ShardAssigner:
         if inf is not None:
             return inf
         sel = f"{LABEL_CRON_NAME},{unassigned_selector(self.count)}" if child else unassigned_selector(self.count)
-        inf = await cache.get_informer(gvk, label_selector=sel, transform=metadata_only)
+        event, page = _metadata_codecs()
+        inf = await cache.get_informer(gvk, label_selector=sel, transform=metadata_only, decoder=event,
+                                       list_decoder=page)
         self.informers[gvk] = inf
         if child:
             self._child_kinds.add(gvk)
