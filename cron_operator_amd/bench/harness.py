@@ -127,6 +127,9 @@ class BenchConfig:
     # trainingop.operator.lifecycle_statuses), each write absorbed by the operator before the
     # next; "instant" -- a single Succeeded write (rounds 1-4)
     lifecycle: str = "realistic"
+    # each Cron gets its own template (a per-Cron container command) instead of one shared by
+    # all: nothing in the caches is then shared across Crons' specs (scripts/bench_scale.py)
+    distinct_templates: bool = False
     # sample the first timed tick every 250 ms (BenchResult.tick_timeline; bench_configs rows)
     tick_timeline: bool = False
     # burst tokens deferrable (low-priority) writes may not spend (cmd/main.py --tick-burst-reserve)
@@ -514,8 +517,11 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
         tmpl = pytorchjob_template()
         crons = []
         for i in range(cfg.n_crons):
-            c = new_cron(f"cron-{i:05d}", cfg.namespace, "* * * * *", jsonutil.deepcopy(tmpl),
-                         history_limit=cfg.history_limit)
+            t = jsonutil.deepcopy(tmpl)
+            if cfg.distinct_templates:  # every Cron's template differs (its own container command)
+                for rs in t["spec"]["pytorchReplicaSpecs"].values():
+                    rs["template"]["spec"]["containers"][0]["command"] = ["python", "-c", f"print('tick {i}')"]
+            c = new_cron(f"cron-{i:05d}", cfg.namespace, "* * * * *", t, history_limit=cfg.history_limit)
             crons.append(await setup_client.create(CRON_GVR, c.to_dict(), cfg.namespace))
         # Seed each Cron with a full history (historyLimit finished jobs from the past hour) so
         # every timed tick exercises history GC, as in a long-running deployment.

@@ -356,7 +356,7 @@ PyObject* cached_value(const char* p, size_t n) {
 // identity: the reconciler's status write re-sends the same history-entry dicts on every
 // tick, so only the changed entries are encoded (a 10-entry status patch: 12 -> 1.3 us).
 
-enum Action : uint8_t { kActNone = 0, kActSkip = 1, kActMemo = 2 };
+enum Action : uint8_t { kActNone = 0, kActSkip = 1, kActMemo = 2, kActRaw = 3 };
 
 struct PlanNode {
   std::vector<std::pair<std::string, int>> kids;
@@ -971,7 +971,15 @@ struct Decoder {
   }
 
   // a value at a memo path: reuse the object remembered for exactly these bytes
-  PyObject* memo_value(int depth) {
+  // a value at a raw path: its JSON text, undecoded
+  PyObject* raw_value() {
+    ws();
+    const char* s = p;
+    if (!skip_value()) return nullptr;
+    return PyBytes_FromStringAndSize(s, static_cast<Py_ssize_t>(p - s));
+  }
+
+  PyObject* memo_value(int depth, int node) {
     ws();
     const char* s = p;
     if (!skip_value()) return nullptr;
@@ -984,7 +992,7 @@ struct Decoder {
     }
     const char* after = p;
     p = s;
-    PyObject* v = value(depth, -1);
+    PyObject* v = value(depth, node, true);  // plan paths below the memo path still apply
     if (!v) return nullptr;
     if (p != after) {  // cannot happen for well-formed input: keep the parse, do not remember it
       return v;
@@ -1000,12 +1008,16 @@ struct Decoder {
     return true;
   }
 
-  PyObject* value(int depth, int node = -1) {
+  PyObject* value(int depth, int node = -1, bool no_memo = false) {
     if (depth > kMaxDepth) {
       PyErr_SetString(PyExc_RecursionError, "JSON nested too deeply");
       return nullptr;
     }
-    if (node >= 0 && memo != nullptr && plan->act(node) == kActMemo) return memo_value(depth);
+    if (node >= 0) {
+      const Action a = plan->act(node);
+      if (a == kActMemo && memo != nullptr && !no_memo) return memo_value(depth, node);
+      if (a == kActRaw) return raw_value();
+    }
     ws();
     if (p >= end) return fail("Expecting value");
     switch (*p) {
@@ -1277,12 +1289,16 @@ struct Encoder {
     return false;
   }
 
-  bool value(PyObject* o, int depth, int node = -1) {
+  bool value(PyObject* o, int depth, int node = -1, bool no_memo = false) {
     if (depth > kMaxDepth) {
       PyErr_SetString(PyExc_ValueError, "Circular reference detected");
       return false;
     }
-    if (node >= 0 && plan->act(node) == kActMemo) {
+    if (node >= 0 && plan->act(node) == kActRaw && PyBytes_Check(o)) {  // raw JSON text, as decoded
+      out.append(PyBytes_AS_STRING(o), static_cast<size_t>(PyBytes_GET_SIZE(o)));
+      return true;
+    }
+    if (node >= 0 && !no_memo && plan->act(node) == kActMemo) {
       if (memo != nullptr) {
         const MemoSlot* b = memo->canonical_bytes(o);
         if (b != nullptr) {
@@ -1291,7 +1307,7 @@ struct Encoder {
         }
       }
       const size_t start = out.size();
-      if (!value(o, depth, -1)) return false;
+      if (!value(o, depth, node, true)) return false;  // plan paths below the memo path still apply
       recs.push_back(Rec{start, out.size(), o});
       return true;
     }
@@ -1901,11 +1917,13 @@ PyObject* codec_decode(CodecObject* c, PyObject* arg) {
 }
 
 PyObject* codec_new(PyTypeObject* type, PyObject* args, PyObject* kwds) {
-  static const char* kw[] = {"skip", "memo_paths", "memo", nullptr};
+  static const char* kw[] = {"skip", "memo_paths", "memo", "raw_paths", nullptr};
   PyObject* skip = nullptr;
   PyObject* memo_paths = nullptr;
   PyObject* memo = nullptr;
-  if (!PyArg_ParseTupleAndKeywords(args, kwds, "|OOO", const_cast<char**>(kw), &skip, &memo_paths, &memo))
+  PyObject* raw_paths = nullptr;
+  if (!PyArg_ParseTupleAndKeywords(args, kwds, "|OOOO", const_cast<char**>(kw), &skip, &memo_paths, &memo,
+                                   &raw_paths))
     return nullptr;
   if (memo == Py_None) memo = nullptr;
   if (memo != nullptr && !PyObject_TypeCheck(memo, &MemoType)) {
@@ -1927,7 +1945,7 @@ PyObject* codec_new(PyTypeObject* type, PyObject* args, PyObject* kwds) {
     Py_DECREF(seq);
     return true;
   };
-  if (!add_all(skip, kActSkip) || !add_all(memo_paths, kActMemo)) {
+  if (!add_all(skip, kActSkip) || !add_all(memo_paths, kActMemo) || !add_all(raw_paths, kActRaw)) {
     delete plan;
     return nullptr;
   }
@@ -2070,7 +2088,7 @@ PyMODINIT_FUNC PyInit__fastjson(void) {
   CodecType.tp_basicsize = sizeof(CodecObject);
   CodecType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_VECTORCALL;
   CodecType.tp_doc =
-      "Codec(skip=(), memo_paths=(), memo=None): JSON decode/encode with skipped and memoised paths; "
+      "Codec(skip=(), memo_paths=(), memo=None, raw_paths=()): JSON decode/encode with skipped, memoised and raw paths; "
       "calling it decodes one watch event line into (type, object)";
   CodecType.tp_new = codec_new_vc;
   CodecType.tp_dealloc = codec_dealloc;

@@ -226,20 +226,61 @@ def _drop(v: Any, path: Any) -> None:
         _drop(v[head], rest)
 
 
-class PyCodec:
-    """Python twin of the native ``Codec(skip, memo_paths, memo)``: ``loads`` decodes and
-    removes the skipped paths ("*" = any list element); memo paths change nothing but
-    speed, so they are ignored here.  Calling it decodes one watch event line into
-    ``(type, object)``."""
+def _rawify(v: Any, path: Any) -> None:
+    """Replace the value at ``path`` ("*" = any list element) by its JSON text (bytes)."""
+    head, rest = path[0], path[1:]
+    if head == "*":
+        if type(v) is list:
+            for i, x in enumerate(v):
+                if rest:
+                    _rawify(x, rest)
+                else:
+                    v[i] = dumpb(x)
+        return
+    if type(v) is not dict or head not in v:
+        return
+    if rest:
+        _rawify(v[head], rest)
+    else:
+        v[head] = dumpb(v[head])
 
-    def __init__(self, skip: Any = (), memo_paths: Any = (), memo: Any = None):
+
+def _unraw(v: Any, path: Any) -> None:
+    head, rest = path[0], path[1:]
+    if head == "*":
+        if type(v) is list:
+            for i, x in enumerate(v):
+                if rest:
+                    _unraw(x, rest)
+                elif isinstance(x, (bytes, bytearray)):
+                    v[i] = loads(x)
+        return
+    if type(v) is not dict or head not in v:
+        return
+    if rest:
+        _unraw(v[head], rest)
+    elif isinstance(v[head], (bytes, bytearray)):
+        v[head] = loads(v[head])
+
+
+class PyCodec:
+    """Python twin of the native ``Codec(skip, memo_paths, memo, raw_paths)``: ``loads``
+    decodes, removes the skipped paths ("*" = any list element) and turns the values at raw
+    paths into their JSON text (bytes; re-encoded compactly here, the input's own text
+    natively); memo paths change nothing but speed, so they are ignored here.  Calling it
+    decodes one watch event line into ``(type, object)``."""
+
+    def __init__(self, skip: Any = (), memo_paths: Any = (), memo: Any = None, raw_paths: Any = ()):
         self.skip = [tuple(p) for p in skip or ()]
+        self.raw = [tuple(p) for p in raw_paths or ()]
         self.memo = memo
 
     def loads(self, data: Any) -> Any:
         v = loads(data)
         for path in self.skip:
             _drop(v, path)
+        for path in self.raw:
+            _rawify(v, path)
         return v
 
     def __call__(self, line: Any) -> Any:
@@ -247,6 +288,10 @@ class PyCodec:
         return ev.get("type", "") or "", ev.get("object") or {}
 
     def dumpb(self, tree: Any) -> bytes:
+        if self.raw:  # raw values (bytes) go back as the JSON they hold
+            tree = deepcopy(tree)
+            for path in self.raw:
+                _unraw(tree, path)
         return dumpb(tree)
 
 

@@ -33,6 +33,8 @@ def main() -> int:
                     help="run a single shard in its own process too (its peak RSS is the operator's alone)")
     ap.add_argument("--lifecycle", choices=["realistic", "instant"], default="instant")
     ap.add_argument("--no-compact", action="store_true", help="A/B: ReconcilerOptions.compact_child_status=False")
+    ap.add_argument("--distinct-templates", action="store_true",
+                    help="every Cron its own template (a per-Cron container command), nothing shared across specs")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
 
@@ -47,7 +49,8 @@ def main() -> int:
             r = run_sync(BenchConfig(n_crons=n, steps=steps, warmup=a.warmup, mode=mode, transport=a.transport,
                                      shards=a.shards if a.transport == "http" else 1,
                                      operator_process=a.operator_process, lifecycle=a.lifecycle,
-                                     compact_children=not a.no_compact))
+                                     compact_children=not a.no_compact,
+                                     distinct_templates=a.distinct_templates))
             rows.append({"mode": mode, "n_crons": n, "steps": steps, "cron_reconciles_per_s": r.cron_reconciles_per_s,
                          "raw_reconciles_per_s": r.raw_reconciles_per_s, "p50_ms": r.p50_latency_ms,
                          "p99_ms": r.p99_latency_ms, "ms_per_step": r.ms_per_step,

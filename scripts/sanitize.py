@@ -132,7 +132,7 @@ def drive(scratch: str, iters: int) -> None:
     # plan-driven codecs: memo paths remembered by the encoder, reused by identity and by bytes
     # (a small table: growth, set overflow, LRU eviction and the object index's rebuilds all run)
     memo = fj.Memo(64, 512)
-    codec = fj.Codec(skip=[("s",)], memo_paths=[("h", "*"), ("m",)], memo=memo)
+    codec = fj.Codec(skip=[("s",)], memo_paths=[("h", "*"), ("m",)], memo=memo, raw_paths=[("m", "r"), ("r",)])
     for _ in range(iters // 8):
         hist = [_tree(rng) for _ in range(rng.randint(0, 4))]
         doc = {"h": hist, "m": _tree(rng), "s": _tree(rng), "x": "y" * rng.randint(0, 40) + "\n\"\\é"}
@@ -140,6 +140,8 @@ def drive(scratch: str, iters: int) -> None:
         assert codec.dumpb(doc) == fj.dumpb(doc)  # second time: memo values copied by identity
         back = codec.loads(codec.dumpb(doc))
         assert back["h"] == hist and "s" not in back
+        raw = codec.loads(fj.dumpb({"r": _tree(rng), "m": {"r": _tree(rng)}}))  # raw paths: the text as bytes
+        assert isinstance(raw["r"], bytes) and codec.dumpb(raw)
         for v in hist + [doc["m"], back["m"]]:  # forgotten values re-encode byte-exactly
             if rng.random() < 0.5:
                 memo.forget(v)

@@ -368,3 +368,25 @@ def test_memo_is_bounded_by_max_slots():
         enc.dumpb({"h": [{"uid": f"v{j}"} for j in range(i, i + 100)]})
     st = memo.stats()
     assert st["slots"] == 256 and st["used"] <= 256 and st["evictions"] > 0, st
+
+
+def test_codec_raw_paths_keep_the_exact_json_text_also_below_a_memo_path():
+    """raw paths: the value's own JSON text comes back as bytes (spacing and key order as sent),
+    also inside a memoised value; the encoder writes such bytes back verbatim."""
+    memo = m.Memo()
+    dec = m.Codec(memo_paths=[("object", "spec")], raw_paths=[("object", "spec", "template", "workload")],
+                  memo=memo)
+    wl = '{"kind": "PyTorchJob",  "spec": {"b": [1, 2], "a": {}}}'
+    line = ('{"type":"ADDED","object":{"metadata":{"name":"c"},"spec":{"schedule":"* * * * *",'
+            '"template":{"workload":' + wl + '}}}}').encode()
+    t, o = dec(line)
+    assert t == "ADDED" and o["spec"]["template"]["workload"] == wl.encode()
+    _, o2 = dec(line)
+    assert o2["spec"] is o["spec"]  # the memoised spec holds the raw text
+    enc = m.Codec(raw_paths=[("spec", "template", "workload")])
+    assert json.loads(enc.dumpb(o)) == {"metadata": {"name": "c"},
+                                        "spec": {"schedule": "* * * * *", "template": {"workload": json.loads(wl)}}}
+    # the Python twin: the same tree, its text re-encoded compactly
+    py = jsonutil.PyCodec(raw_paths=[("object", "spec", "template", "workload")])
+    _, p = py(line)
+    assert json.loads(p["spec"]["template"]["workload"]) == json.loads(wl)

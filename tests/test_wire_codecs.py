@@ -85,6 +85,9 @@ async def _run(opts: ReconcilerOptions):
 async def test_cron_events_carry_the_reconcilers_own_history_entries():
     rec, cached, stored, children = await _run(ReconcilerOptions())
     assert jsonutil.json_equal(cached["status"], stored["status"])  # exactly what a plain decode gives
+    # the template is cached as its JSON text; every job of the 4 ticks was built from it
+    wl = cached["spec"]["template"]["workload"]
+    assert isinstance(wl, bytes) and jsonutil.loads(wl) == stored["spec"]["template"]["workload"]
     key = f"{NS}/c"
     parsed = rec._parsed_status[key][1]
     hist = cached["status"]["history"]
@@ -106,6 +109,7 @@ async def test_reference_mode_decodes_plainly():
                                                                  slim_child_cache=False))
     assert rec.codecs is None
     assert jsonutil.json_equal(cached["status"], stored["status"])
+    assert cached["spec"]["template"]["workload"] == stored["spec"]["template"]["workload"]  # a dict
     assert children and all("spec" in c for c in children)
 
 
@@ -187,3 +191,14 @@ def test_compacting_codecs_never_build_the_child_metadata_the_cache_drops():
     assert set(WireCodecs(compact_metadata=True).child_list.loads(page)["items"][0]["metadata"]) == set(got["metadata"])
     _, full = WireCodecs().child_event(line)  # without the compact cache: all of it
     assert set(full["metadata"]) == set(meta)
+
+
+def test_a_fixed_name_template_kept_as_text_still_runs_as_forbid():
+    """A template with ``metadata.name`` (cron_controller.go:355-362: every run reuses that name,
+    so the ran-tick dedupe must not look for a generated one) is recognised whether the cached
+    template is a dict or its JSON text."""
+    from cron_operator_amd.controller.reconciler import _template_fixed_name
+
+    named = dict(PT_TMPL, metadata={"name": "fixed"})
+    assert _template_fixed_name(jsonutil.dumpb(named)) and not _template_fixed_name(jsonutil.dumpb(PT_TMPL))
+    assert _template_fixed_name(named) and not _template_fixed_name(b"not json")
