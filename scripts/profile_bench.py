@@ -88,6 +88,8 @@ def main() -> int:
     ap.add_argument("--top", type=int, default=45)
     ap.add_argument("--shards", type=int, default=1,
                     help="operator shard processes (then only the apiserver profile is meaningful)")
+    ap.add_argument("--lifecycle", default="instant", choices=["instant", "realistic"],
+                    help="the jobs' status sequence before each tick (the headline's: instant)")
     ap.add_argument("--out", required=True)
     ap.add_argument("--sampler", action="store_true",
                     help="statistical profile (SIGPROF every 0.5 ms of CPU) instead of cProfile: no per-call "
@@ -99,7 +101,7 @@ def main() -> int:
     api_prof = a.out + ".apiserver.pstats" if a.transport == "http" else ""
     shard_prof = a.out + ".shard" if a.shards > 1 else ""
     cfg = BenchConfig(n_crons=a.crons, steps=a.steps, warmup=a.warmup, transport=a.transport, mode=a.mode,
-                      apiserver_profile=api_prof, shards=a.shards, shard_profile=shard_prof)
+                      apiserver_profile=api_prof, shards=a.shards, shard_profile=shard_prof, lifecycle=a.lifecycle)
     prof = Sampler() if a.sampler else cProfile.Profile()
     t0, c0 = time.perf_counter(), time.process_time()
 
