@@ -8,7 +8,7 @@
 #   baseline all five BASELINE.json configs in both reconciler modes (scripts/baseline_configs.py)
 #   scale   cron-reconciles/s at 1 / 10 / 100 / 1000 Crons, both modes (scripts/bench_scale.py)
 #   scale10k  10000 Crons, this operator only: one process and 3 shards (peak RSS)
-#   mem10k  10000 Crons, the operator in its own process: peak RSS with / without the compact child cache
+#   mem10k  10000 Crons, the operator in its own process: peak RSS with a shared and with distinct templates
 #   ranks   the driver's multi-rank line (torch.distributed.run, N=2 and 4 CPU-only ranks): the
 #           N=8 scaling run is the driver's; RANKS overrides the list
 # Stops at the first failure; every GPU step has its own time limit.
@@ -73,13 +73,13 @@ for s in $STEPS; do
         --shards 3 --out "$OUT/scale10k_3shards.json" > "$OUT/scale10k_3shards.log" 2>&1
       check $? scale10k_3shards; tail -4 "$OUT/scale10k_3shards.log" ;;
     mem10k)
-      # peak RSS of the operator alone (its own process) at 10,000 Crons / 110,000 jobs, with
-      # the compact child cache (default) and without (A/B of ReconcilerOptions.compact_child_status)
-      for c in "" "--no-compact"; do
+      # peak RSS of the operator alone (its own process) at 10,000 Crons / 110,000 jobs over 10
+      # ticks: one template shared by every Cron, then a distinct template per Cron
+      for c in "" "--distinct-templates"; do
         step "mem10k $c"
-        timeout -k 10 900 python -u scripts/bench_scale.py --sizes 10000 --modes optimized --steps 3 --warmup 1 \
-          --operator-process $c --out "$OUT/mem10k${c:+_nocompact}.json" > "$OUT/mem10k${c:+_nocompact}.log" 2>&1
-        check $? "mem10k $c"; tail -3 "$OUT/mem10k${c:+_nocompact}.log"
+        timeout -k 10 600 python -u scripts/bench_scale.py --sizes 10000 --modes optimized --steps 10 --warmup 1 \
+          --operator-process $c --out "$OUT/mem10k${c:+_distinct}.json" > "$OUT/mem10k${c:+_distinct}.log" 2>&1
+        check $? "mem10k $c"; tail -3 "$OUT/mem10k${c:+_distinct}.log"
       done ;;
     ranks)
       for n in ${RANKS:-2 4}; do
