@@ -129,8 +129,12 @@ def budget_warnings(fires: int, qps: float, burst: int, requests_per_fire: float
                    f"more than --qps {qps:g}: ticks collapse and scheduled runs are lost; set qps >= "
                    f"{need:.0f} (helm: qps), or shard the fleet (sharding.count)")
     if fires > burst:
-        out.append(f"the busiest minute's {fires} CREATEs exceed --burst {burst}: the last lands about "
-                   f"{(fires - burst) / qps:.1f} s after the tick (raise burst to {fires} for all at once)")
+        # the tick's first `burst` CREATEs go out at once, the rest at qps (the tick reserve keeps
+        # the whole burst for them)
+        p50 = max(0.0, fires / 2 - burst) / qps
+        out.append(f"the busiest minute's {fires} CREATEs exceed --burst {burst}: the median lands about "
+                   f"{p50:.1f} s and the last about {(fires - burst) / qps:.1f} s after the tick (raise burst "
+                   f"to {fires} for all at once)")
     return out
 
 

@@ -169,3 +169,5 @@ def test_preflight_budget_math():
     assert len(budget_warnings(1000, 150, 300)) == 1   # within the QPS budget, beyond the burst
     assert budget_warnings(200, 150, 300) == []
     assert len(budget_warnings(2300, 150, 300)) == 2   # 2300 x 4 / 60 = 153 QPS > 150
+    # the median CREATE of 1000 due together: (500 - 300) / 150 = 1.3 s (the box measured 1.35 s)
+    assert "the median lands about 1.3 s and the last about 4.7 s" in budget_warnings(1000, 150, 300)[0]
