@@ -77,6 +77,8 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
                                             list_decoder=codecs.cron_list if codecs is not None else None)
     rec = CronReconciler(mgr.client, mgr.cache, mgr.get_event_recorder_for(CONTROLLER_NAME), mgr.clock, engine,
                          opts, cron_inf, codecs)
+    if codecs is not None:
+        mgr.add_debug_view("wire-memo", codecs.memo.stats)
     ctrl = Controller(CONTROLLER_NAME, rec, mgr.clock, mgr.opts.max_concurrent_reconciles, log)
     ctrl.set_log_constructor(log_constructor(log, "Cron"))
     assigner: Optional[sharding.ShardAssigner] = None

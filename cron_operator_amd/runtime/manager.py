@@ -14,8 +14,9 @@ Counterpart of ``ctrl.NewManager(cfg, ctrl.Options{...})`` + ``mgr.Start``
 from __future__ import annotations
 
 import asyncio
+import os
 from dataclasses import dataclass, field
-from typing import Awaitable, Callable, List, Optional
+from typing import Any, Awaitable, Callable, Dict, List, Optional
 
 from ..parallel.leaderelection import LeaderElector, in_cluster_namespace
 from ..utils import aio, gctune
@@ -90,6 +91,7 @@ class Manager:
         self.controllers: List[Controller] = []
         self.runnables: List[Callable[[], Awaitable[None]]] = []
         self.probes = ProbeServer(self.opts.health_probe_bind_address)
+        self.probes.debug["caches"] = self.cache_view
         self.metrics_server = MetricsServer(self.opts.metrics_bind_address, self.opts.secure_metrics,
                                             self.opts.metrics_cert_path, self.opts.metrics_cert_name,
                                             self.opts.metrics_cert_key, client=client,
@@ -123,6 +125,25 @@ class Manager:
 
     def add_readyz_check(self, name: str, check: Check = ping) -> None:
         self.probes.readyz[name] = check
+
+    def add_debug_view(self, name: str, fn: Callable[[], Any]) -> None:
+        """``GET /debug/<name>`` on the probe port answers ``fn()`` as JSON."""
+        self.probes.debug[name] = fn
+
+    def cache_view(self) -> Dict[str, Any]:
+        """``/debug/caches``: what each informer holds, and the process's resident memory."""
+        infs = []
+        for inf in self.cache.informers():
+            infs.append({"informer": inf.name, "objects": len(inf.store),
+                         "derived": len(inf.derived) if inf.derive is not None else None,
+                         "synced": inf.synced.is_set(), "relists": inf.relists, "events": inf.events})
+        rss = None
+        try:
+            with open("/proc/self/statm") as fh:
+                rss = round(int(fh.read().split()[1]) * os.sysconf("SC_PAGE_SIZE") / 2**20, 1)
+        except (OSError, ValueError, IndexError):
+            pass
+        return {"informers": infs, "rss_mib": rss}
 
     # -- lifecycle
     async def _start_leading(self) -> None:

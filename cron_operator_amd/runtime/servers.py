@@ -4,7 +4,9 @@
   registered checks like controller-runtime's ``healthz.Ping``
   (``cmd/operator/start.go:195-203``; probed on :8081 by the chart,
   ``charts/cron-operator/templates/deployment.yaml:74-83``).  The same port serves
-  ``/debug/traces`` (Chrome trace JSON of recent reconciles) when tracing is on.
+  ``/debug/traces`` (Chrome trace JSON of recent reconciles) when tracing is on, and
+  ``/debug/<name>`` views registered by the manager and the controller (``/debug/caches``: the
+  objects each informer holds and the process's memory; ``/debug/wire-memo``).
 * Metrics: ``/metrics`` in Prometheus text format.  ``--metrics-secure`` (default
   true, ``start.go:226``) serves HTTPS and guards the endpoint with the
   authn/authz filter: the bearer token is checked with a TokenReview and the
@@ -75,6 +77,8 @@ class ProbeServer:
         self.bind = bind
         self.healthz: Dict[str, Check] = {}
         self.readyz: Dict[str, Check] = {}
+        # /debug/<name>: JSON of what the callable returns (cache sizes, the wire memo, memory)
+        self.debug: Dict[str, Callable[[], Any]] = {}
         self._server: Optional[web.Server] = None
         self.port: Optional[int] = None
 
@@ -109,6 +113,14 @@ class ProbeServer:
             return web.json_response(t.chrome_trace())
 
         app.add_get("/debug/traces", traces)
+
+        async def debug(req: web.Request) -> web.Response:
+            fn = self.debug.get(req.match_info["name"])
+            if fn is None:
+                return web.Response(status=404, text=f"no such debug view; have: {', '.join(sorted(self.debug))}\n")
+            return web.json_response(fn())
+
+        app.add_get("/debug/{name}", debug)
         return app
 
     async def start(self) -> None:

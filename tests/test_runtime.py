@@ -424,6 +424,38 @@ async def test_probe_server():
         await p.stop()
 
 
+async def test_debug_views_report_caches_and_the_wire_memo():
+    """/debug/caches and /debug/wire-memo on the probe port: what each informer holds and the
+    process's memory, for sizing a deployment (docs/operations.md "Memory")."""
+    from cron_operator_amd.api.v1alpha1 import new_cron
+    from cron_operator_amd.controller.setup import setup_with_manager
+    from cron_operator_amd.runtime.manager import Manager, ManagerOptions
+
+    env = TestEnv()
+    await env.create_cron(new_cron("d", "default", "*/1 * * * *", {"apiVersion": "kubeflow.org/v1",
+                                                                   "kind": "PyTorchJob", "spec": {}}))
+    mgr = Manager(env.client, ManagerOptions(clock=env.clock, health_probe_bind_address="127.0.0.1:0",
+                                             metrics_bind_address="0"))
+    await setup_with_manager(mgr)
+    task = asyncio.get_running_loop().create_task(mgr.start())
+    try:
+        await asyncio.wait_for(mgr.started.wait(), 20)
+        async with aiohttp.ClientSession() as s:
+            async with s.get(f"http://127.0.0.1:{mgr.probes.port}/debug/caches") as r:
+                assert r.status == 200
+                view = await r.json()
+            assert view["rss_mib"] > 0
+            crons = [i for i in view["informers"] if i["informer"].startswith("crons")]
+            assert crons and crons[0]["objects"] == 1 and crons[0]["synced"]
+            async with s.get(f"http://127.0.0.1:{mgr.probes.port}/debug/wire-memo") as r:
+                assert r.status == 200 and "slots" in await r.json()
+            async with s.get(f"http://127.0.0.1:{mgr.probes.port}/debug/nope") as r:
+                assert r.status == 404 and "caches" in await r.text()
+    finally:
+        mgr.stop()
+        await asyncio.wait({task}, timeout=10)
+
+
 async def test_metrics_server_insecure_and_secure():
     env = TestEnv()
     env.server.tokens = {"good": {"username": "system:serviceaccount:x:prom", "groups": []}}
