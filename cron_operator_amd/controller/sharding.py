@@ -158,8 +158,10 @@ class ShardAssigner:
             return inf
         sel = f"{LABEL_CRON_NAME},{unassigned_selector(self.count)}" if child else unassigned_selector(self.count)
         event, page = _metadata_codecs()
+        # only this shard's share is stored: the other shards' objects are dropped as they arrive
+        # (on a first start every shard LISTs the whole unassigned fleet)
         inf = await cache.get_informer(gvk, label_selector=sel, transform=metadata_only, decoder=event,
-                                       list_decoder=page)
+                                       list_decoder=page, keep=lambda o: self.owns(o, child))
         self.informers[gvk] = inf
         if child:
             self._child_kinds.add(gvk)

@@ -110,8 +110,14 @@ class Informer:
                  page_size: int = 500, name: str = "", resync_period: float = 0.0,
                  clock: Optional[Clock] = None, transform: Optional[Transform] = None,
                  min_watch_timeout: float = MIN_WATCH_TIMEOUT, watch_idle_timeout: float = WATCH_IDLE_TIMEOUT,
-                 decoder: Any = None, list_decoder: Any = None):
+                 decoder: Any = None, list_decoder: Any = None,
+                 keep: Optional[Callable[[Dict[str, Any]], bool]] = None):
         self.client = client
+        # ``keep`` (after ``transform``): objects it rejects are not stored -- an object that
+        # stops passing it leaves the store as a deletion.  A filter the apiserver cannot apply
+        # (a hash of name and labels: one shard's share of an unassigned fleet), applied as each
+        # LIST page and watch event arrives, so the rest is never held
+        self.keep = keep
         # watch-event decoder for byte transports (a jsonutil.Codec): it may skip subtrees no
         # consumer reads and reuse memoised ones; None decodes plainly.  ``list_decoder`` does
         # the same for LIST pages (paths under ``items/*``): the initial LIST then shares what
@@ -267,6 +273,8 @@ class Informer:
         if self.transform is not None and not self._pretransformed:
             obj = self.transform(obj)
         self.events += 1
+        if self.keep is not None and etype != "DELETED" and not self.keep(obj):
+            etype = "DELETED"
         na = self._napply
         if na is not None:
             # key, store write/delete, derived-memo drop and index upkeep in one native call
@@ -374,6 +382,8 @@ class Informer:
                 items = [tf(o) for o in page.get("items") or []] if self.derive is None else \
                     [self._transform_derive(tf, o) for o in page.get("items") or []]
                 page["items"] = items
+            if self.keep is not None:
+                page["items"] = [o for o in page.get("items") or [] if self.keep(o)]
             if out is None:
                 out = page
             else:
@@ -597,9 +607,10 @@ class Cache:
     async def get_informer(self, target: Any, label_selector: Optional[str] = None,
                            indexers: Optional[Dict[str, IndexFunc]] = None,
                            transform: Optional[Transform] = None, decoder: Any = None,
-                           list_decoder: Any = None) -> Informer:
+                           list_decoder: Any = None,
+                           keep: Optional[Callable[[Dict[str, Any]], bool]] = None) -> Informer:
         """The shared informer for ``(target, namespace, selector)``.  ``transform`` and
-        ``decoder`` apply when this call creates it (like ``cache.Options.ByObject[...].Transform``)."""
+        ``decoder`` (and ``keep``) apply when this call creates it (like ``cache.Options.ByObject[...].Transform``)."""
         gvr = await self._resolve(target)
         key = (gvr, self.namespace, label_selector)
         inf = self._informers.get(key)
@@ -608,7 +619,7 @@ class Cache:
                            name=f"{gvr.resource}.{gvr.group}" if gvr.group else gvr.resource,
                            resync_period=self.resync_period, clock=self.clock, transform=transform,
                            min_watch_timeout=self.min_watch_timeout, watch_idle_timeout=self.watch_idle_timeout,
-                           decoder=decoder, list_decoder=list_decoder)
+                           decoder=decoder, list_decoder=list_decoder, keep=keep)
             self._informers[key] = inf
             if self._started:
                 inf.start()

@@ -423,9 +423,10 @@ async def test_memos_dropped_when_crons_and_children_go_away():
 
 
 async def test_shard_assignment_watches_cache_metadata_only():
-    """Before assignment the "unassigned" watch sees the whole fleet: it keeps names, labels,
-    uid and resourceVersion only, so a shard's memory follows its own share."""
-    from cron_operator_amd.controller.sharding import ShardAssigner
+    """Before assignment the "unassigned" watch sees the whole fleet: it stores only this
+    shard's share, and of that only names, labels, uid and resourceVersion, so a shard's
+    memory follows its own share."""
+    from cron_operator_amd.controller.sharding import ShardAssigner, shard_of
 
     env = TestEnv()
     for i in range(6):
@@ -442,7 +443,10 @@ async def test_shard_assignment_watches_cache_metadata_only():
     jobs = await asg.watch(cache, GroupVersionKind("kubeflow.org", "v1", "PyTorchJob"), child=True)
     cache.start()
     assert await cache.wait_for_sync(10)
-    assert len(crons.store) == 6 and len(jobs.store) == 1
+    mine = {f"{NS}/u{i}" for i in range(6) if shard_of(NS, f"u{i}", 2) == 0}
+    assert 0 < len(mine) < 6  # the names split over both shards
+    assert set(crons.store) == mine
+    assert len(jobs.store) == (f"{NS}/u0" in mine)  # a child follows its Cron's shard
     for o in list(crons.store.values()) + list(jobs.store.values()):
         assert set(o) == {"apiVersion", "kind", "metadata"}
         assert set(o["metadata"]) <= {"name", "namespace", "uid", "resourceVersion", "labels"}

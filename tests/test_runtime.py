@@ -739,6 +739,43 @@ async def test_informer_transforms_list_pages_once():
     await inf.stop()
 
 
+async def test_informer_keep_filter_stores_only_what_passes_it():
+    """``keep`` (the shard assigner's share of an unassigned fleet): rejected LIST items and
+    events are never stored, and an object that stops passing it leaves as a deletion."""
+    env = TestEnv()
+    s = env.server
+    for i in range(12):
+        s.create(CM, "default", {"apiVersion": "v1", "kind": "ConfigMap",
+                                 "metadata": {"name": f"c{i}", "labels": {"mine": str(i % 3 == 0).lower()}}})
+    gone: list = []
+    inf = Informer(env.new_client(), CM, "default", page_size=5,
+                   keep=lambda o: o["metadata"].get("labels", {}).get("mine") == "true")
+    inf.add_handler(EventHandler(on_delete=lambda o: gone.append(o["metadata"]["name"])))
+    inf.start()
+    await asyncio.wait_for(inf.synced.wait(), 5)
+    assert set(inf.store) == {f"default/c{i}" for i in (0, 3, 6, 9)}
+
+    async def until(pred):
+        for _ in range(500):
+            if pred():
+                return
+            await asyncio.sleep(0.002)
+        raise AssertionError("timed out")
+
+    s.patch(CM, "default", "c1", {"metadata": {"labels": {"mine": "true"}}}, "merge")  # now passes
+    await until(lambda: "default/c1" in inf.store)
+    s.patch(CM, "default", "c0", {"metadata": {"labels": {"mine": "false"}}}, "merge")  # stops passing
+    await until(lambda: "default/c0" not in inf.store)
+    assert gone == ["c0"]
+    s.create(CM, "default", {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "x"}})
+    s.delete(CM, "default", "c2")  # never stored: no delete to deliver
+    s.patch(CM, "default", "c3", {"metadata": {"labels": {"other": "y"}}}, "merge")  # a barrier
+    await until(lambda: "other" in inf.store["default/c3"]["metadata"]["labels"])
+    assert "default/x" not in inf.store and gone == ["c0"]
+    assert set(inf.store) == {f"default/c{i}" for i in (1, 3, 6, 9)}
+    await inf.stop()
+
+
 def test_free_port_is_free_and_below_the_ephemeral_range():
     import socket
 
