@@ -8,6 +8,7 @@
 #   baseline all five BASELINE.json configs in both reconciler modes (scripts/baseline_configs.py)
 #   scale   cron-reconciles/s at 1 / 10 / 100 / 1000 Crons, both modes (scripts/bench_scale.py)
 #   scale10k  10000 Crons, this operator only: one process and 3 shards (peak RSS)
+#   shards10k  10000 Crons, 3 label-routed shard processes on a first start (peak RSS per shard)
 #   mem10k  10000 Crons, the operator in its own process: peak RSS with a shared and with distinct templates
 #   ranks   the driver's multi-rank line (torch.distributed.run, N=2 and 4 CPU-only ranks): the
 #           N=8 scaling run is the driver's; RANKS overrides the list
@@ -72,6 +73,11 @@ for s in $STEPS; do
       timeout -k 10 900 python -u scripts/bench_scale.py --sizes 10000 --modes optimized --steps 3 --warmup 1 \
         --shards 3 --out "$OUT/scale10k_3shards.json" > "$OUT/scale10k_3shards.log" 2>&1
       check $? scale10k_3shards; tail -4 "$OUT/scale10k_3shards.log" ;;
+    shards10k)
+      step shards10k
+      timeout -k 10 900 python -u scripts/bench_scale.py --sizes 10000 --modes optimized --steps 5 --warmup 1 \
+        --shards 3 --out "$OUT/shards10k.json" > "$OUT/shards10k.log" 2>&1
+      check $? shards10k; tail -4 "$OUT/shards10k.log" ;;
     mem10k)
       # peak RSS of the operator alone (its own process) at 10,000 Crons / 110,000 jobs over 10
       # ticks: one template shared by every Cron, then a distinct template per Cron
