@@ -598,6 +598,8 @@ class CronReconciler(Reconciler):
         # the child informers' selector, and labels stamped on every child (label-routed sharding)
         self.child_selector = LABEL_CRON_NAME
         self.child_labels: Dict[str, str] = {}
+        # hash-routed sharding: the child informers store only this shard's Crons' jobs
+        self.child_keep: Optional[Callable[[Dict[str, Any]], bool]] = None
         self.shard_assigner: Any = None  # controller.sharding.ShardAssigner with label routing
         # key -> resourceVersion of the Cron object produced by our last status write
         self.own_writes: Dict[str, Tuple[Any, Dict[str, Any]]] = {}  # key -> (generation, status we wrote)
@@ -1088,7 +1090,8 @@ class CronReconciler(Reconciler):
                                                 indexers={CHILD_INDEX: label_index(LABEL_CRON_NAME)},
                                                 transform=self.child_transform(gvk),
                                                 decoder=self.codecs.child_event if self.codecs else None,
-                                                list_decoder=self.codecs.child_list if self.codecs else None)
+                                                list_decoder=self.codecs.child_list if self.codecs else None,
+                                                keep=self.child_keep)
             self.child_informers[gvk] = inf
             self.ensure_derive(inf, gvk)
             inf.start()

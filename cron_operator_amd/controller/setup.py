@@ -69,12 +69,14 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
     if mgr.opts.shard_routing not in sharding.ROUTINGS:
         raise ValueError(f"unknown shard routing {mgr.opts.shard_routing!r}")
     by_label = count > 1 and mgr.opts.shard_routing == "labels"
+    by_hash = count > 1 and not by_label
     codecs = WireCodecs(opts.slim_child_cache, compact_metadata=opts.compact_metadata()) if opts.wire_codecs else None
     cron_inf = await mgr.cache.get_informer(CRON_GVK,
                                             label_selector=sharding.shard_selector(index, count) if by_label else None,
                                             transform=strip_managed_fields if opts.slim_child_cache else None,
                                             decoder=codecs.cron_event if codecs is not None else None,
-                                            list_decoder=codecs.cron_list if codecs is not None else None)
+                                            list_decoder=codecs.cron_list if codecs is not None else None,
+                                            keep=sharding.hash_keep(index, count, False) if by_hash else None)
     rec = CronReconciler(mgr.client, mgr.cache, mgr.get_event_recorder_for(CONTROLLER_NAME), mgr.clock, engine,
                          opts, cron_inf, codecs)
     if codecs is not None:
@@ -84,6 +86,8 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
     assigner: Optional[sharding.ShardAssigner] = None
     if count > 1:
         ctrl.set_shard(index, count)  # with label routing too: a mislabelled object is never reconciled twice
+    if by_hash:
+        rec.child_keep = sharding.hash_keep(index, count, True)
     if by_label:
         rec.child_selector = sharding.child_selector(index, count)
         rec.child_labels = {sharding.LABEL_SHARD: sharding.shard_label_value(index, count)}
@@ -171,11 +175,13 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
                                                    indexers={CHILD_INDEX: label_index(LABEL_CRON_NAME)},
                                                    transform=rec.child_transform(gvk),
                                                    decoder=codecs.child_event if codecs is not None else None,
-                                                   list_decoder=codecs.child_list if codecs is not None else None)
+                                                   list_decoder=codecs.child_list if codecs is not None else None,
+                                                   keep=rec.child_keep)
                 rec.child_informers[gvk] = inf
                 rec.ensure_derive(inf, gvk)
             else:
-                inf = await mgr.cache.get_informer(gvk, label_selector=rec.child_selector if by_label else None)
+                inf = await mgr.cache.get_informer(gvk, label_selector=rec.child_selector if by_label else None,
+                                                   keep=rec.child_keep)
             if assigner is not None:
                 await assigner.watch(mgr.cache, gvk, child=True)
         except errors.ApiError as e:

@@ -4,9 +4,10 @@ The reference runs one leader-elected replica; this operator can 
 its Crons across ``--shard-count`` replicas.  Two routings exist:
 
 ``hash`` (:func:`cron_operator_amd.runtime.controller.shard_of`)
-    every shard's informers hold *all* Crons and children, and the event handler
-    drops the keys of other shards.  Nothing is written to user objects, but N
-    shards decode and cache N times the watch traffic.
+    every shard watches *all* Crons and children, stores only its own share
+    (:func:`hash_keep`, an informer ``keep`` filter), and its event handler drops
+    the keys of other shards.  Nothing is written to user objects, but N shards
+    decode N times the watch traffic.
 ``labels`` (default; this module)
     every Cron and child carries ``kubedl.io/shard=<index>-of-<count>`` and shard
     *i*'s informers select on its own value, so the apiserver sends each event to
@@ -67,6 +68,21 @@ def shard_selector(index: int, count: int) -> str:
 def child_selector(index: int, count: int) -> str:
     """Selector of the children shard ``index`` owns."""
     return f"{LABEL_CRON_NAME},{shard_selector(index, count)}"
+
+
+def hash_keep(index: int, count: int, child: bool) -> Callable[[Dict[str, Any]], bool]:
+    """Informer ``keep`` filter of hash routing: the Crons (children: the jobs of the Crons) that
+    hash to shard ``index``.  A child without a cron-name label is kept, as without sharding."""
+    def keep(obj: Dict[str, Any]) -> bool:
+        m = obj.get("metadata") or {}
+        if child:
+            cron = (m.get("labels") or {}).get(LABEL_CRON_NAME)
+            if cron is None:
+                return True
+        else:
+            cron = m.get("name", "")
+        return shard_of(m.get("namespace", ""), cron, count) == index
+    return keep
 
 
 def unassigned_selector(count: int) -> str:

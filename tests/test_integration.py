@@ -256,7 +256,8 @@ async def test_manager_leader_election_single_active():
 async def test_horizontal_sharding_splits_crons_and_leases(routing):
     """Two replicas with --shard-count 2: every Cron fires exactly once per tick, each shard only
     reconciles its own Crons, and each shard elects its own leader Lease.  With label routing
-    each shard also caches only its own Crons and children, all labelled with their shard."""
+    each shard also caches only its own Crons and children, all labelled with their shard; with
+    hash routing it stores only its own share of what it watches."""
     from cron_operator_amd.api.meta import GroupVersionResource as GVR
     from cron_operator_amd.controller.setup import setup_with_manager
     from cron_operator_amd.runtime.controller import shard_of
@@ -302,14 +303,14 @@ async def test_horizontal_sharding_splits_crons_and_leases(routing):
     assert seen[0] <= owners[0] and seen[1] <= owners[1]
     leases = {o["metadata"]["name"] for o in env.server.list(GVR("coordination.k8s.io", "v1", "leases"), NS)["items"]}
     assert {"619a52b8.kubedl.io-shard-0", "619a52b8.kubedl.io-shard-1"} <= leases
+    for idx, c in enumerate(ctrls):
+        rec = c.reconciler
+        assert {o["metadata"]["name"] for o in rec.cron_informer.store.values()} == owners[idx]
+        assert {o["metadata"]["labels"][LABEL_CRON_NAME]
+                for inf in rec.child_informers.values() for o in inf.store.values()} == owners[idx]
     if routing == "labels":
         from cron_operator_amd.controller.sharding import LABEL_SHARD
 
-        for idx, c in enumerate(ctrls):
-            rec = c.reconciler
-            assert {o["metadata"]["name"] for o in rec.cron_informer.store.values()} == owners[idx]
-            for inf in rec.child_informers.values():
-                assert {o["metadata"]["labels"][LABEL_CRON_NAME] for o in inf.store.values()} <= owners[idx]
         for o in env.server.list(CRON_GVR, NS)["items"]:
             assert o["metadata"]["labels"][LABEL_SHARD] == f"{shard_of(NS, o['metadata']['name'], 2)}-of-2"
         for o in env.server.list(PT, NS)["items"]:
