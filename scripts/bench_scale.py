@@ -29,6 +29,8 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--transport", default="http")
     ap.add_argument("--shards", type=int, default=1, help="operator shard processes")
+    ap.add_argument("--shard-routing", choices=["labels", "hash"], default="labels",
+                    help="how the shards split the watch traffic (controller/sharding.py)")
     ap.add_argument("--operator-process", action="store_true",
                     help="run a single shard in its own process too (its peak RSS is the operator's alone)")
     ap.add_argument("--lifecycle", choices=["realistic", "instant"], default="instant")
@@ -48,10 +50,12 @@ def main() -> int:
             steps = max(a.steps, min(30, -(-30 // n)))
             r = run_sync(BenchConfig(n_crons=n, steps=steps, warmup=a.warmup, mode=mode, transport=a.transport,
                                      shards=a.shards if a.transport == "http" else 1,
+                                     shard_routing=a.shard_routing,
                                      operator_process=a.operator_process, lifecycle=a.lifecycle,
                                      compact_children=not a.no_compact,
                                      distinct_templates=a.distinct_templates))
-            rows.append({"mode": mode, "n_crons": n, "steps": steps, "cron_reconciles_per_s": r.cron_reconciles_per_s,
+            rows.append({"mode": mode, "n_crons": n, "steps": steps, "shards": a.shards,
+                         "shard_routing": a.shard_routing, "cron_reconciles_per_s": r.cron_reconciles_per_s,
                          "raw_reconciles_per_s": r.raw_reconciles_per_s, "p50_ms": r.p50_latency_ms,
                          "p99_ms": r.p99_latency_ms, "ms_per_step": r.ms_per_step,
                          "api_requests_per_fire": r.api_requests_per_fire,

@@ -9,6 +9,7 @@
 #   scale   cron-reconciles/s at 1 / 10 / 100 / 1000 Crons, both modes (scripts/bench_scale.py)
 #   scale10k  10000 Crons, this operator only: one process and 3 shards (peak RSS)
 #   shards10k  10000 Crons, 3 label-routed shard processes on a first start (peak RSS per shard)
+#   routing label vs hash routing on 3 shards, REPS alternating pairs at ROUTING_SIZES Crons (default 3000)
 #   mem10k  10000 Crons, the operator in its own process: peak RSS with a shared and with distinct templates
 #   ranks   the driver's multi-rank line (torch.distributed.run, N=2 and 4 CPU-only ranks): the
 #           N=8 scaling run is the driver's; RANKS overrides the list
@@ -78,6 +79,17 @@ for s in $STEPS; do
       timeout -k 10 900 python -u scripts/bench_scale.py --sizes 10000 --modes optimized --steps 5 --warmup 1 \
         --shards 3 --out "$OUT/shards10k.json" > "$OUT/shards10k.log" 2>&1
       check $? shards10k; tail -4 "$OUT/shards10k.log" ;;
+    routing)
+      # alternating pairs (REPS of them): the box's run-to-run spread is larger than one pair shows
+      for i in $(seq 1 "${REPS:-1}"); do
+        for r in labels hash; do
+          step "routing $r $i"
+          timeout -k 10 900 python -u scripts/bench_scale.py --sizes "${ROUTING_SIZES:-3000}" --modes optimized \
+            --steps 5 --warmup 1 --shards 3 --shard-routing $r --out "$OUT/routing_${r}_$i.json" \
+            > "$OUT/routing_${r}_$i.log" 2>&1
+          check $? "routing $r"; grep "n=" "$OUT/routing_${r}_$i.log"
+        done
+      done ;;
     mem10k)
       # peak RSS of the operator alone (its own process) at 10,000 Crons / 110,000 jobs over 10
       # ticks: one template shared by every Cron, then a distinct template per Cron
