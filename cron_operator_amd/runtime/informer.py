@@ -29,6 +29,7 @@ from __future__ import annotations
 
 import asyncio
 import random
+from functools import partial
 from typing import Any, Callable, Dict, Iterable, List, Optional, Set, Tuple
 
 from ..api import errors
@@ -361,10 +362,13 @@ class Informer:
             self._apply("DELETED", self.store[key])
 
     # ------------------------------------------------------------------ reflector
-    def _transform_derive(self, tf: Transform, obj: Dict[str, Any]) -> Dict[str, Any]:
+    def _transform_derive(self, tf: Transform, obj: Dict[str, Any]) -> Optional[Dict[str, Any]]:
         """A LIST item transformed and derived at once, as a watch event is: a transform may hand
-        the derive function what only the untransformed object had (``compact_child``)."""
+        the derive function what only the untransformed object had (``compact_child``).  None for
+        an item ``keep`` rejects (never derived)."""
         out = tf(obj)
+        if self.keep is not None and not self.keep(out):
+            return None
         self._prederived[id(out)] = self.derive(out)  # type: ignore[misc]
         return out
 
@@ -378,12 +382,15 @@ class Informer:
         while True:
             page = await self.client.list(self.target, self.namespace, self.label_selector,
                                           limit=self.page_size, continue_=cont, decoder=self.list_decoder)
-            if tf is not None:
-                items = [tf(o) for o in page.get("items") or []] if self.derive is None else \
-                    [self._transform_derive(tf, o) for o in page.get("items") or []]
-                page["items"] = items
-            if self.keep is not None:
-                page["items"] = [o for o in page.get("items") or [] if self.keep(o)]
+            keep = self.keep
+            if tf is not None and self.derive is not None:
+                page["items"] = [o for o in map(partial(self._transform_derive, tf), page.get("items") or [])
+                                 if o is not None]
+            elif tf is not None:
+                page["items"] = [tf(o) for o in page.get("items") or []] if keep is None else \
+                    [o for o in map(tf, page.get("items") or []) if keep(o)]
+            elif keep is not None:
+                page["items"] = [o for o in page.get("items") or [] if keep(o)]
             if out is None:
                 out = page
             else:
