@@ -41,8 +41,8 @@ def objects(draw):
     return {"metadata": m, "v": draw(st.integers(0, 3))}
 
 
-def _informer(native: bool, log):
-    inf = Informer(None, "things", indexers={"cron": label_index(LABEL)})
+def _informer(native: bool, log, keep=None):
+    inf = Informer(None, "things", indexers={"cron": label_index(LABEL)}, keep=keep)
     if not native:
         inf._napply = None
     else:
@@ -68,11 +68,17 @@ def _state(inf):
             {n: {v: set(s) for v, s in idx.items()} for n, idx in inf.indices.items()}, inf.events)
 
 
+def _keep_odd(o):
+    """An informer ``keep`` filter (a shard's share): objects whose ``v`` is odd."""
+    return o.get("v", 0) % 2 == 1
+
+
+@pytest.mark.parametrize("keep", [None, _keep_odd], ids=["all", "keep-filter"])
 @settings(max_examples=300, deadline=None)
-@given(st.lists(st.tuples(st.sampled_from(["ADDED", "MODIFIED", "DELETED"]), objects()), max_size=40))
-def test_native_bookkeeping_matches_python(events):
+@given(events=st.lists(st.tuples(st.sampled_from(["ADDED", "MODIFIED", "DELETED"]), objects()), max_size=40))
+def test_native_bookkeeping_matches_python(keep, events):
     la, lb = [], []
-    a, b = _informer(True, la), _informer(False, lb)
+    a, b = _informer(True, la, keep), _informer(False, lb, keep)
     for etype, obj in events:
         # each informer gets its own copy (transforms and stores may keep the object)
         ea = _apply(a, etype, jsonutil.deepcopy(obj))
@@ -83,6 +89,8 @@ def test_native_bookkeeping_matches_python(events):
     assert all(jsonutil.json_equal(sa[0][k], sb[0][k]) for k in sa[0])
     assert sa[1] == sb[1] and sa[2] == sb[2] and sa[3] == sb[3]
     assert [e[0] for e in la] == [e[0] for e in lb]
+    if keep is not None:
+        assert all(keep(o) for o in sa[0].values())  # a rejected version never stays stored
 
 
 def test_native_path_is_taken_for_regular_objects_and_keeps_identity():
