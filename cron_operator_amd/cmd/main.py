@@ -164,6 +164,8 @@ def build_parser() -> argparse.ArgumentParser:
     st.add_argument("--trace-file", default="", help="Also append finished spans here as JSON lines "
                                                      "(implies --enable-tracing).")
     st.add_argument("--trace-sample-rate", type=float, default=1.0, help="Fraction of reconciles traced.")
+    _add_bool(st, "--enable-profiling", False, "Serve a CPU profile of the event loop at "
+                                              "/debug/profile?seconds=N on the probe port.")
 
     fa = sub.add_parser("fake-apiserver", help="Serve the in-process fake Kubernetes API server over HTTP")
     fa.add_argument("--bind-address", default="127.0.0.1")
@@ -228,6 +230,10 @@ async def run_start(a: argparse.Namespace) -> int:
     from ..utils.logging import get_logger
 
     log = get_logger("setup")
+    if a.enable_profiling:
+        from ..runtime import profiler
+
+        profiler.allow()
     if a.enable_tracing or a.trace_file:
         from ..runtime import tracing
 

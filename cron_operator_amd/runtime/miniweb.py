@@ -22,8 +22,8 @@ MAX_BODY = 1 << 20    # a GET with a body is read and ignored up to this size
 IDLE_TIMEOUT = 75.0   # a keep-alive connection with no request in flight is closed after this
 REQUEST_TIMEOUT = 30.0  # a request must be complete (head and body) this long after its first byte
 _REASONS = {200: "OK", 400: "Bad Request", 401: "Unauthorized", 403: "Forbidden", 404: "Not Found",
-            405: "Method Not Allowed", 413: "Payload Too Large", 431: "Request Header Fields Too Large",
-            500: "Internal Server Error", 503: "Service Unavailable"}
+            405: "Method Not Allowed", 409: "Conflict", 413: "Payload Too Large",
+            431: "Request Header Fields Too Large", 500: "Internal Server Error", 503: "Service Unavailable"}
 
 
 class Request:

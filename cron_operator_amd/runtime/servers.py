@@ -6,7 +6,9 @@
   ``charts/cron-operator/templates/deployment.yaml:74-83``).  The same port serves
   ``/debug/traces`` (Chrome trace JSON of recent reconciles) when tracing is on, and
   ``/debug/<name>`` views registered by the manager and the controller (``/debug/caches``: the
-  objects each informer holds and the process's memory; ``/debug/wire-memo``).
+  objects each informer holds and the process's memory; ``/debug/wire-memo``), ``/debug/tasks``
+  (live asyncio tasks by where they wait) and, with ``--enable-profiling``, ``/debug/profile``
+  (a CPU profile of the loop thread; :mod:`.profiler`).
 * Metrics: ``/metrics`` in Prometheus text format.  ``--metrics-secure`` (default
   true, ``start.go:226``) serves HTTPS and guards the endpoint with the
   authn/authz filter: the bearer token is checked with a TokenReview and the
@@ -113,6 +115,28 @@ class ProbeServer:
             return web.json_response(t.chrome_trace())
 
         app.add_get("/debug/traces", traces)
+
+        async def tasks(req: web.Request) -> web.Response:
+            from . import profiler
+
+            return web.json_response(profiler.task_dump(stacks=req.query.get("stacks") in ("1", "true")))
+
+        async def profile(req: web.Request) -> web.Response:
+            from . import profiler
+
+            if not profiler.allowed():
+                return web.Response(status=404, text="profiling disabled (start with --enable-profiling)\n")
+            try:
+                seconds = float(req.query.get("seconds", "10"))
+            except ValueError:
+                return web.Response(status=400, text="seconds: a number\n")
+            try:
+                return web.Response(text=await profiler.cpu_profile(seconds))
+            except RuntimeError as e:
+                return web.Response(status=409, text=f"{e}\n")
+
+        app.add_get("/debug/tasks", tasks)
+        app.add_get("/debug/profile", profile)
 
         async def debug(req: web.Request) -> web.Response:
             fn = self.debug.get(req.match_info["name"])

@@ -456,6 +456,58 @@ async def test_debug_views_report_caches_and_the_wire_memo():
         await asyncio.wait({task}, timeout=10)
 
 
+async def _parked_here(ev: asyncio.Event) -> None:
+    await ev.wait()
+
+
+async def test_debug_tasks_and_the_opt_in_cpu_profile():
+    """/debug/tasks groups live tasks by where they wait (a goroutine dump's analogue);
+    /debug/profile is served only with --enable-profiling, one profile at a time."""
+    from cron_operator_amd.runtime import profiler
+
+    probes = ProbeServer("127.0.0.1:0")
+    await probes.start()
+    ev = asyncio.Event()
+    parked = [asyncio.get_running_loop().create_task(_parked_here(ev)) for _ in range(7)]
+    stop = False
+
+    async def busy() -> None:
+        while not stop:
+            sum(i * i for i in range(2000))
+            await asyncio.sleep(0)
+
+    spin = asyncio.get_running_loop().create_task(busy())
+    base = f"http://127.0.0.1:{probes.port}"
+    try:
+        async with aiohttp.ClientSession() as s:
+            async with s.get(base + "/debug/tasks?stacks=1") as r:
+                view = await r.json()
+            here = [g for g in view["by_location"] if "(_parked_here)" in g["where"]]
+            assert here and here[0]["tasks"] == 7 and view["tasks"] >= 9
+            assert "tests/test_runtime.py" in here[0]["where"] and "locks.py" in here[0]["await_chain"][-1]
+            async with s.get(base + "/debug/profile?seconds=0.3") as r:
+                assert r.status == 404 and "--enable-profiling" in await r.text()
+            profiler.allow()
+            try:
+                first = asyncio.ensure_future(s.get(base + "/debug/profile?seconds=0.5"))
+                await asyncio.sleep(0.1)
+                async with s.get(base + "/debug/profile?seconds=0.2") as r:
+                    assert r.status == 409  # one at a time
+                async with await first as r:
+                    assert r.status == 200
+                    text = await r.text()
+                assert "samples over" in text and "## by self samples" in text and "(busy)" in text
+                async with s.get(base + "/debug/profile?seconds=x") as r:
+                    assert r.status == 400
+            finally:
+                profiler.allow(False)
+    finally:
+        stop = True
+        ev.set()
+        await asyncio.gather(spin, *parked)
+        await probes.stop()
+
+
 async def test_metrics_server_insecure_and_secure():
     env = TestEnv()
     env.server.tokens = {"good": {"username": "system:serviceaccount:x:prom", "groups": []}}
