@@ -235,3 +235,81 @@ async def test_label_routed_shards_converge_under_faults():
     for t in tasks:
         await asyncio.wait_for(t, 30)
     env.server.close_all_watches()
+
+
+@pytest.mark.timeout(300)
+async def test_hash_routed_shards_converge_under_faults():
+    """Two hash-routed shards (each stores only its own Crons and jobs: the informer keep filter)
+    under the same faults: no tick runs twice and status converges after the faults stop."""
+    import asyncio
+
+    from cron_operator_amd.controller.setup import setup_with_manager
+    from cron_operator_amd.runtime.manager import Manager, ManagerOptions
+
+    env = TestEnv(gc=True)
+    crons = {}
+    for i in range(12):
+        policy = POLICIES[i % 3]
+        name = f"hash-{policy.lower()}-{i}"
+        crons[name] = policy
+        await env.create_cron(new_cron(name, NS, "*/1 * * * *", TMPL, concurrency_policy=policy,
+                                          history_limit=HISTORY))
+    inject(env, seed=31)
+    mgrs, ctrls, tasks = [], [], []
+    for idx in range(2):
+        m = Manager(env.new_client(), ManagerOptions(clock=env.clock, shard_index=idx, shard_count=2,
+                                                     shard_routing="hash", max_concurrent_reconciles=4,
+                                                     health_probe_bind_address="0", metrics_bind_address="0"))
+        ctrl, rec = await setup_with_manager(m)
+        mgrs.append(m)
+        ctrls.append(ctrl)
+        tasks.append(asyncio.get_running_loop().create_task(m.start()))
+    for m in mgrs:
+        await asyncio.wait_for(m.started.wait(), 30)
+
+    async def settle():
+        idle = 0
+        for _ in range(20000):
+            await asyncio.sleep(0)
+            if all(c.queue.idle() for c in ctrls) and env._watches_drained():
+                idle += 1
+                if idle >= 3:
+                    return
+            else:
+                idle = 0
+                await asyncio.sleep(0.0005)
+
+    seen = {}
+    for minute in range(4):
+        for sec in range(60):
+            env.clock.advance(1)
+            if sec == 30:
+                complete_running(env, env.clock.now_ns())
+            if sec == 45:
+                env.server.close_all_watches()
+            await settle()
+            if sec % 10 == 0:
+                check_invariants(env, crons, seen)
+    env.server.faults.clear()
+    for _ in range(180):
+        env.clock.advance(1)
+        await settle()
+    complete_running(env, env.clock.now_ns())
+    for _ in range(30):
+        env.clock.advance(1)
+        await settle()
+    check_invariants(env, crons, seen)
+    last_tick = GoTime((env.clock.now_ns() // NANOS) // 60 * 60, 0, UTC)
+    for name in crons:
+        st = env.server.get(CRON_GVR, NS, name).get("status") or {}
+        assert (st.get("lastScheduleTime") or "")[:16] == last_tick.rfc3339()[:16], name
+        jobs = jobs_of(env, name)
+        done = [j for j in jobs if finished(j)]
+        assert len(done) <= HISTORY
+        assert sorted(h["object"]["name"] for h in st.get("history") or []) == \
+            sorted(j["metadata"]["name"] for j in done)
+    for m in mgrs:
+        m.stop()
+    for t in tasks:
+        await asyncio.wait_for(t, 30)
+    env.server.close_all_watches()
