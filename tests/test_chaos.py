@@ -253,7 +253,7 @@ async def test_hash_routed_shards_converge_under_faults():
         name = f"hash-{policy.lower()}-{i}"
         crons[name] = policy
         await env.create_cron(new_cron(name, NS, "*/1 * * * *", TMPL, concurrency_policy=policy,
-                                          history_limit=HISTORY))
+                                       history_limit=HISTORY))
     inject(env, seed=31)
     mgrs, ctrls, tasks = [], [], []
     for idx in range(2):
