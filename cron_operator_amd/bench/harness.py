@@ -947,7 +947,10 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
                                                                                             [0, 0, 0])[g]
                                              for r, b in zip(last, base)) for g in range(3)],
                          "ms": round(sum(r.get("gc_s", 0.0) - b.get("gc_s", 0.0) for r, b in zip(last, base))
-                                     * 1000, 2)})
+                                     * 1000, 2),
+                         "ms_by_generation": [
+                             round(sum(r.get("gc_gen_s", [0.0] * 3)[g] - b.get("gc_gen_s", [0.0] * 3)[g]
+                                       for r, b in zip(last, base)) * 1000, 2) for g in range(3)]})
     finally:
         for s in shards:
             try:

@@ -336,7 +336,9 @@ async def main() -> int:
                         f"inflight {gate.inflight if gate else 0} gate waiting {gate.waiting if gate else 0} "
                         f"watch pending {pend}")
         sampler = loop.create_task(sample())  # noqa: F841
-    reader = asyncio.StreamReader()
+    # an absorb command lists every owned job's resourceVersion: ~45 bytes a job, far past
+    # StreamReader's 64 KiB line limit at 10,000 Crons
+    reader = asyncio.StreamReader(limit=256 << 20)
     await loop.connect_read_pipe(lambda: asyncio.StreamReaderProtocol(reader), sys.stdin)
 
     async def settled(phase: str, tick_ns: int) -> None:
@@ -396,7 +398,7 @@ async def main() -> int:
             out.write(json.dumps({"ok": True, "lat": lat, "reconciles": ctrl.reconciles,
                                   "requests": client.requests, "by_verb": dict(client.requests_by_verb),
                                   "cpu": time.process_time(), "gc_s": gcs.seconds,
-                                  "gc_collections": list(gcs.collections),
+                                  "gc_collections": list(gcs.collections), "gc_gen_s": list(gcs.gen_seconds),
                                   "maxrss_mib": _maxrss_mib(), "rss_mib": _rss_mib()}) + "\n")
             out.flush()
     _trace_dump("end")

@@ -48,6 +48,7 @@ class GcStats:
 
         self._now = time.perf_counter
         self.collections = [0, 0, 0]
+        self.gen_seconds = [0.0, 0.0, 0.0]
         self.seconds = 0.0
         self._t0 = 0.0
         self._on = False
@@ -56,8 +57,11 @@ class GcStats:
         if phase == "start":
             self._t0 = self._now()
         else:
-            self.seconds += self._now() - self._t0
-            self.collections[info.get("generation", 0)] += 1
+            dt = self._now() - self._t0
+            gen = info.get("generation", 0)
+            self.seconds += dt
+            self.gen_seconds[gen] += dt
+            self.collections[gen] += 1
 
     def start(self) -> "GcStats":
         if not self._on:
@@ -72,4 +76,5 @@ class GcStats:
         return self
 
     def to_dict(self):
-        return {"collections": list(self.collections), "ms": round(self.seconds * 1000, 2)}
+        return {"collections": list(self.collections), "ms": round(self.seconds * 1000, 2),
+                "ms_by_generation": [round(x * 1000, 2) for x in self.gen_seconds]}

@@ -93,12 +93,18 @@ for s in $STEPS; do
     mem10k)
       # peak RSS of the operator alone (its own process) at 10,000 Crons / 110,000 jobs over 10
       # ticks: one template shared by every Cron, then a distinct template per Cron
-      for c in "" "--distinct-templates"; do
+      # (MEM_VARIANTS overrides the list; "--lifecycle realistic": the training-operator's status sequence)
+      old_ifs=$IFS; IFS=';'
+      for c in ${MEM_VARIANTS:-";--distinct-templates"}; do
+        IFS=$old_ifs
+        tag=$(echo "$c" | tr -c 'a-z0-9' '_' | sed 's/^_*//; s/_*$//')
         step "mem10k $c"
         timeout -k 10 600 python -u scripts/bench_scale.py --sizes 10000 --modes optimized --steps 10 --warmup 1 \
-          --operator-process $c --out "$OUT/mem10k${c:+_distinct}.json" > "$OUT/mem10k${c:+_distinct}.log" 2>&1
-        check $? "mem10k $c"; tail -3 "$OUT/mem10k${c:+_distinct}.log"
-      done ;;
+          --operator-process $c --out "$OUT/mem10k${tag:+_$tag}.json" > "$OUT/mem10k${tag:+_$tag}.log" 2>&1
+        check $? "mem10k $c"; head -1 "$OUT/mem10k${tag:+_$tag}.log"
+        IFS=';'
+      done
+      IFS=$old_ifs ;;
     ranks)
       for n in ${RANKS:-2 4}; do
         step "ranks $n"
