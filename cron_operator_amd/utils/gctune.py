@@ -12,7 +12,8 @@ by reference counting; measured in the bench, that was ~1.7 s of pauses per run
 * :func:`tune` -- a larger generation-0 threshold, so short-lived reconcile
   garbage is collected in fewer, cheaper passes.
 
-Disabled with ``CRON_OPERATOR_GC_TUNING=0``.
+Disabled with ``CRON_OPERATOR_GC_TUNING=0``; ``CRON_OPERATOR_GC_THRESHOLDS=g0,g1,g2`` replaces
+the thresholds.
 """
 from __future__ import annotations
 
@@ -23,13 +24,22 @@ _ENABLED = os.environ.get("CRON_OPERATOR_GC_TUNING", "1") not in ("0", "false", 
 DEFAULT_THRESHOLDS = (50_000, 20, 100)
 
 
+def _thresholds_from_env():
+    raw = os.environ.get("CRON_OPERATOR_GC_THRESHOLDS", "")
+    try:
+        t = tuple(int(x) for x in raw.split(","))
+    except ValueError:
+        return None
+    return t if len(t) == 3 and all(x >= 0 for x in t) else None
+
+
 def enabled() -> bool:
     return _ENABLED
 
 
 def tune(thresholds=DEFAULT_THRESHOLDS) -> None:
     if _ENABLED:
-        gc.set_threshold(*thresholds)
+        gc.set_threshold(*(_thresholds_from_env() or thresholds))
 
 
 def freeze() -> None:
