@@ -449,10 +449,13 @@ class WireCodecs:
     the Python twin ignores memo paths).  One memo is shared: the status-write encoder
     remembers each history entry it writes, the Cron event decoder hands those objects
     back when the watch echoes the same bytes.  ``slim`` also skips what the caches drop
-    anyway: a child's ``spec`` and every ``managedFields``."""
+    anyway: a child's ``spec`` and every ``managedFields``.  ``shard=(index, count)`` (hash-routed
+    sharding, where every shard watches the whole fleet): the Cron and child decoders build only
+    the metadata of another shard's objects (route paths), which the informers' keep filter
+    then drops."""
 
     def __init__(self, slim: bool = True, memo_slots: int = 1 << 14, memo_max_slots: int = 1 << 19,
-                 compact_metadata: bool = False):
+                 compact_metadata: bool = False, shard: Optional[Tuple[int, int]] = None):
         # grows with the fleet: ~12 values per Cron (its history entries, a labels map and an owner
         # reference) stay remembered up to ~40,000 Crons per process
         self.memo = jsonutil.Memo(memo_slots, memo_max_slots)
@@ -467,21 +470,29 @@ class WireCodecs:
         # new job -- is kept as its JSON text (slim): ~0.6 KB instead of ~6 KB of dicts per Cron
         # when templates differ, decoded afresh per fire instead of deep-copied
         tw = ("spec", "template", "workload")
+
+        def routed(at: Tuple[str, ...], label: Optional[str]) -> Dict[str, Any]:
+            return {} if shard is None else {"route_paths": [at], "route": (shard[0], shard[1], label)}
+
         self.cron_event = jsonutil.Codec(skip=[("object",) + mf] if slim else [],
                                          memo_paths=[("object", "spec"), ("object", "status", "history", "*")],
-                                         memo=self.memo, raw_paths=[("object",) + tw] if slim else [])
+                                         memo=self.memo, raw_paths=[("object",) + tw] if slim else [],
+                                         **routed(("object",), None))
         self.child_event = jsonutil.Codec(skip=[("object",) + p for p in child_skip],
-                                          memo_paths=[("object",) + p for p in child_memo], memo=self.memo)
+                                          memo_paths=[("object",) + p for p in child_memo], memo=self.memo,
+                                          **routed(("object",), LABEL_CRON_NAME))
         self.child_object = jsonutil.Codec(skip=child_skip, memo_paths=child_memo, memo=self.memo)
         # LIST pages: the same plans under items/* (the initial LIST of 110,000 jobs shares labels
         # and owner references as the watch events do, and never builds a spec)
         self.child_list = jsonutil.Codec(skip=[("items", "*") + p for p in child_skip],
-                                         memo_paths=[("items", "*") + p for p in child_memo], memo=self.memo)
+                                         memo_paths=[("items", "*") + p for p in child_memo], memo=self.memo,
+                                         **routed(("items", "*"), LABEL_CRON_NAME))
         # (a LIST's history entries are not remembered: the reconciler's own entries replace them
         # at its first status write, and only those are forgotten when they rotate out)
         self.cron_list = jsonutil.Codec(skip=[("items", "*") + mf] if slim else [],
                                         memo_paths=[("items", "*", "spec")], memo=self.memo,
-                                        raw_paths=[("items", "*") + tw] if slim else [])
+                                        raw_paths=[("items", "*") + tw] if slim else [],
+                                        **routed(("items", "*"), None))
         self.status_patch = jsonutil.Codec(memo_paths=[("status", "history", "*")], memo=self.memo)
 
 

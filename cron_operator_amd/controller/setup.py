@@ -70,7 +70,8 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
         raise ValueError(f"unknown shard routing {mgr.opts.shard_routing!r}")
     by_label = count > 1 and mgr.opts.shard_routing == "labels"
     by_hash = count > 1 and not by_label
-    codecs = WireCodecs(opts.slim_child_cache, compact_metadata=opts.compact_metadata()) if opts.wire_codecs else None
+    codecs = WireCodecs(opts.slim_child_cache, compact_metadata=opts.compact_metadata(),
+                        shard=(index, count) if by_hash else None) if opts.wire_codecs else None
     cron_inf = await mgr.cache.get_informer(CRON_GVK,
                                             label_selector=sharding.shard_selector(index, count) if by_label else None,
                                             transform=strip_managed_fields if opts.slim_child_cache else None,

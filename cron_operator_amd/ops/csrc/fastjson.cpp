@@ -345,6 +345,11 @@ PyObject* cached_value(const char* p, size_t n) {
 //          was decoded from -- or encoded to -- exactly those bytes, returns that object
 //          instead of building a new one; otherwise it builds and remembers it.  The
 //          encoder remembers the bytes of each value it writes at a memo path.
+//   raw    the decoder returns the value's JSON text (bytes) and the encoder writes it back.
+//   route  (hash-routed shards) once the object's `metadata` is decoded, an object that
+//          hashes to another shard gets the rest of its members skipped: a shard that
+//          watches the whole fleet builds only its own share, and only the metadata of
+//          the rest, which its informer's keep filter then drops.
 //
 // Memo values are shared between trees, so they must never be mutated -- the informer
 // cache and the reconciler's status entries are read-only by contract already.  Byte
@@ -356,7 +361,7 @@ PyObject* cached_value(const char* p, size_t n) {
 // identity: the reconciler's status write re-sends the same history-entry dicts on every
 // tick, so only the changed entries are encoded (a 10-entry status patch: 12 -> 1.3 us).
 
-enum Action : uint8_t { kActNone = 0, kActSkip = 1, kActMemo = 2, kActRaw = 3 };
+enum Action : uint8_t { kActNone = 0, kActSkip = 1, kActMemo = 2, kActRaw = 3, kActRoute = 4 };
 
 struct PlanNode {
   std::vector<std::pair<std::string, int>> kids;
@@ -366,6 +371,51 @@ struct PlanNode {
 
 struct Plan {
   std::vector<PlanNode> nodes;  // nodes[0]: the root
+  // route paths (hash-routed shards): an object there whose key hashes to another shard keeps
+  // only what precedes and includes its `metadata`; the rest is skipped, never built.  The key
+  // is `namespace/name`, or `namespace/<labels[route_label]>` when a label is given (an object
+  // without that label is this shard's), hashed as runtime/controller.py shard_of does
+  uint32_t route_index = 0, route_count = 0;
+  std::string route_label;
+  bool route_by_label = false;
+
+  static bool utf8_of(PyObject* s, const char** d, Py_ssize_t* n) {
+    if (!PyUnicode_CheckExact(s)) return false;
+    *d = PyUnicode_AsUTF8AndSize(s, n);
+    if (*d == nullptr) {
+      PyErr_Clear();
+      return false;
+    }
+    return true;
+  }
+  // true only when the object surely belongs to another shard (anything unexpected: kept)
+  bool foreign(PyObject* meta) const {
+    if (route_count <= 1 || !PyDict_CheckExact(meta)) return false;
+    const char* ns = "";
+    Py_ssize_t nn = 0;
+    PyObject* nsv = PyDict_GetItemString(meta, "namespace");
+    if (nsv != nullptr && !utf8_of(nsv, &ns, &nn)) return false;
+    PyObject* keyv;
+    if (route_by_label) {
+      PyObject* labels = PyDict_GetItemString(meta, "labels");
+      if (labels == nullptr || !PyDict_CheckExact(labels)) return false;
+      keyv = PyDict_GetItemString(labels, route_label.c_str());
+      if (keyv == nullptr) return false;
+    } else {
+      keyv = PyDict_GetItemString(meta, "name");
+    }
+    const char* key = "";
+    Py_ssize_t kn = 0;
+    if (keyv != nullptr && !utf8_of(keyv, &key, &kn)) return false;
+    uint32_t h = 0x811C9DC5u;
+    auto mix = [&h](const char* b, Py_ssize_t n) {
+      for (Py_ssize_t i = 0; i < n; ++i) h = (h ^ static_cast<uint8_t>(b[i])) * 0x01000193u;
+    };
+    mix(ns, nn);
+    mix("/", 1);
+    mix(key, kn);
+    return h % route_count != route_index;
+  }
 
   int child(int node, const char* k, size_t n) const {
     if (node < 0) return -1;
@@ -927,6 +977,37 @@ struct Decoder {
   }
 
   // scan past one value (p at its first byte, whitespace skipped); structure only
+  // the members left in an object (after a value): `, "key": value ...}` skipped up to and
+  // including the closing brace, with the same syntax checks as a decode
+  bool skip_members() {
+    while (true) {
+      ws();
+      if (p < end && *p == '}') {
+        ++p;
+        return true;
+      }
+      if (p >= end || *p != ',') {
+        fail("Expecting ',' delimiter");
+        return false;
+      }
+      ++p;
+      ws();
+      if (p >= end || *p != '"') {
+        fail("Expecting property name enclosed in double quotes");
+        return false;
+      }
+      if (!skip_value()) return false;
+      ws();
+      if (p >= end || *p != ':') {
+        fail("Expecting ':' delimiter");
+        return false;
+      }
+      ++p;
+      ws();
+      if (!skip_value()) return false;
+    }
+  }
+
   bool skip_value() {
     if (p >= end) {
       fail("Expecting value");
@@ -1037,10 +1118,14 @@ struct Decoder {
           if (p >= end || *p != ':') { Py_DECREF(k); Py_DECREF(d); return fail("Expecting ':' delimiter"); }
           ++p;
           int kid = -1;
+          bool route_meta = false;
           if (node >= 0) {
             const char* kd;
             size_t kn;
-            if (key_bytes(k, &kd, &kn)) kid = plan->child(node, kd, kn);
+            if (key_bytes(k, &kd, &kn)) {
+              kid = plan->child(node, kd, kn);
+              route_meta = plan->act(node) == kActRoute && kn == 8 && std::memcmp(kd, "metadata", 8) == 0;
+            }
             if (kid >= 0 && plan->act(kid) == kActSkip) {
               Py_DECREF(k);
               ws();
@@ -1055,9 +1140,14 @@ struct Decoder {
           PyObject* v = value(depth + 1, kid);
           if (!v) { Py_DECREF(k); Py_DECREF(d); return nullptr; }
           const int rc = PyDict_SetItem(d, k, v);
+          const bool away = rc >= 0 && route_meta && plan->foreign(v);
           Py_DECREF(k);
           Py_DECREF(v);
           if (rc < 0) { Py_DECREF(d); return nullptr; }
+          if (away) {  // another shard's object: its remaining members are skipped
+            if (!skip_members()) { Py_DECREF(d); return nullptr; }
+            return acyclic(d);
+          }
           ws();
           if (p < end && *p == ',') { ++p; continue; }
           if (p < end && *p == '}') { ++p; return acyclic(d); }
@@ -1917,14 +2007,29 @@ PyObject* codec_decode(CodecObject* c, PyObject* arg) {
 }
 
 PyObject* codec_new(PyTypeObject* type, PyObject* args, PyObject* kwds) {
-  static const char* kw[] = {"skip", "memo_paths", "memo", "raw_paths", nullptr};
+  static const char* kw[] = {"skip", "memo_paths", "memo", "raw_paths", "route_paths", "route", nullptr};
   PyObject* skip = nullptr;
   PyObject* memo_paths = nullptr;
   PyObject* memo = nullptr;
   PyObject* raw_paths = nullptr;
-  if (!PyArg_ParseTupleAndKeywords(args, kwds, "|OOOO", const_cast<char**>(kw), &skip, &memo_paths, &memo,
-                                   &raw_paths))
+  PyObject* route_paths = nullptr;
+  PyObject* route = nullptr;
+  if (!PyArg_ParseTupleAndKeywords(args, kwds, "|OOOOOO", const_cast<char**>(kw), &skip, &memo_paths, &memo,
+                                   &raw_paths, &route_paths, &route))
     return nullptr;
+  unsigned int r_index = 0, r_count = 0;
+  PyObject* r_label = Py_None;
+  const bool routed = route_paths != nullptr && route_paths != Py_None;
+  if (routed) {
+    // route = (index, count, label or None)
+    if (route == nullptr || !PyTuple_Check(route) ||
+        !PyArg_ParseTuple(route, "IIO", &r_index, &r_count, &r_label) || r_count < 1 || r_index >= r_count ||
+        (r_label != Py_None && !PyUnicode_Check(r_label))) {
+      if (!PyErr_Occurred())
+        PyErr_SetString(PyExc_ValueError, "route must be (index, count, label or None) with 0 <= index < count");
+      return nullptr;
+    }
+  }
   if (memo == Py_None) memo = nullptr;
   if (memo != nullptr && !PyObject_TypeCheck(memo, &MemoType)) {
     PyErr_SetString(PyExc_TypeError, "memo must be a Memo");
@@ -1945,9 +2050,24 @@ PyObject* codec_new(PyTypeObject* type, PyObject* args, PyObject* kwds) {
     Py_DECREF(seq);
     return true;
   };
-  if (!add_all(skip, kActSkip) || !add_all(memo_paths, kActMemo) || !add_all(raw_paths, kActRaw)) {
+  if (!add_all(skip, kActSkip) || !add_all(memo_paths, kActMemo) || !add_all(raw_paths, kActRaw) ||
+      (routed && !add_all(route_paths, kActRoute))) {
     delete plan;
     return nullptr;
+  }
+  if (routed) {
+    plan->route_index = r_index;
+    plan->route_count = r_count;
+    if (r_label != Py_None) {
+      Py_ssize_t ln = 0;
+      const char* l = PyUnicode_AsUTF8AndSize(r_label, &ln);
+      if (l == nullptr) {
+        delete plan;
+        return nullptr;
+      }
+      plan->route_label.assign(l, static_cast<size_t>(ln));
+      plan->route_by_label = true;
+    }
   }
   PyObject* self = type->tp_alloc(type, 0);
   if (!self) {
@@ -2088,7 +2208,8 @@ PyMODINIT_FUNC PyInit__fastjson(void) {
   CodecType.tp_basicsize = sizeof(CodecObject);
   CodecType.tp_flags = Py_TPFLAGS_DEFAULT | Py_TPFLAGS_HAVE_VECTORCALL;
   CodecType.tp_doc =
-      "Codec(skip=(), memo_paths=(), memo=None, raw_paths=()): JSON decode/encode with skipped, memoised and raw paths; "
+      "Codec(skip=(), memo_paths=(), memo=None, raw_paths=(), route_paths=None, route=None): JSON decode/encode "
+      "with skipped, memoised, raw and routed paths; "
       "calling it decodes one watch event line into (type, object)";
   CodecType.tp_new = codec_new_vc;
   CodecType.tp_dealloc = codec_dealloc;

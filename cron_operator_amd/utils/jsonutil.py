@@ -245,6 +245,52 @@ def _rawify(v: Any, path: Any) -> None:
         v[head] = dumpb(v[head])
 
 
+def _route_foreign(meta: Any, route: Any) -> bool:
+    """The native codec's route test: True only when ``meta`` surely hashes to another shard
+    (FNV-1a of ``namespace/key``, as ``runtime.controller.shard_of``)."""
+    index, count, label = route
+    if count <= 1 or type(meta) is not dict:
+        return False
+    ns = meta.get("namespace", "")
+    if type(ns) is not str:
+        return False
+    if label is not None:
+        labels = meta.get("labels")
+        if type(labels) is not dict or label not in labels:
+            return False
+        key = labels[label]
+    else:
+        key = meta.get("name", "")
+    if type(key) is not str:
+        return False
+    try:
+        raw = f"{ns}/{key}".encode()
+    except UnicodeEncodeError:
+        return False
+    h = 0x811C9DC5
+    for b in raw:
+        h = ((h ^ b) * 0x01000193) & 0xFFFFFFFF
+    return h % count != index
+
+
+def _route(v: Any, path: Any, route: Any) -> None:
+    """At ``path``: an object of another shard keeps its members up to ``metadata``."""
+    if not path:
+        if type(v) is dict and "metadata" in v and _route_foreign(v["metadata"], route):
+            keys = list(v)
+            for k in keys[keys.index("metadata") + 1:]:
+                del v[k]
+        return
+    head, rest = path[0], path[1:]
+    if head == "*":
+        if type(v) is list:
+            for x in v:
+                _route(x, rest, route)
+        return
+    if type(v) is dict and head in v:
+        _route(v[head], rest, route)
+
+
 def _unraw(v: Any, path: Any) -> None:
     head, rest = path[0], path[1:]
     if head == "*":
@@ -264,19 +310,30 @@ def _unraw(v: Any, path: Any) -> None:
 
 
 class PyCodec:
-    """Python twin of the native ``Codec(skip, memo_paths, memo, raw_paths)``: ``loads``
-    decodes, removes the skipped paths ("*" = any list element) and turns the values at raw
-    paths into their JSON text (bytes; re-encoded compactly here, the input's own text
-    natively); memo paths change nothing but speed, so they are ignored here.  Calling it
+    """Python twin of the native ``Codec(skip, memo_paths, memo, raw_paths, route_paths, route)``:
+    ``loads`` decodes, cuts another shard's objects at route paths after their ``metadata``,
+    removes the skipped paths ("*" = any list element) and turns the values at raw paths into
+    their JSON text (bytes; re-encoded compactly here, the input's own text natively); memo
+    paths change nothing but speed, so they are ignored here.  Calling it
     decodes one watch event line into ``(type, object)``."""
 
-    def __init__(self, skip: Any = (), memo_paths: Any = (), memo: Any = None, raw_paths: Any = ()):
+    def __init__(self, skip: Any = (), memo_paths: Any = (), memo: Any = None, raw_paths: Any = (),
+                 route_paths: Any = None, route: Any = None):
         self.skip = [tuple(p) for p in skip or ()]
         self.raw = [tuple(p) for p in raw_paths or ()]
         self.memo = memo
+        self.route_paths = [tuple(p) for p in route_paths] if route_paths is not None else []
+        if route_paths is not None:
+            index, count, label = route
+            if not (isinstance(index, int) and isinstance(count, int) and 0 <= index < count) or \
+                    not (label is None or isinstance(label, str)):
+                raise ValueError("route must be (index, count, label or None) with 0 <= index < count")
+        self.route = route
 
     def loads(self, data: Any) -> Any:
         v = loads(data)
+        for path in self.route_paths:
+            _route(v, path, self.route)
         for path in self.skip:
             _drop(v, path)
         for path in self.raw:

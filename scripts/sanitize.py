@@ -146,6 +146,22 @@ def drive(scratch: str, iters: int) -> None:
             if rng.random() < 0.5:
                 memo.forget(v)
         assert codec.dumpb(doc) == fj.dumpb(doc)
+    # route paths (hash-routed shards): another shard's objects cut after their metadata, over
+    # random (often ill-typed) metadata and mutated (often malformed) input
+    routers = [fj.Codec(route_paths=[("items", "*")], route=(i, 3, lbl), skip=[("items", "*", "s")])
+               for i in range(3) for lbl in (None, "c")]
+    for _ in range(iters // 8):
+        meta = {"name": rng.choice(["a", "b", "é", "", 5, None]), "namespace": rng.choice(["ns", "", None, 3]),
+                "labels": rng.choice([{"c": rng.choice(["a", "b", 7])}, {}, "x", None])}
+        items = [{"metadata": _tree(rng) if rng.random() < 0.2 else meta, "s": _tree(rng), "t": _tree(rng)}
+                 for _ in range(rng.randint(0, 3))]
+        raw = fj.dumpb({"items": items})
+        for r in routers:
+            r.loads(raw)
+            try:
+                r.loads(_mutate(rng, raw))
+            except (ValueError, RecursionError):
+                pass
     # kubeflow job-status summaries over random (often ill-typed) statuses
     times = ["2026-01-01T12:00:00Z", "2026-01-01T12:00:00.123+02:00", "2026-13-01T00:00:00Z", "", "x" * 30,
              "2026-01-01T12:00:00Z\n", "٢٠٢٦-01-01T12:00:00Z"]

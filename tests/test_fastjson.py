@@ -390,3 +390,69 @@ def test_codec_raw_paths_keep_the_exact_json_text_also_below_a_memo_path():
     py = jsonutil.PyCodec(raw_paths=[("object", "spec", "template", "workload")])
     _, p = py(line)
     assert json.loads(p["spec"]["template"]["workload"]) == json.loads(wl)
+
+
+# ------------------------------------------------------------------ route paths (hash-routed shards)
+
+LBL = "kubedl.io/cron-name"
+route_meta = st.fixed_dictionaries({}, optional={
+    "name": st.one_of(st.text(max_size=6), st.integers(0, 3)),
+    "namespace": st.one_of(st.sampled_from(["", "ns", "tëam"]), st.none(), st.just("\ud800")),
+    "labels": st.one_of(st.dictionaries(st.sampled_from([LBL, "app"]), st.one_of(st.text(max_size=6), st.none()),
+                                        max_size=2), st.text(max_size=2)),
+})
+route_objs = st.lists(st.fixed_dictionaries({"metadata": route_meta}, optional={
+    "apiVersion": st.just("v1"), "spec": json_values, "status": json_values}), max_size=6)
+
+
+@settings(max_examples=300, deadline=None)
+@given(route_objs, st.integers(1, 4), st.data(), st.sampled_from([None, LBL]))
+def test_codec_route_paths_match_python_twin_and_shard_of(items, count, data, label):
+    """Another shard's objects keep their members up to ``metadata`` (natively: the rest is
+    never built); this shard's, and anything the test cannot hash, decode whole.  The cut
+    agrees with ``shard_of`` -- what the informer's keep filter then applies."""
+    from cron_operator_amd.runtime.controller import shard_of
+
+    index = data.draw(st.integers(0, count - 1))
+    raw = json.dumps({"kind": "List", "items": items})
+    kw = {"route_paths": [("items", "*")], "route": (index, count, label)}
+    native = m.Codec(**kw).loads(raw)
+    twin = jsonutil.PyCodec(**kw).loads(raw)
+    assert repr(native) == repr(twin)
+    for full, got in zip(json.loads(raw)["items"], native["items"]):
+        md = full["metadata"]
+        labels = md.get("labels")
+        if label:  # routed by the cron-name label: an object without it is this shard's
+            key = labels.get(LBL) if isinstance(labels, dict) and LBL in labels else None
+        else:
+            key = md.get("name", "")
+        ns = md.get("namespace", "")
+        hashable = isinstance(ns, str) and isinstance(key, str) and "\ud800" not in ns + key
+        mine = not hashable or count == 1 or shard_of(ns, key, count) == index
+        keys = list(full)
+        cut = {k: full[k] for k in keys[:keys.index("metadata") + 1]}  # members up to metadata
+        assert repr(got) == repr(full if mine else cut)
+    ev = json.dumps({"type": "ADDED", "object": items[0]}) if items else None
+    if ev:
+        kw1 = {"route_paths": [("object",)], "route": (index, count, label)}
+        assert repr(m.Codec(**kw1)(ev)) == repr(jsonutil.PyCodec(**kw1)(ev))
+
+
+def test_codec_route_paths_check_their_arguments_and_syntax():
+    for bad in [(2, 2, None), (0, 0, None), (0, 2, 5), "x", None]:
+        with pytest.raises((ValueError, TypeError)):
+            m.Codec(route_paths=[("object",)], route=bad)
+        with pytest.raises((ValueError, TypeError)):
+            jsonutil.PyCodec(route_paths=[("object",)], route=bad)
+    c = m.Codec(route_paths=[("object",)], route=(0, 2, None))  # "a" hashes to shard 1 of 2
+    from cron_operator_amd.runtime.controller import shard_of
+
+    assert shard_of("", "a", 2) == 1
+    ok = b'{"type": "ADDED", "object": {"metadata": {"name": "a"}, "spec": {"x": [1, {"y": 2}]}, "z": 1}}'
+    assert c(ok) == ("ADDED", {"metadata": {"name": "a"}})
+    head = b'{"object": {"metadata": {"name": "a"}'
+    for broken in (head + b', "spec" 1}}', head + b',}}', head + b' "x": 1}}', head + b', "x": [}}', head + b', "x": 1'):
+        with pytest.raises(ValueError):
+            c.loads(broken)
+        with pytest.raises(ValueError):
+            json.loads(broken)

@@ -202,3 +202,36 @@ def test_a_fixed_name_template_kept_as_text_still_runs_as_forbid():
     named = dict(PT_TMPL, metadata={"name": "fixed"})
     assert _template_fixed_name(jsonutil.dumpb(named)) and not _template_fixed_name(jsonutil.dumpb(PT_TMPL))
     assert _template_fixed_name(named) and not _template_fixed_name(b"not json")
+
+
+def test_hash_routed_codecs_build_only_their_shards_objects():
+    """With hash routing every shard watches the whole fleet: its decoders (``WireCodecs(shard=)``)
+    build another shard's Crons and jobs only up to their metadata, which the informers' keep
+    filter then drops; its own decode whole."""
+    import json
+
+    from cron_operator_amd.controller.reconciler import WireCodecs
+    from cron_operator_amd.runtime.controller import shard_of
+
+    names = [f"c{i}" for i in range(8)]
+    mine = {n for n in names if shard_of(NS, n, 2) == 0}
+    assert mine and len(mine) < len(names)
+    c = WireCodecs(shard=(0, 2))
+    for n in names:
+        cron = {"apiVersion": "apps.kubedl.io/v1alpha1", "kind": "Cron", "metadata": {"name": n, "namespace": NS},
+                "spec": {"schedule": "* * * * *", "template": {"workload": PT_TMPL}}, "status": {"history": []}}
+        _, got = c.cron_event(json.dumps({"type": "MODIFIED", "object": cron}).encode())
+        assert ("spec" in got and "status" in got) == (n in mine)
+        job = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+               "metadata": {"name": f"{n}-1", "namespace": NS, "labels": {LABEL_CRON_NAME: n}},
+               "status": {"conditions": [{"type": "Succeeded", "status": "True"}]}}
+        _, got = c.child_event(json.dumps({"type": "MODIFIED", "object": job}).encode())
+        assert ("status" in got) == (n in mine)
+        page = c.cron_list.loads(json.dumps({"kind": "List", "metadata": {}, "items": [cron]}).encode())
+        assert ("spec" in page["items"][0]) == (n in mine)
+    # a job without the cron-name label is routed to every shard (as without sharding)
+    _, got = c.child_event(json.dumps({"type": "ADDED", "object": {"metadata": {"name": "x", "namespace": NS},
+                                                                  "status": {}}}).encode())
+    assert "status" in got
+    assert "spec" in WireCodecs().cron_event(json.dumps({"type": "ADDED", "object": {
+        "metadata": {"name": next(n for n in names if n not in mine)}, "spec": {}}}).encode())[1]
