@@ -451,7 +451,8 @@ def test_codec_route_paths_check_their_arguments_and_syntax():
     ok = b'{"type": "ADDED", "object": {"metadata": {"name": "a"}, "spec": {"x": [1, {"y": 2}]}, "z": 1}}'
     assert c(ok) == ("ADDED", {"metadata": {"name": "a"}})
     head = b'{"object": {"metadata": {"name": "a"}'
-    for broken in (head + b', "spec" 1}}', head + b',}}', head + b' "x": 1}}', head + b', "x": [}}', head + b', "x": 1'):
+    for tail in (b', "spec" 1}}', b',}}', b' "x": 1}}', b', "x": [}}', b', "x": 1'):
+        broken = head + tail
         with pytest.raises(ValueError):
             c.loads(broken)
         with pytest.raises(ValueError):
