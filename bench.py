@@ -350,7 +350,8 @@ def main() -> int:
     mine = {"elapsed_s": res.elapsed_s, "fires": cfg.n_crons * cfg.steps,
             "reconciles": res.raw_reconciles_per_s * res.elapsed_s, "p50": res.p50_latency_ms,
             "p99": res.p99_latency_ms, "req_per_fire": res.api_requests_per_fire,
-            "cpu_op": res.cpu_s_operator, "cpu_api": res.cpu_s_apiserver}
+            "cpu_op": res.cpu_s_operator, "cpu_api": res.cpu_s_apiserver,
+            "shard_rss": max(res.operator_maxrss_mib or [0.0])}
 
     # the shipped default: one operator process (untimed for the headline, like the baseline)
     if a.single_process == "measure" and a.transport == "http":
@@ -476,6 +477,9 @@ def main() -> int:
             # fake apiserver's speed; and how busy that fixture was (CPU s / wall s, max rank)
             "operator_cpu_ms_per_fire": round(sum(r["cpu_op"] for r in allr) * 1000 / fires, 4),
             "apiserver_busy_frac": round(max(r["cpu_api"] / r["elapsed_s"] for r in allr), 3),
+            # peak resident memory of the largest operator shard process (0: the operator ran in
+            # the bench process itself)
+            "operator_shard_peak_rss_mib": round(max(r.get("shard_rss", 0.0) for r in allr), 1),
             "baseline_value": round(base_value, 2) if base_value else None,
             "baseline_source": base_src,
             "baseline_p50_schedule_to_create_ms": round(max(r["ref_p50"] for r in allr), 2)
