@@ -235,3 +235,54 @@ def test_hash_routed_codecs_build_only_their_shards_objects():
     assert "status" in got
     assert "spec" in WireCodecs().cron_event(json.dumps({"type": "ADDED", "object": {
         "metadata": {"name": next(n for n in names if n not in mine)}, "spec": {}}}).encode())[1]
+
+
+async def test_hash_routed_shards_over_http_fire_every_cron_once():
+    """Two hash-routed shards against the HTTP apiserver (route-path decoders + keep-filtered
+    informers): every Cron fires once per tick, by its own shard, and each shard caches only
+    its own Crons and jobs."""
+    from cron_operator_amd.apiserver.http import APIServerApp
+    from cron_operator_amd.runtime.client import Client
+    from cron_operator_amd.runtime.controller import shard_of
+    from cron_operator_amd.runtime.http import HttpTransport
+    from cron_operator_amd.runtime.kubeconfig import RestConfig
+
+    env = TestEnv()
+    names = [f"h{i}" for i in range(8)]
+    for n in names:
+        await env.create_cron(new_cron(n, NS, "*/1 * * * *", PT_TMPL, history_limit=2))
+    app = APIServerApp(env.server)
+    port = await app.start("127.0.0.1", 0)
+    clients, mgrs, recs, tasks = [], [], [], []
+    try:
+        for idx in range(2):
+            client = Client(HttpTransport(RestConfig(host=f"http://127.0.0.1:{port}")), qps=-1)
+            mgr = Manager(client, ManagerOptions(clock=env.clock, health_probe_bind_address="0",
+                                                 metrics_bind_address="0", shard_index=idx, shard_count=2,
+                                                 shard_routing="hash"))
+            _, rec = await setup_with_manager(mgr, ReconcilerOptions())
+            clients.append(client)
+            mgrs.append(mgr)
+            recs.append(rec)
+            tasks.append(asyncio.get_running_loop().create_task(mgr.start()))
+        for mgr in mgrs:
+            await asyncio.wait_for(mgr.started.wait(), 20)
+        env.clock.advance(60)
+        await _until(lambda: len(env.server.list(PT, NS)["items"]) == len(names), "a job per Cron")
+        await asyncio.sleep(0.2)  # a second CREATE would show up by now
+        jobs = env.server.list(PT, NS)["items"]
+        assert sorted(j["metadata"]["labels"][LABEL_CRON_NAME] for j in jobs) == sorted(names)
+        for idx, rec in enumerate(recs):
+            mine = {n for n in names if shard_of(NS, n, 2) == idx}
+            await _until(lambda r=rec, m=mine: {o["metadata"]["labels"][LABEL_CRON_NAME] for inf in
+                                                r.child_informers.values() for o in inf.store.values()} == m,
+                         f"shard {idx}'s jobs cached")
+            assert {o["metadata"]["name"] for o in rec.cron_informer.store.values()} == mine
+            assert rec.codecs is not None
+    finally:
+        for mgr in mgrs:
+            mgr.stop()
+        await asyncio.wait(set(tasks), timeout=10)
+        for client in clients:
+            await client.close()
+        await app.stop()
