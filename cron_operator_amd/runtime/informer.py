@@ -103,7 +103,8 @@ class Informer:
     ``transform`` (client-go ``SetTransform``) rewrites every object before it is
     stored or handed to handlers -- e.g. dropping fields no consumer reads to keep
     a large cache small.  Objects reaching it were decoded for this informer alone,
-    so it may modify them in place.
+    so it may modify them in place.  ``keep`` then decides what is stored at all: a
+    filter the apiserver cannot apply (one shard's hash share of a fleet).
     """
 
     def __init__(self, client: Client, target: Any, namespace: str = "", label_selector: Optional[str] = None,
