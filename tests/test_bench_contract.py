@@ -40,6 +40,7 @@ def test_single_rank_line():
     # operator cost, separated from the fake apiserver fixture
     assert d["operator_cpu_ms_per_fire"] > 0
     assert 0 < d["apiserver_busy_frac"] < 2
+    assert 10 < d["operator_shard_peak_rss_mib"] < 1024  # the largest shard process's peak
     # the denominator is the reference algorithm measured by this same invocation
     assert d["baseline_source"].startswith("measured")
     assert d["baseline_value"] > 0 and d["baseline_p50_schedule_to_create_ms"] > 0
