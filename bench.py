@@ -28,18 +28,17 @@ scaling) and rank 0 reports the whole-job aggregate.  Ranks synchronise with
 gloo barriers; there is no device work to ``torch.cuda.synchronize()``.
 
 ``single_process_*``: the chart ships ONE operator process (``sharding.count: 1``,
-``processes: 1``).  That deployment is operator-bound (its apiserver is about half
-busy), so it is the number that measures the product; it runs in the same invocation
-on the same Crons, after the timed run (``--single-process none`` skips it).
+``processes: 1``); it runs in the same invocation on the same Crons, after the timed run
+(``--single-process none`` skips it).  ``operator_cpu_ms_per_fire`` and ``apiserver_busy_frac``
+(and their ``single_process_`` twins) say which side bounds each number: near 1.0 busy, the fake
+apiserver fixture does (the driver's round-5 record: 0.938 at 3 shards, 0.857 for one process).
 
-``deployment_*``: the headline and its denominator run against a fake apiserver that
-answers as fast as its Python CPU allows, so the 60-70x ``vs_baseline`` mostly measures
-the fixture's O(namespace) label-selected LIST (the reference LISTs live on every
-reconcile).  A real cluster is latency-bound: TLS on every connection and an etcd
-quorum write behind every mutation.  ``deployment_value`` / ``deployment_baseline_value``
-are both algorithms in that shape (one process each, TLS + the harness's ``etcd`` latency
-model), run in this same invocation after the timed run; ``vs_baseline_deployment`` is
-their ratio (``--deployment none`` skips them).
+``deployment_*``: a real cluster is latency-bound, not CPU-bound: TLS on every connection and an
+etcd quorum write behind every mutation.  ``deployment_value`` / ``deployment_baseline_value`` are
+both algorithms in that shape (one process each, TLS + the harness's ``etcd`` latency model, whose
+``list_per_object`` charges the namespace scan a real apiserver does for a label-selected LIST), run
+in this same invocation after the timed run; ``vs_baseline_deployment`` is their ratio
+(``--deployment none`` skips them).
 
 Job lifecycle.  The headline (and its single-process and reference runs) keeps the rounds 1-4
 step: each job of the previous tick is marked Succeeded in one write (``--lifecycle instant``).
@@ -351,7 +350,7 @@ def main() -> int:
             "reconciles": res.raw_reconciles_per_s * res.elapsed_s, "p50": res.p50_latency_ms,
             "p99": res.p99_latency_ms, "req_per_fire": res.api_requests_per_fire,
             "cpu_op": res.cpu_s_operator, "cpu_api": res.cpu_s_apiserver,
-            "shard_rss": max(res.operator_maxrss_mib or [0.0])}
+            "shard_rss": max(res.operator_maxrss_mib or [0.0]), "shard_end_rss": max(res.operator_rss_mib or [0.0])}
 
     # the shipped default: one operator process (untimed for the headline, like the baseline)
     if a.single_process == "measure" and a.transport == "http":
@@ -477,9 +476,11 @@ def main() -> int:
             # fake apiserver's speed; and how busy that fixture was (CPU s / wall s, max rank)
             "operator_cpu_ms_per_fire": round(sum(r["cpu_op"] for r in allr) * 1000 / fires, 4),
             "apiserver_busy_frac": round(max(r["cpu_api"] / r["elapsed_s"] for r in allr), 3),
-            # peak resident memory of the largest operator shard process (0: the operator ran in
-            # the bench process itself)
+            # peak resident memory (VmHWM) of the largest operator shard process (0: the operator
+            # ran in the bench process itself)
             "operator_shard_peak_rss_mib": round(max(r.get("shard_rss", 0.0) for r in allr), 1),
+            # ... and the largest shard's resident size at the end of the run (peak >= end)
+            "operator_shard_end_rss_mib": round(max(r.get("shard_end_rss", 0.0) for r in allr), 1),
             "baseline_value": round(base_value, 2) if base_value else None,
             "baseline_source": base_src,
             "baseline_p50_schedule_to_create_ms": round(max(r["ref_p50"] for r in allr), 2)

@@ -209,7 +209,19 @@ def _mem_dump(tag: str, mgr, rec) -> None:
 
 
 def _maxrss_mib() -> float:
-    return resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024
+    """Peak resident size: the kernel's high-water mark ``VmHWM`` (``/proc/self/status``), never
+    below the resident size now.  ``ru_maxrss`` read below the same moment's ``statm`` RSS on the
+    box (round-5 verdict: a "peak" under the end RSS), so it is only the fallback."""
+    hwm = 0.0
+    try:
+        with open("/proc/self/status") as fh:
+            for line in fh:
+                if line.startswith("VmHWM:"):
+                    hwm = int(line.split()[1]) / 1024  # kB
+                    break
+    except (OSError, ValueError, IndexError):
+        hwm = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss / 1024
+    return max(hwm, _rss_mib())
 
 
 def _rss_mib() -> float:

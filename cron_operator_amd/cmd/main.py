@@ -74,8 +74,10 @@ def _processes(v: str) -> int:
         raise argparse.ArgumentTypeError(f"invalid --shard-processes {v!r} (an integer or 'auto')") from None
 
 
-# client sizing (docs/operations.md "Sizing qps"): ~4 requests per Cron fire, so 150 QPS carries
-# 2250 minutely Crons at 100% of the budget and 1000 at 45%; the burst absorbs a tick's first
+# client sizing (docs/operations.md "Sizing qps"): ~4 requests per Cron fire.  Measured at 150 /
+# 300 (profiles/chart_defaults_mi355x_box_r5.json): 1000 minutely Crons take 28.7 s of each 60 s
+# tick, p50 tick->create 1.35 s; 2000 take 57.4 s, p50 4.7 s -- one slow tick from collapse, so
+# `preflight` warns past 80% of the minute (~1800 Crons).  The burst absorbs a tick's first
 # CREATEs.  The reference ships 30 / 50 (start.go:218-219), which tops out near 450 Crons.
 DEFAULT_QPS = 150.0
 DEFAULT_BURST = 300
@@ -166,6 +168,10 @@ def build_parser() -> argparse.ArgumentParser:
     st.add_argument("--trace-sample-rate", type=float, default=1.0, help="Fraction of reconciles traced.")
     _add_bool(st, "--enable-profiling", False, "Serve a CPU profile of the event loop at "
                                               "/debug/profile?seconds=N on the probe port.")
+    st.add_argument("--debug-views", choices=["local", "all", "off"], default="local",
+                    help="Who may read the probe port's /debug views (/debug/caches, /debug/tasks, "
+                         "/debug/traces, /debug/profile): local (default) -- loopback clients only, e.g. "
+                         "kubectl port-forward; all -- any client (cover the port with a NetworkPolicy); off.")
 
     fa = sub.add_parser("fake-apiserver", help="Serve the in-process fake Kubernetes API server over HTTP")
     fa.add_argument("--bind-address", default="127.0.0.1")
@@ -272,8 +278,8 @@ async def run_start(a: argparse.Namespace) -> int:
                            metrics_bind_address=a.metrics_bind_address, secure_metrics=a.metrics_secure,
                            metrics_cert_path=a.metrics_cert_path, metrics_cert_name=a.metrics_cert_name,
                            metrics_cert_key=a.metrics_cert_key,
-                           health_probe_bind_address=a.health_probe_bind_address, enable_http2=a.enable_http2,
-                           max_concurrent_reconciles=a.max_concurrent_reconciles,
+                           health_probe_bind_address=a.health_probe_bind_address, debug_views=a.debug_views,
+                           enable_http2=a.enable_http2, max_concurrent_reconciles=a.max_concurrent_reconciles,
                            sync_period=sync_period, shard_index=a.shard_index, shard_count=a.shard_count,
                            shard_routing=a.shard_routing)
     try:
@@ -346,7 +352,8 @@ async def run_supervisor(a: argparse.Namespace, argv: List[str]) -> int:
         metrics = MetricsServer(a.metrics_bind_address, secure=a.metrics_secure, cert_dir=a.metrics_cert_path,
                                 cert_name=a.metrics_cert_name, key_name=a.metrics_cert_key, client=client,
                                 enable_http2=a.enable_http2)
-    sup = Supervisor(argv, a.shard_processes, a.shard_count, a.shard_index, metrics, a.health_probe_bind_address)
+    sup = Supervisor(argv, a.shard_processes, a.shard_count, a.shard_index, metrics, a.health_probe_bind_address,
+                     a.debug_views)
     log.info("starting shard processes", processes=a.shard_processes,
              shards=[c.index for c in sup.children], shardCount=a.shard_count * a.shard_processes)
     try:

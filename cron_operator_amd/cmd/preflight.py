@@ -15,7 +15,8 @@ It also sizes the client budget (``--qps`` / ``--burst``, the chart's defaults u
 from the schedules it parses it finds the busiest minute of the next day and warns when that
 minute's fires x :data:`REQUESTS_PER_FIRE` exceed a minute of ``--qps`` -- ticks then
 collapse and runs are lost without an error (the reference's catch-up runs only the last
-missed tick, ``internal/controller/cron_controller.go:408-436``) -- or when its fires exceed
+missed tick, ``internal/controller/cron_controller.go:408-436``) -- or already past
+:data:`TICK_WORK_WARN_FRAC` of it (one slow tick from that cliff), or when its fires exceed
 ``--burst`` (the last CREATEs land (fires - burst) / qps seconds after the tick).  An upgrade
 that keeps the reference's ``qps: 30`` (``/root/reference/cmd/operator/start.go:218-219``)
 collapses ticks from about 450 minutely Crons.
@@ -42,6 +43,12 @@ LEASES = GroupVersionResource("coordination.k8s.io", "v1", "leases")
 # api_requests_per_fire / deployment_api_requests_per_fire, realistic job lifecycle: 4.0)
 REQUESTS_PER_FIRE = 4.0
 HORIZON_MINUTES = 24 * 60  # the busiest minute is looked for over the next day
+# warn before the cliff: the busiest minute's tick work (its fires' requests at --qps) may take at
+# most this share of the minute.  Measured at chart defaults (qps 150 / burst 300, TLS + the etcd
+# latency model, realistic job lifecycle): 1000 minutely Crons take 28.7 s of each 60 s tick, p50
+# tick->create 1.35 s; 2000 take 57.4 s, p50 4.7 s -- one slow tick from collapse
+# (profiles/chart_defaults_mi355x_box_r5.json; docs/benchmarks.md "the chart as installed")
+TICK_WORK_WARN_FRAC = 0.8
 
 
 @dataclass
@@ -96,7 +103,11 @@ def peak_fires(schedules: List[Any], now: Any, engine: Any = None,
                horizon_minutes: int = HORIZON_MINUTES) -> Tuple[int, Any]:
     """(most fires in one minute over the next ``horizon_minutes``, that minute's start).  A
     schedule fires at most once a minute (seconds are fixed at 0), so each contributes at
-    most ``horizon_minutes`` ticks."""
+    most ``horizon_minutes`` ticks.
+
+    ``schedules``: parsed schedules, or ``(schedule, how many Crons use it)`` pairs.  A fleet
+    shares a few schedule strings, so each distinct one is walked once and its ticks counted
+    with its multiplicity (10,000 Crons of 3 schedules: ~4,300 ``next`` calls, not 14 million)."""
     from collections import Counter
 
     from ..cron.engine import default_engine
@@ -105,13 +116,14 @@ def peak_fires(schedules: List[Any], now: Any, engine: Any = None,
     eng = engine or default_engine()
     end = now.sec + horizon_minutes * 60
     per_minute: Counter = Counter()
-    for sched in schedules:
+    for item in schedules:
+        sched, mult = item if isinstance(item, tuple) else (item, 1)
         t = now
         for _ in range(horizon_minutes + 1):
             t = eng.next(sched, t)
             if t.is_zero() or t.sec > end:
                 break
-            per_minute[t.sec // 60] += 1
+            per_minute[t.sec // 60] += mult
     if not per_minute:
         return 0, None
     minute, n = max(per_minute.items(), key=lambda kv: (kv[1], -kv[0]))
@@ -128,6 +140,13 @@ def budget_warnings(fires: int, qps: float, burst: int, requests_per_fire: float
         out.append(f"the busiest minute has {fires} fires x {requests_per_fire:g} API requests = {need:.0f} QPS, "
                    f"more than --qps {qps:g}: ticks collapse and scheduled runs are lost; set qps >= "
                    f"{need:.0f} (helm: qps), or shard the fleet (sharding.count)")
+    elif need > TICK_WORK_WARN_FRAC * qps:
+        work = fires * requests_per_fire / qps
+        out.append(f"the busiest minute's {fires} fires need about {work:.0f} s of the 60 s minute at --qps "
+                   f"{qps:g} ({100 * work / 60:.0f}%, over {100 * TICK_WORK_WARN_FRAC:.0f}%): one slow tick "
+                   f"from collapse (measured: 2000 minutely Crons at the chart's defaults take 57.4 s per "
+                   f"tick); set qps >= {need / TICK_WORK_WARN_FRAC:.0f} (helm: qps), or shard the fleet "
+                   f"(sharding.count)")
     if fires > burst:
         # the tick's first `burst` CREATEs go out at once, the rest at qps (the tick reserve keeps
         # the whole burst for them)
@@ -165,7 +184,9 @@ async def preflight(client: "Client", namespace: str = "", rules: Optional[List[
         from ..utils.clock import RealClock
 
         now = RealClock().now(LOCAL)
-    scheds: List[Any] = []
+    from collections import Counter
+
+    sched_counts: Counter = Counter()  # schedule string -> Crons that fire on it
     for c in crons:
         m = c.get("metadata") or {}
         key = f"{m.get('namespace', '')}/{m.get('name', '')}"
@@ -184,10 +205,7 @@ async def preflight(client: "Client", namespace: str = "", rules: Optional[List[
                 except ValueError:
                     past = False
             if not spec.get("suspend") and not past:
-                try:
-                    scheds.append(engine.parse(sched))
-                except ScheduleError:
-                    pass
+                sched_counts[sched] += 1
         wl = (spec.get("template") or {}).get("workload")
         try:
             gvk = get_workload_gvk(wl)
@@ -209,6 +227,12 @@ async def preflight(client: "Client", namespace: str = "", rules: Optional[List[
             continue
         kr.served, kr.resource = True, gvr.resource
         kr.missing_verbs = rbac_missing(gvk.group, gvr.resource, rules)
+    scheds: List[Tuple[Any, int]] = []
+    for sched, n in sched_counts.items():  # each distinct schedule (its CRON_TZ= included) once
+        try:
+            scheds.append((engine.parse(sched), n))
+        except ScheduleError:
+            pass
     if qps > 0 and scheds:
         rep.peak_fires_per_minute, peak = peak_fires(scheds, now, engine)
         rep.peak_minute = peak.rfc3339() if peak is not None else ""

@@ -93,6 +93,12 @@ def unassigned_selector(count: int) -> str:
 _KEPT_METADATA = ("name", "namespace", "uid", "resourceVersion", "labels")
 
 
+def persistent_failure(e: errors.ApiError) -> bool:
+    """A refusal that retrying will not change: a 4xx other than 404 (gone: nothing to label),
+    409 (a racing write: retry), 429 (throttled: retry).  5xx and transport errors are transient."""
+    return 400 <= e.code < 500 and e.code not in (404, 409, 429)
+
+
 def metadata_only(obj: Dict[str, Any]) -> Dict[str, Any]:
     """Informer transform for the unassigned watches: assignment reads only names and labels.
     Before the first assignment (a fresh install, or a new shard count) those watches hold
@@ -147,6 +153,8 @@ class ShardAssigner:
         # for good; a later event on the child offers it again
         self.max_child_attempts = max(1, max_child_attempts)
         self._attempts: Dict[Tuple[GroupVersionKind, str, str], int] = {}
+        # failures of any kind per key (retry backoff), persistent or not
+        self._failures: Dict[Tuple[GroupVersionKind, str, str], int] = {}
         self.abandoned = 0
         self._child_kinds: Set[GroupVersionKind] = set()
         # (namespace, cron) -> child keys queued for labelling / labelled but maybe not observed yet
@@ -272,36 +280,45 @@ class ShardAssigner:
                 if not errors.is_not_found(e):
                     self.errors += 1
                     self.log.error(e, "Failed to assign shard", kind=gvk.kind, namespace=ns, name=name)
-                    await asyncio.sleep(self.retry_delay)
+                    await asyncio.sleep(self._backoff(key))
                     inf = self.informers.get(gvk)
+                    # only a persistent refusal counts toward giving a child up (403, a webhook's
+                    # 422): throttling (429), conflicts and server errors are retried for as long
+                    # as they last -- a child given up on is invisible to its shard's informer
                     if inf is not None and inf.get(ns, name, copy=False) is not None \
-                            and not (child and self._give_up(key)):
+                            and not (child and persistent_failure(e) and self._give_up(key)):
                         self._queue.put_nowait(key)  # still unassigned: retry
                         continue
                 if child:
                     self._child_finished(key, False)
-                self._attempts.pop(key, None)
-                self._queued.discard(key)
+                self._forget(key)
                 continue
-            except Exception as e:  # noqa: BLE001 - transport errors: retry later
+            except Exception as e:  # noqa: BLE001 - transport errors: retry, never give up
                 self.errors += 1
                 self.log.error(e, "Failed to assign shard", kind=gvk.kind, namespace=ns, name=name)
-                await asyncio.sleep(self.retry_delay)
-                if child and self._give_up(key):
-                    self._child_finished(key, False)
-                    self._attempts.pop(key, None)
-                    self._queued.discard(key)
-                    continue
+                await asyncio.sleep(self._backoff(key))
                 self._queue.put_nowait(key)
                 continue
             if child:
                 self._child_finished(key, True)
-            self._attempts.pop(key, None)
-            self._queued.discard(key)
+            self._forget(key)
+
+    def _backoff(self, key: Tuple[GroupVersionKind, str, str]) -> float:
+        """Seconds to wait before retrying ``key``'s label PATCH: ``retry_delay`` doubled per
+        failure of that key, capped at 32x (a long apiserver outage is not hammered)."""
+        n = self._failures.get(key, 0)
+        self._failures[key] = n + 1
+        return self.retry_delay * (1 << min(n, 5))
+
+    def _forget(self, key: Tuple[GroupVersionKind, str, str]) -> None:
+        self._attempts.pop(key, None)
+        self._failures.pop(key, None)
+        self._queued.discard(key)
 
     def _give_up(self, key: Tuple[GroupVersionKind, str, str]) -> bool:
-        """Count a failed label PATCH of child ``key``; True once it reached ``max_child_attempts``
-        (the caller then releases the child's Cron, which is assigned without it)."""
+        """Count a persistently refused label PATCH of child ``key``; True once it reached
+        ``max_child_attempts`` (the caller then releases the child's Cron, which is assigned
+        without it)."""
         n = self._attempts.get(key, 0) + 1
         if n < self.max_child_attempts:
             self._attempts[key] = n

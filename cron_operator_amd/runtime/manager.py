@@ -56,6 +56,8 @@ class ManagerOptions:
     metrics_cert_name: str = "tls.crt"
     metrics_cert_key: str = "tls.key"
     health_probe_bind_address: str = ":8081"
+    # which clients the probe port's /debug views answer: local (loopback only), all, off
+    debug_views: str = "local"
     enable_http2: bool = False
     max_concurrent_reconciles: int = 10
     cache_sync_timeout: float = 120.0
@@ -90,7 +92,7 @@ class Manager:
         self.broadcaster = Broadcaster(client, self.clock)
         self.controllers: List[Controller] = []
         self.runnables: List[Callable[[], Awaitable[None]]] = []
-        self.probes = ProbeServer(self.opts.health_probe_bind_address)
+        self.probes = ProbeServer(self.opts.health_probe_bind_address, self.opts.debug_views)
         self.probes.debug["caches"] = self.cache_view
         self.metrics_server = MetricsServer(self.opts.metrics_bind_address, self.opts.secure_metrics,
                                             self.opts.metrics_cert_path, self.opts.metrics_cert_name,

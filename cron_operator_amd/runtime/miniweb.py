@@ -30,14 +30,16 @@ class Request:
     """What a handler reads: method, path, query, headers (lower-case names) and the values
     of a ``{name}`` route segment (``match_info``)."""
 
-    __slots__ = ("method", "path", "query", "headers", "match_info")
+    __slots__ = ("method", "path", "query", "headers", "match_info", "peer")
 
-    def __init__(self, method: str, path: str, query: Dict[str, str], headers: Dict[str, str]):
+    def __init__(self, method: str, path: str, query: Dict[str, str], headers: Dict[str, str],
+                 peer: str = ""):
         self.method = method
         self.path = path
         self.query = query
         self.headers = _Headers(headers)
         self.match_info: Dict[str, str] = {}
+        self.peer = peer  # the client's IP address ("" when unknown)
 
 
 class _Headers(dict):
@@ -185,7 +187,9 @@ class _Conn(asyncio.Protocol):
             self.timer = None
         keep = version == "HTTP/1.1" and headers.get("connection", "").lower() != "close"
         path, _, qs = target.partition("?")
-        req = Request(method, unquote(path), dict(parse_qsl(qs, keep_blank_values=True)), headers)
+        peer = self.t.get_extra_info("peername") if self.t is not None else None
+        req = Request(method, unquote(path), dict(parse_qsl(qs, keep_blank_values=True)), headers,
+                      peer[0] if isinstance(peer, tuple) and peer else "")
         self.busy = True
         self.task = asyncio.get_running_loop().create_task(self._serve(req, keep))
 

@@ -18,6 +18,7 @@ from __future__ import annotations
 
 import asyncio
 import collections
+import math
 import os
 import signal
 import threading
@@ -119,6 +120,8 @@ async def cpu_profile(seconds: float, interval: float = 0.001, top: int = 40) ->
     global _running
     if _running is not None:
         raise RuntimeError("a profile is already running")
+    if not math.isfinite(seconds):
+        raise ValueError(f"seconds must be finite, not {seconds!r}")
     seconds = min(max(seconds, 0.1), MAX_SECONDS)
     s = Sampler(interval)
     s.enable()

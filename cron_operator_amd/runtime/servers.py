@@ -8,7 +8,11 @@
   ``/debug/<name>`` views registered by the manager and the controller (``/debug/caches``: the
   objects each informer holds and the process's memory; ``/debug/wire-memo``), ``/debug/tasks``
   (live asyncio tasks by where they wait) and, with ``--enable-profiling``, ``/debug/profile``
-  (a CPU profile of the loop thread; :mod:`.profiler`).
+  (a CPU profile of the loop thread; :mod:`.profiler`).  The ``/debug`` views expose internals
+  (object keys, await chains with source lines), unlike the probes: by default
+  (``--debug-views=local``) they answer only clients on the loopback interface (``kubectl
+  port-forward``, ``kubectl exec ... curl localhost``) and 403 everyone else; ``all`` serves
+  any client (put the probe port behind a NetworkPolicy), ``off`` none.
 * Metrics: ``/metrics`` in Prometheus text format.  ``--metrics-secure`` (default
   true, ``start.go:226``) serves HTTPS and guards the endpoint with the
   authn/authz filter: the bearer token is checked with a TokenReview and the
@@ -22,6 +26,7 @@ Both run on :mod:`.miniweb` (asyncio, HTTP/1.1), not a web framework.
 from __future__ import annotations
 
 import asyncio
+import math
 import os
 import ssl
 import subprocess
@@ -74,8 +79,25 @@ def _render(checks: Dict[str, Check], kind: str, verbose: bool) -> Tuple[int, st
     return 200, "ok"
 
 
+DEBUG_VIEWS = ("local", "all", "off")
+
+
+def is_loopback(addr: str) -> bool:
+    import ipaddress
+
+    try:
+        ip = ipaddress.ip_address(addr.split("%", 1)[0])
+    except ValueError:
+        return False
+    mapped = getattr(ip, "ipv4_mapped", None)
+    return (mapped or ip).is_loopback
+
+
 class ProbeServer:
-    def __init__(self, bind: str):
+    def __init__(self, bind: str, debug_views: str = "local"):
+        if debug_views not in DEBUG_VIEWS:
+            raise ValueError(f"debug_views must be one of {DEBUG_VIEWS}, not {debug_views!r}")
+        self.debug_views = debug_views
         self.bind = bind
         self.healthz: Dict[str, Check] = {}
         self.readyz: Dict[str, Check] = {}
@@ -99,6 +121,17 @@ class ProbeServer:
                 return web.Response(status=code, text=body)
             return h
 
+        def guarded(h):
+            """A /debug view: served to the clients ``debug_views`` allows, 403 to the others."""
+            async def g(req: web.Request) -> web.Response:
+                if self.debug_views == "off":
+                    return web.Response(status=404, text="debug views disabled (--debug-views=off)\n")
+                if self.debug_views == "local" and not is_loopback(req.peer):
+                    return web.Response(status=403, text="debug views are served to loopback clients only "
+                                                         "(--debug-views=local); use kubectl port-forward\n")
+                return await h(req)
+            return g
+
         app.add_get("/healthz", handler(self.healthz, "healthz"))
         app.add_get("/healthz/{check}", handler(self.healthz, "healthz"))
         app.add_get("/readyz", handler(self.readyz, "readyz"))
@@ -114,7 +147,7 @@ class ProbeServer:
                 return web.json_response({"spans": t.spans()})
             return web.json_response(t.chrome_trace())
 
-        app.add_get("/debug/traces", traces)
+        app.add_get("/debug/traces", guarded(traces))
 
         async def tasks(req: web.Request) -> web.Response:
             from . import profiler
@@ -129,14 +162,16 @@ class ProbeServer:
             try:
                 seconds = float(req.query.get("seconds", "10"))
             except ValueError:
-                return web.Response(status=400, text="seconds: a number\n")
+                seconds = math.nan
+            if not math.isfinite(seconds):  # nan/inf would corrupt the loop's timer heap
+                return web.Response(status=400, text="seconds: a finite number\n")
             try:
                 return web.Response(text=await profiler.cpu_profile(seconds))
             except RuntimeError as e:
                 return web.Response(status=409, text=f"{e}\n")
 
-        app.add_get("/debug/tasks", tasks)
-        app.add_get("/debug/profile", profile)
+        app.add_get("/debug/tasks", guarded(tasks))
+        app.add_get("/debug/profile", guarded(profile))
 
         async def debug(req: web.Request) -> web.Response:
             fn = self.debug.get(req.match_info["name"])
@@ -144,7 +179,7 @@ class ProbeServer:
                 return web.Response(status=404, text=f"no such debug view; have: {', '.join(sorted(self.debug))}\n")
             return web.json_response(fn())
 
-        app.add_get("/debug/{name}", debug)
+        app.add_get("/debug/{name}", guarded(debug))
         return app
 
     async def start(self) -> None:

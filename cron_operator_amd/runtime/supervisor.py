@@ -184,7 +184,7 @@ class _Child:
 
 class Supervisor:
     def __init__(self, argv: List[str], processes: int, shard_count: int, shard_index: int,
-                 metrics: Optional[MetricsServer], probe_bind: str):
+                 metrics: Optional[MetricsServer], probe_bind: str, debug_views: str = "local"):
         self.log = get_logger("supervisor")
         total = shard_count * processes
         self.children = [
@@ -193,7 +193,7 @@ class Supervisor:
                     f"--shard-index={shard_index * processes + i}"])
             for i in range(processes)]
         self.metrics = metrics
-        self.probes = ProbeServer(probe_bind)
+        self.probes = ProbeServer(probe_bind, debug_views)
         self.probes.healthz["children"] = self._alive
         self._ready: Dict[int, bool] = {}
         self.probes.readyz["children"] = self._all_ready

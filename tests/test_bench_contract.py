@@ -9,6 +9,8 @@ import socket
 import subprocess
 import sys
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
         "vs_baseline", "dtype", "data", "config"}
@@ -40,7 +42,9 @@ def test_single_rank_line():
     # operator cost, separated from the fake apiserver fixture
     assert d["operator_cpu_ms_per_fire"] > 0
     assert 0 < d["apiserver_busy_frac"] < 2
-    assert 10 < d["operator_shard_peak_rss_mib"] < 1024  # the largest shard process's peak
+    assert 10 < d["operator_shard_peak_rss_mib"] < 1024  # the largest shard process's peak (VmHWM)
+    # round-5 verdict: the "peak" (ru_maxrss) read below the end RSS; a high-water mark cannot
+    assert 10 < d["operator_shard_end_rss_mib"] <= d["operator_shard_peak_rss_mib"]
     # the denominator is the reference algorithm measured by this same invocation
     assert d["baseline_source"].startswith("measured")
     assert d["baseline_value"] > 0 and d["baseline_p50_schedule_to_create_ms"] > 0
@@ -139,3 +143,77 @@ def test_payload_probe_runs_the_ddp_payload_as_a_clean_child_job(monkeypatch):
     assert r["allreduce"]["mb"] == 1 and r["allreduce"]["busbw_gbs"] > 0
     slow = bench._payload_probe(2, 0.5, cpu=True, allreduce_mb=1, steps=2)
     assert slow.get("error", "").startswith("timed out"), slow
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.slow
+def test_eight_ranks_the_drivers_line_shape():
+    """Round-5 verdict #7: the driver's N=8 invocation shape on the CPU (gloo), before any 8-GPU
+    node runs it: 8 ranks under ``torch.distributed.run``, each its own 200-Cron deployment; the
+    shards per rank are chosen from the CPUs the job may use (never oversubscribed); rank 0 prints
+    one line with the whole-job aggregate; the payload probe (``--payload-probe cpu``) runs the
+    8-process DDP child job over gloo while the other ranks wait at the barrier."""
+    from cron_operator_amd.runtime.supervisor import available_cpus
+
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "8",
+                        "--steps", "2", "--warmup", "1", "--crons", "200", "--payload-probe", "cpu"], cwd=ROOT,
+                       env=_env(), capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_line(r.stdout)  # rank 0 only
+    shards = max(1, min(3, available_cpus() // 8 - 1))
+    assert d["n_gpus"] == 8 and d["config"]["global_batch"] == 1600
+    assert d["config"]["operator_shards"] == shards and d["config"]["parallelism"] == f"ranks8x{shards}shards"
+    # aggregate: 8 ranks' fires over the slowest rank's timed window
+    assert abs(d["value"] - 1600 * 2 / (d["ms_per_step"] * 2 / 1000)) / d["value"] < 0.01
+    assert d["api_requests_per_fire"] == 4.0 and d["baseline_value"] > 0
+    assert d["deployment_value"] > 0 and d["deployment_baseline_value"] > 0
+    probe = d["payload_ddp"]
+    assert probe.get("ok") is True and probe["world"] == 8 and probe["backend"] == "gloo", probe
+    assert probe["distinct_devices"] == 8 and probe["allreduce"]["busbw_gbs"] > 0, probe
+
+
+@pytest.mark.slow
+def test_a_killed_rank_fails_the_eight_rank_job_without_a_hang():
+    """One rank of the 8 dies mid-run (SIGKILL, as an OOM kill would): the launcher tears the
+    others down and the job exits non-zero well inside the limit -- no rank waits forever at a
+    barrier for the dead one."""
+    import signal
+    import time
+
+    import psutil
+
+    p = subprocess.Popen([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "8",
+                          "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "8",
+                          "--steps", "400", "--warmup", "1", "--crons", "100", "--baseline", "none",
+                          "--deployment", "none", "--payload-probe", "none"], cwd=ROOT, env=_env(),
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, start_new_session=True)
+    try:
+        victim = None
+        t0 = time.monotonic()
+        while victim is None and time.monotonic() - t0 < 120:
+            ranks = [c for c in psutil.Process(p.pid).children()
+                     if "bench.py" in " ".join(c.cmdline()) and c.environ().get("RANK") == "5"]
+            if ranks:
+                victim = ranks[0]
+            time.sleep(0.5)
+        assert victim is not None, "rank 5 never started"
+        time.sleep(8)  # past setup: the ranks are stepping, at or between barriers
+        assert p.poll() is None, "the job ended before the kill"
+        victim.send_signal(signal.SIGKILL)
+        t_kill = time.monotonic()
+        out, err = p.communicate(timeout=240)
+        assert p.returncode != 0, err[-2000:]
+        took = time.monotonic() - t_kill
+        assert took < 240
+        print(f"job ended {took:.1f} s after the kill, rc={p.returncode}")
+        assert not [ln for ln in out.splitlines() if ln.startswith("{")]  # no partial line reported
+    finally:
+        if p.poll() is None:
+            os.killpg(p.pid, signal.SIGKILL)
+            p.wait()

@@ -153,7 +153,7 @@ async def test_reference_client_budget_collapses_ticks_at_the_same_fleet():
     assert missing, "expected collapsed ticks at the reference's qps 30 / burst 50"
 
 
-CLAIMED = 2250  # the fleet values.yaml's qps comment claims at 100% of the budget (N/15 QPS)
+CLAIMED = 2250  # the fleet at 100% of the chart's budget (N/15 QPS); values.yaml sizes for 80% of it
 
 
 async def test_leader_keeps_the_lease_at_twice_the_claimed_fleet():

@@ -667,3 +667,61 @@ async def test_shard_assigner_gives_up_a_child_it_may_not_label():
         task.cancel()
         await asyncio.gather(task, return_exceptions=True)
         await cache.stop()
+
+
+async def test_shard_assigner_keeps_retrying_a_child_through_transient_errors():
+    """503s (and 429s) are transient -- a child whose label PATCH fails with them more
+    than ``max_child_attempts`` times is NOT given up, so its Cron stays parked until the child is
+    labelled (a given-up child is invisible to its shard's label-selected child informer)."""
+    from cron_operator_amd.api import errors as api_errors
+    from cron_operator_amd.api.meta import GroupVersionKind
+    from cron_operator_amd.api.v1alpha1 import CRON_GVK
+    from cron_operator_amd.controller.sharding import LABEL_SHARD, ShardAssigner, persistent_failure
+    from cron_operator_amd.runtime.informer import Cache
+
+    assert not persistent_failure(api_errors.ApiError(503, "ServiceUnavailable", "x"))
+    assert not persistent_failure(api_errors.ApiError(429, "TooManyRequests", "x"))
+    assert not persistent_failure(api_errors.ApiError(409, "Conflict", "x"))
+    assert persistent_failure(api_errors.ApiError(403, "Forbidden", "x"))
+    assert persistent_failure(api_errors.ApiError(422, "Invalid", "x"))
+
+    env = TestEnv()
+    await env.create_cron(new_cron("t0", NS, "*/1 * * * *", PT_TMPL))
+    env.server.create(PT, NS, {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+                               "metadata": {"name": "t0-1", "labels": {LABEL_CRON_NAME: "t0"}},
+                               "spec": {"pytorchReplicaSpecs": {"Master": {"replicas": 1}}}})
+    client = env.new_client()
+    orig = client.patch
+    failed = []
+
+    async def patch(gvk, ns, name, *a, **kw):
+        if (getattr(gvk, "kind", "") == "PyTorchJob") and len(failed) < 8:
+            failed.append(name)
+            if len(failed) % 2:
+                raise api_errors.ApiError(503, "ServiceUnavailable", "apiserver is shutting down")
+            raise ConnectionResetError("connection reset by peer")
+        return await orig(gvk, ns, name, *a, **kw)
+
+    client.patch = patch  # type: ignore[assignment]
+    cache = Cache(env.new_client(), NS)
+    asg = ShardAssigner(client, 0, 1, retry_delay=0.001, max_child_attempts=3)
+    asg._backoff = lambda key: 0.001  # no exponential wait in the test
+    await asg.watch(cache, CRON_GVK, child=False)
+    await asg.watch(cache, GroupVersionKind("kubeflow.org", "v1", "PyTorchJob"), child=True)
+    cache.start()
+    task = asyncio.get_running_loop().create_task(asg.run())
+    try:
+        for _ in range(500):
+            if LABEL_SHARD in (env.server.get(CRON_GVR, NS, "t0")["metadata"].get("labels") or {}):
+                break
+            # parked while the child's PATCH keeps failing
+            if len(failed) < 8:
+                assert LABEL_SHARD not in (env.server.get(CRON_GVR, NS, "t0")["metadata"].get("labels") or {})
+            await asyncio.sleep(0.01)
+        assert len(failed) == 8 and asg.abandoned == 0
+        assert LABEL_SHARD in (env.server.get(PT, NS, "t0-1")["metadata"].get("labels") or {})
+        assert LABEL_SHARD in (env.server.get(CRON_GVR, NS, "t0")["metadata"].get("labels") or {})
+    finally:
+        task.cancel()
+        await asyncio.gather(task, return_exceptions=True)
+        await cache.stop()

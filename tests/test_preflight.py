@@ -169,5 +169,55 @@ def test_preflight_budget_math():
     assert len(budget_warnings(1000, 150, 300)) == 1   # within the QPS budget, beyond the burst
     assert budget_warnings(200, 150, 300) == []
     assert len(budget_warnings(2300, 150, 300)) == 2   # 2300 x 4 / 60 = 153 QPS > 150
+    assert not any("one slow tick" in w for w in budget_warnings(2300, 150, 300))  # the collapse warning instead
     # the median CREATE of 1000 due together: (500 - 300) / 150 = 1.3 s (the box measured 1.35 s)
     assert "the median lands about 1.3 s and the last about 4.7 s" in budget_warnings(1000, 150, 300)[0]
+
+
+async def test_preflight_warns_before_the_cliff_at_chart_defaults():
+    """Round-5 verdict #6: at the chart's defaults (qps 150 / burst 300) 2000 minutely Crons took
+    57.4 s of every 60 s tick on the box -- under the 100% budget, yet one slow tick from collapse.
+    Preflight warns once the busiest minute needs more than 80% of the minute; 1000 Crons (28.7 s
+    measured) get no such warning."""
+    from cron_operator_amd.api.v1alpha1 import new_cron
+    from cron_operator_amd.cmd.main import DEFAULT_BURST, DEFAULT_QPS
+    from cron_operator_amd.cmd.preflight import TICK_WORK_WARN_FRAC
+    from cron_operator_amd.utils.gotime import UTC
+
+    assert TICK_WORK_WARN_FRAC == 0.8
+    tmpl = {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob", "spec": {}}
+    reports = {}
+    for n in (1000, 2000):
+        env = TestEnv()
+        for i in range(n):
+            env.server.create(CRON_GVR, NS, new_cron(f"m{i:04d}", NS, "* * * * *", tmpl).to_dict())
+        reports[n] = await preflight(env.client, NS, qps=DEFAULT_QPS, burst=DEFAULT_BURST, now=env.clock.now(UTC))
+    cliff = [w for w in reports[2000].budget_warnings if "one slow tick" in w]
+    assert len(cliff) == 1 and "about 53 s of the 60 s minute" in cliff[0] and "(89%" in cliff[0], cliff
+    assert not any("ticks collapse" in w for w in reports[2000].budget_warnings)
+    assert not any("one slow tick" in w for w in reports[1000].budget_warnings), reports[1000].budget_warnings
+    assert "warning: the busiest minute's 2000 fires need about 53 s" in render(reports[2000])
+
+
+def test_peak_fires_walks_each_distinct_schedule_once():
+    """a fleet shares a few schedules; peak_fires counts each distinct one once, with
+    its multiplicity, instead of calling next() ~1441 times per Cron."""
+    from cron_operator_amd.cmd.preflight import peak_fires
+    from cron_operator_amd.cron.engine import default_engine
+    from cron_operator_amd.utils.gotime import UTC, GoTime
+
+    eng = default_engine()
+    calls = [0]
+
+    class Counting:
+        name = "counting"
+
+        def next(self, sched, t):
+            calls[0] += 1
+            return eng.next(sched, t)
+
+    now = GoTime(1767268800, 0, UTC)
+    minutely, nightly = eng.parse("* * * * *"), eng.parse("0 3 * * *")
+    n, _ = peak_fires([(minutely, 9999), (nightly, 1)], now, Counting())
+    assert n == 10000 and calls[0] < 1500
+    assert peak_fires([minutely] * 3 + [nightly], now, eng)[0] == 4  # plain schedules still count once each

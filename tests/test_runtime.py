@@ -499,6 +499,11 @@ async def test_debug_tasks_and_the_opt_in_cpu_profile():
                 assert "samples over" in text and "## by self samples" in text and "(busy)" in text
                 async with s.get(base + "/debug/profile?seconds=x") as r:
                     assert r.status == 400
+                for bad in ("nan", "inf", "-inf", "NaN"):  # a NaN timer corrupts the loop's heap
+                    async with s.get(base + f"/debug/profile?seconds={bad}") as r:
+                        assert r.status == 400, bad
+                with pytest.raises(ValueError):
+                    await profiler.cpu_profile(float("nan"))
             finally:
                 profiler.allow(False)
     finally:
@@ -839,3 +844,34 @@ def test_free_port_is_free_and_below_the_ephemeral_range():
         assert 1024 < p and (p < low or low - 15000 < 1000)
         with socket.socket() as s:
             s.bind(("127.0.0.1", p))  # still free
+
+
+async def test_debug_views_answer_only_loopback_clients_by_default():
+    """the probe port's /debug views expose internals; by default (--debug-views=local)
+    only loopback clients get them, the probes themselves stay open to the kubelet."""
+    from cron_operator_amd.runtime import miniweb
+    from cron_operator_amd.runtime.servers import is_loopback
+
+    assert is_loopback("127.0.0.1") and is_loopback("::1") and is_loopback("::ffff:127.0.0.1")
+    assert not is_loopback("10.244.1.7") and not is_loopback("") and not is_loopback("fe80::1%eth0")
+
+    async def call(probes, path, peer):
+        h, info = probes.app().match(path)
+        req = miniweb.Request("GET", path, {}, {}, peer)
+        req.match_info = info
+        return await h(req)
+
+    local = ProbeServer("127.0.0.1:0")
+    local.debug["caches"] = lambda: {"ok": 1}
+    for path in ("/debug/tasks", "/debug/caches", "/debug/profile", "/debug/traces"):
+        assert (await call(local, path, "10.244.1.7")).status == 403, path
+    assert (await call(local, "/debug/caches", "127.0.0.1")).status == 200
+    assert (await call(local, "/healthz", "10.244.1.7")).status == 200  # the kubelet's probe
+    anyone = ProbeServer("127.0.0.1:0", debug_views="all")
+    anyone.debug["caches"] = lambda: {"ok": 1}
+    assert (await call(anyone, "/debug/caches", "10.244.1.7")).status == 200
+    off = ProbeServer("127.0.0.1:0", debug_views="off")
+    off.debug["caches"] = lambda: {"ok": 1}
+    assert (await call(off, "/debug/caches", "127.0.0.1")).status == 404
+    with pytest.raises(ValueError):
+        ProbeServer(":8081", debug_views="public")
