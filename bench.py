@@ -270,6 +270,9 @@ def main() -> int:
                     help="how shards split the watch traffic (controller/sharding.py)")
     ap.add_argument("--apiserver-latency", choices=["none", "etcd"], default="none",
                     help="server-side per-verb latency model of the fake apiserver (harness LATENCY_PROFILES)")
+    ap.add_argument("--apiserver-impl", choices=["native", "python"], default="native",
+                    help="the fake apiserver fixture: native (C++ _apiserverd, off the critical path) or python "
+                         "(apiserver/server.py + http.py, the rounds 1-5 fixture; A/B)")
     ap.add_argument("--tls", action="store_true",
                     help="the fake apiserver serves HTTPS and the operator verifies it against its CA, as "
                          "against a real cluster (every operator connection is TLS)")
@@ -327,7 +330,8 @@ def main() -> int:
                       mode=a.mode, transport=a.transport, qps=a.qps, burst=a.burst, workers=a.workers,
                       namespace=f"bench-r{rank}", shards=a.shards if a.transport == "http" else 1,
                       shard_routing=a.shard_routing, apiserver_latency=a.apiserver_latency, tls=a.tls,
-                      max_inflight=a.max_inflight, defer_writes=not a.no_defer, lifecycle=a.lifecycle)
+                      max_inflight=a.max_inflight, defer_writes=not a.no_defer, lifecycle=a.lifecycle,
+                      apiserver_impl=a.apiserver_impl)
 
     def on_step(k: int, dt: float, timed: bool) -> None:
         # bracket the K timed steps with barriers so every rank times the same window: the
@@ -361,7 +365,7 @@ def main() -> int:
                                history_limit=a.history_limit, mode=a.mode, transport=a.transport, qps=a.qps,
                                burst=a.burst, workers=a.workers, namespace=f"bench-1p-r{rank}", shards=1,
                                apiserver_latency=a.apiserver_latency, tls=a.tls, max_inflight=a.max_inflight,
-                               defer_writes=not a.no_defer, lifecycle=a.lifecycle)
+                               defer_writes=not a.no_defer, lifecycle=a.lifecycle, apiserver_impl=a.apiserver_impl)
             _barrier(dist)
             sres = run_sync(scfg)
             _barrier(dist)
@@ -379,7 +383,7 @@ def main() -> int:
         bcfg = BenchConfig(n_crons=a.crons, steps=a.baseline_steps, warmup=a.baseline_warmup,
                            history_limit=a.history_limit, mode="reference", transport=a.transport, qps=a.qps,
                            burst=a.burst, workers=a.workers, namespace=f"bench-ref-r{rank}", shards=1,
-                           tls=a.tls, lifecycle=a.lifecycle)
+                           tls=a.tls, lifecycle=a.lifecycle, apiserver_impl=a.apiserver_impl)
         _barrier(dist)
         bres = run_sync(bcfg)
         _barrier(dist)
@@ -397,7 +401,8 @@ def main() -> int:
                                transport="http", qps=a.qps, burst=a.burst, workers=a.workers,
                                max_inflight=a.max_inflight, defer_writes=not a.no_defer,
                                namespace=f"bench-{tag.replace('_', '-')}-r{rank}", shards=1,
-                               apiserver_latency="etcd", tls=True, lifecycle=a.deployment_lifecycle)
+                               apiserver_latency="etcd", tls=True, lifecycle=a.deployment_lifecycle,
+                               apiserver_impl=a.apiserver_impl)
             _barrier(dist)
             try:
                 dres = run_sync(dcfg)
@@ -467,7 +472,8 @@ def main() -> int:
                        "operator_shards": cfg.shards,
                        "shard_routing": cfg.shard_routing if cfg.shards > 1 else None,
                        "apiserver_latency": cfg.apiserver_latency,
-                       "tls": cfg.tls, "qps": cfg.qps, "job_lifecycle": cfg.lifecycle},
+                       "tls": cfg.tls, "qps": cfg.qps, "job_lifecycle": cfg.lifecycle,
+                       "apiserver_impl": cfg.apiserver_impl},
             "p50_schedule_to_create_ms": round(max(r["p50"] for r in allr), 2),
             "p99_schedule_to_create_ms": round(max(r["p99"] for r in allr), 2),
             "raw_reconciles_per_s": round(sum(r["reconciles"] for r in allr) / t_max, 2),

@@ -1,0 +1,160 @@
+"""The fake apiserver's native implementation (``ops/csrc/apiserverd.cpp``) and its test controls.
+
+:class:`~.server.APIServer` + :mod:`.http` is the envtest analog the test suite drives in
+process.  In the benchmark it runs in a process of its own and used to be the bottleneck: one
+Python core answering ~20,000 requests a second sat 86-94% busy, so the headline measured the
+fixture (round-5 verdict #1).  ``_apiserverd`` serves the same REST contract from a C++ store on
+one epoll thread -- merge-patch and ``/status`` semantics, resourceVersions, label-selected LIST
+and WATCH (resume, synthetic ADDED, scope transitions), CRD structural-schema admission, the
+per-verb latency model, TLS -- without the GIL.
+
+What it does not serve natively comes here, to :class:`NativeAPIServer.fallback` on the server
+thread: the ``/debug/fake/*`` test controls the bench drives (clock, latency faults, bulk job
+completion and lifecycle writes, request stats, counts).  Server-side Table printing and JSON
+patch answer 501 -- use :mod:`.http` for those, as for authn/RBAC and ownerReference GC.
+
+``tests/test_apiserverd.py`` replays one request stream against both implementations and
+compares the answers.
+"""
+from __future__ import annotations
+
+import json
+from typing import Any, Dict, Optional, Tuple
+from urllib.parse import parse_qsl
+
+from ..ops import build as _build
+from ..utils import jsonutil
+
+
+def load():
+    """The ``_apiserverd`` module, building it if its source is newer (None if it cannot load)."""
+    try:
+        if _build.needs_build("_apiserverd"):
+            _build.build_extension("_apiserverd")
+        from ..ops import _apiserverd  # type: ignore[attr-defined]
+
+        return _apiserverd
+    except Exception:  # noqa: BLE001 - a missing toolchain leaves the Python server
+        return None
+
+
+PYTORCHJOBS = ("kubeflow.org", "v1", "pytorchjobs")
+
+
+def _status_body(code: int, reason: str, message: str) -> bytes:
+    return json.dumps({"kind": "Status", "apiVersion": "v1", "metadata": {}, "status": "Failure",
+                       "message": message, "reason": reason, "code": code}).encode()
+
+
+class NativeAPIServer:
+    """A ``_apiserverd.Server`` with the CRDs installed and the ``/debug/fake`` controls."""
+
+    def __init__(self, start_ns: int = 0, watch_window: int = 200_000, bookmark_interval: float = 60.0):
+        mod = load()
+        if mod is None:
+            raise RuntimeError("the native fake apiserver (_apiserverd) did not build or load")
+        self.srv = mod.Server(now_ns=start_ns, watch_window=watch_window, bookmark_interval=bookmark_interval)
+        self.srv.set_fallback(self.fallback)
+        self._faults = 0
+
+    # ------------------------------------------------------------------ setup
+    def install_crd(self, crd: Dict[str, Any]) -> None:
+        st, body = self.srv.request("POST", "/apis/apiextensions.k8s.io/v1/customresourcedefinitions",
+                                    body=jsonutil.dumpb(crd), content_type="application/json")
+        if st not in (200, 201):
+            raise RuntimeError(f"installing CRD {crd.get('metadata', {}).get('name')}: {st} {body[:300]!r}")
+
+    def start(self, host: str = "127.0.0.1", port: int = 0, certfile: str = "", keyfile: str = "") -> int:
+        return self.srv.start(host, port, certfile, keyfile)
+
+    def stop(self) -> None:
+        self.srv.stop()
+
+    # ------------------------------------------------------------------ /debug/fake
+    def fallback(self, method: str, path: str, query: str, headers: Dict[str, str],
+                 body: bytes) -> Optional[Tuple[Any, ...]]:
+        if not path.startswith("/debug/fake/"):
+            if path.startswith(("/api/", "/apis/")):
+                return 501, _status_body(501, "NotImplemented", "not served by the native fake apiserver "
+                                                                "(server-side Table, JSON patch): use --impl python")
+            return None
+        try:
+            out = self._debug(method, path[len("/debug/fake/"):], dict(parse_qsl(query)), body)
+        except Exception as e:  # noqa: BLE001 - a broken control answers 500, never kills the server
+            return 500, _status_body(500, "InternalError", f"{type(e).__name__}: {e}")
+        if out is None:
+            return 404, _status_body(404, "NotFound", f"unknown debug endpoint {path}")
+        if isinstance(out, tuple):
+            return out
+        return 200, jsonutil.dumpb(out)
+
+    def _debug(self, method: str, what: str, q: Dict[str, str], raw: bytes) -> Any:
+        srv = self.srv
+        body = jsonutil.loads(raw) if raw else {}
+        if what == "stats":
+            st = srv.stats()
+            return {"total": st["total"], "by_verb": st["by_verb"], "by_resource_verb": st["by_resource_verb"],
+                    "resourceVersion": st["resourceVersion"], "native": True,
+                    "server_thread_cpu_s": st["server_thread_cpu_s"], "verb_cpu": st["verb_cpu"]}
+        if what == "clock":
+            if method == "POST":
+                srv.set_clock(int(body["nowNs"]))
+            return {"nowNs": srv.now_ns()}
+        if what == "faults" and method == "POST":
+            if body.get("clear"):
+                srv.clear_latency()
+                self._faults = 0
+            if body.get("faults"):
+                return 501, _status_body(501, "NotImplemented", "error faults are injected by the Python fake "
+                                                                "apiserver (--impl python); the native one "
+                                                                "models latency only")
+            lat = {str(k): float(v) for k, v in (body.get("latency") or {}).items()}
+            if lat:
+                srv.set_latency(lat)
+            return {"faults": self._faults}
+        if what == "complete" and method == "POST":
+            from ..trainingop.operator import finished_status
+
+            g, v, r = body.get("group", PYTORCHJOBS[0]), body.get("version", PYTORCHJOBS[1]), \
+                body.get("resource", PYTORCHJOBS[2])
+            ts = body.get("time") or ""
+            items = [(name, jsonutil.dumpb({"status": finished_status(kind, name, ts, True)}))
+                     for name, kind, _ in srv.unfinished(g, v, r, body.get("namespace") or "")]
+            rvs = srv.patch_many(g, v, r, body.get("namespace") or "", items, "status")
+            return {"completed": sum(1 for x in rvs if x is not None)}
+        if what == "lifecycle" and method == "POST":
+            from ..trainingop.operator import lifecycle_status, replica_counts
+
+            g, v, r = body.get("group", PYTORCHJOBS[0]), body.get("version", PYTORCHJOBS[1]), \
+                body.get("resource", PYTORCHJOBS[2])
+            ns = body.get("namespace") or ""
+            stage = int(body.get("stage", -1))
+            start, end = body.get("start") or "", body.get("end") or ""
+            items, keys = [], []
+            reps_memo: Dict[bytes, Any] = {}
+            for name, kind, enc in srv.unfinished(g, v, r, ns):
+                obj = jsonutil.loads(enc)
+                spec_key = jsonutil.dumpb(obj.get("spec") or {})
+                reps = reps_memo.get(spec_key)
+                if reps is None:
+                    reps = reps_memo[spec_key] = replica_counts(obj)
+                items.append((name, jsonutil.dumpb({"status": lifecycle_status(obj, stage, start, end, reps)})))
+                keys.append(f"{(obj.get('metadata') or {}).get('namespace', ns)}/{name}")
+            rvs = srv.patch_many(g, v, r, ns, items, "status")
+            return {"resourceVersions": {k: rv for k, rv in zip(keys, rvs) if rv is not None}}
+        if what == "profile" and method == "POST":
+            # the store runs on a C++ thread: cProfile would see only this fallback
+            return {"profiling": False, "native": True,
+                    "note": "the native fake apiserver is profiled with perf / rocprofv3 --sys-trace, not cProfile"}
+        if what == "gc" and method == "POST":
+            from ..utils import gctune
+
+            gctune.tune()
+            gctune.freeze()
+            return {"frozen": True}
+        if what == "count":
+            return {"count": srv.count(q.get("group", ""), q.get("version", "v1"), q["resource"],
+                                       q.get("namespace"))}
+        if what == "watch-log":  # events kept per resource for watch resume (the soak's memory bound)
+            return {"log": srv.log_sizes(), "watchers": srv.watchers()}
+        return None

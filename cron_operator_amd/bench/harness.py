@@ -117,6 +117,12 @@ class BenchConfig:
     shard_routing: str = "labels"
     # per-verb server-side latency (LATENCY_PROFILES name), applied after setup; needs transport="http"
     apiserver_latency: str = "none"
+    # the fake apiserver process: "native" (apiserver/native.py, the C++ _apiserverd: the fixture
+    # off the critical path) or "python" (apiserver/server.py + http.py; the A/B arm)
+    apiserver_impl: str = "native"
+    # events per resource the fake apiserver keeps for watch resume (a bounded watch cache: the
+    # soak's fixture memory stays flat; 20,000 is ~5 ticks of 1000 Crons' job events)
+    watch_window: int = 20_000
     # the fake apiserver serves HTTPS (self-signed CN=localhost) and every operator connection
     # verifies it against that CA, as against a real cluster's apiserver; needs transport="http"
     tls: bool = False
@@ -205,7 +211,9 @@ def _pct(xs: List[float], p: float) -> float:
 class _RemoteServer:
     """The fake apiserver in a child process, driven over HTTP."""
 
-    def __init__(self, tls: bool = False):
+    def __init__(self, tls: bool = False, impl: str = "native", watch_window: int = 20_000):
+        self.impl = impl
+        self.watch_window = watch_window
         self.proc: Optional[subprocess.Popen] = None
         self.url = ""
         self.tls_dir = ""
@@ -241,7 +249,8 @@ class _RemoteServer:
         env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
         extra = ["--tls-dir", self.tls_dir] if self.tls_dir else []
         self.proc = subprocess.Popen([sys.executable, "-m", "cron_operator_amd.bench.apiserver_proc",
-                                      "--start-ns", str(T0_NS)] + extra,
+                                      "--start-ns", str(T0_NS), "--impl", self.impl,
+                                      "--watch-window", str(self.watch_window)] + extra,
                                      stdout=subprocess.PIPE, stderr=subprocess.STDOUT, env=env, text=True)
         assert self.proc.stdout is not None
         line = self.proc.stdout.readline()
@@ -447,7 +456,7 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
 
         from ..runtime.http import HttpTransport
 
-        remote = _RemoteServer(tls=cfg.tls)
+        remote = _RemoteServer(tls=cfg.tls, impl=cfg.apiserver_impl, watch_window=cfg.watch_window)
         remote.start()
         transport = HttpTransport(remote.rest_config(), pool_size=max(16, cfg.workers * 2, cfg.max_inflight))
         sslctx = remote.ssl_context()

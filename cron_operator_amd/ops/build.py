@@ -32,17 +32,21 @@ EXTENSIONS: Dict[str, List[str]] = {
     "_aioloop": ["aioloop.cpp"],
     "_promlite": ["promlite.cpp"],
     "_workqueue": ["workqueue.cpp"],
+    "_apiserverd": ["apiserverd.cpp"],
 }
 # headers each extension includes (a change rebuilds it)
 HEADERS: Dict[str, List[str]] = {
     "_httpcodec": ["httpframe.h"],
     "_netconn": ["httpframe.h"],
+    "_apiserverd": ["jdom.h"],
 }
 # extra linker inputs: _netconn speaks TLS through the system OpenSSL and builds its own SSL_CTX
 # (TlsContext); an ssl.SSLContext is used only when CPython's _ssl resolves to the same libssl
 # (checked at configure() with dlopen/dlsym)
 LIBS: Dict[str, List[str]] = {
     "_netconn": ["-lssl", "-lcrypto", "-ldl"],
+    # the fake apiserver serves HTTPS itself (deployment-shaped runs) and runs its own thread
+    "_apiserverd": ["-lssl", "-lcrypto", "-pthread"],
 }
 
 
