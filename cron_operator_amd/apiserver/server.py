@@ -89,12 +89,26 @@ class Fault:
 
 
 class FaultInjector:
-    """Per-verb error injection and latency (the reference has none)."""
+    """Per-verb error injection and latency (the reference has none), and watch lag.
+
+    ``watch_lag[resource] = (min_s, max_s)`` (``"*"``: every resource) delays each event of a
+    watch stream by a random ``min_s..max_s`` drawn per event from that stream's own generator:
+    the Cron stream and the job streams fall behind independently, as a real apiserver's watch
+    cache and a busy client's informers do.  A stream stays in order (an event never overtakes
+    the one before it), and its end waits for what it still carries."""
 
     def __init__(self, seed: int = 0):
         self.faults: List[Fault] = []
         self.latency: Dict[str, float] = {}  # verb -> seconds ("*" default)
+        self.watch_lag: Dict[str, Tuple[float, float]] = {}  # resource -> (min s, max s)
         self._rng = random.Random(seed)
+
+    def lag_for(self, resource: str) -> Optional[Tuple[float, float]]:
+        return self.watch_lag.get(resource) or self.watch_lag.get("*")
+
+    def lag_rng(self) -> random.Random:
+        """A generator of one watch stream's delays (seeded from this injector's)."""
+        return random.Random(self._rng.random())
 
     def add(self, **kw: Any) -> Fault:
         f = Fault(**kw)
@@ -104,6 +118,7 @@ class FaultInjector:
     def clear(self) -> None:
         self.faults.clear()
         self.latency.clear()
+        self.watch_lag.clear()
 
     def check(self, verb: str, resource: str, sub: Optional[str] = None, name: Optional[str] = None,
               after: bool = False) -> None:
@@ -146,6 +161,12 @@ class Watcher:
         # no end -- like a connection whose peer vanished without a FIN (fault injection)
         self.stalled = False
         self.sent = 0
+        # watch lag (FaultInjector.watch_lag): events scheduled for later delivery, in order
+        self.lagged = 0               # scheduled, not delivered yet
+        self._lag_at = 0.0            # delivery time of the last scheduled event
+        self._lag_rng: Optional[random.Random] = None
+        self._lag_q: Deque[Tuple[float, Optional[Tuple[str, Dict[str, Any]]]]] = deque()
+        self._lag_timer: Optional[asyncio.TimerHandle] = None
 
     def _in_scope(self, obj: Dict[str, Any]) -> bool:
         if self.namespace is not None and (obj.get("metadata") or {}).get("namespace") != self.namespace:
@@ -179,7 +200,47 @@ class Watcher:
         if self.stalled:
             return
         self.sent += 1
-        ev = (etype, jsonutil.deepcopy(obj) if self.copy_events else obj)
+        self._send((etype, jsonutil.deepcopy(obj) if self.copy_events else obj))
+
+    def _send(self, ev: Optional[Tuple[str, Dict[str, Any]]]) -> None:
+        """Deliver now, or -- under watch lag -- after this stream's next delay, never before an
+        event already scheduled (a lagging stream is late, not reordered): one FIFO per stream,
+        drained by one timer at its head (asyncio's timer heap does not keep equal deadlines in
+        order)."""
+        lag = self.server.faults.lag_for(self.info.resource) if self.server.faults.watch_lag else None
+        if lag is None and not self.lagged:
+            self._deliver(ev)
+            return
+        try:
+            loop = asyncio.get_running_loop()
+        except RuntimeError:
+            self._deliver(ev)
+            return
+        if self._lag_rng is None:
+            self._lag_rng = self.server.faults.lag_rng()
+        lo, hi = lag if lag is not None else (0.0, 0.0)
+        at = max(loop.time() + self._lag_rng.uniform(lo, hi), self._lag_at)
+        self._lag_at = at
+        self._lag_q.append((at, ev))
+        self.lagged += 1
+        if self._lag_timer is None:
+            self._lag_timer = loop.call_at(at, self._drain_lagged)
+
+    def _drain_lagged(self) -> None:
+        self._lag_timer = None
+        loop = asyncio.get_running_loop()
+        now = loop.time()
+        q = self._lag_q
+        while q and q[0][0] <= now:
+            _, ev = q.popleft()
+            self.lagged -= 1
+            if self.stalled and ev is not None:
+                continue
+            self._deliver(ev)
+        if q:
+            self._lag_timer = loop.call_at(q[0][0], self._drain_lagged)
+
+    def _deliver(self, ev: Optional[Tuple[str, Dict[str, Any]]]) -> None:
         if self.sink is not None:
             self.sink(ev)
         else:
@@ -187,27 +248,20 @@ class Watcher:
 
     def bookmark(self, rv: int) -> None:
         if self.bookmarks and not self.closed and not self.stalled:
-            ev = ("BOOKMARK", {"kind": self.info.kind, "apiVersion": self.info.api_version,
-                               "metadata": {"resourceVersion": str(rv)}})
-            if self.sink is not None:
-                self.sink(ev)
-            else:
-                self.queue.put_nowait(ev)
+            self._send(("BOOKMARK", {"kind": self.info.kind, "apiVersion": self.info.api_version,
+                                     "metadata": {"resourceVersion": str(rv)}}))
 
     def stop(self) -> None:
         if not self.closed:
             self.closed = True
             self.server._remove_watcher(self)
-            if self.sink is not None:
-                self.sink(None)
-            else:
-                self.queue.put_nowait(None)
+            self._send(None)  # after what the stream still carries
 
     def __aiter__(self):
         return self
 
     async def __anext__(self) -> Tuple[str, Dict[str, Any]]:
-        if self.closed and self.queue.empty():
+        if self.closed and self.queue.empty() and not self.lagged:
             raise StopAsyncIteration
         ev = await self.queue.get()
         if ev is None:

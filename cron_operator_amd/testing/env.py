@@ -85,7 +85,7 @@ class TestEnv:
     def _watches_drained(self) -> bool:
         for lst in self.server._watchers.values():
             for w in lst:
-                if not w.queue.empty():
+                if not w.queue.empty() or w.lagged:
                     return False
         return True
 

@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""Where the benchmark's time goes, fixture side: the fake apiserver's CPU over the timed steps.
+
+Runs the headline harness (1000 Crons, `* * * * *`, historyLimit 10) and reports, per run, the
+apiserver process's CPU and busy fraction and the operator's CPU per fire -- and, for the native
+fake apiserver (``--impl native``), its server thread's CPU by phase (socket reads + request
+parsing, verbs, the Python fallback that runs the harness's job writes, framing + socket writes)
+and per verb.  ``--impl python`` measures the rounds 1-5 fixture the same way (process CPU only).
+
+    python scripts/fixture_split.py --shards 3 1 --impl native python --reps 2 --out split.json
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import urllib.request
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def run(shards: int, impl: str, steps: int, warmup: int, crons: int, lifecycle: str) -> dict:
+    from cron_operator_amd.bench import harness
+
+    snaps = []
+    orig = harness._cpu_times
+
+    def cpu(remote):
+        r = orig(remote)
+        if remote is not None and remote.url and impl == "native":
+            with urllib.request.urlopen(remote.url + "/debug/fake/stats") as f:
+                snaps.append(json.loads(f.read()))
+        return r
+
+    harness._cpu_times = cpu
+    try:
+        res = harness.run_sync(harness.BenchConfig(n_crons=crons, steps=steps, warmup=warmup, shards=shards,
+                                                   lifecycle=lifecycle, apiserver_impl=impl))
+    finally:
+        harness._cpu_times = orig
+    fires = crons * steps
+    out = {"shards": shards, "impl": impl, "value": round(res.cron_reconciles_per_s, 1),
+           "p50_ms": round(res.p50_latency_ms, 2), "elapsed_s": round(res.elapsed_s, 3),
+           "apiserver_busy_frac": round(res.cpu_s_apiserver / res.elapsed_s, 3),
+           "apiserver_cpu_us_per_fire": round(res.cpu_s_apiserver * 1e6 / fires, 1),
+           "operator_cpu_ms_per_fire": round(res.cpu_s_operator * 1000 / fires, 4),
+           "step_ms": [round(x, 1) for x in res.step_ms]}
+    if len(snaps) >= 2:
+        a, b = snaps[0], snaps[-1]
+        out["server_thread_cpu_us_per_fire"] = {
+            k: round((b["server_thread_cpu_s"][k] - a["server_thread_cpu_s"][k]) * 1e6 / fires, 1)
+            for k in b["server_thread_cpu_s"]}
+        per_verb = {}
+        for k, (s1, n1) in b["verb_cpu"].items():
+            s0, n0 = a["verb_cpu"].get(k, (0.0, 0))
+            if n1 > n0:
+                per_verb[k] = {"calls_per_fire": round((n1 - n0) / fires, 3),
+                               "us_per_call": round((s1 - s0) * 1e6 / (n1 - n0), 1)}
+        out["per_verb"] = per_verb
+    return out
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--shards", type=int, nargs="+", default=[3, 1])
+    ap.add_argument("--impl", nargs="+", default=["native", "python"], choices=["native", "python"])
+    ap.add_argument("--reps", type=int, default=1, help="alternating repetitions of every (impl, shards) arm")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--crons", type=int, default=1000)
+    ap.add_argument("--lifecycle", default="instant", choices=["instant", "realistic"])
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    rows = []
+    for rep in range(a.reps):
+        for impl in a.impl:
+            for shards in a.shards:
+                r = run(shards, impl, a.steps, a.warmup, a.crons, a.lifecycle)
+                r["rep"] = rep
+                rows.append(r)
+                print(json.dumps(r), flush=True)
+    if a.out:
+        with open(a.out, "w") as fh:
+            json.dump(rows, fh, indent=1)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -11,6 +11,8 @@
 #   shards10k  10000 Crons, 3 label-routed shard processes on a first start (peak RSS per shard)
 #   routing label vs hash routing on 3 shards, REPS alternating pairs at ROUTING_SIZES Crons (default 3000)
 #   mem10k  10000 Crons, the operator in its own process: peak RSS with a shared and with distinct templates
+#   split   fixture vs operator CPU, native and Python fake apiserver, 3 shards and one process
+#           (scripts/fixture_split.py; REPS alternating repetitions)
 #   ranks   the driver's multi-rank line (torch.distributed.run, N=2 and 4 CPU-only ranks): the
 #           N=8 scaling run is the driver's; RANKS overrides the list
 # Stops at the first failure; every GPU step has its own time limit.
@@ -105,6 +107,11 @@ for s in $STEPS; do
         IFS=';'
       done
       IFS=$old_ifs ;;
+    split)
+      step split
+      timeout -k 10 900 python -u scripts/fixture_split.py --reps "${REPS:-1}" --out "$OUT/split.json" \
+        > "$OUT/split.log" 2>&1
+      check $? split; cut -c1-400 "$OUT/split.log" ;;
     ranks)
       for n in ${RANKS:-2 4}; do
         step "ranks $n"
