@@ -39,6 +39,8 @@ def load():
 
 
 PYTORCHJOBS = ("kubeflow.org", "v1", "pytorchjobs")
+_NAME = "@@name@@"  # stands for each job's name in a bulk status body (never a valid object name)
+_KINDS = {"pytorchjobs": "PyTorchJob", "tfjobs": "TFJob", "mpijobs": "MPIJob"}
 
 
 def _status_body(code: int, reason: str, message: str) -> bytes:
@@ -70,6 +72,13 @@ class NativeAPIServer:
     def stop(self) -> None:
         self.srv.stop()
 
+    def _kind_of(self, group: str, version: str, resource: str) -> str:
+        st, raw = self.srv.request("GET", f"/apis/{group}/{version}" if group else f"/api/{version}")
+        for e in (jsonutil.loads(raw).get("resources") or []) if st == 200 else []:
+            if e.get("name") == resource:
+                return e.get("kind", "")
+        raise KeyError(f"unknown resource {group}/{version}/{resource}")
+
     # ------------------------------------------------------------------ /debug/fake
     def fallback(self, method: str, path: str, query: str, headers: Dict[str, str],
                  body: bytes) -> Optional[Tuple[Any, ...]]:
@@ -95,7 +104,8 @@ class NativeAPIServer:
             st = srv.stats()
             return {"total": st["total"], "by_verb": st["by_verb"], "by_resource_verb": st["by_resource_verb"],
                     "resourceVersion": st["resourceVersion"], "native": True,
-                    "server_thread_cpu_s": st["server_thread_cpu_s"], "verb_cpu": st["verb_cpu"]}
+                    "server_thread_cpu_s": st["server_thread_cpu_s"], "verb_cpu": st["verb_cpu"],
+                    "phase_cycles": st["phase_cycles"]}
         if what == "clock":
             if method == "POST":
                 srv.set_clock(int(body["nowNs"]))
@@ -118,10 +128,11 @@ class NativeAPIServer:
             g, v, r = body.get("group", PYTORCHJOBS[0]), body.get("version", PYTORCHJOBS[1]), \
                 body.get("resource", PYTORCHJOBS[2])
             ts = body.get("time") or ""
-            items = [(name, jsonutil.dumpb({"status": finished_status(kind, name, ts, True)}))
-                     for name, kind, _ in srv.unfinished(g, v, r, body.get("namespace") or "")]
-            rvs = srv.patch_many(g, v, r, body.get("namespace") or "", items, "status")
-            return {"completed": sum(1 for x in rvs if x is not None)}
+            # one body for every job of the kind, the name filled in natively per job
+            kind = _KINDS.get(r) or self._kind_of(g, v, r)
+            tmpl = jsonutil.dumpb({"status": finished_status(kind, _NAME, ts, True)})
+            n = srv.patch_unfinished(g, v, r, body.get("namespace") or "", tmpl, _NAME, "status")
+            return {"completed": n}
         if what == "lifecycle" and method == "POST":
             from ..trainingop.operator import lifecycle_status, replica_counts
 

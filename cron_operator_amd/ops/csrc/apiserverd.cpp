@@ -45,11 +45,14 @@
 #include <random>
 #include <set>
 #include <string>
+#include <string_view>
 #include <thread>
 #include <tuple>
 #include <unordered_map>
 #include <unordered_set>
 #include <vector>
+
+#include <x86intrin.h>
 
 #include "jdom.h"
 
@@ -609,7 +612,11 @@ struct Schema {
   // One pass: prune unknown fields, fill defaults (only on nodes not yet admitted: fresh,
   // private), and check.  Subtrees already admitted (shared with the stored object at the same
   // path) are skipped: CRD validation ratcheting taken to its conclusion, as in schema.py.
-  bool admit(Node* v, bool root) const {
+  // `changed`: set when this node or one below it was pruned or defaulted; an ancestor then drops
+  // the bytes it may carry from the request body (jdom::Parser keeps them as its encoding)
+  bool admit(Node* v, bool root, bool* changed = nullptr) const {
+    bool dummy = false;
+    if (!changed) changed = &dummy;
     if (any) return true;
     if (v->t == T::Null) return nullable || root || type.empty();
     if (v->admitted) return true;
@@ -630,6 +637,7 @@ struct Schema {
       if (has_min && d < min) ok = false;
       if (has_max && d > max) ok = false;
     }
+    bool mine = false;
     if (v->t == T::Obj) {
       const bool keep_unknown = preserve || (!has_props && !addl && !addl_true);
       if (!keep_unknown && !addl && !addl_true) {
@@ -640,13 +648,13 @@ struct Schema {
             continue;
           }
           v->o.erase(v->o.begin() + static_cast<long>(i));
-          v->enc.clear();
+          mine = true;
         }
       }
       for (const auto& d : defaults)
         if (!v->get(d.first)) {
           v->o.emplace_back(d.first, jdom::deep_copy(d.second.get()));
-          v->enc.clear();
+          mine = true;
         }
       for (const auto& r : required)
         if (!v->get(r)) ok = false;
@@ -654,14 +662,18 @@ struct Schema {
         if (root && m.first == "metadata") continue;
         const Schema* sub = prop(m.first);
         if (sub) {
-          if (!sub->admit(m.second.get(), false)) ok = false;
+          if (!sub->admit(m.second.get(), false, &mine)) ok = false;
         } else if (addl) {
-          if (!addl->admit(m.second.get(), false)) ok = false;
+          if (!addl->admit(m.second.get(), false, &mine)) ok = false;
         }
       }
     } else if (v->t == T::Arr && items) {
       for (const Ref& it : v->a)
-        if (!items->admit(it.get(), false)) ok = false;
+        if (!items->admit(it.get(), false, &mine)) ok = false;
+    }
+    if (mine) {
+      v->enc.clear();
+      *changed = true;
     }
     return ok;
   }
@@ -786,7 +798,7 @@ const std::string& meta_str(const Node* obj, const char* k) {
 struct Request {
   std::string method, path, query_string, content_type, accept, authorization;
   std::vector<std::pair<std::string, std::string>> query;
-  std::vector<std::pair<std::string, std::string>> headers;  // lower-cased names (for the fallback)
+  std::string raw_headers;  // the header lines as sent (the Python fallback parses them)
   std::string body;
   bool keep = true;
 
@@ -818,7 +830,11 @@ struct Watcher {
   bool bookmarks = false;
   bool ended = false;
   bool dirty = false;
-  std::string pending;  // event lines not yet framed into a chunk
+  std::string pending;  // event lines before the response head went out (the initial replay)
+  // once streaming, events go straight into the connection's buffer inside an open chunk whose
+  // fixed-width size field (at chunk_at) is filled in when the chunk closes (end of the turn)
+  bool streaming = false;
+  size_t chunk_at = std::string::npos;
   uint64_t sent = 0;
 
   bool in_scope(const Node* obj) const {
@@ -894,6 +910,15 @@ struct Impl {
   // socket writes; and the loop's total
   long long cpu_read = 0, cpu_verbs = 0, cpu_fallback = 0, cpu_write = 0, cpu_loop = 0;
   std::map<std::string, std::pair<long long, long long>> verb_cpu;  // "verb[/sub]:resource" -> (ns, calls)
+  // where a write's time goes, in TSC cycles (nested: `finish` includes `emit`)
+  enum Ph { kParse, kMerge, kPrepare, kFinish, kEmit, kReply, kPhases };
+  unsigned long long phase[kPhases] = {};
+  struct PhaseTimer {
+    unsigned long long* acc;
+    unsigned long long t0;
+    explicit PhaseTimer(unsigned long long* a) : acc(a), t0(__rdtsc()) {}
+    ~PhaseTimer() { *acc += __rdtsc() - t0; }
+  };
 #ifndef APISERVERD_STANDALONE
   PyObject* fallback = nullptr;
 #endif
@@ -1120,10 +1145,21 @@ struct Impl {
   }
 
   // ---------------------------------------------------------------- watch fan-out
+  // where a watcher's next event line goes: its pending buffer, or the open chunk
+  std::string& event_sink(Watcher* w) {
+    if (!w->streaming || !w->conn || w->conn->closed) return w->pending;
+    std::string& o = w->conn->out;
+    if (w->chunk_at == std::string::npos) {
+      w->chunk_at = o.size();
+      o.append("00000000\r\n");  // chunk-size, leading zeros allowed (RFC 9112 7.1)
+    }
+    return o;
+  }
+
   void put_event(Watcher* w, int type, Node* obj) {
     if (w->ended) return;
     ++w->sent;
-    std::string& p = w->pending;
+    std::string& p = event_sink(w);
     p.append("{\"type\":\"");
     p.append(kEventType[type]);
     p.append("\",\"object\":");
@@ -1146,6 +1182,7 @@ struct Impl {
   }
 
   void emit(Resource* ri, int type, const Ref& obj, const Ref& old, long long at) {
+    PhaseTimer pt(&phase[kEmit]);
     Store* st = ri->store;
     st->log.push_back(Event{at, type, obj, old});
     while (st->log.size() > watch_window) {
@@ -1475,10 +1512,19 @@ struct Impl {
       *err = conflict(ri->resource, ri->group, name, kModified);
       return Ref();
     }
-    Ref merged = jdom::merge_patch(old, patch);
+    Ref merged;
+    {
+      PhaseTimer pt(&phase[kMerge]);
+      merged = jdom::merge_patch(old, patch);
+    }
     Node* nm = nullptr;
-    Ref neu = prepare_update(ri, old, merged, sub, &nm, err);
+    Ref neu;
+    {
+      PhaseTimer pt(&phase[kPrepare]);
+      neu = prepare_update(ri, old, merged, sub, &nm, err);
+    }
     if (!neu) return Ref();
+    PhaseTimer pt(&phase[kFinish]);
     return finish_write(ri, ns, name, old, neu, nm, err);
   }
 
@@ -1911,6 +1957,7 @@ struct Impl {
     Ref body;
     if (!r.body.empty()) {
       std::string perr;
+      PhaseTimer pt(&phase[kParse]);
       body = jdom::parse(r.body.data(), r.body.size(), &perr);
       if (!body) {
         reply_err(rep, bad_request("invalid JSON body: " + perr));
@@ -2033,7 +2080,7 @@ struct Impl {
 
   void bookmark(Watcher* w) {
     if (!w->bookmarks || w->ended) return;
-    std::string& p = w->pending;
+    std::string& p = event_sink(w);
     p.append("{\"type\":\"BOOKMARK\",\"object\":{\"kind\":");
     jdom::put_string(&p, w->res->kind);
     p.append(",\"apiVersion\":");
@@ -2084,6 +2131,7 @@ struct Impl {
   // write what is buffered; false: the connection failed (closed)
   bool flush(Conn* c) {
     if (c->closed) return false;
+    if (c->watch && c->watch->chunk_at != std::string::npos) frame_pending(c->watch);
     while (c->out_off < c->out.size()) {
       const char* p = c->out.data() + c->out_off;
       const size_t n = c->out.size() - c->out_off;
@@ -2150,6 +2198,7 @@ struct Impl {
   }
 
   void write_reply(Conn* c, const Reply& rep, bool keep) {
+    PhaseTimer pt(&phase[kReply]);
     const std::string& body = rep.obj ? jdom::encoded(rep.obj.get()) : rep.body;
     std::string& o = c->out;
     o.append("HTTP/1.1 ");
@@ -2227,6 +2276,8 @@ struct Impl {
       c->watch = w;
       c->watch_keep = r.keep;
       c->out.append("HTTP/1.1 200 OK\r\nContent-Type: application/json\r\nTransfer-Encoding: chunked\r\n\r\n");
+      frame_pending(w);  // the initial replay
+      w->streaming = true;
       mark_dirty(c);
       const std::string ts = r.qv("timeoutSeconds");
       const double timeout = ts.empty() ? 1800.0 : std::strtod(ts.c_str(), nullptr);
@@ -2258,13 +2309,24 @@ struct Impl {
 
   void frame_pending(Watcher* w) {
     w->dirty = false;
-    if (w->pending.empty() || !w->conn || w->conn->closed) {
+    Conn* c = w->conn;
+    if (!c || c->closed) {
       w->pending.clear();
+      w->chunk_at = std::string::npos;
       return;
     }
+    if (w->chunk_at != std::string::npos) {  // close the open chunk: fill in its size
+      const size_t body = c->out.size() - w->chunk_at - 10;
+      char hex[9];
+      snprintf(hex, sizeof hex, "%08zx", body);
+      std::memcpy(&c->out[w->chunk_at], hex, 8);
+      c->out.append("\r\n");
+      w->chunk_at = std::string::npos;
+      mark_dirty(c);
+    }
+    if (w->pending.empty()) return;
     char hex[24];
     snprintf(hex, sizeof hex, "%zx\r\n", w->pending.size());
-    Conn* c = w->conn;
     c->out.append(hex);
     c->out.append(w->pending);
     c->out.append("\r\n");
@@ -2284,6 +2346,27 @@ struct Impl {
   }
 
   // 1: a request; 0: need more bytes; -1: error (replied)
+  static std::string_view sv_strip(std::string_view v) {
+    size_t b = 0, e = v.size();
+    while (b < e && (v[b] == ' ' || v[b] == '\t')) ++b;
+    while (e > b && (v[e - 1] == ' ' || v[e - 1] == '\t')) --e;
+    return v.substr(b, e - b);
+  }
+  static bool ieq(std::string_view a, const char* lit) {
+    const size_t n = std::strlen(lit);
+    if (a.size() != n) return false;
+    for (size_t i = 0; i < n; ++i)
+      if (std::tolower(static_cast<unsigned char>(a[i])) != lit[i]) return false;
+    return true;
+  }
+  static std::string lower(std::string_view v) {
+    std::string o(v);
+    for (auto& ch : o) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
+    return o;
+  }
+
+  // 1: a request; 0: need more bytes; -1: error (replied).  Header fields are read in place;
+  // only the few the server uses are copied (the raw block is kept for the Python fallback).
   int parse_request(Conn* c, Request* r) {
     std::string& b = c->in;
     const size_t hend = b.find("\r\n\r\n");
@@ -2294,63 +2377,65 @@ struct Impl {
       }
       return 0;
     }
-    const size_t l_end = b.find("\r\n");
-    const std::string line = b.substr(0, l_end);
+    const std::string_view all(b.data(), hend + 2);
+    const size_t l_end = all.find("\r\n");
+    const std::string_view line = all.substr(0, l_end);
     const size_t sp1 = line.find(' ');
-    const size_t sp2 = sp1 == std::string::npos ? std::string::npos : line.find(' ', sp1 + 1);
-    if (sp1 == std::string::npos || sp2 == std::string::npos) {
+    const size_t sp2 = sp1 == std::string_view::npos ? std::string_view::npos : line.find(' ', sp1 + 1);
+    if (sp1 == std::string_view::npos || sp2 == std::string_view::npos) {
       write_raw_error(c, 400, "bad request line");
       return -1;
     }
-    r->method = line.substr(0, sp1);
+    r->method.assign(line.data(), sp1);
     for (auto& ch : r->method) ch = static_cast<char>(std::toupper(static_cast<unsigned char>(ch)));
-    std::string target = line.substr(sp1 + 1, sp2 - sp1 - 1);
-    const std::string version = line.substr(sp2 + 1);
+    std::string target(line.substr(sp1 + 1, sp2 - sp1 - 1));
+    const std::string_view version = line.substr(sp2 + 1);
     long long clen = 0;
-    bool chunked = false, expect = false;
-    std::string connection;
+    bool chunked = false, expect = false, conn_close = false, conn_keep = false;
     size_t p = l_end + 2;
-    while (p < hend + 2) {
-      const size_t nl = b.find("\r\n", p);
-      if (nl == std::string::npos || nl > hend) break;
-      const size_t colon = b.find(':', p);
-      if (colon != std::string::npos && colon < nl) {
-        std::string k = b.substr(p, colon - p);
-        std::string v = b.substr(colon + 1, nl - colon - 1);
-        k = Selector::strip(k);
-        v = Selector::strip(v);
-        for (auto& ch : k) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
-        if (k == "content-length") {
-          char* e = nullptr;
-          clen = std::strtoll(v.c_str(), &e, 10);
-          if (!e || *e || clen < 0) {
-            write_raw_error(c, 400, "bad request");
-            return -1;
-          }
-        } else if (k == "transfer-encoding") {
-          std::string lv = v;
-          for (auto& ch : lv) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
-          chunked = lv.find("chunked") != std::string::npos;
-        } else if (k == "content-type") {
-          std::string ct = v.substr(0, v.find(';'));
-          ct = Selector::strip(ct);
-          for (auto& ch : ct) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
-          r->content_type = ct;
-        } else if (k == "accept") {
-          r->accept = v;
-        } else if (k == "connection") {
-          connection = v;
-          for (auto& ch : connection) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
-        } else if (k == "expect") {
-          std::string lv = v;
-          for (auto& ch : lv) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
-          expect = lv == "100-continue";
-        } else if (k == "authorization") {
-          r->authorization = v;
-        }
-        r->headers.emplace_back(std::move(k), std::move(v));
-      }
+    r->raw_headers.assign(all.data() + p, all.size() > p ? all.size() - p : 0);
+    while (p < all.size()) {
+      const size_t nl = all.find("\r\n", p);
+      if (nl == std::string_view::npos) break;
+      const std::string_view ln = all.substr(p, nl - p);
       p = nl + 2;
+      const size_t colon = ln.find(':');
+      if (colon == std::string_view::npos) continue;
+      const std::string_view k = sv_strip(ln.substr(0, colon));
+      const std::string_view v = sv_strip(ln.substr(colon + 1));
+      switch (k.size()) {
+        case 14:  // content-length
+          if (ieq(k, "content-length")) {
+            std::string num(v);
+            char* e = nullptr;
+            clen = std::strtoll(num.c_str(), &e, 10);
+            if (num.empty() || !e || *e || clen < 0) {
+              write_raw_error(c, 400, "bad request");
+              return -1;
+            }
+          }
+          break;
+        case 17:  // transfer-encoding
+          if (ieq(k, "transfer-encoding")) chunked = lower(v).find("chunked") != std::string::npos;
+          break;
+        case 12:  // content-type
+          if (ieq(k, "content-type")) r->content_type = lower(sv_strip(v.substr(0, v.find(';'))));
+          break;
+        case 6:  // accept, expect
+          if (ieq(k, "accept")) r->accept.assign(v);
+          else if (ieq(k, "expect")) expect = ieq(v, "100-continue");
+          break;
+        case 10:  // connection
+          if (ieq(k, "connection")) {
+            conn_close = ieq(v, "close");
+            conn_keep = ieq(v, "keep-alive");
+          }
+          break;
+        case 13:  // authorization
+          if (ieq(k, "authorization")) r->authorization.assign(v);
+          break;
+        default: break;
+      }
     }
     size_t pos = hend + 4;
     if (chunked) {
@@ -2396,8 +2481,7 @@ struct Impl {
     }
     b.erase(0, pos);
     c->continued = false;
-    if (version == "HTTP/1.1") r->keep = connection != "close";
-    else r->keep = connection == "keep-alive";
+    r->keep = version == "HTTP/1.1" ? !conn_close : conn_keep;
     // absolute form (a client behind a proxy): routing needs the path and query only
     const size_t scheme = target.find("://");
     if (!target.empty() && target[0] != '/' && scheme != std::string::npos) {
@@ -2681,12 +2765,24 @@ bool Impl::call_fallback(const Request& r, Reply* rep) {
   if (!fallback) return false;
   PyGILState_STATE g = PyGILState_Ensure();
   bool ok = false;
-  PyObject* hdrs = PyDict_New();
-  for (const auto& kv : r.headers) {
-    PyObject* v = PyUnicode_DecodeLatin1(kv.second.data(), static_cast<Py_ssize_t>(kv.second.size()), nullptr);
-    if (v) {
-      PyDict_SetItemString(hdrs, kv.first.c_str(), v);
-      Py_DECREF(v);
+  PyObject* hdrs = PyDict_New();  // lower-cased names
+  {
+    const std::string_view all(r.raw_headers);
+    size_t p = 0;
+    while (p < all.size()) {
+      size_t nl = all.find("\r\n", p);
+      if (nl == std::string_view::npos) nl = all.size();
+      const std::string_view ln = all.substr(p, nl - p);
+      p = nl + 2;
+      const size_t colon = ln.find(':');
+      if (colon == std::string_view::npos) continue;
+      const std::string k = Impl::lower(Impl::sv_strip(ln.substr(0, colon)));
+      const std::string_view v = Impl::sv_strip(ln.substr(colon + 1));
+      PyObject* pv = PyUnicode_DecodeLatin1(v.data(), static_cast<Py_ssize_t>(v.size()), nullptr);
+      if (pv) {
+        PyDict_SetItemString(hdrs, k.c_str(), pv);
+        Py_DECREF(pv);
+      }
     }
   }
   PyObject* res = PyObject_CallFunction(fallback, "ssNNy#", r.method.c_str(), r.path.c_str(),
@@ -2902,6 +2998,7 @@ PyObject* Server_stats(Server* self, PyObject*) {
   Impl* s = self->impl;
   std::map<std::string, long long> bv, brv;
   std::map<std::string, std::pair<long long, long long>> vcpu;
+  unsigned long long ph[Impl::kPhases];
   long long total, rv, reqs;
   long long cpu[6];
   Py_BEGIN_ALLOW_THREADS
@@ -2919,6 +3016,7 @@ PyObject* Server_stats(Server* self, PyObject*) {
     cpu[4] = s->cpu_loop;
     cpu[5] = s->slow_admits;
     vcpu = s->verb_cpu;
+    for (int i = 0; i < Impl::kPhases; ++i) ph[i] = s->phase[i];
   }
   Py_END_ALLOW_THREADS
   PyObject* d = PyDict_New();
@@ -2958,6 +3056,10 @@ PyObject* Server_stats(Server* self, PyObject*) {
     Py_DECREF(t);
   }
   PyDict_SetItemString(d, "verb_cpu", vc);  // "verb[/sub]:resource" -> (server-thread CPU s, calls)
+  PyObject* phd = Py_BuildValue("{s:K,s:K,s:K,s:K,s:K,s:K}", "parse", ph[0], "merge", ph[1], "prepare", ph[2],
+                                "finish", ph[3], "emit", ph[4], "reply", ph[5]);
+  PyDict_SetItemString(d, "phase_cycles", phd);
+  Py_DECREF(phd);
   Py_DECREF(vc);
   PyObject* sa = PyLong_FromLongLong(cpu[5]);
   PyDict_SetItemString(d, "admission_slow_path", sa);
@@ -3133,6 +3235,69 @@ PyObject* Server_patch_many(Server* self, PyObject* args) {
   return lst;
 }
 
+// patch_unfinished(group, version, resource, namespace, template, placeholder, subresource="")
+//   -> int: one merge PATCH per object whose status has no completionTime, its body the template
+//   with `placeholder` replaced by the object's name -- the bench's "every job finishes" write,
+//   without a Python round trip per job
+PyObject* Server_patch_unfinished(Server* self, PyObject* args) {
+  const char *g, *v, *r, *ns, *tmpl, *ph, *sub = "";
+  Py_ssize_t tl, pl;
+  if (!PyArg_ParseTuple(args, "sssss#s#|s", &g, &v, &r, &ns, &tmpl, &tl, &ph, &pl, &sub)) return nullptr;
+  Impl* s = self->impl;
+  long long n = 0;
+  bool known = true;
+  std::string gs(g), vs(v), rs(r), nss(ns), subs(sub), ts(tmpl, static_cast<size_t>(tl)),
+      phs(ph, static_cast<size_t>(pl));
+  Py_BEGIN_ALLOW_THREADS
+  {
+    std::lock_guard<std::recursive_mutex> lk(s->mu);
+    Resource* ri = s->find(gs, vs, rs);
+    if (!ri || phs.empty()) {
+      known = false;
+    } else {
+      // the targets first: the patches change the store being walked
+      std::vector<std::pair<std::string, std::string>> todo;
+      for (auto& kv : ri->store->data) {
+        if (!nss.empty() && kv.first != nss) continue;
+        for (auto& ob : kv.second) {
+          const Node* st = ob.second->getn("status");
+          if (st && st->is_obj()) {
+            const Node* ct = st->getn("completionTime");
+            if (ct && ct->t == T::Str && !ct->s.empty()) continue;
+          }
+          todo.emplace_back(kv.first, ob.first);
+        }
+      }
+      std::string body;
+      for (const auto& t : todo) {
+        body.clear();
+        size_t pos = 0;
+        while (true) {
+          const size_t hit = ts.find(phs, pos);
+          if (hit == std::string::npos) {
+            body.append(ts, pos, std::string::npos);
+            break;
+          }
+          body.append(ts, pos, hit - pos);
+          body.append(t.second);  // names are DNS-1123: nothing to escape
+          pos = hit + phs.size();
+        }
+        Ref patch = jdom::parse(body.data(), body.size());
+        if (!patch) continue;
+        ApiErr err;
+        if (s->v_patch(ri, t.first, t.second, patch, "merge", subs, &err)) ++n;
+      }
+    }
+    if (!s->running || std::this_thread::get_id() != s->thread.get_id()) s->end_of_turn();
+  }
+  Py_END_ALLOW_THREADS
+  if (!known) {
+    PyErr_Format(PyExc_KeyError, "unknown resource %s/%s/%s (or an empty placeholder)", g, v, r);
+    return nullptr;
+  }
+  return PyLong_FromLongLong(n);
+}
+
 PyObject* Server_port(Server* self, void*) { return PyLong_FromLong(self->impl->port); }
 
 PyMethodDef Server_methods[] = {
@@ -3156,6 +3321,8 @@ PyMethodDef Server_methods[] = {
      "events kept per resource for watch resume"},
     {"unfinished", reinterpret_cast<PyCFunction>(Server_unfinished), METH_VARARGS,
      "unfinished(group, version, resource, namespace) -> [(name, kind, bytes)] without status.completionTime"},
+    {"patch_unfinished", reinterpret_cast<PyCFunction>(Server_patch_unfinished), METH_VARARGS,
+     "patch_unfinished(group, version, resource, namespace, template, placeholder, subresource='') -> int"},
     {"patch_many", reinterpret_cast<PyCFunction>(Server_patch_many), METH_VARARGS,
      "patch_many(group, version, resource, namespace, [(name, body)], subresource='') -> [resourceVersion|None]"},
     {nullptr, nullptr, 0, nullptr}};

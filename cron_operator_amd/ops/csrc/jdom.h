@@ -89,6 +89,7 @@ struct Node {
   }
 
   uint32_t rc = 0;
+  uint32_t hint = 0;  // a container's expected encoded size (its previous version's), for reserve
   T t = T::Null;
   // passed schema admission at its path (apiserver admission skips such subtrees)
   bool admitted = false;
@@ -187,6 +188,7 @@ inline Ref mk_bool(bool b) { return Ref(new Node(b ? T::True : T::False)); }
 // shallow copy: a private node sharing the children (copy-on-write of one level)
 inline Ref shallow(const Node* n) {
   Node* c = new Node(n->t);
+  c->hint = static_cast<uint32_t>(n->enc.empty() ? n->hint : n->enc.size());
   c->s = n->s;
   c->a = n->a;
   c->o = n->o;
@@ -194,6 +196,13 @@ inline Ref shallow(const Node* n) {
 }
 
 // ------------------------------------------------------------------ parse
+
+// The parser keeps the source bytes of containers at depth 1 and 2 (at least kSpanMin long) as
+// their encoding: the body a client sent is valid JSON for the node it decoded to, so a subtree
+// that reaches the store unchanged -- a job's spec, a status patch's conditions or history -- is
+// never encoded again.  Whoever mutates such a node clears its enc *and its ancestors'*
+// (Node::set/erase clear the node's own; apiserverd's admission reports changes upward).
+constexpr size_t kSpanMin = 24;
 
 class Parser {
  public:
@@ -375,8 +384,11 @@ class Parser {
   // containers collect their children on a scratch stack, then take them at exact capacity
   std::vector<Ref> astack_;
   std::vector<Member> ostack_;
+  size_t dups_ = 0;  // repeated keys seen so far: a span holding one is not its node's encoding
 
   Ref array(int depth) {
+    const char* start = p_;
+    const size_t dups0 = dups_;
     ++p_;
     Node* n = new Node(T::Arr);
     Ref r(n);
@@ -402,12 +414,16 @@ class Parser {
         n->a.reserve(astack_.size() - base);
         for (size_t i = base; i < astack_.size(); ++i) n->a.push_back(std::move(astack_[i]));
         astack_.resize(base);
+        if ((depth == 1 || depth == 2) && static_cast<size_t>(p_ - start) >= kSpanMin && dups_ == dups0)
+          n->enc.assign(start, p_);
         return r;
       }
       return fail("expected ',' or ']'");
     }
   }
   Ref object(int depth) {
+    const char* start = p_;
+    const size_t dups0 = dups_;
     ++p_;
     Node* n = new Node(T::Obj);
     Ref r(n);
@@ -437,6 +453,7 @@ class Parser {
           break;
         }
       if (!dup) ostack_.emplace_back(std::move(k), std::move(v));
+      else ++dups_;
       ws();
       if (p_ >= e_) return fail("unterminated object");
       if (*p_ == ',') {
@@ -448,6 +465,8 @@ class Parser {
         n->o.reserve(ostack_.size() - base);
         for (size_t i = base; i < ostack_.size(); ++i) n->o.push_back(std::move(ostack_[i]));
         ostack_.resize(base);
+        if ((depth == 1 || depth == 2) && static_cast<size_t>(p_ - start) >= kSpanMin && dups_ == dups0)
+          n->enc.assign(start, p_);
         return r;
       }
       return fail("expected ',' or '}'");
@@ -536,7 +555,7 @@ inline void write(std::string* out, Node* n, int depth, int cache_depth) {
     return;
   }
   if (depth < cache_depth) {  // encode into the node's own buffer, then splice it in
-    n->enc.reserve(depth == 0 ? 1024 : 128);
+    n->enc.reserve(n->hint ? n->hint + 64 : (depth == 0 ? 1024 : 128));
     write_body(&n->enc, n, depth, cache_depth);
     out->append(n->enc);
     return;
@@ -547,7 +566,7 @@ inline void write(std::string* out, Node* n, int depth, int cache_depth) {
 // the node's bytes, encoded (and cached) on first use: a stored object's reply and watch events
 inline const std::string& encoded(Node* n) {
   if (n->enc.empty() && (n->t == T::Obj || n->t == T::Arr)) {
-    n->enc.reserve(1024);
+    n->enc.reserve(n->hint ? n->hint + 64 : 1024);
     write_body(&n->enc, n, 0, 2);
   }
   return n->enc;

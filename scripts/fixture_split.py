@@ -59,6 +59,9 @@ def run(shards: int, impl: str, steps: int, warmup: int, crons: int, lifecycle: 
                 per_verb[k] = {"calls_per_fire": round((n1 - n0) / fires, 3),
                                "us_per_call": round((s1 - s0) * 1e6 / (n1 - n0), 1)}
         out["per_verb"] = per_verb
+        # the verbs' phases (TSC cycles per fire; `finish` includes `emit`)
+        out["phase_kcycles_per_fire"] = {k: round((b["phase_cycles"][k] - a["phase_cycles"][k]) / fires / 1000, 1)
+                                         for k in b["phase_cycles"]}
     return out
 
 

@@ -132,6 +132,15 @@ def test_scripted_stream_agrees():
     p.both("PATCH", CRONS + "/c1/status", st, ctype=MERGE)  # no-op: same resourceVersion
     assert p.both("PATCH", CRONS + "/c1/status", {"status": {"lastScheduleTime": "yesterday"}},
                   ctype=MERGE)[0] == 422
+    # pruning inside a subtree whose request bytes the native parser keeps as its encoding
+    pruned = p.both("PATCH", CRONS + "/c1/status", {"status": {"history": [
+        {"uid": "u1", "object": {"kind": "PyTorchJob", "name": "c1-0", "extra": True}, "status": "Succeeded",
+         "bogus": 1}]}}, ctype=MERGE)[1]
+    assert "bogus" not in pruned["status"]["history"][0]
+    # a repeated key: the last value wins, and the bytes sent are not the stored object's
+    p.both("PATCH", CRONS + "/c1/status", b'{"status":{"history":[{"uid":"u2","uid":"u3","object":{"kind":"PyTorchJob",'
+                                          b'"name":"c1-9"},"status":"Failed"}]}}', ctype=MERGE)
+    assert p.nat_call("GET", CRONS + "/c1", "", b"", "")[1]["status"]["history"][0]["uid"] == "u3"
     p.both("PATCH", CRONS + "/c1", {"status": {"active": None}, "metadata": {"labels": {"a": "1"}}}, ctype=MERGE)
     spec = p.both("PATCH", CRONS + "/c1", {"spec": {"suspend": True}}, ctype=MERGE)[1]
     assert spec["metadata"]["generation"] == 2
