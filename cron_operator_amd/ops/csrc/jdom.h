@@ -319,9 +319,31 @@ class Parser {
     *out = v;
     return true;
   }
+  // bytes that end a plain run inside a string: the quote, a backslash, control characters
+  static const bool* special() {
+    static const struct T {
+      bool t[256];
+      T() : t() {
+        for (int i = 0; i < 0x20; ++i) t[i] = true;
+        t[static_cast<unsigned char>('"')] = true;
+        t[static_cast<unsigned char>('\\')] = true;
+      }
+    } tab;
+    return tab.t;
+  }
+
   bool string(std::string* out) {
     ++p_;  // opening quote
+    const bool* sp = special();
     const char* run = p_;
+    while (p_ < e_ && !sp[static_cast<unsigned char>(*p_)]) ++p_;
+    if (p_ < e_ && *p_ == '"') {  // no escapes: one copy at its final size
+      out->assign(run, static_cast<size_t>(p_ - run));
+      ++p_;
+      return true;
+    }
+    out->assign(run, static_cast<size_t>(p_ - run));
+    run = p_;
     while (true) {
       if (p_ >= e_) {
         fail("unterminated string");
@@ -436,8 +458,8 @@ class Parser {
     while (true) {
       ws();
       if (p_ >= e_ || *p_ != '"') return fail("expected property name");
-      std::string k;
-      if (!string(&k)) return Ref();
+      ostack_.emplace_back();
+      if (!string(&ostack_.back().first)) return Ref();
       ws();
       if (p_ >= e_ || *p_ != ':') return fail("expected ':'");
       ++p_;
@@ -445,15 +467,20 @@ class Parser {
       Ref v = value(depth + 1);
       if (!v) return Ref();
       // a repeated key keeps the last value, as Python's json does
+      const std::string& k = ostack_.back().first;
       bool dup = false;
-      for (size_t i = base; i < ostack_.size(); ++i)
+      for (size_t i = base; i + 1 < ostack_.size(); ++i)
         if (ostack_[i].first == k) {
           ostack_[i].second = std::move(v);
           dup = true;
           break;
         }
-      if (!dup) ostack_.emplace_back(std::move(k), std::move(v));
-      else ++dups_;
+      if (dup) {
+        ostack_.pop_back();
+        ++dups_;
+      } else {
+        ostack_.back().second = std::move(v);
+      }
       ws();
       if (p_ >= e_) return fail("unterminated object");
       if (*p_ == ',') {
