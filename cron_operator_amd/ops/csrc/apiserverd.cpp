@@ -63,6 +63,9 @@ using jdom::T;
 
 namespace {
 
+// a node's string (pooled) as a std::string, for messages and map keys
+inline std::string S(std::string_view v) { return std::string(v); }
+
 // ====================================================================== errors
 
 struct ApiErr {
@@ -144,8 +147,8 @@ std::string rfc3339(long long now_ns) {
 bool is_digit(char c) { return c >= '0' && c <= '9'; }
 
 // ^\d{4}-\d{2}-\d{2}[Tt]\d{2}:\d{2}:\d{2}(\.\d+)?([Zz]|[+-]\d{2}:\d{2})$
-bool is_date_time(const std::string& s) {
-  const char* p = s.c_str();
+bool is_date_time(std::string_view s) {
+  const char* p = s.data();
   const char* e = p + s.size();
   auto digits = [&](int n) {
     for (int i = 0; i < n; ++i, ++p)
@@ -457,11 +460,16 @@ struct Selector {
     return true;
   }
 
-  static const std::string* label(const Node* labels, const std::string& k) {
+  static const jdom::jstr* label(const Node* labels, std::string_view k) {
     if (!labels) return nullptr;
     const Ref* r = labels->get(k);
     if (!r) return nullptr;
     return (*r)->t == T::Str ? &(*r)->s : nullptr;
+  }
+  static bool in(const std::vector<std::string>& vals, std::string_view v) {
+    for (const auto& x : vals)
+      if (x == v) return true;
+    return false;
   }
 
   static std::string field_value(const Node* obj, const std::vector<std::string>& path) {
@@ -473,8 +481,8 @@ struct Selector {
     }
     if (!cur || cur->t == T::Null) return "";
     switch (cur->t) {
-      case T::Str: return cur->s;
-      case T::Num: return cur->s;
+      case T::Str: return S(cur->s);
+      case T::Num: return S(cur->s);
       case T::True: return "True";
       case T::False: return "False";
       default: return jdom::dump(const_cast<Node*>(cur), 0);
@@ -489,19 +497,19 @@ struct Selector {
       const Node* lb = (meta && meta->is_obj()) ? meta->getn("labels") : nullptr;
       if (lb && !lb->is_obj()) lb = nullptr;
       for (const auto& r : labels) {
-        const std::string* v = label(lb, r.key);
+        const jdom::jstr* v = label(lb, r.key);
         switch (r.op) {
           case 0:
-            if (!v || *v != r.vals[0]) return false;
+            if (!v || std::string_view(*v) != r.vals[0]) return false;
             break;
           case 1:
-            if (v && *v == r.vals[0]) return false;
+            if (v && std::string_view(*v) == r.vals[0]) return false;
             break;
           case 2:
-            if (!v || std::find(r.vals.begin(), r.vals.end(), *v) == r.vals.end()) return false;
+            if (!v || !in(r.vals, *v)) return false;
             break;
           case 3:
-            if (v && std::find(r.vals.begin(), r.vals.end(), *v) != r.vals.end()) return false;
+            if (v && in(r.vals, *v)) return false;
             break;
           case 4:
             if (!v) {
@@ -530,7 +538,7 @@ struct Schema {
   std::string type;
   bool nullable = false, preserve = false, date_time = false;
   bool has_enum = false;
-  std::vector<Ref> enumv;
+  jdom::RefVec enumv;
   bool has_min = false, has_max = false;
   double min = 0, max = 0;
   Ref min_lex, max_lex;
@@ -543,7 +551,7 @@ struct Schema {
   std::unique_ptr<Schema> items;
   bool any = true;  // not a dict schema: accepts anything
 
-  const Schema* prop(const std::string& k) const {
+  const Schema* prop(std::string_view k) const {
     for (const auto& p : props)
       if (p.first == k) return p.second.get();
     return nullptr;
@@ -588,7 +596,7 @@ struct Schema {
     if (const Node* r = s->getn("required"))
       if (r->is_arr())
         for (const Ref& x : r->a)
-          if (x->is_str()) out->required.push_back(x->s);
+          if (x->is_str()) out->required.push_back(S(x->s));
     if (const Node* a = s->getn("additionalProperties")) {
       if (a->is_obj()) out->addl = compile(a);
       else if (a->t == T::True) out->addl_true = true;
@@ -642,7 +650,7 @@ struct Schema {
       const bool keep_unknown = preserve || (!has_props && !addl && !addl_true);
       if (!keep_unknown && !addl && !addl_true) {
         for (size_t i = 0; i < v->o.size();) {
-          const std::string& k = v->o[i].first;
+          const jdom::jstr& k = v->o[i].first;
           if (prop(k) || (root && (k == "apiVersion" || k == "kind" || k == "metadata"))) {
             ++i;
             continue;
@@ -702,7 +710,7 @@ struct Schema {
             "Invalid value: \"" + gt + "\": " + fld + " in body must be of type " + type + ": \"" + gt + "\"");
       return;
     }
-    auto lex = [](const Node* n) { return n->t == T::Str ? n->s : jdom::dump(const_cast<Node*>(n), 0); };
+    auto lex = [](const Node* n) { return n->t == T::Str ? S(n->s) : jdom::dump(const_cast<Node*>(n), 0); };
     if (has_enum) {
       bool hit = false;
       for (const Ref& e : enumv)
@@ -718,15 +726,15 @@ struct Schema {
     }
     if (date_time && v->t == T::Str && !is_date_time(v->s))
       cause(fld, "FieldValueInvalid",
-            "Invalid value: \"" + v->s + "\": " + fld + " in body must be of type date-time: \"" + v->s + "\"");
+            "Invalid value: \"" + S(v->s) + "\": " + fld + " in body must be of type date-time: \"" + S(v->s) + "\"");
     if (v->t == T::Num) {
       const double d = std::strtod(v->s.c_str(), nullptr);
       if (has_min && d < min)
-        cause(fld, "FieldValueInvalid", "Invalid value: " + v->s + ": " + fld +
-                                            " in body should be greater than or equal to " + min_lex->s);
+        cause(fld, "FieldValueInvalid", "Invalid value: " + S(v->s) + ": " + fld +
+                                            " in body should be greater than or equal to " + S(min_lex->s));
       if (has_max && d > max)
-        cause(fld, "FieldValueInvalid", "Invalid value: " + v->s + ": " + fld +
-                                            " in body should be less than or equal to " + max_lex->s);
+        cause(fld, "FieldValueInvalid", "Invalid value: " + S(v->s) + ": " + fld +
+                                            " in body should be less than or equal to " + S(max_lex->s));
     }
     if (v->t == T::Obj) {
       for (const auto& r : required)
@@ -738,7 +746,7 @@ struct Schema {
       }
       if (addl)
         for (const Member& m : v->o)
-          if (!prop(m.first)) addl->errors(m.second.get(), path.empty() ? m.first : path + "[" + m.first + "]", out,
+          if (!prop(m.first)) addl->errors(m.second.get(), path.empty() ? S(m.first) : path + "[" + S(m.first) + "]", out,
                                            false);
     } else if (v->t == T::Arr && items) {
       for (size_t i = 0; i < v->a.size(); ++i)
@@ -786,10 +794,9 @@ const Node* labels_of(const Node* obj) {
   return (l && l->is_obj()) ? l : nullptr;
 }
 
-const std::string& meta_str(const Node* obj, const char* k) {
-  static const std::string empty;
+std::string_view meta_str(const Node* obj, const char* k) {
   const Node* m = obj->getn("metadata");
-  if (!m || !m->is_obj()) return empty;
+  if (!m || !m->is_obj()) return std::string_view();
   return m->str(k);
 }
 
@@ -1049,7 +1056,7 @@ struct Impl {
     const Node* spec = crd->getn("spec");
     if (!spec || !spec->is_obj()) return;
     const Node* names = spec->getn("names");
-    const std::string group = spec->str("group");
+    const std::string group = S(spec->str("group"));
     const bool namespaced = spec->str("scope").empty() || spec->str("scope") == "Namespaced";
     std::string plural, kind, singular;
     std::vector<std::string> sn;
@@ -1060,7 +1067,7 @@ struct Impl {
       if (const Node* s = names->getn("shortNames"))
         if (s->is_arr())
           for (const Ref& x : s->a)
-            if (x->is_str()) sn.push_back(x->s);
+            if (x->is_str()) sn.push_back(S(x->s));
     }
     if (const Node* vs = spec->getn("versions"))
       if (vs->is_arr())
@@ -1074,7 +1081,7 @@ struct Impl {
               if (const Ref* oa = sc->get("openAPIV3Schema")) schema = *oa;
           const Node* subs = v->getn("subresources");
           const bool st = subs && subs->is_obj() && subs->get("status");
-          add_resource(group, v->str("name"), plural, kind, namespaced, st, true, false, singular, sn, {}, schema);
+          add_resource(group, S(v->str("name")), plural, kind, namespaced, st, true, false, singular, sn, {}, schema);
         }
     // mark Established like the apiextensions controller
     Ref status = jdom::mk_obj();
@@ -1108,23 +1115,23 @@ struct Impl {
     const Node* nl = neu ? labels_of(neu) : nullptr;
     if (old && neu && (ol == nl || (ol && nl && jdom::equal(ol, nl)))) return;
     for (auto& kv : st->idx) {
-      const std::string* ov = ol ? Selector::label(ol, kv.first) : nullptr;
-      const std::string* nv = nl ? Selector::label(nl, kv.first) : nullptr;
+      const jdom::jstr* ov = ol ? Selector::label(ol, kv.first) : nullptr;
+      const jdom::jstr* nv = nl ? Selector::label(nl, kv.first) : nullptr;
       if (old && neu && ((!ov && !nv) || (ov && nv && *ov == *nv))) continue;
       if (ov) {
-        auto a = kv.second.find(*ov);
+        auto a = kv.second.find(S(*ov));
         if (a != kv.second.end()) {
           auto b = a->second.find(ns);
           if (b != a->second.end()) b->second.erase(name);
         }
       }
-      if (nv) kv.second[*nv][ns].insert(name);
+      if (nv) kv.second[S(*nv)][ns].insert(name);
     }
   }
 
   void put_raw(Resource* ri, const std::string& ns_in, const Ref& obj) {
     const std::string ns = ri->namespaced ? ns_in : std::string();
-    const std::string& name = meta_str(obj.get(), "name");
+    const std::string name = S(meta_str(obj.get(), "name"));
     auto& slot = ri->store->data[ns][name];
     Ref old = slot;
     slot = obj;
@@ -1239,14 +1246,14 @@ struct Impl {
     std::string msg;
     for (size_t i = 0; i < causes.size(); ++i) {
       if (i) msg += "; ";
-      msg += causes[i]->str("field") + ": " + causes[i]->str("message");
+      msg += S(causes[i]->str("field")) + ": " + S(causes[i]->str("message"));
     }
     ApiErr e = mkerr(422, "Invalid", ri->group.empty() ? ri->kind + " \"" + name + "\" is invalid: " + msg
                                                        : ri->kind + "." + ri->group + " \"" + name +
                                                              "\" is invalid: " + msg);
     Ref d = name_details(name, ri->group, ri->kind);
     Ref arr = jdom::mk_arr();
-    arr->a = causes;
+    arr->a.assign(causes.begin(), causes.end());
     d->o.emplace_back("causes", arr);
     e.details = d;
     return e;
@@ -1296,7 +1303,7 @@ struct Impl {
     Node* m = meta.get();
     std::string ns = url_ns;
     if (ri->namespaced) {
-      const std::string& bns = m->str("namespace");
+      const std::string bns = S(m->str("namespace"));
       if (!bns.empty() && !ns.empty() && bns != ns) {
         *err = bad_request("the namespace of the provided object does not match the namespace sent on the request");
         return Ref();
@@ -1310,11 +1317,11 @@ struct Impl {
     if (ri->virt) return review(ri, body);
     b->set("apiVersion", jdom::mk_str(ri->api_version));
     b->set("kind", jdom::mk_str(ri->kind));
-    std::string name = m->str("name");
+    std::string name = S(m->str("name"));
     if (name.empty() && !m->str("generateName").empty()) {
       static const char chars[] = "bcdfghjklmnpqrstvwxz2456789";
       for (int i = 0; i < 16; ++i) {
-        std::string cand = m->str("generateName");
+        std::string cand = S(m->str("generateName"));
         for (int j = 0; j < 5; ++j) cand.push_back(chars[rng() % (sizeof(chars) - 1)]);
         if (!get_raw(ri, ns, cand)) {
           name = cand;
@@ -1412,7 +1419,7 @@ struct Impl {
       }
       if (ri->schema) {
         const Ref* st = neu->get("status");
-        if (st && (*st)->t != T::Null && !admit_status(ri, st->get(), om->str("name"), err)) return Ref();
+        if (st && (*st)->t != T::Null && !admit_status(ri, st->get(), S(om->str("name")), err)) return Ref();
       }
       *nm_out = nm.get();
       return neu;
@@ -1440,9 +1447,9 @@ struct Impl {
       if (const Ref* st = old->get("status")) neu->set("status", *st);
       else neu->erase("status");
     }
-    if (!admit_object(ri, neu.get(), om->str("name"), err)) return Ref();
+    if (!admit_object(ri, neu.get(), S(om->str("name")), err)) return Ref();
     bool spec_changed = false;
-    auto skip = [](const std::string& k) {
+    auto skip = [](std::string_view k) {
       return k == "metadata" || k == "status" || k == "apiVersion" || k == "kind";
     };
     for (const Member& mm : old->o)
@@ -1451,7 +1458,7 @@ struct Impl {
         if (!nv || !jdom::equal(mm.second.get(), nv->get())) spec_changed = true;
       }
     for (const Member& mm : neu->o)
-      if (!skip(mm.first) && !old->get(mm.first)) spec_changed = true;
+      if (!skip(mm.first) && !old->get(std::string_view(mm.first))) spec_changed = true;
     if (spec_changed) {
       long long g = 1;
       if (const Node* gv = om->getn("generation"))
@@ -1476,7 +1483,7 @@ struct Impl {
       *err = not_found(ri->resource, ri->group, name);
       return Ref();
     }
-    const std::string brv = (bm && bm->is_obj()) ? bm->str("resourceVersion") : std::string();
+    const std::string_view brv = (bm && bm->is_obj()) ? bm->str("resourceVersion") : std::string_view();
     if (!brv.empty() && brv != meta_str(old.get(), "resourceVersion")) {
       *err = conflict(ri->resource, ri->group, name, kModified);
       return Ref();
@@ -1507,7 +1514,7 @@ struct Impl {
       return Ref();
     }
     const Node* pm = patch->getn("metadata");
-    const std::string prv = (pm && pm->is_obj()) ? pm->str("resourceVersion") : std::string();
+    const std::string_view prv = (pm && pm->is_obj()) ? pm->str("resourceVersion") : std::string_view();
     if (!prv.empty() && prv != meta_str(old.get(), "resourceVersion")) {
       *err = conflict(ri->resource, ri->group, name, kModified);
       return Ref();
@@ -1553,13 +1560,13 @@ struct Impl {
     }
     const Node* om = old->getn("metadata");
     if (pre && pre->is_obj()) {
-      const std::string puid = pre->str("uid");
+      const std::string puid = S(pre->str("uid"));
       if (!puid.empty() && puid != om->str("uid")) {
         *err = conflict(ri->resource, ri->group, name, "Precondition failed: UID in precondition: " + puid +
-                                                           ", UID in object meta: " + om->str("uid"));
+                                                           ", UID in object meta: " + S(om->str("uid")));
         return Ref();
       }
-      const std::string prv = pre->str("resourceVersion");
+      const std::string_view prv = pre->str("resourceVersion");
       if (!prv.empty() && prv != om->str("resourceVersion")) {
         *err = conflict(ri->resource, ri->group, name, "Precondition failed: ResourceVersion mismatch");
         return Ref();
@@ -1618,8 +1625,8 @@ struct Impl {
         auto& by_val = st->idx[sel.pin_key];
         for (auto& nsk : st->data)
           for (auto& ob : nsk.second) {
-            const std::string* v = Selector::label(labels_of(ob.second.get()), sel.pin_key);
-            if (v) by_val[*v][nsk.first].insert(ob.first);
+            const jdom::jstr* v = Selector::label(labels_of(ob.second.get()), sel.pin_key);
+            if (v) by_val[S(*v)][nsk.first].insert(ob.first);
           }
         it = st->idx.find(sel.pin_key);
       }
@@ -1652,7 +1659,7 @@ struct Impl {
         if (!first) items.push_back(',');
         first = false;
         jdom::write(&items, obj.get());
-        last_key = meta_str(obj.get(), "namespace") + "/" + name;
+        last_key = S(meta_str(obj.get(), "namespace")) + "/" + name;
         ++n;
         return true;
       };
@@ -2199,7 +2206,7 @@ struct Impl {
 
   void write_reply(Conn* c, const Reply& rep, bool keep) {
     PhaseTimer pt(&phase[kReply]);
-    const std::string& body = rep.obj ? jdom::encoded(rep.obj.get()) : rep.body;
+    const std::string_view body = rep.obj ? std::string_view(jdom::encoded(rep.obj.get())) : std::string_view(rep.body);
     std::string& o = c->out;
     o.append("HTTP/1.1 ");
     o.append(std::to_string(rep.status));
@@ -2902,7 +2909,7 @@ PyObject* Server_request(Server* self, PyObject* args, PyObject* kw) {
   }
   Py_END_ALLOW_THREADS
   if (!handled) return Py_BuildValue("(iy)", 404, "");
-  const std::string& body = rep.obj ? jdom::encoded(rep.obj.get()) : rep.body;
+  const std::string_view body = rep.obj ? std::string_view(jdom::encoded(rep.obj.get())) : std::string_view(rep.body);
   return Py_BuildValue("(iy#)", rep.status, body.data(), static_cast<Py_ssize_t>(body.size()));
 }
 

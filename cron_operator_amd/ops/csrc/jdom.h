@@ -10,17 +10,114 @@
 //
 // Reference counts are not atomic: every tree is touched by the server thread only (Python
 // entry points take the server's lock first).
+//
+// Memory: a write builds tens of nodes, member vectors, strings and 1-4 KiB encodings, and
+// retiring a version frees as many.  glibc's malloc cost as much as the JSON work itself (gprof
+// of the standalone driver: _int_malloc + malloc_consolidate + _int_free ~40%), so nodes come
+// from a free list and every container and string of a tree from size-class free lists
+// (PoolAlloc: thread-local LIFO lists, no header -- the containers pass the size back).  Only
+// this header's types use them: nothing crosses into libstdc++'s own allocations.
 #pragma once
 
 #include <cmath>
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <new>
 #include <string>
+#include <string_view>
 #include <utility>
 #include <vector>
 
 namespace jdom {
+
+namespace pool {
+
+constexpr size_t kMax = 16384;  // larger blocks go to operator new
+constexpr int kClasses = 48;
+constexpr uint32_t kMaxFree = 1u << 15;  // spare blocks kept per class and thread
+
+struct Tables {
+  size_t size[kClasses] = {};
+  unsigned char by16[(kMax >> 4) + 1] = {};
+  int n = 0;
+  Tables() {
+    size_t s = 16;
+    while (s < kMax && n < kClasses - 1) {
+      size[n++] = s;
+      s = s < 256 ? s + 16 : (s + s / 4 + 15) / 16 * 16;
+    }
+    size[n++] = kMax;
+    int c = 0;
+    for (size_t i = 0; i <= (kMax >> 4); ++i) {
+      while (size[c] < (i << 4)) ++c;
+      by16[i] = static_cast<unsigned char>(c);
+    }
+  }
+};
+
+inline const Tables& tables() {
+  static const Tables t;
+  return t;
+}
+
+struct Lists {
+  void* head[kClasses] = {};
+  uint32_t count[kClasses] = {};
+};
+
+inline Lists& lists() {
+  static thread_local Lists l;
+  return l;
+}
+
+inline void* alloc(size_t n) {
+  if (n > kMax) return ::operator new(n);
+  const Tables& t = tables();
+  const unsigned c = t.by16[(n + 15) >> 4];
+  Lists& l = lists();
+  if (void* b = l.head[c]) {
+    l.head[c] = *static_cast<void**>(b);
+    --l.count[c];
+    return b;
+  }
+  return ::operator new(t.size[c]);
+}
+
+inline void release(void* p, size_t n) noexcept {
+  if (!p) return;
+  if (n > kMax) {
+    ::operator delete(p);
+    return;
+  }
+  const unsigned c = tables().by16[(n + 15) >> 4];
+  Lists& l = lists();
+  if (l.count[c] >= kMaxFree) {
+    ::operator delete(p);
+    return;
+  }
+  *static_cast<void**>(p) = l.head[c];
+  l.head[c] = p;
+  ++l.count[c];
+}
+
+}  // namespace pool
+
+template <class T>
+struct PoolAlloc {
+  using value_type = T;
+  PoolAlloc() noexcept = default;
+  template <class U>
+  PoolAlloc(const PoolAlloc<U>&) noexcept {}  // NOLINT: rebinding
+  T* allocate(size_t n) { return static_cast<T*>(pool::alloc(n * sizeof(T))); }
+  void deallocate(T* p, size_t n) noexcept { pool::release(p, n * sizeof(T)); }
+  template <class U>
+  bool operator==(const PoolAlloc<U>&) const noexcept { return true; }
+  template <class U>
+  bool operator!=(const PoolAlloc<U>&) const noexcept { return false; }
+};
+
+using jstr = std::basic_string<char, std::char_traits<char>, PoolAlloc<char>>;
 
 enum class T : uint8_t { Null, False, True, Num, Str, Arr, Obj };
 
@@ -47,7 +144,9 @@ class Ref {
   Node* p_ = nullptr;
 };
 
-using Member = std::pair<std::string, Ref>;
+using Member = std::pair<jstr, Ref>;
+using RefVec = std::vector<Ref, PoolAlloc<Ref>>;
+using MemberVec = std::vector<Member, PoolAlloc<Member>>;
 
 // Nodes come and go by the tens per request (a parsed body, merge results, tombstones): a free
 // list keeps them out of malloc, where they cost more than the JSON work itself (gprof of the
@@ -93,10 +192,10 @@ struct Node {
   T t = T::Null;
   // passed schema admission at its path (apiserver admission skips such subtrees)
   bool admitted = false;
-  std::string s;              // Str: the value (unescaped); Num: the lexeme as sent
-  std::vector<Ref> a;         // Arr
-  std::vector<Member> o;      // Obj, insertion order
-  std::string enc;            // Arr/Obj: cached serialisation ("" = not cached)
+  jstr s;                     // Str: the value (unescaped); Num: the lexeme as sent
+  RefVec a;                   // Arr
+  MemberVec o;                // Obj, insertion order
+  jstr enc;                   // Arr/Obj: cached serialisation ("" = not cached)
 
   explicit Node(T t_) : t(t_) {}
 
@@ -110,23 +209,23 @@ struct Node {
       if (m.first.size() == n && std::memcmp(m.first.data(), k, n) == 0) return &m.second;
     return nullptr;
   }
-  const Ref* get(const std::string& k) const { return get(k.data(), k.size()); }
+  const Ref* get(std::string_view k) const { return get(k.data(), k.size()); }
   const Ref* get(const char* k) const { return get(k, std::strlen(k)); }
   Node* getn(const char* k) const {
     const Ref* r = get(k);
     return r ? r->get() : nullptr;
   }
   // string member value ("" when absent or not a string)
-  const std::string& str(const char* k) const;
+  std::string_view str(const char* k) const;
   // set/replace a member (the node must be private to the caller: fresh, not stored)
-  void set(const std::string& k, Ref v) {
+  void set(std::string_view k, Ref v) {
     enc.clear();
     for (auto& m : o)
-      if (m.first == k) {
+      if (std::string_view(m.first) == k) {
         m.second = std::move(v);
         return;
       }
-    o.emplace_back(k, std::move(v));
+    o.emplace_back(jstr(k), std::move(v));
   }
   bool erase(const char* k) {
     const size_t n = std::strlen(k);
@@ -164,20 +263,21 @@ inline Ref& Ref::operator=(Ref&& o) noexcept {
   return *this;
 }
 
-inline const std::string& Node::str(const char* k) const {
-  static const std::string empty;
+inline std::string_view Node::str(const char* k) const {
   const Ref* r = get(k);
-  return (r && (*r)->t == T::Str) ? (*r)->s : empty;
+  return (r && (*r)->t == T::Str) ? std::string_view((*r)->s) : std::string_view();
 }
 
-inline Ref mk_str(std::string v) {
+inline Ref mk_str(std::string_view v) {
   Node* n = new Node(T::Str);
-  n->s = std::move(v);
+  n->s.assign(v.data(), v.size());
   return Ref(n);
 }
 inline Ref mk_num(long long v) {
   Node* n = new Node(T::Num);
-  n->s = std::to_string(v);
+  char buf[24];
+  const int len = snprintf(buf, sizeof buf, "%lld", v);
+  n->s.assign(buf, static_cast<size_t>(len));
   return Ref(n);
 }
 inline Ref mk_obj() { return Ref(new Node(T::Obj)); }
@@ -287,7 +387,7 @@ class Parser {
     n->s.assign(b, static_cast<size_t>(p_ - b));
     return Ref(n);
   }
-  static void put_utf8(std::string* out, unsigned cp) {
+  static void put_utf8(jstr* out, unsigned cp) {
     if (cp < 0x80) {
       out->push_back(static_cast<char>(cp));
     } else if (cp < 0x800) {
@@ -332,7 +432,7 @@ class Parser {
     return tab.t;
   }
 
-  bool string(std::string* out) {
+  bool string(jstr* out) {
     ++p_;  // opening quote
     const bool* sp = special();
     const char* run = p_;
@@ -467,7 +567,7 @@ class Parser {
       Ref v = value(depth + 1);
       if (!v) return Ref();
       // a repeated key keeps the last value, as Python's json does
-      const std::string& k = ostack_.back().first;
+      const jstr& k = ostack_.back().first;
       bool dup = false;
       for (size_t i = base; i + 1 < ostack_.size(); ++i)
         if (ostack_[i].first == k) {
@@ -510,7 +610,8 @@ inline Ref parse(const char* b, size_t n, std::string* err = nullptr) {
 
 // ------------------------------------------------------------------ serialise
 
-inline void put_string(std::string* out, const std::string& s) {
+template <class S>
+inline void put_string(S* out, std::string_view s) {
   static const char* hex = "0123456789abcdef";
   out->push_back('"');
   const char* b = s.data();
@@ -542,9 +643,11 @@ inline void put_string(std::string* out, const std::string& s) {
 // Write `n`.  Containers at depth < cache_depth keep their bytes (n->enc) for the next write --
 // the object itself and its top-level members, so a status write re-encodes status and metadata
 // and splices in the cached spec; a container that already has them is appended as is.
-inline void write(std::string* out, Node* n, int depth = 0, int cache_depth = 2);
+template <class S>
+inline void write(S* out, Node* n, int depth = 0, int cache_depth = 2);
 
-inline void write_body(std::string* out, Node* n, int depth, int cache_depth) {
+template <class S>
+inline void write_body(S* out, Node* n, int depth, int cache_depth) {
   if (n->t == T::Arr) {
     out->push_back('[');
     bool first = true;
@@ -568,30 +671,31 @@ inline void write_body(std::string* out, Node* n, int depth, int cache_depth) {
   }
 }
 
-inline void write(std::string* out, Node* n, int depth, int cache_depth) {
+template <class S>
+inline void write(S* out, Node* n, int depth, int cache_depth) {
   switch (n->t) {
     case T::Null: out->append("null"); return;
     case T::True: out->append("true"); return;
     case T::False: out->append("false"); return;
-    case T::Num: out->append(n->s); return;
+    case T::Num: out->append(n->s.data(), n->s.size()); return;
     case T::Str: put_string(out, n->s); return;
     default: break;
   }
   if (!n->enc.empty()) {
-    out->append(n->enc);
+    out->append(n->enc.data(), n->enc.size());
     return;
   }
   if (depth < cache_depth) {  // encode into the node's own buffer, then splice it in
     n->enc.reserve(n->hint ? n->hint + 64 : (depth == 0 ? 1024 : 128));
     write_body(&n->enc, n, depth, cache_depth);
-    out->append(n->enc);
+    out->append(n->enc.data(), n->enc.size());
     return;
   }
   write_body(out, n, depth, cache_depth);
 }
 
 // the node's bytes, encoded (and cached) on first use: a stored object's reply and watch events
-inline const std::string& encoded(Node* n) {
+inline const jstr& encoded(Node* n) {
   if (n->enc.empty() && (n->t == T::Obj || n->t == T::Arr)) {
     n->enc.reserve(n->hint ? n->hint + 64 : 1024);
     write_body(&n->enc, n, 0, 2);
@@ -607,7 +711,7 @@ inline std::string dump(Node* n, int cache_depth = 2) {
 
 // ------------------------------------------------------------------ compare / merge
 
-inline bool num_equal(const std::string& a, const std::string& b) {
+inline bool num_equal(const jstr& a, const jstr& b) {
   if (a == b) return true;
   return std::strtod(a.c_str(), nullptr) == std::strtod(b.c_str(), nullptr);
 }
@@ -633,7 +737,7 @@ inline bool equal(const Node* a, const Node* b) {
       for (size_t i = 0; i < a->o.size(); ++i) {
         const Member& m = a->o[i];
         // same key order (the common case) first, then a lookup
-        const Ref* bv = (b->o[i].first == m.first) ? &b->o[i].second : b->get(m.first);
+        const Ref* bv = (b->o[i].first == m.first) ? &b->o[i].second : b->get(std::string_view(m.first));
         if (!bv || !equal(m.second.get(), bv->get())) return false;
       }
       return true;
@@ -656,7 +760,7 @@ inline Ref merge_patch(const Ref& target, const Ref& patch) {
         }
       continue;
     }
-    const Ref* cur = o->get(m.first);
+    const Ref* cur = o->get(std::string_view(m.first));
     Ref merged = merge_patch(cur ? *cur : Ref(), m.second);
     if (cur) {
       for (auto& mm : o->o)

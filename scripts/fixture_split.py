@@ -21,7 +21,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def run(shards: int, impl: str, steps: int, warmup: int, crons: int, lifecycle: str) -> dict:
+def run(shards: int, impl: str, steps: int, warmup: int, crons: int, lifecycle: str,
+        watch_window: int = 20_000) -> dict:
     from cron_operator_amd.bench import harness
 
     snaps = []
@@ -37,7 +38,8 @@ def run(shards: int, impl: str, steps: int, warmup: int, crons: int, lifecycle: 
     harness._cpu_times = cpu
     try:
         res = harness.run_sync(harness.BenchConfig(n_crons=crons, steps=steps, warmup=warmup, shards=shards,
-                                                   lifecycle=lifecycle, apiserver_impl=impl))
+                                                   lifecycle=lifecycle, apiserver_impl=impl,
+                                                   watch_window=watch_window))
     finally:
         harness._cpu_times = orig
     fires = crons * steps
@@ -74,13 +76,14 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--crons", type=int, default=1000)
     ap.add_argument("--lifecycle", default="instant", choices=["instant", "realistic"])
+    ap.add_argument("--watch-window", type=int, default=20_000)
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     rows = []
     for rep in range(a.reps):
         for impl in a.impl:
             for shards in a.shards:
-                r = run(shards, impl, a.steps, a.warmup, a.crons, a.lifecycle)
+                r = run(shards, impl, a.steps, a.warmup, a.crons, a.lifecycle, a.watch_window)
                 r["rep"] = rep
                 rows.append(r)
                 print(json.dumps(r), flush=True)
