@@ -48,6 +48,58 @@ def _status_body(code: int, reason: str, message: str) -> bytes:
                        "message": message, "reason": reason, "code": code}).encode()
 
 
+def profile_report(stacks, dropped: int = 0, top: int = 40) -> str:
+    """Rank the sampled stacks' functions (addr2line resolves the frames; frames outside a file
+    addr2line can read keep their module's name)."""
+    import collections
+    import os
+    import subprocess
+
+    names: Dict[Tuple[str, int], str] = {}
+    by_mod: Dict[str, set] = collections.defaultdict(set)
+    for st in stacks:
+        for mod, off in st:
+            by_mod[mod].add(off)
+    for mod, offs in by_mod.items():
+        offs = sorted(offs)
+        resolved = ["?"] * len(offs)
+        if os.path.exists(mod):
+            try:
+                out = subprocess.run(["addr2line", "-f", "-C", "-e", mod] + [hex(o) for o in offs],
+                                     capture_output=True, text=True, timeout=60).stdout.splitlines()
+                resolved = [out[2 * i] if 2 * i < len(out) else "?" for i in range(len(offs))]
+            except (OSError, subprocess.SubprocessError):
+                pass
+        base = os.path.basename(mod)
+        for o, fn in zip(offs, resolved):
+            names[(mod, o)] = f"{fn} [{base}]" if fn != "??" else f"?? [{base}+{o:#x}]"
+    self_c: collections.Counter = collections.Counter()
+    incl_c: collections.Counter = collections.Counter()
+    for st in stacks:
+        if not st:
+            continue
+        self_c[names[st[0]]] += 1
+        for f in {names[x] for x in st}:
+            incl_c[f] += 1
+    # which of the server's own functions the time outside it (malloc, memcpy, syscalls) is spent for
+    via: collections.Counter = collections.Counter()
+    for st in stacks:
+        if not st or "_apiserverd" in names[st[0]]:
+            continue
+        own = next((names[x] for x in st if "_apiserverd" in names[x]), None)
+        if own is not None:
+            via[f"{names[st[0]]}  <-  {own}"] += 1
+    n = max(1, len(stacks))
+    out = [f"# {len(stacks)} samples ({dropped} dropped) of the fake apiserver process on its CPU time\n",
+           "\n## by self samples\n"]
+    out += [f"{100.0 * c / n:6.2f}%  {k}\n" for k, c in self_c.most_common(top)]
+    out.append("\n## by inclusive samples\n")
+    out += [f"{100.0 * c / n:6.2f}%  {k}\n" for k, c in incl_c.most_common(top)]
+    out.append("\n## time outside the extension, by the extension function it ran for\n")
+    out += [f"{100.0 * c / n:6.2f}%  {k}\n" for k, c in via.most_common(top)]
+    return "".join(out)
+
+
 class NativeAPIServer:
     """A ``_apiserverd.Server`` with the CRDs installed and the ``/debug/fake`` controls."""
 
@@ -154,9 +206,17 @@ class NativeAPIServer:
             rvs = srv.patch_many(g, v, r, ns, items, "status")
             return {"resourceVersions": {k: rv for k, rv in zip(keys, rvs) if rv is not None}}
         if what == "profile" and method == "POST":
-            # the store runs on a C++ thread: cProfile would see only this fallback
-            return {"profiling": False, "native": True,
-                    "note": "the native fake apiserver is profiled with perf / rocprofv3 --sys-trace, not cProfile"}
+            # a SIGPROF stack sampler inside the extension (the boxes have no perf): start, then
+            # stop with a path -- the report ranks functions by self and inclusive samples
+            if body.get("action") == "start":
+                srv.profile_start(float(body.get("interval", 0.0005)))
+                return {"profiling": True, "native": True}
+            stacks, dropped = srv.profile_stop()
+            report = profile_report(stacks, dropped)
+            if body.get("path"):
+                with open(body["path"], "w") as fh:
+                    fh.write(report)
+            return {"profiling": False, "native": True, "samples": len(stacks), "path": body.get("path", "")}
         if what == "gc" and method == "POST":
             from ..utils import gctune
 

@@ -22,7 +22,12 @@
 #endif
 
 #include <arpa/inet.h>
+#include <dlfcn.h>
+#include <execinfo.h>
 #include <fcntl.h>
+#include <malloc.h>
+#include <signal.h>
+#include <sys/time.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <openssl/err.h>
@@ -2851,6 +2856,13 @@ int Server_init(Server* self, PyObject* args, PyObject* kw) {
   double bm = 60.0;
   if (!PyArg_ParseTupleAndKeywords(args, kw, "|Lnd", const_cast<char**>(kwlist), &now, &window, &bm)) return -1;
   Impl* s = self->impl;
+  // The server thread allocates from a secondary malloc arena, which glibc grows (mprotect) and
+  // trims back (madvise) around a small top chunk: with trees retired by the thousand per tick
+  // it thrashed -- the stack sampler put __default_morecore + mprotect + the page faults behind
+  // them at a fifth of the server's CPU.  This process only serves: keep what it has.
+  mallopt(M_TRIM_THRESHOLD, 1 << 30);
+  mallopt(M_TOP_PAD, 64 << 20);
+  mallopt(M_MMAP_THRESHOLD, 64 << 20);
   s->now_ns = now;
   s->watch_window = static_cast<size_t>(std::max<Py_ssize_t>(1, window));
   s->bookmark_interval = bm > 0 ? bm : 1e9;
@@ -3305,6 +3317,95 @@ PyObject* Server_patch_unfinished(Server* self, PyObject* args) {
   return PyLong_FromLongLong(n);
 }
 
+// ---------------------------------------------------------------------- sampling profiler
+// There is no perf on the benchmark boxes: a SIGPROF timer on process CPU time samples the stack
+// of whichever thread runs (the server thread, in a benchmark), and profile_stop() returns the
+// stacks as (module path, offset) frames -- tests/scripts resolve them with addr2line.
+namespace prof {
+constexpr size_t kCap = 1 << 21;  // frames
+std::atomic<bool> on{false};
+uint64_t* frames = nullptr;       // stacks, each ended by a 0
+std::atomic<size_t> used{0};
+std::atomic<size_t> dropped{0};
+
+void handler(int, siginfo_t*, void*) {
+  if (!on.load(std::memory_order_relaxed)) return;
+  void* buf[48];
+  const int n = backtrace(buf, 48);
+  const size_t need = static_cast<size_t>(n) + 1;
+  const size_t at = used.fetch_add(need, std::memory_order_relaxed);
+  if (at + need > kCap) {
+    dropped.fetch_add(1, std::memory_order_relaxed);
+    return;
+  }
+  // [0] is this handler and [1] the kernel's signal trampoline: the interrupted frame is [2]
+  size_t k = at;
+  for (int i = 2; i < n; ++i) frames[k++] = reinterpret_cast<uint64_t>(buf[i]);
+  while (k < at + need) frames[k++] = 0;
+}
+}  // namespace prof
+
+// profile_start(interval_s=0.0005)
+PyObject* Server_profile_start(Server*, PyObject* args) {
+  double interval = 0.0005;
+  if (!PyArg_ParseTuple(args, "|d", &interval)) return nullptr;
+  if (!prof::frames) prof::frames = new uint64_t[prof::kCap];
+  void* warm[4];
+  backtrace(warm, 4);  // the unwinder loads (and allocates) on its first use: not in the handler
+  prof::used.store(0);
+  prof::dropped.store(0);
+  struct sigaction sa;
+  std::memset(&sa, 0, sizeof sa);
+  sa.sa_sigaction = prof::handler;
+  sa.sa_flags = SA_SIGINFO | SA_RESTART;
+  sigemptyset(&sa.sa_mask);
+  sigaction(SIGPROF, &sa, nullptr);
+  prof::on.store(true);
+  struct itimerval it;
+  it.it_interval.tv_sec = static_cast<time_t>(interval);
+  it.it_interval.tv_usec = static_cast<suseconds_t>((interval - static_cast<double>(it.it_interval.tv_sec)) * 1e6);
+  it.it_value = it.it_interval;
+  setitimer(ITIMER_PROF, &it, nullptr);
+  Py_RETURN_NONE;
+}
+
+// profile_stop() -> (stacks: [[(module, offset), ...] innermost first], dropped)
+PyObject* Server_profile_stop(Server*, PyObject*) {
+  struct itimerval it;
+  std::memset(&it, 0, sizeof it);
+  setitimer(ITIMER_PROF, &it, nullptr);
+  prof::on.store(false);
+  const size_t n = std::min(prof::used.load(), prof::kCap);
+  PyObject* stacks = PyList_New(0);
+  PyObject* cur = PyList_New(0);
+  std::unordered_map<uint64_t, std::pair<std::string, uint64_t>> memo;
+  for (size_t i = 0; i < n && prof::frames; ++i) {
+    const uint64_t a = prof::frames[i];
+    if (a == 0) {
+      if (PyList_GET_SIZE(cur) > 0) PyList_Append(stacks, cur);
+      Py_DECREF(cur);
+      cur = PyList_New(0);
+      continue;
+    }
+    auto it2 = memo.find(a);
+    if (it2 == memo.end()) {
+      Dl_info info;
+      std::pair<std::string, uint64_t> v("?", a);
+      if (dladdr(reinterpret_cast<void*>(a), &info) && info.dli_fname) {
+        v.first = info.dli_fname;
+        v.second = a - reinterpret_cast<uint64_t>(info.dli_fbase) - 1;  // the call, not the return
+      }
+      it2 = memo.emplace(a, v).first;
+    }
+    PyObject* t = Py_BuildValue("(sK)", it2->second.first.c_str(),
+                                static_cast<unsigned long long>(it2->second.second));
+    PyList_Append(cur, t);
+    Py_DECREF(t);
+  }
+  Py_DECREF(cur);
+  return Py_BuildValue("(Nn)", stacks, static_cast<Py_ssize_t>(prof::dropped.load()));
+}
+
 PyObject* Server_port(Server* self, void*) { return PyLong_FromLong(self->impl->port); }
 
 PyMethodDef Server_methods[] = {
@@ -3324,6 +3425,10 @@ PyMethodDef Server_methods[] = {
     {"stats", reinterpret_cast<PyCFunction>(Server_stats), METH_NOARGS, "request accounting"},
     {"count", reinterpret_cast<PyCFunction>(Server_count), METH_VARARGS, "objects of a resource"},
     {"watchers", reinterpret_cast<PyCFunction>(Server_watchers), METH_NOARGS, "open watches"},
+    {"profile_start", reinterpret_cast<PyCFunction>(Server_profile_start), METH_VARARGS,
+     "profile_start(interval_s=0.0005): sample stacks on process CPU time (SIGPROF)"},
+    {"profile_stop", reinterpret_cast<PyCFunction>(Server_profile_stop), METH_NOARGS,
+     "profile_stop() -> (stacks of (module, offset) frames, innermost first; dropped samples)"},
     {"log_sizes", reinterpret_cast<PyCFunction>(Server_log_sizes), METH_NOARGS,
      "events kept per resource for watch resume"},
     {"unfinished", reinterpret_cast<PyCFunction>(Server_unfinished), METH_VARARGS,

@@ -311,6 +311,8 @@ class Parser {
   Ref parse() {
     ws();
     Ref r = value(0);
+    astack_.clear();  // a failed parse leaves partial containers on the shared stacks
+    ostack_.clear();
     if (!r) return r;
     ws();
     if (p_ != e_) return fail("extra data after JSON value");
@@ -503,9 +505,18 @@ class Parser {
       run = p_;
     }
   }
-  // containers collect their children on a scratch stack, then take them at exact capacity
-  std::vector<Ref> astack_;
-  std::vector<Member> ostack_;
+  // containers collect their children on a scratch stack, then take them at exact capacity; the
+  // stacks live as long as the thread (a parse would otherwise regrow them from empty)
+  static std::vector<Ref>& astack() {
+    static thread_local std::vector<Ref> v;
+    return v;
+  }
+  static std::vector<Member>& ostack() {
+    static thread_local std::vector<Member> v;
+    return v;
+  }
+  std::vector<Ref>& astack_ = astack();
+  std::vector<Member>& ostack_ = ostack();
   size_t dups_ = 0;  // repeated keys seen so far: a span holding one is not its node's encoding
 
   Ref array(int depth) {

@@ -22,7 +22,7 @@ sys.path.insert(0, ROOT)
 
 
 def run(shards: int, impl: str, steps: int, warmup: int, crons: int, lifecycle: str,
-        watch_window: int = 20_000) -> dict:
+        watch_window: int = 20_000, profile: str = "") -> dict:
     from cron_operator_amd.bench import harness
 
     snaps = []
@@ -39,7 +39,7 @@ def run(shards: int, impl: str, steps: int, warmup: int, crons: int, lifecycle: 
     try:
         res = harness.run_sync(harness.BenchConfig(n_crons=crons, steps=steps, warmup=warmup, shards=shards,
                                                    lifecycle=lifecycle, apiserver_impl=impl,
-                                                   watch_window=watch_window))
+                                                   watch_window=watch_window, apiserver_profile=profile))
     finally:
         harness._cpu_times = orig
     fires = crons * steps
@@ -77,13 +77,17 @@ def main() -> int:
     ap.add_argument("--crons", type=int, default=1000)
     ap.add_argument("--lifecycle", default="instant", choices=["instant", "realistic"])
     ap.add_argument("--watch-window", type=int, default=20_000)
+    ap.add_argument("--profile-dir", default="",
+                    help="also sample the native fake apiserver's stacks per run: <dir>/<impl>_<shards>_<rep>.txt")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     rows = []
     for rep in range(a.reps):
         for impl in a.impl:
             for shards in a.shards:
-                r = run(shards, impl, a.steps, a.warmup, a.crons, a.lifecycle, a.watch_window)
+                prof = os.path.join(a.profile_dir, f"{impl}_{shards}_{rep}.txt") if a.profile_dir and impl == "native" \
+                    else ""
+                r = run(shards, impl, a.steps, a.warmup, a.crons, a.lifecycle, a.watch_window, prof)
                 r["rep"] = rep
                 rows.append(r)
                 print(json.dumps(r), flush=True)
