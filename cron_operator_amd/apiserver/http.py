@@ -427,7 +427,10 @@ class APIServerApp:
                 s.faults.add(**f)
             for verb, lat in (body.get("latency") or {}).items():
                 s.faults.latency[verb] = float(lat)
-            return _json({"faults": len(s.faults.faults)})
+            # per-resource watch delivery lag, [min s, max s] per event, each stream on its own
+            for resource, (lo, hi) in (body.get("watchLag") or {}).items():
+                s.faults.watch_lag[resource] = (float(lo), float(hi))
+            return _json({"faults": len(s.faults.faults), "watchLag": sorted(s.faults.watch_lag)})
         if what == "complete" and req.method == "POST":
             # bench helper: mark every job (of the given resource) without completionTime as finished
             body = self._body(req) or {}

@@ -166,10 +166,10 @@ class NativeAPIServer:
             if body.get("clear"):
                 srv.clear_latency()
                 self._faults = 0
-            if body.get("faults"):
-                return 501, _status_body(501, "NotImplemented", "error faults are injected by the Python fake "
-                                                                "apiserver (--impl python); the native one "
-                                                                "models latency only")
+            if body.get("faults") or body.get("watchLag"):
+                return 501, _status_body(501, "NotImplemented", "error faults and watch lag are injected by the "
+                                                                "Python fake apiserver (--impl python); the "
+                                                                "native one models latency only")
             lat = {str(k): float(v) for k, v in (body.get("latency") or {}).items()}
             if lat:
                 srv.set_latency(lat)

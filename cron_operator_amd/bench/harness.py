@@ -195,6 +195,10 @@ class BenchResult:
     # leader_elect: the Lease was lost at some point / the longest successful renewal window (s)
     lease_lost: Optional[bool] = None
     lease_max_renew_s: Optional[float] = None
+    # sharded runs, per timed step: the operator shards' CPU s (summed) and the apiserver's CPU s
+    # (the harness's own lifecycle writes taken out) -- the soak's per-window split
+    step_cpu_operator_s: List[float] = field(default_factory=list)
+    step_cpu_apiserver_s: List[float] = field(default_factory=list)
 
     def to_dict(self) -> Dict[str, Any]:
         return asdict(self)
@@ -876,6 +880,9 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
         write_cpu = 0.0
         if n_pre:
             phase_ms["lifecycle_writes"] = []
+        step_cpu_op: List[float] = []
+        step_cpu_api: List[float] = []
+        prev_op_cpu = 0.0
         for k in range(1, total + 1):
             tick_ns = T0_NS + k * 60 * NANOS
             if k == cfg.warmup + 1:
@@ -889,6 +896,8 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
                 t_start = time.perf_counter()
             t0 = time.perf_counter()
             writes = 0.0
+            step_api0 = _cpu_times(remote)[1]
+            step_write_cpu = 0.0
             if k > 1:
                 for st in range(n_pre):  # the previous tick's jobs start (realistic lifecycle)
                     w0 = time.perf_counter()
@@ -896,6 +905,7 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
                     rvs = await job_stage(st, tick_ns - 59 * NANOS, tick_ns - 30 * NANOS)
                     writes += time.perf_counter() - w0  # the harness's write call: not timed
                     if k > cfg.warmup:
+                        step_write_cpu += _cpu_times(remote)[1] - c0
                         write_cpu += _cpu_times(remote)[1] - c0
                     await asyncio.gather(*(s.send({"cmd": "absorb", "rvs": rvs}) for s in shards))
                     await asyncio.gather(*(s.recv(cfg.step_timeout) for s in shards))
@@ -910,6 +920,9 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
                 base = last
             if k > cfg.warmup:
                 step_ms.append((t2 - t0 - writes) * 1000)
+                op_cpu = sum(r["cpu"] for r in last)
+                step_cpu_op.append(op_cpu - prev_op_cpu)
+                step_cpu_api.append(_cpu_times(remote)[1] - step_api0 - step_write_cpu)
                 phase_ms["completion"].append((t1 - t0 - writes) * 1000)
                 phase_ms["fire"].append((t2 - t1) * 1000)
                 if n_pre:
@@ -917,6 +930,7 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
                 excluded += writes
                 for r in last:
                     timed_lat.extend(r["lat"])
+            prev_op_cpu = sum(r["cpu"] for r in last)
             if on_step is not None:
                 on_step(k, t2 - t0 - writes, k > cfg.warmup)
         elapsed = time.perf_counter() - t_start - excluded
@@ -949,6 +963,7 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
             engine=default_engine().name, fastjson_native=jsonutil.NATIVE,
             cpu_s_operator=sum(r["cpu"] - b["cpu"] for r, b in zip(last, base)),
             cpu_s_apiserver=api1 - api0 - write_cpu,
+            step_cpu_operator_s=step_cpu_op, step_cpu_apiserver_s=step_cpu_api,
             operator_maxrss_mib=[round(r.get("maxrss_mib", 0.0), 1) for r in last],
             operator_ready_maxrss_mib=[round(r.get("maxrss_mib", 0.0), 1) for r in ready],
             operator_rss_mib=[round(r.get("rss_mib", 0.0), 1) for r in last],

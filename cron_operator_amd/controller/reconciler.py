@@ -79,8 +79,9 @@ the CREATE's response is lost after the object was stored, the next reconcile
 sees the same missed tick again: under ``Replace`` it deletes the job it just
 created and creates it anew, and under ``Forbid`` it waits for the job to finish
 and then runs the tick a second time under a new name.  Job names are
-``<cron>-<unix(Next(tick))>`` (B18), so the job a tick produced is recognisable;
-when it already exists the tick is recorded as run instead
+``<cron>-<unix(Next(tick))>`` (B18), so the job a tick produced is recognisable
+(an ``@every`` job is named ``Next(now)`` at its CREATE: a later-named job created at
+or after the tick counts); when it already exists the tick is recorded as run instead
 (``tests/test_chaos.py`` drives exactly these faults).
 
 Time comes from the injected clock (the reference calls ``time.Now()``,
@@ -1039,6 +1040,11 @@ class CronReconciler(Reconciler):
                 self.expect.drop_pending(self._ckey(cron), wm.get("name", ""))
             if isinstance(e, errors.ApiError) and errors.is_already_exists(e):
                 log.info(f"{gvk.kind} already exists", **{gvk.kind: ref})
+                if self.opts.expectations:
+                    # the job is stored (an earlier CREATE whose response was lost): its ADDED
+                    # event may have been dropped as ours while this CREATE was in flight, so no
+                    # event is left to fold it into status.active -- reconcile once more
+                    scheduled = Result(requeue=True)
             else:
                 if isinstance(e, Exception):
                     self.recorder.eventf(cron.to_dict(), Warning, "FailedCreate", "Error creating %s: %s",
@@ -1067,14 +1073,25 @@ class CronReconciler(Reconciler):
         if fixed:
             return False
         try:
-            ran_name = get_default_job_name(cron.name, self.engine.next(self.engine.parse(cron.spec.schedule),
-                                                                        missed_run))
+            ran = self.engine.next(self.engine.parse(cron.spec.schedule), missed_run)
         except ScheduleError:
             return False
+        ran_name = get_default_job_name(cron.name, ran)
+        prefix = cron.name + "-"
         for lst in (active, terminated):
             for info in lst:
                 if info.name == ran_name:
                     return True
+                # the name is Next(now) at the CREATE: for a cron spec that is Next(tick), but an
+                # `@every` job is named for the moment it was created.  A later-named job created
+                # at or after the tick ran it (or a later tick)
+                suffix = info.name[len(prefix):] if info.name.startswith(prefix) else ""
+                if suffix.isdigit() and int(suffix) > ran.sec:
+                    key = info.sort_key
+                    if key is None:
+                        key = _sort_key(((info.obj or {}).get("metadata") or {}).get("creationTimestamp"))
+                    if key[0] >= missed_run.sec:
+                        return True
         return False
 
     # ------------------------------------------------------------------ children

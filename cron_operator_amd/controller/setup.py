@@ -127,7 +127,9 @@ async def setup_with_manager(mgr: Manager, options: Optional[ReconcilerOptions] 
         # one predicate for the child events (no per-event loop over several): creates and deletes
         # that only confirm what the reconciler already folded into status are dropped, and so are
         # updates that change nothing a reconcile reads
-        skip_expected = opts.expectations and opts.skip_expected_events
+        # (an expected event is only redundant when the reconciler folded its own CREATE / DELETE
+        # into status.active itself)
+        skip_expected = opts.expectations and opts.skip_expected_events and opts.fold_created_into_active
         skip_unchanged = opts.skip_unchanged_child_updates and opts.active_ref_resource_version != "live"
         policy = opts.workload
         ex = rec.expect

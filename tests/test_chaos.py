@@ -361,3 +361,27 @@ async def test_watch_lag_keeps_each_stream_in_order_and_ends_it_last():
     assert len(rvs) == 30 and rvs == sorted(rvs)
     await asyncio.sleep(0)
     assert w.lagged == 0
+
+
+def test_watch_lag_is_a_debug_control_of_the_http_fake_apiserver():
+    """``POST /debug/fake/faults {"watchLag": {resource: [min s, max s]}}`` sets the lag an
+    out-of-process operator's watch streams see (``{"clear": true}`` removes it); the native
+    fake apiserver refuses it (501) rather than ignore it."""
+    import json
+
+    from cron_operator_amd.apiserver.http import APIServerApp, Request
+    from cron_operator_amd.apiserver.native import NativeAPIServer, load
+
+    env = TestEnv()
+    app = APIServerApp(env.server)
+    body = json.dumps({"watchLag": {"crons": [0.005, 0.2], "pytorchjobs": [0.01, 0.05]}}).encode()
+    r = app.dispatch(Request("POST", "/debug/fake/faults", {}, {"content-type": "application/json"}, body))
+    assert r.status == 200 and json.loads(r.body)["watchLag"] == ["crons", "pytorchjobs"]
+    assert env.server.faults.lag_for("crons") == (0.005, 0.2)
+    assert env.server.faults.lag_for("pytorchjobs") == (0.01, 0.05)
+    r = app.dispatch(Request("POST", "/debug/fake/faults", {}, {"content-type": "application/json"},
+                             b'{"clear": true}'))
+    assert r.status == 200 and env.server.faults.lag_for("crons") is None
+    if load() is not None:
+        nat = NativeAPIServer()
+        assert nat.fallback("POST", "/debug/fake/faults", "", {}, body)[0] == 501
