@@ -73,6 +73,9 @@ def profile_report(stacks, dropped: int = 0, top: int = 40) -> str:
         base = os.path.basename(mod)
         for o, fn in zip(offs, resolved):
             names[(mod, o)] = f"{fn} [{base}]" if fn != "??" else f"?? [{base}+{o:#x}]"
+    # samples of the server thread waiting in epoll_wait: idle time, not CPU
+    idle = sum(1 for st in stacks if st and "epoll_wait" in names[st[0]])
+    stacks = [st for st in stacks if st and "epoll_wait" not in names[st[0]]]
     self_c: collections.Counter = collections.Counter()
     incl_c: collections.Counter = collections.Counter()
     for st in stacks:
@@ -90,7 +93,8 @@ def profile_report(stacks, dropped: int = 0, top: int = 40) -> str:
         if own is not None:
             via[f"{names[st[0]]}  <-  {own}"] += 1
     n = max(1, len(stacks))
-    out = [f"# {len(stacks)} samples ({dropped} dropped) of the fake apiserver process on its CPU time\n",
+    out = [f"# {len(stacks)} busy samples of the fake apiserver's server thread ({idle} more idle in "
+           f"epoll_wait, {dropped} dropped)\n",
            "\n## by self samples\n"]
     out += [f"{100.0 * c / n:6.2f}%  {k}\n" for k, c in self_c.most_common(top)]
     out.append("\n## by inclusive samples\n")
@@ -157,7 +161,7 @@ class NativeAPIServer:
             return {"total": st["total"], "by_verb": st["by_verb"], "by_resource_verb": st["by_resource_verb"],
                     "resourceVersion": st["resourceVersion"], "native": True,
                     "server_thread_cpu_s": st["server_thread_cpu_s"], "verb_cpu": st["verb_cpu"],
-                    "phase_cycles": st["phase_cycles"]}
+                    "phase_cycles": st["phase_cycles"], "io": st["io"]}
         if what == "clock":
             if method == "POST":
                 srv.set_clock(int(body["nowNs"]))

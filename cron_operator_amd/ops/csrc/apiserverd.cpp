@@ -27,6 +27,7 @@
 #include <fcntl.h>
 #include <malloc.h>
 #include <signal.h>
+#include <sys/syscall.h>
 #include <sys/time.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
@@ -913,15 +914,30 @@ struct Impl {
   std::vector<Resource*> order;                                 // registration order (discovery)
   std::map<std::string, std::unique_ptr<Store>> stores;        // "group/resource"
   std::map<std::string, double> latency;                       // verb -> s ("*": default)
-  std::map<std::string, long long> stats_verb;
-  std::map<std::string, long long> stats_res_verb;             // "resource:verb"
   long long stats_total = 0;
   long long requests = 0;
   // server-thread CPU by phase (ns): socket reads + request parsing, verbs (route, store,
   // admission, encoding, watch fan-out), the Python fallback (/debug/fake controls), framing +
   // socket writes; and the loop's total
-  long long cpu_read = 0, cpu_verbs = 0, cpu_fallback = 0, cpu_write = 0, cpu_loop = 0;
-  std::map<std::string, std::pair<long long, long long>> verb_cpu;  // "verb[/sub]:resource" -> (ns, calls)
+  // the server thread's time by phase, in TSC cycles (a thread-CPU clock read is a system call:
+  // per request it cost more than the accounting is worth); the thread's CPU per turn scales them
+  unsigned long long cyc_read = 0, cyc_verbs = 0, cyc_fallback = 0, cyc_write = 0, cyc_loop = 0;
+  long long cpu_loop = 0;  // ns of thread CPU over the same turns as cyc_loop
+  struct VerbKey {
+    const Resource* ri;
+    std::string verb, sub;
+    bool operator<(const VerbKey& o) const {
+      return std::tie(ri, verb, sub) < std::tie(o.ri, o.verb, o.sub);
+    }
+  };
+  std::map<VerbKey, std::pair<unsigned long long, long long>> verb_cpu;  // -> (cycles, calls)
+  std::pair<const VerbKey, std::pair<unsigned long long, long long>>* last_vk = nullptr;
+  struct RecHash {
+    size_t operator()(const std::pair<const Resource*, const char*>& p) const {
+      return std::hash<const void*>()(p.first) * 1000003u ^ std::hash<const void*>()(p.second);
+    }
+  };
+  std::unordered_map<std::pair<const Resource*, const char*>, long long, RecHash> rec_counts;
   // where a write's time goes, in TSC cycles (nested: `finish` includes `emit`)
   enum Ph { kParse, kMerge, kPrepare, kFinish, kEmit, kReply, kPhases };
   unsigned long long phase[kPhases] = {};
@@ -940,6 +956,7 @@ struct Impl {
   int port = 0;
   SSL_CTX* ssl_ctx = nullptr;
   std::thread thread;
+  std::atomic<pid_t> loop_tid{0};  // the server thread's kernel id (the sampler's target)
   std::atomic<bool> stopping{false};
   bool running = false;
   double bookmark_interval = 60.0;
@@ -949,6 +966,13 @@ struct Impl {
   std::priority_queue<Timer, std::vector<Timer>, std::greater<Timer>> timers;
   std::vector<Watcher*> dirty_watchers;
   std::vector<Conn*> dirty_conns;
+  // watch streams are flushed when the server has nothing else ready (or after kWatchDefer s):
+  // under load one send carries many events instead of one send per event per turn
+  // (APISERVERD_WATCH_DEFER_S overrides; 0 flushes every turn, as rounds 1-5 did)
+  double watch_defer_s = 0.002;
+  bool watch_deferred = false;
+  double watch_defer_since = 0.0;
+  long long sends = 0, turns = 0;
 
   ~Impl() {
     for (auto& kv : conns) delete kv.second;
@@ -1150,9 +1174,8 @@ struct Impl {
     return n;
   }
 
-  void record(const char* verb, const std::string& resource) {
-    ++stats_verb[verb];
-    ++stats_res_verb[resource + ":" + verb];
+  void record(const char* verb, const Resource* ri) {
+    ++rec_counts[{ri, verb}];
     ++stats_total;
   }
 
@@ -1276,7 +1299,7 @@ struct Impl {
   // Each returns the stored object (or an error): the caller serialises it.
 
   Ref v_get(Resource* ri, const std::string& ns, const std::string& name, ApiErr* err) {
-    record("get", ri->resource);
+    record("get", ri);
     Ref o = get_raw(ri, ns, name);
     if (!o) *err = not_found(ri->resource, ri->group, name);
     return o;
@@ -1296,7 +1319,7 @@ struct Impl {
   }
 
   Ref v_create(Resource* ri, const std::string& url_ns, Ref body, bool dry_run, ApiErr* err) {
-    record("create", ri->resource);
+    record("create", ri);
     Node* b = body.get();
     Ref meta;
     if (const Ref* m = b->get("metadata"); m && (*m)->is_obj()) {
@@ -1476,7 +1499,7 @@ struct Impl {
 
   Ref v_update(Resource* ri, const std::string& ns_in, const std::string& name, Ref body, const std::string& sub,
                ApiErr* err) {
-    record("update", ri->resource);
+    record("update", ri);
     const std::string ns = ri->namespaced ? ns_in : std::string();
     Ref old = get_raw(ri, ns, name);
     const Node* bm = body->getn("metadata");
@@ -1501,7 +1524,7 @@ struct Impl {
 
   Ref v_patch(Resource* ri, const std::string& ns_in, const std::string& name, Ref patch, const std::string& ptype,
               const std::string& sub, ApiErr* err) {
-    record("patch", ri->resource);
+    record("patch", ri);
     const std::string ns = ri->namespaced ? ns_in : std::string();
     Ref old = get_raw(ri, ns, name);
     if (!old) {
@@ -1556,7 +1579,7 @@ struct Impl {
 
   Ref v_delete(Resource* ri, const std::string& ns_in, const std::string& name, const std::string& policy,
                const Node* pre, ApiErr* err) {
-    record("delete", ri->resource);
+    record("delete", ri);
     const std::string ns = ri->namespaced ? ns_in : std::string();
     Ref old = get_raw(ri, ns, name);
     if (!old) {
@@ -1599,7 +1622,7 @@ struct Impl {
   // LIST; writes the response body into *out
   bool v_list(Resource* ri, const std::string& ns, const Selector& sel, long long limit, const std::string& cont,
               std::string* out, ApiErr* err) {
-    record("list", ri->resource);
+    record("list", ri);
     Store* st = ri->store;
     std::string start_after;
     long long list_rv = rv;
@@ -2025,7 +2048,7 @@ struct Impl {
         if (rt.ns.empty() || !ri->namespaced || kv.first == rt.ns)
           for (auto& ob : kv.second)
             if (sel.match(ob.second.get())) victims.emplace_back(kv.first, ob.first);
-      record("list", ri->resource);
+      record("list", ri);
       long long n = 0;
       for (auto& v : victims) {
         ApiErr e2;
@@ -2045,7 +2068,7 @@ struct Impl {
   // ---------------------------------------------------------------- watches
   // start a watch on connection c (or, c == nullptr, validate only); false + err on a bad request
   Watcher* start_watch(Conn* c, const Request& r, const Route& rt, ApiErr* err) {
-    record("watch", rt.ri->resource);
+    record("watch", rt.ri);
     auto w = std::make_unique<Watcher>();
     w->conn = c;
     w->res = rt.ri;
@@ -2110,6 +2133,12 @@ struct Impl {
     w->ended = true;
   }
 
+  // delete a dropped watcher (no pointer to it may stay in the end-of-turn list)
+  void free_watcher(Watcher* w) {
+    dirty_watchers.erase(std::remove(dirty_watchers.begin(), dirty_watchers.end(), w), dirty_watchers.end());
+    delete w;
+  }
+
   // ---------------------------------------------------------------- event loop
   void arm(Conn* c, bool out) {
     struct epoll_event ev;
@@ -2128,7 +2157,7 @@ struct Impl {
     c->closed = true;
     if (c->watch) {
       drop_watcher(c->watch);
-      delete c->watch;
+      free_watcher(c->watch);
       c->watch = nullptr;
     }
     epoll_ctl(epfd, EPOLL_CTL_DEL, c->fd, nullptr);
@@ -2160,6 +2189,7 @@ struct Impl {
         }
         c->out_off += static_cast<size_t>(w);
       } else {
+        ++sends;
         const ssize_t w = ::send(c->fd, p, n, MSG_NOSIGNAL);
         if (w < 0) {
           if (errno == EAGAIN || errno == EWOULDBLOCK) {
@@ -2247,9 +2277,9 @@ struct Impl {
 
   // run one request on connection c (after parsing, or when its injected latency elapsed)
   void run_request(Conn* c, Request& r, bool delayed_done) {
-    const long long t0 = thread_cpu_ns();
+    const unsigned long long t0 = __rdtsc();
     run_request_(c, r, delayed_done);
-    cpu_verbs += thread_cpu_ns() - t0;
+    cyc_verbs += __rdtsc() - t0;
   }
 
   void run_request_(Conn* c, Request& r, bool delayed_done) {
@@ -2257,12 +2287,12 @@ struct Impl {
     Route rt;
     double delay = 0.0;
     if (!handle(r, &rep, &rt, delayed_done ? nullptr : &delay)) {
-      const long long f0 = thread_cpu_ns();
+      const unsigned long long f0 = __rdtsc();
       if (!call_fallback(r, &rep)) reply_err(&rep, mkerr(404, "NotFound", "the server could not find the "
                                                                           "requested resource"));
-      const long long f = thread_cpu_ns() - f0;
-      cpu_fallback += f;
-      cpu_verbs -= f;  // counted once, as fallback
+      const unsigned long long f = __rdtsc() - f0;
+      cyc_fallback += f;
+      cyc_verbs -= f;  // counted once, as fallback
       write_reply(c, rep, r.keep);
       return;
     }
@@ -2296,20 +2326,27 @@ struct Impl {
       push_timer(mono() + (timeout > 0 ? timeout : 1800.0), 1, c->id);
       return;
     }
-    const long long a0 = thread_cpu_ns();
+    const unsigned long long a0 = __rdtsc();
     apply(r, rt, &rep);
     write_reply(c, rep, r.keep);
-    const std::string key = rt.verb + (rt.sub.empty() ? "" : "/" + rt.sub) + ":" + rt.ri->resource;
-    auto& vc = verb_cpu[key];
-    vc.first += thread_cpu_ns() - a0;
-    ++vc.second;
+    const unsigned long long a = __rdtsc() - a0;
+    if (last_vk && last_vk->first.ri == rt.ri && last_vk->first.verb == rt.verb && last_vk->first.sub == rt.sub) {
+      last_vk->second.first += a;
+      ++last_vk->second.second;
+    } else {
+      auto it = verb_cpu.find(VerbKey{rt.ri, rt.verb, rt.sub});
+      if (it == verb_cpu.end()) it = verb_cpu.emplace(VerbKey{rt.ri, rt.verb, rt.sub}, std::make_pair(0ULL, 0LL)).first;
+      it->second.first += a;
+      ++it->second.second;
+      last_vk = &*it;
+    }
   }
   void end_watch(Conn* c) {
     Watcher* w = c->watch;
     if (!w) return;
     frame_pending(w);
     drop_watcher(w);
-    delete w;
+    free_watcher(w);
     c->watch = nullptr;
     c->out.append("0\r\n\r\n");
     const bool keep = c->watch_keep;
@@ -2541,11 +2578,11 @@ struct Impl {
   }
 
   void on_readable(Conn* c) {
-    const long long t0 = thread_cpu_ns();
-    const long long v0 = cpu_verbs + cpu_fallback;
+    const unsigned long long t0 = __rdtsc();
+    const unsigned long long v0 = cyc_verbs + cyc_fallback;
     on_readable_(c);
     // reading and parsing: what the verbs run from here did not take
-    cpu_read += thread_cpu_ns() - t0 - (cpu_verbs + cpu_fallback - v0);
+    cyc_read += __rdtsc() - t0 - (cyc_verbs + cyc_fallback - v0);
   }
 
   void on_readable_(Conn* c) {
@@ -2636,25 +2673,48 @@ struct Impl {
     }
   }
 
-  void end_of_turn() {
-    const long long t0 = thread_cpu_ns();
-    end_of_turn_();
-    cpu_write += thread_cpu_ns() - t0;
+  void end_of_turn(bool flush_watches = true) {
+    const unsigned long long t0 = __rdtsc();
+    end_of_turn_(flush_watches);
+    cyc_write += __rdtsc() - t0;
   }
 
-  void end_of_turn_() {
-    for (Watcher* w : dirty_watchers)
-      if (w->dirty) frame_pending(w);
-    dirty_watchers.clear();
+  static bool streaming_watch(const Conn* c) { return c->watch && c->watch->streaming && !c->close_after; }
+
+  void end_of_turn_(bool flush_watches) {
+    // a streaming watch's events may wait for a quiet turn; everything else goes out now
+    bool deferred = false;
+    std::vector<Watcher*> ws;
+    ws.swap(dirty_watchers);
+    for (Watcher* w : ws) {
+      if (!w->dirty) continue;
+      if (!flush_watches && w->conn && !w->conn->closed && streaming_watch(w->conn)) {
+        dirty_watchers.push_back(w);
+        deferred = true;
+        continue;
+      }
+      frame_pending(w);
+    }
     // flush each dirty connection once
     std::vector<Conn*> cs;
     cs.swap(dirty_conns);
     std::unordered_set<Conn*> seen;
     for (Conn* c : cs) {
       if (!seen.insert(c).second) continue;
-      if (!c->closed) flush(c);
+      if (c->closed) continue;
+      if (!flush_watches && streaming_watch(c)) {
+        dirty_conns.push_back(c);
+        deferred = true;
+        continue;
+      }
+      flush(c);  // frames the watch's open chunk first
     }
-    // reap closed connections
+    if (deferred && !watch_deferred) watch_defer_since = mono();
+    watch_deferred = deferred;
+    // reap closed connections (none may stay deferred)
+    if (!dirty_conns.empty())
+      dirty_conns.erase(std::remove_if(dirty_conns.begin(), dirty_conns.end(), [](Conn* c) { return c->closed; }),
+                        dirty_conns.end());
     for (auto it = conns.begin(); it != conns.end();) {
       if (it->second->closed) {
         delete it->second;
@@ -2666,6 +2726,8 @@ struct Impl {
   }
 
   void loop() {
+    loop_tid.store(static_cast<pid_t>(syscall(SYS_gettid)));
+    if (const char* e = std::getenv("APISERVERD_WATCH_DEFER_S")) watch_defer_s = std::strtod(e, nullptr);
     std::vector<struct epoll_event> evs(256);
     push_timer(mono() + bookmark_interval, 2, 0);
     while (!stopping.load()) {
@@ -2674,9 +2736,11 @@ struct Impl {
         const double d = timers.top().due - mono();
         timeout_ms = d <= 0 ? 0 : static_cast<int>(std::min(1000.0, std::ceil(d * 1000.0)));
       }
+      if (watch_deferred) timeout_ms = 0;  // poll: the deferred watch events go out once idle
       const int n = epoll_wait(epfd, evs.data(), static_cast<int>(evs.size()), timeout_ms);
       std::lock_guard<std::recursive_mutex> g(mu);
       const long long turn0 = thread_cpu_ns();
+      const unsigned long long tc0 = __rdtsc();
       for (int i = 0; i < n; ++i) {
         const uint64_t id = evs[i].data.u64;
         if (id == UINT64_MAX - 1) {
@@ -2696,7 +2760,9 @@ struct Impl {
         if (!c->closed && (e & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR))) on_readable(c);
       }
       run_timers();
-      end_of_turn();
+      ++turns;
+      end_of_turn(n == 0 || watch_defer_s <= 0.0 || (watch_deferred && mono() - watch_defer_since >= watch_defer_s));
+      cyc_loop += __rdtsc() - tc0;
       cpu_loop += thread_cpu_ns() - turn0;
     }
     // shutdown: end every watch and close every connection
@@ -2705,7 +2771,7 @@ struct Impl {
       Conn* c = kv.second;
       if (c->watch) {
         drop_watcher(c->watch);
-        delete c->watch;
+        free_watcher(c->watch);
         c->watch = nullptr;
       }
       if (!c->closed) close_conn(c);
@@ -3020,21 +3086,34 @@ PyObject* Server_stats(Server* self, PyObject*) {
   unsigned long long ph[Impl::kPhases];
   long long total, rv, reqs;
   long long cpu[6];
+  long long io[2];
   Py_BEGIN_ALLOW_THREADS
   {
     std::lock_guard<std::recursive_mutex> g(s->mu);
-    bv = s->stats_verb;
-    brv = s->stats_res_verb;
+    for (auto& kv : s->rec_counts) {
+      bv[kv.first.second] += kv.second;
+      brv[kv.first.first->resource + ":" + kv.first.second] += kv.second;
+    }
     total = s->stats_total;
     rv = s->rv;
     reqs = s->requests;
-    cpu[0] = s->cpu_read;
-    cpu[1] = s->cpu_verbs;
-    cpu[2] = s->cpu_fallback;
-    cpu[3] = s->cpu_write;
+    // cycles -> thread CPU ns, at the ratio the turns ran at
+    const double ns_per_cyc = s->cyc_loop ? static_cast<double>(s->cpu_loop) / static_cast<double>(s->cyc_loop) : 0.0;
+    cpu[0] = static_cast<long long>(static_cast<double>(s->cyc_read) * ns_per_cyc);
+    cpu[1] = static_cast<long long>(static_cast<double>(s->cyc_verbs) * ns_per_cyc);
+    cpu[2] = static_cast<long long>(static_cast<double>(s->cyc_fallback) * ns_per_cyc);
+    cpu[3] = static_cast<long long>(static_cast<double>(s->cyc_write) * ns_per_cyc);
     cpu[4] = s->cpu_loop;
     cpu[5] = s->slow_admits;
-    vcpu = s->verb_cpu;
+    io[0] = s->sends;
+    io[1] = s->turns;
+    for (auto& kv : s->verb_cpu) {
+      const std::string key = kv.first.verb + (kv.first.sub.empty() ? "" : "/" + kv.first.sub) + ":" +
+                              kv.first.ri->resource;
+      auto& e = vcpu[key];
+      e.first += static_cast<long long>(static_cast<double>(kv.second.first) * ns_per_cyc);
+      e.second += kv.second.second;
+    }
     for (int i = 0; i < Impl::kPhases; ++i) ph[i] = s->phase[i];
   }
   Py_END_ALLOW_THREADS
@@ -3064,6 +3143,9 @@ PyObject* Server_stats(Server* self, PyObject*) {
   PyObject* q = PyLong_FromLongLong(reqs);
   PyDict_SetItemString(d, "requests", q);
   Py_DECREF(q);
+  PyObject* io_d = Py_BuildValue("{s:L,s:L}", "sends", io[0], "turns", io[1]);
+  PyDict_SetItemString(d, "io", io_d);  // send() calls and event-loop turns
+  Py_DECREF(io_d);
   PyObject* c = Py_BuildValue("{s:d,s:d,s:d,s:d,s:d}", "read_parse", cpu[0] * 1e-9, "verbs", cpu[1] * 1e-9,
                               "fallback", cpu[2] * 1e-9, "frame_write", cpu[3] * 1e-9, "loop", cpu[4] * 1e-9);
   PyDict_SetItemString(d, "server_thread_cpu_s", c);
@@ -3327,6 +3409,8 @@ std::atomic<bool> on{false};
 uint64_t* frames = nullptr;       // stacks, each ended by a 0
 std::atomic<size_t> used{0};
 std::atomic<size_t> dropped{0};
+timer_t timer;
+bool has_timer = false;
 
 void handler(int, siginfo_t*, void*) {
   if (!on.load(std::memory_order_relaxed)) return;
@@ -3346,9 +3430,16 @@ void handler(int, siginfo_t*, void*) {
 }  // namespace prof
 
 // profile_start(interval_s=0.0005)
-PyObject* Server_profile_start(Server*, PyObject* args) {
+// With the server thread running, a CLOCK_MONOTONIC timer signals that thread alone (hrtimer
+// resolution: process-CPU itimers tick at the kernel's HZ, 100-250 samples a second); samples
+// that land in epoll_wait are the thread idling, which the report counts apart.
+PyObject* Server_profile_start(Server* self, PyObject* args) {
   double interval = 0.0005;
   if (!PyArg_ParseTuple(args, "|d", &interval)) return nullptr;
+  if (!(interval > 0.0) || interval > 1.0) {
+    PyErr_SetString(PyExc_ValueError, "interval_s must be in (0, 1]");
+    return nullptr;
+  }
   if (!prof::frames) prof::frames = new uint64_t[prof::kCap];
   void* warm[4];
   backtrace(warm, 4);  // the unwinder loads (and allocates) on its first use: not in the handler
@@ -3361,6 +3452,23 @@ PyObject* Server_profile_start(Server*, PyObject* args) {
   sigemptyset(&sa.sa_mask);
   sigaction(SIGPROF, &sa, nullptr);
   prof::on.store(true);
+  const pid_t tid = self->impl->running ? self->impl->loop_tid.load() : 0;
+  if (tid > 0) {
+    struct sigevent sev;
+    std::memset(&sev, 0, sizeof sev);
+    sev.sigev_notify = SIGEV_THREAD_ID;
+    sev.sigev_signo = SIGPROF;
+    sev._sigev_un._tid = tid;
+    if (timer_create(CLOCK_MONOTONIC, &sev, &prof::timer) == 0) {
+      prof::has_timer = true;
+      struct itimerspec its;
+      its.it_interval.tv_sec = static_cast<time_t>(interval);
+      its.it_interval.tv_nsec = static_cast<long>((interval - static_cast<double>(its.it_interval.tv_sec)) * 1e9);
+      its.it_value = its.it_interval;
+      timer_settime(prof::timer, 0, &its, nullptr);
+      Py_RETURN_NONE;
+    }
+  }
   struct itimerval it;
   it.it_interval.tv_sec = static_cast<time_t>(interval);
   it.it_interval.tv_usec = static_cast<suseconds_t>((interval - static_cast<double>(it.it_interval.tv_sec)) * 1e6);
@@ -3371,6 +3479,10 @@ PyObject* Server_profile_start(Server*, PyObject* args) {
 
 // profile_stop() -> (stacks: [[(module, offset), ...] innermost first], dropped)
 PyObject* Server_profile_stop(Server*, PyObject*) {
+  if (prof::has_timer) {
+    timer_delete(prof::timer);
+    prof::has_timer = false;
+  }
   struct itimerval it;
   std::memset(&it, 0, sizeof it);
   setitimer(ITIMER_PROF, &it, nullptr);

@@ -25,21 +25,36 @@ def run(shards: int, impl: str, steps: int, warmup: int, crons: int, lifecycle: 
         watch_window: int = 20_000, profile: str = "") -> dict:
     from cron_operator_amd.bench import harness
 
+    # the native server's counters when the timed region opens (after the last warmup step) and
+    # once it closed (the first CPU read after the last step)
     snaps = []
     orig = harness._cpu_times
+    url = [""]
+    at = [0]
+
+    def snap():
+        with urllib.request.urlopen(url[0] + "/debug/fake/stats") as f:
+            snaps.append(json.loads(f.read()))
 
     def cpu(remote):
         r = orig(remote)
-        if remote is not None and remote.url and impl == "native":
-            with urllib.request.urlopen(remote.url + "/debug/fake/stats") as f:
-                snaps.append(json.loads(f.read()))
+        if remote is not None and remote.url:
+            url[0] = remote.url
+            if impl == "native" and at[0] == warmup + steps and len(snaps) == 1:
+                snap()
         return r
+
+    def on_step(k, dt, timed):
+        at[0] = k
+        if k == warmup and impl == "native" and url[0]:
+            snap()
 
     harness._cpu_times = cpu
     try:
         res = harness.run_sync(harness.BenchConfig(n_crons=crons, steps=steps, warmup=warmup, shards=shards,
                                                    lifecycle=lifecycle, apiserver_impl=impl,
-                                                   watch_window=watch_window, apiserver_profile=profile))
+                                                   watch_window=watch_window, apiserver_profile=profile),
+                               on_step=on_step)
     finally:
         harness._cpu_times = orig
     fires = crons * steps
@@ -62,6 +77,7 @@ def run(shards: int, impl: str, steps: int, warmup: int, crons: int, lifecycle: 
                                "us_per_call": round((s1 - s0) * 1e6 / (n1 - n0), 1)}
         out["per_verb"] = per_verb
         # the verbs' phases (TSC cycles per fire; `finish` includes `emit`)
+        out["io_per_fire"] = {k: round((b["io"][k] - a["io"][k]) / fires, 2) for k in b.get("io", {})}
         out["phase_kcycles_per_fire"] = {k: round((b["phase_cycles"][k] - a["phase_cycles"][k]) / fires / 1000, 1)
                                          for k in b["phase_cycles"]}
     return out
