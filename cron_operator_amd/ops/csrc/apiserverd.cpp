@@ -791,6 +791,7 @@ struct Resource {
   std::unique_ptr<Schema> schema, status_schema;
   Ref schema_src;
   Store* store = nullptr;
+  jdom::Intern intern;  // subtrees this resource's request bodies repeat (jdom.h)
 };
 
 const Node* labels_of(const Node* obj) {
@@ -1993,7 +1994,7 @@ struct Impl {
     if (!r.body.empty()) {
       std::string perr;
       PhaseTimer pt(&phase[kParse]);
-      body = jdom::parse(r.body.data(), r.body.size(), &perr);
+      body = jdom::parse(r.body.data(), r.body.size(), &perr, &ri->intern);
       if (!body) {
         reply_err(rep, bad_request("invalid JSON body: " + perr));
         return;
@@ -3086,7 +3087,7 @@ PyObject* Server_stats(Server* self, PyObject*) {
   unsigned long long ph[Impl::kPhases];
   long long total, rv, reqs;
   long long cpu[6];
-  long long io[2];
+  long long io[4];
   Py_BEGIN_ALLOW_THREADS
   {
     std::lock_guard<std::recursive_mutex> g(s->mu);
@@ -3107,6 +3108,11 @@ PyObject* Server_stats(Server* self, PyObject*) {
     cpu[5] = s->slow_admits;
     io[0] = s->sends;
     io[1] = s->turns;
+    io[2] = io[3] = 0;
+    for (auto& kv : s->resources) {
+      io[2] += kv.second->intern.hits;
+      io[3] += kv.second->intern.misses;
+    }
     for (auto& kv : s->verb_cpu) {
       const std::string key = kv.first.verb + (kv.first.sub.empty() ? "" : "/" + kv.first.sub) + ":" +
                               kv.first.ri->resource;
@@ -3143,7 +3149,8 @@ PyObject* Server_stats(Server* self, PyObject*) {
   PyObject* q = PyLong_FromLongLong(reqs);
   PyDict_SetItemString(d, "requests", q);
   Py_DECREF(q);
-  PyObject* io_d = Py_BuildValue("{s:L,s:L}", "sends", io[0], "turns", io[1]);
+  PyObject* io_d = Py_BuildValue("{s:L,s:L,s:L,s:L}", "sends", io[0], "turns", io[1], "shared_subtrees", io[2],
+                                 "kept_subtrees", io[3]);
   PyDict_SetItemString(d, "io", io_d);  // send() calls and event-loop turns
   Py_DECREF(io_d);
   PyObject* c = Py_BuildValue("{s:d,s:d,s:d,s:d,s:d}", "read_parse", cpu[0] * 1e-9, "verbs", cpu[1] * 1e-9,

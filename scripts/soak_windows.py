@@ -18,6 +18,7 @@ import json
 import os
 import statistics
 import sys
+import time
 import urllib.request
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -26,6 +27,23 @@ sys.path.insert(0, ROOT)
 
 def windows(series, size):
     return [series[i:i + size] for i in range(0, len(series) - size + 1, size)]
+
+
+def _fixture_windows(snaps, fires):
+    """Per window: the fixture's requests, sends and phase kcycles per fire, and its RSS."""
+    out = []
+    for a, b in zip(snaps, snaps[1:]):
+        if not a.get("io") or not b.get("io"):
+            continue
+        row = {"requests_per_fire": round((b["requests"] - a["requests"]) / fires, 3),
+               "rss_mib": b.get("rss_mib")}
+        row.update({k + "_per_fire": round((b["io"][k] - a["io"][k]) / fires, 3) for k in b["io"]})
+        row["phase_kcycles_per_fire"] = {k: round((b["phase_cycles"][k] - a["phase_cycles"][k]) / fires / 1000, 1)
+                                         for k in b["phase_cycles"]}
+        row["thread_cpu_us_per_fire"] = {k: round((b["server_thread_cpu_s"][k] - a["server_thread_cpu_s"][k]) * 1e6
+                                                  / fires, 1) for k in b["server_thread_cpu_s"]}
+        out.append(row)
+    return out
 
 
 def main() -> int:
@@ -46,15 +64,47 @@ def main() -> int:
     fixture = {}
     orig = harness._cpu_times
     done = [False]
+    url = [""]
+    pid = [0]
+    per_window = []  # the fixture's counters (and resident size) at each window boundary
+
+    def fixture_snapshot():
+        row = {}
+        try:
+            with urllib.request.urlopen(url[0] + "/debug/fake/stats", timeout=10) as f:
+                st = json.loads(f.read())
+            row = {"requests": st.get("total"), "io": st.get("io"), "phase_cycles": st.get("phase_cycles"),
+                   "server_thread_cpu_s": st.get("server_thread_cpu_s")}
+            with open(f"/proc/{pid[0]}/status") as fh:
+                for line in fh:
+                    if line.startswith("VmRSS"):
+                        row["rss_mib"] = round(int(line.split()[1]) / 1024, 1)
+        except (OSError, ValueError):
+            pass
+        return row
+
+    calib = []  # ms for a fixed CPU-bound loop at each window boundary: the core's speed over the run
+
+    def calibrate():
+        t0 = time.perf_counter()
+        x = 0
+        for i in range(300_000):
+            x += i * i
+        return round((time.perf_counter() - t0) * 1000, 2)
 
     def progress(k, dt, timed):
         if k % 20 == 0:
             print(f"tick {k}: {dt * 1000:.0f} ms", flush=True)
+        if url[0] and k >= a.warmup and (k - a.warmup) % a.window == 0:
+            per_window.append(fixture_snapshot())
+            calib.append(calibrate())
         done[0] = k == a.warmup + a.steps
 
     # the fixture's holdings at the end of the run: read once, after the timed region closed
     def cpu(remote):
         r = orig(remote)
+        if remote is not None and remote.url and remote.proc is not None:
+            url[0], pid[0] = remote.url, remote.proc.pid
         if done[0] and not fixture and remote is not None and remote.url:
             try:
                 with urllib.request.urlopen(remote.url + "/debug/fake/watch-log", timeout=10) as f:
@@ -92,7 +142,9 @@ def main() -> int:
            "apiserver_cpu_us_per_fire_by_window": [round(x, 1) for x in api_w],
            "within_tolerance": all(abs(x) <= a.tolerance for x in rel),
            "shard_peak_rss_mib": res.operator_maxrss_mib, "shard_end_rss_mib": res.operator_rss_mib,
-           "fixture_end": fixture, "operator_gc": res.operator_gc}
+           "fixture_end": fixture, "operator_gc": res.operator_gc,
+           "fixture_by_window": _fixture_windows(per_window, n),
+           "calibration_loop_ms_at_window_starts": calib}
     print(json.dumps(out), flush=True)
     if a.out:
         with open(a.out, "w") as fh:
