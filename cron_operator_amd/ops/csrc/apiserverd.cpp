@@ -971,6 +971,7 @@ struct Impl {
   // under load one send carries many events instead of one send per event per turn
   // (APISERVERD_WATCH_DEFER_S overrides; 0 flushes every turn, as rounds 1-5 did)
   double watch_defer_s = 0.002;
+  bool share_subtrees = true;  // APISERVERD_SHARE_SUBTREES=0: parse every body whole (jdom::Intern)
   bool watch_deferred = false;
   double watch_defer_since = 0.0;
   long long sends = 0, turns = 0;
@@ -1994,7 +1995,7 @@ struct Impl {
     if (!r.body.empty()) {
       std::string perr;
       PhaseTimer pt(&phase[kParse]);
-      body = jdom::parse(r.body.data(), r.body.size(), &perr, &ri->intern);
+      body = jdom::parse(r.body.data(), r.body.size(), &perr, share_subtrees ? &ri->intern : nullptr);
       if (!body) {
         reply_err(rep, bad_request("invalid JSON body: " + perr));
         return;
@@ -2729,6 +2730,7 @@ struct Impl {
   void loop() {
     loop_tid.store(static_cast<pid_t>(syscall(SYS_gettid)));
     if (const char* e = std::getenv("APISERVERD_WATCH_DEFER_S")) watch_defer_s = std::strtod(e, nullptr);
+    if (const char* e = std::getenv("APISERVERD_SHARE_SUBTREES")) share_subtrees = std::strcmp(e, "0") != 0;
     std::vector<struct epoll_event> evs(256);
     push_timer(mono() + bookmark_interval, 2, 0);
     while (!stopping.load()) {

@@ -21,6 +21,7 @@
 
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <new>
@@ -389,10 +390,10 @@ class Parser {
     }
     return nullptr;
   }
-  // a shared node for the container at p_ (p_ moves past it), or null; *h: its bytes' hash
-  // when it is worth keeping (0: not)
-  Ref reuse(uint64_t path, uint64_t* h) {
-    *h = 0;
+  // a shared node for the container at p_ (p_ moves past it), or null; *keep: worth keeping
+  // (then *h is its bytes' hash)
+  Ref reuse(uint64_t path, uint64_t* h, bool* keep_it) {
+    *keep_it = false;
     const char* end = skip_container(p_, e_);
     if (!end || static_cast<size_t>(end - p_) < kSpanMin) return Ref();
     const size_t len = static_cast<size_t>(end - p_);
@@ -404,14 +405,15 @@ class Parser {
       ++in_->hits;
       return sl.n;
     }
-    *h = hb | 1;  // never 0
+    *h = hb;
+    *keep_it = true;
     return Ref();
   }
   void keep(const char* start, Node* n, uint64_t path, uint64_t h) {
     n->enc.assign(start, p_);
-    Intern::Slot& sl = in_->slot((h & ~1ull) ^ path);
+    Intern::Slot& sl = in_->slot(h ^ path);
     ++in_->misses;
-    sl.h = h & ~1ull;
+    sl.h = h;
     sl.path = path;
     sl.n = Ref(n);
   }
@@ -615,8 +617,9 @@ class Parser {
     const char* start = p_;
     const size_t dups0 = dups_;
     uint64_t h = 0;
+    bool keep_it = false;
     if (share && in_) {
-      Ref hit = reuse(path, &h);
+      Ref hit = reuse(path, &h, &keep_it);
       if (hit) return hit;
     }
     const uint64_t elem = mix(path, 0x5bd1e995ull);
@@ -646,7 +649,7 @@ class Parser {
         for (size_t i = base; i < astack_.size(); ++i) n->a.push_back(std::move(astack_[i]));
         astack_.resize(base);
         if (dups_ == dups0) {
-          if (h) keep(start, n, path, h);
+          if (keep_it) keep(start, n, path, h);
           else if ((depth == 1 || depth == 2) && static_cast<size_t>(p_ - start) >= kSpanMin) n->enc.assign(start, p_);
         }
         return r;
@@ -658,8 +661,9 @@ class Parser {
     const char* start = p_;
     const size_t dups0 = dups_;
     uint64_t h = 0;
+    bool keep_it = false;
     if (share && in_) {
-      Ref hit = reuse(path, &h);
+      Ref hit = reuse(path, &h, &keep_it);
       if (hit) return hit;
     }
     ++p_;
@@ -712,7 +716,7 @@ class Parser {
         for (size_t i = base; i < ostack_.size(); ++i) n->o.push_back(std::move(ostack_[i]));
         ostack_.resize(base);
         if (dups_ == dups0) {
-          if (h) keep(start, n, path, h);
+          if (keep_it) keep(start, n, path, h);
           else if ((depth == 1 || depth == 2) && static_cast<size_t>(p_ - start) >= kSpanMin) n->enc.assign(start, p_);
         }
         return r;
