@@ -19,6 +19,7 @@
 // this header's types use them: nothing crosses into libstdc++'s own allocations.
 #pragma once
 
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -36,10 +37,12 @@ namespace pool {
 
 constexpr size_t kMax = 16384;  // larger blocks go to operator new
 constexpr int kClasses = 48;
-constexpr uint32_t kMaxFree = 1u << 15;  // spare blocks kept per class and thread
+constexpr uint32_t kMaxFree = 1u << 15;  // spare blocks kept per class and thread ...
+constexpr size_t kMaxFreeBytes = 4u << 20;  // ... and at most this many bytes of them
 
 struct Tables {
   size_t size[kClasses] = {};
+  uint32_t cap[kClasses] = {};
   unsigned char by16[(kMax >> 4) + 1] = {};
   int n = 0;
   Tables() {
@@ -49,6 +52,8 @@ struct Tables {
       s = s < 256 ? s + 16 : (s + s / 4 + 15) / 16 * 16;
     }
     size[n++] = kMax;
+    for (int i = 0; i < n; ++i)
+      cap[i] = static_cast<uint32_t>(std::max<size_t>(64, std::min<size_t>(kMaxFree, kMaxFreeBytes / size[i])));
     int c = 0;
     for (size_t i = 0; i <= (kMax >> 4); ++i) {
       while (size[c] < (i << 4)) ++c;
@@ -91,9 +96,10 @@ inline void release(void* p, size_t n) noexcept {
     ::operator delete(p);
     return;
   }
-  const unsigned c = tables().by16[(n + 15) >> 4];
+  const Tables& t = tables();
+  const unsigned c = t.by16[(n + 15) >> 4];
   Lists& l = lists();
-  if (l.count[c] >= kMaxFree) {
+  if (l.count[c] >= t.cap[c]) {
     ::operator delete(p);
     return;
   }
@@ -178,7 +184,7 @@ struct Node {
   }
   static void operator delete(void* ptr) {
     NodePool& p = NodePool::get();
-    if (p.cached >= (1u << 20)) {  // keep at most ~1M spare nodes
+    if (p.cached >= (1u << 18)) {  // keep at most 256K spare nodes (~32 MiB)
       ::operator delete(ptr);
       return;
     }
