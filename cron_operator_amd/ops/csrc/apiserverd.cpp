@@ -791,7 +791,6 @@ struct Resource {
   std::unique_ptr<Schema> schema, status_schema;
   Ref schema_src;
   Store* store = nullptr;
-  jdom::Intern intern;  // subtrees this resource's request bodies repeat (jdom.h)
 };
 
 const Node* labels_of(const Node* obj) {
@@ -971,7 +970,6 @@ struct Impl {
   // under load one send carries many events instead of one send per event per turn
   // (APISERVERD_WATCH_DEFER_S overrides; 0 flushes every turn, as rounds 1-5 did)
   double watch_defer_s = 0.002;
-  bool share_subtrees = true;  // APISERVERD_SHARE_SUBTREES=0: parse every body whole (jdom::Intern)
   bool watch_deferred = false;
   double watch_defer_since = 0.0;
   long long sends = 0, turns = 0;
@@ -1995,7 +1993,7 @@ struct Impl {
     if (!r.body.empty()) {
       std::string perr;
       PhaseTimer pt(&phase[kParse]);
-      body = jdom::parse(r.body.data(), r.body.size(), &perr, share_subtrees ? &ri->intern : nullptr);
+      body = jdom::parse(r.body.data(), r.body.size(), &perr);
       if (!body) {
         reply_err(rep, bad_request("invalid JSON body: " + perr));
         return;
@@ -2730,7 +2728,6 @@ struct Impl {
   void loop() {
     loop_tid.store(static_cast<pid_t>(syscall(SYS_gettid)));
     if (const char* e = std::getenv("APISERVERD_WATCH_DEFER_S")) watch_defer_s = std::strtod(e, nullptr);
-    if (const char* e = std::getenv("APISERVERD_SHARE_SUBTREES")) share_subtrees = std::strcmp(e, "0") != 0;
     std::vector<struct epoll_event> evs(256);
     push_timer(mono() + bookmark_interval, 2, 0);
     while (!stopping.load()) {
@@ -3089,7 +3086,7 @@ PyObject* Server_stats(Server* self, PyObject*) {
   unsigned long long ph[Impl::kPhases];
   long long total, rv, reqs;
   long long cpu[6];
-  long long io[4];
+  long long io[2];
   Py_BEGIN_ALLOW_THREADS
   {
     std::lock_guard<std::recursive_mutex> g(s->mu);
@@ -3110,11 +3107,6 @@ PyObject* Server_stats(Server* self, PyObject*) {
     cpu[5] = s->slow_admits;
     io[0] = s->sends;
     io[1] = s->turns;
-    io[2] = io[3] = 0;
-    for (auto& kv : s->resources) {
-      io[2] += kv.second->intern.hits;
-      io[3] += kv.second->intern.misses;
-    }
     for (auto& kv : s->verb_cpu) {
       const std::string key = kv.first.verb + (kv.first.sub.empty() ? "" : "/" + kv.first.sub) + ":" +
                               kv.first.ri->resource;
@@ -3151,8 +3143,7 @@ PyObject* Server_stats(Server* self, PyObject*) {
   PyObject* q = PyLong_FromLongLong(reqs);
   PyDict_SetItemString(d, "requests", q);
   Py_DECREF(q);
-  PyObject* io_d = Py_BuildValue("{s:L,s:L,s:L,s:L}", "sends", io[0], "turns", io[1], "shared_subtrees", io[2],
-                                 "kept_subtrees", io[3]);
+  PyObject* io_d = Py_BuildValue("{s:L,s:L}", "sends", io[0], "turns", io[1]);
   PyDict_SetItemString(d, "io", io_d);  // send() calls and event-loop turns
   Py_DECREF(io_d);
   PyObject* c = Py_BuildValue("{s:d,s:d,s:d,s:d,s:d}", "read_parse", cpu[0] * 1e-9, "verbs", cpu[1] * 1e-9,

@@ -311,53 +311,13 @@ inline Ref shallow(const Node* n) {
 // (Node::set/erase clear the node's own; apiserverd's admission reports changes upward).
 constexpr size_t kSpanMin = 24;
 
-// 64-bit hash of a byte run (8 bytes a step)
-inline uint64_t hash_bytes(const char* p, size_t n) {
-  uint64_t h = 0x9E3779B97F4A7C15ull ^ (n * 0xff51afd7ed558ccdull);
-  while (n >= 8) {
-    uint64_t v;
-    std::memcpy(&v, p, 8);
-    h = (h ^ v) * 0xff51afd7ed558ccdull;
-    h ^= h >> 32;
-    p += 8;
-    n -= 8;
-  }
-  uint64_t v = 0;
-  std::memcpy(&v, p, n);
-  h = (h ^ v) * 0xc4ceb9fe1a85ec53ull;
-  return h ^ (h >> 29);
-}
-
-// Subtrees a resource's request bodies repeat byte for byte -- a job's spec (every job a
-// template makes is the same), the history and active entries a Cron's status patch carries
-// from one write to the next -- are parsed once and shared: the parser finds the value's end,
-// hashes its bytes with its path (key names, array positions folded), and reuses the node that
-// decoded to exactly those bytes at that path.  A reused node is one the store already holds
-// (admission marked it, so admission skips it) or one a rejected request left (still private:
-// whoever mutates a node clears its enc, which is what a hit is checked against).  Direct-mapped:
-// a slot holds the last subtree that hashed there.  Per resource (one schema per path).
-struct Intern {
-  struct Slot {
-    uint64_t h = 0, path = 0;
-    Ref n;
-  };
-  static constexpr size_t kSlots = 1 << 14;
-  std::vector<Slot> slots;
-  long long hits = 0, misses = 0;
-  Slot& slot(uint64_t key) {
-    if (slots.empty()) slots.resize(kSlots);
-    return slots[key & (kSlots - 1)];
-  }
-  void clear() { slots.clear(); }
-};
-
 class Parser {
  public:
-  Parser(const char* b, size_t n, Intern* in = nullptr) : p_(b), e_(b + n), in_(in) {}
+  Parser(const char* b, size_t n) : p_(b), e_(b + n) {}
   // nullptr Ref + err() on malformed input
   Ref parse() {
     ws();
-    Ref r = value(0, 0, false);
+    Ref r = value(0);
     astack_.clear();  // a failed parse leaves partial containers on the shared stacks
     ostack_.clear();
     if (!r) return r;
@@ -370,59 +330,7 @@ class Parser {
  private:
   const char* p_;
   const char* e_;
-  Intern* in_;
   std::string err_;
-
-  static uint64_t mix(uint64_t a, uint64_t b) {
-    const uint64_t h = (a ^ b) * 0x100000001b3ull + 0x9E3779B97F4A7C15ull;
-    return h ^ (h >> 31);
-  }
-  // the end of the container at p (strings skipped with their escapes), or nullptr
-  static const char* skip_container(const char* p, const char* e) {
-    int d = 0;
-    while (p < e) {
-      const char c = *p++;
-      if (c == '"') {
-        while (p < e) {
-          const char x = *p++;
-          if (x == '\\') ++p;
-          else if (x == '"') break;
-        }
-      } else if (c == '{' || c == '[') {
-        ++d;
-      } else if (c == '}' || c == ']') {
-        if (--d == 0) return p;
-      }
-    }
-    return nullptr;
-  }
-  // a shared node for the container at p_ (p_ moves past it), or null; *keep: worth keeping
-  // (then *h is its bytes' hash)
-  Ref reuse(uint64_t path, uint64_t* h, bool* keep_it) {
-    *keep_it = false;
-    const char* end = skip_container(p_, e_);
-    if (!end || static_cast<size_t>(end - p_) < kSpanMin) return Ref();
-    const size_t len = static_cast<size_t>(end - p_);
-    const uint64_t hb = hash_bytes(p_, len);
-    Intern::Slot& sl = in_->slot(hb ^ path);
-    if (sl.n && sl.h == hb && sl.path == path && sl.n->enc.size() == len &&
-        std::memcmp(sl.n->enc.data(), p_, len) == 0) {
-      p_ = end;
-      ++in_->hits;
-      return sl.n;
-    }
-    *h = hb;
-    *keep_it = true;
-    return Ref();
-  }
-  void keep(const char* start, Node* n, uint64_t path, uint64_t h) {
-    n->enc.assign(start, p_);
-    Intern::Slot& sl = in_->slot(h ^ path);
-    ++in_->misses;
-    sl.h = h;
-    sl.path = path;
-    sl.n = Ref(n);
-  }
 
   Ref fail(const char* m) {
     if (err_.empty()) err_ = m;
@@ -431,13 +339,12 @@ class Parser {
   void ws() {
     while (p_ < e_ && (*p_ == ' ' || *p_ == '\t' || *p_ == '\n' || *p_ == '\r')) ++p_;
   }
-  // path: the hash of the keys (and array positions) leading here; share: may reuse/keep
-  Ref value(int depth, uint64_t path, bool share) {
+  Ref value(int depth) {
     if (depth > 512) return fail("nesting too deep");
     if (p_ >= e_) return fail("unexpected end of JSON");
     switch (*p_) {
-      case '{': return object(depth, path, share);
-      case '[': return array(depth, path, share);
+      case '{': return object(depth);
+      case '[': return array(depth);
       case '"': {
         Node* n = new Node(T::Str);
         Ref r(n);
@@ -619,16 +526,9 @@ class Parser {
   std::vector<Member>& ostack_ = ostack();
   size_t dups_ = 0;  // repeated keys seen so far: a span holding one is not its node's encoding
 
-  Ref array(int depth, uint64_t path, bool share) {
+  Ref array(int depth) {
     const char* start = p_;
     const size_t dups0 = dups_;
-    uint64_t h = 0;
-    bool keep_it = false;
-    if (share && in_) {
-      Ref hit = reuse(path, &h, &keep_it);
-      if (hit) return hit;
-    }
-    const uint64_t elem = mix(path, 0x5bd1e995ull);
     ++p_;
     Node* n = new Node(T::Arr);
     Ref r(n);
@@ -640,7 +540,7 @@ class Parser {
     const size_t base = astack_.size();
     while (true) {
       ws();
-      Ref v = value(depth + 1, elem, true);
+      Ref v = value(depth + 1);
       if (!v) return Ref();
       astack_.push_back(std::move(v));
       ws();
@@ -654,24 +554,16 @@ class Parser {
         n->a.reserve(astack_.size() - base);
         for (size_t i = base; i < astack_.size(); ++i) n->a.push_back(std::move(astack_[i]));
         astack_.resize(base);
-        if (dups_ == dups0) {
-          if (keep_it) keep(start, n, path, h);
-          else if ((depth == 1 || depth == 2) && static_cast<size_t>(p_ - start) >= kSpanMin) n->enc.assign(start, p_);
-        }
+        if ((depth == 1 || depth == 2) && static_cast<size_t>(p_ - start) >= kSpanMin && dups_ == dups0)
+          n->enc.assign(start, p_);
         return r;
       }
       return fail("expected ',' or ']'");
     }
   }
-  Ref object(int depth, uint64_t path, bool share) {
+  Ref object(int depth) {
     const char* start = p_;
     const size_t dups0 = dups_;
-    uint64_t h = 0;
-    bool keep_it = false;
-    if (share && in_) {
-      Ref hit = reuse(path, &h, &keep_it);
-      if (hit) return hit;
-    }
     ++p_;
     Node* n = new Node(T::Obj);
     Ref r(n);
@@ -690,10 +582,7 @@ class Parser {
       if (p_ >= e_ || *p_ != ':') return fail("expected ':'");
       ++p_;
       ws();
-      const jstr& key = ostack_.back().first;
-      // the root's metadata is written in place by create and update: never shared
-      const bool child_share = depth > 0 || key != "metadata";
-      Ref v = value(depth + 1, in_ ? mix(path, hash_bytes(key.data(), key.size())) : 0, child_share);
+      Ref v = value(depth + 1);
       if (!v) return Ref();
       // a repeated key keeps the last value, as Python's json does
       const jstr& k = ostack_.back().first;
@@ -721,10 +610,8 @@ class Parser {
         n->o.reserve(ostack_.size() - base);
         for (size_t i = base; i < ostack_.size(); ++i) n->o.push_back(std::move(ostack_[i]));
         ostack_.resize(base);
-        if (dups_ == dups0) {
-          if (keep_it) keep(start, n, path, h);
-          else if ((depth == 1 || depth == 2) && static_cast<size_t>(p_ - start) >= kSpanMin) n->enc.assign(start, p_);
-        }
+        if ((depth == 1 || depth == 2) && static_cast<size_t>(p_ - start) >= kSpanMin && dups_ == dups0)
+          n->enc.assign(start, p_);
         return r;
       }
       return fail("expected ',' or '}'");
@@ -732,8 +619,8 @@ class Parser {
   }
 };
 
-inline Ref parse(const char* b, size_t n, std::string* err = nullptr, Intern* in = nullptr) {
-  Parser p(b, n, in);
+inline Ref parse(const char* b, size_t n, std::string* err = nullptr) {
+  Parser p(b, n);
   Ref r = p.parse();
   if (!r && err) *err = p.err();
   return r;

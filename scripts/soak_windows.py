@@ -83,14 +83,22 @@ def main() -> int:
             pass
         return row
 
-    calib = []  # ms for a fixed CPU-bound loop at each window boundary: the core's speed over the run
+    # at each window boundary: ms for a fixed CPU-bound loop (the core's speed) and for a walk
+    # over 64 MiB (what the memory system gives under the neighbours' load) -- the box is shared
+    calib = []
+    import numpy as np
+
+    walk = np.random.default_rng(0).permutation(1 << 23).astype(np.int64)  # 64 MiB of indices
 
     def calibrate():
         t0 = time.perf_counter()
         x = 0
         for i in range(300_000):
             x += i * i
-        return round((time.perf_counter() - t0) * 1000, 2)
+        t1 = time.perf_counter()
+        int(walk[walk[::16]].sum())  # a gather over the whole array: cache-missing loads
+        t2 = time.perf_counter()
+        return [round((t1 - t0) * 1000, 2), round((t2 - t1) * 1000, 2)]
 
     def progress(k, dt, timed):
         if k % 20 == 0:
@@ -144,7 +152,8 @@ def main() -> int:
            "shard_peak_rss_mib": res.operator_maxrss_mib, "shard_end_rss_mib": res.operator_rss_mib,
            "fixture_end": fixture, "operator_gc": res.operator_gc,
            "fixture_by_window": _fixture_windows(per_window, n),
-           "calibration_loop_ms_at_window_starts": calib}
+           "calibration_ms_at_window_starts": {"cpu_loop": [c[0] for c in calib],
+                                               "memory_walk_64mib": [c[1] for c in calib]}}
     print(json.dumps(out), flush=True)
     if a.out:
         with open(a.out, "w") as fh:
