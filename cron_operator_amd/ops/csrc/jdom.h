@@ -52,8 +52,11 @@ struct Tables {
       s = s < 256 ? s + 16 : (s + s / 4 + 15) / 16 * 16;
     }
     size[n++] = kMax;
+    // JDOM_POOL=0: no spare blocks at all (every block back to malloc: the soak's A/B arm)
+    const char* env = std::getenv("JDOM_POOL");
+    const bool off = env && env[0] == '0';
     for (int i = 0; i < n; ++i)
-      cap[i] = static_cast<uint32_t>(std::max<size_t>(64, std::min<size_t>(kMaxFree, kMaxFreeBytes / size[i])));
+      cap[i] = off ? 0u : static_cast<uint32_t>(std::max<size_t>(64, std::min<size_t>(kMaxFree, kMaxFreeBytes / size[i])));
     int c = 0;
     for (size_t i = 0; i <= (kMax >> 4); ++i) {
       while (size[c] < (i << 4)) ++c;
@@ -165,6 +168,11 @@ struct NodePool {
   };
   Free* head = nullptr;
   size_t cached = 0;
+  size_t cap = 1u << 18;  // at most 256K spare nodes (~32 MiB); JDOM_POOL=0: none
+  NodePool() {
+    const char* env = std::getenv("JDOM_POOL");
+    if (env && env[0] == '0') cap = 0;
+  }
   static NodePool& get() {
     static NodePool p;
     return p;
@@ -184,7 +192,7 @@ struct Node {
   }
   static void operator delete(void* ptr) {
     NodePool& p = NodePool::get();
-    if (p.cached >= (1u << 18)) {  // keep at most 256K spare nodes (~32 MiB)
+    if (p.cached >= p.cap) {
       ::operator delete(ptr);
       return;
     }
