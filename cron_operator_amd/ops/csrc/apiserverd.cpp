@@ -285,12 +285,13 @@ std::string b64url_encode(const std::string& in) {
 }
 
 bool b64url_decode(const std::string& in, std::string* out) {
-  int val = 0, bits = -8;
+  unsigned val = 0;  // only the low 14 bits are ever pending: masked, it never overflows
+  int bits = -8;
   for (char c : in) {
     if (c == '=') break;
     const char* p = std::strchr(b64url_chars, c);
     if (!p || !*p) return false;
-    val = (val << 6) + static_cast<int>(p - b64url_chars);
+    val = ((val << 6) | static_cast<unsigned>(p - b64url_chars)) & 0xFFFFFFu;
     bits += 6;
     if (bits >= 0) {
       out->push_back(static_cast<char>((val >> bits) & 0xFF));
@@ -3340,6 +3341,51 @@ PyObject* Server_patch_many(Server* self, PyObject* args) {
 //   -> int: one merge PATCH per object whose status has no completionTime, its body the template
 //   with `placeholder` replaced by the object's name -- the bench's "every job finishes" write,
 //   without a Python round trip per job
+// `t` with every `ph` inside its strings replaced by `name` (keys untouched): a node whose
+// subtree holds no placeholder is shared, not copied
+Ref subst(const Ref& t, const std::string& ph, const std::string& name) {
+  switch (t->t) {
+    case T::Str: {
+      if (t->s.find(ph.data(), 0, ph.size()) == jdom::jstr::npos) return t;
+      std::string v;
+      size_t pos = 0;
+      const std::string_view sv(t->s);
+      while (true) {
+        const size_t hit = sv.find(ph, pos);
+        if (hit == std::string_view::npos) {
+          v.append(sv.substr(pos));
+          break;
+        }
+        v.append(sv.substr(pos, hit - pos));
+        v.append(name);
+        pos = hit + ph.size();
+      }
+      return jdom::mk_str(v);
+    }
+    case T::Arr: {
+      Ref out;
+      for (size_t i = 0; i < t->a.size(); ++i) {
+        Ref c = subst(t->a[i], ph, name);
+        if (c == t->a[i]) continue;
+        if (!out) out = jdom::shallow(t.get());
+        out->a[i] = std::move(c);
+      }
+      return out ? out : t;
+    }
+    case T::Obj: {
+      Ref out;
+      for (size_t i = 0; i < t->o.size(); ++i) {
+        Ref c = subst(t->o[i].second, ph, name);
+        if (c == t->o[i].second) continue;
+        if (!out) out = jdom::shallow(t.get());
+        out->o[i].second = std::move(c);
+      }
+      return out ? out : t;
+    }
+    default: return t;
+  }
+}
+
 PyObject* Server_patch_unfinished(Server* self, PyObject* args) {
   const char *g, *v, *r, *ns, *tmpl, *ph, *sub = "";
   Py_ssize_t tl, pl;
@@ -3369,22 +3415,12 @@ PyObject* Server_patch_unfinished(Server* self, PyObject* args) {
           todo.emplace_back(kv.first, ob.first);
         }
       }
-      std::string body;
+      // the template parsed once; each job's patch copies only the nodes whose strings hold
+      // the placeholder (a condition's message), the rest is shared
+      Ref tree = jdom::parse(ts.data(), ts.size());
       for (const auto& t : todo) {
-        body.clear();
-        size_t pos = 0;
-        while (true) {
-          const size_t hit = ts.find(phs, pos);
-          if (hit == std::string::npos) {
-            body.append(ts, pos, std::string::npos);
-            break;
-          }
-          body.append(ts, pos, hit - pos);
-          body.append(t.second);  // names are DNS-1123: nothing to escape
-          pos = hit + phs.size();
-        }
-        Ref patch = jdom::parse(body.data(), body.size());
-        if (!patch) continue;
+        if (!tree) break;
+        Ref patch = subst(tree, phs, t.second);
         ApiErr err;
         if (s->v_patch(ri, t.first, t.second, patch, "merge", subs, &err)) ++n;
       }

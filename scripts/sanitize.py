@@ -24,6 +24,12 @@ every entry point with mutated and generated inputs:
   cancelled waiters;
 * ``_cron_engine``: random and malformed cron specs through parse/next/missed, mutated and
   out-of-range RFC 3339 timestamps through rfc3339_z/format_rfc3339;
+* ``_apiserverd`` (the benchmark's fake apiserver): random request streams in process (create,
+  update, merge patch, status, delete, LIST with selectors and garbage continue tokens) with
+  valid and mutated bodies against the installed CRDs' admission; the bulk controls
+  (``patch_many``, ``patch_unfinished``, ``unfinished``); and over HTTP on its epoll thread:
+  mutated raw requests in random splits, watches opened at random resourceVersions and
+  dropped mid-stream while writes fan out to them, then ``stop``;
 
 Any memory error or undefined behaviour aborts with the sanitizer report.
 ``make sanitize`` runs it.  Host code only: the operator has no GPU code.
@@ -41,8 +47,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CSRC = os.path.join(ROOT, "cron_operator_amd", "ops", "csrc")
 EXTS = {"_cron_engine": "cron_engine.cpp", "_fastjson": "fastjson.cpp", "_httpcodec": "httpcodec.cpp",
         "_netconn": "netconn.cpp", "_aioloop": "aioloop.cpp", "_promlite": "promlite.cpp",
-        "_workqueue": "workqueue.cpp"}
-LIBS = {"_netconn": ["-lssl", "-lcrypto", "-ldl"]}
+        "_workqueue": "workqueue.cpp", "_apiserverd": "apiserverd.cpp"}
+LIBS = {"_netconn": ["-lssl", "-lcrypto", "-ldl"], "_apiserverd": ["-lssl", "-lcrypto", "-pthread"]}
 
 
 def build(out_dir: str) -> None:
@@ -559,10 +565,144 @@ def drive_tls(rng: random.Random, cases: int, scratch: str) -> int:
     return built + handshakes
 
 
+def drive_apiserverd(scratch: str, iters: int) -> int:
+    """The native fake apiserver under the sanitizers: in-process request streams, the bulk
+    controls, then HTTP on its own thread with watches that come and go."""
+    import json
+    import socket
+    import time
+
+    sys.path.insert(0, scratch)
+    sys.path.insert(0, ROOT)
+    import _apiserverd as ad  # noqa: E402
+
+    from cron_operator_amd.api.v1alpha1.crd import crd  # noqa: E402
+    from cron_operator_amd.trainingop.crds import kubeflow_crds  # noqa: E402
+
+    rng = random.Random(11)
+    srv = ad.Server(now_ns=1767268800 * 10**9, watch_window=64, bookmark_interval=0.05)
+    srv.set_fallback(lambda *a: None)
+    for c in [crd(), *kubeflow_crds()]:
+        st, _ = srv.request("POST", "/apis/apiextensions.k8s.io/v1/customresourcedefinitions", "",
+                            json.dumps(c).encode(), "application/json")
+        assert st in (200, 201), st
+    srv.request("POST", "/api/v1/namespaces", "", b'{"metadata":{"name":"ns"}}', "application/json")
+    crons = "/apis/apps.kubedl.io/v1alpha1/namespaces/ns/crons"
+    jobs = "/apis/kubeflow.org/v1/namespaces/ns/pytorchjobs"
+    cms = "/api/v1/namespaces/ns/configmaps"
+
+    def cron(i):
+        return {"apiVersion": "apps.kubedl.io/v1alpha1", "kind": "Cron",
+                "metadata": {"name": f"c{i}", "labels": {"app": rng.choice("ab"), "n": str(i % 3)}},
+                "spec": {"schedule": rng.choice(["* * * * *", "bad", "*/5 * * * *"]),
+                         "concurrencyPolicy": rng.choice(["Allow", "Forbid", "Replace", "Nope"]),
+                         "historyLimit": rng.choice([1, 10, -1, "x"]),
+                         "template": {"workload": {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+                                                   "spec": _tree(rng)}}, "extra": _tree(rng)}}
+
+    def job(i):
+        return {"apiVersion": "kubeflow.org/v1", "kind": "PyTorchJob",
+                "metadata": {"name": f"j{i}", "labels": {"kubedl.io/cron-name": f"c{i % 7}"}},
+                "spec": {"pytorchReplicaSpecs": {"Master": {"replicas": rng.choice([1, 2, "x"])}}},
+                "status": _tree(rng)}
+
+    def body(obj):
+        raw = json.dumps(obj).encode()
+        return _mutate(rng, raw) if rng.random() < 0.2 else raw
+
+    n = 0
+    for _ in range(iters):
+        i = rng.randrange(20)
+        base, mk = rng.choice([(crons, cron), (jobs, job), (cms, lambda i: {"metadata": {"name": f"m{i}"},
+                                                                          "data": {"k": str(rng.random())}})])
+        op = rng.random()
+        if op < 0.25:
+            srv.request("POST", base, "", body(mk(i)), "application/json")
+        elif op < 0.4:
+            srv.request("PUT", f"{base}/{mk(i)['metadata']['name']}", "", body(mk(i)), "application/json")
+        elif op < 0.6:
+            sub = rng.choice(["", "/status"])
+            patch = rng.choice([{"status": _tree(rng)}, {"metadata": {"labels": {"app": rng.choice(["a", None])}}},
+                                {"spec": _tree(rng)}, _tree(rng)])
+            srv.request("PATCH", f"{base}/{mk(i)['metadata']['name']}{sub}", "", body(patch),
+                        rng.choice(["application/merge-patch+json", "application/json-patch+json",
+                                    "application/strategic-merge-patch+json"]))
+        elif op < 0.72:
+            srv.request("DELETE", f"{base}/{mk(i)['metadata']['name']}", "",
+                        body(rng.choice([{}, {"preconditions": {"uid": "x"}}, {"propagationPolicy": "Foreground"}])),
+                        "application/json")
+        elif op < 0.9:
+            q = rng.choice(["", "labelSelector=app%3Da", "labelSelector=n+in+(1,2),app!=b", "limit=2",
+                            "limit=1&continue=" + rng.choice(["", "eyJ4Ijox", "%%%", "abc"]),
+                            "fieldSelector=metadata.name%3Dc1", "labelSelector=%21%21", "watch=true"])
+            srv.request("GET", base, q)
+        else:
+            srv.request("DELETE", base, rng.choice(["", "labelSelector=app%3Db"]))
+        if rng.random() < 0.02:
+            srv.set_clock((1767268800 + rng.randrange(10**6)) * 10**9)
+        n += 1
+    tmpl = json.dumps({"status": {"conditions": [{"type": "Succeeded", "status": "True",
+                                                  "message": "@@name@@ done"}],
+                                  "completionTime": "2026-01-01T00:00:00Z"}}).encode()
+    for name, kind, enc in srv.unfinished("kubeflow.org", "v1", "pytorchjobs", "ns"):
+        json.loads(enc)
+    srv.patch_many("kubeflow.org", "v1", "pytorchjobs", "ns",
+                   [(f"j{i}", _mutate(rng, tmpl) if i % 3 == 0 else tmpl) for i in range(20)], "status")
+    srv.patch_unfinished("kubeflow.org", "v1", "pytorchjobs", "ns", tmpl, b"@@name@@", "status")
+    srv.stats()
+    srv.log_sizes()
+
+    # HTTP: the epoll thread, watches dropped mid-stream while writes fan out
+    port = srv.start("127.0.0.1", 0, "", "")
+    socks = []
+    for k in range(iters // 20):
+        r = rng.random()
+        if r < 0.3:
+            s = socket.create_connection(("127.0.0.1", port))
+            rv = rng.choice(["0", "1", "", str(rng.randrange(10**6)), "x"])
+            s.sendall(f"GET {rng.choice([crons, jobs])}?watch=true&resourceVersion={rv}"
+                      f"&allowWatchBookmarks=true HTTP/1.1\r\nHost: x\r\n\r\n".encode())
+            socks.append(s)
+        elif r < 0.8:
+            i = rng.randrange(20)
+            raw = json.dumps(job(i)).encode()
+            req = (f"POST {jobs} HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\n"
+                   f"Content-Length: {len(raw)}\r\n\r\n").encode() + raw
+            if rng.random() < 0.3:
+                req = _mutate(rng, req)
+            s = socket.create_connection(("127.0.0.1", port))
+            for j in range(0, len(req), rng.randint(1, 64)):
+                s.sendall(req[j:j + 64])
+            if rng.random() < 0.5:
+                s.settimeout(1)
+                try:
+                    s.recv(65536)
+                except OSError:
+                    pass
+            s.close()
+        else:
+            srv.request("DELETE", f"{jobs}/j{rng.randrange(20)}", "", b"{}", "application/json")
+        if socks and rng.random() < 0.3:
+            s = socks.pop(rng.randrange(len(socks)))
+            s.setblocking(False)
+            try:
+                s.recv(rng.randint(1, 4096))
+            except OSError:
+                pass
+            s.close()
+    time.sleep(0.2)
+    for s in socks:
+        s.close()
+    srv.stop()
+    return n
+
+
 def main() -> int:
     iters = int(os.environ.get("SANITIZE_ITERS", "20000"))
     if os.environ.get("_SANITIZE_CHILD"):
         drive(os.environ["_SANITIZE_CHILD"], iters)
+        n = drive_apiserverd(os.environ["_SANITIZE_CHILD"], max(200, iters // 10))
+        print(f"sanitize ok: _apiserverd {n} in-process requests, {max(200, iters // 10) // 20} HTTP cases")
         return 0
     with tempfile.TemporaryDirectory(prefix="sanitize-") as d:
         build(d)
