@@ -767,10 +767,16 @@ struct Schema {
 struct Watcher;
 struct Conn;
 
+// One event of the watch log.  The log keeps what a resuming watch needs -- the bytes the
+// event carries and, for its scope, the object's (and for MODIFIED its previous version's)
+// name, namespace and labels -- not the object trees: a superseded version is freed when the
+// store replaces it, while its nodes are still in cache, instead of watch_window events later
+// (when the log held the trees, the fixture's CPU per fire drifted with the heap's age).
 struct Event {
   long long rv;
   int type;  // 0 ADDED 1 MODIFIED 2 DELETED
-  Ref obj, old;
+  Ref scope, old_scope;                      // {"metadata": {name, namespace, labels}}
+  std::shared_ptr<const std::string> bytes;  // the object as encoded in the event
 };
 
 const char* kEventType[] = {"ADDED", "MODIFIED", "DELETED"};
@@ -1192,23 +1198,28 @@ struct Impl {
     return o;
   }
 
-  void put_event(Watcher* w, int type, Node* obj) {
+  void put_event(Watcher* w, int type, std::string_view obj) {
     if (w->ended) return;
     ++w->sent;
     std::string& p = event_sink(w);
     p.append("{\"type\":\"");
     p.append(kEventType[type]);
     p.append("\",\"object\":");
-    jdom::write(&p, obj);
+    p.append(obj.data(), obj.size());
     p.append("}\n");
     if (!w->dirty) {
       w->dirty = true;
       dirty_watchers.push_back(w);
     }
   }
+  void put_event(Watcher* w, int type, Node* obj) {
+    const jdom::jstr& e = jdom::encoded(obj);
+    put_event(w, type, std::string_view(e));
+  }
 
-  void offer(Watcher* w, int type, Node* obj, Node* old, bool now_in, bool was_in) {
-    if (type == 1 && old) {
+  // a MODIFIED that moves an object into or out of a watcher's scope is an ADDED / DELETED
+  void offer(Watcher* w, int type, std::string_view obj, bool modified_with_old, bool now_in, bool was_in) {
+    if (type == 1 && modified_with_old) {
       if (was_in && !now_in) put_event(w, 2, obj);
       else if (now_in && !was_in) put_event(w, 0, obj);
       else if (now_in) put_event(w, 1, obj);
@@ -1217,10 +1228,26 @@ struct Impl {
     if (now_in) put_event(w, type, obj);
   }
 
+  // what a resuming watcher's scope reads of an object: its name, namespace and labels
+  static Ref scope_of(const Node* obj) {
+    Ref sc = jdom::mk_obj();
+    const Node* m = obj->getn("metadata");
+    if (m && m->is_obj()) {
+      Ref mm = jdom::mk_obj();
+      for (const char* k : {"name", "namespace", "labels"})
+        if (const Ref* v = m->get(k)) mm->o.emplace_back(k, *v);
+      sc->o.emplace_back("metadata", mm);
+    }
+    return sc;
+  }
+
   void emit(Resource* ri, int type, const Ref& obj, const Ref& old, long long at) {
     PhaseTimer pt(&phase[kEmit]);
     Store* st = ri->store;
-    st->log.push_back(Event{at, type, obj, old});
+    const jdom::jstr& enc = jdom::encoded(obj.get());
+    const bool with_old = type == 1 && old;
+    st->log.push_back(Event{at, type, scope_of(obj.get()), with_old ? scope_of(old.get()) : Ref(),
+                            std::make_shared<const std::string>(enc.data(), enc.size())});
     while (st->log.size() > watch_window) {
       st->floor = st->log.front().rv;
       st->log.pop_front();
@@ -1238,12 +1265,13 @@ struct Impl {
                      om->str("namespace") == nm->str("namespace");
       }
     }
+    const std::string_view bytes(enc);
     for (Watcher* w : st->watchers) {
       if (w->ended) continue;
       const bool now_in = w->in_scope(obj.get());
       bool was_in = false;
       if (modified) was_in = (same_scope && w->sel.labels_only) ? now_in : w->in_scope(old.get());
-      if (now_in || was_in) offer(w, type, obj.get(), old.get(), now_in, was_in);
+      if (now_in || was_in) offer(w, type, bytes, with_old, now_in, was_in);
     }
   }
 
@@ -2102,11 +2130,19 @@ struct Impl {
                                          std::to_string(st->floor + 1) + ")");
         return nullptr;
       }
+      // the log keeps each event's name, namespace and labels: a field selector on any other
+      // field cannot be replayed, and the watcher relists (as past a compacted revision)
+      for (const FieldReq& f : w->sel.fields)
+        if (!(f.path.size() == 2 && f.path[0] == "metadata" && (f.path[1] == "name" || f.path[1] == "namespace"))) {
+          *err = mkerr(410, "Expired", "too old resource version: " + std::to_string(since) + " (" +
+                                           std::to_string(rv + 1) + ")");
+          return nullptr;
+        }
       for (const Event& ev : st->log)
         if (ev.rv > since) {
-          const bool now_in = w->in_scope(ev.obj.get());
-          const bool was_in = ev.type == 1 && ev.old ? w->in_scope(ev.old.get()) : false;
-          offer(w.get(), ev.type, ev.obj.get(), ev.old.get(), now_in, was_in);
+          const bool now_in = w->in_scope(ev.scope.get());
+          const bool was_in = ev.type == 1 && ev.old_scope ? w->in_scope(ev.old_scope.get()) : false;
+          offer(w.get(), ev.type, std::string_view(*ev.bytes), static_cast<bool>(ev.old_scope), now_in, was_in);
         }
     }
     Watcher* out = w.release();
