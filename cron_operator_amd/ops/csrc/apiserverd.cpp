@@ -777,6 +777,7 @@ struct Event {
   int type;  // 0 ADDED 1 MODIFIED 2 DELETED
   Ref scope, old_scope;                      // {"metadata": {name, namespace, labels}}
   std::shared_ptr<const std::string> bytes;  // the object as encoded in the event
+  Ref held, held_old;  // APISERVERD_LOG_TREES=1 only: the trees too, as rounds 1-5 kept them (A/B arm)
 };
 
 const char* kEventType[] = {"ADDED", "MODIFIED", "DELETED"};
@@ -977,6 +978,7 @@ struct Impl {
   // under load one send carries many events instead of one send per event per turn
   // (APISERVERD_WATCH_DEFER_S overrides; 0 flushes every turn, as rounds 1-5 did)
   double watch_defer_s = 0.002;
+  bool log_trees = false;  // APISERVERD_LOG_TREES=1: the log also holds the object trees (A/B)
   bool watch_deferred = false;
   double watch_defer_since = 0.0;
   long long sends = 0, turns = 0;
@@ -1247,7 +1249,8 @@ struct Impl {
     const jdom::jstr& enc = jdom::encoded(obj.get());
     const bool with_old = type == 1 && old;
     st->log.push_back(Event{at, type, scope_of(obj.get()), with_old ? scope_of(old.get()) : Ref(),
-                            std::make_shared<const std::string>(enc.data(), enc.size())});
+                            std::make_shared<const std::string>(enc.data(), enc.size()),
+                            log_trees ? obj : Ref(), log_trees ? old : Ref()});
     while (st->log.size() > watch_window) {
       st->floor = st->log.front().rv;
       st->log.pop_front();
@@ -2765,6 +2768,7 @@ struct Impl {
   void loop() {
     loop_tid.store(static_cast<pid_t>(syscall(SYS_gettid)));
     if (const char* e = std::getenv("APISERVERD_WATCH_DEFER_S")) watch_defer_s = std::strtod(e, nullptr);
+    if (const char* e = std::getenv("APISERVERD_LOG_TREES")) log_trees = e[0] == '1';
     std::vector<struct epoll_event> evs(256);
     push_timer(mono() + bookmark_interval, 2, 0);
     while (!stopping.load()) {
