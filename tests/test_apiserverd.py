@@ -342,6 +342,45 @@ async def test_too_old_resource_version_is_gone_and_the_log_stays_bounded():
         nat.stop()
 
 
+async def test_the_log_replays_bytes_and_scope_only():
+    """The watch log keeps each event's bytes and its object's name, namespace and labels, not
+    the object: a resume replays the events as they were sent (a relabel still moves an object
+    between label scopes, a metadata.name field selector still filters), and a resume with a
+    field selector on any other field answers 410 so the client relists."""
+    nat = NativeAPIServer(T0)
+    srv = nat.srv
+    srv.request("POST", "/api/v1/namespaces", "", b'{"metadata":{"name":"bench"}}', "application/json")
+    st, raw = srv.request("GET", "/api/v1/namespaces/bench/configmaps")
+    rv0 = json.loads(raw)["metadata"]["resourceVersion"]
+    cm = "/api/v1/namespaces/bench/configmaps"
+    for i in range(3):
+        srv.request("POST", cm, "", json.dumps({"metadata": {"name": f"m{i}", "labels": {"a": "x"}},
+                                                "data": {"k": str(i)}}).encode(), "application/json")
+    srv.request("PATCH", f"{cm}/m1", "", b'{"metadata":{"labels":{"a":"y"}},"data":{"k":"changed"}}', MERGE)
+    srv.request("DELETE", f"{cm}/m2", "", b"{}", "application/json")
+    port = nat.start("127.0.0.1", 0)
+    try:
+        r, w = await _open_watch(port, cm, f"labelSelector=a%3Dx&resourceVersion={rv0}")
+        evs = await _read_events(r, 5)
+        assert [(e["type"], e["object"]["metadata"]["name"]) for e in evs] == [
+            ("ADDED", "m0"), ("ADDED", "m1"), ("ADDED", "m2"), ("DELETED", "m1"), ("DELETED", "m2")], evs
+        assert evs[3]["object"]["data"] == {"k": "changed"}  # the bytes of the event, as first sent
+        w.close()
+        r, w = await _open_watch(port, cm, f"fieldSelector=metadata.name%3Dm1&resourceVersion={rv0}")
+        evs = await _read_events(r, 2)
+        assert [(e["type"], e["object"]["metadata"]["name"]) for e in evs] == [("ADDED", "m1"), ("MODIFIED", "m1")]
+        w.close()
+        r, w = await asyncio.open_connection("127.0.0.1", port)
+        w.write(f"GET {cm}?watch=true&fieldSelector=data.k%3D1&resourceVersion={rv0} HTTP/1.1\r\nHost: x\r\n\r\n"
+                .encode())
+        await w.drain()
+        head = await asyncio.wait_for(r.readuntil(b"\r\n\r\n"), 5)
+        assert head.startswith(b"HTTP/1.1 410"), head
+        w.close()
+    finally:
+        nat.stop()
+
+
 def test_bench_controls_complete_and_lifecycle():
     """The /debug/fake controls the harness drives: a lifecycle stage reaches every unfinished
     job (their new resourceVersions returned), ``complete`` finishes them, stats count verbs."""
