@@ -135,8 +135,12 @@ def main() -> int:
         sst.sort_stats("cumulative").print_stats(a.top)
     if api_prof and os.path.exists(api_prof):
         buf.write("\n\n# ===== fake apiserver process, same timed steps =====\n")
-        ast = pstats.Stats(api_prof, stream=buf)
-        ast.sort_stats("tottime").print_stats(a.top)
+        try:
+            ast = pstats.Stats(api_prof, stream=buf)
+            ast.sort_stats("tottime").print_stats(a.top)
+        except ValueError:  # the native fake apiserver's sampler writes a text report
+            with open(api_prof) as fh:
+                buf.write(fh.read())
     with open(a.out, "w") as fh:
         fh.write(buf.getvalue())
     print(summarize(res))
