@@ -31,7 +31,10 @@ gloo barriers; there is no device work to ``torch.cuda.synchronize()``.
 ``processes: 1``); it runs in the same invocation on the same Crons, after the timed run
 (``--single-process none`` skips it).  ``operator_cpu_ms_per_fire`` and ``apiserver_busy_frac``
 (and their ``single_process_`` twins) say which side bounds each number: near 1.0 busy, the fake
-apiserver fixture does (the driver's round-5 record: 0.938 at 3 shards, 0.857 for one process).
+apiserver fixture does.  Since round 6 the fixture is native C++ (``--apiserver-impl native``,
+``ops/csrc/apiserverd.cpp``): at the round-6 head 0.87 busy at 3 shards (still partly the
+fixture's), 0.36 for one process (the operator's); the Python fixture of rounds 1-5 ran 0.94 and
+0.86 (``--apiserver-impl python``).
 
 ``deployment_*``: a real cluster is latency-bound, not CPU-bound: TLS on every connection and an
 etcd quorum write behind every mutation.  ``deployment_value`` / ``deployment_baseline_value`` are

@@ -55,6 +55,8 @@ def main() -> int:
     ap.add_argument("--window", type=int, default=20)
     ap.add_argument("--impl", default="native", choices=["native", "python"])
     ap.add_argument("--watch-window", type=int, default=20_000)
+    ap.add_argument("--lifecycle", default="instant", choices=["instant", "realistic"],
+                    help="the jobs' status sequence (the headline's, bench.py --lifecycle: instant)")
     ap.add_argument("--tolerance", type=float, default=0.05, help="allowed |window / first window - 1|")
     ap.add_argument("--out", default="")
     a = ap.parse_args()
@@ -132,7 +134,7 @@ def main() -> int:
     harness._cpu_times = cpu
     try:
         res = harness.run_sync(harness.BenchConfig(n_crons=a.crons, steps=a.steps, warmup=a.warmup,
-                                                   shards=a.shards, apiserver_impl=a.impl,
+                                                   shards=a.shards, apiserver_impl=a.impl, lifecycle=a.lifecycle,
                                                    watch_window=a.watch_window), on_step=progress)
     finally:
         harness._cpu_times = orig
@@ -142,7 +144,7 @@ def main() -> int:
     api_w = [sum(w) * 1e6 / n for w in windows(res.step_cpu_apiserver_s, a.window)]
     rel = [round(x / step_w[0] - 1, 4) for x in step_w]
     out = {"config": {"crons": a.crons, "steps": a.steps, "warmup": a.warmup, "shards": a.shards,
-                      "impl": a.impl, "watch_window": a.watch_window, "window": a.window},
+                      "impl": a.impl, "watch_window": a.watch_window, "window": a.window, "lifecycle": a.lifecycle},
            "value": round(res.cron_reconciles_per_s, 1),
            "ms_per_step_by_window": [round(x, 1) for x in step_w],
            "step_vs_first_window": rel,
