@@ -88,7 +88,10 @@ def build():
         def __init__(self):
             self.requests = 0
 
-        async def create(self, target, obj, namespace=None, dry_run=False, decoder=None):
+        def gate_saturated(self) -> bool:  # no in-flight cap: a reconcile may release its slot
+            return False
+
+        async def create(self, target, obj, namespace=None, dry_run=False, decoder=None, priority=None):
             self.requests += 1
             m = obj["metadata"]
             state["uid"] += 1
@@ -129,6 +132,7 @@ def build():
         status = rec.own_writes.get(key, (None, None))[1]
         cur = cron_inf.store.get(key) or cron
         obj = dict(cur)
+        obj["spec"] = cron["spec"]  # the cache holds the template as its raw JSON text; the wire has JSON
         obj["metadata"] = dict(cur["metadata"], resourceVersion=next_rv())
         if status is not None:
             obj["status"] = status
