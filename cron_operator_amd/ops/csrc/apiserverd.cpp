@@ -776,7 +776,7 @@ struct Event {
   long long rv;
   int type;  // 0 ADDED 1 MODIFIED 2 DELETED
   Ref scope, old_scope;                      // {"metadata": {name, namespace, labels}}
-  std::shared_ptr<const std::string> bytes;  // the object as encoded in the event
+  jdom::jstr bytes;  // the object as encoded in the event (pool-allocated: the log turns over FIFO)
   Ref held, held_old;  // APISERVERD_LOG_TREES=1 only: the trees too, as rounds 1-5 kept them (A/B arm)
 };
 
@@ -1249,7 +1249,7 @@ struct Impl {
     const jdom::jstr& enc = jdom::encoded(obj.get());
     const bool with_old = type == 1 && old;
     st->log.push_back(Event{at, type, scope_of(obj.get()), with_old ? scope_of(old.get()) : Ref(),
-                            std::make_shared<const std::string>(enc.data(), enc.size()),
+                            jdom::jstr(enc.data(), enc.size()),
                             log_trees ? obj : Ref(), log_trees ? old : Ref()});
     while (st->log.size() > watch_window) {
       st->floor = st->log.front().rv;
@@ -2145,7 +2145,7 @@ struct Impl {
         if (ev.rv > since) {
           const bool now_in = w->in_scope(ev.scope.get());
           const bool was_in = ev.type == 1 && ev.old_scope ? w->in_scope(ev.old_scope.get()) : false;
-          offer(w.get(), ev.type, std::string_view(*ev.bytes), static_cast<bool>(ev.old_scope), now_in, was_in);
+          offer(w.get(), ev.type, std::string_view(ev.bytes), static_cast<bool>(ev.old_scope), now_in, was_in);
         }
     }
     Watcher* out = w.release();
