@@ -206,8 +206,15 @@ async def run(fires: int, profile: str) -> None:
     c0 = time.process_time()
     if prof:
         prof.enable()
+    chunk_cpu = []  # CPU per fire over each tenth of the run: whether a long run slows down
+    c_chunk = c0
+    step = max(1, fires // 10)
     for k in range(200, 200 + fires):
         await one_fire(k)
+        if (k - 199) % step == 0:
+            now = time.process_time()
+            chunk_cpu.append(round((now - c_chunk) * 1e6 / step, 1))
+            c_chunk = now
     if prof:
         prof.disable()
     cpu = time.process_time() - c0
@@ -217,6 +224,7 @@ async def run(fires: int, profile: str) -> None:
     print("  completion reconcile {:.1f} us, fire reconcile {:.1f} us (incl. its CREATE's ADDED event), "
           "status-echo events {:.1f} us per fire".format(*(spent[k] * 1e6 / fires for k in
                                                           ("completion", "fire", "echo"))), flush=True)
+    print(f"  us per fire by tenth of the run: {chunk_cpu}", flush=True)
     if prof:
         buf = io.StringIO()
         pstats.Stats(prof, stream=buf).sort_stats("tottime").print_stats(40)
