@@ -14,8 +14,10 @@
 // Threads: the server thread owns everything.  Python entry points release the GIL, then take
 // the server's (recursive) lock; the server thread takes the GIL only to call the fallback, and
 // never while another thread could hold the lock and wait for the GIL (they released it).
-// APISERVERD_STANDALONE builds the server without CPython (no fallback, no module): the
-// sanitizer and profiling drivers (scripts/sanitize.py) link it into a plain C++ program.
+// APISERVERD_STANDALONE compiles the server without CPython (no fallback, no module), for a
+// C++-only harness (a gprof build); the tree builds the module.  The sanitizer run
+// (scripts/sanitize.py) builds the module with ASan/UBSan and drives it from Python; the
+// in-process stack sampler (profile_start/profile_stop) is what the boxes use.
 #ifndef APISERVERD_STANDALONE
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
