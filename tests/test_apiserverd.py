@@ -381,6 +381,40 @@ async def test_the_log_replays_bytes_and_scope_only():
         nat.stop()
 
 
+async def test_tls_requests_and_a_watch(tmp_path):
+    """The deployment-shaped arm's transport: HTTPS on the server's own OpenSSL context, a
+    request and a watch over it, verified against the self-signed CA (CN=localhost)."""
+    import ssl
+
+    from cron_operator_amd.runtime.servers import self_signed_cert
+
+    cert, key = self_signed_cert(str(tmp_path), host="localhost")
+    nat = NativeAPIServer(T0)
+    port = nat.start("127.0.0.1", 0, cert, key)
+    ctx = ssl.create_default_context(cafile=cert)
+    try:
+        r, w = await asyncio.open_connection("127.0.0.1", port, ssl=ctx, server_hostname="localhost")
+        body = b'{"metadata":{"name":"bench"}}'
+        w.write(b"POST /api/v1/namespaces HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\n"
+                b"Content-Length: %d\r\n\r\n" % len(body) + body)
+        await w.drain()
+        head = await asyncio.wait_for(r.readuntil(b"\r\n\r\n"), 5)
+        assert head.startswith(b"HTTP/1.1 201"), head
+        n = int([ln for ln in head.split(b"\r\n") if ln.lower().startswith(b"content-length")][0].split(b":")[1])
+        assert json.loads(await r.readexactly(n))["metadata"]["name"] == "bench"
+        w.write(b"GET /api/v1/namespaces/bench/configmaps?watch=true&resourceVersion=0 HTTP/1.1\r\nHost: x\r\n\r\n")
+        await w.drain()
+        head = await asyncio.wait_for(r.readuntil(b"\r\n\r\n"), 5)
+        assert head.startswith(b"HTTP/1.1 200") and b"chunked" in head.lower(), head
+        nat.srv.request("POST", "/api/v1/namespaces/bench/configmaps", "", b'{"metadata":{"name":"m"}}',
+                        "application/json")
+        evs = await _read_events(r, 1)
+        assert evs[0]["type"] == "ADDED" and evs[0]["object"]["metadata"]["name"] == "m"
+        w.close()
+    finally:
+        nat.stop()
+
+
 def test_bench_controls_complete_and_lifecycle():
     """The /debug/fake controls the harness drives: a lifecycle stage reaches every unfinished
     job (their new resourceVersions returned), ``complete`` finishes them, stats count verbs."""
