@@ -545,6 +545,7 @@ struct Selector {
 
 struct Schema {
   std::string type;
+  enum class Kind : uint8_t { Any, Object, Array, String, Integer, Number, Boolean } kind = Kind::Any;  // of `type`
   bool nullable = false, preserve = false, date_time = false;
   bool has_enum = false;
   jdom::RefVec enumv;
@@ -571,6 +572,13 @@ struct Schema {
     if (!s || !s->is_obj()) return out;
     out->any = false;
     out->type = s->str("type");
+    out->kind = out->type == "object"    ? Kind::Object
+                : out->type == "array"   ? Kind::Array
+                : out->type == "string"  ? Kind::String
+                : out->type == "integer" ? Kind::Integer
+                : out->type == "number"  ? Kind::Number
+                : out->type == "boolean" ? Kind::Boolean
+                                         : Kind::Any;
     if (const Node* v = s->getn("nullable")) out->nullable = v->t == T::True;
     if (const Node* v = s->getn("x-kubernetes-preserve-unknown-fields")) out->preserve = v->t == T::True;
     out->date_time = s->str("format") == "date-time";
@@ -616,14 +624,15 @@ struct Schema {
   }
 
   bool type_ok(const Node* v) const {
-    if (type.empty()) return true;
-    if (type == "object") return v->t == T::Obj;
-    if (type == "array") return v->t == T::Arr;
-    if (type == "string") return v->t == T::Str;
-    if (type == "integer") return v->t == T::Num && num_is_integral(v);
-    if (type == "number") return v->t == T::Num;
-    if (type == "boolean") return v->t == T::True || v->t == T::False;
-    return true;
+    switch (kind) {
+      case Kind::Object: return v->t == T::Obj;
+      case Kind::Array: return v->t == T::Arr;
+      case Kind::String: return v->t == T::Str;
+      case Kind::Integer: return v->t == T::Num && num_is_integral(v);
+      case Kind::Number: return v->t == T::Num;
+      case Kind::Boolean: return v->t == T::True || v->t == T::False;
+      default: return true;  // no type, or one admission does not check
+    }
   }
 
   // One pass: prune unknown fields, fill defaults (only on nodes not yet admitted: fresh,
