@@ -3539,6 +3539,10 @@ PyObject* Server_profile_start(Server* self, PyObject* args) {
   sigemptyset(&sa.sa_mask);
   sigaction(SIGPROF, &sa, nullptr);
   prof::on.store(true);
+  if (prof::has_timer) {  // started again without a stop: the old timer goes first
+    timer_delete(prof::timer);
+    prof::has_timer = false;
+  }
   const pid_t tid = self->impl->running ? self->impl->loop_tid.load() : 0;
   if (tid > 0) {
     struct sigevent sev;
