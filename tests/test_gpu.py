@@ -60,6 +60,11 @@ def test_native_components_loaded():
     assert jsonutil.NATIVE
     assert fasthttp._codec is not None and srvhttp._codec is not None
     assert os.path.realpath(fasthttp._codec.__file__).startswith(os.path.realpath(ROOT))
+    # the benchmark's fake apiserver: the in-tree C++ server, not the Python one
+    from cron_operator_amd.apiserver.native import load
+
+    mod = load()
+    assert mod is not None and os.path.realpath(mod.__file__).startswith(os.path.realpath(ROOT))
 
 
 def test_train_smoke_payload_on_gpu(gpu):
@@ -137,6 +142,7 @@ def test_headline_bench_short_run():
     assert out.returncode == 0, out.stdout[-2000:] + out.stderr[-2000:]
     res = json.loads(out.stdout.strip().splitlines()[-1])
     assert res["value"] > 0 and res["cron_engine"] == "native"
+    assert res["config"]["apiserver_impl"] == "native"  # served by the in-tree _apiserverd
     assert res["baseline_source"].startswith("measured") and res["vs_baseline"] > 1
     # the untimed payload probe ran the scheduled DDP payload over RCCL on this box's GPU
     probe = res["payload_ddp"]
