@@ -385,3 +385,30 @@ def test_watch_lag_is_a_debug_control_of_the_http_fake_apiserver():
     if load() is not None:
         nat = NativeAPIServer()
         assert nat.fallback("POST", "/debug/fake/faults", "", {}, body)[0] == 501
+
+
+@pytest.mark.parametrize("policy", ["Forbid", "Replace", "Allow"])
+async def test_a_lost_create_response_runs_an_every_tick_once(policy):
+    """An ``@every`` job is named ``Next(now)`` at its CREATE, not ``Next(tick)``: after a lost
+    CREATE response the retry must still recognise the job it created (found by the widened mode
+    differential).  The tick is recorded, the job is active, and nothing is created twice."""
+    from cron_operator_amd.api.v1alpha1 import CRON_GVR, new_cron
+    from cron_operator_amd.controller.reconciler import ReconcilerOptions
+
+    env = TestEnv()
+    await env.create_cron(new_cron("ev", NS, "@every 90s", TMPL, concurrency_policy=policy, history_limit=2))
+    await env.start_manager(ReconcilerOptions())
+    await env.settle()
+    env.server.faults.add(verb="create", resource="pytorchjobs", code=504, reason="Timeout", after=True, times=1)
+    try:
+        env.clock.advance(100)
+        await env.settle()
+        env.clock.advance(1)  # the retry's backoff
+        await env.settle()
+        jobs = list(env.server.objects(PT, NS))
+        st = env.server.get(CRON_GVR, NS, "ev").get("status") or {}
+        assert len(jobs) == 1, [j["metadata"]["name"] for j in jobs]
+        assert st.get("lastScheduleTime"), st
+        assert [a["name"] for a in st.get("active") or []] == [jobs[0]["metadata"]["name"]], st
+    finally:
+        await env.stop()
