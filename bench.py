@@ -485,6 +485,8 @@ def main() -> int:
             # fake apiserver's speed; and how busy that fixture was (CPU s / wall s, max rank)
             "operator_cpu_ms_per_fire": round(sum(r["cpu_op"] for r in allr) * 1000 / fires, 4),
             "apiserver_busy_frac": round(max(r["cpu_api"] / r["elapsed_s"] for r in allr), 3),
+            # the fixture's own CPU per fire (all ranks' fake apiservers): its speed, apart from the load
+            "apiserver_cpu_us_per_fire": round(sum(r["cpu_api"] for r in allr) * 1e6 / fires, 1),
             # peak resident memory (VmHWM) of the largest operator shard process (0: the operator
             # ran in the bench process itself)
             "operator_shard_peak_rss_mib": round(max(r.get("shard_rss", 0.0) for r in allr), 1),
