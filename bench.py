@@ -36,6 +36,13 @@ apiserver fixture does.  Since round 6 the fixture is native C++ (``--apiserver-
 fixture's), 0.36 for one process (the operator's); the Python fixture of rounds 1-5 ran 0.94 and
 0.86 (``--apiserver-impl python``).
 
+``partitioned_*``: the headline's shards again, each against a fake apiserver process of its own
+that holds the Crons hashing to that shard and their jobs -- a partitioned cluster, as if the
+apiserver had a core per shard.  Run in this invocation after the timed run (``--partitioned
+none`` skips it; it needs two CPUs per shard per rank).  With no single-threaded fixture in the
+way it is the operator's sharded throughput; ``partitioned_apiserver_busy_frac`` is the busiest
+partition's CPU s per wall s.
+
 ``deployment_*``: a real cluster is latency-bound, not CPU-bound: TLS on every connection and an
 etcd quorum write behind every mutation.  ``deployment_value`` / ``deployment_baseline_value`` are
 both algorithms in that shape (one process each, TLS + the harness's ``etcd`` latency model, whose
@@ -288,6 +295,11 @@ def main() -> int:
                          "processes=1) -- on the same 1000 Crons in this invocation, outside the headline's timed "
                          "region, and report it as single_process_*: operator-bound, so it measures the product "
                          "rather than the fake apiserver")
+    ap.add_argument("--partitioned", choices=["measure", "none"], default="measure",
+                    help="also run the headline's shards against a partitioned fake cluster -- one apiserver "
+                         "process per shard holding that shard's Crons and jobs -- outside the headline's timed "
+                         "region: partitioned_* keys, the operator's sharded throughput with no single-threaded "
+                         "fixture in its way (needs 2 CPUs per shard per rank; skipped otherwise)")
     ap.add_argument("--single-steps", type=int, default=10)
     ap.add_argument("--single-warmup", type=int, default=3)
     ap.add_argument("--deployment", choices=["measure", "none"], default="measure",
@@ -358,6 +370,27 @@ def main() -> int:
             "p99": res.p99_latency_ms, "req_per_fire": res.api_requests_per_fire,
             "cpu_op": res.cpu_s_operator, "cpu_api": res.cpu_s_apiserver,
             "shard_rss": max(res.operator_maxrss_mib or [0.0]), "shard_end_rss": max(res.operator_rss_mib or [0.0])}
+
+    # the same shards, each against its own fake apiserver partition (untimed for the headline)
+    from cron_operator_amd.runtime.supervisor import available_cpus
+
+    if (a.partitioned == "measure" and a.transport == "http" and cfg.shards > 1 and a.shard_routing == "labels"
+            and available_cpus() // world >= 2 * cfg.shards):
+        pcfg = BenchConfig(n_crons=a.crons, steps=a.steps, warmup=a.warmup, history_limit=a.history_limit,
+                           mode=a.mode, transport="http", qps=a.qps, burst=a.burst, workers=a.workers,
+                           namespace=f"bench-part-r{rank}", shards=cfg.shards, apiserver_partitions=cfg.shards,
+                           shard_routing="labels", apiserver_latency=a.apiserver_latency, tls=a.tls,
+                           max_inflight=a.max_inflight, defer_writes=not a.no_defer, lifecycle=a.lifecycle,
+                           apiserver_impl=a.apiserver_impl)
+        _barrier(dist)
+        pres = run_sync(pcfg)
+        _barrier(dist)
+        _progress(rank, f"partitioned fixture done: {pcfg.n_crons * pcfg.steps / pres.elapsed_s:.1f}")
+        mine["part_elapsed_s"] = pres.elapsed_s
+        mine["part_fires"] = pcfg.n_crons * pcfg.steps
+        mine["part_p50"] = pres.p50_latency_ms
+        mine["part_cpu_op"] = pres.cpu_s_operator
+        mine["part_cpu_api_max"] = max(pres.cpu_s_apiserver_parts)
 
     # the shipped default: one operator process (untimed for the headline, like the baseline)
     if a.single_process == "measure" and a.transport == "http":
@@ -503,6 +536,19 @@ def main() -> int:
             "cron_engine": res.engine,
             "wall_s": round(wall, 2),
         }
+        if all("part_fires" in r for r in allr):
+            part_fires = sum(r["part_fires"] for r in allr)
+            out.update({
+                # the headline's shards, each against its own fake apiserver partition: what the
+                # operator's shards do when no one fixture process bounds them
+                "partitioned_value": round(part_fires / max(r["part_elapsed_s"] for r in allr), 2),
+                "partitioned_p50_ms": round(max(r["part_p50"] for r in allr), 2),
+                "partitioned_operator_cpu_ms_per_fire": round(sum(r["part_cpu_op"] for r in allr) * 1000
+                                                              / part_fires, 4),
+                # the busiest partition of any rank (CPU s / wall s)
+                "partitioned_apiserver_busy_frac": round(max(r["part_cpu_api_max"] / r["part_elapsed_s"]
+                                                             for r in allr), 3),
+            })
         if "sp_fires" in allr[0]:
             sp_fires = sum(r["sp_fires"] for r in allr)
             out.update({

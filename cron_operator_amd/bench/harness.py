@@ -120,6 +120,10 @@ class BenchConfig:
     # the fake apiserver process: "native" (apiserver/native.py, the C++ _apiserverd: the fixture
     # off the critical path) or "python" (apiserver/server.py + http.py; the A/B arm)
     apiserver_impl: str = "native"
+    # fake apiserver processes: 1 (every shard against one server), or `shards` with label
+    # routing -- a partitioned cluster, server i holding the Crons that hash to shard i (shard_of)
+    # and their jobs, so no one single-threaded fixture bounds the shards (bench.py partitioned_*)
+    apiserver_partitions: int = 1
     # events per resource the fake apiserver keeps for watch resume (a bounded watch cache: the
     # soak's fixture memory stays flat; 20,000 is ~5 ticks of 1000 Crons' job events)
     watch_window: int = 20_000
@@ -199,6 +203,8 @@ class BenchResult:
     # (the harness's own lifecycle writes taken out) -- the soak's per-window split
     step_cpu_operator_s: List[float] = field(default_factory=list)
     step_cpu_apiserver_s: List[float] = field(default_factory=list)
+    # apiserver_partitions > 1: each fake apiserver's CPU s over the timed steps (writes taken out)
+    cpu_s_apiserver_parts: List[float] = field(default_factory=list)
 
     def to_dict(self) -> Dict[str, Any]:
         return asdict(self)
@@ -401,18 +407,26 @@ def completed_pred(want_hist: int):
     return pred
 
 
-def _cpu_times(remote: Optional["_RemoteServer"]) -> "tuple[float, float]":
-    """(operator process CPU s, apiserver process CPU s) -- the apiserver shares our process in memory mode."""
+def _proc_cpu(remote: "_RemoteServer") -> float:
+    """CPU s (user + system) of a fake apiserver process so far."""
+    if remote.proc is None:
+        return 0.0
+    try:
+        with open(f"/proc/{remote.proc.pid}/stat") as fh:
+            f = fh.read().rsplit(")", 1)[1].split()
+        return (int(f[11]) + int(f[12])) / os.sysconf("SC_CLK_TCK")
+    except (OSError, IndexError, ValueError):
+        return float("nan")
+
+
+def _cpu_times(remote) -> "tuple[float, float]":
+    """(operator process CPU s, apiserver CPU s) -- the apiserver shares our process in memory
+    mode; ``remote`` may be a list of partitions (their CPU summed)."""
     me = time.process_time()
-    other = 0.0
-    if remote is not None and remote.proc is not None:
-        try:
-            with open(f"/proc/{remote.proc.pid}/stat") as fh:
-                f = fh.read().rsplit(")", 1)[1].split()
-            other = (int(f[11]) + int(f[12])) / os.sysconf("SC_CLK_TCK")
-        except (OSError, IndexError, ValueError):
-            other = float("nan")
-    return me, other
+    if remote is None:
+        return me, 0.0
+    parts = remote if isinstance(remote, list) else [remote]
+    return me, sum(_proc_cpu(r) for r in parts)
 
 
 async def run(cfg: BenchConfig, on_step=None) -> BenchResult:
@@ -443,8 +457,14 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
 
     clock = FakeClock(T0_NS)
     remote: Optional[_RemoteServer] = None
+    remotes: List[_RemoteServer] = []
+    ssl_of: Dict[str, Any] = {}
+    transports: List[Any] = []
     server = None
     admin = None
+    parts = max(1, cfg.apiserver_partitions)
+    if parts > 1 and (cfg.transport != "http" or parts != cfg.shards or cfg.shard_routing != "labels"):
+        raise ValueError("apiserver_partitions > 1 needs transport='http', label routing and one partition per shard")
     if cfg.transport == "memory":
         from ..api.v1alpha1.crd import crd
         from ..apiserver.server import APIServer
@@ -460,17 +480,30 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
 
         from ..runtime.http import HttpTransport
 
-        remote = _RemoteServer(tls=cfg.tls, impl=cfg.apiserver_impl, watch_window=cfg.watch_window)
-        remote.start()
-        transport = HttpTransport(remote.rest_config(), pool_size=max(16, cfg.workers * 2, cfg.max_inflight))
-        sslctx = remote.ssl_context()
+        for _ in range(parts):
+            remotes.append(_RemoteServer(tls=cfg.tls, impl=cfg.apiserver_impl, watch_window=cfg.watch_window))
+            remotes[-1].start()
+            transports.append(HttpTransport(remotes[-1].rest_config(),
+                                            pool_size=max(16, cfg.workers * 2, cfg.max_inflight)))
+        remote, transport = remotes[0], transports[0]
+        ssl_of = {r.url: r.ssl_context() for r in remotes}
+        sslctx = ssl_of[remote.url]
         admin = aiohttp.ClientSession(connector=aiohttp.TCPConnector(ssl=sslctx) if sslctx else None)
+
+    async def admin_post(path: str, payload: Dict[str, Any]) -> List[Any]:
+        """POST a /debug/fake control to every fake apiserver (partition); their JSON answers."""
+        async def one(r: _RemoteServer) -> Any:
+            # each partition has its own self-signed CA under TLS
+            kw = {"ssl": ssl_of[r.url]} if ssl_of.get(r.url) is not None else {}
+            async with admin.post(r.url + path, json=payload, **kw) as resp:
+                body = await resp.read()
+                return json.loads(body) if body else None
+        return list(await asyncio.gather(*(one(r) for r in remotes)))
 
     async def set_time(ns: int) -> None:
         clock.set(ns)
         if admin is not None:
-            async with admin.post(remote.url + "/debug/fake/clock", json={"nowNs": ns}) as r:
-                await r.read()
+            await admin_post("/debug/fake/clock", {"nowNs": ns})
 
     def _ts(ns: int) -> str:
         from ..utils.gotime import UTC, GoTime
@@ -493,10 +526,11 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
                                    {"status": lifecycle_status(obj, stage, start, end)}, "merge", "status")
                 rvs[f"{cfg.namespace}/{m['name']}"] = out["metadata"]["resourceVersion"]
             return rvs
-        async with admin.post(remote.url + "/debug/fake/lifecycle",
-                              json={"namespace": cfg.namespace, "stage": stage, "start": start,
-                                    "end": end}) as r:
-            return (await r.json())["resourceVersions"]
+        rvs = {}
+        for ans in await admin_post("/debug/fake/lifecycle",
+                                    {"namespace": cfg.namespace, "stage": stage, "start": start, "end": end}):
+            rvs.update(ans["resourceVersions"])
+        return rvs
 
     async def complete_jobs(tick_ns: int) -> None:
         ts = _ts(tick_ns)
@@ -513,20 +547,29 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
                     server.patch(PYTORCHJOBS, cfg.namespace, m["name"],
                                  {"status": finished_status("PyTorchJob", m["name"], ts, True)}, "merge", "status")
         else:
-            async with admin.post(remote.url + "/debug/fake/complete",
-                                  json={"namespace": cfg.namespace, "time": ts}) as r:
-                await r.read()
+            await admin_post("/debug/fake/complete", {"namespace": cfg.namespace, "time": ts})
 
 
     try:
         # ---------------------------------------------------------------- setup (untimed)
-        setup_client = Client(transport, qps=-1)
-        try:
-            await setup_client.create(GroupVersionResource("", "v1", "namespaces"),
-                                      {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": cfg.namespace}},
-                                      "")
-        except Exception:
-            pass
+        # one setup client per fake apiserver: a Cron (and its jobs) goes to the partition of the
+        # shard it hashes to
+        setup_clients = [Client(t, qps=-1) for t in (transports or [transport])]
+        setup_client = setup_clients[0]
+
+        def part_of(name: str) -> int:
+            if parts == 1:
+                return 0
+            from ..runtime.controller import shard_of
+
+            return shard_of(cfg.namespace, name, parts)
+
+        for sc in setup_clients:
+            try:
+                await sc.create(GroupVersionResource("", "v1", "namespaces"),
+                                {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": cfg.namespace}}, "")
+            except Exception:
+                pass
         tmpl = pytorchjob_template()
         crons = []
         for i in range(cfg.n_crons):
@@ -535,7 +578,7 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
                 for rs in t["spec"]["pytorchReplicaSpecs"].values():
                     rs["template"]["spec"]["containers"][0]["command"] = ["python", "-c", f"print('tick {i}')"]
             c = new_cron(f"cron-{i:05d}", cfg.namespace, "* * * * *", t, history_limit=cfg.history_limit)
-            crons.append(await setup_client.create(CRON_GVR, c.to_dict(), cfg.namespace))
+            crons.append(await setup_clients[part_of(c.name)].create(CRON_GVR, c.to_dict(), cfg.namespace))
         # Seed each Cron with a full history (historyLimit finished jobs from the past hour) so
         # every timed tick exercises history GC, as in a long-running deployment.
         if cfg.seed_history:
@@ -554,26 +597,25 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
                     job["metadata"] = {"name": name, "namespace": cfg.namespace,
                                        "labels": {"app": "bench", LABEL_CRON_NAME: cobj["metadata"]["name"]},
                                        "ownerReferences": [new_controller_ref(cobj, CRON_GVK)]}
-                    await setup_client.create(PYTORCHJOBS, job, cfg.namespace)
-                    await setup_client.patch(PYTORCHJOBS, cfg.namespace, name,
-                                             {"status": finished_status("PyTorchJob", name, ts, True)}, "merge",
-                                             "status")
+                    sc = setup_clients[part_of(cobj["metadata"]["name"])]
+                    await sc.create(PYTORCHJOBS, job, cfg.namespace)
+                    await sc.patch(PYTORCHJOBS, cfg.namespace, name,
+                                   {"status": finished_status("PyTorchJob", name, ts, True)}, "merge", "status")
         await set_time(T0_NS + NANOS // 2)
         if admin is not None:  # the apiserver process holds the seeded store for the whole run
-            async with admin.post(remote.url + "/debug/fake/gc", json={}) as r:
-                await r.read()
+            await admin_post("/debug/fake/gc", {})
         latency = LATENCY_PROFILES[cfg.apiserver_latency]
         if latency:
             if admin is None:
                 raise ValueError("apiserver_latency needs transport='http'")
-            async with admin.post(remote.url + "/debug/fake/faults", json={"latency": latency}) as r:
-                await r.read()
+            await admin_post("/debug/fake/faults", {"latency": latency})
 
         if cfg.shards > 1 or cfg.operator_process:
             if remote is None:
                 raise ValueError("shards > 1 / operator_process need transport='http'")
-            await setup_client.close()
-            return await _run_sharded(cfg, remote, admin, set_time, complete_jobs, on_step, job_stage)
+            for sc in setup_clients:
+                await sc.close()
+            return await _run_sharded(cfg, remotes, admin, set_time, complete_jobs, on_step, job_stage)
 
         client = Client(transport, qps=cfg.qps, burst=cfg.burst, max_inflight=cfg.max_inflight,
                         low_reserve=cfg.tick_reserve)
@@ -808,8 +850,8 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
     finally:
         if admin is not None:
             await admin.close()
-        if remote is not None:
-            remote.stop()
+        for r in remotes:
+            r.stop()
 
 
 class _Shard:
@@ -832,9 +874,10 @@ class _Shard:
         return json.loads(line)
 
 
-async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_time, complete_jobs,
+async def _run_sharded(cfg: BenchConfig, remotes: List["_RemoteServer"], admin, set_time, complete_jobs,
                        on_step, job_stage=None) -> BenchResult:
-    """The step loop of :func:`run` with the operator split over ``cfg.shards`` processes."""
+    """The step loop of :func:`run` with the operator split over ``cfg.shards`` processes (shard
+    i against ``remotes[i % len(remotes)]``: one fake apiserver, or one partition per shard)."""
     from ..cron.engine import default_engine
     from ..utils import jsonutil
 
@@ -846,6 +889,7 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
     shards: List[_Shard] = []
     try:
         for i in range(cfg.shards):
+            remote = remotes[i % len(remotes)]
             p = await asyncio.create_subprocess_exec(
                 sys.executable, "-m", "cron_operator_amd.bench.shard_worker", "--url", remote.url,
                 "--namespace", cfg.namespace, "--shard-index", str(i), "--shard-count", str(cfg.shards),
@@ -859,6 +903,9 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
                 env=env, stdin=asyncio.subprocess.PIPE, stdout=asyncio.subprocess.PIPE,
                 stderr=asyncio.subprocess.PIPE, limit=1 << 24)
             shards.append(_Shard(p))
+        remote = remotes[0]
+        # what _cpu_times reads: the one server (scripts wrap _cpu_times and read its url), or the list
+        cpu_of = remotes[0] if len(remotes) == 1 else remotes
         ready = await asyncio.gather(*(s.recv(300) for s in shards))
         assert sum(r["owned"] for r in ready) == cfg.n_crons, ready
 
@@ -883,6 +930,8 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
         step_cpu_op: List[float] = []
         step_cpu_api: List[float] = []
         prev_op_cpu = 0.0
+        parts0 = [0.0] * len(remotes)
+        parts_write = [0.0] * len(remotes)
         for k in range(1, total + 1):
             tick_ns = T0_NS + k * 60 * NANOS
             if k == cfg.warmup + 1:
@@ -892,21 +941,24 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
                 if cfg.apiserver_profile:
                     async with admin.post(remote.url + "/debug/fake/profile", json={"action": "start"}) as r:
                         await r.read()
-                api0 = _cpu_times(remote)[1]
+                api0 = _cpu_times(cpu_of)[1]
+                parts0 = [_proc_cpu(r) for r in remotes]
                 t_start = time.perf_counter()
             t0 = time.perf_counter()
             writes = 0.0
-            step_api0 = _cpu_times(remote)[1]
+            step_api0 = _cpu_times(cpu_of)[1]
             step_write_cpu = 0.0
             if k > 1:
                 for st in range(n_pre):  # the previous tick's jobs start (realistic lifecycle)
                     w0 = time.perf_counter()
-                    c0 = _cpu_times(remote)[1]
+                    c0 = [_proc_cpu(r) for r in remotes]
                     rvs = await job_stage(st, tick_ns - 59 * NANOS, tick_ns - 30 * NANOS)
                     writes += time.perf_counter() - w0  # the harness's write call: not timed
                     if k > cfg.warmup:
-                        step_write_cpu += _cpu_times(remote)[1] - c0
-                        write_cpu += _cpu_times(remote)[1] - c0
+                        dw = [_proc_cpu(r) - c for r, c in zip(remotes, c0)]
+                        step_write_cpu += sum(dw)
+                        write_cpu += sum(dw)
+                        parts_write = [a + b for a, b in zip(parts_write, dw)]
                     await asyncio.gather(*(s.send({"cmd": "absorb", "rvs": rvs}) for s in shards))
                     await asyncio.gather(*(s.recv(cfg.step_timeout) for s in shards))
                 await complete_jobs(tick_ns - 30 * NANOS)
@@ -922,7 +974,7 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
                 step_ms.append((t2 - t0 - writes) * 1000)
                 op_cpu = sum(r["cpu"] for r in last)
                 step_cpu_op.append(op_cpu - prev_op_cpu)
-                step_cpu_api.append(_cpu_times(remote)[1] - step_api0 - step_write_cpu)
+                step_cpu_api.append(_cpu_times(cpu_of)[1] - step_api0 - step_write_cpu)
                 phase_ms["completion"].append((t1 - t0 - writes) * 1000)
                 phase_ms["fire"].append((t2 - t1) * 1000)
                 if n_pre:
@@ -934,7 +986,8 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
             if on_step is not None:
                 on_step(k, t2 - t0 - writes, k > cfg.warmup)
         elapsed = time.perf_counter() - t_start - excluded
-        api1 = _cpu_times(remote)[1]
+        api1 = _cpu_times(cpu_of)[1]
+        parts1 = [_proc_cpu(r) for r in remotes]
         if cfg.shard_profile:
             await asyncio.gather(*(s.send({"cmd": "profile", "action": "stop",
                                            "path": os.path.abspath(f"{cfg.shard_profile}.{i}.pstats")})
@@ -964,6 +1017,8 @@ async def _run_sharded(cfg: BenchConfig, remote: "_RemoteServer", admin, set_tim
             cpu_s_operator=sum(r["cpu"] - b["cpu"] for r, b in zip(last, base)),
             cpu_s_apiserver=api1 - api0 - write_cpu,
             step_cpu_operator_s=step_cpu_op, step_cpu_apiserver_s=step_cpu_api,
+            cpu_s_apiserver_parts=[b - a - w for a, b, w in zip(parts0, parts1, parts_write)]
+            if len(remotes) > 1 else [],
             operator_maxrss_mib=[round(r.get("maxrss_mib", 0.0), 1) for r in last],
             operator_ready_maxrss_mib=[round(r.get("maxrss_mib", 0.0), 1) for r in ready],
             operator_rss_mib=[round(r.get("rss_mib", 0.0), 1) for r in last],

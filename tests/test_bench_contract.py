@@ -54,6 +54,9 @@ def test_single_rank_line():
     assert d["single_process_value"] > 0 and d["single_process_p50_ms"] > 0
     assert d["single_process_p99_ms"] >= d["single_process_p50_ms"]
     assert d["single_process_operator_cpu_ms_per_fire"] > 0 and 0 < d["single_process_apiserver_busy_frac"] < 2
+    # the same shards, each against a fake apiserver process of its own (a partitioned cluster)
+    assert d["partitioned_value"] > 0 and d["partitioned_p50_ms"] > 0
+    assert d["partitioned_operator_cpu_ms_per_fire"] > 0 and 0 < d["partitioned_apiserver_busy_frac"] < 2
     # the deployment-shaped pair (TLS + etcd latency, one process, both algorithms), same invocation
     assert d["deployment_config"]["tls"] is True and d["deployment_config"]["apiserver_latency"] == "etcd"
     assert d["deployment_value"] > 0 and d["deployment_baseline_value"] > 0
@@ -82,6 +85,7 @@ def test_tls_apiserver_option():
     assert r.returncode == 0, r.stderr[-2000:]
     d = _json_line(r.stdout)
     assert d["config"]["tls"] is True and d["value"] > 0 and d["single_process_value"] > 0
+    assert d["partitioned_value"] > 0  # each partition with its own CA
     assert d["api_requests_per_fire"] == 4.0
 
 
