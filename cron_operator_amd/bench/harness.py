@@ -205,6 +205,9 @@ class BenchResult:
     step_cpu_apiserver_s: List[float] = field(default_factory=list)
     # apiserver_partitions > 1: each fake apiserver's CPU s over the timed steps (writes taken out)
     cpu_s_apiserver_parts: List[float] = field(default_factory=list)
+    # sharded runs: the shard processes' context switches over the timed steps, summed
+    # [voluntary (waits for I/O), involuntary (preempted)]
+    operator_ctx_switches: List[int] = field(default_factory=list)
 
     def to_dict(self) -> Dict[str, Any]:
         return asdict(self)
@@ -1019,6 +1022,8 @@ async def _run_sharded(cfg: BenchConfig, remotes: List["_RemoteServer"], admin, 
             step_cpu_operator_s=step_cpu_op, step_cpu_apiserver_s=step_cpu_api,
             cpu_s_apiserver_parts=[b - a - w for a, b, w in zip(parts0, parts1, parts_write)]
             if len(remotes) > 1 else [],
+            operator_ctx_switches=[sum(r.get("csw", [0, 0])[i] - b.get("csw", [0, 0])[i] for r, b in zip(last, base))
+                                   for i in range(2)],
             operator_maxrss_mib=[round(r.get("maxrss_mib", 0.0), 1) for r in last],
             operator_ready_maxrss_mib=[round(r.get("maxrss_mib", 0.0), 1) for r in ready],
             operator_rss_mib=[round(r.get("rss_mib", 0.0), 1) for r in last],

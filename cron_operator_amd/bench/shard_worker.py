@@ -407,11 +407,15 @@ async def main() -> int:
                              f"maxrss {_maxrss_mib():.1f} | peak: {peak[1]}\n")
                 peak[0] = 0.0
             # counters are cumulative: the harness differences them over its timed window
+            ru = resource.getrusage(resource.RUSAGE_SELF)
             out.write(json.dumps({"ok": True, "lat": lat, "reconciles": ctrl.reconciles,
                                   "requests": client.requests, "by_verb": dict(client.requests_by_verb),
                                   "cpu": time.process_time(), "gc_s": gcs.seconds,
                                   "gc_collections": list(gcs.collections), "gc_gen_s": list(gcs.gen_seconds),
-                                  "maxrss_mib": _maxrss_mib(), "rss_mib": _rss_mib()}) + "\n")
+                                  "maxrss_mib": _maxrss_mib(), "rss_mib": _rss_mib(),
+                                  # context switches (voluntary: the loop slept on I/O; involuntary:
+                                  # preempted by another runnable task on this CPU)
+                                  "csw": [ru.ru_nvcsw, ru.ru_nivcsw]}) + "\n")
             out.flush()
     _trace_dump("end")
     _mem_dump("end", mgr, rec)
