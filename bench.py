@@ -383,14 +383,21 @@ def main() -> int:
                            max_inflight=a.max_inflight, defer_writes=not a.no_defer, lifecycle=a.lifecycle,
                            apiserver_impl=a.apiserver_impl)
         _barrier(dist)
-        pres = run_sync(pcfg)
+        try:
+            pres = run_sync(pcfg)
+        except Exception as e:  # noqa: BLE001 - an extra comparison must not cost the headline line
+            pres = None
+            mine["part_error"] = f"{type(e).__name__}: {e}"[:300]
         _barrier(dist)
-        _progress(rank, f"partitioned fixture done: {pcfg.n_crons * pcfg.steps / pres.elapsed_s:.1f}")
-        mine["part_elapsed_s"] = pres.elapsed_s
-        mine["part_fires"] = pcfg.n_crons * pcfg.steps
-        mine["part_p50"] = pres.p50_latency_ms
-        mine["part_cpu_op"] = pres.cpu_s_operator
-        mine["part_cpu_api_max"] = max(pres.cpu_s_apiserver_parts)
+        if pres is not None:
+            _progress(rank, f"partitioned fixture done: {pcfg.n_crons * pcfg.steps / pres.elapsed_s:.1f}")
+            mine["part_elapsed_s"] = pres.elapsed_s
+            mine["part_fires"] = pcfg.n_crons * pcfg.steps
+            mine["part_p50"] = pres.p50_latency_ms
+            mine["part_cpu_op"] = pres.cpu_s_operator
+            mine["part_cpu_api_max"] = max(pres.cpu_s_apiserver_parts)
+        else:
+            _progress(rank, f"partitioned fixture failed: {mine['part_error']}")
 
     # the shipped default: one operator process (untimed for the headline, like the baseline)
     if a.single_process == "measure" and a.transport == "http":
@@ -536,7 +543,10 @@ def main() -> int:
             "cron_engine": res.engine,
             "wall_s": round(wall, 2),
         }
-        if all("part_fires" in r for r in allr):
+        part_errors = sorted({r["part_error"] for r in allr if "part_error" in r})
+        if part_errors:
+            out["partitioned_error"] = "; ".join(part_errors)
+        elif all("part_fires" in r for r in allr):
             part_fires = sum(r["part_fires"] for r in allr)
             out.update({
                 # the headline's shards, each against its own fake apiserver partition: what the
