@@ -41,7 +41,7 @@ def test_single_rank_line():
     assert abs(d["value"] - 20 * 2 / (d["ms_per_step"] * 2 / 1000)) / d["value"] < 0.01
     # operator cost, separated from the fake apiserver fixture
     assert d["operator_cpu_ms_per_fire"] > 0
-    assert 0 < d["apiserver_busy_frac"] < 2
+    assert 0 <= d["apiserver_busy_frac"] < 2  # /proc CPU ticks are 10 ms: a 40-fire run may read 0
     assert 10 < d["operator_shard_peak_rss_mib"] < 1024  # the largest shard process's peak (VmHWM)
     # round-5 verdict: the "peak" (ru_maxrss) read below the end RSS; a high-water mark cannot
     assert 10 < d["operator_shard_end_rss_mib"] <= d["operator_shard_peak_rss_mib"]
@@ -53,10 +53,10 @@ def test_single_rank_line():
     # the shipped default (one operator process), measured in the same invocation
     assert d["single_process_value"] > 0 and d["single_process_p50_ms"] > 0
     assert d["single_process_p99_ms"] >= d["single_process_p50_ms"]
-    assert d["single_process_operator_cpu_ms_per_fire"] > 0 and 0 < d["single_process_apiserver_busy_frac"] < 2
+    assert d["single_process_operator_cpu_ms_per_fire"] > 0 and 0 <= d["single_process_apiserver_busy_frac"] < 2
     # the same shards, each against a fake apiserver process of its own (a partitioned cluster)
     assert d["partitioned_value"] > 0 and d["partitioned_p50_ms"] > 0
-    assert d["partitioned_operator_cpu_ms_per_fire"] > 0 and 0 < d["partitioned_apiserver_busy_frac"] < 2
+    assert d["partitioned_operator_cpu_ms_per_fire"] > 0 and 0 <= d["partitioned_apiserver_busy_frac"] < 2
     # the deployment-shaped pair (TLS + etcd latency, one process, both algorithms), same invocation
     assert d["deployment_config"]["tls"] is True and d["deployment_config"]["apiserver_latency"] == "etcd"
     assert d["deployment_value"] > 0 and d["deployment_baseline_value"] > 0
