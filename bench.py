@@ -258,8 +258,10 @@ def _latency_ceiling(allr, workers: int, crons: int, history_limit: int, model: 
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[1])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    # no flags: 10 ticks after 5 of warm-up (the first ticks of a fresh set of processes run up to
+    # ~1.5x slower on the box: fixture and shard heaps growing to their working set)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--crons", type=int, default=1000)
     ap.add_argument("--history-limit", type=int, default=10)
     ap.add_argument("--workers", type=int, default=10, help="--max-concurrent-reconciles")
