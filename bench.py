@@ -258,8 +258,9 @@ def _latency_ceiling(allr, workers: int, crons: int, history_limit: int, model: 
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[1])
     ap.add_argument("--gpus", type=int, default=1)
-    # no flags: 10 ticks after 5 of warm-up (the first ticks of a fresh set of processes run up to
-    # ~1.5x slower on the box: fixture and shard heaps growing to their working set)
+    # no flags: 10 ticks after 5 of warm-up (on the box the first two or three ticks of fresh
+    # processes run 2.5-3x slower than the rest: `r6w_startup_ticks` in
+    # profiles/bench_driver_shape_mi355x_box_r6g.json)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--crons", type=int, default=1000)
