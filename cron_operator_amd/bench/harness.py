@@ -920,9 +920,12 @@ async def _run_sharded(cfg: BenchConfig, remotes: List["_RemoteServer"], admin, 
         n_pre = lifecycle_stages(cfg)
         total = cfg.warmup + cfg.steps
         step_ms: List[float] = []
-        phase_ms: Dict[str, List[float]] = {"completion": [], "fire": []}
+        phase_ms: Dict[str, List[float]] = {"completion": [], "fire": [], "completion_calls": [],
+                                            "completion_settle_max": [], "fire_settle_max": []}
+        comp: List[Dict[str, Any]] = []
         timed_lat: List[float] = []
         base: Optional[List[Dict[str, Any]]] = None
+        tc = 0.0
         last: List[Dict[str, Any]] = []
         api0 = api1 = 0.0
         t_start = 0.0
@@ -964,9 +967,11 @@ async def _run_sharded(cfg: BenchConfig, remotes: List["_RemoteServer"], admin, 
                         parts_write = [a + b for a, b in zip(parts_write, dw)]
                     await asyncio.gather(*(s.send({"cmd": "absorb", "rvs": rvs}) for s in shards))
                     await asyncio.gather(*(s.recv(cfg.step_timeout) for s in shards))
+                tc = time.perf_counter()
                 await complete_jobs(tick_ns - 30 * NANOS)
                 await set_time(tick_ns - 30 * NANOS)
-                await phase(tick_ns - 30 * NANOS, "completion", tick_ns)
+                tc = time.perf_counter() - tc
+                comp = await phase(tick_ns - 30 * NANOS, "completion", tick_ns)
             t1 = time.perf_counter()
             await set_time(tick_ns)
             last = await phase(tick_ns, "fire", tick_ns)
@@ -980,6 +985,12 @@ async def _run_sharded(cfg: BenchConfig, remotes: List["_RemoteServer"], admin, 
                 step_cpu_api.append(_cpu_times(cpu_of)[1] - step_api0 - step_write_cpu)
                 phase_ms["completion"].append((t1 - t0 - writes) * 1000)
                 phase_ms["fire"].append((t2 - t1) * 1000)
+                # inside the completion phase: the harness's completion write and clock calls
+                phase_ms["completion_calls"].append(tc * 1000 if k > 1 else 0.0)
+                # ... and the slowest shard's own wait for its Crons to settle after the clock moved
+                phase_ms["completion_settle_max"].append(
+                    max(r.get("settle_s", 0.0) for r in comp) * 1000 if k > 1 else 0.0)
+                phase_ms["fire_settle_max"].append(max(r.get("settle_s", 0.0) for r in last) * 1000)
                 if n_pre:
                     phase_ms["lifecycle_writes"].append(writes * 1000)
                 excluded += writes

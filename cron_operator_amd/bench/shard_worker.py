@@ -408,7 +408,8 @@ async def main() -> int:
                 peak[0] = 0.0
             # counters are cumulative: the harness differences them over its timed window
             ru = resource.getrusage(resource.RUSAGE_SELF)
-            out.write(json.dumps({"ok": True, "lat": lat, "reconciles": ctrl.reconciles,
+            out.write(json.dumps({"ok": True, "lat": lat, "settle_s": time.perf_counter() - tick_wall[0],
+                                  "reconciles": ctrl.reconciles,
                                   "requests": client.requests, "by_verb": dict(client.requests_by_verb),
                                   "cpu": time.process_time(), "gc_s": gcs.seconds,
                                   "gc_collections": list(gcs.collections), "gc_gen_s": list(gcs.gen_seconds),
