@@ -324,6 +324,11 @@ def main() -> int:
                          "one replicaStatuses write per pod, Running, Succeeded), each absorbed by the operator")
     ap.add_argument("--deployment-lifecycle", choices=["realistic", "instant"], default="realistic",
                     help="the same for the deployment-shaped pair (default realistic)")
+    ap.add_argument("--completion-writes", choices=["interleaved", "batch"], default="interleaved",
+                    help="instant lifecycle on the native fixture: the harness's job-completion writes are "
+                         "applied a few per server loop turn between the operator's requests ('interleaved', as "
+                         "at a real apiserver), or all in one call that holds the server for its length ('batch', "
+                         "rounds 1-5); the fixture's CPU for them is inside the timed region either way")
     ap.add_argument("--out", default="", help="also write the full result JSON here")
     a = ap.parse_args()
 
@@ -349,7 +354,7 @@ def main() -> int:
                       namespace=f"bench-r{rank}", shards=a.shards if a.transport == "http" else 1,
                       shard_routing=a.shard_routing, apiserver_latency=a.apiserver_latency, tls=a.tls,
                       max_inflight=a.max_inflight, defer_writes=not a.no_defer, lifecycle=a.lifecycle,
-                      apiserver_impl=a.apiserver_impl)
+                      apiserver_impl=a.apiserver_impl, completion_writes=a.completion_writes)
 
     def on_step(k: int, dt: float, timed: bool) -> None:
         # bracket the K timed steps with barriers so every rank times the same window: the
@@ -384,7 +389,7 @@ def main() -> int:
                            namespace=f"bench-part-r{rank}", shards=cfg.shards, apiserver_partitions=cfg.shards,
                            shard_routing="labels", apiserver_latency=a.apiserver_latency, tls=a.tls,
                            max_inflight=a.max_inflight, defer_writes=not a.no_defer, lifecycle=a.lifecycle,
-                           apiserver_impl=a.apiserver_impl)
+                           apiserver_impl=a.apiserver_impl, completion_writes=a.completion_writes)
         _barrier(dist)
         try:
             pres = run_sync(pcfg)
@@ -411,7 +416,8 @@ def main() -> int:
                                history_limit=a.history_limit, mode=a.mode, transport=a.transport, qps=a.qps,
                                burst=a.burst, workers=a.workers, namespace=f"bench-1p-r{rank}", shards=1,
                                apiserver_latency=a.apiserver_latency, tls=a.tls, max_inflight=a.max_inflight,
-                               defer_writes=not a.no_defer, lifecycle=a.lifecycle, apiserver_impl=a.apiserver_impl)
+                               defer_writes=not a.no_defer, lifecycle=a.lifecycle, apiserver_impl=a.apiserver_impl,
+                               completion_writes=a.completion_writes)
             _barrier(dist)
             sres = run_sync(scfg)
             _barrier(dist)
@@ -429,7 +435,8 @@ def main() -> int:
         bcfg = BenchConfig(n_crons=a.crons, steps=a.baseline_steps, warmup=a.baseline_warmup,
                            history_limit=a.history_limit, mode="reference", transport=a.transport, qps=a.qps,
                            burst=a.burst, workers=a.workers, namespace=f"bench-ref-r{rank}", shards=1,
-                           tls=a.tls, lifecycle=a.lifecycle, apiserver_impl=a.apiserver_impl)
+                           tls=a.tls, lifecycle=a.lifecycle, apiserver_impl=a.apiserver_impl,
+                           completion_writes=a.completion_writes)
         _barrier(dist)
         bres = run_sync(bcfg)
         _barrier(dist)
@@ -448,7 +455,7 @@ def main() -> int:
                                max_inflight=a.max_inflight, defer_writes=not a.no_defer,
                                namespace=f"bench-{tag.replace('_', '-')}-r{rank}", shards=1,
                                apiserver_latency="etcd", tls=True, lifecycle=a.deployment_lifecycle,
-                               apiserver_impl=a.apiserver_impl)
+                               apiserver_impl=a.apiserver_impl, completion_writes=a.completion_writes)
             _barrier(dist)
             try:
                 dres = run_sync(dcfg)
@@ -519,7 +526,7 @@ def main() -> int:
                        "shard_routing": cfg.shard_routing if cfg.shards > 1 else None,
                        "apiserver_latency": cfg.apiserver_latency,
                        "tls": cfg.tls, "qps": cfg.qps, "job_lifecycle": cfg.lifecycle,
-                       "apiserver_impl": cfg.apiserver_impl},
+                       "apiserver_impl": cfg.apiserver_impl, "completion_writes": cfg.completion_writes},
             "p50_schedule_to_create_ms": round(max(r["p50"] for r in allr), 2),
             "p99_schedule_to_create_ms": round(max(r["p99"] for r in allr), 2),
             "raw_reconciles_per_s": round(sum(r["reconciles"] for r in allr) / t_max, 2),

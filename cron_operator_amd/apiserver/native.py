@@ -114,6 +114,7 @@ class NativeAPIServer:
         self.srv = mod.Server(now_ns=start_ns, watch_window=watch_window, bookmark_interval=bookmark_interval)
         self.srv.set_fallback(self.fallback)
         self._faults = 0
+        self._serving = False
 
     # ------------------------------------------------------------------ setup
     def install_crd(self, crd: Dict[str, Any]) -> None:
@@ -123,10 +124,13 @@ class NativeAPIServer:
             raise RuntimeError(f"installing CRD {crd.get('metadata', {}).get('name')}: {st} {body[:300]!r}")
 
     def start(self, host: str = "127.0.0.1", port: int = 0, certfile: str = "", keyfile: str = "") -> int:
-        return self.srv.start(host, port, certfile, keyfile)
+        port = self.srv.start(host, port, certfile, keyfile)
+        self._serving = True
+        return port
 
     def stop(self) -> None:
         self.srv.stop()
+        self._serving = False
 
     def _kind_of(self, group: str, version: str, resource: str) -> str:
         st, raw = self.srv.request("GET", f"/apis/{group}/{version}" if group else f"/api/{version}")
@@ -187,8 +191,11 @@ class NativeAPIServer:
             # one body for every job of the kind, the name filled in natively per job
             kind = _KINDS.get(r) or self._kind_of(g, v, r)
             tmpl = jsonutil.dumpb({"status": finished_status(kind, _NAME, ts, True)})
-            n = srv.patch_unfinished(g, v, r, body.get("namespace") or "", tmpl, _NAME, "status")
-            return {"completed": n}
+            # perTurn > 0: queued, the server applies that many per loop turn between the turns
+            # serving the other clients (the response comes back before they are all applied)
+            per_turn = int(body.get("perTurn") or 0)
+            n = srv.patch_unfinished(g, v, r, body.get("namespace") or "", tmpl, _NAME, "status", per_turn)
+            return {"completed": n, "queued": per_turn > 0 and self._serving}
         if what == "lifecycle" and method == "POST":
             from ..trainingop.operator import lifecycle_status, replica_counts
 

@@ -60,6 +60,8 @@ PYTORCHJOBS = GroupVersionResource("kubeflow.org", "v1", "pytorchjobs")
 
 # 2026-01-01T12:00:00Z: crons are created here; step k ticks at +k minutes
 T0_NS = 1767268800 * NANOS
+# completion_writes="interleaved": completion PATCHes the fake apiserver applies per loop turn
+COMPLETION_WRITES_PER_TURN = 32
 
 
 # Server-side latency models for the fake apiserver (seconds per verb, applied after setup).
@@ -124,6 +126,12 @@ class BenchConfig:
     # routing -- a partitioned cluster, server i holding the Crons that hash to shard i (shard_of)
     # and their jobs, so no one single-threaded fixture bounds the shards (bench.py partitioned_*)
     apiserver_partitions: int = 1
+    # instant lifecycle, native fixture: how the harness's "every job finishes" writes reach the
+    # fake apiserver -- "interleaved" (queued, a few applied per server loop turn between the turns
+    # serving the operator, as a training operator's writes interleave with everyone else's at a
+    # real apiserver) or "batch" (rounds 1-5 and most of 6: all of them in one call that holds the
+    # server and its watches for its length); the fixture's CPU for them is counted either way
+    completion_writes: str = "interleaved"
     # events per resource the fake apiserver keeps for watch resume (a bounded watch cache: the
     # soak's fixture memory stays flat; 20,000 is ~5 ticks of 1000 Crons' job events)
     watch_window: int = 20_000
@@ -550,7 +558,10 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
                     server.patch(PYTORCHJOBS, cfg.namespace, m["name"],
                                  {"status": finished_status("PyTorchJob", m["name"], ts, True)}, "merge", "status")
         else:
-            await admin_post("/debug/fake/complete", {"namespace": cfg.namespace, "time": ts})
+            req = {"namespace": cfg.namespace, "time": ts}
+            if cfg.completion_writes == "interleaved":
+                req["perTurn"] = COMPLETION_WRITES_PER_TURN
+            await admin_post("/debug/fake/complete", req)
 
 
     try:

@@ -923,6 +923,8 @@ struct Server {
 };
 #endif
 
+Ref subst(const Ref& t, const std::string& ph, const std::string& name);
+
 struct Impl {
   std::recursive_mutex mu;
   long long now_ns = 0;
@@ -993,6 +995,19 @@ struct Impl {
   bool watch_deferred = false;
   double watch_defer_since = 0.0;
   long long sends = 0, turns = 0;
+  // patch_unfinished with a per-turn budget: the harness's completion writes applied a few per
+  // loop turn, between the turns that serve the other clients -- as a training operator's writes
+  // interleave with everyone else's at a real apiserver -- instead of one batch that holds the
+  // server (and every watch) for its whole length
+  struct PendingPatches {
+    std::string g, v, r;  // looked up each turn: a resource may go away meanwhile
+    std::string sub, ph;
+    Ref tree;
+    std::vector<std::pair<std::string, std::string>> todo;  // (namespace, name)
+    size_t next = 0, per_turn = 1;
+  };
+  std::deque<PendingPatches> pending_patches;
+  long long pending_applied = 0;
 
   ~Impl() {
     for (auto& kv : conns) delete kv.second;
@@ -2776,6 +2791,22 @@ struct Impl {
     }
   }
 
+  // one turn's share of the queued completion writes (accounted with the fallback's controls)
+  void run_pending_patches() {
+    const unsigned long long t0 = __rdtsc();
+    PendingPatches& p = pending_patches.front();
+    Resource* ri = find(p.g, p.v, p.r);
+    if (!ri) p.next = p.todo.size();
+    for (size_t k = 0; k < p.per_turn && p.next < p.todo.size(); ++k) {
+      const auto& t = p.todo[p.next++];
+      Ref patch = subst(p.tree, p.ph, t.second);
+      ApiErr err;
+      if (v_patch(ri, t.first, t.second, patch, "merge", p.sub, &err)) ++pending_applied;
+    }
+    if (p.next >= p.todo.size()) pending_patches.pop_front();
+    cyc_fallback += __rdtsc() - t0;
+  }
+
   void loop() {
     loop_tid.store(static_cast<pid_t>(syscall(SYS_gettid)));
     if (const char* e = std::getenv("APISERVERD_WATCH_DEFER_S")) watch_defer_s = std::strtod(e, nullptr);
@@ -2788,7 +2819,8 @@ struct Impl {
         const double d = timers.top().due - mono();
         timeout_ms = d <= 0 ? 0 : static_cast<int>(std::min(1000.0, std::ceil(d * 1000.0)));
       }
-      if (watch_deferred) timeout_ms = 0;  // poll: the deferred watch events go out once idle
+      // poll: the deferred watch events go out once idle; queued completion writes continue
+      if (watch_deferred || !pending_patches.empty()) timeout_ms = 0;
       const int n = epoll_wait(epfd, evs.data(), static_cast<int>(evs.size()), timeout_ms);
       std::lock_guard<std::recursive_mutex> g(mu);
       const long long turn0 = thread_cpu_ns();
@@ -2812,6 +2844,7 @@ struct Impl {
         if (!c->closed && (e & (EPOLLIN | EPOLLRDHUP | EPOLLHUP | EPOLLERR))) on_readable(c);
       }
       run_timers();
+      if (!pending_patches.empty()) run_pending_patches();
       ++turns;
       end_of_turn(n == 0 || watch_defer_s <= 0.0 || (watch_deferred && mono() - watch_defer_since >= watch_defer_s));
       cyc_loop += __rdtsc() - tc0;
@@ -2870,6 +2903,12 @@ struct Impl {
     running = true;
     thread = std::thread([this] { loop(); });
     return true;
+  }
+
+  // make the loop's epoll_wait return (work queued from another thread)
+  void wake() {
+    const uint64_t one = 1;
+    (void)!::write(evfd, &one, sizeof one);
   }
 
   void stop() {
@@ -3388,10 +3427,12 @@ PyObject* Server_patch_many(Server* self, PyObject* args) {
   return lst;
 }
 
-// patch_unfinished(group, version, resource, namespace, template, placeholder, subresource="")
-//   -> int: one merge PATCH per object whose status has no completionTime, its body the template
-//   with `placeholder` replaced by the object's name -- the bench's "every job finishes" write,
-//   without a Python round trip per job
+// patch_unfinished(group, version, resource, namespace, template, placeholder, subresource="",
+//   per_turn=0) -> int: one merge PATCH per object whose status has no completionTime, its body
+//   the template with `placeholder` replaced by the object's name -- the bench's "every job
+//   finishes" write, without a Python round trip per job.  per_turn > 0 on a running server:
+//   the patches are queued and the server thread applies that many per loop turn, between the
+//   turns serving other clients (returns the number queued)
 // `t` with every `ph` inside its strings replaced by `name` (keys untouched): a node whose
 // subtree holds no placeholder is shared, not copied
 Ref subst(const Ref& t, const std::string& ph, const std::string& name) {
@@ -3439,8 +3480,8 @@ Ref subst(const Ref& t, const std::string& ph, const std::string& name) {
 
 PyObject* Server_patch_unfinished(Server* self, PyObject* args) {
   const char *g, *v, *r, *ns, *tmpl, *ph, *sub = "";
-  Py_ssize_t tl, pl;
-  if (!PyArg_ParseTuple(args, "sssss#s#|s", &g, &v, &r, &ns, &tmpl, &tl, &ph, &pl, &sub)) return nullptr;
+  Py_ssize_t tl, pl, per_turn = 0;
+  if (!PyArg_ParseTuple(args, "sssss#s#|sn", &g, &v, &r, &ns, &tmpl, &tl, &ph, &pl, &sub, &per_turn)) return nullptr;
   Impl* s = self->impl;
   long long n = 0;
   bool known = true;
@@ -3469,11 +3510,27 @@ PyObject* Server_patch_unfinished(Server* self, PyObject* args) {
       // the template parsed once; each job's patch copies only the nodes whose strings hold
       // the placeholder (a condition's message), the rest is shared
       Ref tree = jdom::parse(ts.data(), ts.size());
-      for (const auto& t : todo) {
-        if (!tree) break;
-        Ref patch = subst(tree, phs, t.second);
-        ApiErr err;
-        if (s->v_patch(ri, t.first, t.second, patch, "merge", subs, &err)) ++n;
+      if (tree && per_turn > 0 && s->running) {
+        // queued: the server thread applies `per_turn` of them per loop turn (run_pending_patches)
+        n = static_cast<long long>(todo.size());
+        Impl::PendingPatches p;
+        p.g = gs;
+        p.v = vs;
+        p.r = rs;
+        p.sub = subs;
+        p.ph = phs;
+        p.tree = tree;
+        p.todo = std::move(todo);
+        p.per_turn = static_cast<size_t>(per_turn);
+        if (n) s->pending_patches.push_back(std::move(p));
+        if (std::this_thread::get_id() != s->thread.get_id()) s->wake();
+      } else {
+        for (const auto& t : todo) {
+          if (!tree) break;
+          Ref patch = subst(tree, phs, t.second);
+          ApiErr err;
+          if (s->v_patch(ri, t.first, t.second, patch, "merge", subs, &err)) ++n;
+        }
       }
     }
     if (!s->running || std::this_thread::get_id() != s->thread.get_id()) s->end_of_turn();
@@ -3637,7 +3694,8 @@ PyMethodDef Server_methods[] = {
     {"unfinished", reinterpret_cast<PyCFunction>(Server_unfinished), METH_VARARGS,
      "unfinished(group, version, resource, namespace) -> [(name, kind, bytes)] without status.completionTime"},
     {"patch_unfinished", reinterpret_cast<PyCFunction>(Server_patch_unfinished), METH_VARARGS,
-     "patch_unfinished(group, version, resource, namespace, template, placeholder, subresource='') -> int"},
+     "patch_unfinished(group, version, resource, namespace, template, placeholder, subresource='', per_turn=0) -> int "
+     "(per_turn > 0 on a running server: queued, that many applied per loop turn)"},
     {"patch_many", reinterpret_cast<PyCFunction>(Server_patch_many), METH_VARARGS,
      "patch_many(group, version, resource, namespace, [(name, body)], subresource='') -> [resourceVersion|None]"},
     {nullptr, nullptr, 0, nullptr}};

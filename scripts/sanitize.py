@@ -29,7 +29,8 @@ every entry point with mutated and generated inputs:
   valid and mutated bodies against the installed CRDs' admission; the bulk controls
   (``patch_many``, ``patch_unfinished``, ``unfinished``); and over HTTP on its epoll thread:
   mutated raw requests in random splits, watches opened at random resourceVersions and
-  dropped mid-stream while writes fan out to them, then ``stop``;
+  dropped mid-stream while writes fan out to them, completion writes queued a few per loop
+  turn among them, then ``stop`` (some still queued);
 
 Any memory error or undefined behaviour aborts with the sanitizer report.
 ``make sanitize`` runs it.  Host code only: the operator has no GPU code.
@@ -684,8 +685,11 @@ def drive_apiserverd(scratch: str, iters: int) -> int:
                 except OSError:
                     pass
             s.close()
-        else:
+        elif r < 0.9:
             srv.request("DELETE", f"{jobs}/j{rng.randrange(20)}", "", b"{}", "application/json")
+        else:  # completion writes queued on the running server, a few per loop turn (some left at stop)
+            srv.patch_unfinished("kubeflow.org", "v1", "pytorchjobs", "ns", tmpl, b"@@name@@", "status",
+                                 rng.randint(1, 8))
         if socks and rng.random() < 0.3:
             s = socks.pop(rng.randrange(len(socks)))
             s.setblocking(False)

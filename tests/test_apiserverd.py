@@ -434,11 +434,57 @@ def test_bench_controls_complete_and_lifecycle():
     rvs = ctl("lifecycle", {"namespace": NS, "stage": 0, "start": "2026-01-01T12:00:00Z",
                             "end": "2026-01-01T12:00:30Z"})["resourceVersions"]
     assert sorted(rvs) == [f"{NS}/j{i}" for i in range(5)]
-    assert ctl("complete", {"namespace": NS, "time": "2026-01-01T12:00:30Z"}) == {"completed": 5}
-    assert ctl("complete", {"namespace": NS, "time": "2026-01-01T12:00:30Z"}) == {"completed": 0}
+    # perTurn on a server that is not running: applied at once, as without it
+    assert ctl("complete", {"namespace": NS, "time": "2026-01-01T12:00:30Z", "perTurn": 2}) == \
+        {"completed": 5, "queued": False}
+    assert ctl("complete", {"namespace": NS, "time": "2026-01-01T12:00:30Z"}) == {"completed": 0, "queued": False}
     job = json.loads(srv.request("GET", JOBS + "/j0")[1])
     assert job["status"]["completionTime"] == "2026-01-01T12:00:30Z"
     assert job["status"]["conditions"][-1]["type"] == "Succeeded"
     stats = json.loads(nat.fallback("GET", "/debug/fake/stats", "", {}, b"")[1])
     assert stats["by_verb"]["patch"] == 10 and stats["native"] is True
     assert nat.fallback("POST", "/debug/fake/faults", "", {}, b'{"faults":[{"verb":"create"}]}')[0] == 501
+
+
+async def test_interleaved_completion_writes_are_applied_a_few_per_turn():
+    """``complete`` with ``perTurn`` on a running server answers at once with the number queued;
+    the server thread then applies that many per loop turn, serving other requests between them:
+    a GET sent right after the control is answered while writes are still queued, and a watch
+    sees every job's MODIFIED event."""
+    nat = NativeAPIServer(T0)
+    for c in kubeflow_crds():
+        nat.install_crd(c)
+    srv = nat.srv
+    srv.request("POST", "/api/v1/namespaces", "", b'{"metadata":{"name":"bench"}}', "application/json")
+    n = 400
+    for i in range(n):
+        srv.request("POST", JOBS, "", json.dumps(_job(f"j{i}")).encode(), "application/json")
+    port = nat.start("127.0.0.1", 0)
+    try:
+        r, w = await _open_watch(port, JOBS, "resourceVersion=" + json.loads(srv.request("GET", JOBS)[1])
+                                 ["metadata"]["resourceVersion"])
+        cr, cw = await asyncio.open_connection("127.0.0.1", port)
+
+        async def call(method: str, path: str, body: bytes = b"") -> Tuple[bytes, bytes]:
+            cw.write(f"{method} {path} HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\n"
+                     f"Content-Length: {len(body)}\r\n\r\n".encode() + body)
+            await cw.drain()
+            head = await asyncio.wait_for(cr.readuntil(b"\r\n\r\n"), 5)
+            ln = int([x for x in head.split(b"\r\n") if x.lower().startswith(b"content-length")][0].split(b":")[1])
+            return head, await cr.readexactly(ln)
+
+        head, body = await call("POST", "/debug/fake/complete",
+                                json.dumps({"namespace": NS, "time": "2026-01-01T12:00:30Z", "perTurn": 1}).encode())
+        assert head.startswith(b"HTTP/1.1 200") and json.loads(body) == {"completed": n, "queued": True}
+        head, body = await call("GET", JOBS + "?limit=1")  # served between the queued writes
+        assert head.startswith(b"HTTP/1.1 200")
+        evs = await _read_events(r, n, timeout=20)
+        assert {e["type"] for e in evs} == {"MODIFIED"} and len({e["object"]["metadata"]["name"] for e in evs}) == n
+        assert all(e["object"]["status"]["completionTime"] == "2026-01-01T12:00:30Z" for e in evs)
+        head, body = await call("POST", "/debug/fake/complete",
+                                json.dumps({"namespace": NS, "time": "2026-01-01T12:00:30Z", "perTurn": 1}).encode())
+        assert json.loads(body) == {"completed": 0, "queued": True}
+        w.close()
+        cw.close()
+    finally:
+        nat.stop()
