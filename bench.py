@@ -52,6 +52,9 @@ in this same invocation after the timed run; ``vs_baseline_deployment`` is their
 
 Job lifecycle.  The headline (and its single-process and reference runs) keeps the rounds 1-4
 step: each job of the previous tick is marked Succeeded in one write (``--lifecycle instant``).
+The fake apiserver applies those writes a few per loop turn, between the turns serving the
+operator (``--completion-writes interleaved``; ``batch`` applies all of them in one call, as in
+rounds 1-5); their fixture CPU is inside the timed region either way.
 The deployment-shaped pair runs the realistic sequence (``--deployment-lifecycle realistic``):
 the training-operator's ``Created``, one ``replicaStatuses`` write per pod, ``Running``, then
 ``Succeeded``, each absorbed by the operator before the next.  Every such write changes the job's
