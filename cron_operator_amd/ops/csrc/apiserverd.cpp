@@ -783,10 +783,17 @@ struct Conn;
 // name, namespace and labels -- not the object trees: a superseded version is freed when the
 // store replaces it, while its nodes are still in cache, instead of watch_window events later
 // (when the log held the trees, the fixture's CPU per fire drifted with the heap's age).
+// An object's scope: its metadata's name, namespace and labels, shared with the object (no
+// allocation per event); a replay builds the {"metadata": {...}} a selector reads from it.
+struct Scope {
+  Ref name, ns, labels;
+  bool set = false;  // a MODIFIED event's previous version, or none
+};
+
 struct Event {
   long long rv;
   int type;  // 0 ADDED 1 MODIFIED 2 DELETED
-  Ref scope, old_scope;                      // {"metadata": {name, namespace, labels}}
+  Scope scope, old_scope;
   jdom::jstr bytes;  // the object as encoded in the event (pool-allocated: the log turns over FIFO)
   Ref held, held_old;  // APISERVERD_LOG_TREES=1 only: the trees too, as rounds 1-5 kept them (A/B arm)
 };
@@ -1257,16 +1264,26 @@ struct Impl {
   }
 
   // what a resuming watcher's scope reads of an object: its name, namespace and labels
-  static Ref scope_of(const Node* obj) {
-    Ref sc = jdom::mk_obj();
+  static Scope scope_of(const Node* obj) {
+    Scope sc;
+    sc.set = true;
     const Node* m = obj->getn("metadata");
     if (m && m->is_obj()) {
-      Ref mm = jdom::mk_obj();
-      for (const char* k : {"name", "namespace", "labels"})
-        if (const Ref* v = m->get(k)) mm->o.emplace_back(k, *v);
-      sc->o.emplace_back("metadata", mm);
+      if (const Ref* v = m->get("name")) sc.name = *v;
+      if (const Ref* v = m->get("namespace")) sc.ns = *v;
+      if (const Ref* v = m->get("labels")) sc.labels = *v;
     }
     return sc;
+  }
+  // ... as the object a selector matches (a replay only)
+  static Ref scope_tree(const Scope& sc) {
+    Ref t = jdom::mk_obj();
+    Ref mm = jdom::mk_obj();
+    if (sc.name) mm->o.emplace_back("name", sc.name);
+    if (sc.ns) mm->o.emplace_back("namespace", sc.ns);
+    if (sc.labels) mm->o.emplace_back("labels", sc.labels);
+    t->o.emplace_back("metadata", mm);
+    return t;
   }
 
   void emit(Resource* ri, int type, const Ref& obj, const Ref& old, long long at) {
@@ -1274,7 +1291,7 @@ struct Impl {
     Store* st = ri->store;
     const jdom::jstr& enc = jdom::encoded(obj.get());
     const bool with_old = type == 1 && old;
-    st->log.push_back(Event{at, type, scope_of(obj.get()), with_old ? scope_of(old.get()) : Ref(),
+    st->log.push_back(Event{at, type, scope_of(obj.get()), with_old ? scope_of(old.get()) : Scope(),
                             jdom::jstr(enc.data(), enc.size()),
                             log_trees ? obj : Ref(), log_trees ? old : Ref()});
     while (st->log.size() > watch_window) {
@@ -2169,9 +2186,9 @@ struct Impl {
         }
       for (const Event& ev : st->log)
         if (ev.rv > since) {
-          const bool now_in = w->in_scope(ev.scope.get());
-          const bool was_in = ev.type == 1 && ev.old_scope ? w->in_scope(ev.old_scope.get()) : false;
-          offer(w.get(), ev.type, std::string_view(ev.bytes), static_cast<bool>(ev.old_scope), now_in, was_in);
+          const bool now_in = w->in_scope(scope_tree(ev.scope).get());
+          const bool was_in = ev.type == 1 && ev.old_scope.set ? w->in_scope(scope_tree(ev.old_scope).get()) : false;
+          offer(w.get(), ev.type, std::string_view(ev.bytes), ev.old_scope.set, now_in, was_in);
         }
     }
     Watcher* out = w.release();
