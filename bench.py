@@ -12,12 +12,23 @@ its own process, over HTTP + watch streams.  Synthetic objects, no cluster.
 
 Each rank runs the operator as ``--shards`` (default 3; fewer when the CPUs available
 to the job cannot give each rank a core per shard plus one for its apiserver) shard processes of the
-operator's horizontal sharding feature against one apiserver: the reference's Go
-controller spreads its 10 reconcile workers over all cores as goroutines, and
-sharding is how this asyncio operator uses more than one core.  ``--shards 1``
-keeps a single operator process.  ``--shard-routing labels`` (default) has each
-shard watch only its own Crons and children (``kubedl.io/shard`` labels, assigned
-by the shards during setup); ``hash`` has every shard watch everything.
+operator's horizontal sharding feature: the reference's Go controller spreads its 10 reconcile
+workers over all cores as goroutines, and sharding is how this asyncio operator uses more than
+one core.  ``--shards 1`` keeps a single operator process.  ``--shard-routing labels`` (default)
+has each shard watch only its own Crons and children (``kubedl.io/shard`` labels, assigned by
+the shards during setup); ``hash`` has every shard watch everything.
+
+The fake cluster (``--fixture``).  A real apiserver serves from many cores; the fake one is one
+server thread, and one of them saturates under 3 shards (0.87-0.93 busy in round 6: the number
+then measured the fixture as much as the operator).  So by default (``partitioned``) each shard
+gets a fake apiserver process of its own, holding the Crons that hash to that shard and their
+jobs -- exactly what that shard watches and writes under label routing -- and the headline
+measures the shards (busiest partition ~0.5-0.6 busy on the box).  It needs two CPUs per shard
+plus one per rank; with fewer the headline falls back to ``shared``: every shard against one
+fake apiserver, the rounds 1-5 layout.  ``shared_fixture_*`` (or ``partitioned_*`` when the
+headline is shared) is the same shards against the other layout, in this same invocation after
+the timed run (``--other-fixture none`` skips it); ``config.fixture`` says which one the
+headline used.
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
 it runs under ``torch.distributed.run`` with one rank per GPU (without a launcher,
@@ -30,18 +41,11 @@ gloo barriers; there is no device work to ``torch.cuda.synchronize()``.
 ``single_process_*``: the chart ships ONE operator process (``sharding.count: 1``,
 ``processes: 1``); it runs in the same invocation on the same Crons, after the timed run
 (``--single-process none`` skips it).  ``operator_cpu_ms_per_fire`` and ``apiserver_busy_frac``
-(and their ``single_process_`` twins) say which side bounds each number: near 1.0 busy, the fake
-apiserver fixture does.  Since round 6 the fixture is native C++ (``--apiserver-impl native``,
-``ops/csrc/apiserverd.cpp``): at the round-6 head 0.87 busy at 3 shards (still partly the
-fixture's), 0.36 for one process (the operator's); the Python fixture of rounds 1-5 ran 0.94 and
-0.86 (``--apiserver-impl python``).
-
-``partitioned_*``: the headline's shards again, each against a fake apiserver process of its own
-that holds the Crons hashing to that shard and their jobs -- a partitioned cluster, as if the
-apiserver had a core per shard.  Run in this invocation after the timed run (``--partitioned
-none`` skips it; it needs two CPUs per shard per rank).  With no single-threaded fixture in the
-way it is the operator's sharded throughput; ``partitioned_apiserver_busy_frac`` is the busiest
-partition's CPU s per wall s.
+(and their ``single_process_`` / ``shared_fixture_`` twins) say which side bounds each number:
+near 1.0 busy, the fake apiserver does (``apiserver_busy_frac`` is the busiest fake apiserver's
+CPU s per wall s; ``apiserver_cpu_us_per_fire`` counts all of them).  Since round 6 the fixture
+is native C++ (``--apiserver-impl native``, ``ops/csrc/apiserverd.cpp``); the Python fixture of
+rounds 1-5 ran 0.94 busy at 3 shards and 0.86 for one process (``--apiserver-impl python``).
 
 ``deployment_*``: a real cluster is latency-bound, not CPU-bound: TLS on every connection and an
 etcd quorum write behind every mutation.  ``deployment_value`` / ``deployment_baseline_value`` are
@@ -301,11 +305,14 @@ def main() -> int:
                          "processes=1) -- on the same 1000 Crons in this invocation, outside the headline's timed "
                          "region, and report it as single_process_*: operator-bound, so it measures the product "
                          "rather than the fake apiserver")
-    ap.add_argument("--partitioned", choices=["measure", "none"], default="measure",
-                    help="also run the headline's shards against a partitioned fake cluster -- one apiserver "
-                         "process per shard holding that shard's Crons and jobs -- outside the headline's timed "
-                         "region: partitioned_* keys, the operator's sharded throughput with no single-threaded "
-                         "fixture in its way (needs 2 CPUs per shard per rank; skipped otherwise)")
+    ap.add_argument("--fixture", choices=["partitioned", "shared"], default="partitioned",
+                    help="the headline's fake apiserver with more than one shard: 'partitioned' (default) -- one "
+                         "apiserver process per shard, holding the Crons that hash to it and their jobs, so no "
+                         "single-threaded fixture bounds the shards (needs 2 CPUs per shard + 1 per rank; 'shared' "
+                         "otherwise) -- or 'shared', every shard against one apiserver process (rounds 1-5)")
+    ap.add_argument("--other-fixture", choices=["measure", "none"], default="measure",
+                    help="also run the headline's shards against the other fixture layout, outside the "
+                         "headline's timed region: shared_fixture_* (or partitioned_*) keys")
     ap.add_argument("--single-steps", type=int, default=10)
     ap.add_argument("--single-warmup", type=int, default=3)
     ap.add_argument("--deployment", choices=["measure", "none"], default="measure",
@@ -352,12 +359,23 @@ def main() -> int:
         # 3 shards saturate one fake apiserver process; never oversubscribe the CPUs the ranks share
         a.shards = max(1, min(3, available_cpus() // world - 1))
 
-    cfg = BenchConfig(n_crons=a.crons, steps=a.steps, warmup=a.warmup, history_limit=a.history_limit,
-                      mode=a.mode, transport=a.transport, qps=a.qps, burst=a.burst, workers=a.workers,
-                      namespace=f"bench-r{rank}", shards=a.shards if a.transport == "http" else 1,
-                      shard_routing=a.shard_routing, apiserver_latency=a.apiserver_latency, tls=a.tls,
-                      max_inflight=a.max_inflight, defer_writes=not a.no_defer, lifecycle=a.lifecycle,
-                      apiserver_impl=a.apiserver_impl, completion_writes=a.completion_writes)
+    from cron_operator_amd.runtime.supervisor import available_cpus
+
+    shards = a.shards if a.transport == "http" else 1
+    # a partitioned fixture: a fake apiserver process per shard, each with a core of its own
+    can_partition = (shards > 1 and a.shard_routing == "labels"
+                     and available_cpus() // world >= 2 * shards + 1)
+    parts = shards if a.fixture == "partitioned" and can_partition else 1
+
+    def bench_cfg(namespace: str, partitions: int) -> "BenchConfig":
+        return BenchConfig(n_crons=a.crons, steps=a.steps, warmup=a.warmup, history_limit=a.history_limit,
+                           mode=a.mode, transport=a.transport, qps=a.qps, burst=a.burst, workers=a.workers,
+                           namespace=namespace, shards=shards, apiserver_partitions=partitions,
+                           shard_routing=a.shard_routing, apiserver_latency=a.apiserver_latency, tls=a.tls,
+                           max_inflight=a.max_inflight, defer_writes=not a.no_defer, lifecycle=a.lifecycle,
+                           apiserver_impl=a.apiserver_impl, completion_writes=a.completion_writes)
+
+    cfg = bench_cfg(f"bench-r{rank}", parts)
 
     def on_step(k: int, dt: float, timed: bool) -> None:
         # bracket the K timed steps with barriers so every rank times the same window: the
@@ -379,36 +397,32 @@ def main() -> int:
     mine = {"elapsed_s": res.elapsed_s, "fires": cfg.n_crons * cfg.steps,
             "reconciles": res.raw_reconciles_per_s * res.elapsed_s, "p50": res.p50_latency_ms,
             "p99": res.p99_latency_ms, "req_per_fire": res.api_requests_per_fire,
-            "cpu_op": res.cpu_s_operator, "cpu_api": res.cpu_s_apiserver,
+            "cpu_op": res.cpu_s_operator, "cpu_api_total": res.cpu_s_apiserver,
+            # busy fraction: the busiest fake apiserver (one, or one per shard)
+            "cpu_api": max(res.cpu_s_apiserver_parts) if res.cpu_s_apiserver_parts else res.cpu_s_apiserver,
             "shard_rss": max(res.operator_maxrss_mib or [0.0]), "shard_end_rss": max(res.operator_rss_mib or [0.0])}
 
-    # the same shards, each against its own fake apiserver partition (untimed for the headline)
-    from cron_operator_amd.runtime.supervisor import available_cpus
-
-    if (a.partitioned == "measure" and a.transport == "http" and cfg.shards > 1 and a.shard_routing == "labels"
-            and available_cpus() // world >= 2 * cfg.shards):
-        pcfg = BenchConfig(n_crons=a.crons, steps=a.steps, warmup=a.warmup, history_limit=a.history_limit,
-                           mode=a.mode, transport="http", qps=a.qps, burst=a.burst, workers=a.workers,
-                           namespace=f"bench-part-r{rank}", shards=cfg.shards, apiserver_partitions=cfg.shards,
-                           shard_routing="labels", apiserver_latency=a.apiserver_latency, tls=a.tls,
-                           max_inflight=a.max_inflight, defer_writes=not a.no_defer, lifecycle=a.lifecycle,
-                           apiserver_impl=a.apiserver_impl, completion_writes=a.completion_writes)
+    # the same shards against the other fixture layout (untimed for the headline)
+    if a.other_fixture == "measure" and can_partition:
+        ocfg = bench_cfg(f"bench-alt-r{rank}", 1 if parts > 1 else shards)
         _barrier(dist)
         try:
-            pres = run_sync(pcfg)
+            ores = run_sync(ocfg)
         except Exception as e:  # noqa: BLE001 - an extra comparison must not cost the headline line
-            pres = None
-            mine["part_error"] = f"{type(e).__name__}: {e}"[:300]
+            ores = None
+            mine["alt_error"] = f"{type(e).__name__}: {e}"[:300]
         _barrier(dist)
-        if pres is not None:
-            _progress(rank, f"partitioned fixture done: {pcfg.n_crons * pcfg.steps / pres.elapsed_s:.1f}")
-            mine["part_elapsed_s"] = pres.elapsed_s
-            mine["part_fires"] = pcfg.n_crons * pcfg.steps
-            mine["part_p50"] = pres.p50_latency_ms
-            mine["part_cpu_op"] = pres.cpu_s_operator
-            mine["part_cpu_api_max"] = max(pres.cpu_s_apiserver_parts)
+        if ores is not None:
+            _progress(rank, f"{'shared' if parts > 1 else 'partitioned'} fixture done: "
+                            f"{ocfg.n_crons * ocfg.steps / ores.elapsed_s:.1f}")
+            mine["alt_elapsed_s"] = ores.elapsed_s
+            mine["alt_fires"] = ocfg.n_crons * ocfg.steps
+            mine["alt_p50"] = ores.p50_latency_ms
+            mine["alt_cpu_op"] = ores.cpu_s_operator
+            mine["alt_cpu_api"] = (max(ores.cpu_s_apiserver_parts) if ores.cpu_s_apiserver_parts
+                                   else ores.cpu_s_apiserver)
         else:
-            _progress(rank, f"partitioned fixture failed: {mine['part_error']}")
+            _progress(rank, f"other fixture failed: {mine['alt_error']}")
 
     # the shipped default: one operator process (untimed for the headline, like the baseline)
     if a.single_process == "measure" and a.transport == "http":
@@ -519,7 +533,9 @@ def main() -> int:
             "vs_baseline": round(value / base_value, 3) if base_value else None,
             "dtype": "n/a (control plane; no tensor compute)",
             "data": f"synthetic: {cfg.n_crons} random-free Cron CRs per rank (* * * * *, "
-                    f"historyLimit={cfg.history_limit}) + PyTorchJob children on a fake apiserver process per rank",
+                    f"historyLimit={cfg.history_limit}) + PyTorchJob children on "
+                    + (f"a fake apiserver process per shard ({cfg.apiserver_partitions} per rank, each holding its "
+                       f"shard's Crons)" if cfg.apiserver_partitions > 1 else "a fake apiserver process per rank"),
             "config": {"model": "cron-operator Cron reconciler (apps.kubedl.io/v1alpha1)",
                        "global_batch": fires // a.steps, "seq_len": None,
                        "parallelism": f"ranks{world}x{cfg.shards}shards", "crons_per_rank": cfg.n_crons,
@@ -529,7 +545,9 @@ def main() -> int:
                        "shard_routing": cfg.shard_routing if cfg.shards > 1 else None,
                        "apiserver_latency": cfg.apiserver_latency,
                        "tls": cfg.tls, "qps": cfg.qps, "job_lifecycle": cfg.lifecycle,
-                       "apiserver_impl": cfg.apiserver_impl, "completion_writes": cfg.completion_writes},
+                       "apiserver_impl": cfg.apiserver_impl, "completion_writes": cfg.completion_writes,
+                       "fixture": "partitioned" if cfg.apiserver_partitions > 1 else "shared",
+                       "apiserver_partitions": cfg.apiserver_partitions},
             "p50_schedule_to_create_ms": round(max(r["p50"] for r in allr), 2),
             "p99_schedule_to_create_ms": round(max(r["p99"] for r in allr), 2),
             "raw_reconciles_per_s": round(sum(r["reconciles"] for r in allr) / t_max, 2),
@@ -537,9 +555,10 @@ def main() -> int:
             # operator-side cost (all shard processes), the number to track rather than the
             # fake apiserver's speed; and how busy that fixture was (CPU s / wall s, max rank)
             "operator_cpu_ms_per_fire": round(sum(r["cpu_op"] for r in allr) * 1000 / fires, 4),
+            # (the busiest fake apiserver of any rank: with a partitioned fixture, its busiest partition)
             "apiserver_busy_frac": round(max(r["cpu_api"] / r["elapsed_s"] for r in allr), 3),
             # the fixture's own CPU per fire (all ranks' fake apiservers): its speed, apart from the load
-            "apiserver_cpu_us_per_fire": round(sum(r["cpu_api"] for r in allr) * 1e6 / fires, 1),
+            "apiserver_cpu_us_per_fire": round(sum(r["cpu_api_total"] for r in allr) * 1e6 / fires, 1),
             # peak resident memory (VmHWM) of the largest operator shard process (0: the operator
             # ran in the bench process itself)
             "operator_shard_peak_rss_mib": round(max(r.get("shard_rss", 0.0) for r in allr), 1),
@@ -556,21 +575,21 @@ def main() -> int:
             "cron_engine": res.engine,
             "wall_s": round(wall, 2),
         }
-        part_errors = sorted({r["part_error"] for r in allr if "part_error" in r})
-        if part_errors:
-            out["partitioned_error"] = "; ".join(part_errors)
-        elif all("part_fires" in r for r in allr):
-            part_fires = sum(r["part_fires"] for r in allr)
+        # the headline's shards against the other fixture layout: shared_fixture_* when the
+        # headline is partitioned (rounds 1-5's layout, one fake apiserver for every shard), else
+        # partitioned_*
+        alt = "shared_fixture" if cfg.apiserver_partitions > 1 else "partitioned"
+        alt_errors = sorted({r["alt_error"] for r in allr if "alt_error" in r})
+        if alt_errors:
+            out[f"{alt}_error"] = "; ".join(alt_errors)
+        elif all("alt_fires" in r for r in allr):
+            alt_fires = sum(r["alt_fires"] for r in allr)
             out.update({
-                # the headline's shards, each against its own fake apiserver partition: what the
-                # operator's shards do when no one fixture process bounds them
-                "partitioned_value": round(part_fires / max(r["part_elapsed_s"] for r in allr), 2),
-                "partitioned_p50_ms": round(max(r["part_p50"] for r in allr), 2),
-                "partitioned_operator_cpu_ms_per_fire": round(sum(r["part_cpu_op"] for r in allr) * 1000
-                                                              / part_fires, 4),
-                # the busiest partition of any rank (CPU s / wall s)
-                "partitioned_apiserver_busy_frac": round(max(r["part_cpu_api_max"] / r["part_elapsed_s"]
-                                                             for r in allr), 3),
+                f"{alt}_value": round(alt_fires / max(r["alt_elapsed_s"] for r in allr), 2),
+                f"{alt}_p50_ms": round(max(r["alt_p50"] for r in allr), 2),
+                f"{alt}_operator_cpu_ms_per_fire": round(sum(r["alt_cpu_op"] for r in allr) * 1000 / alt_fires, 4),
+                # the busiest fake apiserver of any rank (CPU s / wall s)
+                f"{alt}_apiserver_busy_frac": round(max(r["alt_cpu_api"] / r["alt_elapsed_s"] for r in allr), 3),
             })
         if "sp_fires" in allr[0]:
             sp_fires = sum(r["sp_fires"] for r in allr)

@@ -111,7 +111,8 @@ class BenchConfig:
     seed_history: bool = True  # requires history_limit >= 1
     apiserver_profile: str = ""  # write a cProfile of the apiserver process over the timed steps here
     shard_profile: str = ""      # shards > 1: cProfile of each shard over the timed steps, <prefix>.<i>.pstats
-    # operator shards (--shard-count): >1 runs one operator process per shard against the same apiserver
+    # operator shards (--shard-count): >1 runs one operator process per shard against the apiserver (or,
+    # with apiserver_partitions, against its own partition)
     # (bench/shard_worker.py); 1 keeps the operator in this process
     shards: int = 1
     # how shards split the watch traffic: "hash" (every shard sees every event) or "labels"
