@@ -547,7 +547,9 @@ def main() -> int:
                        "tls": cfg.tls, "qps": cfg.qps, "job_lifecycle": cfg.lifecycle,
                        "apiserver_impl": cfg.apiserver_impl, "completion_writes": cfg.completion_writes,
                        "fixture": "partitioned" if cfg.apiserver_partitions > 1 else "shared",
-                       "apiserver_partitions": cfg.apiserver_partitions},
+                       "apiserver_partitions": cfg.apiserver_partitions,
+                       # CPUs the job may use per rank (cgroup quota / affinity): what chose shards and fixture
+                       "cpus_per_rank": available_cpus() // world},
             "p50_schedule_to_create_ms": round(max(r["p50"] for r in allr), 2),
             "p99_schedule_to_create_ms": round(max(r["p99"] for r in allr), 2),
             "raw_reconciles_per_s": round(sum(r["reconciles"] for r in allr) / t_max, 2),
