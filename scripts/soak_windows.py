@@ -53,6 +53,9 @@ def main() -> int:
     ap.add_argument("--crons", type=int, default=1000)
     ap.add_argument("--shards", type=int, default=3)
     ap.add_argument("--window", type=int, default=20)
+    ap.add_argument("--partitions", type=int, default=1,
+                    help="fake apiserver processes (1: shared by the shards; --shards: one per shard, the "
+                         "headline's layout -- the fixture counters then come from the first partition)")
     ap.add_argument("--impl", default="native", choices=["native", "python"])
     ap.add_argument("--watch-window", type=int, default=20_000)
     ap.add_argument("--lifecycle", default="instant", choices=["instant", "realistic"],
@@ -113,6 +116,8 @@ def main() -> int:
     # the fixture's holdings at the end of the run: read once, after the timed region closed
     def cpu(remote):
         r = orig(remote)
+        if isinstance(remote, list):  # partitions: the first one's counters and holdings
+            remote = remote[0] if remote else None
         if remote is not None and remote.url and remote.proc is not None:
             url[0], pid[0] = remote.url, remote.proc.pid
         if done[0] and not fixture and remote is not None and remote.url:
@@ -135,7 +140,8 @@ def main() -> int:
     try:
         res = harness.run_sync(harness.BenchConfig(n_crons=a.crons, steps=a.steps, warmup=a.warmup,
                                                    shards=a.shards, apiserver_impl=a.impl, lifecycle=a.lifecycle,
-                                                   watch_window=a.watch_window), on_step=progress)
+                                                   watch_window=a.watch_window,
+                                                   apiserver_partitions=a.partitions), on_step=progress)
     finally:
         harness._cpu_times = orig
     n = a.crons * a.window
@@ -144,6 +150,7 @@ def main() -> int:
     api_w = [sum(w) * 1e6 / n for w in windows(res.step_cpu_apiserver_s, a.window)]
     rel = [round(x / step_w[0] - 1, 4) for x in step_w]
     out = {"config": {"crons": a.crons, "steps": a.steps, "warmup": a.warmup, "shards": a.shards,
+                      "partitions": a.partitions,
                       "impl": a.impl, "watch_window": a.watch_window, "window": a.window, "lifecycle": a.lifecycle},
            "value": round(res.cron_reconciles_per_s, 1),
            "ms_per_step_by_window": [round(x, 1) for x in step_w],
