@@ -4,7 +4,8 @@
 #   bench   the driver's bench invocation (20 timed steps), JSON kept
 #   configs deployment-shaped rows (etcd latency, TLS, chart defaults at 1000 Crons)
 #   rocprof kernel stats of the scheduled payload (rocprofv3 --kernel-trace --stats)
-#   soak    200 ticks, 3 shards, 20-tick windows: step time, operator and fixture CPU per fire,
+#   soak    200 ticks, 3 shards (SOAK_PARTITIONS fake apiservers, default 3: the headline's layout),
+#           20-tick windows: step time, operator and fixture CPU per fire,
 #           fixture counters, box calibrations (scripts/soak_windows.py)
 #   baseline all five BASELINE.json configs in both reconciler modes (scripts/baseline_configs.py)
 #   scale   cron-reconciles/s at 1 / 10 / 100 / 1000 Crons, both modes (scripts/bench_scale.py)
@@ -56,7 +57,8 @@ for s in $STEPS; do
       check $? rocprof; find "$OUT/prof" -name "*kernel_stats.csv" | head -2 ;;
     soak)
       step soak
-      timeout -k 10 600 python -u scripts/soak_windows.py --steps 200 --out "$OUT/soak200.json" \
+      timeout -k 10 600 python -u scripts/soak_windows.py --steps 200 --partitions "${SOAK_PARTITIONS:-3}" \
+        --out "$OUT/soak200.json" \
         > "$OUT/soak200.log" 2>&1
       check $? soak; tail -1 "$OUT/soak200.log" | cut -c1-400 ;;
     baseline)
