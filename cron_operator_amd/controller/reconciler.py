@@ -695,10 +695,11 @@ class CronReconciler(Reconciler):
                     result = await self._sync(cron, log, gc, release)
                 except Exception as e:  # noqa: BLE001 - joined with the patch error below
                     err = e
-                if self.opts.defer_status_write and (gc or not old_status.semantic_equal(cron.status)):
+                changed = not old_status.semantic_equal(cron.status)
+                if self.opts.defer_status_write and (gc or changed):
                     release_worker()  # only writes are left: another Cron may use the slot
                 # B2: deferred status patch when status changed semantically (cron_controller.go:107-120)
-                if not old_status.semantic_equal(cron.status):
+                if changed:
                     try:
                         await self._patch_status(old_obj, cron, log, key)  # overlaps the running GC DELETEs
                     except Exception as pe:  # noqa: BLE001
