@@ -202,9 +202,10 @@ class CronStatus:
             return False
         if not _t_eq(self.last_schedule_time, o.last_schedule_time):
             return False
-        if any(a != b for a, b in zip(self.active, o.active)):
+        # a snapshot shares its entries: the same object is equal without a field compare
+        if any(a is not b and a != b for a, b in zip(self.active, o.active)):
             return False
-        return all(a.semantic_equal(b) for a, b in zip(self.history, o.history))
+        return all(a is b or a.semantic_equal(b) for a, b in zip(self.history, o.history))
 
 
 # The workload template is kept as parsed JSON (dict) when it came from the API,
