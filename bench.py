@@ -356,8 +356,14 @@ def main() -> int:
     if a.shards <= 0:
         from cron_operator_amd.runtime.supervisor import available_cpus
 
-        # 3 shards saturate one fake apiserver process; never oversubscribe the CPUs the ranks share
-        a.shards = max(1, min(3, available_cpus() // world - 1))
+        # never oversubscribe the CPUs the ranks share: with a partitioned fixture a core per shard
+        # and per partition plus one (3 shards from 7 CPUs per rank, 2 from 5); otherwise a core
+        # per shard plus one for the shared fake apiserver (3 shards saturate it)
+        cpus = available_cpus() // world
+        if a.fixture == "partitioned" and a.shard_routing == "labels" and a.transport == "http" and cpus >= 5:
+            a.shards = min(3, (cpus - 1) // 2)
+        else:
+            a.shards = max(1, min(3, cpus - 1))
 
     from cron_operator_amd.runtime.supervisor import available_cpus
 

@@ -231,3 +231,20 @@ def test_a_killed_rank_fails_the_eight_rank_job_without_a_hang():
         if p.poll() is None:
             os.killpg(p.pid, signal.SIGKILL)
             p.wait()
+
+
+def test_five_cpus_per_rank_run_two_partitioned_shards():
+    """With 5-6 CPUs per rank the headline keeps a fake apiserver partition per shard and runs
+    2 shards (a core each, a core per partition, one for the harness) rather than 3 shards
+    against one shared fixture."""
+    import shutil
+
+    if shutil.which("taskset") is None or (os.cpu_count() or 1) < 5:
+        pytest.skip("needs taskset and 5 CPUs")
+    r = subprocess.run(["taskset", "-c", "0-4", sys.executable, "bench.py", "--steps", "1", "--warmup", "1",
+                        "--crons", "12", "--baseline", "none", "--deployment", "none", "--single-process", "none",
+                        "--payload-probe", "none"], cwd=ROOT, env=_env(), capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _json_line(r.stdout)
+    assert d["config"]["cpus_per_rank"] == 5 and d["config"]["parallelism"] == "ranks1x2shards"
+    assert d["config"]["fixture"] == "partitioned" and d["config"]["apiserver_partitions"] == 2
