@@ -23,9 +23,9 @@ server thread, and one of them saturates under 3 shards (0.87-0.93 busy in round
 then measured the fixture as much as the operator).  So by default (``partitioned``) each shard
 gets a fake apiserver process of its own, holding the Crons that hash to that shard and their
 jobs -- exactly what that shard watches and writes under label routing -- and the headline
-measures the shards (busiest partition ~0.5-0.6 busy on the box).  It needs two CPUs per shard
-plus one per rank; with fewer the headline falls back to ``shared``: every shard against one
-fake apiserver, the rounds 1-5 layout.  ``shared_fixture_*`` (or ``partitioned_*`` when the
+measures the shards (busiest partition ~0.4-0.6 busy on the box).  It needs two CPUs per shard
+plus one per rank (3 shards from 7 CPUs per rank, 2 from 5); below 5 the headline falls back to
+``shared``: every shard against one fake apiserver, the rounds 1-5 layout.  ``shared_fixture_*`` (or ``partitioned_*`` when the
 headline is shared) is the same shards against the other layout, in this same invocation after
 the timed run (``--other-fixture none`` skips it); ``config.fixture`` says which one the
 headline used.
