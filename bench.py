@@ -25,9 +25,9 @@ gets a fake apiserver process of its own, holding the Crons that hash to that sh
 jobs -- exactly what that shard watches and writes under label routing -- and the headline
 measures the shards (busiest partition ~0.4-0.6 busy on the box).  It needs two CPUs per shard
 plus one per rank (3 shards from 7 CPUs per rank, 2 from 5); below 5 the headline falls back to
-``shared``: every shard against one fake apiserver, the rounds 1-5 layout.  ``shared_fixture_*`` (or ``partitioned_*`` when the
-headline is shared) is the same shards against the other layout, in this same invocation after
-the timed run (``--other-fixture none`` skips it); ``config.fixture`` says which one the
+``shared``: every shard against one fake apiserver, the rounds 1-5 layout.
+``shared_fixture_*`` (or ``partitioned_*`` when the headline is shared) is the same shards
+against the other layout, in this same invocation after the timed run (``--other-fixture none`` skips it); ``config.fixture`` says which one the
 headline used.
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
