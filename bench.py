@@ -27,8 +27,8 @@ measures the shards (busiest partition ~0.4-0.6 busy on the box).  It needs two 
 plus one per rank (3 shards from 7 CPUs per rank, 2 from 5); below 5 the headline falls back to
 ``shared``: every shard against one fake apiserver, the rounds 1-5 layout.
 ``shared_fixture_*`` (or ``partitioned_*`` when the headline is shared) is the same shards
-against the other layout, in this same invocation after the timed run (``--other-fixture none`` skips it); ``config.fixture`` says which one the
-headline used.
+against the other layout, in this same invocation after the timed run (``--other-fixture
+none`` skips it); ``config.fixture`` says which one the headline used.
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
 it runs under ``torch.distributed.run`` with one rank per GPU (without a launcher,
