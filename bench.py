@@ -34,8 +34,8 @@ Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1
 it runs under ``torch.distributed.run`` with one rank per GPU (without a launcher,
 ``--gpus N`` spawns the N rank processes itself).  The operator is
 pure control plane, so ranks do not use the GPU: each
-rank is one operator shard (its own apiserver process and 1000 Crons, weak
-scaling) and rank 0 reports the whole-job aggregate.  Ranks synchronise with
+rank is one operator deployment (its shards, its own fake apiserver processes and 1000
+Crons: weak scaling) and rank 0 reports the whole-job aggregate.  Ranks synchronise with
 gloo barriers; there is no device work to ``torch.cuda.synchronize()``.
 
 ``single_process_*``: the chart ships ONE operator process (``sharding.count: 1``,
