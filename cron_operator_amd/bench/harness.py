@@ -62,6 +62,8 @@ PYTORCHJOBS = GroupVersionResource("kubeflow.org", "v1", "pytorchjobs")
 T0_NS = 1767268800 * NANOS
 # completion_writes="interleaved": completion PATCHes the fake apiserver applies per loop turn
 COMPLETION_WRITES_PER_TURN = 32
+# a settle wait's poll once no Cron is pending (the controller's queue draining its last items)
+SETTLE_POLL_S = 0.0005
 
 
 # Server-side latency models for the fake apiserver (seconds per verb, applied after setup).
@@ -319,6 +321,7 @@ class SettleTracker:
         self.keys = set(keys) if keys is not None else None
         self.pred = None
         self.pending: set = set()
+        self.drained: Optional[asyncio.Event] = None  # set while nothing is pending
         informer.add_handler(EventHandler(on_add=self._on, on_update=lambda old, new: self._on(new)))
 
     def _on(self, obj: Dict[str, Any]) -> None:
@@ -331,8 +334,12 @@ class SettleTracker:
             return
         if self.pred(obj):
             self.pending.discard(k)
+            if not self.pending and self.drained is not None:
+                self.drained.set()
         else:
             self.pending.add(k)
+            if self.drained is not None:
+                self.drained.clear()
 
     def begin(self, pred) -> None:
         self.pred = pred
@@ -340,6 +347,23 @@ class SettleTracker:
                         if (self.keys is None or k in self.keys) and not pred(o)}
         if self.keys is not None:
             self.pending |= {k for k in self.keys if k not in self.inf.store}
+        if self.drained is None:
+            self.drained = asyncio.Event()
+        if self.pending:
+            self.drained.clear()
+        else:
+            self.drained.set()
+
+    async def wait_drained(self, timeout: float = 0.05) -> None:
+        """Until nothing is pending (an event wakes the waiter: no polling while the phase's
+        events arrive), or ``timeout`` -- then the caller checks its full condition again."""
+        if self.pending and self.drained is not None:
+            try:
+                await asyncio.wait_for(self.drained.wait(), timeout)
+            except asyncio.TimeoutError:
+                pass
+        else:
+            await asyncio.sleep(SETTLE_POLL_S)
 
 
 class RvTracker:
@@ -671,7 +695,7 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
                     raise TimeoutError(f"step {k} did not settle (creates={creates_this_tick[0]})")
                 if creates_this_tick[0] >= cfg.n_crons and not tracker.pending and ctrl.queue.idle():
                     return
-                await asyncio.sleep(0.002)
+                await tracker.wait_drained()
 
         want_hist = cfg.history_limit
 
@@ -683,7 +707,7 @@ async def _run(cfg: BenchConfig, on_step=None) -> BenchResult:
                     raise TimeoutError("completion phase did not settle")
                 if not tracker.pending and ctrl.queue.idle():
                     return
-                await asyncio.sleep(0.002)
+                await tracker.wait_drained()
 
         n_pre = lifecycle_stages(cfg)
         rv_tracker = RvTracker(job_informer(mgr, rec)) if n_pre else None

@@ -359,7 +359,7 @@ async def main() -> int:
         while True:
             if (phase == "completion" or creates[0] >= n_owned) and not tracker.pending and ctrl.queue.idle():
                 return
-            await asyncio.sleep(0.002)
+            await tracker.wait_drained()
 
     prof = None
     while True:
